@@ -1,0 +1,51 @@
+"""Loader for the in-tree native extension (``ops/_C*.so``).
+
+Policy: on a machine with a GPU the native path is mandatory — if the
+extension is missing it is built in-tree once (``ops/build.py``) and, if
+that fails, every GPU op raises. There is no silent eager fallback for
+GPU tensors. CPU tensors never need the extension.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import threading
+
+_lock = threading.Lock()
+_mod = None
+_err: Exception | None = None
+
+
+def load(build_if_missing: bool = True):
+    """Return the ``_C`` module, building it in-tree if needed. Raises on failure."""
+    global _mod, _err
+    if _mod is not None:
+        return _mod
+    with _lock:
+        if _mod is not None:
+            return _mod
+        import torch  # noqa: F401  (loads torch's HIP runtime first)
+
+        try:
+            _mod = importlib.import_module(f"{__package__}._C")
+            return _mod
+        except ImportError as e:  # not built yet
+            _err = e
+        if build_if_missing and os.environ.get("PDMB_NO_AUTOBUILD", "0") != "1":
+            from . import build as _build
+
+            _build.build()
+            importlib.invalidate_caches()
+            _mod = importlib.import_module(f"{__package__}._C")
+            return _mod
+        raise RuntimeError(
+            "pytorch_distributed_matmul_benchmark_amd: native extension _C is not built "
+            "(python -m pytorch_distributed_matmul_benchmark_amd.ops.build)") from _err
+
+
+def available() -> bool:
+    try:
+        load(build_if_missing=False)
+        return True
+    except Exception:
+        return False

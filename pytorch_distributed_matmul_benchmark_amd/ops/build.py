@@ -1,0 +1,133 @@
+"""In-tree build of the native extension ``ops/_C*.so`` for gfx950.
+
+No hipify, no ``torch.utils.cpp_extension.CUDAExtension`` (which would
+run hipify over the sources): the HIP kernels are compiled directly with
+``hipcc --offload-arch=gfx950`` and the pybind/torch binding with the host
+compiler, then linked against PyTorch-ROCm's own HIP runtime
+(``torch/lib/libamdhip64.so``, SONAME ``libamdhip64.so.7``) so the process
+has exactly one HIP runtime.
+
+Usage: ``python -m pytorch_distributed_matmul_benchmark_amd.ops.build``
+(or ``build()`` from Python). Rebuilds only when a source is newer than
+the library.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+CSRC = HERE / "csrc"
+BUILD = HERE / "_build"
+ARCH = os.environ.get("PDMB_OFFLOAD_ARCH", "gfx950")
+EXT_NAME = "_C"
+
+HIP_SOURCES = ["gemm_mfma256.hip", "gemm_generic.hip", "gemm_dispatch.cpp"]
+HOST_SOURCES = ["bindings.cpp"]
+
+
+def rocm_path() -> Path:
+    return Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+
+
+def hipcc() -> str:
+    p = rocm_path() / "bin" / "hipcc"
+    return str(p) if p.exists() else (shutil.which("hipcc") or "hipcc")
+
+
+def lib_path() -> Path:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return HERE / f"{EXT_NAME}{suffix}"
+
+
+def _torch_paths():
+    import torch  # noqa: F401
+    from torch.utils import cpp_extension
+
+    return cpp_extension.include_paths(), cpp_extension.library_paths()
+
+
+def _needs_build(out: Path, deps) -> bool:
+    if not out.exists():
+        return True
+    t = out.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(str(c) for c in cmd), flush=True)
+    r = subprocess.run([str(c) for c in cmd], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build step failed ({r.returncode}): {' '.join(map(str, cmd))}\n"
+                           f"{r.stdout}\n{r.stderr}")
+    return r
+
+
+def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -> Path:
+    """Compile every HIP/C++ source for gfx950 and link ``_C``. Returns the .so path."""
+    headers = sorted(CSRC.glob("*.h"))
+    out = lib_path()
+    all_src = [CSRC / s for s in HIP_SOURCES + HOST_SOURCES]
+    if not force and not _needs_build(out, all_src + headers + [Path(__file__)]):
+        return out
+    BUILD.mkdir(exist_ok=True)
+    inc, libdirs = _torch_paths()
+    py_inc = sysconfig.get_paths()["include"]
+    import torch
+
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    hip_flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+                 "-Wno-unused-result", "-munsafe-fp-atomics", f"-I{CSRC}"]
+    host_flags = ["-O2", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+                  f"-DTORCH_EXTENSION_NAME={EXT_NAME}", "-DTORCH_API_INCLUDE_EXTENSION_H",
+                  "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", f"-I{CSRC}",
+                  f"-I{rocm_path() / 'include'}", f"-I{py_inc}"] + [f"-I{p}" for p in inc]
+
+    steps = []
+    objs = []
+    for s in HIP_SOURCES:
+        src = CSRC / s
+        obj = BUILD / (src.stem + ".o")
+        objs.append(obj)
+        if force or _needs_build(obj, [src] + headers):
+            lang = ["-x", "hip"] if src.suffix == ".cpp" else []
+            steps.append([hipcc()] + hip_flags + lang + ["-c", src, "-o", obj])
+    cxx = os.environ.get("CXX", "g++")
+    for s in HOST_SOURCES:
+        src = CSRC / s
+        obj = BUILD / (src.stem + ".o")
+        objs.append(obj)
+        if force or _needs_build(obj, [src] + headers):
+            steps.append([cxx] + host_flags + ["-c", src, "-o", obj])
+
+    jobs = jobs or min(len(steps) or 1, max(1, (os.cpu_count() or 2) // 2), 8)
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        list(ex.map(lambda c: _run(c, verbose), steps))
+
+    torch_lib = libdirs[0]
+    link = [cxx, "-shared", "-o", out] + objs + [
+        f"-L{torch_lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+        "-ltorch_python", "-lamdhip64", f"-Wl,-rpath,{torch_lib}"]
+    _run(link, verbose)
+    return out
+
+
+def main(argv=None):
+    import argparse
+
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    p = build(verbose=a.verbose, force=a.force)
+    print(p)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,43 @@
+// Host-side C++ API of the native GEMM library (no torch dependency).
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <stddef.h>
+
+namespace pdmb {
+
+enum Kernel : int {
+  kAuto = 0,      // fastest kernel that supports the problem
+  kMfma256 = 1,   // gemm_mfma256.hip (LDS-DMA, 256x256, ping-pong)
+  kGeneric = 2,   // gemm_generic.hip (any shape)
+};
+
+struct Problem {
+  int dtype;  // DType
+  const void* A;
+  const void* B;
+  void* C;
+  int M, N, K;
+  int lda, ldb, ldc;
+  long long sA, sB, sC;
+  int batch;
+};
+
+// Which kernel `kernel` (kAuto allowed) resolves to for this problem;
+// -1 if the requested kernel cannot run it.
+int resolve_kernel(const Problem& p, int kernel);
+
+// Enqueue C = A @ B on `stream`. Returns hipSuccess or an error; *used (if
+// non-null) receives the kernel that ran.
+hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used);
+
+// Native timing loop: `warmup` untimed launches, then `iters` launches
+// bracketed by hipEvents on `stream` (optionally captured once into a
+// hipGraph and replayed, which removes host launch gaps). Returns the
+// total elapsed milliseconds of the timed region in *ms.
+hipError_t bench_gemm(const Problem& p, int kernel, int iters, int warmup, bool use_graph,
+                      hipStream_t stream, float* ms);
+
+const char* kernel_name(int kernel);
+
+}  // namespace pdmb

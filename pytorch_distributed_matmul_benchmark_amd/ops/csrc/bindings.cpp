@@ -1,0 +1,134 @@
+// Python bindings of the native GEMM library (torch tensors in, enqueue on
+// the caller's current HIP stream). Built with the host compiler against
+// the PyTorch-ROCm headers; the kernels themselves live in the .hip files.
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+#include <string>
+
+#include "api.h"
+
+namespace {
+
+int dtype_code(at::ScalarType t) {
+  switch (t) {
+    case at::kFloat:
+      return 0;
+    case at::kHalf:
+      return 1;
+    case at::kBFloat16:
+      return 2;
+    default:
+      TORCH_CHECK(false, "pdmb: unsupported dtype ", t, " (float32 / float16 / bfloat16 only)");
+  }
+  return -1;
+}
+
+void check_hip(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "pdmb: ", what, " failed: ", hipGetErrorString(e));
+}
+
+// A: [M,K] | [b,M,K], B: [K,N] | [b,K,N] (2-D B broadcasts over the batch),
+// C: [M,N] | [b,M,N]; innermost stride must be 1 (leading dims free).
+pdmb::Problem make_problem(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "pdmb: tensors must be on the GPU");
+  TORCH_CHECK(A.device() == B.device() && A.device() == C.device(), "pdmb: device mismatch");
+  TORCH_CHECK(A.scalar_type() == B.scalar_type() && A.scalar_type() == C.scalar_type(),
+              "pdmb: dtype mismatch");
+  TORCH_CHECK(A.dim() == 2 || A.dim() == 3, "pdmb: A must be 2-D or 3-D");
+  TORCH_CHECK(B.dim() == 2 || B.dim() == 3, "pdmb: B must be 2-D or 3-D");
+  TORCH_CHECK(C.dim() == std::max(A.dim(), B.dim()), "pdmb: bad output rank");
+  const bool batched = C.dim() == 3;
+  const int64_t batch = batched ? C.size(0) : 1;
+  const int64_t M = A.size(-2), K = A.size(-1), N = B.size(-1);
+  TORCH_CHECK(B.size(-2) == K, "pdmb: inner dimensions differ: ", A.sizes(), " @ ", B.sizes());
+  TORCH_CHECK(C.size(-2) == M && C.size(-1) == N, "pdmb: output shape mismatch");
+  if (batched) {
+    TORCH_CHECK(A.dim() == 2 || A.size(0) == batch, "pdmb: batch mismatch");
+    TORCH_CHECK(B.dim() == 2 || B.size(0) == batch, "pdmb: batch mismatch");
+  }
+  auto inner_ok = [](const at::Tensor& t) {
+    return t.size(-1) <= 1 || t.stride(-1) == 1;
+  };
+  TORCH_CHECK(inner_ok(A) && inner_ok(B) && inner_ok(C), "pdmb: innermost dim must be contiguous");
+  auto ld = [](const at::Tensor& t) {
+    int64_t l = t.stride(-2);
+    return std::max<int64_t>(l, std::max<int64_t>(t.size(-1), 1));
+  };
+  TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31) && batch < (1LL << 31),
+              "pdmb: dimension too large");
+  pdmb::Problem p{};
+  p.dtype = dtype_code(A.scalar_type());
+  p.A = A.data_ptr();
+  p.B = B.data_ptr();
+  p.C = C.data_ptr();
+  p.M = (int)M;
+  p.N = (int)N;
+  p.K = (int)K;
+  p.lda = (int)ld(A);
+  p.ldb = (int)ld(B);
+  p.ldc = (int)ld(C);
+  p.sA = (batched && A.dim() == 3) ? A.stride(0) : 0;
+  p.sB = (batched && B.dim() == 3) ? B.stride(0) : 0;
+  p.sC = batched ? C.stride(0) : 0;
+  p.batch = (int)batch;
+  return p;
+}
+
+at::Tensor alloc_out(const at::Tensor& A, const at::Tensor& B) {
+  std::vector<int64_t> shape;
+  if (A.dim() == 3 || B.dim() == 3) shape.push_back(A.dim() == 3 ? A.size(0) : B.size(0));
+  shape.push_back(A.size(-2));
+  shape.push_back(B.size(-1));
+  return at::empty(shape, A.options());
+}
+
+at::Tensor matmul(const at::Tensor& A, const at::Tensor& B, c10::optional<at::Tensor> out,
+                  int64_t kernel) {
+  at::Tensor C = out.has_value() ? *out : alloc_out(A, B);
+  pdmb::Problem p = make_problem(A, B, C);
+  c10::hip::HIPGuard guard(A.device().index());
+  hipStream_t s = c10::hip::getCurrentHIPStream(A.device().index()).stream();
+  int used = -1;
+  hipError_t e = pdmb::gemm(p, (int)kernel, s, &used);
+  TORCH_CHECK(used >= 0, "pdmb: kernel ", kernel, " cannot run this problem");
+  check_hip(e, "gemm launch");
+  return C;
+}
+
+int64_t resolve(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t kernel) {
+  return pdmb::resolve_kernel(make_problem(A, B, C), (int)kernel);
+}
+
+// Total milliseconds for `iters` timed launches (after `warmup`).
+double bench(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t iters,
+             int64_t warmup, bool graph, int64_t kernel) {
+  pdmb::Problem p = make_problem(A, B, C);
+  TORCH_CHECK(pdmb::resolve_kernel(p, (int)kernel) >= 0, "pdmb: kernel cannot run this problem");
+  c10::hip::HIPGuard guard(A.device().index());
+  hipStream_t s = c10::hip::getCurrentHIPStream(A.device().index()).stream();
+  float ms = 0.f;
+  check_hip(pdmb::bench_gemm(p, (int)kernel, (int)iters, (int)warmup, graph, s, &ms), "bench_gemm");
+  return (double)ms;
+}
+
+std::string kernel_name(int64_t k) { return pdmb::kernel_name((int)k); }
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "MI355X (gfx950) native GEMM kernels and timing loop";
+  m.def("matmul", &matmul, "C = A @ B on gfx950 MFMA", py::arg("A"), py::arg("B"),
+        py::arg("out") = py::none(), py::arg("kernel") = 0);
+  m.def("resolve", &resolve, "kernel id that would run (or -1)", py::arg("A"), py::arg("B"),
+        py::arg("out"), py::arg("kernel") = 0);
+  m.def("bench", &bench, "native hipEvent timing loop; returns total ms", py::arg("A"),
+        py::arg("B"), py::arg("out"), py::arg("iters"), py::arg("warmup"),
+        py::arg("graph") = false, py::arg("kernel") = 0);
+  m.def("kernel_name", &kernel_name);
+  m.attr("KERNEL_AUTO") = (int)pdmb::kAuto;
+  m.attr("KERNEL_MFMA256") = (int)pdmb::kMfma256;
+  m.attr("KERNEL_GENERIC") = (int)pdmb::kGeneric;
+  m.attr("ARCH") = "gfx950";
+}

@@ -1,0 +1,125 @@
+// Shared types and helpers for the gfx950 (CDNA4 / MI355X) GEMM kernels.
+//
+// Everything here is written for gfx950 only: wave64, MFMA 16x16x32 for
+// 16-bit inputs, MFMA 16x16x4 for exact fp32, LDS-DMA (buffer_load ... lds)
+// staging. See docs/ARCHITECTURE.md for the design notes.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pdmb {
+
+// ---- element / fragment types -------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(3))) s16x8 lds_s16x8;
+
+// Data-type tags shared by host and device code. Values are part of the
+// binding ABI (ops/gemm.py mirrors them).
+enum DType : int { kF32 = 0, kF16 = 1, kBF16 = 2 };
+
+// One MFMA 16x16x32 step on 16-bit operands (a: 8 elements/lane, b: 8).
+template <int DT>
+__device__ __forceinline__ f32x4 mfma16x16x32(s16x8 a, s16x8 b, f32x4 c);
+
+template <>
+__device__ __forceinline__ f32x4 mfma16x16x32<kBF16>(s16x8 a, s16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ f32x4 mfma16x16x32<kF16>(s16x8 a, s16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
+// fp32 -> 16-bit with round-to-nearest-even (hipcc emits v_cvt_pk_bf16_f32 /
+// v_cvt_pk_f16_f32 on gfx950; NaN stays NaN).
+template <int DT>
+__device__ __forceinline__ unsigned int pack2(float lo, float hi);
+template <>
+__device__ __forceinline__ unsigned int pack2<kBF16>(float lo, float hi) {
+  __bf16 l = (__bf16)lo, h = (__bf16)hi;
+  return (unsigned int)__builtin_bit_cast(unsigned short, l) |
+         ((unsigned int)__builtin_bit_cast(unsigned short, h) << 16);
+}
+template <>
+__device__ __forceinline__ unsigned int pack2<kF16>(float lo, float hi) {
+  _Float16 l = (_Float16)lo, h = (_Float16)hi;
+  return (unsigned int)__builtin_bit_cast(unsigned short, l) |
+         ((unsigned int)__builtin_bit_cast(unsigned short, h) << 16);
+}
+
+template <int DT>
+__device__ __forceinline__ float to_f32(unsigned short v);
+template <>
+__device__ __forceinline__ float to_f32<kBF16>(unsigned short v) {
+  return __uint_as_float(((unsigned int)v) << 16);
+}
+template <>
+__device__ __forceinline__ float to_f32<kF16>(unsigned short v) {
+  return (float)__builtin_bit_cast(_Float16, v);
+}
+
+// ---- kernel argument block ----------------------------------------------
+// Row-major C[b] = A[b] @ B[b]: A is [M,K] (lda), B is [K,N] (ldb), C is
+// [M,N] (ldc); all strides in elements. Batch strides in elements.
+struct GemmArgs {
+  const void* A;
+  const void* B;
+  void* C;
+  int M, N, K;
+  int lda, ldb, ldc;
+  long long sA, sB, sC;
+  int batch;
+  int tiles_m, tiles_n;  // output tiles per batch element
+  int supertile;         // 1: XCD-aware 16x16 super-tile order, 0: grouped order
+};
+
+// ---- block -> output tile mapping -------------------------------------
+// Speed only (never correctness): workgroups are dealt round-robin over the
+// 8 XCDs (blocks b and b+8 share an XCD). In super-tile mode every "round"
+// of 256 workgroups (one per CU) covers one 16x16-tile super-tile, and each
+// XCD's 32 workgroups cover a 4x8 sub-block of it, so an XCD's L2 serves
+// 4 A-panels + 8 B-panels per K-step (12 fetches instead of 64) and the
+// whole chip touches 32 panels per K-step (shared through Infinity Cache).
+// Super-tiles sweep N fastest so A panels stay Infinity-Cache resident.
+// Otherwise: grouped order with 16 tile-rows per group (chip-wide locality).
+__device__ __forceinline__ void map_tile(const GemmArgs& a, int b, int& bz, int& tm, int& tn) {
+  const int tpb = a.tiles_m * a.tiles_n;
+  if (a.supertile) {
+    const int x = b & 7, j = b >> 3;
+    const int round = j >> 5, i = j & 31;
+    const int st_n = a.tiles_n >> 4;
+    const int st_per_b = (a.tiles_m >> 4) * st_n;
+    bz = round / st_per_b;
+    const int s = round - bz * st_per_b;
+    const int sr = s / st_n, sc = s - sr * st_n;
+    tm = (sr << 4) + ((x >> 1) << 2) + (i >> 3);
+    tn = (sc << 4) + ((x & 1) << 3) + (i & 7);
+  } else {
+    bz = b / tpb;
+    const int L = b - bz * tpb;
+    const int gsz = 16 * a.tiles_n;
+    const int grp = L / gsz;
+    const int first_m = grp * 16;
+    int gm = a.tiles_m - first_m;
+    gm = gm < 16 ? gm : 16;
+    const int r = L - grp * gsz;
+    tm = first_m + r % gm;
+    tn = r / gm;
+  }
+}
+
+}  // namespace pdmb

@@ -1,0 +1,108 @@
+"""GEMM entry points: ``matmul`` / ``bmm`` / ``bench_matmul``.
+
+GPU tensors run on the hand-written gfx950 MFMA kernels of ``ops/csrc``
+(``gemm_mfma256.hip`` for the benchmark shapes, ``gemm_generic.hip`` for
+everything else and for fp32). CPU tensors use ``torch.matmul`` — the
+reference's own compute call (matmul_benchmark.py:46) — which is the
+BASELINE config #1 CPU path ("4k fp32 matmul, single process on CPU").
+
+Every call writes into a caller-provided (or freshly allocated) ``out``
+and is enqueued on the current HIP stream, so it composes with
+``torch.cuda.stream(...)`` and events exactly like an ATen op.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _native
+
+KERNELS = {"auto": 0, "mfma256": 1, "generic": 2}
+KERNEL_NAMES = {0: "auto", 1: "pdmb_mfma256_nn", 2: "pdmb_generic_nn", -1: "unsupported"}
+SUPPORTED_DTYPES = (torch.float32, torch.float16, torch.bfloat16)
+
+
+def _kid(kernel) -> int:
+    if isinstance(kernel, int):
+        return kernel
+    try:
+        return KERNELS[kernel]
+    except KeyError:
+        raise ValueError(f"unknown kernel {kernel!r}; choose from {sorted(KERNELS)}") from None
+
+
+def _out_shape(A: torch.Tensor, B: torch.Tensor):
+    batch = []
+    if A.dim() == 3 or B.dim() == 3:
+        batch = [A.shape[0] if A.dim() == 3 else B.shape[0]]
+    return (*batch, A.shape[-2], B.shape[-1])
+
+
+def _prep(t: torch.Tensor) -> torch.Tensor:
+    # Kernels need a unit innermost stride; leading dims may be strided.
+    if t.dim() >= 1 and t.shape[-1] > 1 and t.stride(-1) != 1:
+        return t.contiguous()
+    return t
+
+
+def matmul(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
+           kernel="auto") -> torch.Tensor:
+    """``out = A @ B`` for 2-D/3-D row-major operands (3-D = batched)."""
+    if A.dim() not in (2, 3) or B.dim() not in (2, 3):
+        raise ValueError("matmul: operands must be 2-D or 3-D")
+    if A.shape[-1] != B.shape[-2]:
+        raise ValueError(f"matmul: shape mismatch {tuple(A.shape)} @ {tuple(B.shape)}")
+    if A.device.type != "cuda":
+        if A.dim() == 3 or B.dim() == 3:
+            res = torch.matmul(A, B)
+            if out is None:
+                return res
+            out.copy_(res)
+            return out
+        return torch.matmul(A, B, out=out) if out is not None else torch.matmul(A, B)
+    if A.dtype not in SUPPORTED_DTYPES:
+        raise TypeError(f"matmul: unsupported dtype {A.dtype}")
+    C = _native.load()
+    A, B = _prep(A), _prep(B)
+    if out is None:
+        out = torch.empty(_out_shape(A, B), dtype=A.dtype, device=A.device)
+    C.matmul(A, B, out, _kid(kernel))
+    return out
+
+
+def bmm(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
+        kernel="auto") -> torch.Tensor:
+    """Batched ``out[b] = A[b] @ B[b]`` (the reference's ``torch.bmm``)."""
+    if A.dim() != 3 or B.dim() != 3:
+        raise ValueError("bmm: operands must be 3-D")
+    if A.device.type != "cuda":
+        return torch.bmm(A, B, out=out) if out is not None else torch.bmm(A, B)
+    return matmul(A, B, out=out, kernel=kernel)
+
+
+def kernel_for(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
+               kernel="auto") -> str:
+    """Name of the native kernel that ``matmul`` would launch for these operands."""
+    if A.device.type != "cuda":
+        return "torch.matmul(cpu)"
+    C = _native.load()
+    if out is None:
+        out = torch.empty(_out_shape(A, B), dtype=A.dtype, device=A.device)
+    return KERNEL_NAMES[int(C.resolve(_prep(A), _prep(B), out, _kid(kernel)))]
+
+
+def bench_matmul(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, iters: int,
+                 warmup: int, graph: bool = False, kernel="auto") -> float:
+    """Native timing loop (hipEvents around ``iters`` launches). Returns TOTAL ms."""
+    if A.device.type != "cuda":
+        import time
+
+        for _ in range(warmup):
+            torch.matmul(A, B, out=out)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            torch.matmul(A, B, out=out)
+        return (time.perf_counter() - t0) * 1e3
+    C = _native.load()
+    return float(C.bench(_prep(A), _prep(B), out, int(iters), int(warmup), bool(graph), _kid(kernel)))

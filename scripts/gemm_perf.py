@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Single-GPU GEMM throughput: native gfx950 kernel vs torch.matmul (hipBLASLt).
+
+Interleaves the arms in one process (cdna rule 24) on the same random data.
+Usage: python scripts/gemm_perf.py --sizes 4096 8192 16384 --dtype bfloat16
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from pytorch_distributed_matmul_benchmark_amd.ops import gemm  # noqa: E402
+
+DT = {"bfloat16": torch.bfloat16, "float16": torch.float16, "float32": torch.float32}
+
+
+def torch_ms(A, B, out, iters, warmup):
+    for _ in range(warmup):
+        torch.matmul(A, B, out=out)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        torch.matmul(A, B, out=out)
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sizes", type=int, nargs="+", default=[4096, 8192, 16384])
+    ap.add_argument("--dtype", default="bfloat16", choices=list(DT))
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--no-torch", action="store_true")
+    ap.add_argument("--kernel", default="auto")
+    a = ap.parse_args()
+    dt = DT[a.dtype]
+    for n in a.sizes:
+        torch.manual_seed(0)
+        A = torch.randn(n, n, device="cuda", dtype=dt)
+        B = torch.randn(n, n, device="cuda", dtype=dt)
+        out = torch.empty(n, n, device="cuda", dtype=dt)
+        flop = 2.0 * n ** 3
+        res = {"n": n, "dtype": a.dtype, "kernel": gemm.kernel_for(A, B, out, kernel=a.kernel)}
+        ours, ours_g, theirs = [], [], []
+        for _ in range(a.rounds):
+            ms = gemm.bench_matmul(A, B, out, a.iters, a.warmup, graph=False, kernel=a.kernel) / a.iters
+            ours.append(flop / ms / 1e9)
+            ms = gemm.bench_matmul(A, B, out, a.iters, a.warmup, graph=True, kernel=a.kernel) / a.iters
+            ours_g.append(flop / ms / 1e9)
+            if not a.no_torch:
+                ms = torch_ms(A, B, out, a.iters, a.warmup) / a.iters
+                theirs.append(flop / ms / 1e9)
+        ref = torch.matmul(A.float(), B.float())
+        C = gemm.matmul(A, B, kernel=a.kernel)
+        res["relerr"] = ((C.float() - ref).norm() / ref.norm()).item()
+        res["native_tflops"] = [round(x, 1) for x in ours]
+        res["native_graph_tflops"] = [round(x, 1) for x in ours_g]
+        if theirs:
+            res["torch_tflops"] = [round(x, 1) for x in theirs]
+        print(json.dumps(res), flush=True)
+        del A, B, out, ref, C
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    t0 = time.time()
+    main()
+    print(f"# done in {time.time() - t0:.1f}s")

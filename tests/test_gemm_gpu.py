@@ -1,0 +1,173 @@
+"""Numerics of the native gfx950 GEMM kernels against a plain PyTorch fp32/fp64
+reference of the same op (cdna rule: A=I with asymmetric B, exact small-integer
+data, full-tensor norm-relative error on random data)."""
+import pytest
+import torch
+
+from pytorch_distributed_matmul_benchmark_amd.ops import _native, gemm
+
+pytestmark = pytest.mark.gpu
+
+DT = {"bfloat16": torch.bfloat16, "float16": torch.float16, "float32": torch.float32}
+# norm-relative error budgets (output rounding dominates for 16-bit outputs)
+TOL = {torch.bfloat16: 8e-3, torch.float16: 1.5e-3, torch.float32: 2e-6}
+
+
+def _ref(A, B):
+    return torch.matmul(A.double(), B.double())
+
+
+def _relerr(C, R):
+    return ((C.double() - R).norm() / R.norm().clamp_min(1e-30)).item()
+
+
+def test_native_extension_is_loaded():
+    mod = _native.load(build_if_missing=False)
+    assert mod.ARCH == "gfx950"
+    assert mod.__file__.endswith(".so")
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 128), (1000, 1048, 320),
+                                   (300, 200, 128), (4352, 4352, 448)])
+def test_mfma256_exact_small_integers(dtype, M, N, K):
+    dt = DT[dtype]
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N)
+    A = torch.randint(-1, 2, (M, K), device="cuda", generator=g).to(dt)
+    B = torch.randint(-1, 2, (K, N), device="cuda", generator=g).to(dt)
+    assert gemm.kernel_for(A, B) == "pdmb_mfma256_nn"
+    C = gemm.matmul(A, B)
+    R = _ref(A, B)  # |R| <= K <= 448: exact in fp16; bf16 rounds > 256 only
+    if dt == torch.float16 or K <= 256:
+        assert torch.equal(C.double(), R)
+    else:
+        assert _relerr(C, R) < TOL[dt]
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+def test_mfma256_identity_asymmetric(dtype):
+    dt = DT[dtype]
+    n = 512
+    A = torch.eye(n, device="cuda", dtype=dt)
+    B = (torch.arange(n, device="cuda").view(n, 1) * 3 + torch.arange(n, device="cuda").view(1, n) * 0.5)
+    B = (B % 61).to(dt)
+    C = gemm.matmul(A, B)
+    assert torch.equal(C, B)
+    C2 = gemm.matmul(B, A)
+    assert torch.equal(C2, B)
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+@pytest.mark.parametrize("n", [2048, 4096])
+def test_mfma256_random(dtype, n):
+    dt = DT[dtype]
+    torch.manual_seed(0)
+    A = torch.randn(n, n, device="cuda", dtype=dt)
+    B = torch.randn(n, n, device="cuda", dtype=dt)
+    C = gemm.matmul(A, B)
+    R = torch.matmul(A.float(), B.float()).double()
+    assert _relerr(C, R) < TOL[dt]
+
+
+def test_mfma256_batched_and_broadcast():
+    dt = torch.bfloat16
+    torch.manual_seed(1)
+    A = torch.randn(3, 512, 320, device="cuda", dtype=dt)
+    B = torch.randn(3, 320, 768, device="cuda", dtype=dt)
+    B = torch.randn(3, 384, 768, device="cuda", dtype=dt)[:, :320]  # strided batch
+    C = gemm.bmm(A, B)
+    R = torch.bmm(A.double(), B.double())
+    assert _relerr(C, R) < TOL[dt]
+    B2 = torch.randn(320, 768, device="cuda", dtype=dt)
+    C2 = gemm.matmul(A, B2)
+    assert _relerr(C2, torch.matmul(A.double(), B2.double())) < TOL[dt]
+
+
+def test_mfma256_column_shard_views():
+    """matrix_parallel computes A @ B[:, shard] — a strided column view."""
+    dt = torch.bfloat16
+    torch.manual_seed(2)
+    A = torch.randn(1024, 1024, device="cuda", dtype=dt)
+    B = torch.randn(1024, 1024, device="cuda", dtype=dt)
+    for ws in (2, 4, 8):
+        cols = 1024 // ws
+        for r in range(ws):
+            Bs = B[:, r * cols:(r + 1) * cols]
+            C = gemm.matmul(A, Bs)
+            assert _relerr(C, _ref(A, Bs)) < TOL[dt]
+
+
+def test_out_is_written_in_place_and_stream_ordered():
+    dt = torch.bfloat16
+    A = torch.randn(512, 512, device="cuda", dtype=dt)
+    B = torch.randn(512, 512, device="cuda", dtype=dt)
+    out = torch.full((512, 512), float("nan"), device="cuda", dtype=dt)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        r = gemm.matmul(A, B, out=out)
+    s.synchronize()
+    assert r.data_ptr() == out.data_ptr()
+    assert not torch.isnan(out).any()
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16", "float32"])
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (100, 72, 50), (257, 129, 33), (640, 384, 512),
+                                   (129, 1000, 1001)])
+def test_generic_random(dtype, M, N, K):
+    dt = DT[dtype]
+    torch.manual_seed(M + N + K)
+    A = torch.randn(M, K, device="cuda", dtype=dt)
+    B = torch.randn(K, N, device="cuda", dtype=dt)
+    C = gemm.matmul(A, B, kernel="generic")
+    assert _relerr(C, _ref(A, B)) < TOL[dt]
+    # auto must also be right (it may pick either kernel)
+    C2 = gemm.matmul(A, B)
+    assert _relerr(C2, _ref(A, B)) < TOL[dt]
+
+
+def test_generic_unaligned_strides():
+    dt = torch.bfloat16
+    A = torch.randn(300, 203, device="cuda", dtype=dt)[:, 1:202]  # lda=203, misaligned base
+    B = torch.randn(201, 150, device="cuda", dtype=dt)
+    assert gemm.kernel_for(A, B) == "pdmb_generic_nn"
+    C = gemm.matmul(A, B)
+    assert _relerr(C, _ref(A, B)) < TOL[dt]
+
+
+def test_fp32_exact_mfma_path():
+    torch.manual_seed(3)
+    A = torch.randn(512, 512, device="cuda", dtype=torch.float32)
+    B = torch.randn(512, 512, device="cuda", dtype=torch.float32)
+    C = gemm.matmul(A, B)
+    assert gemm.kernel_for(A, B) == "pdmb_generic_nn"
+    assert _relerr(C, _ref(A, B)) < TOL[torch.float32]
+
+
+def test_zero_k():
+    A = torch.randn(64, 0, device="cuda", dtype=torch.bfloat16)
+    B = torch.randn(0, 64, device="cuda", dtype=torch.bfloat16)
+    out = torch.ones(64, 64, device="cuda", dtype=torch.bfloat16)
+    gemm.matmul(A, B, out=out)
+    assert (out == 0).all()
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_native_bench_loop(graph):
+    A = torch.randn(1024, 1024, device="cuda", dtype=torch.bfloat16)
+    B = torch.randn(1024, 1024, device="cuda", dtype=torch.bfloat16)
+    out = torch.empty(1024, 1024, device="cuda", dtype=torch.bfloat16)
+    ms = gemm.bench_matmul(A, B, out, iters=5, warmup=2, graph=graph)
+    assert ms > 0
+    assert _relerr(out, _ref(A, B)) < TOL[torch.bfloat16]
+
+
+def test_race_screen_repeated_runs():
+    """LDS-DMA pipeline race screen: identical outputs over many launches at several sizes."""
+    for n in (768, 2048, 2560):
+        torch.manual_seed(n)
+        A = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
+        B = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
+        ref = gemm.matmul(A, B)
+        assert _relerr(ref, _ref(A, B)) < TOL[torch.bfloat16]
+        for _ in range(20):
+            assert torch.equal(gemm.matmul(A, B), ref)
