@@ -1,0 +1,143 @@
+"""Shared pieces of every workload ("mode"): config, result, GEMM dispatch,
+seeded operand generation and the correctness check.
+
+A workload here is the reference's ``benchmark_*`` function
+(matmul_scaling_benchmark.py:69-238, backup/matmul_distributed_benchmark.py:
+35-174, backup/matmul_overlap_benchmark.py:36-278): allocate seeded random
+operands, warm up, align ranks, run the timed loop, return times + FLOPs.
+
+GEMMs on GPU run on this package's gfx950 MFMA kernels (``ops.gemm``), not
+on torch.matmul/hipBLASLt; ``backend="torch"`` exists only to A/B against
+the vendor library. All outputs are preallocated (the reference allocates a
+new C — and a new gather list — every iteration).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Dict, Optional
+
+import torch
+
+from ..ops import gemm as _gemm
+from ..parallel.dist import DistContext, barrier
+from ..utils.timing import synchronize
+
+
+@dataclass
+class Workload:
+    n: int
+    dtype: torch.dtype = torch.bfloat16
+    iters: int = 50
+    warmup: int = 10
+    seed: int = 0
+    backend: str = "native"     # native (gfx950 MFMA kernels) | torch (vendor BLAS, for A/B only)
+    kernel: str = "auto"        # native kernel selection (auto | mfma256 | generic)
+    batch: int = 4              # batch_parallel requested global batch (rounded up to a multiple of ws)
+    overlap: bool = False       # comm/compute overlap on a second stream
+    chunks: int = 4             # overlap granularity (row chunks per GEMM)
+    graph: bool = False         # independent: replay the timed loop as one hipGraph
+    check: bool = False         # verify the result against a float64 reference
+
+
+@dataclass
+class ModeResult:
+    mode: str
+    n: int
+    world_size: int
+    avg_ms: float                     # per-iteration time on this rank
+    flops_local: float                # FLOPs this rank executes per iteration
+    flops_total: float                # FLOPs all ranks execute per iteration
+    tflops: float                     # this rank's TFLOPS, mode-specific definition (see each mode)
+    compute_ms: Optional[float] = None
+    comm_ms: Optional[float] = None
+    compute_only_tflops: Optional[float] = None
+    relerr: Optional[float] = None
+    kernel: str = ""
+    extra: Dict[str, object] = field(default_factory=dict)
+
+
+def gemm_fn(w: Workload, device: torch.device) -> Callable:
+    """``mm(A, B, out)`` for this workload's device/backend (2-D or batched 3-D)."""
+    if device.type != "cuda" or w.backend == "torch":
+        def mm(A, B, out):
+            if A.dim() == 3:
+                return torch.bmm(A, B, out=out)
+            return torch.matmul(A, B, out=out)
+        return mm
+    if w.backend != "native":
+        raise ValueError(f"unknown backend {w.backend!r}")
+    kernel = w.kernel
+
+    def mm(A, B, out):
+        return _gemm.matmul(A, B, out=out, kernel=kernel)
+    return mm
+
+
+def kernel_label(w: Workload, A, B, out) -> str:
+    if A.device.type != "cuda":
+        return "torch.matmul(cpu)"
+    if w.backend == "torch":
+        return "torch.matmul(hipBLASLt)"
+    return _gemm.kernel_for(A, B, out, kernel=w.kernel)
+
+
+def generator(device: torch.device, seed: int) -> torch.Generator:
+    g = torch.Generator(device=device)
+    g.manual_seed(int(seed))
+    return g
+
+
+def randn(shape, w: Workload, device: torch.device, seed: int) -> torch.Tensor:
+    """N(0,1) operands (random, non-zero data matters on MI355X: DVFS runs
+    zero-filled GEMMs ~15-20% fast — cdna_hip_programming.md §5.4 rule 25)."""
+    return torch.randn(*shape, generator=generator(device, seed), device=device, dtype=w.dtype)
+
+
+def align_ranks(ctx: DistContext) -> None:
+    """Drain this rank's queue, then barrier (matmul_scaling_benchmark.py:78-82)."""
+    synchronize(ctx.device)
+    barrier(ctx)
+
+
+def sampled_relerr(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, rows: int = 64,
+                   seed: int = 1234) -> float:
+    """Norm-relative error of ``C`` vs a float64 ``A @ B`` on ``rows`` sampled rows
+    (all rows when M ≤ ``rows``). Replaces the dead, K-truncating
+    ``validate_result`` of matmul_scaling_benchmark.py:240-249."""
+    M = A.shape[-2]
+    if M <= rows:
+        idx = torch.arange(M, device=A.device)
+    else:
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        idx = torch.randperm(M, generator=g)[:rows].sort().values.to(A.device)
+    Ar = A.index_select(-2, idx).double()
+    ref = torch.matmul(Ar, B.double())
+    got = C.index_select(-2, idx).double()
+    den = ref.norm().clamp_min(1e-30)
+    return float(((got - ref).norm() / den).item())
+
+
+def allreduced_relerr(ctx: DistContext, A: torch.Tensor, B: torch.Tensor, C: torch.Tensor,
+                      rows: int = 64, seed: int = 4321) -> float:
+    """Check an all-reduced GEMM output: ``C`` must equal Σ_ranks A_r @ B_r.
+
+    Every rank picks the same sampled rows, computes its own float64 partial
+    product for them and the partials are SUM-all-reduced in float64, so the
+    whole compute → (overlapped) collective path is verified without moving
+    any operand between ranks. Collective: every rank must call it."""
+    import torch.distributed as dist
+
+    M = A.shape[-2]
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    idx = (torch.arange(M) if M <= rows else torch.randperm(M, generator=g)[:rows].sort().values)
+    idx = idx.to(A.device)
+    part = torch.matmul(A.index_select(-2, idx).double(), B.double())
+    if ctx.is_distributed:
+        dist.all_reduce(part)
+    got = C.index_select(-2, idx).double()
+    return float(((got - part).norm() / part.norm().clamp_min(1e-30)).item())
+
+
+def tolerance(dtype: torch.dtype) -> float:
+    """Norm-relative error budget of a fp32-accumulated GEMM with dtype outputs."""
+    return {torch.bfloat16: 1e-2, torch.float16: 2e-3, torch.float32: 1e-5}[dtype]

@@ -1,0 +1,147 @@
+"""``matrix_parallel`` mode: 1-D column-parallel GEMM + RCCL all-gather.
+
+Reference: matmul_scaling_benchmark.py:167-238. A is replicated, B is split
+by columns, each rank computes C_local = A @ B_local ([N, N/ws]) and the
+column blocks are all-gathered into a list of ws tensors (re-allocated each
+iteration, never concatenated). TFLOPS = 2N³ / t / ws per rank
+("portion"), system = AVG of that, "Actual" = 2N³ / t.
+
+Differences:
+  * Q15: A comes from one seed on every rank (replicated by construction),
+    and each B_local is the rank's column slice of ONE global B, so the
+    gathered result is exactly A @ B and can be checked.
+  * Q4: shards are padded to a uniform width (``column_shard``), so the
+    all-gather is valid for any N and ws; padding columns are zero.
+  * Q16: the gather target is one preallocated buffer
+    ``[ws*N, shard]`` filled by ``all_gather_into_tensor`` (block r =
+    C[:, r*shard:(r+1)*shard]); no per-iteration allocation and no list
+    copy-out.
+  * ``overlap=True``: C_local is computed in row chunks; chunk j is
+    all-gathered on the high-priority comm stream while chunk j+1 is
+    computed (event-ordered). Gather layout: per chunk ``[ws*rows_j, shard]``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ..parallel.comm import CommStream, current_stream, new_event
+from ..parallel.dist import DistContext
+from ..parallel.partition import column_shard, row_chunks
+from ..utils.metrics import gemm_flops, tflops_from
+from ..utils.timing import SegmentTimer, Stopwatch, synchronize, time_loop_ms
+from . import independent
+from .common import (ModeResult, Workload, align_ranks, gemm_fn, kernel_label, randn,
+                     sampled_relerr)
+
+
+def make_operands(w: Workload, ctx: DistContext):
+    """(A replicated, B_local padded column shard, shard) for this rank."""
+    dev, n, ws = ctx.device, w.n, ctx.world_size
+    sh = column_shard(n, ws, ctx.rank, align=8)
+    A = randn((n, n), w, dev, seed=10_000 + w.seed)
+    Bg = randn((n, n), w, dev, seed=10_001 + w.seed)   # the one global B
+    B_local = torch.zeros((n, sh.padded), device=dev, dtype=w.dtype)
+    if sh.width:
+        B_local[:, :sh.width].copy_(Bg[:, sh.start:sh.stop])
+    del Bg
+    return A, B_local, sh
+
+
+def assemble(gathered, n: int, ws: int) -> torch.Tensor:
+    """Full [N, N] C from gather buffer(s) of shape [ws*rows, shard] (drops padding).
+
+    ``gathered`` is one buffer or a list of per-row-chunk buffers."""
+    bufs = gathered if isinstance(gathered, (list, tuple)) else [gathered]
+    parts = []
+    for g in bufs:
+        rows = g.shape[0] // ws
+        parts.append(g.view(ws, rows, -1).permute(1, 0, 2).reshape(rows, -1)[:, :n])
+    return torch.cat(parts, dim=0)
+
+
+def run(w: Workload, ctx: DistContext) -> ModeResult:
+    ws = ctx.world_size
+    if ws == 1 or not ctx.is_distributed:
+        # matmul_scaling_benchmark.py:171-172 — one GPU does the whole product.
+        r = independent.run(w, ctx, mode_name="matrix_parallel")
+        return r
+    dev, n = ctx.device, w.n
+    A, B_local, sh = make_operands(w, ctx)
+    C_local = torch.empty((n, sh.padded), device=dev, dtype=w.dtype)
+    mm = gemm_fn(w, dev)
+    label = kernel_label(w, A, B_local, C_local)
+    flops_local = gemm_flops(n, sh.padded, n)
+    flops_total = gemm_flops(n, n, n)
+    extra = {"shard_cols": sh.padded, "overlap": bool(w.overlap)}
+
+    if not w.overlap:
+        # dim-0 concatenation [ws*N, shard] (the layout both gloo and RCCL accept);
+        # block r = gathered.view(ws, N, shard)[r] = C[:, r*shard:(r+1)*shard].
+        gathered = torch.empty((ws * n, sh.padded), device=dev, dtype=w.dtype)
+
+        def comm():
+            dist.all_gather_into_tensor(gathered, C_local)
+
+        for _ in range(w.warmup):
+            mm(A, B_local, C_local)
+            comm()
+        align_ranks(ctx)
+        seg = SegmentTimer(dev)
+        st = current_stream(dev)
+        seg.begin(st)
+        for _ in range(w.iters):
+            mm(A, B_local, C_local)
+            seg.mark("compute", st)
+            comm()
+            seg.mark("comm", st)
+        tot = seg.totals_ms()
+        it = max(w.iters, 1)
+        comp, cm = tot.get("compute", 0.0) / it, tot.get("comm", 0.0) / it
+        avg = comp + cm
+        full = (lambda: assemble(gathered, n, ws))
+    else:
+        rc = row_chunks(n, w.chunks)
+        extra["chunks"] = len(rc)
+        bufs = [torch.empty((ws * (e - s), sh.padded), device=dev, dtype=w.dtype) for s, e in rc]
+        cs = CommStream(dev)
+        ready = [new_event(dev) for _ in rc]
+        done = [new_event(dev) for _ in rc]
+        compute = current_stream(dev)
+
+        def step():
+            for j, (s, e) in enumerate(rc):
+                mm(A[s:e], B_local, C_local[s:e])
+                ready[j].record(compute)
+                cs.all_gather_into(bufs[j], C_local[s:e], after=ready[j], done=done[j])
+            if compute is not None:
+                for d in done:
+                    compute.wait_event(d)
+
+        for _ in range(w.warmup):
+            step()
+        align_ranks(ctx)
+        sw = Stopwatch(dev)
+        sw.start(compute)
+        for _ in range(w.iters):
+            step()
+        sw.stop(compute)
+        avg = sw.elapsed_ms() / max(w.iters, 1)
+        synchronize(dev)
+        k = max(1, min(w.iters, 10))
+        comp = time_loop_ms(lambda: mm(A, B_local, C_local), k, 1, dev) / k
+        cm = max(avg - comp, 0.0)
+        full = (lambda: assemble(bufs, n, ws))
+
+    res = ModeResult(mode="matrix_parallel", n=n, world_size=ws, avg_ms=avg,
+                     flops_local=flops_local, flops_total=flops_total,
+                     tflops=tflops_from(flops_total, avg / 1e3) / ws,
+                     compute_ms=comp, comm_ms=cm,
+                     compute_only_tflops=tflops_from(flops_local, comp / 1e3),
+                     kernel=label, extra=extra)
+    if w.check:
+        synchronize(dev)
+        C = full()
+        Bg = randn((n, n), w, dev, seed=10_001 + w.seed)
+        res.relerr = sampled_relerr(A, Bg, C)
+    return res

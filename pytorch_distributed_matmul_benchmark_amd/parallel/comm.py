@@ -1,0 +1,116 @@
+"""Communication streams with explicit event ordering (compute ∥ RCCL).
+
+The reference's overlap variants (backup/matmul_overlap_benchmark.py:93-278)
+put collectives on a side stream with no dependency on the GEMM that
+produced the buffer and drop the async handle, so the all-reduce can read a
+half-written C and the next GEMM can overwrite a buffer that is still being
+reduced. Here every hand-off is an event:
+
+    compute: GEMM(buf) → record(ready[buf])
+    comm:    wait(ready[buf]) → RCCL collective(buf) → record(done[buf])
+    compute: wait(done[buf]) before the next GEMM writes buf
+
+``CommStream.collective`` issues the RCCL op while the comm stream is
+current, so ProcessGroupNCCL orders its internal stream after the comm
+stream's prior work (the ready-event wait), and ``work.wait()`` makes the
+comm stream (not the host) wait for the collective, so ``done`` really
+means "reduced". On MI355X the comm stream is created with the highest
+priority so RCCL's workgroups are dispatched ahead of queued GEMM
+workgroups as CUs free up (the GEMM grid is ≫256 WGs at 1 WG/CU).
+
+On CPU tensors (gloo) streams/events are no-ops and collectives are
+synchronous, which keeps the same code path testable without a GPU.
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+class _NullEvent:
+    def record(self, stream=None):
+        pass
+
+    def wait(self, stream=None):
+        pass
+
+    def synchronize(self):
+        pass
+
+    def elapsed_time(self, other):
+        return 0.0
+
+
+def new_event(device: torch.device, timing: bool = False):
+    if device.type == "cuda":
+        return torch.cuda.Event(enable_timing=timing)
+    return _NullEvent()
+
+
+def new_stream(device: torch.device, high_priority: bool = False):
+    if device.type != "cuda":
+        return None
+    if high_priority:
+        lo, hi = torch.cuda.Stream.priority_range()
+        return torch.cuda.Stream(device=device, priority=hi)
+    return torch.cuda.Stream(device=device)
+
+
+def stream_ctx(stream):
+    return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+
+
+def current_stream(device: torch.device):
+    return torch.cuda.current_stream(device) if device.type == "cuda" else None
+
+
+class CommStream:
+    """A dedicated stream for RCCL collectives, ordered by events against compute."""
+
+    def __init__(self, device: torch.device, group=None, high_priority: bool = True):
+        self.device = device
+        self.group = group
+        self.stream = new_stream(device, high_priority=high_priority)
+
+    def wait_event(self, ev) -> None:
+        if self.stream is not None and ev is not None:
+            self.stream.wait_event(ev)
+
+    def collective(self, fn, *args, after=None, done=None, **kw):
+        """Run ``fn(*args, async_op=True, **kw)`` on the comm stream.
+
+        ``after``: event the collective must wait for (the producer GEMM).
+        ``done``: event recorded once the collective has completed on the GPU.
+        """
+        with stream_ctx(self.stream):
+            if after is not None:
+                self.wait_event(after)
+            work = fn(*args, group=self.group, async_op=True, **kw)
+            if work is not None:
+                work.wait()  # NCCL: stream-side wait only; gloo: blocks (CPU)
+            if done is not None:
+                done.record(self.stream)
+        return work
+
+    def all_reduce(self, t: torch.Tensor, after=None, done=None):
+        return self.collective(dist.all_reduce, t, after=after, done=done)
+
+    def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor, after=None, done=None):
+        return self.collective(dist.all_gather_into_tensor, out, inp, after=after, done=done)
+
+    def synchronize(self) -> None:
+        if self.stream is not None:
+            self.stream.synchronize()
+
+
+def all_reduce_(t: torch.Tensor, group=None) -> None:
+    """Synchronous (stream-ordered) in-place SUM all-reduce on the current stream."""
+    dist.all_reduce(t, group=group)
+
+
+def all_gather_into_(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+    dist.all_gather_into_tensor(out, inp, group=group)
+

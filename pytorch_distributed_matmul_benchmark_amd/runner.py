@@ -1,0 +1,301 @@
+"""The per-size benchmark driver behind every CLI entry point.
+
+One implementation of the reference's four copy-pasted ``run_benchmarks`` /
+``main`` pairs (SURVEY §1 "no shared module"):
+
+  kind          entry point                               reference
+  ----------    ---------------------------------------   -------------------------------------------
+  basic         matmul_benchmark.py                       matmul_benchmark.py:81-200
+  scaling       matmul_scaling_benchmark.py               matmul_scaling_benchmark.py:251-404
+  distributed   backup/matmul_distributed_benchmark.py    backup/matmul_distributed_benchmark.py:176-319
+  overlap       backup/matmul_overlap_benchmark.py        backup/matmul_overlap_benchmark.py:280-414
+
+Same flags and defaults (``--sizes 4096 8192 16384 --iterations 50
+--warmup 10 --dtype bfloat16 [--mode …]``), same rank-0 lines, plus opt-in
+MI355X flags: ``--device``, ``--batch``, ``--overlap``, ``--chunks``,
+``--graph``, ``--backend``, ``--kernel``, ``--check``, ``--json``,
+``--single-gpu-tflops``.
+
+Per size, every rank: run the mode → agree on success (error-flag
+all-reduce) → reduce metrics → rank 0 prints and records.
+"""
+from __future__ import annotations
+
+import argparse
+import traceback
+from typing import Dict, List, Optional
+
+import torch
+
+from .models import DISTRIBUTED_MODES, OVERLAP_MODES, SCALING_MODES, ModeResult, Workload, run_mode
+from .models.common import tolerance
+from .parallel.dist import (DistContext, all_ok, barrier, cleanup_distributed, reduce_scalar,
+                            setup_distributed, verify_collectives)
+from .utils.metrics import (balance_efficiency, bytes_per_element, dtype_from_name, dtype_name,
+                            overlap_efficiency, peak_for_device, percent_of_peak,
+                            scaling_efficiency, square_flops, tflops_from)
+from .utils.report import Reporter, device_banner
+
+KINDS = {
+    "basic": dict(title="Matrix Multiplication Benchmark", width=60, modes=("independent",),
+                  default_mode="independent",
+                  desc="Distributed PyTorch Matrix Multiplication Benchmark (MI355X)"),
+    "scaling": dict(title="Matrix Multiplication Scaling Benchmark", width=70,
+                    modes=SCALING_MODES, default_mode="independent",
+                    desc="Matrix Multiplication Scaling Benchmark (MI355X)"),
+    "distributed": dict(title="Distributed Matrix Multiplication Benchmark", width=70,
+                        modes=DISTRIBUTED_MODES, default_mode="data_parallel",
+                        desc="Distributed Matrix Multiplication Benchmark with Communication"),
+    "overlap": dict(title="Overlapped Communication/Computation Benchmark", width=70,
+                    modes=OVERLAP_MODES, default_mode="overlap",
+                    desc="Overlapped Communication/Computation Benchmark"),
+}
+
+
+def build_parser(kind: str) -> argparse.ArgumentParser:
+    k = KINDS[kind]
+    p = argparse.ArgumentParser(description=k["desc"])
+    p.add_argument("--sizes", type=int, nargs="+", default=[4096, 8192, 16384],
+                   help="Matrix sizes to benchmark (default: 4096 8192 16384)")
+    p.add_argument("--iterations", type=int, default=50,
+                   help="Number of iterations per benchmark (default: 50)")
+    p.add_argument("--warmup", type=int, default=10,
+                   help="Number of warmup iterations (default: 10)")
+    p.add_argument("--dtype", type=str, default="bfloat16",
+                   choices=["float32", "float16", "bfloat16"],
+                   help="Data type for matrices (default: bfloat16)")
+    if kind != "basic":
+        p.add_argument("--mode", type=str, default=k["default_mode"], choices=list(k["modes"]),
+                       help=f"Benchmark mode (default: {k['default_mode']})")
+    g = p.add_argument_group("MI355X options")
+    g.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"],
+                   help="auto: this rank's GPU if present, else CPU (torch.matmul reference path)")
+    g.add_argument("--backend", default="native", choices=["native", "torch"],
+                   help="GEMM implementation on GPU: native gfx950 MFMA kernels (default) or "
+                        "torch.matmul/hipBLASLt for A/B comparison")
+    g.add_argument("--kernel", default="auto", choices=["auto", "mfma256", "generic"],
+                   help="native kernel selection")
+    g.add_argument("--batch", type=int, default=4,
+                   help="batch_parallel global batch (rounded up to a multiple of the world size)")
+    g.add_argument("--overlap", action="store_true",
+                   help="batch/matrix_parallel: overlap the collective with the GEMM on a second stream")
+    g.add_argument("--chunks", type=int, default=4, help="overlap granularity (row chunks per GEMM)")
+    g.add_argument("--graph", action="store_true",
+                   help="independent: replay the timed loop as one hipGraph")
+    g.add_argument("--check", action="store_true",
+                   help="verify results against a float64 reference (sampled rows)")
+    g.add_argument("--seed", type=int, default=0)
+    g.add_argument("--json", default=None, help="append one JSON record per result to this file")
+    g.add_argument("--single-gpu-tflops", type=float, default=None,
+                   help="measured 1-GPU TFLOPS for the 'efficiency vs 1 GPU' line")
+    g.add_argument("--timeout", type=float, default=600.0, help="process-group timeout (s)")
+    g.add_argument("--debug", action="store_true", help="print tracebacks of failed sizes")
+    return p
+
+
+def _mode_of(kind: str, args) -> str:
+    return getattr(args, "mode", None) or KINDS[kind]["default_mode"]
+
+
+def _workload(args, n: int, dtype: torch.dtype) -> Workload:
+    return Workload(n=n, dtype=dtype, iters=args.iterations, warmup=args.warmup, seed=args.seed,
+                    backend=args.backend, kernel=args.kernel, batch=args.batch,
+                    overlap=args.overlap, chunks=args.chunks, graph=args.graph, check=args.check)
+
+
+def _aggregate(ctx: DistContext, r: ModeResult) -> Dict[str, Optional[float]]:
+    """Cross-rank reductions (collective: every rank calls this in the same order)."""
+    agg: Dict[str, Optional[float]] = {}
+    agg["avg_ms"] = reduce_scalar(ctx, r.avg_ms, "avg")
+    agg["max_ms"] = reduce_scalar(ctx, r.avg_ms, "max")
+    agg["tflops_sum"] = reduce_scalar(ctx, r.tflops, "sum")
+    agg["tflops_avg"] = reduce_scalar(ctx, r.tflops, "avg")
+    agg["compute_ms"] = reduce_scalar(ctx, r.compute_ms or 0.0, "avg")
+    agg["comm_ms"] = reduce_scalar(ctx, r.comm_ms or 0.0, "avg")
+    agg["compute_only_tflops"] = reduce_scalar(ctx, r.compute_only_tflops or 0.0, "avg")
+    agg["relerr"] = reduce_scalar(ctx, r.relerr if r.relerr is not None else -1.0, "max")
+    if agg["relerr"] is not None and agg["relerr"] < 0:
+        agg["relerr"] = None
+    # Whole-node throughput: all FLOPs executed in one iteration ÷ slowest rank's time.
+    agg["node_tflops"] = tflops_from(r.flops_total, agg["max_ms"] / 1e3)
+    return agg
+
+
+def _peak(ctx: DistContext):
+    if not ctx.is_cuda:
+        return None
+    p = torch.cuda.get_device_properties(ctx.device)
+    return peak_for_device(torch.cuda.get_device_name(ctx.device), getattr(p, "gcnArchName", ""))
+
+
+def _print_results(kind: str, mode: str, rep: Reporter, ctx: DistContext, n: int,
+                   dtype: torch.dtype, r: ModeResult, agg: Dict, args) -> Dict:
+    ws = ctx.world_size
+    extra: Dict[str, object] = {}
+    rep.line(f"\nResults for {n}x{n}:")
+    peak = _peak(ctx)
+    if kind == "basic":
+        rep.line(f"  - Average time per multiplication: {agg['avg_ms']:.3f} ms")
+        rep.line(f"  - TFLOPS per GPU: {r.tflops:.2f}")
+        rep.line(f"  - Total TFLOPS (all GPUs): {agg['tflops_sum']:.2f}")
+        rep.line(f"  - Required FLOPs per operation: {square_flops(n) / 1e12:.2f} TFLOPs")
+        pct = percent_of_peak(r.tflops, peak, dtype)
+        if pct is not None:
+            rep.line(f"  - GPU Efficiency: {pct:.1f}% of {peak.gpu} theoretical peak "
+                     f"({peak.for_dtype(dtype):.1f} TFLOPS dense)")
+    elif kind == "scaling":
+        rep.line(f"  - Average time per operation: {agg['avg_ms']:.3f} ms")
+        if mode == "independent":
+            rep.line(f"  - TFLOPS per GPU: {r.tflops:.2f}")
+            rep.line(f"  - Total system TFLOPS: {agg['tflops_sum']:.2f}")
+            bal = balance_efficiency(agg["tflops_sum"], r.tflops, ws)
+            rep.line(f"  - Scaling efficiency: {bal:.1f}% (rank balance: sum / (ws x rank 0))")
+        elif mode == "batch_parallel":
+            lb = r.extra.get("local_batch")
+            gb = r.extra.get("global_batch")
+            rep.line(f"  - Compute time: {agg['compute_ms']:.3f} ms, Comm time: {agg['comm_ms']:.3f} ms"
+                     + (" (overlapped; comm = exposed part)" if r.extra.get("overlap") else ""))
+            rep.line(f"  - TFLOPS per GPU: {r.tflops:.2f}")
+            rep.line(f"  - Total system TFLOPS: {r.tflops * ws:.2f}")
+            rep.line(f"  - Processing {gb} total batches across {ws} GPU(s) ({lb} per GPU)")
+        else:
+            rep.line(f"  - Compute time: {agg['compute_ms']:.3f} ms, Comm time: {agg['comm_ms']:.3f} ms"
+                     + (" (overlapped; comm = exposed part)" if r.extra.get("overlap") else ""))
+            rep.line(f"  - TFLOPS per GPU (portion): {r.tflops:.2f}")
+            rep.line(f"  - Effective system TFLOPS: {agg['tflops_avg']:.2f}")
+            rep.line(f"  - Each GPU processes 1/{ws} of the matrix")
+        total_flops = {"independent": square_flops(n, ws),
+                       "batch_parallel": square_flops(n, r.extra.get("global_batch", 4)),
+                       "matrix_parallel": square_flops(n)}[mode]
+        actual = tflops_from(total_flops, agg["avg_ms"] / 1e3)
+        extra["actual_tflops"] = actual
+        rep.line(f"  - Actual TFLOPS (total FLOPs / time): {actual:.2f}")
+    elif kind == "distributed":
+        rep.line(f"  - Total time per operation: {agg['avg_ms']:.3f} ms")
+        if mode != "independent" and ws > 1:
+            rep.line(f"  - Compute time: {agg['compute_ms']:.3f} ms")
+            rep.line(f"  - Communication time: {agg['comm_ms']:.3f} ms")
+            ov = 100.0 * agg["comm_ms"] / agg["avg_ms"] if agg["avg_ms"] > 0 else 0.0
+            rep.line(f"  - Communication overhead: {ov:.1f}%")
+        if mode == "independent":
+            rep.line(f"  - TFLOPS per GPU: {r.tflops:.2f}")
+            rep.line(f"  - Total TFLOPS (all GPUs): {agg['tflops_sum']:.2f}")
+        else:
+            rep.line(f"  - Effective TFLOPS: {agg['tflops_avg']:.2f}")
+        rep.line(f"  - Required FLOPs per operation: {square_flops(n) / 1e12:.2f} TFLOPs")
+        if ws > 1 and mode != "independent":
+            eff = overlap_efficiency(agg["compute_ms"], agg["avg_ms"])
+            rep.line(f"  - Scaling efficiency: {eff:.1f}% (compute / total time)")
+    else:  # overlap
+        rep.line(f"  - Average time per operation: {agg['avg_ms']:.3f} ms")
+        actual = tflops_from(square_flops(n), agg["avg_ms"] / 1e3)
+        extra["actual_tflops"] = actual
+        rep.line(f"  - Actual TFLOPS: {actual:.2f} (FLOPs/Time)")
+        rep.line(f"  - Compute-only TFLOPS: {agg['compute_only_tflops']:.2f} "
+                 f"(GEMM alone, {agg['compute_ms']:.3f} ms)")
+        if ws > 1:
+            eff = overlap_efficiency(agg["compute_ms"], agg["avg_ms"])
+            rep.line(f"  - Communication overhead: {100.0 - eff:.1f}% of each iteration is exposed comm")
+            rep.line(f"  - Note: In data parallel, each GPU does full matrix multiply")
+            rep.line(f"  - System is achieving {actual * ws:.2f} TFLOPS across {ws} GPUs")
+        rep.line(f"  - Required FLOPs per operation: {square_flops(n) / 1e12:.2f} TFLOPs")
+
+    # MI355X additions, identical for every kind.
+    rep.line(f"  - Node TFLOPS (all FLOPs / slowest rank): {agg['node_tflops']:.2f}")
+    if args.single_gpu_tflops:
+        eff = scaling_efficiency(agg["node_tflops"], ws, args.single_gpu_tflops)
+        extra["scaling_efficiency_vs_1gpu"] = eff
+        rep.line(f"  - Scaling efficiency vs 1 GPU: {eff:.1f}%")
+    if kind != "basic":
+        pct = percent_of_peak(r.tflops if mode != "matrix_parallel" else r.compute_only_tflops or 0.0,
+                              peak, dtype)
+        if pct is not None:
+            extra["pct_peak"] = pct
+    rep.line(f"  - Kernel: {r.kernel}")
+    if agg.get("relerr") is not None:
+        ok = agg["relerr"] < tolerance(dtype)
+        extra["check_ok"] = ok
+        rep.line(f"  - Check: max rel. error {agg['relerr']:.2e} ({'PASS' if ok else 'FAIL'})")
+    return extra
+
+
+def run_benchmarks(kind: str, ctx: DistContext, rep: Reporter, args) -> List[Dict]:
+    k = KINDS[kind]
+    mode = _mode_of(kind, args)
+    dtype = dtype_from_name(args.dtype)
+    rep.line(f"\n{'=' * k['width']}")
+    rep.line(k["title"])
+    rep.line("=" * k["width"])
+    rep.line("Configuration:")
+    if kind != "basic":
+        rep.line(f"  - Mode: {mode}")
+    rep.line(f"  - Number of GPUs: {ctx.world_size}" if ctx.is_cuda
+             else f"  - Number of processes: {ctx.world_size}")
+    rep.line(f"  - Data type: {dtype}")
+    rep.line(f"  - Device: {'GPU (' + torch.cuda.get_device_name(ctx.device) + ')' if ctx.is_cuda else 'CPU'}")
+    rep.line(f"  - GEMM: {args.backend}" + (" (gfx950 MFMA kernels)" if args.backend == "native" and ctx.is_cuda else ""))
+    rep.line(f"  - Iterations per test: {args.iterations}")
+    rep.line(f"  - Warmup iterations: {args.warmup}")
+    rep.line(f"{'=' * k['width']}\n")
+    out = []
+    for n in args.sizes:
+        if n <= 0:
+            rep.line(f"\n  ERROR: invalid size {n}")
+            continue
+        bpe = bytes_per_element(dtype)
+        rep.line(f"\nBenchmarking {n}x{n} matrix multiplication:")
+        rep.line(f"  - Memory per matrix: {n * n * bpe / (1024 ** 3):.2f} GB ({dtype_name(dtype)})")
+        if kind == "basic":
+            rep.line(f"  - Total memory for A, B, C: {3 * n * n * bpe / (1024 ** 3):.2f} GB")
+        else:
+            rep.line(f"  - Mode: {mode}")
+        if kind in ("distributed", "overlap"):
+            rep.line("  - Running warmup and benchmark...")
+        res, err = None, None
+        try:
+            res = run_mode(mode, _workload(args, n, dtype), ctx)
+        except torch.cuda.OutOfMemoryError:
+            err = f"Out of memory for {n}x{n} matrices"
+        except Exception as e:  # reported by every rank, never swallowed
+            err = f"{type(e).__name__}: {e}"
+            if getattr(args, "debug", False):
+                traceback.print_exc()
+        if err is not None:
+            print(f"[rank {ctx.rank}] ERROR: {err}", flush=True)
+        if not all_ok(ctx, err is None):
+            rep.line(f"\n  ERROR: {err or 'failed on another rank'}")
+            out.append({"n": n, "mode": mode, "error": err or "failed on another rank"})
+        else:
+            agg = _aggregate(ctx, res)
+            extra = _print_results(kind, mode, rep, ctx, n, dtype, res, agg, args)
+            rec = {"script": kind, "mode": mode, "n": n, "dtype": dtype_name(dtype),
+                   "world_size": ctx.world_size, "device": ctx.device.type,
+                   "backend": args.backend, "iterations": args.iterations,
+                   "warmup": args.warmup, "tflops_rank0": res.tflops, "kernel": res.kernel,
+                   "flops_per_iter_total": res.flops_total, **agg, **extra, **res.extra}
+            rep.record(rec)
+            out.append(rec)
+        del res
+        if ctx.is_cuda:
+            torch.cuda.empty_cache()
+        barrier(ctx)
+    return out
+
+
+def main(kind: str, argv=None) -> int:
+    args = build_parser(kind).parse_args(argv)
+    ctx = setup_distributed(args.device, timeout_s=args.timeout)
+    rep = Reporter(is_main=ctx.is_main, json_path=args.json)
+    device_banner(rep, ctx.device)
+    try:
+        if ctx.world_size > 1 and kind != "basic" and not verify_collectives(ctx):
+            rep.line("ERROR: Collective operations verification failed!")
+            return 1
+        run_benchmarks(kind, ctx, rep, args)
+    finally:
+        cleanup_distributed()
+    w = KINDS[kind]["width"]
+    rep.line(f"\n{'=' * w}")
+    rep.line("Benchmark completed!")
+    rep.line(f"{'=' * w}\n")
+    return 0

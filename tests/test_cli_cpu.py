@@ -1,0 +1,110 @@
+"""CLI entry points end-to-end on CPU (BASELINE config #1: fp32 torch.matmul on CPU),
+single process and under torchrun with gloo; output keeps the reference's
+scraped substrings (backup/compare_benchmarks.py:22-26)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ENV = dict(os.environ, PYTHONUNBUFFERED="1", OMP_NUM_THREADS="2")
+
+
+def _run(args, timeout=240):
+    r = subprocess.run(args, cwd="/tmp", capture_output=True, text=True, timeout=timeout, env=ENV)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return r.stdout
+
+
+def _torchrun(nproc, script, *args, port=29700):
+    return _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                 f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1",
+                 f"--master-port={port}", os.path.join(ROOT, script), *args])
+
+
+def test_basic_cpu_fp32(tmp_path):
+    js = tmp_path / "r.jsonl"
+    out = _run([sys.executable, os.path.join(ROOT, "matmul_benchmark.py"), "--device", "cpu",
+                "--sizes", "256", "384", "--iterations", "2", "--warmup", "1",
+                "--dtype", "float32", "--check", "--json", str(js)])
+    for s in ("Results for 256x256", "Average time per multiplication", "TFLOPS per GPU",
+              "Total TFLOPS (all GPUs)", "Required FLOPs per operation", "Benchmark completed!",
+              "Check: max rel. error"):
+        assert s in out, s
+    assert "FAIL" not in out
+    recs = [json.loads(l) for l in js.read_text().splitlines()]
+    assert [r["n"] for r in recs] == [256, 384]
+    assert all(r["check_ok"] for r in recs)
+    assert recs[0]["tflops_rank0"] > 0
+
+
+@pytest.mark.parametrize("mode", ["independent", "batch_parallel", "matrix_parallel"])
+def test_scaling_single_process(mode):
+    out = _run([sys.executable, os.path.join(ROOT, "matmul_scaling_benchmark.py"), "--device",
+                "cpu", "--sizes", "200", "--iterations", "2", "--warmup", "1", "--dtype",
+                "float32", "--mode", mode, "--check"])
+    assert "Actual TFLOPS (total FLOPs / time)" in out
+    assert "PASS" in out and "FAIL" not in out and "ERROR" not in out
+
+
+@pytest.mark.parametrize("mode,extra", [("independent", []), ("batch_parallel", []),
+                                        ("batch_parallel", ["--overlap", "--chunks", "2"]),
+                                        ("matrix_parallel", []),
+                                        ("matrix_parallel", ["--overlap", "--chunks", "3"])])
+def test_scaling_torchrun_gloo(mode, extra, tmp_path):
+    js = tmp_path / "r.jsonl"
+    out = _torchrun(2, "matmul_scaling_benchmark.py", "--device", "cpu", "--sizes", "300",
+                    "--iterations", "2", "--warmup", "1", "--dtype", "float32", "--mode", mode,
+                    "--check", "--json", str(js), *extra)
+    assert "Collective operations verified successfully across 2" in out
+    assert "Results for 300x300" in out
+    assert "PASS" in out and "FAIL" not in out and "ERROR" not in out
+    rec = json.loads(js.read_text().splitlines()[-1])
+    assert rec["world_size"] == 2 and rec["mode"] == mode
+    if mode == "batch_parallel":
+        assert rec["global_batch"] == 4 and rec["local_batch"] == 2
+    if mode == "matrix_parallel":
+        assert rec["shard_cols"] == 152
+
+
+def test_batch_parallel_ws3_reports_real_batch(tmp_path):
+    out = _torchrun(3, "matmul_scaling_benchmark.py", "--device", "cpu", "--sizes", "128",
+                    "--iterations", "1", "--warmup", "1", "--dtype", "float32", "--mode",
+                    "batch_parallel", "--check", port=29701)
+    assert "Processing 6 total batches across 3 GPU(s) (2 per GPU)" in out
+    assert "PASS" in out
+
+
+@pytest.mark.parametrize("mode", ["independent", "data_parallel", "model_parallel"])
+def test_backup_distributed(mode):
+    out = _torchrun(2, "backup/matmul_distributed_benchmark.py", "--device", "cpu", "--sizes",
+                    "256", "--iterations", "2", "--warmup", "1", "--mode", mode, "--check",
+                    port=29702)
+    assert "Total time per operation" in out and "PASS" in out and "ERROR" not in out
+    if mode != "independent":
+        assert "Communication overhead" in out
+
+
+@pytest.mark.parametrize("mode", ["no_overlap", "overlap", "pipeline"])
+def test_backup_overlap(mode):
+    out = _torchrun(2, "backup/matmul_overlap_benchmark.py", "--device", "cpu", "--sizes", "256",
+                    "--iterations", "3", "--warmup", "1", "--mode", mode, "--check", port=29703)
+    assert "Actual TFLOPS" in out and "Compute-only TFLOPS" in out
+    assert "PASS" in out and "ERROR" not in out
+
+
+def test_compare_benchmarks_any_cwd():
+    out = _run([sys.executable, os.path.join(ROOT, "backup", "compare_benchmarks.py"), "--gpus",
+                "2", "--dtype", "float32", "--size", "128", "--extra",
+                "--device cpu --sizes 128 --iterations 1 --warmup 1"], timeout=400)
+    assert out.count("Results for 128x128") == 4
+    assert "FAILED" not in out
+
+
+def test_launcher_single_process():
+    out = _run(["bash", os.path.join(ROOT, "run_scaling_benchmark.sh"), "1", "matrix_parallel",
+                "float32", "--device", "cpu", "--sizes", "128", "--iterations", "1",
+                "--warmup", "1"])
+    assert "Running in single GPU mode" in out and "Results for 128x128" in out
