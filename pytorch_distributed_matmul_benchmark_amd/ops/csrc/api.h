@@ -10,6 +10,8 @@ enum Kernel : int {
   kAuto = 0,      // fastest kernel that supports the problem
   kMfma256 = 1,   // gemm_mfma256.hip (LDS-DMA, 256x256, ping-pong)
   kGeneric = 2,   // gemm_generic.hip (any shape)
+  kMfma256b = 3,  // gemm_mfma256.hip, DMA issued in the read slot (SCHED 1)
+  kMfma256c = 4,  // SCHED 1 + fragment reads balanced over the read slots (SCHED 2)
 };
 
 struct Problem {

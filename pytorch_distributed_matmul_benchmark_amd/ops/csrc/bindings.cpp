@@ -130,5 +130,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("KERNEL_AUTO") = (int)pdmb::kAuto;
   m.attr("KERNEL_MFMA256") = (int)pdmb::kMfma256;
   m.attr("KERNEL_GENERIC") = (int)pdmb::kGeneric;
+  m.attr("KERNEL_MFMA256B") = (int)pdmb::kMfma256b;
+  m.attr("KERNEL_MFMA256C") = (int)pdmb::kMfma256c;
   m.attr("ARCH") = "gfx950";
 }

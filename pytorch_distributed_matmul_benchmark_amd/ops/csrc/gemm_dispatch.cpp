@@ -13,7 +13,7 @@
 namespace pdmb {
 
 bool gemm256_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
-hipError_t gemm256_launch(int dt, GemmArgs a, hipStream_t stream);
+hipError_t gemm256_launch(int dt, GemmArgs a, int sched, hipStream_t stream);
 hipError_t gemm_generic_launch(int dt, GemmArgs a, bool vec, hipStream_t stream);
 
 static GemmArgs to_args(const Problem& p) {
@@ -47,8 +47,10 @@ static bool generic_vec_ok(const Problem& p) {
 int resolve_kernel(const Problem& p, int kernel) {
   const GemmArgs a = to_args(p);
   const bool fast = gemm256_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
-  if (kernel == kAuto) return fast ? kMfma256 : kGeneric;
+  if (kernel == kAuto) return fast ? kMfma256c : kGeneric;
   if (kernel == kMfma256) return fast ? kMfma256 : -1;
+  if (kernel == kMfma256b) return fast ? kMfma256b : -1;
+  if (kernel == kMfma256c) return fast ? kMfma256c : -1;
   if (kernel == kGeneric) return kGeneric;
   return -1;
 }
@@ -69,7 +71,9 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     }
     return hipSuccess;
   }
-  if (k == kMfma256) return gemm256_launch(p.dtype, a, stream);
+  if (k == kMfma256) return gemm256_launch(p.dtype, a, 0, stream);
+  if (k == kMfma256b) return gemm256_launch(p.dtype, a, 1, stream);
+  if (k == kMfma256c) return gemm256_launch(p.dtype, a, 2, stream);
   return gemm_generic_launch(p.dtype, a, generic_vec_ok(p), stream);
 }
 
@@ -127,6 +131,10 @@ const char* kernel_name(int kernel) {
       return "pdmb_mfma256_nn";
     case kGeneric:
       return "pdmb_generic_nn";
+    case kMfma256b:
+      return "pdmb_mfma256b_nn";
+    case kMfma256c:
+      return "pdmb_mfma256c_nn";
     default:
       return "auto";
   }

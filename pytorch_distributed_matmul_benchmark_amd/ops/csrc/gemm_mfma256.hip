@@ -24,13 +24,19 @@
 //    columns of one row -> 8-byte stores in the epilogue.
 //  * Ping-pong schedule: each K-tile is 4 phases (one 64x32 quadrant of the
 //    wave tile x K=64 = 16 MFMAs). A phase is two barrier-separated slots:
-//    R (ds_read fragments) and C (issue 2 LDS-DMA + 16 MFMA). Waves 4..7
-//    run one slot behind waves 0..3, so on every SIMD one wave does MFMA
-//    while its partner reads LDS.
+//    R (ds_read fragments + issue one LDS-DMA unit) and C (16 MFMA). Waves
+//    4..7 run one slot behind waves 0..3, so on every SIMD one wave does
+//    MFMA while its partner reads LDS and issues the next DMA.
+//    Three schedules are kept for A/B (kernel ids in api.h); SCHED 2 is the
+//    default: 0 = DMA issued in the C slot (the first version), 1 = DMA in
+//    the R slot, 2 = 1 + reads balanced to 8 per R slot by prefetching the
+//    next tile's A0 fragments in phase 3 into a second A register set.
+//    Measured on MI355X, 16384^3 bf16 random data: 1315 / 1370 / 1440 TF
+//    (hipBLASLt 1362 on the same data).
 //  * LDS-DMA units (A-half = 16 KiB, B-half = 16 KiB) are refilled as soon
-//    as their last reader of tile t-2 has retired (WAR: one phase later),
-//    so every unit has ~5 phases of flight time. The wait is a counted
-//    s_waitcnt vmcnt(8/10) once per slot, never vmcnt(0) in the loop;
+//    as the last reader of their previous contents has retired, so every
+//    unit has ~5-6 phases of flight time. The wait is a counted
+//    s_waitcnt vmcnt(10) once per slot, never vmcnt(0) in the loop;
 //    barriers are raw s_barrier (a __syncthreads would drain the DMA).
 //  * XCD-aware tile order (common.h: map_tile).
 //
@@ -179,46 +185,135 @@ __device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[8][4], const s16x8 (&r
   __builtin_amdgcn_s_setprio(0);
 }
 
+#define PDMB_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+
 // One K-tile (4 phases) from LDS stage STG. Phase P = 4t+q issues unit P+7.
-template <int DT, int STG>
+//
+// SCHED 0: the unit's LDS-DMA is issued in the compute slot, ahead of the
+//   16 MFMAs (vmcnt 8 after the read slot, 10 after the compute slot).
+// SCHED 1: the DMA is issued in the READ slot, right after the fragment
+//   reads, so its issue cost overlaps the partner wave's MFMAs instead of
+//   delaying this wave's own (cdna_hip_programming.md §5 8-phase template:
+//   "ds-load subtile; stage prefetch; barrier; MFMA"). Moving the issue one
+//   slot earlier makes two things explicit:
+//   WAR — the unit refilled in phase P was last read in the read slot of
+//     P-1 (or earlier); every wave waits lgkmcnt(0) before the barrier that
+//     closes its read slot, so by the time the group one slot ahead issues
+//     the DMA, all reads of the old contents have returned.
+//   RAW — after issuing unit P+7 a wave waits vmcnt(10): units <= P+2 have
+//     landed, which the read slot of P+1 (one barrier later for the lagging
+//     group) needs. Each unit now gets one more slot of flight time.
+template <int DT, int STG, int SCHED>
 __device__ __forceinline__ void tile_body(const Ctx& c, char* smem, int t, f32x4 (&acc)[8][4],
-                                          s16x8 (&ra)[4][2], s16x8 (&rb0)[2][2],
-                                          s16x8 (&rb1)[2][2]) {
-  // phase q=0: quadrant (0,0)
-  read_a<STG, 0>(c, smem, ra);
-  read_b<STG, 0>(c, smem, rb0);
-  PDMB_VMCNT(8);
-  PDMB_SLOT_BARRIER();
-  issue_unit<3, STG ^ 1>(c, smem, t + 1);
-  mma_quadrant<DT, 0, 0>(acc, ra, rb0);
-  PDMB_VMCNT(10);
-  PDMB_SLOT_BARRIER();
-  // phase q=1: quadrant (0,1)
-  read_b<STG, 1>(c, smem, rb1);
-  PDMB_VMCNT(8);
-  PDMB_SLOT_BARRIER();
-  issue_unit<0, STG>(c, smem, t + 2);
-  mma_quadrant<DT, 0, 1>(acc, ra, rb1);
-  PDMB_VMCNT(10);
-  PDMB_SLOT_BARRIER();
-  // phase q=2: quadrant (1,1)
-  read_a<STG, 1>(c, smem, ra);
-  PDMB_VMCNT(8);
-  PDMB_SLOT_BARRIER();
-  issue_unit<1, STG>(c, smem, t + 2);
-  mma_quadrant<DT, 1, 1>(acc, ra, rb1);
-  PDMB_VMCNT(10);
-  PDMB_SLOT_BARRIER();
-  // phase q=3: quadrant (1,0) — operands already in registers
-  PDMB_VMCNT(8);
-  PDMB_SLOT_BARRIER();
-  issue_unit<2, STG>(c, smem, t + 2);
-  mma_quadrant<DT, 1, 0>(acc, ra, rb0);
-  PDMB_VMCNT(10);
-  PDMB_SLOT_BARRIER();
+                                          s16x8 (&ra)[4][2], s16x8 (&ra2)[4][2],
+                                          s16x8 (&rb0)[2][2], s16x8 (&rb1)[2][2]) {
+  if constexpr (SCHED == 0) {
+    // phase q=0: quadrant (0,0)
+    read_a<STG, 0>(c, smem, ra);
+    read_b<STG, 0>(c, smem, rb0);
+    PDMB_VMCNT(8);
+    PDMB_SLOT_BARRIER();
+    issue_unit<3, STG ^ 1>(c, smem, t + 1);
+    mma_quadrant<DT, 0, 0>(acc, ra, rb0);
+    PDMB_VMCNT(10);
+    PDMB_SLOT_BARRIER();
+    // phase q=1: quadrant (0,1)
+    read_b<STG, 1>(c, smem, rb1);
+    PDMB_VMCNT(8);
+    PDMB_SLOT_BARRIER();
+    issue_unit<0, STG>(c, smem, t + 2);
+    mma_quadrant<DT, 0, 1>(acc, ra, rb1);
+    PDMB_VMCNT(10);
+    PDMB_SLOT_BARRIER();
+    // phase q=2: quadrant (1,1)
+    read_a<STG, 1>(c, smem, ra);
+    PDMB_VMCNT(8);
+    PDMB_SLOT_BARRIER();
+    issue_unit<1, STG>(c, smem, t + 2);
+    mma_quadrant<DT, 1, 1>(acc, ra, rb1);
+    PDMB_VMCNT(10);
+    PDMB_SLOT_BARRIER();
+    // phase q=3: quadrant (1,0) — operands already in registers
+    PDMB_VMCNT(8);
+    PDMB_SLOT_BARRIER();
+    issue_unit<2, STG>(c, smem, t + 2);
+    mma_quadrant<DT, 1, 0>(acc, ra, rb0);
+    PDMB_VMCNT(10);
+    PDMB_SLOT_BARRIER();
+  } else if constexpr (SCHED == 2) {
+    // SCHED 1 with the fragment reads balanced over the four read slots
+    // (8 reads each): A0 of the NEXT tile is read in phase 3 into a second
+    // A register set (ra2 = A0, ra = A1), so phase 0 reads only B0.
+    // RAW: phase 3 (P = 4t+3) may read units <= P+1 = 4(t+1)+0 = next A0.
+    // WAR: next tile's A0 unit is refilled in phase 4(t+1)+1 > P+1.
+    // phase q=0: quadrant (0,0) — A0 already in ra2
+    read_b<STG, 0>(c, smem, rb0);
+    issue_unit<3, STG ^ 1>(c, smem, t + 1);
+    PDMB_LGKM0();
+    PDMB_VMCNT(10);
+    PDMB_SLOT_BARRIER();
+    mma_quadrant<DT, 0, 0>(acc, ra2, rb0);
+    PDMB_SLOT_BARRIER();
+    // phase q=1: quadrant (0,1)
+    read_b<STG, 1>(c, smem, rb1);
+    issue_unit<0, STG>(c, smem, t + 2);
+    PDMB_LGKM0();
+    PDMB_VMCNT(10);
+    PDMB_SLOT_BARRIER();
+    mma_quadrant<DT, 0, 1>(acc, ra2, rb1);
+    PDMB_SLOT_BARRIER();
+    // phase q=2: quadrant (1,1)
+    read_a<STG, 1>(c, smem, ra);
+    issue_unit<1, STG>(c, smem, t + 2);
+    PDMB_LGKM0();
+    PDMB_VMCNT(10);
+    PDMB_SLOT_BARRIER();
+    mma_quadrant<DT, 1, 1>(acc, ra, rb1);
+    PDMB_SLOT_BARRIER();
+    // phase q=3: quadrant (1,0); prefetch next tile's A0 fragments
+    read_a<STG ^ 1, 0>(c, smem, ra2);
+    issue_unit<2, STG>(c, smem, t + 2);
+    PDMB_LGKM0();
+    PDMB_VMCNT(10);
+    PDMB_SLOT_BARRIER();
+    mma_quadrant<DT, 1, 0>(acc, ra, rb0);
+    PDMB_SLOT_BARRIER();
+  } else {
+    // phase q=0: quadrant (0,0)
+    read_b<STG, 0>(c, smem, rb0);
+    read_a<STG, 0>(c, smem, ra);
+    issue_unit<3, STG ^ 1>(c, smem, t + 1);
+    PDMB_LGKM0();
+    PDMB_VMCNT(10);
+    PDMB_SLOT_BARRIER();
+    mma_quadrant<DT, 0, 0>(acc, ra, rb0);
+    PDMB_SLOT_BARRIER();
+    // phase q=1: quadrant (0,1)
+    read_b<STG, 1>(c, smem, rb1);
+    issue_unit<0, STG>(c, smem, t + 2);
+    PDMB_LGKM0();
+    PDMB_VMCNT(10);
+    PDMB_SLOT_BARRIER();
+    mma_quadrant<DT, 0, 1>(acc, ra, rb1);
+    PDMB_SLOT_BARRIER();
+    // phase q=2: quadrant (1,1)
+    read_a<STG, 1>(c, smem, ra);
+    issue_unit<1, STG>(c, smem, t + 2);
+    PDMB_LGKM0();
+    PDMB_VMCNT(10);
+    PDMB_SLOT_BARRIER();
+    mma_quadrant<DT, 1, 1>(acc, ra, rb1);
+    PDMB_SLOT_BARRIER();
+    // phase q=3: quadrant (1,0) — operands already in registers
+    issue_unit<2, STG>(c, smem, t + 2);
+    PDMB_VMCNT(10);
+    PDMB_SLOT_BARRIER();
+    mma_quadrant<DT, 1, 0>(acc, ra, rb0);
+    PDMB_SLOT_BARRIER();
+  }
 }
 
-template <int DT>
+template <int DT, int SCHED>
 __global__ void __launch_bounds__(NTHREADS, 2) gemm256_nn(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
@@ -283,7 +378,7 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm256_nn(GemmArgs a) {
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  s16x8 ra[4][2], rb0[2][2], rb1[2][2];
+  s16x8 ra[4][2], ra2[4][2], rb0[2][2], rb1[2][2];
 
   // Prologue: units 0..6 = A0,B0,B1,A1 of tile 0 and A0,B0,B1 of tile 1.
   issue_unit<0, 0>(c, smem, 0);
@@ -297,11 +392,14 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm256_nn(GemmArgs a) {
   PDMB_SLOT_BARRIER();
   // Stagger: waves 4..7 run one slot behind waves 0..3.
   if (wr == 1) PDMB_SLOT_BARRIER();
+  // SCHED 2 reads each tile's A0 fragments one phase early; tile 0's here
+  // (units 0,1 were retired by every wave before the prologue barrier).
+  if constexpr (SCHED == 2) read_a<0, 0>(c, smem, ra2);
 
   const int nk = c.nk;
   for (int t = 0; t < nk; t += 2) {
-    tile_body<DT, 0>(c, smem, t, acc, ra, rb0, rb1);
-    if (t + 1 < nk) tile_body<DT, 1>(c, smem, t + 1, acc, ra, rb0, rb1);
+    tile_body<DT, 0, SCHED>(c, smem, t, acc, ra, ra2, rb0, rb1);
+    if (t + 1 < nk) tile_body<DT, 1, SCHED>(c, smem, t + 1, acc, ra, ra2, rb0, rb1);
   }
   if (wr == 0) PDMB_SLOT_BARRIER();
   PDMB_VMCNT(0);  // drain the clamped tail DMAs before the LDS is released
@@ -343,7 +441,7 @@ bool gemm256_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b
   return true;
 }
 
-hipError_t gemm256_launch(int dt, GemmArgs a, hipStream_t stream) {
+hipError_t gemm256_launch(int dt, GemmArgs a, int sched, hipStream_t stream) {
   a.tiles_m = (a.M + k256::BM - 1) / k256::BM;
   a.tiles_n = (a.N + k256::BN - 1) / k256::BN;
   a.supertile = (a.tiles_m % 16 == 0 && a.tiles_n % 16 == 0) ? 1 : 0;
@@ -351,10 +449,17 @@ hipError_t gemm256_launch(int dt, GemmArgs a, hipStream_t stream) {
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
   dim3 grid((unsigned)nblocks), block(k256::NTHREADS);
-  if (dt == kBF16)
-    hipLaunchKernelGGL(k256::gemm256_nn<kBF16>, grid, block, 0, stream, a);
-  else
-    hipLaunchKernelGGL(k256::gemm256_nn<kF16>, grid, block, 0, stream, a);
+#define PDMB_LAUNCH256(D, S) hipLaunchKernelGGL((k256::gemm256_nn<D, S>), grid, block, 0, stream, a)
+  if (dt == kBF16) {
+    if (sched == 2) PDMB_LAUNCH256(kBF16, 2);
+    else if (sched == 1) PDMB_LAUNCH256(kBF16, 1);
+    else PDMB_LAUNCH256(kBF16, 0);
+  } else {
+    if (sched == 2) PDMB_LAUNCH256(kF16, 2);
+    else if (sched == 1) PDMB_LAUNCH256(kF16, 1);
+    else PDMB_LAUNCH256(kF16, 0);
+  }
+#undef PDMB_LAUNCH256
   return hipGetLastError();
 }
 

@@ -18,8 +18,9 @@ import torch
 
 from . import _native
 
-KERNELS = {"auto": 0, "mfma256": 1, "generic": 2}
-KERNEL_NAMES = {0: "auto", 1: "pdmb_mfma256_nn", 2: "pdmb_generic_nn", -1: "unsupported"}
+KERNELS = {"auto": 0, "mfma256": 1, "generic": 2, "mfma256b": 3, "mfma256c": 4}
+KERNEL_NAMES = {0: "auto", 1: "pdmb_mfma256_nn", 2: "pdmb_generic_nn", 3: "pdmb_mfma256b_nn", 4: "pdmb_mfma256c_nn",
+                -1: "unsupported"}
 SUPPORTED_DTYPES = (torch.float32, torch.float16, torch.bfloat16)
 
 

@@ -1,0 +1,23 @@
+#!/bin/bash
+# PMC passes over the GEMM arms (each counter set in its own rocprofv3 run,
+# kernel-trace + pmc only). Stops at any crash/timeout exit status.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/pmc
+mkdir -p $OUT
+N=${N:-16384}
+KS=${KS:-auto}
+pass() {
+  local name=$1; shift
+  timeout -k 10 240 rocprofv3 --kernel-trace "$@" --output-format csv -d $OUT/$name -o run -- \
+      python3 scripts/prof_gemm_arms.py --n $N --reps 3 --kernels $KS > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "pass $name rc=$rc"
+  case $rc in 124|134|137|139) exit $rc;; esac
+  return 0
+}
+pass trace
+pass p1 --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU
+pass p2 --pmc GRBM_GUI_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES
+pass p3 --pmc GRBM_GUI_ACTIVE TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum
+find $OUT -name "*.csv" | head -50

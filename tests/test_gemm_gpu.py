@@ -27,16 +27,20 @@ def test_native_extension_is_loaded():
     assert mod.__file__.endswith(".so")
 
 
+FAST = ["mfma256", "mfma256b", "mfma256c"]
+
+
+@pytest.mark.parametrize("kernel", FAST)
 @pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 128), (1000, 1048, 320),
                                    (300, 200, 128), (4352, 4352, 448)])
-def test_mfma256_exact_small_integers(dtype, M, N, K):
+def test_mfma256_exact_small_integers(dtype, M, N, K, kernel):
     dt = DT[dtype]
     g = torch.Generator(device="cuda").manual_seed(M * 7 + N)
     A = torch.randint(-1, 2, (M, K), device="cuda", generator=g).to(dt)
     B = torch.randint(-1, 2, (K, N), device="cuda", generator=g).to(dt)
-    assert gemm.kernel_for(A, B) == "pdmb_mfma256_nn"
-    C = gemm.matmul(A, B)
+    assert gemm.kernel_for(A, B, kernel=kernel) == gemm.KERNEL_NAMES[gemm.KERNELS[kernel]]
+    C = gemm.matmul(A, B, kernel=kernel)
     R = _ref(A, B)  # |R| <= K <= 448: exact in fp16; bf16 rounds > 256 only
     if dt == torch.float16 or K <= 256:
         assert torch.equal(C.double(), R)
@@ -57,29 +61,31 @@ def test_mfma256_identity_asymmetric(dtype):
     assert torch.equal(C2, B)
 
 
+@pytest.mark.parametrize("kernel", FAST)
 @pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
 @pytest.mark.parametrize("n", [2048, 4096])
-def test_mfma256_random(dtype, n):
+def test_mfma256_random(dtype, n, kernel):
     dt = DT[dtype]
     torch.manual_seed(0)
     A = torch.randn(n, n, device="cuda", dtype=dt)
     B = torch.randn(n, n, device="cuda", dtype=dt)
-    C = gemm.matmul(A, B)
+    C = gemm.matmul(A, B, kernel=kernel)
     R = torch.matmul(A.float(), B.float()).double()
     assert _relerr(C, R) < TOL[dt]
 
 
-def test_mfma256_batched_and_broadcast():
+@pytest.mark.parametrize("kernel", FAST)
+def test_mfma256_batched_and_broadcast(kernel):
     dt = torch.bfloat16
     torch.manual_seed(1)
     A = torch.randn(3, 512, 320, device="cuda", dtype=dt)
     B = torch.randn(3, 320, 768, device="cuda", dtype=dt)
     B = torch.randn(3, 384, 768, device="cuda", dtype=dt)[:, :320]  # strided batch
-    C = gemm.bmm(A, B)
+    C = gemm.bmm(A, B, kernel=kernel)
     R = torch.bmm(A.double(), B.double())
     assert _relerr(C, R) < TOL[dt]
     B2 = torch.randn(320, 768, device="cuda", dtype=dt)
-    C2 = gemm.matmul(A, B2)
+    C2 = gemm.matmul(A, B2, kernel=kernel)
     assert _relerr(C2, torch.matmul(A.double(), B2.double())) < TOL[dt]
 
 
@@ -161,13 +167,16 @@ def test_native_bench_loop(graph):
     assert _relerr(out, _ref(A, B)) < TOL[torch.bfloat16]
 
 
-def test_race_screen_repeated_runs():
-    """LDS-DMA pipeline race screen: identical outputs over many launches at several sizes."""
-    for n in (768, 2048, 2560):
+@pytest.mark.parametrize("kernel", FAST)
+def test_race_screen_repeated_runs(kernel):
+    """LDS-DMA pipeline race screen: identical outputs over many launches at several
+    sizes, including one big enough to keep every CU busy for many rounds."""
+    for n in (768, 2048, 2560, 8192):
         torch.manual_seed(n)
         A = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
         B = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
-        ref = gemm.matmul(A, B)
-        assert _relerr(ref, _ref(A, B)) < TOL[torch.bfloat16]
-        for _ in range(20):
-            assert torch.equal(gemm.matmul(A, B), ref)
+        ref = gemm.matmul(A, B, kernel=kernel)
+        R = torch.matmul(A.float(), B.float()).double()
+        assert _relerr(ref, R) < TOL[torch.bfloat16]
+        for _ in range(10 if n == 8192 else 20):
+            assert torch.equal(gemm.matmul(A, B, kernel=kernel), ref)
