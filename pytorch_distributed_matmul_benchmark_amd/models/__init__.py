@@ -7,6 +7,7 @@
 """
 from __future__ import annotations
 
+from enum import Enum
 from functools import partial
 
 from . import batch_parallel, data_parallel, independent, matrix_parallel, model_parallel, overlap
@@ -24,11 +25,32 @@ MODES = {
 }
 
 SCALING_MODES = ("independent", "batch_parallel", "matrix_parallel")
+
+
+class ScalingMode(Enum):
+    """matmul_scaling_benchmark.py:10-13."""
+    INDEPENDENT = "independent"
+    BATCH_PARALLEL = "batch_parallel"
+    MATRIX_PARALLEL = "matrix_parallel"
+
+
+class BenchmarkMode(Enum):
+    """backup/matmul_distributed_benchmark.py:10-13 and backup/matmul_overlap_benchmark.py:11-14."""
+    INDEPENDENT = "independent"
+    DATA_PARALLEL = "data_parallel"
+    MODEL_PARALLEL = "model_parallel"
+    NO_OVERLAP = "no_overlap"
+    OVERLAP = "overlap"
+    PIPELINE = "pipeline"
+
+
 DISTRIBUTED_MODES = ("independent", "data_parallel", "model_parallel")
 OVERLAP_MODES = ("no_overlap", "overlap", "pipeline")
 
 
-def run_mode(name: str, w: Workload, ctx) -> ModeResult:
+def run_mode(name, w: Workload, ctx) -> ModeResult:
+    if isinstance(name, Enum):
+        name = name.value
     try:
         fn = MODES[name]
     except KeyError:
@@ -37,4 +59,4 @@ def run_mode(name: str, w: Workload, ctx) -> ModeResult:
 
 
 __all__ = ["MODES", "SCALING_MODES", "DISTRIBUTED_MODES", "OVERLAP_MODES", "ModeResult",
-           "Workload", "run_mode"]
+           "Workload", "run_mode", "ScalingMode", "BenchmarkMode"]

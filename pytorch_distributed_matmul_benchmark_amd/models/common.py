@@ -117,6 +117,15 @@ def sampled_relerr(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, rows: int 
     return float(((got - ref).norm() / den).item())
 
 
+def validate_result(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor,
+                    tol: Optional[float] = None) -> bool:
+    """``C ≈ A @ B`` over the FULL reduction dimension (the reference's
+    ``validate_result``, matmul_scaling_benchmark.py:240-249, truncates K to
+    10 and is never called). Sampled rows, float64 reference, norm-relative
+    tolerance of the dtype (``tolerance``) unless ``tol`` is given."""
+    return sampled_relerr(A, B, C) < (tol if tol is not None else tolerance(C.dtype))
+
+
 def allreduced_relerr(ctx: DistContext, A: torch.Tensor, B: torch.Tensor, C: torch.Tensor,
                       rows: int = 64, seed: int = 4321) -> float:
     """Check an all-reduced GEMM output: ``C`` must equal Σ_ranks A_r @ B_r.

@@ -35,6 +35,7 @@ from .utils.metrics import (balance_efficiency, bytes_per_element, dtype_from_na
                             overlap_efficiency, peak_for_device, percent_of_peak,
                             scaling_efficiency, square_flops, tflops_from)
 from .utils.report import Reporter, device_banner
+from .utils.timing import marker
 
 KINDS = {
     "basic": dict(title="Matrix Multiplication Benchmark", width=60, modes=("independent",),
@@ -90,6 +91,10 @@ def build_parser(kind: str) -> argparse.ArgumentParser:
                    help="measured 1-GPU TFLOPS for the 'efficiency vs 1 GPU' line")
     g.add_argument("--timeout", type=float, default=600.0, help="process-group timeout (s)")
     g.add_argument("--debug", action="store_true", help="print tracebacks of failed sizes")
+    g.add_argument("--profile", action="store_true",
+                   help="wrap each size in a roctx range (rocprofv3 --marker-trace --kernel-trace)")
+    g.add_argument("--resume", action="store_true",
+                   help="with --json: skip sizes whose (script, mode, dtype, ws) record already exists")
     return p
 
 
@@ -219,6 +224,29 @@ def _print_results(kind: str, mode: str, rep: Reporter, ctx: DistContext, n: int
     return extra
 
 
+def _completed(args, kind: str, mode: str, ctx: DistContext) -> set:
+    """Sizes already recorded in ``--json`` for this (script, mode, dtype, ws, backend).
+
+    Every rank reads the same file, so all ranks skip the same sizes."""
+    import json
+    import os
+
+    if not args.json or not os.path.exists(args.json):
+        return set()
+    got = set()
+    with open(args.json) as f:
+        for line in f:
+            try:
+                r = json.loads(line)
+            except ValueError:
+                continue
+            if (r.get("script") == kind and r.get("mode") == mode and r.get("dtype") == args.dtype
+                    and r.get("world_size") == ctx.world_size and r.get("backend") == args.backend
+                    and bool(r.get("overlap", False)) == bool(args.overlap) and "error" not in r):
+                got.add(int(r["n"]))
+    return got
+
+
 def run_benchmarks(kind: str, ctx: DistContext, rep: Reporter, args) -> List[Dict]:
     k = KINDS[kind]
     mode = _mode_of(kind, args)
@@ -238,9 +266,13 @@ def run_benchmarks(kind: str, ctx: DistContext, rep: Reporter, args) -> List[Dic
     rep.line(f"  - Warmup iterations: {args.warmup}")
     rep.line(f"{'=' * k['width']}\n")
     out = []
+    done = _completed(args, kind, mode, ctx) if getattr(args, "resume", False) else set()
     for n in args.sizes:
         if n <= 0:
             rep.line(f"\n  ERROR: invalid size {n}")
+            continue
+        if n in done:
+            rep.line(f"\nSkipping {n}x{n}: already recorded in {args.json} (--resume)")
             continue
         bpe = bytes_per_element(dtype)
         rep.line(f"\nBenchmarking {n}x{n} matrix multiplication:")
@@ -253,7 +285,9 @@ def run_benchmarks(kind: str, ctx: DistContext, rep: Reporter, args) -> List[Dic
             rep.line("  - Running warmup and benchmark...")
         res, err = None, None
         try:
-            res = run_mode(mode, _workload(args, n, dtype), ctx)
+            with marker(f"{kind}/{mode}/{n}x{n}/{dtype_name(dtype)}/ws{ctx.world_size}",
+                        enabled=getattr(args, "profile", False) and ctx.is_cuda):
+                res = run_mode(mode, _workload(args, n, dtype), ctx)
         except torch.cuda.OutOfMemoryError:
             err = f"Out of memory for {n}x{n} matrices"
         except Exception as e:  # reported by every rank, never swallowed

@@ -10,6 +10,7 @@ once, after the loop — no host synchronisation inside the timed region.
 """
 from __future__ import annotations
 
+import contextlib
 import time
 from typing import Dict, List, Optional
 
@@ -117,3 +118,20 @@ class Timings(dict):
 
     def get_ms(self, key: str, default: Optional[float] = 0.0) -> float:
         return float(self.get(key, default))
+
+
+@contextlib.contextmanager
+def marker(name: str, enabled: bool = True):
+    """A named range in the profiler timeline (roctx on PyTorch-ROCm:
+    ``torch.cuda.nvtx`` is routed to roctx). Visible with
+    ``rocprofv3 --marker-trace --kernel-trace``. No-op when disabled."""
+    if not enabled:
+        yield
+        return
+    import torch.cuda.nvtx as nvtx
+
+    nvtx.range_push(name)
+    try:
+        yield
+    finally:
+        nvtx.range_pop()

@@ -108,3 +108,30 @@ def test_launcher_single_process():
                 "float32", "--device", "cpu", "--sizes", "128", "--iterations", "1",
                 "--warmup", "1"])
     assert "Running in single GPU mode" in out and "Results for 128x128" in out
+
+
+def test_resume_skips_recorded_sizes(tmp_path):
+    js = tmp_path / "r.jsonl"
+    args = [sys.executable, os.path.join(ROOT, "matmul_scaling_benchmark.py"), "--device", "cpu",
+            "--iterations", "1", "--warmup", "0", "--dtype", "float32", "--json", str(js)]
+    _run(args + ["--sizes", "64"])
+    out = _run(args + ["--sizes", "64", "96", "--resume"])
+    assert "Skipping 64x64" in out and "Results for 96x96" in out
+    assert len(js.read_text().splitlines()) == 2
+
+
+def test_mode_enums_and_validate_result():
+    import torch
+
+    from pytorch_distributed_matmul_benchmark_amd.models import (BenchmarkMode, ScalingMode,
+                                                                 Workload, run_mode)
+    from pytorch_distributed_matmul_benchmark_amd.models.common import validate_result
+    from pytorch_distributed_matmul_benchmark_amd.parallel.dist import DistContext
+
+    assert [m.value for m in ScalingMode] == ["independent", "batch_parallel", "matrix_parallel"]
+    assert BenchmarkMode("pipeline") is BenchmarkMode.PIPELINE
+    r = run_mode(ScalingMode.BATCH_PARALLEL,
+                 Workload(n=64, dtype=torch.float32, iters=1, warmup=0, check=True), DistContext())
+    assert r.relerr < 1e-5 and r.extra["global_batch"] == 4
+    A, B = torch.randn(70, 33), torch.randn(33, 20)
+    assert validate_result(A, B, A @ B) and not validate_result(A, B, A @ B + 0.1)
