@@ -12,6 +12,9 @@ enum Kernel : int {
   kGeneric = 2,   // gemm_generic.hip (any shape)
   kMfma256b = 3,  // gemm_mfma256.hip, DMA issued in the read slot (SCHED 1)
   kMfma256c = 4,  // SCHED 1 + fragment reads balanced over the read slots (SCHED 2)
+  kF32_256 = 6,   // gemm_f32_256.hip: exact-fp32 MFMA, 256x256 LDS-DMA tile
+  kF32_256s = 7,  // same, DMA issue staggered between the two waves of a SIMD
+  kMfma256Stamp = 5,  // diagnostic: SCHED 2 with in-kernel barrier-wait stamps (needs a debug buffer)
 };
 
 struct Problem {
@@ -41,5 +44,8 @@ hipError_t bench_gemm(const Problem& p, int kernel, int iters, int warmup, bool 
                       hipStream_t stream, float* ms);
 
 const char* kernel_name(int kernel);
+
+// Diagnostic builds write per-wave stamps here (device memory; nullptr = off).
+void set_debug_buffer(void* p);
 
 }  // namespace pdmb

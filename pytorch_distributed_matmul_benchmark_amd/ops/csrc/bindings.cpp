@@ -115,6 +115,17 @@ double bench(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int6
 
 std::string kernel_name(int64_t k) { return pdmb::kernel_name((int)k); }
 
+// Diagnostic: set (or clear, with None) the device buffer the stamp kernel writes.
+void set_debug_buffer(c10::optional<at::Tensor> buf) {
+  if (buf.has_value()) {
+    TORCH_CHECK(buf->is_cuda() && buf->scalar_type() == at::kLong && buf->is_contiguous(),
+                "pdmb: debug buffer must be a contiguous int64 GPU tensor");
+    pdmb::set_debug_buffer(buf->data_ptr());
+  } else {
+    pdmb::set_debug_buffer(nullptr);
+  }
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -127,10 +138,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("B"), py::arg("out"), py::arg("iters"), py::arg("warmup"),
         py::arg("graph") = false, py::arg("kernel") = 0);
   m.def("kernel_name", &kernel_name);
+  m.def("set_debug_buffer", &set_debug_buffer, py::arg("buf") = py::none());
   m.attr("KERNEL_AUTO") = (int)pdmb::kAuto;
   m.attr("KERNEL_MFMA256") = (int)pdmb::kMfma256;
   m.attr("KERNEL_GENERIC") = (int)pdmb::kGeneric;
   m.attr("KERNEL_MFMA256B") = (int)pdmb::kMfma256b;
   m.attr("KERNEL_MFMA256C") = (int)pdmb::kMfma256c;
+  m.attr("KERNEL_MFMA256_STAMP") = (int)pdmb::kMfma256Stamp;
+  m.attr("KERNEL_F32_256") = (int)pdmb::kF32_256;
   m.attr("ARCH") = "gfx950";
 }

@@ -85,7 +85,45 @@ struct GemmArgs {
   int batch;
   int tiles_m, tiles_n;  // output tiles per batch element
   int supertile;         // 1: XCD-aware 16x16 super-tile order, 0: grouped order
+  unsigned long long* dbg;  // diagnostic builds only (in-kernel stamps); nullptr otherwise
 };
+
+// ---- LDS-DMA helpers (shared by the LDS-DMA kernels) ----------------------
+// Raw buffer descriptor (gfx950 dword3 = 0x00020000: 32-bit data format,
+// raw addressing). Bytes at or beyond num_records read as zero, which
+// handles the M / N edges with no masking in the K-loop. num_records is
+// clamped with 32-bit scalar logic (SALU has no 64-bit less-than).
+__device__ __forceinline__ u32x4 make_rsrc(const char* base, long long bytes) {
+  const unsigned long long p = (unsigned long long)base;
+  const unsigned int hi = (unsigned int)((unsigned long long)bytes >> 32);
+  const unsigned int lo = (unsigned int)bytes;
+  const unsigned int nr = (hi & 0x80000000u) ? 0u : (hi ? 0xffffffffu : lo);
+  u32x4 r;
+  r.x = (unsigned int)p;
+  r.y = (unsigned int)(p >> 32) & 0xffffu;
+  r.z = nr;
+  r.w = 0x00020000u;
+  return r;
+}
+
+// One LDS-DMA wave-instruction: 64 lanes x 16 B from rsrc+voff into LDS at
+// lds_base + lane*16. Written as inline asm on purpose: hipcc (ROCm 7.2)
+// otherwise treats every later ds_read_b64_tr_b16 as possibly aliasing the
+// in-flight DMA and inserts s_waitcnt vmcnt(0), which drains the pipeline.
+// The count is ours to keep: every wait on these is an explicit vmcnt(N).
+// M0 is saved/restored around the statement (compiler-reserved register).
+__device__ __forceinline__ void dma16(u32x4 rsrc, uint32_t voff, uint32_t lds_base) {
+  unsigned int keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rsrc), "s"(lds_base)
+      : "memory");
+}
 
 // ---- block -> output tile mapping -------------------------------------
 // Speed only (never correctness): workgroups are dealt round-robin over the

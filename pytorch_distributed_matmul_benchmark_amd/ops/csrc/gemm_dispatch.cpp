@@ -15,6 +15,12 @@ namespace pdmb {
 bool gemm256_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 hipError_t gemm256_launch(int dt, GemmArgs a, int sched, hipStream_t stream);
 hipError_t gemm_generic_launch(int dt, GemmArgs a, bool vec, hipStream_t stream);
+bool gemm_f32_256_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
+hipError_t gemm_f32_256_launch(GemmArgs a, bool stagger, hipStream_t stream);
+
+static unsigned long long* g_debug_buffer = nullptr;
+
+void set_debug_buffer(void* p) { g_debug_buffer = (unsigned long long*)p; }
 
 static GemmArgs to_args(const Problem& p) {
   GemmArgs a{};
@@ -31,6 +37,7 @@ static GemmArgs to_args(const Problem& p) {
   a.sB = p.sB;
   a.sC = p.sC;
   a.batch = p.batch < 1 ? 1 : p.batch;
+  a.dbg = g_debug_buffer;
   return a;
 }
 
@@ -47,10 +54,15 @@ static bool generic_vec_ok(const Problem& p) {
 int resolve_kernel(const Problem& p, int kernel) {
   const GemmArgs a = to_args(p);
   const bool fast = gemm256_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
-  if (kernel == kAuto) return fast ? kMfma256c : kGeneric;
+  const bool f32fast = p.dtype == kF32 &&
+                       gemm_f32_256_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
+  if (kernel == kAuto) return fast ? kMfma256c : (f32fast ? kF32_256s : kGeneric);
+  if (kernel == kF32_256) return f32fast ? kF32_256 : -1;
+  if (kernel == kF32_256s) return f32fast ? kF32_256s : -1;
   if (kernel == kMfma256) return fast ? kMfma256 : -1;
   if (kernel == kMfma256b) return fast ? kMfma256b : -1;
   if (kernel == kMfma256c) return fast ? kMfma256c : -1;
+  if (kernel == kMfma256Stamp) return (fast && p.dtype == kBF16) ? kMfma256Stamp : -1;
   if (kernel == kGeneric) return kGeneric;
   return -1;
 }
@@ -74,6 +86,9 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
   if (k == kMfma256) return gemm256_launch(p.dtype, a, 0, stream);
   if (k == kMfma256b) return gemm256_launch(p.dtype, a, 1, stream);
   if (k == kMfma256c) return gemm256_launch(p.dtype, a, 2, stream);
+  if (k == kMfma256Stamp) return gemm256_launch(p.dtype, a, 3, stream);
+  if (k == kF32_256) return gemm_f32_256_launch(a, false, stream);
+  if (k == kF32_256s) return gemm_f32_256_launch(a, true, stream);
   return gemm_generic_launch(p.dtype, a, generic_vec_ok(p), stream);
 }
 
@@ -135,6 +150,12 @@ const char* kernel_name(int kernel) {
       return "pdmb_mfma256b_nn";
     case kMfma256c:
       return "pdmb_mfma256c_nn";
+    case kMfma256Stamp:
+      return "pdmb_mfma256c_stamp";
+    case kF32_256:
+      return "pdmb_f32_256_nn";
+    case kF32_256s:
+      return "pdmb_f32_256s_nn";
     default:
       return "auto";
   }

@@ -1,0 +1,210 @@
+// gemm_f32_256.hip — exact-fp32 C = A @ B (row-major NN) on gfx950 MFMA
+// v_mfma_f32_16x16x4_f32 (f32 in, f32 accumulate; gfx950 has no TF32/xf32,
+// so this IS the fp32 path of the reference's `--dtype float32`,
+// matmul_benchmark.py:163-174 / matmul_scaling_benchmark.py:365-374).
+//
+// fp32 MFMA runs at 64 FLOP/clk/SIMD (1/16 of bf16), so a 256×256 tile is
+// MFMA-bound by a wide margin: per K-tile of 32 each wave issues 256 MFMAs
+// (8192 cycles) against 48 LDS reads and 8 LDS-DMA pieces. The design goal is
+// therefore just "never let the MFMA pipe idle":
+//  * 256×256 tile, BK = 32, 8 waves (2 M × 4 N), each wave 128×64 =
+//    8×4 MFMA tiles → 128 accumulators/lane, 2 waves per SIMD.
+//  * Operands land in LDS by LDS-DMA, double-buffered (2 × 65 KiB). One
+//    barrier per K-tile; the next tile's DMA is in flight for a whole tile.
+//  * A image [256][32] fp32 (128-B rows), 16-B chunk c of row r stored at
+//    c ^ ((r>>1)&7) (swizzle applied on the DMA source address): the
+//    ds_read_b128 A fragments are conflict-free. One b128 read gives a lane
+//    4 consecutive k of its row: k-step e of the 16-k block uses element e,
+//    i.e. MFMA k-slot g holds k = 4g + e (a k-permutation the B read copies).
+//  * B image [32][260] fp32 (1040-B rows: one DMA wave-instruction = one
+//    256-column k-row, the 4-float pad puts k-rows 4 apart on opposite bank
+//    halves): B fragment element = ds_read_b32 of B[4g+e][col] — conflict-free.
+//  * Operands swapped in the MFMA (B fragment as "A") so each lane owns 4
+//    consecutive output columns → 16-B stores.
+// Fast-path constraints (host-checked, else gemm_generic.hip): K % 32 == 0,
+// N % 4 == 0, lda/ldb % 4 == 0, ldc % 4 == 0, 16-B aligned A/B/C.
+#include "common.h"
+
+namespace pdmb {
+namespace kf32 {
+
+constexpr int BM = 256, BN = 256, BK = 32, NT = 512;
+constexpr int A_BYTES = BM * BK * 4;         // 32 KiB
+constexpr int B_PITCH = (BN + 4) * 4;        // 1040 B per k-row
+constexpr int B_BYTES = BK * B_PITCH;        // 33,280 B
+constexpr int STAGE = A_BYTES + B_BYTES;     // 66,048 B (16-B multiple)
+constexpr int LDS_BYTES = 2 * STAGE;         // 132,096 B
+
+struct Ctx {
+  const char* Ab;
+  const char* Bb;
+  long long a_bytes, b_bytes;
+  int lda4, ldb4, nk, wu;
+  uint32_t voffA[4], voffB[4];
+  uint32_t lds0;
+};
+
+// DMA of K-tile `tile` into stage STG: 4 A pieces (8 rows each) + 4 B pieces
+// (one k-row each) per wave.
+template <int STG>
+__device__ __forceinline__ void issue_tile(const Ctx& c, int tile) {
+  const long long offA = (long long)tile * BK * 4;
+  const u32x4 ra = make_rsrc(c.Ab + offA, c.a_bytes - offA);
+  const long long offB = (long long)tile * BK * c.ldb4;
+  const u32x4 rb = make_rsrc(c.Bb + offB, c.b_bytes - offB);
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+    dma16(ra, c.voffA[h], c.lds0 + STG * STAGE + (h * 8 + c.wu) * 8 * 128);
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+    dma16(rb, c.voffB[h], c.lds0 + STG * STAGE + A_BYTES + (h * 8 + c.wu) * B_PITCH);
+}
+
+template <int STG, int KB>
+__device__ __forceinline__ void compute_half(const char* smem, int wr, int wc, int l16, int g,
+                                             f32x4 (&acc)[8][4]) {
+  {
+    constexpr int kb = KB;
+    f32x4 af[8];
+    float bf[4][4];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+      const int r = wr * 128 + mi * 16 + l16;
+      const int ch = (kb * 4 + g) ^ ((r >> 1) & 7);
+      af[mi] = *(const f32x4*)(smem + STG * STAGE + r * 128 + ch * 16);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int k = kb * 16 + 4 * g + e;
+        const int col = wc * 64 + ni * 16 + l16;
+        bf[ni][e] = *(const float*)(smem + STG * STAGE + A_BYTES + k * B_PITCH + col * 4);
+      }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(bf[ni][e], af[mi][e], acc[mi][ni],
+                                                             0, 0, 0);
+  }
+}
+
+// One K-tile from stage STG with the prefetch of tile `next` into the other
+// stage. STAGGER: the two waves that share a SIMD (wave w and w+4) issue
+// their DMA pieces at different points — waves 0..3 before the first 16-k
+// half, waves 4..7 between the halves — so while one wave of the pair is
+// issuing DMA (~60 cycles per piece) its partner keeps the MFMA pipe busy.
+template <int STG, bool STAGGER>
+__device__ __forceinline__ void tile_step(const Ctx& c, const char* smem, int wr, int wc, int l16,
+                                          int g, f32x4 (&acc)[8][4], int next) {
+  const bool pf = next < c.nk;
+  if (pf && (!STAGGER || wr == 0)) issue_tile<STG ^ 1>(c, next);
+  compute_half<STG, 0>(smem, wr, wc, l16, g, acc);
+  if (STAGGER && pf && wr == 1) issue_tile<STG ^ 1>(c, next);
+  compute_half<STG, 1>(smem, wr, wc, l16, g, acc);
+}
+
+__device__ __forceinline__ void tile_barrier() {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <bool STAGGER>
+__global__ void __launch_bounds__(NT, 2) gemm_f32_256(GemmArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+
+  int bz, tm, tn;
+  map_tile(a, blockIdx.x, bz, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wu >> 2, wc = wu & 3;
+  const int l16 = lane & 15, g = lane >> 4;
+
+  Ctx c;
+  c.wu = wu;
+  c.lds0 = (uint32_t)(size_t)((lds_void*)smem);
+  c.lda4 = a.lda * 4;
+  c.ldb4 = a.ldb * 4;
+  c.nk = a.K / BK;
+  c.Ab = (const char*)a.A + ((long long)bz * a.sA + (long long)m0 * a.lda) * 4;
+  c.Bb = (const char*)a.B + ((long long)bz * a.sB + n0) * 4;
+  c.a_bytes = ((long long)(a.M - m0 - 1) * a.lda + a.K) * 4;
+  c.b_bytes = ((long long)(a.K - 1) * a.ldb + (a.N - n0)) * 4;
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    const int r = (h * 8 + wu) * 8 + (lane >> 3);
+    const int src_chunk = (lane & 7) ^ ((r >> 1) & 7);
+    c.voffA[h] = (uint32_t)(r * c.lda4 + src_chunk * 16);
+    const int k = h * 8 + wu;
+    c.voffB[h] = (uint32_t)(k * c.ldb4 + lane * 16);
+  }
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue_tile<0>(c, 0);
+  tile_barrier();
+  const int nk = c.nk;
+  for (int t = 0; t < nk; t += 2) {
+    // The stage being refilled was last read in the previous K-tile, which
+    // ended with a barrier (WAR); the refill has a whole K-tile to land and
+    // is retired by the vmcnt(0) + barrier that closes this one (RAW).
+    tile_step<0, STAGGER>(c, smem, wr, wc, l16, g, acc, t + 1);
+    tile_barrier();
+    if (t + 1 < nk) {
+      tile_step<1, STAGGER>(c, smem, wr, wc, l16, g, acc, t + 2);
+      tile_barrier();
+    }
+  }
+
+  float* Cb = (float*)a.C + (long long)bz * a.sC;
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    const int row = m0 + wr * 128 + mi * 16 + l16;
+    if (row < a.M) {
+      float* crow = Cb + (long long)row * a.ldc;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int col = n0 + wc * 64 + ni * 16 + 4 * g;
+        if (col < a.N) *(f32x4*)(crow + col) = acc[mi][ni];
+      }
+    }
+  }
+}
+
+}  // namespace kf32
+
+bool gemm_f32_256_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c) {
+  if (a.K % 32 != 0 || a.K <= 0 || a.N % 4 != 0 || a.M <= 0 || a.N <= 0) return false;
+  if (a.lda % 4 || a.ldb % 4 || a.ldc % 4) return false;
+  if (a.batch > 1 && (a.sA % 4 || a.sB % 4 || a.sC % 4)) return false;
+  if (align_a % 16 || align_b % 16 || align_c % 16) return false;
+  // 32-bit per-lane DMA offsets: 255 rows * lda and 31 rows * ldb.
+  if ((long long)256 * a.lda * 4 >= (1LL << 31) || (long long)32 * a.ldb * 4 >= (1LL << 31))
+    return false;
+  return true;
+}
+
+hipError_t gemm_f32_256_launch(GemmArgs a, bool stagger, hipStream_t stream) {
+  a.tiles_m = (a.M + kf32::BM - 1) / kf32::BM;
+  a.tiles_n = (a.N + kf32::BN - 1) / kf32::BN;
+  a.supertile = (a.tiles_m % 16 == 0 && a.tiles_n % 16 == 0) ? 1 : 0;
+  const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch;
+  if (nblocks <= 0) return hipSuccess;
+  if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
+  if (stagger)
+    hipLaunchKernelGGL(kf32::gemm_f32_256<true>, dim3((unsigned)nblocks), dim3(kf32::NT), 0,
+                       stream, a);
+  else
+    hipLaunchKernelGGL(kf32::gemm_f32_256<false>, dim3((unsigned)nblocks), dim3(kf32::NT), 0,
+                       stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace pdmb

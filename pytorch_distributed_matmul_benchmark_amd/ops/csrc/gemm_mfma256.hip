@@ -83,42 +83,6 @@ struct Ctx {
   uint32_t lds0;     // LDS byte address of smem (uniform)
 };
 
-// Raw buffer descriptor (gfx950 dword3 = 0x00020000: 32-bit data format,
-// raw addressing). Bytes at or beyond num_records read as zero, which
-// handles the M / N edges with no masking in the K-loop. num_records is
-// clamped with 32-bit scalar logic (SALU has no 64-bit less-than).
-__device__ __forceinline__ u32x4 make_rsrc(const char* base, long long bytes) {
-  const unsigned long long p = (unsigned long long)base;
-  const unsigned int hi = (unsigned int)((unsigned long long)bytes >> 32);
-  const unsigned int lo = (unsigned int)bytes;
-  const unsigned int nr = (hi & 0x80000000u) ? 0u : (hi ? 0xffffffffu : lo);
-  u32x4 r;
-  r.x = (unsigned int)p;
-  r.y = (unsigned int)(p >> 32) & 0xffffu;
-  r.z = nr;
-  r.w = 0x00020000u;
-  return r;
-}
-
-// One LDS-DMA wave-instruction: 64 lanes x 16 B from rsrc+voff into LDS at
-// lds_base + lane*16. Written as inline asm on purpose: hipcc (ROCm 7.2)
-// otherwise treats every later ds_read_b64_tr_b16 as possibly aliasing the
-// in-flight DMA and inserts s_waitcnt vmcnt(0), which drains the pipeline.
-// The count is ours to keep: every wait on these is an explicit vmcnt(N).
-// M0 is saved/restored around the statement (compiler-reserved register).
-__device__ __forceinline__ void dma16(u32x4 rsrc, uint32_t voff, uint32_t lds_base) {
-  unsigned int keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(rsrc), "s"(lds_base)
-      : "memory");
-}
-
 // Issue the two LDS-DMA loads of one unit. TYPE: 0 = A rows of quadrant-row
 // mq=0, 1 = B half nq=0, 2 = B half nq=1, 3 = A rows mq=1. Tile index is
 // clamped so the (harmless) tail loads re-read the last tile.
@@ -187,6 +151,37 @@ __device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[8][4], const s16x8 (&r
 
 #define PDMB_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 
+// Diagnostic build only (STAMP = true, kernel id kMfma256Stamp): per wave,
+// the cycles spent waiting in the barrier that closes a read slot (wr) and
+// in the one that closes a compute slot (wc). A wave that waits after its
+// read slot was faster than its partner's MFMAs; a wave that waits after its
+// compute slot was waiting for the readers. Stamps go only to a debug buffer.
+struct Stamp {
+  unsigned long long wr = 0, wc = 0;
+};
+
+__device__ __forceinline__ unsigned long long stamp_now() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
+template <bool STAMP>
+__device__ __forceinline__ void slot_barrier(unsigned long long& sum) {
+  if constexpr (STAMP) {
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long t0 = stamp_now();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long t1 = stamp_now();
+    __builtin_amdgcn_sched_barrier(0);
+    sum += t1 - t0;
+  } else {
+    PDMB_SLOT_BARRIER();
+  }
+}
+
 // One K-tile (4 phases) from LDS stage STG. Phase P = 4t+q issues unit P+7.
 //
 // SCHED 0: the unit's LDS-DMA is issued in the compute slot, ahead of the
@@ -203,10 +198,10 @@ __device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[8][4], const s16x8 (&r
 //   RAW — after issuing unit P+7 a wave waits vmcnt(10): units <= P+2 have
 //     landed, which the read slot of P+1 (one barrier later for the lagging
 //     group) needs. Each unit now gets one more slot of flight time.
-template <int DT, int STG, int SCHED>
+template <int DT, int STG, int SCHED, bool STAMP = false>
 __device__ __forceinline__ void tile_body(const Ctx& c, char* smem, int t, f32x4 (&acc)[8][4],
                                           s16x8 (&ra)[4][2], s16x8 (&ra2)[4][2],
-                                          s16x8 (&rb0)[2][2], s16x8 (&rb1)[2][2]) {
+                                          s16x8 (&rb0)[2][2], s16x8 (&rb1)[2][2], Stamp& st) {
   if constexpr (SCHED == 0) {
     // phase q=0: quadrant (0,0)
     read_a<STG, 0>(c, smem, ra);
@@ -251,33 +246,33 @@ __device__ __forceinline__ void tile_body(const Ctx& c, char* smem, int t, f32x4
     issue_unit<3, STG ^ 1>(c, smem, t + 1);
     PDMB_LGKM0();
     PDMB_VMCNT(10);
-    PDMB_SLOT_BARRIER();
+    slot_barrier<STAMP>(st.wr);
     mma_quadrant<DT, 0, 0>(acc, ra2, rb0);
-    PDMB_SLOT_BARRIER();
+    slot_barrier<STAMP>(st.wc);
     // phase q=1: quadrant (0,1)
     read_b<STG, 1>(c, smem, rb1);
     issue_unit<0, STG>(c, smem, t + 2);
     PDMB_LGKM0();
     PDMB_VMCNT(10);
-    PDMB_SLOT_BARRIER();
+    slot_barrier<STAMP>(st.wr);
     mma_quadrant<DT, 0, 1>(acc, ra2, rb1);
-    PDMB_SLOT_BARRIER();
+    slot_barrier<STAMP>(st.wc);
     // phase q=2: quadrant (1,1)
     read_a<STG, 1>(c, smem, ra);
     issue_unit<1, STG>(c, smem, t + 2);
     PDMB_LGKM0();
     PDMB_VMCNT(10);
-    PDMB_SLOT_BARRIER();
+    slot_barrier<STAMP>(st.wr);
     mma_quadrant<DT, 1, 1>(acc, ra, rb1);
-    PDMB_SLOT_BARRIER();
+    slot_barrier<STAMP>(st.wc);
     // phase q=3: quadrant (1,0); prefetch next tile's A0 fragments
     read_a<STG ^ 1, 0>(c, smem, ra2);
     issue_unit<2, STG>(c, smem, t + 2);
     PDMB_LGKM0();
     PDMB_VMCNT(10);
-    PDMB_SLOT_BARRIER();
+    slot_barrier<STAMP>(st.wr);
     mma_quadrant<DT, 1, 0>(acc, ra, rb0);
-    PDMB_SLOT_BARRIER();
+    slot_barrier<STAMP>(st.wc);
   } else {
     // phase q=0: quadrant (0,0)
     read_b<STG, 0>(c, smem, rb0);
@@ -313,7 +308,7 @@ __device__ __forceinline__ void tile_body(const Ctx& c, char* smem, int t, f32x4
   }
 }
 
-template <int DT, int SCHED>
+template <int DT, int SCHED, bool STAMP = false>
 __global__ void __launch_bounds__(NTHREADS, 2) gemm256_nn(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
@@ -397,9 +392,22 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm256_nn(GemmArgs a) {
   if constexpr (SCHED == 2) read_a<0, 0>(c, smem, ra2);
 
   const int nk = c.nk;
+  Stamp st;
+  unsigned long long t_loop0 = 0;
+  if constexpr (STAMP) t_loop0 = stamp_now();
   for (int t = 0; t < nk; t += 2) {
-    tile_body<DT, 0, SCHED>(c, smem, t, acc, ra, ra2, rb0, rb1);
-    if (t + 1 < nk) tile_body<DT, 1, SCHED>(c, smem, t + 1, acc, ra, ra2, rb0, rb1);
+    tile_body<DT, 0, SCHED, STAMP>(c, smem, t, acc, ra, ra2, rb0, rb1, st);
+    if (t + 1 < nk) tile_body<DT, 1, SCHED, STAMP>(c, smem, t + 1, acc, ra, ra2, rb0, rb1, st);
+  }
+  if constexpr (STAMP) {
+    const unsigned long long t_loop1 = stamp_now();
+    if (lane == 0 && a.dbg) {
+      unsigned long long* d = a.dbg + ((size_t)blockIdx.x * 8 + wu) * 4;
+      d[0] = st.wr;
+      d[1] = st.wc;
+      d[2] = t_loop1 - t_loop0;
+      d[3] = (unsigned long long)nk;
+    }
   }
   if (wr == 0) PDMB_SLOT_BARRIER();
   PDMB_VMCNT(0);  // drain the clamped tail DMAs before the LDS is released
@@ -450,6 +458,11 @@ hipError_t gemm256_launch(int dt, GemmArgs a, int sched, hipStream_t stream) {
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
   dim3 grid((unsigned)nblocks), block(k256::NTHREADS);
 #define PDMB_LAUNCH256(D, S) hipLaunchKernelGGL((k256::gemm256_nn<D, S>), grid, block, 0, stream, a)
+  if (sched == 3) {  // diagnostic stamp build of SCHED 2 (bf16 only)
+    if (dt != kBF16 || !a.dbg) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k256::gemm256_nn<kBF16, 2, true>), grid, block, 0, stream, a);
+    return hipGetLastError();
+  }
   if (dt == kBF16) {
     if (sched == 2) PDMB_LAUNCH256(kBF16, 2);
     else if (sched == 1) PDMB_LAUNCH256(kBF16, 1);

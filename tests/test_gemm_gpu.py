@@ -144,9 +144,10 @@ def test_fp32_exact_mfma_path():
     torch.manual_seed(3)
     A = torch.randn(512, 512, device="cuda", dtype=torch.float32)
     B = torch.randn(512, 512, device="cuda", dtype=torch.float32)
-    C = gemm.matmul(A, B)
-    assert gemm.kernel_for(A, B) == "pdmb_generic_nn"
-    assert _relerr(C, _ref(A, B)) < TOL[torch.float32]
+    assert gemm.kernel_for(A, B) == "pdmb_f32_256s_nn"
+    for k in ("auto", "generic"):
+        C = gemm.matmul(A, B, kernel=k)
+        assert _relerr(C, _ref(A, B)) < TOL[torch.float32]
 
 
 def test_zero_k():
@@ -180,3 +181,48 @@ def test_race_screen_repeated_runs(kernel):
         assert _relerr(ref, R) < TOL[torch.bfloat16]
         for _ in range(10 if n == 8192 else 20):
             assert torch.equal(gemm.matmul(A, B, kernel=kernel), ref)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 32), (512, 768, 96), (1000, 1052, 320),
+                                   (300, 200, 64), (2304, 2048, 1024)])
+@pytest.mark.parametrize("kernel", ["f32_256", "f32_256s"])
+def test_f32_256_exact_and_random(M, N, K, kernel):
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
+    A = torch.randint(-3, 4, (M, K), device="cuda", generator=g).float()
+    B = torch.randint(-3, 4, (K, N), device="cuda", generator=g).float()
+    assert gemm.kernel_for(A, B, kernel=kernel).startswith("pdmb_f32_256")
+    C = gemm.matmul(A, B, kernel=kernel)
+    assert torch.equal(C.double(), _ref(A, B))  # small integers: exact in fp32
+    A = torch.randn(M, K, device="cuda", generator=g)
+    B = torch.randn(K, N, device="cuda", generator=g)
+    C = gemm.matmul(A, B, kernel=kernel)
+    assert _relerr(C, _ref(A, B)) < TOL[torch.float32]
+
+
+def test_f32_256_identity_batched_and_shards():
+    n = 512
+    A = torch.eye(n, device="cuda")
+    B = (torch.arange(n * n, device="cuda").view(n, n) % 97).float()
+    assert torch.equal(gemm.matmul(A, B), B) and torch.equal(gemm.matmul(B, A), B)
+    torch.manual_seed(7)
+    A3 = torch.randn(3, 384, 256, device="cuda")
+    B3 = torch.randn(3, 256, 640, device="cuda")
+    assert gemm.kernel_for(A3, B3) == "pdmb_f32_256s_nn"
+    assert _relerr(gemm.bmm(A3, B3), torch.bmm(A3.double(), B3.double())) < TOL[torch.float32]
+    Bf = torch.randn(1024, 1024, device="cuda")
+    Af = torch.randn(1024, 1024, device="cuda")
+    for r in range(4):  # matrix_parallel column shards (strided views)
+        Bs = Bf[:, r * 256:(r + 1) * 256]
+        assert _relerr(gemm.matmul(Af, Bs), _ref(Af, Bs)) < TOL[torch.float32]
+
+
+@pytest.mark.parametrize("kernel", ["f32_256", "f32_256s"])
+def test_f32_256_race_screen(kernel):
+    torch.manual_seed(11)
+    A = torch.randn(4096, 4096, device="cuda")
+    B = torch.randn(4096, 4096, device="cuda")
+    ref = gemm.matmul(A, B, kernel=kernel)
+    R = torch.matmul(A.double(), B.double())
+    assert _relerr(ref, R) < TOL[torch.float32]
+    for _ in range(10):
+        assert torch.equal(gemm.matmul(A, B, kernel=kernel), ref)
