@@ -59,9 +59,12 @@ def main() -> int:
                     help="batch/matrix_parallel: hide the collective behind the GEMM chunks")
     ap.add_argument("--chunks", type=int, default=4)
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: torch.matmul + gloo, to exercise the multi-rank path without a GPU")
     a = ap.parse_args()
 
-    ctx = setup_distributed("cuda")
+    ctx = setup_distributed(a.device)
+    cuda = ctx.device.type == "cuda"
     ws = ctx.world_size
     if ws != a.gpus and ctx.is_main:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={ws}; using {ws}", file=sys.stderr)
@@ -74,15 +77,24 @@ def main() -> int:
         return torch.randn(*shape, generator=g, device=dev, dtype=dt)
 
     def mm(A, B, out):
-        if a.backend == "torch":
+        if a.backend == "torch" or not cuda:
             return torch.matmul(A, B, out=out)
         return gemm.matmul(A, B, out=out)
+
+    def label(A, B, C):
+        if not cuda:
+            return "torch.matmul(cpu)"
+        return gemm.kernel_for(A, B, C) if a.backend == "native" else "hipBLASLt"
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize(dev)
 
     flop_gemm = 2.0 * n * n * n
     if a.mode == "independent":
         A, B = rnd(n, n, seed=2 * ctx.rank), rnd(n, n, seed=2 * ctx.rank + 1)
         C = torch.empty(n, n, device=dev, dtype=dt)
-        kernel = gemm.kernel_for(A, B, C) if a.backend == "native" else "hipBLASLt"
+        kernel = label(A, B, C)
 
         def step():
             mm(A, B, C)
@@ -92,8 +104,8 @@ def main() -> int:
         lb, gb = local_batch(ws), global_batch(ws)
         A, B = rnd(lb, n, n, seed=2 * ctx.rank), rnd(lb, n, n, seed=2 * ctx.rank + 1)
         C = torch.empty(lb, n, n, device=dev, dtype=dt)
-        kernel = gemm.kernel_for(A, B, C) if a.backend == "native" else "hipBLASLt"
-        comp = torch.cuda.current_stream(dev)
+        kernel = label(A, B, C)
+        comp = torch.cuda.current_stream(dev) if cuda else None
         if a.overlap and ws > 1:
             cs = CommStream(dev)
             units = [(b, s, e) for b in range(lb) for (s, e) in row_chunks(n, a.chunks)]
@@ -102,12 +114,14 @@ def main() -> int:
 
             def step():
                 for u, (b, s, e) in enumerate(units):
-                    comp.wait_event(done[u])
+                    if cuda:
+                        comp.wait_event(done[u])
                     mm(A[b, s:e], B[b], C[b, s:e])
                     ready[u].record(comp)
                     cs.all_reduce(C[b, s:e], after=ready[u], done=done[u])
-                for d in done:
-                    comp.wait_event(d)
+                if cuda:
+                    for d in done:
+                        comp.wait_event(d)
         else:
             def step():
                 mm(A, B, C)
@@ -124,8 +138,8 @@ def main() -> int:
         del Bg
         Cl = torch.empty(n, sh.padded, device=dev, dtype=dt)
         gathered = torch.empty(ws * n, sh.padded, device=dev, dtype=dt)
-        kernel = gemm.kernel_for(A, Bl, Cl) if a.backend == "native" else "hipBLASLt"
-        comp = torch.cuda.current_stream(dev)
+        kernel = label(A, Bl, Cl)
+        comp = torch.cuda.current_stream(dev) if cuda else None
         if a.overlap and ws > 1:
             cs = CommStream(dev)
             rc = row_chunks(n, a.chunks)
@@ -135,12 +149,14 @@ def main() -> int:
 
             def step():
                 for j, (s, e) in enumerate(rc):
-                    comp.wait_event(done[j])
+                    if cuda:
+                        comp.wait_event(done[j])
                     mm(A[s:e], Bl, Cl[s:e])
                     ready[j].record(comp)
                     cs.all_gather_into(bufs[j], Cl[s:e], after=ready[j], done=done[j])
-                for d in done:
-                    comp.wait_event(d)
+                if cuda:
+                    for d in done:
+                        comp.wait_event(d)
         else:
             def step():
                 mm(A, Bl, Cl)
@@ -151,15 +167,15 @@ def main() -> int:
 
     for _ in range(a.warmup):
         step()
-    torch.cuda.synchronize(dev)
+    sync()
     barrier(ctx)
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
-    torch.cuda.synchronize(dev)
+    sync()
     barrier(ctx)
-    torch.cuda.synchronize(dev)
+    sync()
     elapsed = time.perf_counter() - t0
     if ctx.is_distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -167,7 +183,8 @@ def main() -> int:
         elapsed = float(t.item())
     ms_step = elapsed / max(a.steps, 1) * 1e3
     value = flops_step * a.steps / elapsed / 1e12 if elapsed > 0 else 0.0
-    base = BASELINE_TFLOPS[a.mode].get(ws) if dt == torch.bfloat16 and n == 16384 else None
+    base = (BASELINE_TFLOPS[a.mode].get(ws)
+            if dt == torch.bfloat16 and n == 16384 and cuda else None)
     if ctx.is_main:
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "TFLOPS",
@@ -177,6 +194,7 @@ def main() -> int:
             "vs_baseline": round(value / base, 3) if base else None,
             "dtype": {"bfloat16": "bf16", "float16": "fp16", "float32": "fp32"}[a.dtype],
             "data": "synthetic (torch.randn N(0,1) operands, seeded per rank)",
+            "device": ctx.device.type,
             "config": {"model": f"gemm_{n}x{n}x{n}_{a.dtype}", "global_batch": cfg["global_batch"],
                        "seq_len": n, "parallelism": cfg["parallelism"], "mode": a.mode,
                        "overlap": bool(a.overlap), "backend": a.backend, "kernel": kernel},
