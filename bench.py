@@ -37,7 +37,7 @@ from pytorch_distributed_matmul_benchmark_amd.parallel.comm import (CommStream, 
 from pytorch_distributed_matmul_benchmark_amd.parallel.dist import (  # noqa: E402
     barrier, cleanup_distributed, setup_distributed)
 from pytorch_distributed_matmul_benchmark_amd.parallel.partition import (  # noqa: E402
-    column_shard, local_batch, global_batch, row_chunks)
+    column_shard, effective_chunks, global_batch, local_batch, row_chunks)
 
 # Reference numbers (README.md:43-46): whole-system TFLOPS at 16k bf16.
 BASELINE_TFLOPS = {"independent": {1: 140.0, 2: 294.0},
@@ -108,7 +108,8 @@ def main() -> int:
         comp = torch.cuda.current_stream(dev) if cuda else None
         if a.overlap and ws > 1:
             cs = CommStream(dev)
-            units = [(b, s, e) for b in range(lb) for (s, e) in row_chunks(n, a.chunks)]
+            ch = effective_chunks(n, n, a.chunks) if cuda else a.chunks
+            units = [(b, s, e) for b in range(lb) for (s, e) in row_chunks(n, ch)]
             ready = [new_event(dev) for _ in units]
             done = [new_event(dev) for _ in units]
 
@@ -142,7 +143,7 @@ def main() -> int:
         comp = torch.cuda.current_stream(dev) if cuda else None
         if a.overlap and ws > 1:
             cs = CommStream(dev)
-            rc = row_chunks(n, a.chunks)
+            rc = row_chunks(n, effective_chunks(n, sh.padded, a.chunks) if cuda else a.chunks)
             bufs = [torch.empty(ws * (e - s), sh.padded, device=dev, dtype=dt) for s, e in rc]
             ready = [new_event(dev) for _ in rc]
             done = [new_event(dev) for _ in rc]

@@ -26,7 +26,7 @@ import torch
 
 from ..parallel.comm import CommStream, current_stream, new_event
 from ..parallel.dist import DistContext
-from ..parallel.partition import global_batch, local_batch, row_chunks
+from ..parallel.partition import effective_chunks, global_batch, local_batch, row_chunks
 from ..utils.metrics import gemm_flops, tflops_from
 from ..utils.timing import SegmentTimer, Stopwatch, synchronize, time_loop_ms
 import torch.distributed as dist
@@ -85,7 +85,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
                          compute_only_tflops=tflops_from(flops, comp / 1e3), kernel=label,
                          extra=extra)
     else:
-        units = _units(lb, n, w.chunks)
+        units = _units(lb, n, effective_chunks(n, n, w.chunks) if dev.type == "cuda" else w.chunks)
         extra["units"] = len(units)
         comm = CommStream(dev)
         ready = [new_event(dev) for _ in units]

@@ -27,7 +27,7 @@ import torch.distributed as dist
 
 from ..parallel.comm import CommStream, current_stream, new_event
 from ..parallel.dist import DistContext
-from ..parallel.partition import column_shard, row_chunks
+from ..parallel.partition import column_shard, effective_chunks, row_chunks
 from ..utils.metrics import gemm_flops, tflops_from
 from ..utils.timing import SegmentTimer, Stopwatch, synchronize, time_loop_ms
 from . import independent
@@ -101,7 +101,8 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         avg = comp + cm
         full = (lambda: assemble(gathered, n, ws))
     else:
-        rc = row_chunks(n, w.chunks)
+        rc = row_chunks(n, effective_chunks(n, sh.padded, w.chunks) if dev.type == "cuda"
+                        else w.chunks)
         extra["chunks"] = len(rc)
         bufs = [torch.empty((ws * (e - s), sh.padded), device=dev, dtype=w.dtype) for s, e in rc]
         cs = CommStream(dev)
