@@ -69,6 +69,34 @@ def _run(cmd, verbose):
     return r
 
 
+RUNTIME = HERE.parent / "runtime"
+BENCH_SRC = RUNTIME / "pdmb_bench.cpp"
+
+
+def bench_path() -> Path:
+    return RUNTIME / "pdmb_bench"
+
+
+def build_bench(verbose: bool = False, force: bool = False) -> Path:
+    """Link the Python-free native executor ``runtime/pdmb_bench`` (HIP + RCCL) from
+    ``runtime/pdmb_bench.cpp`` and the same kernel objects as ``_C``."""
+    build(verbose=verbose, force=force)  # kernel objects
+    out = bench_path()
+    objs = [BUILD / (Path(s).stem + ".o") for s in HIP_SOURCES]
+    deps = [BENCH_SRC, CSRC / "api.h"] + objs
+    if not force and not _needs_build(out, deps):
+        return out
+    rocm = rocm_path()
+    obj = BUILD / "pdmb_bench.o"
+    # compile and link separately: hipcc's implicit "-x hip" would otherwise
+    # also apply to the kernel objects on the link line
+    _run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", f"-I{CSRC}",
+          f"-I{rocm / 'include'}", "-c", BENCH_SRC, "-o", obj], verbose)
+    _run([hipcc(), f"--offload-arch={ARCH}", obj, *objs, "-o", out, f"-L{rocm / 'lib'}", "-lrccl",
+          "-lpthread", f"-Wl,-rpath,{rocm / 'lib'}"], verbose)
+    return out
+
+
 def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -> Path:
     """Compile every HIP/C++ source for gfx950 and link ``_C``. Returns the .so path."""
     headers = sorted(CSRC.glob("*.h"))
@@ -124,9 +152,12 @@ def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--no-bench", action="store_true", help="skip the native pdmb_bench executable")
     a = ap.parse_args(argv)
     p = build(verbose=a.verbose, force=a.force)
     print(p)
+    if not a.no_bench:
+        print(build_bench(verbose=a.verbose))
 
 
 if __name__ == "__main__":

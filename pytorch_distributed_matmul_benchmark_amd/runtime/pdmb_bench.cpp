@@ -1,0 +1,687 @@
+// pdmb_bench — Python-free native executor of the benchmark (HIP + RCCL).
+//
+// The same workloads as matmul_scaling_benchmark.py (independent |
+// batch_parallel | matrix_parallel, reference matmul_scaling_benchmark.py:
+// 69-238) driven entirely from C++: one host thread per GPU in one process,
+// RCCL communicators from ncclCommInitAll over xGMI, the gfx950 MFMA GEMM
+// library of ops/csrc (pdmb::gemm), hipEvents for timing and an
+// event-ordered comm stream for the --overlap variants. No PyTorch, no Python:
+// useful to separate framework overhead from kernel/fabric behaviour and as a
+// reference implementation of the scaling modes for MI355X nodes.
+//
+//   pdmb_bench --gpus 8 --mode batch_parallel --overlap --sizes 16384 --check
+//
+// Output: the reference's result lines (Results for NxN, Average time per
+// operation, TFLOPS per GPU, Total system TFLOPS, Actual TFLOPS) and, with
+// --json FILE, one JSON record per size.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../ops/csrc/api.h"
+
+namespace {
+
+#define HIP_OK(x)                                                                        \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess)                                                                \
+      throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e_));          \
+  } while (0)
+#define NCCL_OK(x)                                                                       \
+  do {                                                                                   \
+    ncclResult_t r_ = (x);                                                               \
+    if (r_ != ncclSuccess)                                                               \
+      throw std::runtime_error(std::string(#x) + ": " + ncclGetErrorString(r_));         \
+  } while (0)
+
+enum Mode { kIndependent, kBatchParallel, kMatrixParallel };
+
+struct Opts {
+  int gpus = 1;
+  std::vector<int> sizes{4096, 8192, 16384};
+  int iters = 50, warmup = 10;
+  int dtype = 2;  // pdmb::DType: 0 f32, 1 f16, 2 bf16
+  Mode mode = kIndependent;
+  int batch = 4, chunks = 4, kernel = 0;
+  bool overlap = false, check = false;
+  std::string json;
+};
+
+const char* mode_name(Mode m) {
+  return m == kIndependent ? "independent" : m == kBatchParallel ? "batch_parallel" : "matrix_parallel";
+}
+const char* dtype_name(int d) { return d == 0 ? "float32" : d == 1 ? "float16" : "bfloat16"; }
+size_t esize(int d) { return d == 0 ? 4 : 2; }
+ncclDataType_t nccl_type(int d) { return d == 0 ? ncclFloat32 : d == 1 ? ncclFloat16 : ncclBfloat16; }
+int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// ---- device helpers -------------------------------------------------------
+__device__ __forceinline__ float to_float(const void* p, long long i, int dt) {
+  if (dt == 0) return ((const float*)p)[i];
+  const unsigned short v = ((const unsigned short*)p)[i];
+  if (dt == 2) return __uint_as_float(((unsigned int)v) << 16);
+  return (float)__builtin_bit_cast(_Float16, v);
+}
+
+// Uniform [-1, 1) from a counter hash (random, non-zero data: zero-filled
+// operands run ~20 % fast on MI355X through DVFS).
+__global__ void fill_uniform(void* p, long long n, int dt, unsigned long long seed) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    unsigned long long x = (unsigned long long)i * 0x9E3779B97F4A7C15ull + seed * 0xD1B54A32D192ED03ull;
+    x ^= x >> 31;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 29;
+    const float u = (float)(x >> 40) * (1.0f / 8388608.0f) - 1.0f;  // 24 random bits
+    if (dt == 0) {
+      ((float*)p)[i] = u;
+    } else if (dt == 2) {
+      __bf16 h = (__bf16)u;
+      ((__bf16*)p)[i] = h;
+    } else {
+      ((_Float16*)p)[i] = (_Float16)u;
+    }
+  }
+}
+
+// out[r][j] = sum_k A[rows[r]][k] * B[k][j] in float64 (the check's reference).
+__global__ void ref_rows(const void* A, const void* B, const int* rows, int R, int K, int N, int lda,
+                         int ldb, int dt, double* out) {
+  const long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (idx >= (long long)R * N) return;
+  const int r = (int)(idx / N), j = (int)(idx % N);
+  double s = 0.0;
+  const long long arow = (long long)rows[r] * lda;
+  for (int k = 0; k < K; ++k)
+    s += (double)to_float(A, arow + k, dt) * (double)to_float(B, (long long)k * ldb + j, dt);
+  out[idx] = s;
+}
+
+// Gather sampled rows of a [M, ld] matrix (N columns) into float64.
+__global__ void take_rows(const void* C, const int* rows, int R, int N, int ld, int dt, double* out) {
+  const long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (idx >= (long long)R * N) return;
+  const int r = (int)(idx / N), j = (int)(idx % N);
+  out[idx] = (double)to_float(C, (long long)rows[r] * ld + j, dt);
+}
+
+// ---- host helpers ---------------------------------------------------------
+class Barrier {
+ public:
+  explicit Barrier(int n) : n_(n) {}
+  // Throws if another rank aborted (so no rank waits forever on a dead peer).
+  void wait() {
+    std::unique_lock<std::mutex> lk(m_);
+    if (aborted_) throw std::runtime_error("another rank failed");
+    const int gen = gen_;
+    if (++count_ == n_) {
+      count_ = 0;
+      ++gen_;
+      cv_.notify_all();
+    } else {
+      cv_.wait(lk, [&] { return gen != gen_ || aborted_; });
+      if (aborted_) throw std::runtime_error("another rank failed");
+    }
+  }
+  void abort() {
+    std::lock_guard<std::mutex> lk(m_);
+    aborted_ = true;
+    cv_.notify_all();
+  }
+
+ private:
+  std::mutex m_;
+  std::condition_variable cv_;
+  int n_, count_ = 0, gen_ = 0;
+  bool aborted_ = false;
+};
+
+struct Buf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  Buf() = default;
+  explicit Buf(size_t b) : bytes(b) { HIP_OK(hipMalloc(&p, b ? b : 16)); }
+  ~Buf() {
+    if (p) (void)hipFree(p);
+  }
+  Buf(const Buf&) = delete;
+  Buf& operator=(const Buf&) = delete;
+  Buf(Buf&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; }
+  template <class T>
+  T* as() const { return (T*)p; }
+};
+
+void fill(void* p, long long n, int dt, unsigned long long seed, hipStream_t s) {
+  hipLaunchKernelGGL(fill_uniform, dim3(2048), dim3(256), 0, s, p, n, dt, seed);
+  HIP_OK(hipGetLastError());
+}
+
+pdmb::Problem problem(int dt, const void* A, const void* B, void* C, int M, int N, int K, int lda,
+                      int ldb, int ldc, int batch = 1, long long sA = 0, long long sB = 0,
+                      long long sC = 0) {
+  pdmb::Problem p{};
+  p.dtype = dt;
+  p.A = A;
+  p.B = B;
+  p.C = C;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.lda = lda;
+  p.ldb = ldb;
+  p.ldc = ldc;
+  p.sA = sA;
+  p.sB = sB;
+  p.sC = sC;
+  p.batch = batch;
+  return p;
+}
+
+void gemm(const pdmb::Problem& p, int kernel, hipStream_t s) {
+  int used = -1;
+  HIP_OK(pdmb::gemm(p, kernel, s, &used));
+  if (used < 0) throw std::runtime_error("requested kernel cannot run this problem");
+}
+
+float elapsed(hipEvent_t a, hipEvent_t b) {
+  float ms = 0.f;
+  HIP_OK(hipEventElapsedTime(&ms, a, b));
+  return ms;
+}
+
+struct Result {
+  double avg_ms = 0, comp_ms = 0, comm_ms = 0, flops_local = 0, flops_total = 0;
+  std::string kernel, error;
+  std::vector<double> ref;  // sampled-row float64 reference (this rank's part)
+  std::vector<double> got;  // sampled-row output as computed/communicated on this rank
+  int shard = 0, local_batch = 1, global_batch = 1, chunks = 1;
+};
+
+std::vector<int> sample_rows(int M, int R) {
+  std::vector<int> rows;
+  unsigned long long x = 0x1234567ull;
+  for (int i = 0; i < std::min(M, R); ++i) {
+    x = x * 6364136223846793005ull + 1442695040888963407ull;
+    rows.push_back(M <= R ? i : (int)((x >> 33) % (unsigned long long)M));
+  }
+  return rows;
+}
+
+// Sampled rows of A@B (float64) and of C, both copied to the host.
+void check_rows(int dt, const void* A, const void* B, const void* C, int M, int N, int K, int lda,
+                int ldb, int ldc, hipStream_t s, std::vector<double>& ref, std::vector<double>& got) {
+  const std::vector<int> rows = sample_rows(M, 32);
+  const int R = (int)rows.size();
+  Buf drows(R * sizeof(int)), dref((size_t)R * N * 8), dgot((size_t)R * N * 8);
+  HIP_OK(hipMemcpyAsync(drows.p, rows.data(), R * sizeof(int), hipMemcpyHostToDevice, s));
+  const long long tot = (long long)R * N;
+  hipLaunchKernelGGL(ref_rows, dim3(ceil_div(tot, 256)), dim3(256), 0, s, A, B, drows.as<int>(), R,
+                     K, N, lda, ldb, dt, dref.as<double>());
+  hipLaunchKernelGGL(take_rows, dim3(ceil_div(tot, 256)), dim3(256), 0, s, C, drows.as<int>(), R, N,
+                     ldc, dt, dgot.as<double>());
+  HIP_OK(hipGetLastError());
+  ref.resize(tot);
+  got.resize(tot);
+  HIP_OK(hipMemcpyAsync(ref.data(), dref.p, tot * 8, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(got.data(), dgot.p, tot * 8, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+}
+
+int effective_chunks(int m, int n, int chunks) {
+  const long long tiles = (long long)ceil_div(m, 256) * ceil_div(n, 256);
+  return std::max(1, (int)std::min<long long>(chunks, tiles / 256));
+}
+
+std::vector<std::pair<int, int>> row_chunks(int m, int chunks) {
+  const int step = ceil_div(ceil_div(m, chunks), 256) * 256;
+  std::vector<std::pair<int, int>> out;
+  for (int s = 0; s < m; s += step) out.push_back({s, std::min(m, s + step)});
+  return out;
+}
+
+// ---- one rank ---------------------------------------------------------------
+void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Result& res) {
+  HIP_OK(hipSetDevice(rank));
+  const int ws = o.gpus, dt = o.dtype;
+  const size_t es = esize(dt);
+  hipStream_t st, cs;
+  int lo = 0, hi = 0;
+  HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  HIP_OK(hipStreamCreateWithPriority(&cs, hipStreamNonBlocking, hi));
+  std::vector<hipEvent_t> ev;
+  auto event = [&]() {
+    hipEvent_t e;
+    HIP_OK(hipEventCreate(&e));
+    ev.push_back(e);
+    return e;
+  };
+  const double flop = 2.0 * n * (double)n * n;
+  // Collectives run at every world size (a 1-rank RCCL communicator still
+  // executes the collective kernels), so the 1-GPU run exercises the same path.
+  const bool dist = comm != nullptr;
+
+  if (o.mode == kIndependent) {
+    Buf A((size_t)n * n * es), B((size_t)n * n * es), C((size_t)n * n * es);
+    fill(A.p, (long long)n * n, dt, 2 * rank + 1, st);
+    fill(B.p, (long long)n * n, dt, 2 * rank + 2, st);
+    const pdmb::Problem p = problem(dt, A.p, B.p, C.p, n, n, n, n, n, n);
+    res.kernel = pdmb::kernel_name(pdmb::resolve_kernel(p, o.kernel));
+    for (int i = 0; i < o.warmup; ++i) gemm(p, o.kernel, st);
+    HIP_OK(hipStreamSynchronize(st));
+    bar.wait();
+    hipEvent_t e0 = event(), e1 = event();
+    HIP_OK(hipEventRecord(e0, st));
+    for (int i = 0; i < o.iters; ++i) gemm(p, o.kernel, st);
+    HIP_OK(hipEventRecord(e1, st));
+    HIP_OK(hipEventSynchronize(e1));
+    res.avg_ms = res.comp_ms = elapsed(e0, e1) / std::max(o.iters, 1);
+    res.flops_local = flop;
+    res.flops_total = o.mode == kIndependent ? flop * ws : flop;
+    if (o.check) check_rows(dt, A.p, B.p, C.p, n, n, n, n, n, n, st, res.ref, res.got);
+  } else if (o.mode == kBatchParallel) {
+    const int gb = std::max(ceil_div(std::max(o.batch, 1), ws) * ws, ws), lb = gb / ws;
+    res.local_batch = lb;
+    res.global_batch = gb;
+    const size_t mat = (size_t)n * n;
+    Buf A(lb * mat * es), B(lb * mat * es), C(lb * mat * es);
+    fill(A.p, (long long)(lb * mat), dt, 2 * rank + 1, st);
+    fill(B.p, (long long)(lb * mat), dt, 2 * rank + 2, st);
+    const pdmb::Problem p = problem(dt, A.p, B.p, C.p, n, n, n, n, n, n, lb, mat, mat, mat);
+    res.kernel = pdmb::kernel_name(pdmb::resolve_kernel(p, o.kernel));
+    struct Unit { int b, r0, r1; };
+    std::vector<Unit> units;
+    const int ch = o.overlap ? effective_chunks(n, n, o.chunks) : 1;
+    for (int b = 0; b < lb; ++b)
+      for (auto rc : row_chunks(n, ch)) units.push_back({b, rc.first, rc.second});
+    res.chunks = ch;
+    std::vector<hipEvent_t> ready, done;
+    for (size_t u = 0; u < units.size(); ++u) {
+      ready.push_back(event());
+      done.push_back(event());
+    }
+    std::vector<bool> used(units.size(), false);
+    auto serial_iter = [&](hipEvent_t em) {
+      gemm(p, o.kernel, st);
+      if (em) HIP_OK(hipEventRecord(em, st));
+      if (dist) NCCL_OK(ncclAllReduce(C.p, C.p, lb * mat, nccl_type(dt), ncclSum, comm, st));
+    };
+    auto overlap_iter = [&]() {
+      for (size_t u = 0; u < units.size(); ++u) {
+        const Unit& un = units[u];
+        char* a = (char*)A.p + (un.b * mat + (size_t)un.r0 * n) * es;
+        char* b = (char*)B.p + un.b * mat * es;
+        char* c = (char*)C.p + (un.b * mat + (size_t)un.r0 * n) * es;
+        if (used[u]) HIP_OK(hipStreamWaitEvent(st, done[u], 0));
+        gemm(problem(dt, a, b, c, un.r1 - un.r0, n, n, n, n, n), o.kernel, st);
+        HIP_OK(hipEventRecord(ready[u], st));
+        HIP_OK(hipStreamWaitEvent(cs, ready[u], 0));
+        NCCL_OK(ncclAllReduce(c, c, (size_t)(un.r1 - un.r0) * n, nccl_type(dt), ncclSum, comm, cs));
+        HIP_OK(hipEventRecord(done[u], cs));
+        used[u] = true;
+      }
+      for (size_t u = 0; u < units.size(); ++u) HIP_OK(hipStreamWaitEvent(st, done[u], 0));
+    };
+    const bool ov = o.overlap && dist;
+    for (int i = 0; i < o.warmup; ++i) ov ? overlap_iter() : serial_iter(nullptr);
+    HIP_OK(hipStreamSynchronize(st));
+    // compute-only reference time
+    {
+      hipEvent_t c0 = event(), c1 = event();
+      HIP_OK(hipEventRecord(c0, st));
+      for (int i = 0; i < std::min(o.iters, 10); ++i) gemm(p, o.kernel, st);
+      HIP_OK(hipEventRecord(c1, st));
+      HIP_OK(hipEventSynchronize(c1));
+      res.comp_ms = elapsed(c0, c1) / std::max(1, std::min(o.iters, 10));
+    }
+    bar.wait();
+    if (ov) {
+      hipEvent_t e0 = event(), e1 = event();
+      HIP_OK(hipEventRecord(e0, st));
+      for (int i = 0; i < o.iters; ++i) overlap_iter();
+      HIP_OK(hipEventRecord(e1, st));
+      HIP_OK(hipEventSynchronize(e1));
+      res.avg_ms = elapsed(e0, e1) / std::max(o.iters, 1);
+      res.comm_ms = std::max(0.0, res.avg_ms - res.comp_ms);
+    } else {
+      std::vector<hipEvent_t> marks;
+      for (int i = 0; i <= o.iters; ++i) marks.push_back(event());
+      std::vector<hipEvent_t> mids;
+      for (int i = 0; i < o.iters; ++i) mids.push_back(event());
+      HIP_OK(hipEventRecord(marks[0], st));
+      for (int i = 0; i < o.iters; ++i) {
+        serial_iter(mids[i]);
+        HIP_OK(hipEventRecord(marks[i + 1], st));
+      }
+      HIP_OK(hipEventSynchronize(marks[o.iters]));
+      double comp = 0, cm = 0;
+      for (int i = 0; i < o.iters; ++i) {
+        comp += elapsed(marks[i], mids[i]);
+        cm += elapsed(mids[i], marks[i + 1]);
+      }
+      const int it = std::max(o.iters, 1);
+      res.comp_ms = comp / it;
+      res.comm_ms = cm / it;
+      res.avg_ms = res.comp_ms + res.comm_ms;
+    }
+    res.flops_local = flop * lb;
+    res.flops_total = flop * gb;
+    if (o.check)  // C[0] = sum over ranks of A_r[0] @ B_r[0]: partial refs are summed on the host
+      check_rows(dt, A.p, B.p, C.p, n, n, n, n, n, n, st, res.ref, res.got);
+  } else {  // matrix_parallel: replicated A, padded column shard of one global B
+    const int shard = ceil_div(ceil_div(n, ws), 8) * 8;
+    const int c0 = std::min(rank * shard, n), width = std::max(0, std::min(n, c0 + shard) - c0);
+    res.shard = shard;
+    Buf A((size_t)n * n * es), Bg((size_t)n * n * es), Bl((size_t)n * shard * es);
+    Buf Cl((size_t)n * shard * es), G((size_t)ws * n * shard * es);
+    fill(A.p, (long long)n * n, dt, 1000, st);
+    fill(Bg.p, (long long)n * n, dt, 1001, st);
+    HIP_OK(hipMemsetAsync(Bl.p, 0, Bl.bytes, st));
+    if (width)
+      HIP_OK(hipMemcpy2DAsync(Bl.p, shard * es, (char*)Bg.p + c0 * es, n * es, width * es, n,
+                              hipMemcpyDeviceToDevice, st));
+    const pdmb::Problem p = problem(dt, A.p, Bl.p, Cl.p, n, shard, n, n, shard, shard);
+    res.kernel = pdmb::kernel_name(pdmb::resolve_kernel(p, o.kernel));
+    const int ch = o.overlap ? effective_chunks(n, shard, o.chunks) : 1;
+    res.chunks = ch;
+    const auto rcs = row_chunks(n, ch);
+    // per-chunk gather buffers [ws * rows, shard] carved out of G
+    std::vector<char*> gb;
+    size_t off = 0;
+    for (auto rc : rcs) {
+      gb.push_back((char*)G.p + off);
+      off += (size_t)ws * (rc.second - rc.first) * shard * es;
+    }
+    std::vector<hipEvent_t> ready, done;
+    for (size_t j = 0; j < rcs.size(); ++j) {
+      ready.push_back(event());
+      done.push_back(event());
+    }
+    std::vector<bool> used(rcs.size(), false);
+    auto iter = [&](hipEvent_t em) {
+      if (!o.overlap) {
+        gemm(p, o.kernel, st);
+        if (em) HIP_OK(hipEventRecord(em, st));
+        NCCL_OK(ncclAllGather(Cl.p, G.p, (size_t)n * shard, nccl_type(dt), comm, st));
+        return;
+      }
+      for (size_t j = 0; j < rcs.size(); ++j) {
+        const int r0 = rcs[j].first, r1 = rcs[j].second;
+        char* a = (char*)A.p + (size_t)r0 * n * es;
+        char* c = (char*)Cl.p + (size_t)r0 * shard * es;
+        if (used[j]) HIP_OK(hipStreamWaitEvent(st, done[j], 0));
+        gemm(problem(dt, a, Bl.p, c, r1 - r0, shard, n, n, shard, shard), o.kernel, st);
+        HIP_OK(hipEventRecord(ready[j], st));
+        HIP_OK(hipStreamWaitEvent(cs, ready[j], 0));
+        NCCL_OK(ncclAllGather(c, gb[j], (size_t)(r1 - r0) * shard, nccl_type(dt), comm, cs));
+        HIP_OK(hipEventRecord(done[j], cs));
+        used[j] = true;
+      }
+      for (size_t j = 0; j < rcs.size(); ++j) HIP_OK(hipStreamWaitEvent(st, done[j], 0));
+    };
+    for (int i = 0; i < o.warmup; ++i) iter(nullptr);
+    HIP_OK(hipStreamSynchronize(st));
+    {
+      hipEvent_t q0 = event(), q1 = event();
+      HIP_OK(hipEventRecord(q0, st));
+      for (int i = 0; i < std::min(o.iters, 10); ++i) gemm(p, o.kernel, st);
+      HIP_OK(hipEventRecord(q1, st));
+      HIP_OK(hipEventSynchronize(q1));
+      res.comp_ms = elapsed(q0, q1) / std::max(1, std::min(o.iters, 10));
+    }
+    bar.wait();
+    std::vector<hipEvent_t> marks, mids;
+    for (int i = 0; i <= o.iters; ++i) marks.push_back(event());
+    for (int i = 0; i < o.iters; ++i) mids.push_back(event());
+    HIP_OK(hipEventRecord(marks[0], st));
+    for (int i = 0; i < o.iters; ++i) {
+      iter(o.overlap ? nullptr : mids[i]);
+      HIP_OK(hipEventRecord(marks[i + 1], st));
+    }
+    HIP_OK(hipEventSynchronize(marks[o.iters]));
+    const int it = std::max(o.iters, 1);
+    res.avg_ms = elapsed(marks[0], marks[o.iters]) / it;
+    if (!o.overlap) {
+      double comp = 0;
+      for (int i = 0; i < o.iters; ++i) comp += elapsed(marks[i], mids[i]);
+      res.comp_ms = comp / it;
+    }
+    res.comm_ms = std::max(0.0, res.avg_ms - res.comp_ms);
+    res.flops_local = 2.0 * n * (double)shard * n;
+    res.flops_total = flop;
+    if (o.check) {
+      // This rank's reference: sampled rows of A @ B_local (its shard). The
+      // gathered rows of EVERY shard as seen on this rank go to `got`
+      // ([ws][rows][shard] order); the host matches got(0)[r] with ref(r).
+      std::vector<double> own;
+      check_rows(dt, A.p, Bl.p, Cl.p, n, shard, n, n, shard, shard, st, res.ref, own);
+      const std::vector<int> rows = sample_rows(n, 32);
+      std::vector<unsigned short> h16;
+      std::vector<float> h32;
+      res.got.clear();
+      for (int r = 0; r < ws; ++r)
+        for (int row : rows) {
+          size_t j = 0;
+          while (j + 1 < rcs.size() && row >= rcs[j].second) ++j;
+          const int r0 = rcs[j].first, rows_j = rcs[j].second - r0;
+          const char* base = o.overlap ? gb[j] + ((size_t)r * rows_j + (row - r0)) * shard * es
+                                       : (char*)G.p + ((size_t)r * n + row) * shard * es;
+          if (dt == 0) {
+            h32.resize(shard);
+            HIP_OK(hipMemcpy(h32.data(), base, shard * 4, hipMemcpyDeviceToHost));
+            for (float v : h32) res.got.push_back(v);
+          } else {
+            h16.resize(shard);
+            HIP_OK(hipMemcpy(h16.data(), base, shard * 2, hipMemcpyDeviceToHost));
+            for (unsigned short v : h16) {
+              float f;
+              if (dt == 2) {
+                unsigned int u = (unsigned int)v << 16;
+                std::memcpy(&f, &u, 4);
+              } else {
+                f = (float)__builtin_bit_cast(_Float16, v);
+              }
+              res.got.push_back(f);
+            }
+          }
+        }
+    }
+  }
+  for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(st);
+  (void)hipStreamDestroy(cs);
+}
+
+double norm_relerr(const std::vector<double>& got, const std::vector<double>& ref) {
+  double num = 0, den = 0;
+  for (size_t i = 0; i < ref.size() && i < got.size(); ++i) {
+    num += (got[i] - ref[i]) * (got[i] - ref[i]);
+    den += ref[i] * ref[i];
+  }
+  return std::sqrt(num / std::max(den, 1e-300));
+}
+
+void usage() {
+  std::printf(
+      "pdmb_bench [--gpus N] [--sizes N ...] [--iterations I] [--warmup W]\n"
+      "           [--dtype bfloat16|float16|float32] [--mode independent|batch_parallel|matrix_parallel]\n"
+      "           [--batch B] [--overlap] [--chunks C] [--kernel ID] [--check] [--json FILE]\n");
+}
+
+Opts parse(int argc, char** argv) {
+  Opts o;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto next = [&]() -> std::string {
+      if (i + 1 >= argc) throw std::runtime_error("missing value for " + a);
+      return argv[++i];
+    };
+    if (a == "--gpus") o.gpus = std::stoi(next());
+    else if (a == "--iterations") o.iters = std::stoi(next());
+    else if (a == "--warmup") o.warmup = std::stoi(next());
+    else if (a == "--batch") o.batch = std::stoi(next());
+    else if (a == "--chunks") o.chunks = std::stoi(next());
+    else if (a == "--kernel") o.kernel = std::stoi(next());
+    else if (a == "--overlap") o.overlap = true;
+    else if (a == "--check") o.check = true;
+    else if (a == "--json") o.json = next();
+    else if (a == "--dtype") {
+      const std::string d = next();
+      o.dtype = d == "float32" ? 0 : d == "float16" ? 1 : d == "bfloat16" ? 2 : -1;
+      if (o.dtype < 0) throw std::runtime_error("bad --dtype " + d);
+    } else if (a == "--mode") {
+      const std::string m = next();
+      if (m == "independent") o.mode = kIndependent;
+      else if (m == "batch_parallel") o.mode = kBatchParallel;
+      else if (m == "matrix_parallel") o.mode = kMatrixParallel;
+      else throw std::runtime_error("bad --mode " + m);
+    } else if (a == "--sizes") {
+      o.sizes.clear();
+      while (i + 1 < argc && argv[i + 1][0] != '-') o.sizes.push_back(std::stoi(argv[++i]));
+    } else if (a == "-h" || a == "--help") {
+      usage();
+      std::exit(0);
+    } else {
+      throw std::runtime_error("unknown argument " + a);
+    }
+  }
+  return o;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Opts o;
+  try {
+    o = parse(argc, argv);
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "error: %s\n", e.what());
+    usage();
+    return 2;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < o.gpus || o.gpus < 1) {
+    std::fprintf(stderr, "error: %d GPU(s) requested, %d visible\n", o.gpus, ndev);
+    return 2;
+  }
+  hipDeviceProp_t prop;
+  (void)hipGetDeviceProperties(&prop, 0);
+  std::printf("pdmb_bench (native HIP + RCCL executor)\n  GPU 0: %s (%s), %d CUs\n", prop.name,
+              prop.gcnArchName, prop.multiProcessorCount);
+  std::printf("  Mode: %s%s, GPUs: %d, dtype: %s, iterations: %d, warmup: %d\n", mode_name(o.mode),
+              o.overlap ? " (overlap)" : "", o.gpus, dtype_name(o.dtype), o.iters, o.warmup);
+  std::vector<ncclComm_t> comms(o.gpus, nullptr);
+  if (o.mode != kIndependent) {
+    std::vector<int> devs(o.gpus);
+    for (int i = 0; i < o.gpus; ++i) devs[i] = i;
+    try {
+      NCCL_OK(ncclCommInitAll(comms.data(), o.gpus, devs.data()));
+    } catch (const std::exception& e) {
+      std::fprintf(stderr, "error: %s\n", e.what());
+      return 1;
+    }
+  }
+  FILE* js = o.json.empty() ? nullptr : std::fopen(o.json.c_str(), "a");
+  int failures = 0;
+  for (int n : o.sizes) {
+    std::printf("\nBenchmarking %dx%d matrix multiplication:\n", n, n);
+    std::vector<Result> res(o.gpus);
+    Barrier bar(o.gpus);
+    std::vector<std::thread> th;
+    for (int r = 0; r < o.gpus; ++r)
+      th.emplace_back([&, r] {
+        try {
+          run_rank(r, o, n, comms[r], bar, res[r]);
+        } catch (const std::exception& e) {
+          res[r].error = e.what();
+          bar.abort();
+        }
+      });
+    for (auto& t : th) t.join();
+    std::string err;
+    for (auto& r : res)
+      if (!r.error.empty()) err = r.error;
+    if (!err.empty()) {
+      std::printf("\n  ERROR: %s\n", err.c_str());
+      ++failures;
+      continue;  // (a failed rank may leave peers' collectives pending; abort the sweep)
+    }
+    double avg = 0, mx = 0, comp = 0, cm = 0;
+    for (auto& r : res) {
+      avg += r.avg_ms / o.gpus;
+      mx = std::max(mx, r.avg_ms);
+      comp += r.comp_ms / o.gpus;
+      cm += r.comm_ms / o.gpus;
+    }
+    const Result& r0 = res[0];
+    const double per_gpu = r0.flops_local / (r0.avg_ms * 1e-3) / 1e12;
+    const double node = r0.flops_total / (mx * 1e-3) / 1e12;
+    const double actual = r0.flops_total / (avg * 1e-3) / 1e12;
+    std::printf("\nResults for %dx%d:\n", n, n);
+    std::printf("  - Average time per operation: %.3f ms\n", avg);
+    if (o.mode != kIndependent)
+      std::printf("  - Compute time: %.3f ms, Comm time: %.3f ms%s\n", comp, cm,
+                  o.overlap ? " (overlapped; comm = exposed part)" : "");
+    std::printf("  - TFLOPS per GPU: %.2f\n", per_gpu);
+    if (o.mode == kBatchParallel)
+      std::printf("  - Processing %d total batches across %d GPU(s) (%d per GPU)\n", r0.global_batch,
+                  o.gpus, r0.local_batch);
+    std::printf("  - Total system TFLOPS: %.2f\n", o.mode == kMatrixParallel ? actual : per_gpu * o.gpus);
+    std::printf("  - Actual TFLOPS (total FLOPs / time): %.2f\n", actual);
+    std::printf("  - Node TFLOPS (all FLOPs / slowest rank): %.2f\n", node);
+    std::printf("  - Kernel: %s\n", r0.kernel.c_str());
+    double relerr = -1;
+    if (o.check) {
+      if (o.mode == kBatchParallel) {
+        std::vector<double> sum(r0.ref.size(), 0.0);
+        for (auto& r : res)
+          for (size_t i = 0; i < sum.size(); ++i) sum[i] += r.ref[i];
+        for (auto& r : res) relerr = std::max(relerr, norm_relerr(r.got, sum));
+      } else if (o.mode == kMatrixParallel) {
+        const size_t blk = r0.ref.size();
+        for (auto& r : res)
+          for (int q = 0; q < o.gpus; ++q) {
+            std::vector<double> g(r.got.begin() + q * blk, r.got.begin() + (q + 1) * blk);
+            relerr = std::max(relerr, norm_relerr(g, res[q].ref));
+          }
+      } else {
+        for (auto& r : res) relerr = std::max(relerr, norm_relerr(r.got, r.ref));
+      }
+      const double tol = o.dtype == 0 ? 1e-5 : o.dtype == 1 ? 2e-3 : 1e-2;
+      const bool ok = relerr < tol;
+      failures += !ok;
+      std::printf("  - Check: max rel. error %.2e (%s)\n", relerr, ok ? "PASS" : "FAIL");
+    }
+    if (js) {
+      std::fprintf(js,
+                   "{\"script\": \"pdmb_bench\", \"mode\": \"%s\", \"overlap\": %s, \"n\": %d, "
+                   "\"dtype\": \"%s\", \"world_size\": %d, \"iterations\": %d, \"warmup\": %d, "
+                   "\"avg_ms\": %.6f, \"max_ms\": %.6f, \"compute_ms\": %.6f, \"comm_ms\": %.6f, "
+                   "\"tflops_rank0\": %.3f, \"node_tflops\": %.3f, \"actual_tflops\": %.3f, "
+                   "\"kernel\": \"%s\", \"relerr\": %s}\n",
+                   mode_name(o.mode), o.overlap ? "true" : "false", n, dtype_name(o.dtype), o.gpus,
+                   o.iters, o.warmup, avg, mx, comp, cm, per_gpu, node, actual, r0.kernel.c_str(),
+                   relerr < 0 ? "null" : std::to_string(relerr).c_str());
+      std::fflush(js);
+    }
+  }
+  if (js) std::fclose(js);
+  for (auto c : comms)
+    if (c) ncclCommDestroy(c);
+  std::printf("\nBenchmark completed!\n");
+  return failures ? 1 : 0;
+}

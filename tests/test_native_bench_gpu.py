@@ -1,0 +1,37 @@
+"""The Python-free native executor (runtime/pdmb_bench: HIP threads + RCCL) on the GPU:
+every scaling mode, serialized and overlapped, with the float64 end-to-end check."""
+import json
+import os
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "pytorch_distributed_matmul_benchmark_amd", "runtime", "pdmb_bench")
+
+
+@pytest.fixture(scope="module")
+def exe():
+    if not os.path.exists(EXE):
+        from pytorch_distributed_matmul_benchmark_amd.ops import build
+        build.build_bench()
+    return EXE
+
+
+@pytest.mark.parametrize("mode,extra", [("independent", []), ("batch_parallel", []),
+                                        ("batch_parallel", ["--overlap"]),
+                                        ("matrix_parallel", []),
+                                        ("matrix_parallel", ["--overlap"])])
+@pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
+def test_native_executor_modes(exe, mode, extra, dtype, tmp_path):
+    js = tmp_path / "r.jsonl"
+    r = subprocess.run([exe, "--gpus", "1", "--sizes", "1024", "2304", "--iterations", "3",
+                        "--warmup", "1", "--dtype", dtype, "--mode", mode, "--check",
+                        "--json", str(js), *extra],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.stdout.count("PASS") == 2 and "FAIL" not in r.stdout
+    recs = [json.loads(l) for l in js.read_text().splitlines()]
+    assert [x["n"] for x in recs] == [1024, 2304]
+    assert all(x["node_tflops"] > 0 and x["relerr"] is not None for x in recs)
