@@ -16,7 +16,7 @@ bool gemm256_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b
 hipError_t gemm256_launch(int dt, GemmArgs a, int sched, hipStream_t stream);
 hipError_t gemm_generic_launch(int dt, GemmArgs a, bool vec, hipStream_t stream);
 bool gemm_f32_256_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
-hipError_t gemm_f32_256_launch(GemmArgs a, bool stagger, hipStream_t stream);
+hipError_t gemm_f32_256_launch(GemmArgs a, int variant, hipStream_t stream);
 
 static unsigned long long* g_debug_buffer = nullptr;
 
@@ -87,8 +87,8 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
   if (k == kMfma256b) return gemm256_launch(p.dtype, a, 1, stream);
   if (k == kMfma256c) return gemm256_launch(p.dtype, a, 2, stream);
   if (k == kMfma256Stamp) return gemm256_launch(p.dtype, a, 3, stream);
-  if (k == kF32_256) return gemm_f32_256_launch(a, false, stream);
-  if (k == kF32_256s) return gemm_f32_256_launch(a, true, stream);
+  if (k == kF32_256) return gemm_f32_256_launch(a, 0, stream);
+  if (k == kF32_256s) return gemm_f32_256_launch(a, 1, stream);
   return gemm_generic_launch(p.dtype, a, generic_vec_ok(p), stream);
 }
 

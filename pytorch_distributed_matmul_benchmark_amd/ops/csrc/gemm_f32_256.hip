@@ -48,16 +48,17 @@ struct Ctx {
 // (one k-row each) per wave.
 template <int STG>
 __device__ __forceinline__ void issue_tile(const Ctx& c, int tile) {
+  constexpr int ST = STAGE, BP = B_PITCH;
   const long long offA = (long long)tile * BK * 4;
   const u32x4 ra = make_rsrc(c.Ab + offA, c.a_bytes - offA);
   const long long offB = (long long)tile * BK * c.ldb4;
   const u32x4 rb = make_rsrc(c.Bb + offB, c.b_bytes - offB);
 #pragma unroll
   for (int h = 0; h < 4; ++h)
-    dma16(ra, c.voffA[h], c.lds0 + STG * STAGE + (h * 8 + c.wu) * 8 * 128);
+    dma16(ra, c.voffA[h], c.lds0 + STG * ST + (h * 8 + c.wu) * 8 * 128);
 #pragma unroll
   for (int h = 0; h < 4; ++h)
-    dma16(rb, c.voffB[h], c.lds0 + STG * STAGE + A_BYTES + (h * 8 + c.wu) * B_PITCH);
+    dma16(rb, c.voffB[h], c.lds0 + STG * ST + A_BYTES + (h * 8 + c.wu) * BP);
 }
 
 template <int STG, int KB>
@@ -148,9 +149,9 @@ __global__ void __launch_bounds__(NT, 2) gemm_f32_256(GemmArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  const int nk = c.nk;
   issue_tile<0>(c, 0);
   tile_barrier();
-  const int nk = c.nk;
   for (int t = 0; t < nk; t += 2) {
     // The stage being refilled was last read in the previous K-tile, which
     // ended with a barrier (WAR); the refill has a whole K-tile to land and
@@ -191,19 +192,18 @@ bool gemm_f32_256_supported(const GemmArgs& a, size_t align_a, size_t align_b, s
   return true;
 }
 
-hipError_t gemm_f32_256_launch(GemmArgs a, bool stagger, hipStream_t stream) {
+hipError_t gemm_f32_256_launch(GemmArgs a, int variant, hipStream_t stream) {
   a.tiles_m = (a.M + kf32::BM - 1) / kf32::BM;
   a.tiles_n = (a.N + kf32::BN - 1) / kf32::BN;
   a.supertile = (a.tiles_m % 16 == 0 && a.tiles_n % 16 == 0) ? 1 : 0;
   const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch;
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
-  if (stagger)
-    hipLaunchKernelGGL(kf32::gemm_f32_256<true>, dim3((unsigned)nblocks), dim3(kf32::NT), 0,
-                       stream, a);
+  const dim3 grid((unsigned)nblocks), block(kf32::NT);
+  if (variant == 1)
+    hipLaunchKernelGGL(kf32::gemm_f32_256<true>, grid, block, 0, stream, a);
   else
-    hipLaunchKernelGGL(kf32::gemm_f32_256<false>, dim3((unsigned)nblocks), dim3(kf32::NT), 0,
-                       stream, a);
+    hipLaunchKernelGGL(kf32::gemm_f32_256<false>, grid, block, 0, stream, a);
   return hipGetLastError();
 }
 
