@@ -89,6 +89,9 @@ def build_parser(kind: str) -> argparse.ArgumentParser:
     g.add_argument("--json", default=None, help="append one JSON record per result to this file")
     g.add_argument("--single-gpu-tflops", type=float, default=None,
                    help="measured 1-GPU TFLOPS for the 'efficiency vs 1 GPU' line")
+    g.add_argument("--scaling-ref", action="store_true",
+                   help="before each size, time the N×N GEMM on rank 0 ALONE (other ranks idle) "
+                        "and report scaling efficiency = node TFLOPS / (ws × that)")
     g.add_argument("--timeout", type=float, default=600.0, help="process-group timeout (s)")
     g.add_argument("--debug", action="store_true", help="print tracebacks of failed sizes")
     g.add_argument("--profile", action="store_true",
@@ -106,6 +109,28 @@ def _workload(args, n: int, dtype: torch.dtype) -> Workload:
     return Workload(n=n, dtype=dtype, iters=args.iterations, warmup=args.warmup, seed=args.seed,
                     backend=args.backend, kernel=args.kernel, batch=args.batch,
                     overlap=args.overlap, chunks=args.chunks, graph=args.graph, check=args.check)
+
+
+def _single_gpu_reference(ctx: DistContext, args, n: int, dtype: torch.dtype) -> float:
+    """TFLOPS of one N×N GEMM on rank 0 while every other rank idles at a barrier:
+    the '1 GPU' denominator of the scaling efficiency, measured in the same job
+    on the same device and data distribution (broadcast to all ranks)."""
+    from .models import independent
+
+    val = 0.0
+    barrier(ctx)
+    if ctx.rank == 0:
+        try:  # never skip the collectives below: a failure here becomes "no reference"
+            w = _workload(args, n, dtype)
+            w.iters, w.warmup, w.check = max(3, min(args.iterations, 10)), max(1, min(args.warmup, 3)), False
+            one = DistContext(rank=0, world_size=1, local_rank=ctx.local_rank, device=ctx.device)
+            val = independent.run(w, one).tflops
+        except Exception as e:  # pragma: no cover
+            print(f"[rank 0] single-GPU reference failed: {e!r}", flush=True)
+            val = 0.0
+    barrier(ctx)
+    v = reduce_scalar(ctx, val, "sum")
+    return v if v > 0 else None
 
 
 def _aggregate(ctx: DistContext, r: ModeResult) -> Dict[str, Optional[float]]:
@@ -207,8 +232,10 @@ def _print_results(kind: str, mode: str, rep: Reporter, ctx: DistContext, n: int
 
     # MI355X additions, identical for every kind.
     rep.line(f"  - Node TFLOPS (all FLOPs / slowest rank): {agg['node_tflops']:.2f}")
-    if args.single_gpu_tflops:
-        eff = scaling_efficiency(agg["node_tflops"], ws, args.single_gpu_tflops)
+    ref1 = agg.get("single_gpu_tflops") or args.single_gpu_tflops
+    if ref1:
+        extra["single_gpu_tflops"] = ref1
+        eff = scaling_efficiency(agg["node_tflops"], ws, ref1)
         extra["scaling_efficiency_vs_1gpu"] = eff
         rep.line(f"  - Scaling efficiency vs 1 GPU: {eff:.1f}%")
     if kind != "basic":
@@ -283,8 +310,10 @@ def run_benchmarks(kind: str, ctx: DistContext, rep: Reporter, args) -> List[Dic
             rep.line(f"  - Mode: {mode}")
         if kind in ("distributed", "overlap"):
             rep.line("  - Running warmup and benchmark...")
-        res, err = None, None
+        res, err, ref1 = None, None, None
         try:
+            if getattr(args, "scaling_ref", False):
+                ref1 = _single_gpu_reference(ctx, args, n, dtype)
             with marker(f"{kind}/{mode}/{n}x{n}/{dtype_name(dtype)}/ws{ctx.world_size}",
                         enabled=getattr(args, "profile", False) and ctx.is_cuda):
                 res = run_mode(mode, _workload(args, n, dtype), ctx)
@@ -301,6 +330,8 @@ def run_benchmarks(kind: str, ctx: DistContext, rep: Reporter, args) -> List[Dic
             out.append({"n": n, "mode": mode, "error": err or "failed on another rank"})
         else:
             agg = _aggregate(ctx, res)
+            if ref1:
+                agg["single_gpu_tflops"] = ref1
             extra = _print_results(kind, mode, rep, ctx, n, dtype, res, agg, args)
             rec = {"script": kind, "mode": mode, "n": n, "dtype": dtype_name(dtype),
                    "world_size": ctx.world_size, "device": ctx.device.type,

@@ -135,3 +135,13 @@ def test_mode_enums_and_validate_result():
     assert r.relerr < 1e-5 and r.extra["global_batch"] == 4
     A, B = torch.randn(70, 33), torch.randn(33, 20)
     assert validate_result(A, B, A @ B) and not validate_result(A, B, A @ B + 0.1)
+
+
+def test_scaling_ref_reports_efficiency_vs_one_rank(tmp_path):
+    js = tmp_path / "r.jsonl"
+    out = _torchrun(2, "matmul_scaling_benchmark.py", "--device", "cpu", "--sizes", "160",
+                    "--iterations", "2", "--warmup", "1", "--dtype", "float32", "--mode",
+                    "independent", "--scaling-ref", "--json", str(js), port=29704)
+    assert "Scaling efficiency vs 1 GPU:" in out
+    rec = json.loads(js.read_text().splitlines()[-1])
+    assert rec["single_gpu_tflops"] > 0 and rec["scaling_efficiency_vs_1gpu"] > 0
