@@ -1,0 +1,60 @@
+"""Static checks of the generated gfx950 code (CPU only: hipcc cross-compiles).
+
+Guards the properties the kernels' performance depends on, so a source edit
+that silently de-pipelines them fails here instead of on the GPU:
+no register spills, the intended occupancy, exactly one vmcnt(0) drain (after
+the K-loop) in the LDS-DMA kernels, and the MFMA / LDS-DMA instruction mix."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                    "pytorch_distributed_matmul_benchmark_amd", "ops", "csrc")
+HIPCC = "/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else shutil.which("hipcc")
+pytestmark = pytest.mark.skipif(HIPCC is None, reason="hipcc not available")
+
+
+def _kernels(src, tmp_path):
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{CSRC}", "-c",
+                    os.path.join(CSRC, src), "-o", str(tmp_path / "k.o"), "-save-temps"],
+                   cwd=tmp_path, check=True, capture_output=True, timeout=600)
+    s = next(tmp_path.glob("*gfx950*.s")).read_text()
+    out = {}
+    for m in re.finditer(r"^([A-Za-z_][\w.$]*):\s*;\s*@", s, re.M):
+        name = m.group(1)
+        body = s[m.end():s.find(".Lfunc_end", m.end())]
+        i = s.find(f".amdhsa_kernel {name}")
+        kd = s[i:s.find(".end_amdhsa_kernel", i)]
+        vg = int(re.search(re.escape(name) + r"\.num_vgpr, (\d+)", s).group(1))
+        out[name] = dict(body=body, vgpr=vg,
+                         spill=int(re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", kd).group(1)),
+                         lds=int(re.search(r"\.amdhsa_group_segment_fixed_size (\d+)", kd).group(1)))
+    return out
+
+
+def test_bf16_lds_dma_kernel_stays_pipelined(tmp_path):
+    ks = _kernels("gemm_mfma256.hip", tmp_path)
+    main = [k for k in ks if "gemm256_nn" in k and "ILi2ELi2ELb0E" in k]
+    assert main, sorted(ks)
+    k = ks[main[0]]
+    b = k["body"]
+    assert k["spill"] == 0 and "scratch_" not in b
+    assert k["vgpr"] <= 256  # 2 waves per SIMD
+    assert k["lds"] == 131072
+    assert len(re.findall(r"s_waitcnt vmcnt\(0\)", b)) == 1  # only the post-loop drain
+    assert len(re.findall(r"s_waitcnt vmcnt\(10\)", b)) >= 8  # counted waits in the loop
+    assert len(re.findall(r"v_mfma_f32_16x16x32_bf16", b)) == 128  # 2 K-tiles unrolled
+    assert len(re.findall(r"buffer_load_dwordx4 .* lds", b)) >= 16
+    assert len(re.findall(r"ds_read_b64_tr_b16", b)) >= 32  # NN B operand, no transposed copy
+
+
+def test_f32_kernel_no_spill(tmp_path):
+    ks = _kernels("gemm_f32_256.hip", tmp_path)
+    assert ks
+    for name, k in ks.items():
+        assert k["spill"] == 0 and "scratch_" not in k["body"], name
+        assert k["vgpr"] <= 256, name
+        assert len(re.findall(r"v_mfma_f32_16x16x4_f32", k["body"])) == 512, name
