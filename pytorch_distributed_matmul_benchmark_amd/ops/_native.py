@@ -34,7 +34,18 @@ def load(build_if_missing: bool = True):
         if build_if_missing and os.environ.get("PDMB_NO_AUTOBUILD", "0") != "1":
             from . import build as _build
 
-            _build.build()
+            # One builder at a time: torchrun starts one process per GPU and all of
+            # them may find the extension missing; the others wait on the lock and
+            # then import what the first one built.
+            import fcntl
+
+            lock_path = os.path.join(os.path.dirname(os.path.abspath(__file__)), ".build.lock")
+            with open(lock_path, "w") as lk:
+                fcntl.flock(lk, fcntl.LOCK_EX)
+                try:
+                    _build.build()
+                finally:
+                    fcntl.flock(lk, fcntl.LOCK_UN)
             importlib.invalidate_caches()
             _mod = importlib.import_module(f"{__package__}._C")
             return _mod
