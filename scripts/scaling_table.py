@@ -34,6 +34,8 @@ def load(paths):
                 else:
                     if r.get("overlap"):
                         r = dict(r, mode=r["mode"] + "+overlap")
+                    if r.get("backend", "native") != "native":
+                        r = dict(r, mode=f"{r['mode']} [{r['backend']}]")
                 recs.append(r)
     return recs
 
