@@ -78,6 +78,10 @@ def kernel_label(w: Workload, A, B, out) -> str:
         return "torch.matmul(cpu)"
     if w.backend == "torch":
         return "torch.matmul(hipBLASLt)"
+    if w.kernel == "auto":
+        padded = _gemm.padded_kernel_for(A, B)
+        if padded:
+            return f"{padded} (zero-padded K/N)"
     return _gemm.kernel_for(A, B, out, kernel=w.kernel)
 
 

@@ -33,7 +33,9 @@ struct Problem {
 int resolve_kernel(const Problem& p, int kernel);
 
 // Enqueue C = A @ B on `stream`. Returns hipSuccess or an error; *used (if
-// non-null) receives the kernel that ran.
+// non-null) receives the kernel that ran. With kAuto, a large problem whose K /
+// N / alignment miss the fast kernels runs on them through zero-padded
+// workspace copies (gemm_dispatch.cpp "padded fast path").
 hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used);
 
 // Native timing loop: `warmup` untimed launches, then `iters` launches

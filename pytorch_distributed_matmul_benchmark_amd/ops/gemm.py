@@ -72,8 +72,22 @@ def matmul(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
     A, B = _prep(A), _prep(B)
     if out is None:
         out = torch.empty(_out_shape(A, B), dtype=A.dtype, device=A.device)
-    C.matmul(A, B, out, _kid(kernel))
+    C.matmul(A, B, out, _kid(kernel))  # auto: odd K/N/alignment padded onto the fast path (C++)
     return out
+
+
+PAD_MIN_FLOPS = 2.0 ** 31  # gemm_dispatch.cpp kPadMinFlops
+
+
+def padded_kernel_for(A: torch.Tensor, B: torch.Tensor) -> Optional[str]:
+    """Fast kernel an ``auto`` call runs through zero-padded copies, or None."""
+    if A.device.type != "cuda" or A.dtype not in SUPPORTED_DTYPES:
+        return None
+    M, K, N = A.shape[-2], A.shape[-1], B.shape[-1]
+    batch = max(A.shape[0] if A.dim() == 3 else 1, B.shape[0] if B.dim() == 3 else 1)
+    if 2.0 * M * N * K * batch < PAD_MIN_FLOPS or kernel_for(A, B) != "pdmb_generic_nn":
+        return None
+    return "pdmb_f32_256s_nn" if A.dtype == torch.float32 else "pdmb_mfma256c_nn"
 
 
 def bmm(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,

@@ -226,3 +226,37 @@ def test_f32_256_race_screen(kernel):
     assert _relerr(ref, R) < TOL[torch.float32]
     for _ in range(10):
         assert torch.equal(gemm.matmul(A, B, kernel=kernel), ref)
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16", "float32"])
+@pytest.mark.parametrize("M,N,K", [(2000, 1999, 1000), (1536, 1030, 2050)])
+def test_odd_sizes_padded_to_fast_path(dtype, M, N, K):
+    """Big problems with K / N off the fast kernels' granule run padded on the fast path."""
+    dt = DT[dtype]
+    torch.manual_seed(M + N)
+    A = torch.randn(M, K, device="cuda", dtype=dt)
+    B = torch.randn(K, N, device="cuda", dtype=dt)
+    assert gemm.kernel_for(A, B) == "pdmb_generic_nn"  # unpadded, only generic could run it
+    assert gemm.padded_kernel_for(A, B) in ("pdmb_mfma256c_nn", "pdmb_f32_256s_nn")
+    C = gemm.matmul(A, B)
+    assert C.shape == (M, N)
+    assert _relerr(C, _ref(A, B)) < TOL[dt]
+    out = torch.full((M, N), float("nan"), device="cuda", dtype=dt)
+    assert gemm.matmul(A, B, out=out).data_ptr() == out.data_ptr()
+    assert _relerr(out, _ref(A, B)) < TOL[dt]
+
+
+def test_padded_path_misaligned_views_and_batches():
+    torch.manual_seed(9)
+    big = torch.randn(1100, 2051, device="cuda", dtype=torch.bfloat16)
+    A = big[:, 1:2049]            # lda = 2051 (misaligned), K = 2048
+    B = torch.randn(2048, 1500, device="cuda", dtype=torch.bfloat16)
+    assert gemm.padded_kernel_for(A, B) == "pdmb_mfma256c_nn"
+    assert _relerr(gemm.matmul(A, B), _ref(A, B)) < TOL[torch.bfloat16]
+    A3 = torch.randn(3, 700, 1000, device="cuda", dtype=torch.float16)
+    B3 = torch.randn(3, 1000, 1300, device="cuda", dtype=torch.float16)
+    assert gemm.padded_kernel_for(A3, B3) == "pdmb_mfma256c_nn"
+    assert _relerr(gemm.bmm(A3, B3), torch.bmm(A3.double(), B3.double())) < TOL[torch.float16]
+    out = torch.empty(1100, 1500, device="cuda", dtype=torch.bfloat16)
+    ms = gemm.bench_matmul(A, B, out, iters=3, warmup=1)  # native loop takes the padded path too
+    assert ms > 0 and _relerr(out, _ref(A, B)) < TOL[torch.bfloat16]
