@@ -1,8 +1,10 @@
 """GEMM entry points: ``matmul`` / ``bmm`` / ``bench_matmul``.
 
-GPU tensors run on the hand-written gfx950 MFMA kernels of ``ops/csrc``
-(``gemm_mfma256.hip`` for the benchmark shapes, ``gemm_generic.hip`` for
-everything else and for fp32). CPU tensors use ``torch.matmul`` — the
+GPU tensors run on the hand-written gfx950 MFMA kernels of ``ops/csrc``:
+``gemm_mfma256.hip`` (bf16/fp16) and ``gemm_f32_256.hip`` (exact fp32) for
+every shape whose K / N / alignment fit their LDS-DMA granule — larger
+problems that do not are zero-padded onto them by the C++ dispatch — and
+``gemm_generic.hip`` for the rest. CPU tensors use ``torch.matmul`` — the
 reference's own compute call (matmul_benchmark.py:46) — which is the
 BASELINE config #1 CPU path ("4k fp32 matmul, single process on CPU").
 

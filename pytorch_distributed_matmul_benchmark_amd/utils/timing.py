@@ -109,17 +109,6 @@ def time_loop_ms(fn, iters: int, warmup: int, device: torch.device, stream=None,
     return sw.elapsed_ms()
 
 
-class Timings(dict):
-    """Convenience: ``Timings(compute=…, comm=…)`` in ms with a ``total``."""
-
-    @property
-    def total(self) -> float:
-        return float(sum(self.values()))
-
-    def get_ms(self, key: str, default: Optional[float] = 0.0) -> float:
-        return float(self.get(key, default))
-
-
 @contextlib.contextmanager
 def marker(name: str, enabled: bool = True):
     """A named range in the profiler timeline (roctx on PyTorch-ROCm:
