@@ -135,7 +135,8 @@ __device__ __forceinline__ void dma16(u32x4 rsrc, uint32_t voff, uint32_t lds_ba
 // whole chip touches 32 panels per K-step (shared through Infinity Cache).
 // Super-tiles sweep N fastest so A panels stay Infinity-Cache resident.
 // Otherwise: grouped order with 16 tile-rows per group (chip-wide locality).
-__device__ __forceinline__ void map_tile(const GemmArgs& a, int b, int& bz, int& tm, int& tn) {
+__device__ __forceinline__ void map_tile(const GemmArgs& a, int b, int& bz, int& tm, int& tn,
+                                         bool tall = false) {
   const int tpb = a.tiles_m * a.tiles_n;
   if (a.supertile) {
     const int x = b & 7, j = b >> 3;
@@ -145,8 +146,13 @@ __device__ __forceinline__ void map_tile(const GemmArgs& a, int b, int& bz, int&
     bz = round / st_per_b;
     const int s = round - bz * st_per_b;
     const int sr = s / st_n, sc = s - sr * st_n;
-    tm = (sr << 4) + ((x >> 1) << 2) + (i >> 3);
-    tn = (sc << 4) + ((x & 1) << 3) + (i & 7);
+    if (tall) {  // XCD sub-block 8 (M) x 4 (N)
+      tm = (sr << 4) + ((x & 1) << 3) + (i >> 2);
+      tn = (sc << 4) + ((x >> 1) << 2) + (i & 3);
+    } else {     // XCD sub-block 4 (M) x 8 (N)
+      tm = (sr << 4) + ((x >> 1) << 2) + (i >> 3);
+      tn = (sc << 4) + ((x & 1) << 3) + (i & 7);
+    }
   } else {
     bz = b / tpb;
     const int L = b - bz * tpb;

@@ -61,6 +61,8 @@ int resolve_kernel(const Problem& p, int kernel) {
                        gemm_f32_256_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   if (kernel == kAuto) return fast ? kMfma256c : (f32fast ? kF32_256s : kGeneric);
   if (kernel == kF32_256) return f32fast ? kF32_256 : -1;
+  if (kernel >= kMfma256X1 && kernel <= kMfma256X4)
+    return (fast && p.dtype == kBF16) ? kernel : -1;
   if (kernel == kF32_256s) return f32fast ? kF32_256s : -1;
   if (kernel == kMfma256) return fast ? kMfma256 : -1;
   if (kernel == kMfma256b) return fast ? kMfma256b : -1;
@@ -246,6 +248,7 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
   if (k == kMfma256c) return gemm256_launch(p.dtype, a, 2, stream);
   if (k == kMfma256Stamp) return gemm256_launch(p.dtype, a, 3, stream);
   if (k == kF32_256) return gemm_f32_256_launch(a, 0, stream);
+  if (k >= kMfma256X1 && k <= kMfma256X4) return gemm256_launch(p.dtype, a, 10 + (k - kMfma256X1 + 1), stream);
   if (k == kF32_256s) return gemm_f32_256_launch(a, 1, stream);
   return gemm_generic_launch(p.dtype, a, generic_vec_ok(p), stream);
 }

@@ -134,10 +134,13 @@ __device__ __forceinline__ void read_b(const Ctx& c, const char* smem, s16x8 (&r
     }
 }
 
-template <int DT, int MQ, int NQ>
+// XF: experiment flags of the SCHED 2 kernel (A/B only; 0 = shipped default).
+//   1: no s_setprio around the MFMA cluster;  2: static priority (waves 4..7
+//   raised once, no per-cluster flips);  4: XCD sub-block 8 (M) x 4 (N).
+template <int DT, int MQ, int NQ, int XF = 0>
 __device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[8][4], const s16x8 (&ra)[4][2],
                                              const s16x8 (&rb)[2][2]) {
-  __builtin_amdgcn_s_setprio(1);
+  if constexpr (!(XF & 3)) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -146,7 +149,7 @@ __device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[8][4], const s16x8 (&r
       for (int ni = 0; ni < 2; ++ni)
         acc[MQ * 4 + mi][NQ * 2 + ni] =
             mfma16x16x32<DT>(rb[ni][ks], ra[mi][ks], acc[MQ * 4 + mi][NQ * 2 + ni]);
-  __builtin_amdgcn_s_setprio(0);
+  if constexpr (!(XF & 3)) __builtin_amdgcn_s_setprio(0);
 }
 
 #define PDMB_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
@@ -198,7 +201,7 @@ __device__ __forceinline__ void slot_barrier(unsigned long long& sum) {
 //   RAW — after issuing unit P+7 a wave waits vmcnt(10): units <= P+2 have
 //     landed, which the read slot of P+1 (one barrier later for the lagging
 //     group) needs. Each unit now gets one more slot of flight time.
-template <int DT, int STG, int SCHED, bool STAMP = false>
+template <int DT, int STG, int SCHED, bool STAMP = false, int XF = 0>
 __device__ __forceinline__ void tile_body(const Ctx& c, char* smem, int t, f32x4 (&acc)[8][4],
                                           s16x8 (&ra)[4][2], s16x8 (&ra2)[4][2],
                                           s16x8 (&rb0)[2][2], s16x8 (&rb1)[2][2], Stamp& st) {
@@ -247,7 +250,7 @@ __device__ __forceinline__ void tile_body(const Ctx& c, char* smem, int t, f32x4
     PDMB_LGKM0();
     PDMB_VMCNT(10);
     slot_barrier<STAMP>(st.wr);
-    mma_quadrant<DT, 0, 0>(acc, ra2, rb0);
+    mma_quadrant<DT, 0, 0, XF>(acc, ra2, rb0);
     slot_barrier<STAMP>(st.wc);
     // phase q=1: quadrant (0,1)
     read_b<STG, 1>(c, smem, rb1);
@@ -255,7 +258,7 @@ __device__ __forceinline__ void tile_body(const Ctx& c, char* smem, int t, f32x4
     PDMB_LGKM0();
     PDMB_VMCNT(10);
     slot_barrier<STAMP>(st.wr);
-    mma_quadrant<DT, 0, 1>(acc, ra2, rb1);
+    mma_quadrant<DT, 0, 1, XF>(acc, ra2, rb1);
     slot_barrier<STAMP>(st.wc);
     // phase q=2: quadrant (1,1)
     read_a<STG, 1>(c, smem, ra);
@@ -263,7 +266,7 @@ __device__ __forceinline__ void tile_body(const Ctx& c, char* smem, int t, f32x4
     PDMB_LGKM0();
     PDMB_VMCNT(10);
     slot_barrier<STAMP>(st.wr);
-    mma_quadrant<DT, 1, 1>(acc, ra, rb1);
+    mma_quadrant<DT, 1, 1, XF>(acc, ra, rb1);
     slot_barrier<STAMP>(st.wc);
     // phase q=3: quadrant (1,0); prefetch next tile's A0 fragments
     read_a<STG ^ 1, 0>(c, smem, ra2);
@@ -271,7 +274,7 @@ __device__ __forceinline__ void tile_body(const Ctx& c, char* smem, int t, f32x4
     PDMB_LGKM0();
     PDMB_VMCNT(10);
     slot_barrier<STAMP>(st.wr);
-    mma_quadrant<DT, 1, 0>(acc, ra, rb0);
+    mma_quadrant<DT, 1, 0, XF>(acc, ra, rb0);
     slot_barrier<STAMP>(st.wc);
   } else {
     // phase q=0: quadrant (0,0)
@@ -308,17 +311,20 @@ __device__ __forceinline__ void tile_body(const Ctx& c, char* smem, int t, f32x4
   }
 }
 
-template <int DT, int SCHED, bool STAMP = false>
+template <int DT, int SCHED, bool STAMP = false, int XF = 0>
 __global__ void __launch_bounds__(NTHREADS, 2) gemm256_nn(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
   int bz, tm, tn;
-  map_tile(a, blockIdx.x, bz, tm, tn);
+  map_tile(a, blockIdx.x, bz, tm, tn, (XF & 4) != 0);
   const int m0 = tm * BM, n0 = tn * BN;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wu = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if constexpr ((XF & 2) != 0) {
+    if (wu >= 4) __builtin_amdgcn_s_setprio(1);
+  }
   const int wr = wu >> 2, wc = wu & 3;
   const int l16 = lane & 15, g = lane >> 4;
 
@@ -396,8 +402,8 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm256_nn(GemmArgs a) {
   unsigned long long t_loop0 = 0;
   if constexpr (STAMP) t_loop0 = stamp_now();
   for (int t = 0; t < nk; t += 2) {
-    tile_body<DT, 0, SCHED, STAMP>(c, smem, t, acc, ra, ra2, rb0, rb1, st);
-    if (t + 1 < nk) tile_body<DT, 1, SCHED, STAMP>(c, smem, t + 1, acc, ra, ra2, rb0, rb1, st);
+    tile_body<DT, 0, SCHED, STAMP, XF>(c, smem, t, acc, ra, ra2, rb0, rb1, st);
+    if (t + 1 < nk) tile_body<DT, 1, SCHED, STAMP, XF>(c, smem, t + 1, acc, ra, ra2, rb0, rb1, st);
   }
   if constexpr (STAMP) {
     const unsigned long long t_loop1 = stamp_now();
@@ -458,6 +464,16 @@ hipError_t gemm256_launch(int dt, GemmArgs a, int sched, hipStream_t stream) {
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
   dim3 grid((unsigned)nblocks), block(k256::NTHREADS);
 #define PDMB_LAUNCH256(D, S) hipLaunchKernelGGL((k256::gemm256_nn<D, S>), grid, block, 0, stream, a)
+  if (sched >= 10) {  // SCHED 2 experiment flags (bf16 only, A/B builds)
+    if (dt != kBF16) return hipErrorInvalidValue;
+    switch (sched - 10) {
+      case 1: hipLaunchKernelGGL((k256::gemm256_nn<kBF16, 2, false, 1>), grid, block, 0, stream, a); break;
+      case 2: hipLaunchKernelGGL((k256::gemm256_nn<kBF16, 2, false, 2>), grid, block, 0, stream, a); break;
+      case 4: hipLaunchKernelGGL((k256::gemm256_nn<kBF16, 2, false, 4>), grid, block, 0, stream, a); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   if (sched == 3) {  // diagnostic stamp build of SCHED 2 (bf16 only)
     if (dt != kBF16 || !a.dbg) return hipErrorInvalidValue;
     hipLaunchKernelGGL((k256::gemm256_nn<kBF16, 2, true>), grid, block, 0, stream, a);
