@@ -14,7 +14,7 @@ enum Kernel : int {
   kMfma256c = 4,  // SCHED 1 + fragment reads balanced over the read slots (SCHED 2)
   kF32_256 = 6,   // gemm_f32_256.hip: exact-fp32 MFMA, 256x256 LDS-DMA tile
   kF32_256s = 7,  // same, DMA issue staggered between the two waves of a SIMD
-  kMfma256X1 = 10,  // SCHED 2 experiment builds (A/B only): 10 = no setprio,
+  kMfma256X1 = 10,  // SCHED 2 experiment builds (A/B only): 10 = per-cluster setprio,
   kMfma256X2 = 11,  //   11 = static priority of waves 4..7,
   kMfma256X4 = 13,  //   13 = XCD sub-block 8x4 (12 unused)
   kMfma256Stamp = 5,  // diagnostic: SCHED 2 with in-kernel barrier-wait stamps (needs a debug buffer)

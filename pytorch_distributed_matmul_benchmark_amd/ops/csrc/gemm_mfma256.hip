@@ -32,7 +32,8 @@
 //    the R slot, 2 = 1 + reads balanced to 8 per R slot by prefetching the
 //    next tile's A0 fragments in phase 3 into a second A register set.
 //    Measured on MI355X, 16384^3 bf16 random data: 1315 / 1370 / 1440 TF
-//    (hipBLASLt 1362 on the same data).
+//    (hipBLASLt 1362 on the same data); SCHED 2 without per-cluster
+//    s_setprio is a further +0.9 % (scripts/ab_kernels.py).
 //  * LDS-DMA units (A-half = 16 KiB, B-half = 16 KiB) are refilled as soon
 //    as the last reader of their previous contents has retired, so every
 //    unit has ~5-6 phases of flight time. The wait is a counted
@@ -135,8 +136,10 @@ __device__ __forceinline__ void read_b(const Ctx& c, const char* smem, s16x8 (&r
 }
 
 // XF: experiment flags of the SCHED 2 kernel (A/B only; 0 = shipped default).
-//   1: no s_setprio around the MFMA cluster;  2: static priority (waves 4..7
-//   raised once, no per-cluster flips);  4: XCD sub-block 8 (M) x 4 (N).
+//   1: s_setprio(1)/(0) around every MFMA cluster (the SCHED 0/1 style; the
+//      default SCHED 2 build has none: +0.9 % at 8k and 16k, A/B in one process);
+//   2: static priority (waves 4..7 raised once);  4: XCD sub-block 8 (M) x 4 (N)
+//      (-1.5 % at 16k). Inside mma_quadrant, bit 0 set = NO per-cluster priority.
 template <int DT, int MQ, int NQ, int XF = 0>
 __device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[8][4], const s16x8 (&ra)[4][2],
                                              const s16x8 (&rb)[2][2]) {
@@ -250,7 +253,7 @@ __device__ __forceinline__ void tile_body(const Ctx& c, char* smem, int t, f32x4
     PDMB_LGKM0();
     PDMB_VMCNT(10);
     slot_barrier<STAMP>(st.wr);
-    mma_quadrant<DT, 0, 0, XF>(acc, ra2, rb0);
+    mma_quadrant<DT, 0, 0, (XF ^ 1)>(acc, ra2, rb0);
     slot_barrier<STAMP>(st.wc);
     // phase q=1: quadrant (0,1)
     read_b<STG, 1>(c, smem, rb1);
@@ -258,7 +261,7 @@ __device__ __forceinline__ void tile_body(const Ctx& c, char* smem, int t, f32x4
     PDMB_LGKM0();
     PDMB_VMCNT(10);
     slot_barrier<STAMP>(st.wr);
-    mma_quadrant<DT, 0, 1, XF>(acc, ra2, rb1);
+    mma_quadrant<DT, 0, 1, (XF ^ 1)>(acc, ra2, rb1);
     slot_barrier<STAMP>(st.wc);
     // phase q=2: quadrant (1,1)
     read_a<STG, 1>(c, smem, ra);
@@ -266,7 +269,7 @@ __device__ __forceinline__ void tile_body(const Ctx& c, char* smem, int t, f32x4
     PDMB_LGKM0();
     PDMB_VMCNT(10);
     slot_barrier<STAMP>(st.wr);
-    mma_quadrant<DT, 1, 1, XF>(acc, ra, rb1);
+    mma_quadrant<DT, 1, 1, (XF ^ 1)>(acc, ra, rb1);
     slot_barrier<STAMP>(st.wc);
     // phase q=3: quadrant (1,0); prefetch next tile's A0 fragments
     read_a<STG ^ 1, 0>(c, smem, ra2);
@@ -274,7 +277,7 @@ __device__ __forceinline__ void tile_body(const Ctx& c, char* smem, int t, f32x4
     PDMB_LGKM0();
     PDMB_VMCNT(10);
     slot_barrier<STAMP>(st.wr);
-    mma_quadrant<DT, 1, 0, XF>(acc, ra, rb0);
+    mma_quadrant<DT, 1, 0, (XF ^ 1)>(acc, ra, rb0);
     slot_barrier<STAMP>(st.wc);
   } else {
     // phase q=0: quadrant (0,0)
