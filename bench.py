@@ -61,9 +61,10 @@ def main() -> int:
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: torch.matmul + gloo, to exercise the multi-rank path without a GPU")
+    ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"])
     a = ap.parse_args()
 
-    ctx = setup_distributed(a.device)
+    ctx = setup_distributed(a.device, backend=None if a.dist_backend == "auto" else a.dist_backend)
     cuda = ctx.device.type == "cuda"
     ws = ctx.world_size
     if ws != a.gpus and ctx.is_main:

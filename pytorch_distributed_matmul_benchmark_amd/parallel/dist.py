@@ -71,9 +71,11 @@ def resolve_device(device: str = "auto", local_rank: int = 0) -> torch.device:
         if not torch.cuda.is_available():
             raise RuntimeError("--device cuda requested but no GPU is visible")
         n = torch.cuda.device_count()
-        if local_rank >= n:
-            raise RuntimeError(f"LOCAL_RANK {local_rank} but only {n} GPU(s) visible")
-        return torch.device("cuda", local_rank)
+        # One rank per GPU in production. More ranks than GPUs (rank % n, as the
+        # reference does) is only meaningful with the gloo backend, which lets a
+        # single-GPU box rehearse the multi-rank GPU code paths; RCCL refuses two
+        # ranks on one device.
+        return torch.device("cuda", local_rank % n)
     if device == "cpu":
         return torch.device("cpu")
     return torch.device(device)
@@ -112,7 +114,7 @@ def cleanup_distributed() -> None:
 def barrier(ctx: DistContext) -> None:
     if not ctx.is_distributed:
         return
-    if ctx.backend == "nccl":
+    if ctx.backend == "nccl" and ctx.is_cuda:
         dist.barrier(device_ids=[ctx.device.index])
     else:
         dist.barrier()

@@ -93,6 +93,9 @@ def build_parser(kind: str) -> argparse.ArgumentParser:
                    help="before each size, time the N×N GEMM on rank 0 ALONE (other ranks idle) "
                         "and report scaling efficiency = node TFLOPS / (ws × that)")
     g.add_argument("--timeout", type=float, default=600.0, help="process-group timeout (s)")
+    g.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
+                   help="auto: nccl (= RCCL) for GPU tensors, gloo for CPU; gloo on GPU tensors "
+                        "lets several ranks share one GPU to rehearse the multi-rank paths")
     g.add_argument("--debug", action="store_true", help="print tracebacks of failed sizes")
     g.add_argument("--profile", action="store_true",
                    help="wrap each size in a roctx range (rocprofv3 --marker-trace --kernel-trace)")
@@ -349,7 +352,8 @@ def run_benchmarks(kind: str, ctx: DistContext, rep: Reporter, args) -> List[Dic
 
 def main(kind: str, argv=None) -> int:
     args = build_parser(kind).parse_args(argv)
-    ctx = setup_distributed(args.device, timeout_s=args.timeout)
+    ctx = setup_distributed(args.device, timeout_s=args.timeout,
+                            backend=None if args.dist_backend == "auto" else args.dist_backend)
     rep = Reporter(is_main=ctx.is_main, json_path=args.json)
     device_banner(rep, ctx.device)
     try:
