@@ -12,6 +12,7 @@ enum Kernel : int {
   kGeneric = 2,   // gemm_generic.hip (any shape)
   kMfma256b = 3,  // gemm_mfma256.hip, DMA issued in the read slot (SCHED 1)
   kMfma256c = 4,  // SCHED 1 + fragment reads balanced over the read slots (SCHED 2)
+  kMfma256d = 9,  // SCHED 3: two quadrants (32 MFMAs) per compute slot, 4 barriers per K-tile
   kF32_256 = 6,   // gemm_f32_256.hip: exact-fp32 MFMA, 256x256 LDS-DMA tile
   kF32_256s = 7,  // same, DMA issue staggered between the two waves of a SIMD
   kMfma256X1 = 10,  // SCHED 2 experiment builds (A/B only): 10 = per-cluster setprio,

@@ -67,6 +67,7 @@ int resolve_kernel(const Problem& p, int kernel) {
   if (kernel == kMfma256) return fast ? kMfma256 : -1;
   if (kernel == kMfma256b) return fast ? kMfma256b : -1;
   if (kernel == kMfma256c) return fast ? kMfma256c : -1;
+  if (kernel == kMfma256d) return fast ? kMfma256d : -1;
   if (kernel == kMfma256Stamp) return (fast && p.dtype == kBF16) ? kMfma256Stamp : -1;
   if (kernel == kGeneric) return kGeneric;
   return -1;
@@ -246,6 +247,7 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
   if (k == kMfma256) return gemm256_launch(p.dtype, a, 0, stream);
   if (k == kMfma256b) return gemm256_launch(p.dtype, a, 1, stream);
   if (k == kMfma256c) return gemm256_launch(p.dtype, a, 2, stream);
+  if (k == kMfma256d) return gemm256_launch(p.dtype, a, 4, stream);
   if (k == kMfma256Stamp) return gemm256_launch(p.dtype, a, 3, stream);
   if (k == kF32_256) return gemm_f32_256_launch(a, 0, stream);
   if (k >= kMfma256X1 && k <= kMfma256X4) return gemm256_launch(p.dtype, a, 10 + (k - kMfma256X1 + 1), stream);
@@ -311,6 +313,8 @@ const char* kernel_name(int kernel) {
       return "pdmb_mfma256b_nn";
     case kMfma256c:
       return "pdmb_mfma256c_nn";
+    case kMfma256d:
+      return "pdmb_mfma256d_nn";
     case kMfma256Stamp:
       return "pdmb_mfma256c_stamp";
     case kF32_256:

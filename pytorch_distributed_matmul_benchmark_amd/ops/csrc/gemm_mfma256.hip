@@ -279,6 +279,42 @@ __device__ __forceinline__ void tile_body(const Ctx& c, char* smem, int t, f32x4
     slot_barrier<STAMP>(st.wr);
     mma_quadrant<DT, 1, 0, (XF ^ 1)>(acc, ra, rb0);
     slot_barrier<STAMP>(st.wc);
+  } else if constexpr (SCHED == 3) {
+    // Two quadrants per compute slot (32 MFMAs): a K-tile is 2 phases, X =
+    // quadrants (0,0)+(0,1) from A0,B0,B1 and Y = (1,1)+(1,0) from A1,B1,B0,
+    // so there are 4 barriers per K-tile instead of 8. Operand registers stay
+    // at SCHED 2's 96 (B0/B1 live across X and Y; A0 of the NEXT tile is
+    // prefetched in Y into ra2). Read slots: X reads B0,B1 (16 tr reads), Y
+    // reads A1 and next A0 (16 b128). Units (u = 4t + {A0,B0,B1,A1}) are issued
+    // two per read slot, 6 ahead: phase P issues u = 2P+6, 2P+7.
+    // RAW: phase P reads units <= 2P+2, retired by vmcnt(6) (3 units in flight)
+    //   at the end of the previous read slot (one barrier more for the lagging
+    //   group, as in SCHED 1/2).
+    // WAR: each refilled unit was last read in the read slot of P-1 or earlier
+    //   (B1/A1 of t+1 in X(t): last read X(t-1) / Y(t-1); A0/B0 of t+2 in
+    //   Y(t): last read Y(t-1) / X(t)), and every read slot ends with lgkmcnt(0).
+    // phase X: quadrants (0,0),(0,1)
+    read_b<STG, 0>(c, smem, rb0);
+    read_b<STG, 1>(c, smem, rb1);
+    issue_unit<2, STG ^ 1>(c, smem, t + 1);
+    issue_unit<3, STG ^ 1>(c, smem, t + 1);
+    PDMB_LGKM0();
+    PDMB_VMCNT(6);
+    slot_barrier<STAMP>(st.wr);
+    mma_quadrant<DT, 0, 0, (XF ^ 1)>(acc, ra2, rb0);
+    mma_quadrant<DT, 0, 1, (XF ^ 1)>(acc, ra2, rb1);
+    slot_barrier<STAMP>(st.wc);
+    // phase Y: quadrants (1,1),(1,0); prefetch next tile's A0
+    read_a<STG, 1>(c, smem, ra);
+    read_a<STG ^ 1, 0>(c, smem, ra2);
+    issue_unit<0, STG>(c, smem, t + 2);
+    issue_unit<1, STG>(c, smem, t + 2);
+    PDMB_LGKM0();
+    PDMB_VMCNT(6);
+    slot_barrier<STAMP>(st.wr);
+    mma_quadrant<DT, 1, 1, (XF ^ 1)>(acc, ra, rb1);
+    mma_quadrant<DT, 1, 0, (XF ^ 1)>(acc, ra, rb0);
+    slot_barrier<STAMP>(st.wc);
   } else {
     // phase q=0: quadrant (0,0)
     read_b<STG, 0>(c, smem, rb0);
@@ -391,14 +427,18 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm256_nn(GemmArgs a) {
   issue_unit<3, 0>(c, smem, 0);
   issue_unit<0, 1>(c, smem, 1);
   issue_unit<1, 1>(c, smem, 1);
-  issue_unit<2, 1>(c, smem, 1);
-  PDMB_VMCNT(10);  // units 0,1 landed (for this wave)
+  if constexpr (SCHED == 3) {
+    PDMB_VMCNT(6);  // units 0..2 landed (for this wave); 3..5 in flight
+  } else {
+    issue_unit<2, 1>(c, smem, 1);
+    PDMB_VMCNT(10);  // units 0,1 landed (for this wave)
+  }
   PDMB_SLOT_BARRIER();
   // Stagger: waves 4..7 run one slot behind waves 0..3.
   if (wr == 1) PDMB_SLOT_BARRIER();
   // SCHED 2 reads each tile's A0 fragments one phase early; tile 0's here
   // (units 0,1 were retired by every wave before the prologue barrier).
-  if constexpr (SCHED == 2) read_a<0, 0>(c, smem, ra2);
+  if constexpr (SCHED >= 2) read_a<0, 0>(c, smem, ra2);
 
   const int nk = c.nk;
   Stamp st;
@@ -483,11 +523,13 @@ hipError_t gemm256_launch(int dt, GemmArgs a, int sched, hipStream_t stream) {
     return hipGetLastError();
   }
   if (dt == kBF16) {
-    if (sched == 2) PDMB_LAUNCH256(kBF16, 2);
+    if (sched == 4) PDMB_LAUNCH256(kBF16, 3);
+    else if (sched == 2) PDMB_LAUNCH256(kBF16, 2);
     else if (sched == 1) PDMB_LAUNCH256(kBF16, 1);
     else PDMB_LAUNCH256(kBF16, 0);
   } else {
-    if (sched == 2) PDMB_LAUNCH256(kF16, 2);
+    if (sched == 4) PDMB_LAUNCH256(kF16, 3);
+    else if (sched == 2) PDMB_LAUNCH256(kF16, 2);
     else if (sched == 1) PDMB_LAUNCH256(kF16, 1);
     else PDMB_LAUNCH256(kF16, 0);
   }

@@ -27,7 +27,7 @@ def test_native_extension_is_loaded():
     assert mod.__file__.endswith(".so")
 
 
-FAST = ["mfma256", "mfma256b", "mfma256c"]
+FAST = ["mfma256", "mfma256b", "mfma256c", "mfma256d"]
 
 
 @pytest.mark.parametrize("kernel", FAST)

@@ -58,3 +58,16 @@ def test_f32_kernel_no_spill(tmp_path):
         assert k["spill"] == 0 and "scratch_" not in k["body"], name
         assert k["vgpr"] <= 256, name
         assert len(re.findall(r"v_mfma_f32_16x16x4_f32", k["body"])) == 512, name
+
+
+def test_bf16_two_quadrant_schedule(tmp_path):
+    """SCHED 3: 32 MFMAs per compute slot, 4 barriers per K-tile, vmcnt(6) waits."""
+    ks = _kernels("gemm_mfma256.hip", tmp_path)
+    name = [k for k in ks if "gemm256_nn" in k and "ILi2ELi3ELb0ELi0E" in k]
+    assert name, sorted(ks)
+    k = ks[name[0]]
+    b = k["body"]
+    assert k["spill"] == 0 and k["vgpr"] <= 256
+    assert len(re.findall(r"s_waitcnt vmcnt\(0\)", b)) == 1
+    assert len(re.findall(r"s_waitcnt vmcnt\(6\)", b)) >= 4
+    assert len(re.findall(r"v_mfma_f32_16x16x32_bf16", b)) == 128
