@@ -291,7 +291,12 @@ def run_benchmarks(kind: str, ctx: DistContext, rep: Reporter, args) -> List[Dic
              else f"  - Number of processes: {ctx.world_size}")
     rep.line(f"  - Data type: {dtype}")
     rep.line(f"  - Device: {'GPU (' + torch.cuda.get_device_name(ctx.device) + ')' if ctx.is_cuda else 'CPU'}")
-    rep.line(f"  - GEMM: {args.backend}" + (" (gfx950 MFMA kernels)" if args.backend == "native" and ctx.is_cuda else ""))
+    if not ctx.is_cuda:
+        rep.line("  - GEMM: torch.matmul (CPU reference path)")
+    elif args.backend == "native":
+        rep.line("  - GEMM: native gfx950 MFMA kernels")
+    else:
+        rep.line("  - GEMM: torch.matmul (hipBLASLt), A/B comparison")
     rep.line(f"  - Iterations per test: {args.iterations}")
     rep.line(f"  - Warmup iterations: {args.warmup}")
     rep.line(f"{'=' * k['width']}\n")
