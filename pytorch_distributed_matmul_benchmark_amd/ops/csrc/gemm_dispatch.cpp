@@ -59,7 +59,7 @@ int resolve_kernel(const Problem& p, int kernel) {
   const bool fast = gemm256_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   const bool f32fast = p.dtype == kF32 &&
                        gemm_f32_256_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
-  if (kernel == kAuto) return fast ? kMfma256c : (f32fast ? kF32_256s : kGeneric);
+  if (kernel == kAuto) return fast ? kMfma256d : (f32fast ? kF32_256s : kGeneric);
   if (kernel == kF32_256) return f32fast ? kF32_256 : -1;
   if (kernel >= kMfma256X1 && kernel <= kMfma256X4)
     return (fast && p.dtype == kBF16) ? kernel : -1;
@@ -215,7 +215,7 @@ static hipError_t gemm_padded(const Problem& p, hipStream_t stream, int* used) {
   if (used) *used = k;
   if (k == kGeneric || k < 0) return hipErrorInvalidValue;  // cannot happen: q is aligned
   GemmArgs a = to_args(q);
-  e = k == kF32_256s ? gemm_f32_256_launch(a, 1, stream) : gemm256_launch(q.dtype, a, 2, stream);
+  e = k == kF32_256s ? gemm_f32_256_launch(a, 1, stream) : gemm256_launch(q.dtype, a, 4, stream);
   if (e != hipSuccess) return e;
   for (int b = 0; b < batch; ++b) {
     char* C = (char*)p.C + (size_t)b * p.sC * es;

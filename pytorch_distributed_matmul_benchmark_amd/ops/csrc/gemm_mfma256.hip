@@ -27,13 +27,18 @@
 //    R (ds_read fragments + issue one LDS-DMA unit) and C (16 MFMA). Waves
 //    4..7 run one slot behind waves 0..3, so on every SIMD one wave does
 //    MFMA while its partner reads LDS and issues the next DMA.
-//    Three schedules are kept for A/B (kernel ids in api.h); SCHED 2 is the
+//    Four schedules are kept for A/B (kernel ids in api.h); SCHED 3 is the
 //    default: 0 = DMA issued in the C slot (the first version), 1 = DMA in
 //    the R slot, 2 = 1 + reads balanced to 8 per R slot by prefetching the
-//    next tile's A0 fragments in phase 3 into a second A register set.
+//    next tile's A0 fragments in phase 3 into a second A register set,
+//    3 = two quadrants (32 MFMAs) per compute slot: 4 barriers per K-tile
+//    instead of 8 with the same 96 operand registers.
 //    Measured on MI355X, 16384^3 bf16 random data: 1315 / 1370 / 1440 TF
 //    (hipBLASLt 1362 on the same data); SCHED 2 without per-cluster
-//    s_setprio is a further +0.9 % (scripts/ab_kernels.py).
+//    s_setprio is a further +0.9 % and SCHED 3 another +1.0 % (1446 TF;
+//    scripts/ab_kernels.py). PMC: SCHED 3 lifts MFMA utilisation 73.9 → 77.1 %
+//    but the clock falls 1.80 → 1.75 GHz — on random data the chip is
+//    power-bound, so schedule gains return only partly as wall time.
 //  * LDS-DMA units (A-half = 16 KiB, B-half = 16 KiB) are refilled as soon
 //    as the last reader of their previous contents has retired, so every
 //    unit has ~5-6 phases of flight time. The wait is a counted

@@ -90,7 +90,7 @@ def padded_kernel_for(A: torch.Tensor, B: torch.Tensor) -> Optional[str]:
     batch = max(A.shape[0] if A.dim() == 3 else 1, B.shape[0] if B.dim() == 3 else 1)
     if 2.0 * M * N * K * batch < PAD_MIN_FLOPS or kernel_for(A, B) != "pdmb_generic_nn":
         return None
-    return "pdmb_f32_256s_nn" if A.dtype == torch.float32 else "pdmb_mfma256c_nn"
+    return "pdmb_f32_256s_nn" if A.dtype == torch.float32 else "pdmb_mfma256d_nn"
 
 
 def bmm(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,

@@ -237,7 +237,7 @@ def test_odd_sizes_padded_to_fast_path(dtype, M, N, K):
     A = torch.randn(M, K, device="cuda", dtype=dt)
     B = torch.randn(K, N, device="cuda", dtype=dt)
     assert gemm.kernel_for(A, B) == "pdmb_generic_nn"  # unpadded, only generic could run it
-    assert gemm.padded_kernel_for(A, B) in ("pdmb_mfma256c_nn", "pdmb_f32_256s_nn")
+    assert gemm.padded_kernel_for(A, B) in ("pdmb_mfma256d_nn", "pdmb_f32_256s_nn")
     C = gemm.matmul(A, B)
     assert C.shape == (M, N)
     assert _relerr(C, _ref(A, B)) < TOL[dt]
@@ -251,11 +251,11 @@ def test_padded_path_misaligned_views_and_batches():
     big = torch.randn(1100, 2051, device="cuda", dtype=torch.bfloat16)
     A = big[:, 1:2049]            # lda = 2051 (misaligned), K = 2048
     B = torch.randn(2048, 1500, device="cuda", dtype=torch.bfloat16)
-    assert gemm.padded_kernel_for(A, B) == "pdmb_mfma256c_nn"
+    assert gemm.padded_kernel_for(A, B) == "pdmb_mfma256d_nn"
     assert _relerr(gemm.matmul(A, B), _ref(A, B)) < TOL[torch.bfloat16]
     A3 = torch.randn(3, 700, 1000, device="cuda", dtype=torch.float16)
     B3 = torch.randn(3, 1000, 1300, device="cuda", dtype=torch.float16)
-    assert gemm.padded_kernel_for(A3, B3) == "pdmb_mfma256c_nn"
+    assert gemm.padded_kernel_for(A3, B3) == "pdmb_mfma256d_nn"
     assert _relerr(gemm.bmm(A3, B3), torch.bmm(A3.double(), B3.double())) < TOL[torch.float16]
     out = torch.empty(1100, 1500, device="cuda", dtype=torch.bfloat16)
     ms = gemm.bench_matmul(A, B, out, iters=3, warmup=1)  # native loop takes the padded path too
