@@ -356,7 +356,10 @@ def run_benchmarks(kind: str, ctx: DistContext, rep: Reporter, args) -> List[Dic
 
 
 def main(kind: str, argv=None) -> int:
-    args = build_parser(kind).parse_args(argv)
+    parser = build_parser(kind)
+    args = parser.parse_args(argv)
+    if args.iterations < 1 or args.warmup < 0 or args.chunks < 1 or args.batch < 1:
+        parser.error("--iterations and --chunks must be >= 1, --batch >= 1, --warmup >= 0")
     ctx = setup_distributed(args.device, timeout_s=args.timeout,
                             backend=None if args.dist_backend == "auto" else args.dist_backend)
     rep = Reporter(is_main=ctx.is_main, json_path=args.json)
