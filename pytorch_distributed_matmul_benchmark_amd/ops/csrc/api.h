@@ -15,6 +15,7 @@ enum Kernel : int {
   kMfma256d = 9,  // SCHED 3: two quadrants (32 MFMAs) per compute slot, 4 barriers per K-tile
   kF32_256 = 6,   // gemm_f32_256.hip: exact-fp32 MFMA, 256x256 LDS-DMA tile
   kF32_256s = 7,  // same, DMA issue staggered between the two waves of a SIMD
+  kF32NoDma = 20,  // diagnostic: f32 K-loop without loads (timing only, wrong results)
   kMfma256X1 = 10,  // SCHED 2 experiment builds (A/B only): 10 = per-cluster setprio,
   kMfma256X2 = 11,  //   11 = static priority of waves 4..7,
   kMfma256X4 = 13,  //   13 = XCD sub-block 8x4 (12 unused)

@@ -64,6 +64,7 @@ int resolve_kernel(const Problem& p, int kernel) {
   if (kernel >= kMfma256X1 && kernel <= kMfma256X4)
     return (fast && p.dtype == kBF16) ? kernel : -1;
   if (kernel == kF32_256s) return f32fast ? kF32_256s : -1;
+  if (kernel == kF32NoDma) return f32fast ? kF32NoDma : -1;
   if (kernel == kMfma256) return fast ? kMfma256 : -1;
   if (kernel == kMfma256b) return fast ? kMfma256b : -1;
   if (kernel == kMfma256c) return fast ? kMfma256c : -1;
@@ -252,6 +253,7 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
   if (k == kF32_256) return gemm_f32_256_launch(a, 0, stream);
   if (k >= kMfma256X1 && k <= kMfma256X4) return gemm256_launch(p.dtype, a, 10 + (k - kMfma256X1 + 1), stream);
   if (k == kF32_256s) return gemm_f32_256_launch(a, 1, stream);
+  if (k == kF32NoDma) return gemm_f32_256_launch(a, 9, stream);
   return gemm_generic_launch(p.dtype, a, generic_vec_ok(p), stream);
 }
 

@@ -98,10 +98,10 @@ __device__ __forceinline__ void compute_half(const char* smem, int wr, int wc, i
 // their DMA pieces at different points — waves 0..3 before the first 16-k
 // half, waves 4..7 between the halves — so while one wave of the pair is
 // issuing DMA (~60 cycles per piece) its partner keeps the MFMA pipe busy.
-template <int STG, bool STAGGER>
+template <int STG, bool STAGGER, bool NODMA = false>
 __device__ __forceinline__ void tile_step(const Ctx& c, const char* smem, int wr, int wc, int l16,
                                           int g, f32x4 (&acc)[8][4], int next) {
-  const bool pf = next < c.nk;
+  const bool pf = !NODMA && next < c.nk;
   if (pf && (!STAGGER || wr == 0)) issue_tile<STG ^ 1>(c, next);
   compute_half<STG, 0>(smem, wr, wc, l16, g, acc);
   if (STAGGER && pf && wr == 1) issue_tile<STG ^ 1>(c, next);
@@ -112,7 +112,9 @@ __device__ __forceinline__ void tile_barrier() {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <bool STAGGER>
+// NODMA: timing-only diagnostic (the K-loop issues no loads, results are
+// wrong): the ceiling of the compute + barrier structure alone.
+template <bool STAGGER, bool NODMA = false>
 __global__ void __launch_bounds__(NT, 2) gemm_f32_256(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
@@ -156,10 +158,10 @@ __global__ void __launch_bounds__(NT, 2) gemm_f32_256(GemmArgs a) {
     // The stage being refilled was last read in the previous K-tile, which
     // ended with a barrier (WAR); the refill has a whole K-tile to land and
     // is retired by the vmcnt(0) + barrier that closes this one (RAW).
-    tile_step<0, STAGGER>(c, smem, wr, wc, l16, g, acc, t + 1);
+    tile_step<0, STAGGER, NODMA>(c, smem, wr, wc, l16, g, acc, t + 1);
     tile_barrier();
     if (t + 1 < nk) {
-      tile_step<1, STAGGER>(c, smem, wr, wc, l16, g, acc, t + 2);
+      tile_step<1, STAGGER, NODMA>(c, smem, wr, wc, l16, g, acc, t + 2);
       tile_barrier();
     }
   }
@@ -200,7 +202,9 @@ hipError_t gemm_f32_256_launch(GemmArgs a, int variant, hipStream_t stream) {
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
   const dim3 grid((unsigned)nblocks), block(kf32::NT);
-  if (variant == 1)
+  if (variant == 9)
+    hipLaunchKernelGGL((kf32::gemm_f32_256<false, true>), grid, block, 0, stream, a);
+  else if (variant == 1)
     hipLaunchKernelGGL(kf32::gemm_f32_256<true>, grid, block, 0, stream, a);
   else
     hipLaunchKernelGGL(kf32::gemm_f32_256<false>, grid, block, 0, stream, a);
