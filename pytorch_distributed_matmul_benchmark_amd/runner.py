@@ -99,6 +99,8 @@ def build_parser(kind: str) -> argparse.ArgumentParser:
     g.add_argument("--debug", action="store_true", help="print tracebacks of failed sizes")
     g.add_argument("--profile", action="store_true",
                    help="wrap each size in a roctx range (rocprofv3 --marker-trace --kernel-trace)")
+    g.add_argument("--show-topology", action="store_true",
+                   help="rank 0 prints the GPU interconnect (rocm-smi --showtopotype --showtopohops)")
     g.add_argument("--resume", action="store_true",
                    help="with --json: skip sizes whose (script, mode, dtype, ws) record already exists")
     return p
@@ -364,6 +366,13 @@ def main(kind: str, argv=None) -> int:
                             backend=None if args.dist_backend == "auto" else args.dist_backend)
     rep = Reporter(is_main=ctx.is_main, json_path=args.json)
     device_banner(rep, ctx.device)
+    if ctx.is_main and ctx.is_cuda and (args.show_topology or
+                                        (kind == "overlap" and torch.cuda.device_count() > 1)):
+        from .utils.topology import topology_lines
+
+        rep.line("\nGPU interconnect (xGMI on MI355X nodes):")
+        for line in topology_lines():
+            rep.line(f"  {line}")
     try:
         if ctx.world_size > 1 and kind != "basic" and not verify_collectives(ctx):
             rep.line("ERROR: Collective operations verification failed!")
