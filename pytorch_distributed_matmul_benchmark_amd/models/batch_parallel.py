@@ -32,7 +32,7 @@ from ..utils.timing import SegmentTimer, Stopwatch, synchronize, time_loop_ms
 import torch.distributed as dist
 
 from .common import (ModeResult, Workload, align_ranks, allreduced_relerr, gemm_fn, kernel_label,
-                     randn)
+                     randn, warmup)
 
 
 def _units(lb: int, n: int, chunks: int):
@@ -62,9 +62,11 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
 
     extra = {"global_batch": gb, "local_batch": lb, "overlap": bool(w.overlap and distributed)}
     if not (w.overlap and distributed):
-        for _ in range(w.warmup):
+        def serial_step():
             mm(A, B, C)
             reduce_all()
+
+        warmup(serial_step, w, ctx)
         align_ranks(ctx)
         seg = SegmentTimer(dev)
         stream = current_stream(dev)
@@ -106,8 +108,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
                 for d in done:
                     compute.wait_event(d)
 
-        for _ in range(w.warmup):
-            step()
+        warmup(step, w, ctx)
         # compute-only reference time (reference: 10 GEMM-only iterations), taken
         # BEFORE the timed loop so the loop's last reduced C stays checkable.
         synchronize(dev)

@@ -37,6 +37,7 @@ class Workload:
     chunks: int = 4             # overlap granularity (row chunks per GEMM)
     graph: bool = False         # independent: replay the timed loop as one hipGraph
     check: bool = False         # verify the result against a float64 reference
+    min_warmup_ms: float = 0.0  # extend the warm-up until this much GPU time has run (DVFS)
 
 
 @dataclass
@@ -95,6 +96,33 @@ def randn(shape, w: Workload, device: torch.device, seed: int) -> torch.Tensor:
     """N(0,1) operands (random, non-zero data matters on MI355X: DVFS runs
     zero-filled GEMMs ~15-20% fast — cdna_hip_programming.md §5.4 rule 25)."""
     return torch.randn(*shape, generator=generator(device, seed), device=device, dtype=w.dtype)
+
+
+def warmup(step: Callable[[], None], w: Workload, ctx: DistContext) -> None:
+    """``w.warmup`` untimed steps, then — if ``w.min_warmup_ms`` is set — enough
+    extra steps to reach that much warm-up time. MI355X clocks settle only after
+    tens of ms of MFMA load (DVFS), so ten 0.1-ms GEMMs at 4k would leave the
+    timed loop on a ramping clock. The extra count is agreed by a MAX all-reduce,
+    so ranks running collectives in ``step`` stay in lock-step."""
+    import math
+    import time
+
+    from ..parallel.dist import reduce_scalar
+
+    for _ in range(w.warmup):
+        step()
+    if w.min_warmup_ms <= 0 or ctx.device.type != "cuda":
+        return
+    synchronize(ctx.device)
+    t0 = time.perf_counter()
+    step()
+    synchronize(ctx.device)
+    one = max((time.perf_counter() - t0) * 1e3, 1e-3)
+    done_ms = one * (w.warmup + 1)
+    extra = 0 if done_ms >= w.min_warmup_ms else min(10_000, math.ceil((w.min_warmup_ms - done_ms) / one))
+    extra = int(reduce_scalar(ctx, float(extra), "max"))
+    for _ in range(extra):
+        step()
 
 
 def align_ranks(ctx: DistContext) -> None:

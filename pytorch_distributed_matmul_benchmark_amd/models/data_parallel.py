@@ -18,7 +18,7 @@ from ..parallel.dist import DistContext
 from ..utils.metrics import gemm_flops, tflops_from
 from ..utils.timing import SegmentTimer
 from .common import (ModeResult, Workload, align_ranks, allreduced_relerr, gemm_fn, kernel_label,
-                     randn)
+                     randn, warmup)
 
 
 def run(w: Workload, ctx: DistContext) -> ModeResult:
@@ -29,10 +29,12 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     mm = gemm_fn(w, dev)
     label = kernel_label(w, A, B, C)
     distributed = ctx.is_distributed
-    for _ in range(w.warmup):
+    def step():
         mm(A, B, C)
         if distributed:
             dist.all_reduce(C)
+
+    warmup(step, w, ctx)
     align_ranks(ctx)
     seg = SegmentTimer(dev)
     st = current_stream(dev)

@@ -19,7 +19,7 @@ from ..parallel.dist import DistContext
 from ..utils.metrics import gemm_flops, tflops_from
 from ..utils.timing import time_loop_ms
 from .common import (ModeResult, Workload, align_ranks, gemm_fn, kernel_label, randn,
-                     sampled_relerr)
+                     sampled_relerr, warmup)
 
 
 def run(w: Workload, ctx: DistContext, mode_name: str = "independent") -> ModeResult:
@@ -31,8 +31,7 @@ def run(w: Workload, ctx: DistContext, mode_name: str = "independent") -> ModeRe
     mm = gemm_fn(w, dev)
     label = kernel_label(w, A, B, C)
 
-    for _ in range(w.warmup):
-        mm(A, B, C)
+    warmup(lambda: mm(A, B, C), w, ctx)
     align_ranks(ctx)
     if dev.type == "cuda" and w.backend == "native":
         total_ms = _gemm.bench_matmul(A, B, C, w.iters, 0, graph=w.graph, kernel=w.kernel)

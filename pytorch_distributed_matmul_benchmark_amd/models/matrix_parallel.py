@@ -32,7 +32,7 @@ from ..utils.metrics import gemm_flops, tflops_from
 from ..utils.timing import SegmentTimer, Stopwatch, synchronize, time_loop_ms
 from . import independent
 from .common import (ModeResult, Workload, align_ranks, gemm_fn, kernel_label, randn,
-                     sampled_relerr)
+                     sampled_relerr, warmup)
 
 
 def make_operands(w: Workload, ctx: DistContext):
@@ -83,9 +83,11 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         def comm():
             dist.all_gather_into_tensor(gathered, C_local)
 
-        for _ in range(w.warmup):
+        def serial_step():
             mm(A, B_local, C_local)
             comm()
+
+        warmup(serial_step, w, ctx)
         align_ranks(ctx)
         seg = SegmentTimer(dev)
         st = current_stream(dev)
@@ -119,8 +121,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
                 for d in done:
                     compute.wait_event(d)
 
-        for _ in range(w.warmup):
-            step()
+        warmup(step, w, ctx)
         align_ranks(ctx)
         sw = Stopwatch(dev)
         sw.start(compute)

@@ -36,7 +36,7 @@ from ..parallel.dist import DistContext
 from ..utils.metrics import gemm_flops, tflops_from
 from ..utils.timing import Stopwatch, synchronize, time_loop_ms
 from .common import (ModeResult, Workload, align_ranks, allreduced_relerr, gemm_fn, kernel_label,
-                     randn)
+                     randn, warmup)
 
 DEPTH = {"no_overlap": 1, "overlap": 2, "pipeline": 3}
 
@@ -86,7 +86,7 @@ def run(w: Workload, ctx: DistContext, mode: str = "overlap") -> ModeResult:
                     if used[i]:
                         compute.wait_event(done[i])
 
-    run_iters(w.warmup)
+    warmup(lambda: run_iters(1), w, ctx)
     finish()
     # Compute-only time (backup/matmul_overlap_benchmark.py:77-89 re-measures 10
     # GEMM-only iterations), taken before the timed loop so the loop's reduced

@@ -86,6 +86,9 @@ def build_parser(kind: str) -> argparse.ArgumentParser:
     g.add_argument("--check", action="store_true",
                    help="verify results against a float64 reference (sampled rows)")
     g.add_argument("--seed", type=int, default=0)
+    g.add_argument("--min-warmup-ms", type=float, default=100.0,
+                   help="extend the --warmup iterations until this much GPU time has run "
+                        "(MI355X clocks settle under sustained MFMA load; 0 = exactly --warmup)")
     g.add_argument("--json", default=None, help="append one JSON record per result to this file")
     g.add_argument("--single-gpu-tflops", type=float, default=None,
                    help="measured 1-GPU TFLOPS for the 'efficiency vs 1 GPU' line")
@@ -113,7 +116,8 @@ def _mode_of(kind: str, args) -> str:
 def _workload(args, n: int, dtype: torch.dtype) -> Workload:
     return Workload(n=n, dtype=dtype, iters=args.iterations, warmup=args.warmup, seed=args.seed,
                     backend=args.backend, kernel=args.kernel, batch=args.batch,
-                    overlap=args.overlap, chunks=args.chunks, graph=args.graph, check=args.check)
+                    overlap=args.overlap, chunks=args.chunks, graph=args.graph, check=args.check,
+                    min_warmup_ms=args.min_warmup_ms)
 
 
 def _single_gpu_reference(ctx: DistContext, args, n: int, dtype: torch.dtype) -> float:
