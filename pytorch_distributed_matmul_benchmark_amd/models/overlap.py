@@ -41,11 +41,13 @@ from .common import (ModeResult, Workload, align_ranks, allreduced_relerr, gemm_
 DEPTH = {"no_overlap": 1, "overlap": 2, "pipeline": 3}
 
 
-def run(w: Workload, ctx: DistContext, mode: str = "overlap") -> ModeResult:
+def run(w: Workload, ctx: DistContext, mode: str = "overlap", depth: int = None) -> ModeResult:
+    """``depth`` overrides the ring depth (reference ``pipeline_depth``,
+    backup/matmul_overlap_benchmark.py:184); default 1 / 2 / 3 by mode."""
     if mode not in DEPTH:
         raise ValueError(f"unknown overlap mode {mode!r}")
     dev, n, ws = ctx.device, w.n, ctx.world_size
-    depth = DEPTH[mode]
+    depth = DEPTH[mode] if depth is None else max(1, int(depth))
     As = [randn((n, n), w, dev, seed=100 * (w.seed + ctx.rank) + 2 * i) for i in range(depth)]
     Bs = [randn((n, n), w, dev, seed=100 * (w.seed + ctx.rank) + 2 * i + 1) for i in range(depth)]
     Cs = [torch.empty((n, n), device=dev, dtype=w.dtype) for _ in range(depth)]

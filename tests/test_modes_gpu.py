@@ -99,3 +99,11 @@ def test_autograd_batched_broadcast():
     (Ar @ Br).sum().backward()
     for g, r in ((A.grad, Ar.grad), (B.grad, Br.grad)):
         assert ((g.double() - r).norm() / r.norm()).item() < 1e-2
+
+
+def test_reference_function_api_on_gpu():
+    from pytorch_distributed_matmul_benchmark_amd import api
+    t, tf = api.benchmark_matmul(2048, torch.bfloat16, "cuda:0", 5, 2)
+    assert t > 0 and tf > 100
+    t, tf, tc = api.benchmark_pipeline(1024, torch.bfloat16, "cuda:0", 0, 4, 1, pipeline_depth=3)
+    assert t > 0 and tf > 0
