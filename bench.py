@@ -189,7 +189,7 @@ def main() -> int:
             if dt == torch.bfloat16 and n == 16384 and cuda else None)
     if ctx.is_main:
         out = {
-            "metric": METRIC, "value": round(value, 2), "unit": "TFLOPS",
+            "metric": METRIC, "value": round(value, 4), "unit": "TFLOPS",
             "n_gpus": ws, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms_step, 4), "higher_is_better": True,
             "scaling": "strong" if a.mode == "matrix_parallel" else "weak",

@@ -7,6 +7,7 @@ import subprocess
 import sys
 
 import pytest
+from conftest import free_port
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ENV = dict(os.environ, PYTHONUNBUFFERED="1", OMP_NUM_THREADS="2")
@@ -18,7 +19,8 @@ def _run(args, timeout=240):
     return r.stdout
 
 
-def _torchrun(nproc, script, *args, port=29700):
+def _torchrun(nproc, script, *args, port=None):
+    port = port or free_port()
     return _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                  f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1",
                  f"--master-port={port}", os.path.join(ROOT, script), *args])
@@ -72,7 +74,7 @@ def test_scaling_torchrun_gloo(mode, extra, tmp_path):
 def test_batch_parallel_ws3_reports_real_batch(tmp_path):
     out = _torchrun(3, "matmul_scaling_benchmark.py", "--device", "cpu", "--sizes", "128",
                     "--iterations", "1", "--warmup", "1", "--dtype", "float32", "--mode",
-                    "batch_parallel", "--check", port=29701)
+                    "batch_parallel", "--check")
     assert "Processing 6 total batches across 3 GPU(s) (2 per GPU)" in out
     assert "PASS" in out
 
@@ -81,7 +83,7 @@ def test_batch_parallel_ws3_reports_real_batch(tmp_path):
 def test_backup_distributed(mode):
     out = _torchrun(2, "backup/matmul_distributed_benchmark.py", "--device", "cpu", "--sizes",
                     "256", "--iterations", "2", "--warmup", "1", "--mode", mode, "--check",
-                    port=29702)
+                    )
     assert "Total time per operation" in out and "PASS" in out and "ERROR" not in out
     if mode != "independent":
         assert "Communication overhead" in out
@@ -90,7 +92,7 @@ def test_backup_distributed(mode):
 @pytest.mark.parametrize("mode", ["no_overlap", "overlap", "pipeline"])
 def test_backup_overlap(mode):
     out = _torchrun(2, "backup/matmul_overlap_benchmark.py", "--device", "cpu", "--sizes", "256",
-                    "--iterations", "3", "--warmup", "1", "--mode", mode, "--check", port=29703)
+                    "--iterations", "3", "--warmup", "1", "--mode", mode, "--check")
     assert "Actual TFLOPS" in out and "Compute-only TFLOPS" in out
     assert "PASS" in out and "ERROR" not in out
 
@@ -141,7 +143,7 @@ def test_scaling_ref_reports_efficiency_vs_one_rank(tmp_path):
     js = tmp_path / "r.jsonl"
     out = _torchrun(2, "matmul_scaling_benchmark.py", "--device", "cpu", "--sizes", "160",
                     "--iterations", "2", "--warmup", "1", "--dtype", "float32", "--mode",
-                    "independent", "--scaling-ref", "--json", str(js), port=29704)
+                    "independent", "--scaling-ref", "--json", str(js))
     assert "Scaling efficiency vs 1 GPU:" in out
     rec = json.loads(js.read_text().splitlines()[-1])
     assert rec["single_gpu_tflops"] > 0 and rec["scaling_efficiency_vs_1gpu"] > 0

@@ -6,6 +6,7 @@ import subprocess
 import sys
 
 import pytest
+from conftest import free_port
 import torch
 
 from pytorch_distributed_matmul_benchmark_amd.models import MODES, Workload, run_mode
@@ -64,7 +65,7 @@ def _run(args, timeout=400):
                                         ("matrix_parallel", [])])
 def test_torchrun_rccl_single_rank(mode, extra):
     out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
-                "--master-addr=127.0.0.1", "--master-port=29760", "matmul_scaling_benchmark.py",
+                "--master-addr=127.0.0.1", f"--master-port={free_port()}", "matmul_scaling_benchmark.py",
                 "--sizes", "1024", "2048", "--iterations", "3", "--warmup", "1", "--mode", mode,
                 "--check", *extra])
     assert "Results for 2048x2048" in out and "PASS" in out

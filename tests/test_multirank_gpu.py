@@ -8,12 +8,14 @@ import subprocess
 import sys
 
 import pytest
+from conftest import free_port
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(nproc, script, *args, port):
+def _run(nproc, script, *args, port=None):
+    port = port or free_port()
     env = dict(os.environ, PYTHONUNBUFFERED="1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1",
@@ -28,7 +30,7 @@ def _run(nproc, script, *args, port):
                                         ("matrix_parallel", ["--overlap", "--chunks", "2"])])
 def test_two_ranks_share_gpu_scaling_modes(mode, extra):
     out = _run(2, "matmul_scaling_benchmark.py", "--sizes", "2048", "4608", "--iterations", "3",
-               "--warmup", "1", "--mode", mode, "--check", *extra, port=29770)
+               "--warmup", "1", "--mode", mode, "--check", *extra)
     assert "Collective operations verified successfully across 2 GPUs" in out
     assert out.count("PASS") == 2 and "FAIL" not in out and "ERROR" not in out
 
@@ -36,19 +38,19 @@ def test_two_ranks_share_gpu_scaling_modes(mode, extra):
 @pytest.mark.parametrize("mode", ["data_parallel", "model_parallel"])
 def test_two_ranks_share_gpu_backup_distributed(mode):
     out = _run(2, "backup/matmul_distributed_benchmark.py", "--sizes", "2048", "--iterations", "2",
-               "--warmup", "1", "--mode", mode, "--check", port=29771)
+               "--warmup", "1", "--mode", mode, "--check")
     assert "PASS" in out and "ERROR" not in out
 
 
 @pytest.mark.parametrize("mode", ["overlap", "pipeline"])
 def test_two_ranks_share_gpu_overlap_ring(mode):
     out = _run(2, "backup/matmul_overlap_benchmark.py", "--sizes", "2048", "--iterations", "4",
-               "--warmup", "1", "--mode", mode, "--check", port=29772)
+               "--warmup", "1", "--mode", mode, "--check")
     assert "PASS" in out and "ERROR" not in out
 
 
 def test_two_ranks_share_gpu_bench_json():
     out = _run(2, "bench.py", "--gpus", "2", "--size", "2048", "--steps", "3", "--warmup", "1",
-               "--mode", "batch_parallel", "--overlap", port=29773)
+               "--mode", "batch_parallel", "--overlap")
     d = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
     assert d["n_gpus"] == 2 and d["value"] > 0
