@@ -48,3 +48,23 @@ def test_bench_four_ranks_batch_never_empty():
     d = _bench(4, "--size", "128", "--steps", "2", "--warmup", "1", "--mode", "batch_parallel",
                )
     assert d["config"]["global_batch"] == 4 and d["config"]["parallelism"] == "dp4"
+
+
+def test_bench_reports_secondary_modes():
+    """The headline line also carries batch_parallel / matrix_parallel (serialized and
+    overlapped) timed in the same job, each with its own whole-job value."""
+    d = _bench(2, "--size", "256", "--steps", "2", "--warmup", "1", "--extra-steps", "2",
+               "--extra-warmup", "1")
+    assert set(d["modes"]) == {"batch_parallel", "batch_parallel+overlap", "matrix_parallel",
+                               "matrix_parallel+overlap"}
+    for key, m in d["modes"].items():
+        assert m["value"] > 0 and m["ms_per_step"] > 0 and m["steps"] == 2
+        gb = 4 if key.startswith("batch") else 1
+        assert m["global_batch"] == gb
+        assert m["parallelism"] == ("dp2" if gb == 4 else "tp2")
+        assert m["value"] == pytest.approx(2.0 * 256 ** 3 * gb / (m["ms_per_step"] / 1e3) / 1e12,
+                                           rel=0.02, abs=1e-4)
+    assert d["config"]["mode"] == "independent"
+    d0 = _bench(2, "--size", "128", "--steps", "1", "--warmup", "0", "--extra-steps", "0",
+                "--mode", "batch_parallel")
+    assert d0["modes"] == {}

@@ -54,3 +54,6 @@ def test_two_ranks_share_gpu_bench_json():
                "--mode", "batch_parallel", "--overlap")
     d = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
     assert d["n_gpus"] == 2 and d["value"] > 0
+    # the secondary modes ran on the same ranks: the other three scaling variants
+    assert set(d["modes"]) == {"batch_parallel", "matrix_parallel", "matrix_parallel+overlap"}
+    assert all(m["value"] > 0 for m in d["modes"].values())
