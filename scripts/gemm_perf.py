@@ -3,6 +3,7 @@
 
 Interleaves the arms in one process (cdna rule 24) on the same random data.
 Usage: python scripts/gemm_perf.py --sizes 4096 8192 16384 --dtype bfloat16
+       python scripts/gemm_perf.py --shapes 16384x2048x16384 8192x2048x16384   (MxNxK)
 """
 import argparse
 import json
@@ -41,15 +42,20 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--no-torch", action="store_true")
     ap.add_argument("--kernel", default="auto")
+    ap.add_argument("--shapes", nargs="+", default=None,
+                    help="rectangular MxNxK problems (e.g. the per-rank shards of matrix_parallel)")
     a = ap.parse_args()
     dt = DT[a.dtype]
-    for n in a.sizes:
+    probs = ([tuple(int(x) for x in s.lower().split("x")) for s in a.shapes] if a.shapes
+             else [(n, n, n) for n in a.sizes])
+    for m, n, k in probs:
         torch.manual_seed(0)
-        A = torch.randn(n, n, device="cuda", dtype=dt)
-        B = torch.randn(n, n, device="cuda", dtype=dt)
-        out = torch.empty(n, n, device="cuda", dtype=dt)
-        flop = 2.0 * n ** 3
-        res = {"n": n, "dtype": a.dtype, "kernel": gemm.kernel_for(A, B, out, kernel=a.kernel)}
+        A = torch.randn(m, k, device="cuda", dtype=dt)
+        B = torch.randn(k, n, device="cuda", dtype=dt)
+        out = torch.empty(m, n, device="cuda", dtype=dt)
+        flop = 2.0 * m * n * k
+        res = {"n": n, "shape": f"{m}x{n}x{k}", "dtype": a.dtype,
+               "kernel": gemm.kernel_for(A, B, out, kernel=a.kernel)}
         ours, ours_g, theirs = [], [], []
         for _ in range(a.rounds):
             ms = gemm.bench_matmul(A, B, out, a.iters, a.warmup, graph=False, kernel=a.kernel) / a.iters
