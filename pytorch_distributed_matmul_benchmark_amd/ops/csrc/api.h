@@ -20,8 +20,11 @@ enum Kernel : int {
   kMfma256X2 = 11,  //   11 = static priority of waves 4..7,
   kMfma256X4 = 13,  //   13 = XCD sub-block 8x4 (12 unused)
   kMfma256Stamp = 5,  // diagnostic: SCHED 2 with in-kernel barrier-wait stamps (needs a debug buffer)
+  kFp8 = 15,      // gemm_fp8.hip: e4m3 A [M,K] x column-major B, block-scaled MFMA 16x16x128, bf16 out
 };
 
+// dtype kFP8: A, B are OCP fp8 e4m3, B is COLUMN-major (ldb = distance between
+// columns, i.e. B is stored as Bt [N,K]), C is bf16 and C = alpha * (A @ B).
 struct Problem {
   int dtype;  // DType
   const void* A;
@@ -31,6 +34,7 @@ struct Problem {
   int lda, ldb, ldc;
   long long sA, sB, sC;
   int batch;
+  float alpha = 1.0f;
 };
 
 // Which kernel `kernel` (kAuto allowed) resolves to for this problem;

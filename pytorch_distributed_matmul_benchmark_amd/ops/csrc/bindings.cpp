@@ -19,8 +19,11 @@ int dtype_code(at::ScalarType t) {
       return 1;
     case at::kBFloat16:
       return 2;
+    case at::kFloat8_e4m3fn:
+      return 3;
     default:
-      TORCH_CHECK(false, "pdmb: unsupported dtype ", t, " (float32 / float16 / bfloat16 only)");
+      TORCH_CHECK(false, "pdmb: unsupported dtype ", t,
+                  " (float32 / float16 / bfloat16 / float8_e4m3fn only)");
   }
   return -1;
 }
@@ -31,11 +34,16 @@ void check_hip(hipError_t e, const char* what) {
 
 // A: [M,K] | [b,M,K], B: [K,N] | [b,K,N] (2-D B broadcasts over the batch),
 // C: [M,N] | [b,M,N]; innermost stride must be 1 (leading dims free).
-pdmb::Problem make_problem(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C) {
+// float8_e4m3fn: B must be column-major (stride(-2) == 1, e.g. Bt.t() of a
+// row-major [N,K] Bt) and C is bfloat16.
+pdmb::Problem make_problem(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C,
+                           double alpha = 1.0) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "pdmb: tensors must be on the GPU");
   TORCH_CHECK(A.device() == B.device() && A.device() == C.device(), "pdmb: device mismatch");
-  TORCH_CHECK(A.scalar_type() == B.scalar_type() && A.scalar_type() == C.scalar_type(),
-              "pdmb: dtype mismatch");
+  const bool fp8 = A.scalar_type() == at::kFloat8_e4m3fn;
+  TORCH_CHECK(A.scalar_type() == B.scalar_type() &&
+                  C.scalar_type() == (fp8 ? at::kBFloat16 : A.scalar_type()),
+              "pdmb: dtype mismatch (fp8 operands take a bfloat16 output)");
   TORCH_CHECK(A.dim() == 2 || A.dim() == 3, "pdmb: A must be 2-D or 3-D");
   TORCH_CHECK(B.dim() == 2 || B.dim() == 3, "pdmb: B must be 2-D or 3-D");
   TORCH_CHECK(C.dim() == std::max(A.dim(), B.dim()), "pdmb: bad output rank");
@@ -51,7 +59,12 @@ pdmb::Problem make_problem(const at::Tensor& A, const at::Tensor& B, const at::T
   auto inner_ok = [](const at::Tensor& t) {
     return t.size(-1) <= 1 || t.stride(-1) == 1;
   };
-  TORCH_CHECK(inner_ok(A) && inner_ok(B) && inner_ok(C), "pdmb: innermost dim must be contiguous");
+  auto colmajor_ok = [](const at::Tensor& t) {
+    return t.size(-2) <= 1 || t.stride(-2) == 1;
+  };
+  TORCH_CHECK(inner_ok(A) && (fp8 ? colmajor_ok(B) : inner_ok(B)) && inner_ok(C),
+              fp8 ? "pdmb: fp8 needs row-major A / C and column-major B"
+                  : "pdmb: innermost dim must be contiguous");
   auto ld = [](const at::Tensor& t) {
     int64_t l = t.stride(-2);
     return std::max<int64_t>(l, std::max<int64_t>(t.size(-1), 1));
@@ -67,7 +80,13 @@ pdmb::Problem make_problem(const at::Tensor& A, const at::Tensor& B, const at::T
   p.N = (int)N;
   p.K = (int)K;
   p.lda = (int)ld(A);
-  p.ldb = (int)ld(B);
+  if (fp8) {
+    const int64_t lb = std::max<int64_t>(B.stride(-1), std::max<int64_t>(K, 1));
+    p.ldb = (int)lb;  // distance between columns (Bt row stride)
+  } else {
+    p.ldb = (int)ld(B);
+  }
+  p.alpha = (float)alpha;
   p.ldc = (int)ld(C);
   p.sA = (batched && A.dim() == 3) ? A.stride(0) : 0;
   p.sB = (batched && B.dim() == 3) ? B.stride(0) : 0;
@@ -81,13 +100,14 @@ at::Tensor alloc_out(const at::Tensor& A, const at::Tensor& B) {
   if (A.dim() == 3 || B.dim() == 3) shape.push_back(A.dim() == 3 ? A.size(0) : B.size(0));
   shape.push_back(A.size(-2));
   shape.push_back(B.size(-1));
-  return at::empty(shape, A.options());
+  const bool fp8 = A.scalar_type() == at::kFloat8_e4m3fn;
+  return at::empty(shape, A.options().dtype(fp8 ? at::kBFloat16 : A.scalar_type()));
 }
 
 at::Tensor matmul(const at::Tensor& A, const at::Tensor& B, c10::optional<at::Tensor> out,
-                  int64_t kernel) {
+                  int64_t kernel, double alpha) {
   at::Tensor C = out.has_value() ? *out : alloc_out(A, B);
-  pdmb::Problem p = make_problem(A, B, C);
+  pdmb::Problem p = make_problem(A, B, C, alpha);
   c10::hip::HIPGuard guard(A.device().index());
   hipStream_t s = c10::hip::getCurrentHIPStream(A.device().index()).stream();
   int used = -1;
@@ -130,8 +150,9 @@ void set_debug_buffer(c10::optional<at::Tensor> buf) {
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) native GEMM kernels and timing loop";
-  m.def("matmul", &matmul, "C = A @ B on gfx950 MFMA", py::arg("A"), py::arg("B"),
-        py::arg("out") = py::none(), py::arg("kernel") = 0);
+  m.def("matmul", &matmul, "C = A @ B on gfx950 MFMA (fp8: C = alpha * A @ B, bf16 out)",
+        py::arg("A"), py::arg("B"), py::arg("out") = py::none(), py::arg("kernel") = 0,
+        py::arg("alpha") = 1.0);
   m.def("resolve", &resolve, "kernel id that would run (or -1)", py::arg("A"), py::arg("B"),
         py::arg("out"), py::arg("kernel") = 0);
   m.def("bench", &bench, "native hipEvent timing loop; returns total ms", py::arg("A"),

@@ -28,7 +28,7 @@ typedef __attribute__((address_space(3))) s16x8 lds_s16x8;
 
 // Data-type tags shared by host and device code. Values are part of the
 // binding ABI (ops/gemm.py mirrors them).
-enum DType : int { kF32 = 0, kF16 = 1, kBF16 = 2 };
+enum DType : int { kF32 = 0, kF16 = 1, kBF16 = 2, kFP8 = 3 /* OCP e4m3fn in, bf16 out */ };
 
 // One MFMA 16x16x32 step on 16-bit operands (a: 8 elements/lane, b: 8).
 template <int DT>
@@ -86,6 +86,7 @@ struct GemmArgs {
   int batch;
   int tiles_m, tiles_n;  // output tiles per batch element
   int supertile;         // 1: XCD-aware 16x16 super-tile order, 0: grouped order
+  float alpha;           // fp8 only: C = alpha * (A @ B) (per-tensor scales folded)
   unsigned long long* dbg;  // diagnostic builds only (in-kernel stamps); nullptr otherwise
 };
 

@@ -20,6 +20,8 @@ hipError_t gemm256_launch(int dt, GemmArgs a, int sched, hipStream_t stream);
 hipError_t gemm_generic_launch(int dt, GemmArgs a, bool vec, hipStream_t stream);
 bool gemm_f32_256_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 hipError_t gemm_f32_256_launch(GemmArgs a, int variant, hipStream_t stream);
+bool gemm_fp8_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
+hipError_t gemm_fp8_launch(GemmArgs a, hipStream_t stream);
 
 static unsigned long long* g_debug_buffer = nullptr;
 
@@ -41,6 +43,7 @@ static GemmArgs to_args(const Problem& p) {
   a.sC = p.sC;
   a.batch = p.batch < 1 ? 1 : p.batch;
   a.dbg = g_debug_buffer;
+  a.alpha = p.alpha;
   return a;
 }
 
@@ -56,6 +59,12 @@ static bool generic_vec_ok(const Problem& p) {
 
 int resolve_kernel(const Problem& p, int kernel) {
   const GemmArgs a = to_args(p);
+  if (p.dtype == kFP8)  // one kernel, no generic / padded fallback
+    return (kernel == kAuto || kernel == kFp8) &&
+                   gemm_fp8_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C)
+               ? kFp8
+               : -1;
+  if (kernel == kFp8) return -1;
   const bool fast = gemm256_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   const bool f32fast = p.dtype == kF32 &&
                        gemm_f32_256_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
@@ -167,6 +176,7 @@ static hipError_t unpad_copy_launch(const void* src, long long lds, int rows, in
 }
 
 static bool wants_padding(const Problem& p, int kernel) {
+  if (p.dtype == kFP8) return false;
   if (kernel != kAuto || p.M <= 0 || p.N <= 0 || p.K <= 0) return false;
   const double flops = 2.0 * p.M * (double)p.N * p.K * (p.batch < 1 ? 1 : p.batch);
   if (flops < kPadMinFlops) return false;
@@ -245,6 +255,7 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     }
     return hipSuccess;
   }
+  if (k == kFp8) return gemm_fp8_launch(a, stream);
   if (k == kMfma256) return gemm256_launch(p.dtype, a, 0, stream);
   if (k == kMfma256b) return gemm256_launch(p.dtype, a, 1, stream);
   if (k == kMfma256c) return gemm256_launch(p.dtype, a, 2, stream);
@@ -323,6 +334,8 @@ const char* kernel_name(int kernel) {
       return "pdmb_f32_256_nn";
     case kF32_256s:
       return "pdmb_f32_256s_nn";
+    case kFp8:
+      return "pdmb_fp8_256_nt";
     default:
       return "auto";
   }

@@ -1,0 +1,299 @@
+// gemm_fp8.hip — C = alpha * (A @ B) with A, B in OCP fp8 e4m3 (gfx950's
+// float8_e4m3fn, not MI300's fnuz), fp32 accumulate, bf16 out, on the
+// block-scaled MFMA v_mfma_scale_f32_16x16x128_f8f6f4.
+//
+// An MI355X extension beyond the reference's float32/float16/bfloat16
+// (matmul_benchmark.py:163-174): the fp8 MFMA with K = 128 runs at twice the
+// bf16 rate (MI355X_MICROARCH.md § Matrix cores: ~5 PF dense), so the same
+// `--dtype` sweep can show what the matrix cores do at fp8.
+//
+// Layout: A row-major [M,K]; B column-major, i.e. stored as Bt [N,K]
+// row-major (torch._scaled_mm's convention, and what a weight matrix is).
+// Both operands are then K-contiguous, so both reach their MFMA fragments
+// with ds_read_b128 — no transposed LDS read is needed.
+//
+// Design: the schedule of gemm_mfma256.hip SCHED 3 carried over byte for
+// byte. A K-tile of 128 fp8 is 128 bytes per row — the same LDS image as a
+// 64-deep bf16 tile (A 32 KiB + two 16 KiB B halves per stage, 2 stages =
+// 128 KiB, 1 workgroup / CU, 8 waves 2 (M) x 4 (N), 128x64 per wave) — and
+// each 16x16x128 MFMA takes twice the cycles of a 16x16x32 bf16 one, so a
+// compute slot of 16 fp8 MFMAs is as long as SCHED 3's 32 bf16 MFMAs while
+// doing twice the FLOPs. LDS-DMA units, counted vmcnt(6), the one-slot
+// stagger of waves 4..7 and the XCD-aware tile order are unchanged.
+//
+// MFMA fragments (16x16x128, e4m3): lane l holds 32 consecutive k of one
+// row, k = 32 * (l >> 4) + j (j = 0..31), i.e. two 16-B LDS chunks 2g and
+// 2g+1 of the 128-B row. The block scales are fixed at e8m0 127 (= 1.0); the
+// per-tensor scale alpha is applied in the epilogue. Operands are swapped
+// (B fragment as the MFMA's A) so each lane owns 4 consecutive output
+// columns -> 8-byte bf16 stores.
+//
+// Fast-path constraints (host-checked, no fallback for fp8): K % 128 == 0,
+// N % 4 == 0, lda / ldb % 16 == 0 (16-B rows), ldc % 4 == 0, 16-B aligned
+// A / B, 8-B aligned C. M and N edges read zeros through the buffer
+// descriptor's extent and are masked at the store.
+#include "common.h"
+
+namespace pdmb {
+namespace k8 {
+
+constexpr int BM = 256, BN = 256, BK = 128;  // BK in fp8 elements (= bytes)
+constexpr int NTHREADS = 512;
+constexpr int A_BYTES = BM * BK;             // 32 KiB
+constexpr int BH_BYTES = (BN / 2) * BK;      // 16 KiB per B half
+constexpr int STAGE = A_BYTES + 2 * BH_BYTES;
+constexpr int LDS_BYTES = 2 * STAGE;         // 128 KiB
+constexpr int kScaleOne = 0x7F7F7F7F;        // e8m0 127 = 2^0 in every byte
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+
+#define PDMB8_BARRIER()                     \
+  do {                                      \
+    __builtin_amdgcn_sched_barrier(0);      \
+    asm volatile("s_barrier" ::: "memory"); \
+    __builtin_amdgcn_sched_barrier(0);      \
+  } while (0)
+#define PDMB8_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+#define PDMB8_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+
+struct Ctx {
+  const char* Ab;     // A of this batch element at row m0
+  const char* Bb;     // Bt of this batch element at row (= output column) n0
+  long long a_bytes;  // bytes from Ab to the end of A's extent
+  long long b_bytes;  // bytes from Bb to the end of Bt's extent
+  int nk;             // K / 128
+  uint32_t voffA[2][2];  // [mq][h] per-lane DMA source offsets
+  uint32_t voffB[2][2];  // [nq][h]
+  uint32_t aoff[2];      // [h] per-lane LDS read offsets (stage 0, quadrant 0)
+  uint32_t boff[2];
+  int wu;
+  uint32_t lds0;
+};
+
+// One LDS-DMA unit (2 wave-instructions per wave). TYPE: 0 = A rows of
+// quadrant-row 0, 1 = B half 0, 2 = B half 1, 3 = A rows of quadrant-row 1.
+// A unit holds the 128 rows {mq*64 + [0,64)} U {128 + mq*64 + [0,64)}; a B
+// half holds the 128 output columns wc*64 + nq*32 + [0,32) of the 4 wave
+// columns, LDS row i <-> column (i>>5)*64 + nq*32 + (i&31). 16-B chunk c of
+// LDS row r holds source chunk c ^ swz(r) (conflict-free b128 reads).
+template <int TYPE, int STG>
+__device__ __forceinline__ void issue_unit(const Ctx& c, int tile) {
+  tile = tile < c.nk ? tile : c.nk - 1;  // tail re-reads the last tile (harmless)
+  const long long off = (long long)tile * BK;
+  if constexpr (TYPE == 0 || TYPE == 3) {
+    constexpr int mq = TYPE == 0 ? 0 : 1;
+    const u32x4 rs = make_rsrc(c.Ab + off, c.a_bytes - off);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      dma16(rs, c.voffA[mq][h], c.lds0 + STG * STAGE + (h * 128 + mq * 64 + c.wu * 8) * BK);
+  } else {
+    constexpr int nq = TYPE == 1 ? 0 : 1;
+    const u32x4 rs = make_rsrc(c.Bb + off, c.b_bytes - off);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      dma16(rs, c.voffB[nq][h],
+            c.lds0 + STG * STAGE + A_BYTES + nq * BH_BYTES + (h * 64 + c.wu * 8) * BK);
+  }
+}
+
+// LDS swizzle of a 128-B row r: 16-B chunk c is stored at c ^ swz(r).
+// A lane's fragment is chunks 2g, 2g+1 of row l16, and ds_read_b128 serves
+// lanes in the groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32): in each
+// group the rows are all 16 distinct, but lanes on rows 4..11 fetch a chunk
+// 2 apart from the others (g differs by one). The plain (r>>1)&7 swizzle of
+// the bf16 kernel then collides (PMC: 4.0e8 conflict cycles of 8.1e8); the
+// extra XOR by 2 on rows 4..11 cancels that offset, so each group covers all
+// 64 banks once.
+__device__ __forceinline__ int swz(int r) {
+  return ((r >> 1) & 7) ^ ((((r & 15) - 4) & 15) < 8 ? 2 : 0);
+}
+
+__device__ __forceinline__ i32x8 join(u32x4 lo, u32x4 hi) {
+  const u32x4 v[2] = {lo, hi};
+  return __builtin_bit_cast(i32x8, v);
+}
+
+// A fragments of quadrant-row MQ: 4 m-blocks x 32 B.
+template <int STG, int MQ>
+__device__ __forceinline__ void read_a(const Ctx& c, const char* smem, i32x8 (&ra)[4]) {
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const char* p = smem + STG * STAGE + (MQ * 64 + mi * 16) * BK;
+    ra[mi] = join(*(const lds_u32x4*)(p + c.aoff[0]), *(const lds_u32x4*)(p + c.aoff[1]));
+  }
+}
+
+// B fragments of half NQ: 2 n-blocks x 32 B.
+template <int STG, int NQ>
+__device__ __forceinline__ void read_b(const Ctx& c, const char* smem, i32x8 (&rb)[2]) {
+#pragma unroll
+  for (int nn = 0; nn < 2; ++nn) {
+    const char* p = smem + STG * STAGE + A_BYTES + NQ * BH_BYTES + nn * 16 * BK;
+    rb[nn] = join(*(const lds_u32x4*)(p + c.boff[0]), *(const lds_u32x4*)(p + c.boff[1]));
+  }
+}
+
+template <int MQ, int NQ>
+__device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[8][4], const i32x8 (&ra)[4],
+                                             const i32x8 (&rb)[2]) {
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int nn = 0; nn < 2; ++nn)
+      acc[MQ * 4 + mi][NQ * 2 + nn] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+          rb[nn], ra[mi], acc[MQ * 4 + mi][NQ * 2 + nn], 0 /*A: e4m3*/, 0 /*B: e4m3*/, 0,
+          kScaleOne, 0, kScaleOne);
+}
+
+// One K-tile from stage STG in two phases (SCHED 3 of gemm_mfma256.hip; the
+// RAW / WAR argument there carries over unit for unit):
+//   X: read B0,B1 | issue B0',B1' of t+1 | MFMA quadrants (0,0),(0,1)
+//   Y: read A1 and the next tile's A0 | issue A0,A1 of t+2 | MFMA (1,1),(1,0)
+template <int STG>
+__device__ __forceinline__ void tile_body(const Ctx& c, char* smem, int t, f32x4 (&acc)[8][4],
+                                          i32x8 (&ra)[4], i32x8 (&ra2)[4], i32x8 (&rb0)[2],
+                                          i32x8 (&rb1)[2]) {
+  read_b<STG, 0>(c, smem, rb0);
+  read_b<STG, 1>(c, smem, rb1);
+  issue_unit<2, STG ^ 1>(c, t + 1);
+  issue_unit<3, STG ^ 1>(c, t + 1);
+  PDMB8_LGKM0();
+  PDMB8_VMCNT(6);
+  PDMB8_BARRIER();
+  mma_quadrant<0, 0>(acc, ra2, rb0);
+  mma_quadrant<0, 1>(acc, ra2, rb1);
+  PDMB8_BARRIER();
+  read_a<STG, 1>(c, smem, ra);
+  read_a<STG ^ 1, 0>(c, smem, ra2);
+  issue_unit<0, STG>(c, t + 2);
+  issue_unit<1, STG>(c, t + 2);
+  PDMB8_LGKM0();
+  PDMB8_VMCNT(6);
+  PDMB8_BARRIER();
+  mma_quadrant<1, 1>(acc, ra, rb1);
+  mma_quadrant<1, 0>(acc, ra, rb0);
+  PDMB8_BARRIER();
+}
+
+__global__ void __launch_bounds__(NTHREADS, 2) gemm_fp8_nt(GemmArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+
+  int bz, tm, tn;
+  map_tile(a, blockIdx.x, bz, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wu >> 2, wc = wu & 3;
+  const int l16 = lane & 15, g = lane >> 4;
+
+  Ctx c;
+  c.wu = wu;
+  c.lds0 = (uint32_t)(size_t)((lds_void*)smem);
+  c.nk = a.K / BK;
+  c.Ab = (const char*)a.A + (long long)bz * a.sA + (long long)m0 * a.lda;
+  c.Bb = (const char*)a.B + (long long)bz * a.sB + (long long)n0 * a.ldb;
+  // Exact extents: rows >= M (A) and columns >= N (Bt rows) read zeros.
+  c.a_bytes = (long long)(a.M - m0 - 1) * a.lda + a.K;
+  c.b_bytes = (long long)(a.N - n0 - 1) * a.ldb + a.K;
+  {
+    const int lr8 = lane >> 3, lc8 = lane & 7;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int mq = 0; mq < 2; ++mq) {
+        const int r = h * 128 + mq * 64 + wu * 8 + lr8;
+        c.voffA[mq][h] = (uint32_t)(r * a.lda + ((lc8 ^ swz(r)) * 16));
+      }
+#pragma unroll
+      for (int nq = 0; nq < 2; ++nq) {
+        const int i = h * 64 + wu * 8 + lr8;
+        const int col = (i >> 5) * 64 + nq * 32 + (i & 31);
+        c.voffB[nq][h] = (uint32_t)(col * a.ldb + ((lc8 ^ swz(i)) * 16));
+      }
+    }
+    const int sw = swz(l16);  // rows read are 16-aligned bases + l16
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      c.aoff[h] = (uint32_t)((wr * 128 + l16) * BK + (((2 * g + h) ^ sw) * 16));
+      c.boff[h] = (uint32_t)((wc * 32 + l16) * BK + (((2 * g + h) ^ sw) * 16));
+    }
+  }
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  i32x8 ra[4], ra2[4], rb0[2], rb1[2];
+
+  // Prologue: units 0..5 = A0,B0,B1,A1 of tile 0 and A0,B0 of tile 1.
+  issue_unit<0, 0>(c, 0);
+  issue_unit<1, 0>(c, 0);
+  issue_unit<2, 0>(c, 0);
+  issue_unit<3, 0>(c, 0);
+  issue_unit<0, 1>(c, 1);
+  issue_unit<1, 1>(c, 1);
+  PDMB8_VMCNT(6);  // units 0..2 landed (for this wave); 3..5 in flight
+  PDMB8_BARRIER();
+  if (wr == 1) PDMB8_BARRIER();  // waves 4..7 run one slot behind waves 0..3
+  read_a<0, 0>(c, smem, ra2);
+
+  const int nk = c.nk;
+  for (int t = 0; t < nk; t += 2) {
+    tile_body<0>(c, smem, t, acc, ra, ra2, rb0, rb1);
+    if (t + 1 < nk) tile_body<1>(c, smem, t + 1, acc, ra, ra2, rb0, rb1);
+  }
+  if (wr == 0) PDMB8_BARRIER();
+  PDMB8_VMCNT(0);  // drain the clamped tail DMAs before the LDS is released
+
+  // Epilogue: acc[i][j] holds C^T of a 16x16 tile — lane owns row l16 and
+  // columns 4g..4g+3; scale by alpha, round to bf16.
+  const float alpha = a.alpha;
+  char* Cb = (char*)a.C + (long long)bz * a.sC * 2;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = m0 + wr * 128 + i * 16 + l16;
+    if (row < a.M) {
+      char* crow = Cb + (long long)row * a.ldc * 2;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wc * 64 + j * 16 + 4 * g;
+        if (col < a.N) {
+          u32x2 v;
+          v.x = pack2<kBF16>(acc[i][j].x * alpha, acc[i][j].y * alpha);
+          v.y = pack2<kBF16>(acc[i][j].z * alpha, acc[i][j].w * alpha);
+          *(u32x2*)(crow + col * 2) = v;
+        }
+      }
+    }
+  }
+}
+
+}  // namespace k8
+
+bool gemm_fp8_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c) {
+  if (a.K % 128 != 0 || a.K <= 0 || a.N % 4 != 0 || a.M <= 0 || a.N <= 0) return false;
+  if (a.lda % 16 || a.ldb % 16 || a.ldc % 4) return false;
+  if (a.lda < a.K || a.ldb < a.K) return false;
+  if (a.batch > 1 && (a.sA % 16 || a.sB % 16 || a.sC % 4)) return false;
+  if (align_a % 16 || align_b % 16 || align_c % 8) return false;
+  // 32-bit per-lane DMA offsets: up to 255 rows of A / Bt.
+  if ((long long)256 * a.lda >= (1LL << 31) || (long long)256 * a.ldb >= (1LL << 31)) return false;
+  return true;
+}
+
+hipError_t gemm_fp8_launch(GemmArgs a, hipStream_t stream) {
+  a.tiles_m = (a.M + k8::BM - 1) / k8::BM;
+  a.tiles_n = (a.N + k8::BN - 1) / k8::BN;
+  a.supertile = (a.tiles_m % 16 == 0 && a.tiles_n % 16 == 0) ? 1 : 0;
+  const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch;
+  if (nblocks <= 0) return hipSuccess;
+  if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k8::gemm_fp8_nt, dim3((unsigned)nblocks), dim3(k8::NTHREADS), 0, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace pdmb

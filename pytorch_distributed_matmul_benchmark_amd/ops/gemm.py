@@ -22,13 +22,14 @@ from . import _native
 
 KERNELS = {"auto": 0, "mfma256": 1, "generic": 2, "mfma256b": 3, "mfma256c": 4, "mfma256d": 9,
            "mfma256c_stamp": 5, "f32_256": 6,
-           "f32_256s": 7, "diag_f32_nodma": 20, "x_clusterprio": 10, "x_staticprio": 11, "x_tall": 13}
+           "f32_256s": 7, "fp8": 15, "diag_f32_nodma": 20, "x_clusterprio": 10, "x_staticprio": 11, "x_tall": 13}
 KERNEL_NAMES = {0: "auto", 1: "pdmb_mfma256_nn", 2: "pdmb_generic_nn", 3: "pdmb_mfma256b_nn", 4: "pdmb_mfma256c_nn",
                 9: "pdmb_mfma256d_nn",
                 5: "pdmb_mfma256c_stamp", 6: "pdmb_f32_256_nn",
-                7: "pdmb_f32_256s_nn",
+                7: "pdmb_f32_256s_nn", 15: "pdmb_fp8_256_nt",
                 -1: "unsupported"}
 SUPPORTED_DTYPES = (torch.float32, torch.float16, torch.bfloat16)
+FP8 = torch.float8_e4m3fn  # OCP e4m3 (gfx950), bf16 output, column-major B
 
 
 def _kid(kernel) -> int:
@@ -54,13 +55,52 @@ def _prep(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
+def _prep_colmajor(t: torch.Tensor) -> torch.Tensor:
+    # fp8 B operand: unit stride along K (column-major [K,N], i.e. a row-major Bt [N,K]).
+    if t.shape[-2] > 1 and t.stride(-2) != 1:
+        return t.transpose(-1, -2).contiguous().transpose(-1, -2)
+    return t
+
+
+def _prep_pair(A: torch.Tensor, B: torch.Tensor):
+    if A.dtype == FP8:
+        return _prep(A), _prep_colmajor(B)
+    return _prep(A), _prep(B)
+
+
+def out_dtype(dtype: torch.dtype) -> torch.dtype:
+    """Output dtype of a native GEMM on ``dtype`` operands (fp8 → bf16)."""
+    return torch.bfloat16 if dtype == FP8 else dtype
+
+
+def fp8_quantize(x: torch.Tensor, colmajor: bool = False):
+    """Per-tensor scaled OCP e4m3 copy of ``x``: returns ``(x8, scale)`` with
+    ``x ≈ scale * x8.float()`` (amax mapped to 448, e4m3's largest finite).
+    ``colmajor=True`` lays the copy out column-major (the fp8 B operand)."""
+    amax = x.detach().abs().amax().float().clamp(min=1e-12)
+    scale = float(amax) / 448.0
+    src = x.transpose(-1, -2) if colmajor else x
+    x8 = (src.float() / scale).to(FP8).contiguous()
+    return (x8.transpose(-1, -2) if colmajor else x8), scale
+
+
 def matmul(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
-           kernel="auto") -> torch.Tensor:
-    """``out = A @ B`` for 2-D/3-D row-major operands (3-D = batched)."""
+           kernel="auto", alpha: float = 1.0) -> torch.Tensor:
+    """``out = A @ B`` for 2-D/3-D row-major operands (3-D = batched).
+
+    float8_e4m3fn operands: ``out = alpha * (A @ B)`` in bfloat16 on the
+    block-scaled fp8 MFMA (B is used column-major; a row-major B is copied).
+    ``alpha`` folds the per-tensor scales (see ``fp8_quantize``)."""
     if A.dim() not in (2, 3) or B.dim() not in (2, 3):
         raise ValueError("matmul: operands must be 2-D or 3-D")
     if A.shape[-1] != B.shape[-2]:
         raise ValueError(f"matmul: shape mismatch {tuple(A.shape)} @ {tuple(B.shape)}")
+    if A.device.type != "cuda" and A.dtype == FP8:
+        res = (torch.matmul(A.float(), B.float()) * alpha).to(torch.bfloat16)
+        if out is None:
+            return res
+        out.copy_(res)
+        return out
     if A.device.type != "cuda":
         if A.dim() == 3 or B.dim() == 3:
             res = torch.matmul(A, B)
@@ -69,13 +109,14 @@ def matmul(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
             out.copy_(res)
             return out
         return torch.matmul(A, B, out=out) if out is not None else torch.matmul(A, B)
-    if A.dtype not in SUPPORTED_DTYPES:
+    if A.dtype not in SUPPORTED_DTYPES and A.dtype != FP8:
         raise TypeError(f"matmul: unsupported dtype {A.dtype}")
     C = _native.load()
-    A, B = _prep(A), _prep(B)
+    A, B = _prep_pair(A, B)
     if out is None:
-        out = torch.empty(_out_shape(A, B), dtype=A.dtype, device=A.device)
-    C.matmul(A, B, out, _kid(kernel))  # auto: odd K/N/alignment padded onto the fast path (C++)
+        out = torch.empty(_out_shape(A, B), dtype=out_dtype(A.dtype), device=A.device)
+    # auto: odd K/N/alignment padded onto the fast path (C++; not for fp8)
+    C.matmul(A, B, out, _kid(kernel), float(alpha))
     return out
 
 
@@ -98,7 +139,7 @@ def bmm(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
     """Batched ``out[b] = A[b] @ B[b]`` (the reference's ``torch.bmm``)."""
     if A.dim() != 3 or B.dim() != 3:
         raise ValueError("bmm: operands must be 3-D")
-    if A.device.type != "cuda":
+    if A.device.type != "cuda" and A.dtype != FP8:
         return torch.bmm(A, B, out=out) if out is not None else torch.bmm(A, B)
     return matmul(A, B, out=out, kernel=kernel)
 
@@ -110,8 +151,9 @@ def kernel_for(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = N
         return "torch.matmul(cpu)"
     C = _native.load()
     if out is None:
-        out = torch.empty(_out_shape(A, B), dtype=A.dtype, device=A.device)
-    return KERNEL_NAMES[int(C.resolve(_prep(A), _prep(B), out, _kid(kernel)))]
+        out = torch.empty(_out_shape(A, B), dtype=out_dtype(A.dtype), device=A.device)
+    A, B = _prep_pair(A, B)
+    return KERNEL_NAMES[int(C.resolve(A, B, out, _kid(kernel)))]
 
 
 def bench_matmul(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, iters: int,
@@ -121,10 +163,11 @@ def bench_matmul(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, iters: int
         import time
 
         for _ in range(warmup):
-            torch.matmul(A, B, out=out)
+            matmul(A, B, out=out)
         t0 = time.perf_counter()
         for _ in range(iters):
-            torch.matmul(A, B, out=out)
+            matmul(A, B, out=out)
         return (time.perf_counter() - t0) * 1e3
     C = _native.load()
-    return float(C.bench(_prep(A), _prep(B), out, int(iters), int(warmup), bool(graph), _kid(kernel)))
+    A, B = _prep_pair(A, B)
+    return float(C.bench(A, B, out, int(iters), int(warmup), bool(graph), _kid(kernel)))

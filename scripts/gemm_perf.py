@@ -17,7 +17,29 @@ import torch  # noqa: E402
 
 from pytorch_distributed_matmul_benchmark_amd.ops import gemm  # noqa: E402
 
-DT = {"bfloat16": torch.bfloat16, "float16": torch.float16, "float32": torch.float32}
+DT = {"bfloat16": torch.bfloat16, "float16": torch.float16, "float32": torch.float32,
+      "float8_e4m3fn": torch.float8_e4m3fn}
+
+
+def scaled_mm_ms(A8, B8, out, iters, warmup):
+    """hipBLASLt fp8 through torch._scaled_mm (None if this build lacks it)."""
+    one = torch.ones((), device=A8.device)
+    try:
+        torch._scaled_mm(A8, B8, scale_a=one, scale_b=one, out_dtype=torch.bfloat16)
+    except Exception as e:  # noqa: BLE001
+        print(f"# torch._scaled_mm unavailable: {e!r}"[:200], flush=True)
+        return None
+    f = lambda: torch._scaled_mm(A8, B8, scale_a=one, scale_b=one, out_dtype=torch.bfloat16)  # noqa: E731
+    for _ in range(warmup):
+        f()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        f()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e)
 
 
 def torch_ms(A, B, out, iters, warmup):
@@ -50,9 +72,14 @@ def main():
              else [(n, n, n) for n in a.sizes])
     for m, n, k in probs:
         torch.manual_seed(0)
-        A = torch.randn(m, k, device="cuda", dtype=dt)
-        B = torch.randn(k, n, device="cuda", dtype=dt)
-        out = torch.empty(m, n, device="cuda", dtype=dt)
+        fp8 = dt == torch.float8_e4m3fn
+        if fp8:  # per-tensor scaled e4m3, B column-major (alpha folds the scales)
+            A, sa = gemm.fp8_quantize(torch.randn(m, k, device="cuda"))
+            B, sb = gemm.fp8_quantize(torch.randn(k, n, device="cuda"), colmajor=True)
+        else:
+            A = torch.randn(m, k, device="cuda", dtype=dt)
+            B = torch.randn(k, n, device="cuda", dtype=dt)
+        out = torch.empty(m, n, device="cuda", dtype=gemm.out_dtype(dt))
         flop = 2.0 * m * n * k
         res = {"n": n, "shape": f"{m}x{n}x{k}", "dtype": a.dtype,
                "kernel": gemm.kernel_for(A, B, out, kernel=a.kernel)}
@@ -63,8 +90,10 @@ def main():
             ms = gemm.bench_matmul(A, B, out, a.iters, a.warmup, graph=True, kernel=a.kernel) / a.iters
             ours_g.append(flop / ms / 1e9)
             if not a.no_torch:
-                ms = torch_ms(A, B, out, a.iters, a.warmup) / a.iters
-                theirs.append(flop / ms / 1e9)
+                ms = (scaled_mm_ms(A, B, out, a.iters, a.warmup) if fp8
+                      else torch_ms(A, B, out, a.iters, a.warmup))
+                if ms is not None:
+                    theirs.append(flop / (ms / a.iters) / 1e9)
         ref = torch.matmul(A.float(), B.float())
         C = gemm.matmul(A, B, kernel=a.kernel)
         res["relerr"] = ((C.float() - ref).norm() / ref.norm()).item()

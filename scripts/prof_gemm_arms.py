@@ -28,21 +28,32 @@ def main():
     dt = getattr(torch, a.dtype)
     n = a.n
     torch.manual_seed(0)
-    A = torch.randn(n, n, device="cuda", dtype=dt)
-    B = torch.randn(n, n, device="cuda", dtype=dt)
-    C = torch.empty(n, n, device="cuda", dtype=dt)
+    if dt == torch.float8_e4m3fn:  # per-tensor scaled e4m3, B column-major; torch arm = _scaled_mm
+        A, _ = gemm.fp8_quantize(torch.randn(n, n, device="cuda"))
+        B, _ = gemm.fp8_quantize(torch.randn(n, n, device="cuda"), colmajor=True)
+        one = torch.ones((), device="cuda")
+
+        def torch_mm(A, B, out):
+            torch._scaled_mm(A, B, scale_a=one, scale_b=one, out_dtype=torch.bfloat16)
+    else:
+        A = torch.randn(n, n, device="cuda", dtype=dt)
+        B = torch.randn(n, n, device="cuda", dtype=dt)
+
+        def torch_mm(A, B, out):
+            torch.matmul(A, B, out=out)
+    C = torch.empty(n, n, device="cuda", dtype=gemm.out_dtype(dt))
     ks = a.kernels.split(",")
     for _ in range(2):  # warm (clocks, caches, code objects)
         for k in ks:
             gemm.matmul(A, B, out=C, kernel=k)
         if not a.no_torch:
-            torch.matmul(A, B, out=C)
+            torch_mm(A, B, C)
     torch.cuda.synchronize()
     for _ in range(a.reps):
         for k in ks:
             gemm.matmul(A, B, out=C, kernel=k)
         if not a.no_torch:
-            torch.matmul(A, B, out=C)
+            torch_mm(A, B, C)
     torch.cuda.synchronize()
     print("done")
 

@@ -1,0 +1,110 @@
+"""fp8 (OCP e4m3fn) GEMM on the block-scaled MFMA (gemm_fp8.hip) vs a float64
+reference of the same dequantized operands. bf16 output: exact-integer cases
+compare bit-for-bit after rounding the fp64 reference to bf16."""
+import pytest
+import torch
+
+from pytorch_distributed_matmul_benchmark_amd.ops import gemm
+
+pytestmark = pytest.mark.gpu
+FP8 = torch.float8_e4m3fn
+
+
+def _ints(shape, g, lo=-3, hi=4):
+    return torch.randint(lo, hi, shape, device="cuda", generator=g).float()
+
+
+def _colmajor(x):
+    """[K,N] view of a row-major [N,K] copy (the fp8 B layout)."""
+    return x.transpose(-1, -2).contiguous().transpose(-1, -2)
+
+
+def _relerr(x, ref):
+    return ((x.double() - ref).norm() / ref.norm()).item()
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 256), (1000, 1052, 384),
+                                   (300, 200, 128), (2304, 2048, 1024)])
+def test_fp8_exact_small_integers(M, N, K):
+    g = torch.Generator(device="cuda").manual_seed(M + 7 * N + K)
+    Af, Bf = _ints((M, K), g), _ints((K, N), g)
+    A8, B8 = Af.to(FP8), _colmajor(Bf.to(FP8))
+    assert gemm.kernel_for(A8, B8) == "pdmb_fp8_256_nt"
+    C = gemm.matmul(A8, B8)
+    assert C.dtype == torch.bfloat16 and C.shape == (M, N)
+    ref = (Af.double() @ Bf.double()).to(torch.bfloat16)
+    assert torch.equal(C, ref)
+
+
+def test_fp8_identity_with_asymmetric_b():
+    n = 512
+    A = torch.eye(n, device="cuda")
+    B = ((torch.arange(n * n, device="cuda").view(n, n) * 7) % 13 - 6).float()  # asymmetric
+    C = gemm.matmul(A.to(FP8), _colmajor(B.to(FP8)))
+    assert torch.equal(C.float(), B)
+    C = gemm.matmul(B.to(FP8), _colmajor(A.to(FP8)))
+    assert torch.equal(C.float(), B)
+
+
+def test_fp8_row_major_b_is_accepted():
+    g = torch.Generator(device="cuda").manual_seed(5)
+    Af, Bf = _ints((512, 256), g), _ints((256, 384), g)
+    C = gemm.matmul(Af.to(FP8), Bf.to(FP8))  # row-major B: copied to column-major
+    assert torch.equal(C, (Af.double() @ Bf.double()).to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 4096, 4096), (1536, 1280, 2048)])
+def test_fp8_random_scaled(M, N, K):
+    torch.manual_seed(M + N)
+    A = torch.randn(M, K, device="cuda")
+    B = torch.randn(K, N, device="cuda")
+    A8, sa = gemm.fp8_quantize(A)
+    B8, sb = gemm.fp8_quantize(B, colmajor=True)
+    assert B8.stride(-2) == 1
+    C = gemm.matmul(A8, B8, alpha=sa * sb)
+    ref = (A8.double() * sa) @ (B8.double() * sb)  # same quantized operands
+    assert _relerr(C, ref) < 8e-3  # bf16 output rounding
+    assert _relerr(C, A.double() @ B.double()) < 8e-2  # vs unquantized: e4m3 error
+
+
+def test_fp8_batched_and_column_shards():
+    g = torch.Generator(device="cuda").manual_seed(3)
+    Af, Bf = _ints((3, 384, 256), g), _ints((3, 256, 640), g)
+    A8, B8 = Af.to(FP8), _colmajor(Bf.to(FP8))
+    C = gemm.matmul(A8, B8)
+    assert torch.equal(C, torch.bmm(Af.double(), Bf.double()).to(torch.bfloat16))
+    # matrix_parallel-style column shards of a column-major B are row slices of Bt
+    Bt = _ints((1024, 512), g).to(FP8)  # [N, K]
+    Ai = _ints((640, 512), g)
+    for r in range(4):
+        Bs = Bt[r * 256:(r + 1) * 256].t()  # [K, 256] column-major view, no copy
+        assert Bs.stride(-2) == 1
+        C = gemm.matmul(Ai.to(FP8), Bs)
+        ref = (Ai.double() @ Bs.double()).to(torch.bfloat16)
+        assert torch.equal(C, ref)
+
+
+def test_fp8_race_screen():
+    torch.manual_seed(11)
+    A8, sa = gemm.fp8_quantize(torch.randn(4096, 4096, device="cuda"))
+    B8, sb = gemm.fp8_quantize(torch.randn(4096, 4096, device="cuda"), colmajor=True)
+    ref = gemm.matmul(A8, B8, alpha=sa * sb)
+    for _ in range(20):
+        assert torch.equal(gemm.matmul(A8, B8, alpha=sa * sb), ref)
+
+
+def test_fp8_unsupported_shape_fails_loudly():
+    A8 = torch.zeros(256, 96, device="cuda").to(FP8)  # K % 128 != 0: no fp8 fallback
+    B8 = _colmajor(torch.zeros(96, 256, device="cuda").to(FP8))
+    assert gemm.kernel_for(A8, B8) == "unsupported"
+    with pytest.raises(RuntimeError):
+        gemm.matmul(A8, B8)
+
+
+def test_fp8_bench_loop():
+    A8, _ = gemm.fp8_quantize(torch.randn(8192, 8192, device="cuda"))
+    B8, _ = gemm.fp8_quantize(torch.randn(8192, 8192, device="cuda"), colmajor=True)
+    C = torch.empty(8192, 8192, device="cuda", dtype=torch.bfloat16)
+    ms = gemm.bench_matmul(A8, B8, C, 10, 3) / 10
+    tflops = 2 * 8192 ** 3 / ms / 1e9
+    assert tflops > 1500, tflops  # above any bf16 rate: the fp8 MFMA path really runs
