@@ -53,7 +53,8 @@ BASELINE_TFLOPS = {"independent": {1: 140.0, 2: 294.0},
                    "batch_parallel": {1: 140.0, 2: 237.0},
                    "matrix_parallel": {1: 140.0, 2: 141.0}}
 METRIC = "TFLOPS (whole node) + scaling efficiency, 16k×16k bf16 GEMM at 1/2/4/8 GPUs"
-DTYPES = {"bfloat16": torch.bfloat16, "float16": torch.float16, "float32": torch.float32}
+DTYPES = {"bfloat16": torch.bfloat16, "float16": torch.float16, "float32": torch.float32,
+          "float8_e4m3fn": torch.float8_e4m3fn}
 
 
 class Workload:
@@ -65,14 +66,15 @@ class Workload:
         self.dt = DTYPES[a.dtype]
         self.backend = a.backend
         dev, n, ws, dt = ctx.device, a.size, ctx.world_size, self.dt
+        odt = gemm.out_dtype(dt)  # fp8 operands write a bf16 C
         self._g = torch.Generator(device=dev)
         flop_gemm = 2.0 * n * n * n
         comp = torch.cuda.current_stream(dev) if self.cuda else None
         overlap = overlap and ws > 1
 
         if mode == "independent":
-            A, B = self._rnd(n, n, seed=2 * ctx.rank), self._rnd(n, n, seed=2 * ctx.rank + 1)
-            C = torch.empty(n, n, device=dev, dtype=dt)
+            A, B = self._rnd(n, n, seed=2 * ctx.rank), self._rnd(n, n, seed=2 * ctx.rank + 1, b=True)
+            C = torch.empty(n, n, device=dev, dtype=odt)
             self.kernel = self._label(A, B, C)
 
             def step():
@@ -81,8 +83,9 @@ class Workload:
             self.global_batch, self.parallelism = ws, f"independent{ws}"
         elif mode == "batch_parallel":
             lb, gb = local_batch(ws), global_batch(ws)
-            A, B = self._rnd(lb, n, n, seed=2 * ctx.rank), self._rnd(lb, n, n, seed=2 * ctx.rank + 1)
-            C = torch.empty(lb, n, n, device=dev, dtype=dt)
+            A = self._rnd(lb, n, n, seed=2 * ctx.rank)
+            B = self._rnd(lb, n, n, seed=2 * ctx.rank + 1, b=True)
+            C = torch.empty(lb, n, n, device=dev, dtype=odt)
             self.kernel = self._label(A, B, C)
             if overlap:
                 cs = CommStream(dev)
@@ -111,17 +114,18 @@ class Workload:
         elif mode == "matrix_parallel":
             sh = column_shard(n, ws, ctx.rank, align=8)
             A = self._rnd(n, n, seed=10_000)
-            Bg = self._rnd(n, n, seed=10_001)
-            Bl = torch.zeros(n, sh.padded, device=dev, dtype=dt)
+            Bg = self._rnd(n, n, seed=10_001, b=True)
+            Bl = (torch.zeros(sh.padded, n, device=dev, dtype=dt).t() if dt == gemm.FP8
+                  else torch.zeros(n, sh.padded, device=dev, dtype=dt))
             Bl[:, :sh.width].copy_(Bg[:, sh.start:sh.stop])
             del Bg
-            Cl = torch.empty(n, sh.padded, device=dev, dtype=dt)
+            Cl = torch.empty(n, sh.padded, device=dev, dtype=odt)
             self.kernel = self._label(A, Bl, Cl)
             if overlap:
                 cs = CommStream(dev)
                 rc = row_chunks(n, effective_chunks(n, sh.padded, a.chunks) if self.cuda
                                 else a.chunks)
-                bufs = [torch.empty(ws * (e - s), sh.padded, device=dev, dtype=dt) for s, e in rc]
+                bufs = [torch.empty(ws * (e - s), sh.padded, device=dev, dtype=odt) for s, e in rc]
                 ready = [new_event(dev) for _ in rc]
                 done = [new_event(dev) for _ in rc]
 
@@ -136,7 +140,7 @@ class Workload:
                         for d in done:
                             comp.wait_event(d)
             else:
-                gathered = torch.empty(ws * n, sh.padded, device=dev, dtype=dt)
+                gathered = torch.empty(ws * n, sh.padded, device=dev, dtype=odt)
 
                 def step():
                     self._mm(A, Bl, Cl)
@@ -148,12 +152,22 @@ class Workload:
             raise ValueError(mode)
         self.step = step
 
-    def _rnd(self, *shape, seed):
+    def _rnd(self, *shape, seed, b=False):
+        """N(0,1) operand; fp8: rounded to e4m3 (scale 1), a B operand column-major."""
         self._g.manual_seed(seed)
-        return torch.randn(*shape, generator=self._g, device=self.ctx.device, dtype=self.dt)
+        if self.dt != gemm.FP8:
+            return torch.randn(*shape, generator=self._g, device=self.ctx.device, dtype=self.dt)
+        x = torch.randn(*shape, generator=self._g, device=self.ctx.device, dtype=torch.float32)
+        if b:
+            return x.transpose(-1, -2).contiguous().to(gemm.FP8).transpose(-1, -2)
+        return x.to(gemm.FP8)
 
     def _mm(self, A, B, out):
-        if self.backend == "torch" or not self.cuda:
+        if self.dt == gemm.FP8 and self.cuda and self.backend == "torch":
+            one = torch.ones((), device=A.device)
+            return torch._scaled_mm(A, B, scale_a=one, scale_b=one, out_dtype=torch.bfloat16,
+                                    out=out)
+        if (self.backend == "torch" or not self.cuda) and self.dt != gemm.FP8:
             return torch.matmul(A, B, out=out)
         return gemm.matmul(A, B, out=out)
 
@@ -263,7 +277,8 @@ def main() -> int:
             "ms_per_step": round(ms_step, 4), "higher_is_better": True,
             "scaling": "strong" if a.mode == "matrix_parallel" else "weak",
             "vs_baseline": vs_base(a.mode, value),
-            "dtype": {"bfloat16": "bf16", "float16": "fp16", "float32": "fp32"}[a.dtype],
+            "dtype": {"bfloat16": "bf16", "float16": "fp16", "float32": "fp32",
+                      "float8_e4m3fn": "fp8_e4m3"}[a.dtype],
             "data": "synthetic (torch.randn N(0,1) operands, seeded per rank)",
             "device": ctx.device.type,
             "config": {"model": f"gemm_{a.size}x{a.size}x{a.size}_{a.dtype}",

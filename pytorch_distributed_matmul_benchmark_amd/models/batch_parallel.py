@@ -32,7 +32,7 @@ from ..utils.timing import SegmentTimer, Stopwatch, synchronize, time_loop_ms
 import torch.distributed as dist
 
 from .common import (ModeResult, Workload, align_ranks, allreduced_relerr, gemm_fn, kernel_label,
-                     randn, warmup)
+                     out_dtype, randn, warmup)
 
 
 def _units(lb: int, n: int, chunks: int):
@@ -49,8 +49,8 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     gb = global_batch(ws, w.batch)
     lb = local_batch(ws, w.batch)
     A = randn((lb, n, n), w, dev, seed=2 * (w.seed + ctx.rank))
-    B = randn((lb, n, n), w, dev, seed=2 * (w.seed + ctx.rank) + 1)
-    C = torch.empty((lb, n, n), device=dev, dtype=w.dtype)
+    B = randn((lb, n, n), w, dev, seed=2 * (w.seed + ctx.rank) + 1, operand="B")
+    C = torch.empty((lb, n, n), device=dev, dtype=out_dtype(w))
     mm = gemm_fn(w, dev)
     label = kernel_label(w, A, B, C)
     distributed = ctx.is_distributed

@@ -59,6 +59,20 @@ class ModeResult:
 
 def gemm_fn(w: Workload, device: torch.device) -> Callable:
     """``mm(A, B, out)`` for this workload's device/backend (2-D or batched 3-D)."""
+    if w.dtype == _gemm.FP8 and (device.type != "cuda" or w.backend == "torch"):
+        if device.type != "cuda":
+            return lambda A, B, out: _gemm.matmul(A, B, out=out)  # float64-exact dequant path
+        one = torch.ones((), device=device)
+
+        def mm(A, B, out):  # hipBLASLt fp8 (A/B only)
+            if A.dim() == 3:
+                for b in range(A.shape[0]):
+                    torch._scaled_mm(A[b], B[b], scale_a=one, scale_b=one,
+                                     out_dtype=torch.bfloat16, out=out[b])
+                return out
+            return torch._scaled_mm(A, B, scale_a=one, scale_b=one, out_dtype=torch.bfloat16,
+                                    out=out)
+        return mm
     if device.type != "cuda" or w.backend == "torch":
         def mm(A, B, out):
             if A.dim() == 3:
@@ -78,7 +92,7 @@ def kernel_label(w: Workload, A, B, out) -> str:
     if A.device.type != "cuda":
         return "torch.matmul(cpu)"
     if w.backend == "torch":
-        return "torch.matmul(hipBLASLt)"
+        return "torch._scaled_mm(hipBLASLt)" if w.dtype == _gemm.FP8 else "torch.matmul(hipBLASLt)"
     if w.kernel == "auto":
         padded = _gemm.padded_kernel_for(A, B)
         if padded:
@@ -92,10 +106,32 @@ def generator(device: torch.device, seed: int) -> torch.Generator:
     return g
 
 
-def randn(shape, w: Workload, device: torch.device, seed: int) -> torch.Tensor:
+def randn(shape, w: Workload, device: torch.device, seed: int, operand: str = "A") -> torch.Tensor:
     """N(0,1) operands (random, non-zero data matters on MI355X: DVFS runs
-    zero-filled GEMMs ~15-20% fast — cdna_hip_programming.md §5.4 rule 25)."""
-    return torch.randn(*shape, generator=generator(device, seed), device=device, dtype=w.dtype)
+    zero-filled GEMMs ~15-20% fast — cdna_hip_programming.md §5.4 rule 25).
+
+    float8_e4m3fn: the N(0,1) draw rounded to e4m3 (well inside its ±448
+    range, so the per-tensor scale is 1); a B operand (``operand="B"``) is
+    laid out column-major, the fp8 kernel's B layout (same values)."""
+    g = generator(device, seed)
+    if w.dtype == _gemm.FP8:
+        x = torch.randn(*shape, generator=g, device=device, dtype=torch.float32)
+        if operand == "B":
+            return x.transpose(-1, -2).contiguous().to(_gemm.FP8).transpose(-1, -2)
+        return x.to(_gemm.FP8)
+    return torch.randn(*shape, generator=g, device=device, dtype=w.dtype)
+
+
+def out_dtype(w: Workload) -> torch.dtype:
+    """dtype of the GEMM output C (bf16 for fp8 operands, else the operand dtype)."""
+    return _gemm.out_dtype(w.dtype)
+
+
+def zeros_b(rows: int, cols: int, w: Workload, device: torch.device) -> torch.Tensor:
+    """A zeroed [rows, cols] B-operand buffer in the layout ``randn(..., operand="B")`` uses."""
+    if w.dtype == _gemm.FP8:
+        return torch.zeros((cols, rows), device=device, dtype=w.dtype).t()
+    return torch.zeros((rows, cols), device=device, dtype=w.dtype)
 
 
 def warmup(step: Callable[[], None], w: Workload, ctx: DistContext) -> None:
@@ -181,4 +217,7 @@ def allreduced_relerr(ctx: DistContext, A: torch.Tensor, B: torch.Tensor, C: tor
 
 def tolerance(dtype: torch.dtype) -> float:
     """Norm-relative error budget of a fp32-accumulated GEMM with dtype outputs."""
-    return {torch.bfloat16: 1e-2, torch.float16: 2e-3, torch.float32: 1e-5}[dtype]
+    # fp8 operands: the reference is float64 of the SAME e4m3 values, so only the
+    # bf16 output rounding remains.
+    return {torch.bfloat16: 1e-2, torch.float16: 2e-3, torch.float32: 1e-5,
+            _gemm.FP8: 1e-2}[dtype]

@@ -18,14 +18,14 @@ from ..parallel.dist import DistContext
 from ..utils.metrics import gemm_flops, tflops_from
 from ..utils.timing import SegmentTimer
 from .common import (ModeResult, Workload, align_ranks, allreduced_relerr, gemm_fn, kernel_label,
-                     randn, warmup)
+                     out_dtype, randn, warmup)
 
 
 def run(w: Workload, ctx: DistContext) -> ModeResult:
     dev, n, ws = ctx.device, w.n, ctx.world_size
     A = randn((n, n), w, dev, seed=2 * (w.seed + ctx.rank))
-    B = randn((n, n), w, dev, seed=2 * (w.seed + ctx.rank) + 1)
-    C = torch.empty((n, n), device=dev, dtype=w.dtype)
+    B = randn((n, n), w, dev, seed=2 * (w.seed + ctx.rank) + 1, operand="B")
+    C = torch.empty((n, n), device=dev, dtype=out_dtype(w))
     mm = gemm_fn(w, dev)
     label = kernel_label(w, A, B, C)
     distributed = ctx.is_distributed

@@ -18,7 +18,7 @@ from ..ops import gemm as _gemm
 from ..parallel.dist import DistContext
 from ..utils.metrics import gemm_flops, tflops_from
 from ..utils.timing import time_loop_ms
-from .common import (ModeResult, Workload, align_ranks, gemm_fn, kernel_label, randn,
+from .common import (ModeResult, Workload, align_ranks, gemm_fn, kernel_label, out_dtype, randn,
                      sampled_relerr, warmup)
 
 
@@ -26,8 +26,8 @@ def run(w: Workload, ctx: DistContext, mode_name: str = "independent") -> ModeRe
     dev = ctx.device
     n = w.n
     A = randn((n, n), w, dev, seed=2 * (w.seed + ctx.rank))
-    B = randn((n, n), w, dev, seed=2 * (w.seed + ctx.rank) + 1)
-    C = torch.empty((n, n), device=dev, dtype=w.dtype)
+    B = randn((n, n), w, dev, seed=2 * (w.seed + ctx.rank) + 1, operand="B")
+    C = torch.empty((n, n), device=dev, dtype=out_dtype(w))
     mm = gemm_fn(w, dev)
     label = kernel_label(w, A, B, C)
 

@@ -31,8 +31,8 @@ from ..parallel.partition import column_shard, effective_chunks, row_chunks
 from ..utils.metrics import gemm_flops, tflops_from
 from ..utils.timing import SegmentTimer, Stopwatch, synchronize, time_loop_ms
 from . import independent
-from .common import (ModeResult, Workload, align_ranks, gemm_fn, kernel_label, randn,
-                     sampled_relerr, warmup)
+from .common import (ModeResult, Workload, align_ranks, gemm_fn, kernel_label, out_dtype, randn,
+                     sampled_relerr, warmup, zeros_b)
 
 
 def make_operands(w: Workload, ctx: DistContext):
@@ -40,8 +40,8 @@ def make_operands(w: Workload, ctx: DistContext):
     dev, n, ws = ctx.device, w.n, ctx.world_size
     sh = column_shard(n, ws, ctx.rank, align=8)
     A = randn((n, n), w, dev, seed=10_000 + w.seed)
-    Bg = randn((n, n), w, dev, seed=10_001 + w.seed)   # the one global B
-    B_local = torch.zeros((n, sh.padded), device=dev, dtype=w.dtype)
+    Bg = randn((n, n), w, dev, seed=10_001 + w.seed, operand="B")   # the one global B
+    B_local = zeros_b(n, sh.padded, w, dev)
     if sh.width:
         B_local[:, :sh.width].copy_(Bg[:, sh.start:sh.stop])
     del Bg
@@ -68,7 +68,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         return r
     dev, n = ctx.device, w.n
     A, B_local, sh = make_operands(w, ctx)
-    C_local = torch.empty((n, sh.padded), device=dev, dtype=w.dtype)
+    C_local = torch.empty((n, sh.padded), device=dev, dtype=out_dtype(w))
     mm = gemm_fn(w, dev)
     label = kernel_label(w, A, B_local, C_local)
     flops_local = gemm_flops(n, sh.padded, n)
@@ -78,7 +78,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     if not w.overlap:
         # dim-0 concatenation [ws*N, shard] (the layout both gloo and RCCL accept);
         # block r = gathered.view(ws, N, shard)[r] = C[:, r*shard:(r+1)*shard].
-        gathered = torch.empty((ws * n, sh.padded), device=dev, dtype=w.dtype)
+        gathered = torch.empty((ws * n, sh.padded), device=dev, dtype=out_dtype(w))
 
         def comm():
             dist.all_gather_into_tensor(gathered, C_local)
@@ -106,7 +106,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         rc = row_chunks(n, effective_chunks(n, sh.padded, w.chunks) if dev.type == "cuda"
                         else w.chunks)
         extra["chunks"] = len(rc)
-        bufs = [torch.empty((ws * (e - s), sh.padded), device=dev, dtype=w.dtype) for s, e in rc]
+        bufs = [torch.empty((ws * (e - s), sh.padded), device=dev, dtype=out_dtype(w)) for s, e in rc]
         cs = CommStream(dev)
         ready = [new_event(dev) for _ in rc]
         done = [new_event(dev) for _ in rc]
@@ -144,6 +144,6 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     if w.check:
         synchronize(dev)
         C = full()
-        Bg = randn((n, n), w, dev, seed=10_001 + w.seed)
+        Bg = randn((n, n), w, dev, seed=10_001 + w.seed, operand="B")
         res.relerr = sampled_relerr(A, Bg, C)
     return res

@@ -36,7 +36,7 @@ from ..parallel.dist import DistContext
 from ..utils.metrics import gemm_flops, tflops_from
 from ..utils.timing import Stopwatch, synchronize, time_loop_ms
 from .common import (ModeResult, Workload, align_ranks, allreduced_relerr, gemm_fn, kernel_label,
-                     randn, warmup)
+                     out_dtype, randn, warmup)
 
 DEPTH = {"no_overlap": 1, "overlap": 2, "pipeline": 3}
 
@@ -49,8 +49,8 @@ def run(w: Workload, ctx: DistContext, mode: str = "overlap", depth: int = None)
     dev, n, ws = ctx.device, w.n, ctx.world_size
     depth = DEPTH[mode] if depth is None else max(1, int(depth))
     As = [randn((n, n), w, dev, seed=100 * (w.seed + ctx.rank) + 2 * i) for i in range(depth)]
-    Bs = [randn((n, n), w, dev, seed=100 * (w.seed + ctx.rank) + 2 * i + 1) for i in range(depth)]
-    Cs = [torch.empty((n, n), device=dev, dtype=w.dtype) for _ in range(depth)]
+    Bs = [randn((n, n), w, dev, seed=100 * (w.seed + ctx.rank) + 2 * i + 1, operand="B") for i in range(depth)]
+    Cs = [torch.empty((n, n), device=dev, dtype=out_dtype(w)) for _ in range(depth)]
     mm = gemm_fn(w, dev)
     label = kernel_label(w, As[0], Bs[0], Cs[0])
     distributed = ctx.is_distributed

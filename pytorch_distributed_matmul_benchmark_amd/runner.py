@@ -29,6 +29,7 @@ import torch
 
 from .models import DISTRIBUTED_MODES, OVERLAP_MODES, SCALING_MODES, ModeResult, Workload, run_mode
 from .models.common import tolerance
+from .ops.gemm import out_dtype as _gemm_out_dtype
 from .parallel.dist import (DistContext, all_ok, barrier, cleanup_distributed, reduce_scalar,
                             setup_distributed, verify_collectives)
 from .utils.metrics import (balance_efficiency, bytes_per_element, dtype_from_name, dtype_name,
@@ -63,8 +64,9 @@ def build_parser(kind: str) -> argparse.ArgumentParser:
     p.add_argument("--warmup", type=int, default=10,
                    help="Number of warmup iterations (default: 10)")
     p.add_argument("--dtype", type=str, default="bfloat16",
-                   choices=["float32", "float16", "bfloat16"],
-                   help="Data type for matrices (default: bfloat16)")
+                   choices=["float32", "float16", "bfloat16", "float8_e4m3fn"],
+                   help="Data type for matrices (default: bfloat16; float8_e4m3fn: OCP e4m3 "
+                        "operands, bf16 output, on gfx950's block-scaled fp8 MFMA)")
     if kind != "basic":
         p.add_argument("--mode", type=str, default=k["default_mode"], choices=list(k["modes"]),
                        help=f"Benchmark mode (default: {k['default_mode']})")
@@ -319,7 +321,8 @@ def run_benchmarks(kind: str, ctx: DistContext, rep: Reporter, args) -> List[Dic
         rep.line(f"\nBenchmarking {n}x{n} matrix multiplication:")
         rep.line(f"  - Memory per matrix: {n * n * bpe / (1024 ** 3):.2f} GB ({dtype_name(dtype)})")
         if kind == "basic":
-            rep.line(f"  - Total memory for A, B, C: {3 * n * n * bpe / (1024 ** 3):.2f} GB")
+            obpe = bytes_per_element(_gemm_out_dtype(dtype))  # fp8 operands write a bf16 C
+            rep.line(f"  - Total memory for A, B, C: {(2 * bpe + obpe) * n * n / (1024 ** 3):.2f} GB")
         else:
             rep.line(f"  - Mode: {mode}")
         if kind in ("distributed", "overlap"):

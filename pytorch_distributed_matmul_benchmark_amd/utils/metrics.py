@@ -23,7 +23,9 @@ from typing import Optional
 
 import torch
 
-DTYPES = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16}
+DTYPES = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16,
+          # MI355X extension: OCP e4m3 operands, bf16 output (ops/csrc/gemm_fp8.hip)
+          "float8_e4m3fn": torch.float8_e4m3fn}
 DTYPE_NAMES = {v: k for k, v in DTYPES.items()}
 
 
@@ -69,14 +71,18 @@ class Peak:
     gpu: str
     half: float  # bf16 / fp16 dense TFLOPS
     fp32: float
+    fp8: Optional[float] = None  # e4m3 dense TFLOPS (None: not listed)
 
-    def for_dtype(self, dt: torch.dtype) -> float:
+    def for_dtype(self, dt: torch.dtype) -> Optional[float]:
+        if dt == torch.float8_e4m3fn:
+            return self.fp8
         return self.fp32 if dt == torch.float32 else self.half
 
 
 PEAKS = {
-    "mi355x": Peak("AMD Instinct MI355X", 2516.6, 157.3),
-    "mi350x": Peak("AMD Instinct MI350X", 2306.9, 144.2),
+    # fp8 dense = 2x bf16 (block-scaled 16x16x128 / 32x32x64 MFMA, MI355X_MICROARCH.md)
+    "mi355x": Peak("AMD Instinct MI355X", 2516.6, 157.3, 5033.2),
+    "mi350x": Peak("AMD Instinct MI350X", 2306.9, 144.2, 4613.7),
     "rtx6000ada": Peak("RTX 6000 Ada", 182.2, 91.1),
     "rx7900xtx": Peak("Radeon RX 7900 XTX", 123.0, 61.4),
 }
@@ -102,7 +108,7 @@ def peak_for_device(device_name: str, gcn_arch: Optional[str] = None) -> Optiona
 
 
 def percent_of_peak(tflops: float, peak: Optional[Peak], dt: torch.dtype) -> Optional[float]:
-    if peak is None:
+    if peak is None or not peak.for_dtype(dt):
         return None
     return 100.0 * tflops / peak.for_dtype(dt)
 

@@ -147,3 +147,17 @@ def test_scaling_ref_reports_efficiency_vs_one_rank(tmp_path):
     assert "Scaling efficiency vs 1 GPU:" in out
     rec = json.loads(js.read_text().splitlines()[-1])
     assert rec["single_gpu_tflops"] > 0 and rec["scaling_efficiency_vs_1gpu"] > 0
+
+
+def test_fp8_cli_cpu_and_gloo(tmp_path):
+    """--dtype float8_e4m3fn end to end: e4m3 operands (B column-major), bf16 C, float64
+    check of the same quantized values; single process and 2 gloo ranks with overlap."""
+    out = _run([sys.executable, os.path.join(ROOT, "matmul_benchmark.py"), "--device", "cpu",
+                "--sizes", "256", "--iterations", "2", "--warmup", "1",
+                "--dtype", "float8_e4m3fn", "--check"])
+    assert "Check: max rel. error" in out and "PASS" in out and "FAIL" not in out
+    for mode in ("batch_parallel", "matrix_parallel"):
+        out = _torchrun(2, "matmul_scaling_benchmark.py", "--device", "cpu", "--sizes", "300",
+                        "--iterations", "2", "--warmup", "1", "--dtype", "float8_e4m3fn",
+                        "--mode", mode, "--overlap", "--chunks", "2", "--check")
+        assert out.count("PASS") == 1 and "FAIL" not in out and "ERROR" not in out

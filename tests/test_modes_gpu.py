@@ -22,13 +22,13 @@ def _ctx():
 
 
 @pytest.mark.parametrize("mode", sorted(MODES))
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float8_e4m3fn])
 def test_mode_single_gpu(mode, dtype):
     w = Workload(n=1024, dtype=dtype, iters=3, warmup=1, check=True, batch=2)
     r = run_mode(mode, w, _ctx())
     assert r.relerr is not None and r.relerr < tolerance(dtype), r.relerr
     assert r.avg_ms > 0 and r.tflops > 0
-    assert r.kernel.startswith("pdmb_mfma256")
+    assert r.kernel.startswith("pdmb_fp8" if dtype == torch.float8_e4m3fn else "pdmb_mfma256")
 
 
 def test_fp32_independent_uses_exact_mfma():
