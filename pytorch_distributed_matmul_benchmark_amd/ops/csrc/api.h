@@ -20,6 +20,10 @@ enum Kernel : int {
   kMfma256X2 = 11,  //   11 = static priority of waves 4..7,
   kMfma256X4 = 13,  //   13 = XCD sub-block 8x4 (12 unused)
   kMfma256Stamp = 5,  // diagnostic: SCHED 2 with in-kernel barrier-wait stamps (needs a debug buffer)
+  kFp8W4 = 16,    // gemm_fp8.hip experiment: 4 waves x 128x128, AGPR accumulators via asm MFMA
+  kFp8W4Diag = 17,  // diagnostic: kFp8W4 without the DMA wait (timing only, wrong results)
+  kFp8W4Diag2 = 18,  // diagnostic: kFp8W4 with no wait at all before the barrier
+  kFp8W4Diag3 = 19,  // diagnostic: kFp8W4 MFMAs + barriers only (no loads)
   kFp8 = 15,      // gemm_fp8.hip: e4m3 A [M,K] x column-major B, block-scaled MFMA 16x16x128, bf16 out
 };
 

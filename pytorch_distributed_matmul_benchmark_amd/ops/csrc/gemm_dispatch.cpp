@@ -21,7 +21,7 @@ hipError_t gemm_generic_launch(int dt, GemmArgs a, bool vec, hipStream_t stream)
 bool gemm_f32_256_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 hipError_t gemm_f32_256_launch(GemmArgs a, int variant, hipStream_t stream);
 bool gemm_fp8_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
-hipError_t gemm_fp8_launch(GemmArgs a, hipStream_t stream);
+hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream);
 
 static unsigned long long* g_debug_buffer = nullptr;
 
@@ -60,11 +60,14 @@ static bool generic_vec_ok(const Problem& p) {
 int resolve_kernel(const Problem& p, int kernel) {
   const GemmArgs a = to_args(p);
   if (p.dtype == kFP8)  // one kernel, no generic / padded fallback
-    return (kernel == kAuto || kernel == kFp8) &&
+    return (kernel == kAuto || kernel == kFp8 || kernel == kFp8W4 || kernel == kFp8W4Diag ||
+                    kernel == kFp8W4Diag2 || kernel == kFp8W4Diag3) &&
                    gemm_fp8_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C)
-               ? kFp8
+               ? (kernel == kAuto ? kFp8W4 : kernel)
                : -1;
-  if (kernel == kFp8) return -1;
+  if (kernel == kFp8 || kernel == kFp8W4 || kernel == kFp8W4Diag || kernel == kFp8W4Diag2 ||
+      kernel == kFp8W4Diag3)
+    return -1;
   const bool fast = gemm256_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   const bool f32fast = p.dtype == kF32 &&
                        gemm_f32_256_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
@@ -255,7 +258,11 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     }
     return hipSuccess;
   }
-  if (k == kFp8) return gemm_fp8_launch(a, stream);
+  if (k == kFp8) return gemm_fp8_launch(a, 0, stream);
+  if (k == kFp8W4) return gemm_fp8_launch(a, 1, stream);
+  if (k == kFp8W4Diag) return gemm_fp8_launch(a, 9, stream);
+  if (k == kFp8W4Diag2) return gemm_fp8_launch(a, 10, stream);
+  if (k == kFp8W4Diag3) return gemm_fp8_launch(a, 11, stream);
   if (k == kMfma256) return gemm256_launch(p.dtype, a, 0, stream);
   if (k == kMfma256b) return gemm256_launch(p.dtype, a, 1, stream);
   if (k == kMfma256c) return gemm256_launch(p.dtype, a, 2, stream);
@@ -336,6 +343,8 @@ const char* kernel_name(int kernel) {
       return "pdmb_f32_256s_nn";
     case kFp8:
       return "pdmb_fp8_256_nt";
+    case kFp8W4:
+      return "pdmb_fp8_w4_nt";
     default:
       return "auto";
   }

@@ -272,6 +272,261 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_fp8_nt(GemmArgs a) {
   }
 }
 
+
+// ---- W4 (default): 4 waves, one per SIMD, 128x128 output per wave --------
+// The 8-wave kernel above reads 192 KiB of LDS fragments per K-tile; with
+// 128x128 per wave a workgroup reads 128 KiB (each A / B fragment is shared
+// by 2 waves, not 4 / 2), the LDS energy that kept hipBLASLt's fp8 kernel
+// ~5 % higher in clock (profiles/r1_s3_pmc_fp8.md). 256 fp32 accumulators
+// per lane live in AGPRs: the MFMA is issued by inline asm with "+a"
+// operands, since with the builtin hipcc shuffles and spills them
+// (profiles/r1_fp32_ablation.md). What it took (each step measured, 16k):
+//  * every load in an MFMA's shadow, about one per 32-cycle gap (kW4Items):
+//    loads issued back to back after each m-block's MFMAs left the MFMA pipe
+//    idle — 66 % utilisation, 2750 TF;
+//  * ~1.5 K-tiles of LDS-DMA flight: B of tile t+1 is read in m-blocks 0-3 and
+//    A in 4-7, with a second barrier between, so each operand half is
+//    refilled half a K-tile after its last read (one K-tile of flight cost
+//    17 %, measured with a no-wait diagnostic build);
+//  * LDS-DMA pieces that clobber M0 instead of saving / restoring it, and one
+//    base VGPR per stage so fragment reads need no address adds: 3157 → 3217 TF.
+// 3217 TF vs 3079 for the 8-wave kernel (hipBLASLt 3343).
+constexpr int NT4 = 256;
+constexpr int STAGE4 = 2 * A_BYTES;  // A [256][128 B] + Bt [256][128 B]
+
+__device__ __forceinline__ void mfma_f8_acc(f32x4& acc, const i32x8& a, const i32x8& b, int sc) {
+  asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0]"
+               : "+a"(acc)
+               : "v"(a), "v"(b), "v"(sc));
+}
+
+// LDS-DMA with a scalar offset (the 8 pieces of one operand differ by 32 rows).
+__device__ __forceinline__ void dma16_so(u32x4 rsrc, uint32_t voff, uint32_t soff, uint32_t lds) {
+  unsigned int keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %4\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds)
+      : "memory");
+}
+
+// As dma16_so, but M0 is simply clobbered (declared to hipcc) instead of
+// saved and restored around every piece: 3 instructions per piece, not 5.
+__device__ __forceinline__ void dma16_m0(u32x4 rsrc, uint32_t voff, uint32_t soff, uint32_t lds) {
+  asm volatile(
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %0, %1, %2 offen lds"
+      :
+      : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds)
+      : "memory", "m0");
+}
+
+struct Ctx4 {
+  u32x4 ra, rb;       // buffer descriptors at K = 0
+  int lda, ldb, nk;
+  uint32_t voffA, voffB;  // per-lane DMA offsets of piece 0
+  // Per-lane LDS fragment offsets [stage][16-B chunk h], B's including A_BYTES;
+  // one VGPR per (stage, h) so every fragment read is ds_read_b128 off:imm
+  // with no address add (the immediate field stops at 64 KiB = one stage).
+  uint32_t aoff[2][2], boff[2][2];
+  int wu;
+  uint32_t lds0;
+};
+
+// DMA piece h (0..15) of tile `tile` into stage `so`: h < 8 -> A rows
+// (h*4+wu)*8 + [0,8), else Bt rows ((h-8)*4+wu)*8 + [0,8).
+__device__ __forceinline__ void issue_piece(const Ctx4& c, int so, int tile, int h) {
+  const uint32_t koff = (uint32_t)tile * BK;
+  if (h < 8)
+    dma16_m0(c.ra, c.voffA, koff + (uint32_t)(h * 32 * c.lda),
+             c.lds0 + so + (h * 4 + c.wu) * 8 * BK);
+  else
+    dma16_m0(c.rb, c.voffB, koff + (uint32_t)((h - 8) * 32 * c.ldb),
+             c.lds0 + so + A_BYTES + ((h - 8) * 4 + c.wu) * 8 * BK);
+}
+
+__device__ __forceinline__ i32x8 frag(const char* p, const uint32_t (&off)[2]) {
+  return join(*(const lds_u32x4*)(p + off[0]), *(const lds_u32x4*)(p + off[1]));
+}
+
+// What a wave issues in MFMA gap `gap` of m-block `blk`. With one wave per
+// SIMD a load must sit in an MFMA's shadow (~one per 32-cycle gap) or it
+// delays the next MFMA: loads issued back to back after each m-block's MFMAs
+// ran at 66 % MFMA utilisation. 0: nothing; 1: next LDS-DMA piece (blocks
+// 0-3: A of tile t+2, blocks 4-7: B of tile t+3); 10+s: B fragment s of tile
+// t+1; 20+m: A fragment m of tile t+1 (27: into the second A7 set).
+constexpr int kW4Items[8][8] = {
+    {10, 1, 11, 1, 0, 0, 0, 0}, {12, 1, 13, 1, 0, 0, 0, 0}, {14, 1, 15, 1, 0, 0, 0, 0},
+    {16, 1, 17, 1, 0, 0, 0, 0}, {20, 1, 21, 1, 0, 0, 0, 0}, {22, 1, 23, 1, 0, 0, 0, 0},
+    {24, 1, 25, 1, 27, 0, 0, 0}, {26, 1, 1, 0, 0, 0, 0, 0}};
+
+constexpr int w4_piece(int blk, int gap) {  // running index of a DMA item (0..15)
+  int n = 0;
+  for (int b = 0; b < 8; ++b)
+    for (int g = 0; g < 8; ++g) {
+      if (b == blk && g == gap) return n;
+      if (kW4Items[b][g] == 1) ++n;
+    }
+  return n;
+}
+
+// One K-tile t (stage S = SO, tile t+1 in SN = S^1), two barriers:
+//   Bar0: B(t+1) landed (vmcnt 16: A(t+1), B(t+2) may still fly); every wave
+//         finished reading A(t) from S.A in K-tile t-1 (lgkmcnt 0).
+//   blocks 0-3: MFMAs of tile t | read B(t+1) from S^1.B | DMA A(t+2) -> S.A
+//   Bar_mid: A(t+1) landed (vmcnt 16: B(t+2), A(t+2) may fly); every wave
+//         finished reading B(t+1) from S^1.B.
+//   blocks 4-7: MFMAs | read A(t+1) from S^1.A | DMA B(t+3) -> S^1.B
+// Each operand half thus gets ~1.5 K-tiles of DMA flight (one K-tile was not
+// enough: the same kernel without the DMA wait ran 17 % faster).
+template <int SO, int DIAG_NOWAIT = 0>
+__device__ __forceinline__ void ktile_w4(const Ctx4& c, const char* smem, int t, f32x4 (&acc)[8][8],
+                                         i32x8 (&A)[8], i32x8& A7c, i32x8& A7n, i32x8 (&Bc)[8],
+                                         i32x8 (&Bn)[8], int sc) {
+  constexpr int SN = STAGE4 - SO;  // stage of tile t+1
+  const int ta = t + 2 < c.nk ? t + 2 : c.nk - 1;  // clamped tail DMAs (harmless re-reads)
+  const int tb = t + 3 < c.nk ? t + 3 : c.nk - 1;
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    if (mi == 0 || mi == 4) {
+      if constexpr (DIAG_NOWAIT == 1)  // timing-only diagnostic: never wait for the DMA
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else if constexpr (DIAG_NOWAIT == 2)  // timing-only diagnostic: no waits, no barriers
+        asm volatile("" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int ni = 0; ni < 8; ++ni) {
+      mfma_f8_acc(acc[mi][ni], Bc[ni], mi == 7 ? A7c : A[mi], sc);
+      if constexpr (DIAG_NOWAIT != 3) {  // 3: timing-only, MFMAs + barriers alone
+        const int it = kW4Items[mi][ni];
+        if (it == 1) {
+          const int h = w4_piece(mi, ni);  // 0..7: A of t+2 into S; 8..15: B of t+3 into S^1
+          if (h < 8)
+            issue_piece(c, SO, ta, h);
+          else
+            issue_piece(c, SN, tb, h);
+        } else if (it >= 10 && it < 20) {
+          Bn[it - 10] = frag(smem + (it - 10) * 16 * BK, c.boff[SN / STAGE4]);
+        } else if (it == 27) {
+          A7n = frag(smem + 7 * 16 * BK, c.aoff[SN / STAGE4]);
+        } else if (it >= 20) {
+          A[it - 20] = frag(smem + (it - 20) * 16 * BK, c.aoff[SN / STAGE4]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+template <int DIAG_NOWAIT>
+__global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4(GemmArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE4];
+
+  int bz, tm, tn;
+  map_tile(a, blockIdx.x, bz, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int lane = threadIdx.x & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wu >> 1, wc = wu & 1;
+  const int l16 = lane & 15, g = lane >> 4;
+
+  Ctx4 c;
+  c.wu = wu;
+  c.lds0 = (uint32_t)(size_t)((lds_void*)smem);
+  c.lda = a.lda;
+  c.ldb = a.ldb;
+  c.nk = a.K / BK;
+  const char* Ab = (const char*)a.A + (long long)bz * a.sA + (long long)m0 * a.lda;
+  const char* Bb = (const char*)a.B + (long long)bz * a.sB + (long long)n0 * a.ldb;
+  c.ra = make_rsrc(Ab, (long long)(a.M - m0 - 1) * a.lda + a.K);
+  c.rb = make_rsrc(Bb, (long long)(a.N - n0 - 1) * a.ldb + a.K);
+  {
+    const int r = wu * 8 + (lane >> 3), lc8 = lane & 7;  // row of piece 0 (swz(r + 32h) = swz(r))
+    c.voffA = (uint32_t)(r * a.lda + ((lc8 ^ swz(r)) * 16));
+    c.voffB = (uint32_t)(r * a.ldb + ((lc8 ^ swz(r)) * 16));
+    const int sw = swz(l16);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        uint32_t ao = (uint32_t)(st * STAGE4 + (wr * 128 + l16) * BK + (((2 * g + h) ^ sw) * 16));
+        uint32_t bo = (uint32_t)(st * STAGE4 + A_BYTES + (wc * 128 + l16) * BK +
+                                 (((2 * g + h) ^ sw) * 16));
+        asm volatile("" : "+v"(ao), "+v"(bo));  // opaque: keep each as its own base VGPR
+        c.aoff[st][h] = ao;
+        c.boff[st][h] = bo;
+      }
+    }
+  }
+  const int sc = __builtin_amdgcn_readfirstlane(kScaleOne);
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Prologue, in the DMA order the loop's counted waits assume:
+  // A(0), B(0) -> stage 0; B(1), A(1) -> stage 1; tile 0's fragments to
+  // registers; then B(2) -> stage 0.B (the loop's "Bar_mid(-1)" issue).
+  const int nk = c.nk;
+  const int t1 = nk > 1 ? 1 : 0, t2 = nk > 2 ? 2 : nk - 1;
+#pragma unroll
+  for (int h = 0; h < 16; ++h) issue_piece(c, 0, 0, h);
+#pragma unroll
+  for (int h = 8; h < 16; ++h) issue_piece(c, STAGE4, t1, h);
+#pragma unroll
+  for (int h = 0; h < 8; ++h) issue_piece(c, STAGE4, t1, h);
+  asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");  // tile 0 landed everywhere
+  i32x8 A[8], A7a, A7b, B0[8], B1[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    A[i] = frag(smem + i * 16 * BK, c.aoff[0]);
+    B0[i] = frag(smem + i * 16 * BK, c.boff[0]);
+  }
+  A7a = A[7];
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // stage 0.B read by all
+#pragma unroll
+  for (int h = 8; h < 16; ++h) issue_piece(c, 0, t2, h);
+  int t = 0;
+  for (; t + 1 < nk; t += 2) {  // branch-free body: B0/B1 and A7a/A7b swap roles every K-tile
+    ktile_w4<0, DIAG_NOWAIT>(c, smem, t, acc, A, A7a, A7b, B0, B1, sc);
+    ktile_w4<STAGE4, DIAG_NOWAIT>(c, smem, t + 1, acc, A, A7b, A7a, B1, B0, sc);
+  }
+  if (t < nk) ktile_w4<0, DIAG_NOWAIT>(c, smem, t, acc, A, A7a, A7b, B0, B1, sc);  // odd count
+  // Drain the tail DMAs and give the last MFMAs time to write their AGPRs
+  // (asm MFMAs are invisible to hipcc's hazard recognizer).
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+
+  const float alpha = a.alpha;
+  char* Cb = (char*)a.C + (long long)bz * a.sC * 2;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = m0 + wr * 128 + i * 16 + l16;
+    if (row < a.M) {
+      char* crow = Cb + (long long)row * a.ldc * 2;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int col = n0 + wc * 128 + j * 16 + 4 * g;
+        if (col < a.N) {
+          u32x2 v;
+          v.x = pack2<kBF16>(acc[i][j].x * alpha, acc[i][j].y * alpha);
+          v.y = pack2<kBF16>(acc[i][j].z * alpha, acc[i][j].w * alpha);
+          *(u32x2*)(crow + col * 2) = v;
+        }
+      }
+    }
+  }
+}
+
 }  // namespace k8
 
 bool gemm_fp8_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c) {
@@ -285,14 +540,23 @@ bool gemm_fp8_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_
   return true;
 }
 
-hipError_t gemm_fp8_launch(GemmArgs a, hipStream_t stream) {
+hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream) {
   a.tiles_m = (a.M + k8::BM - 1) / k8::BM;
   a.tiles_n = (a.N + k8::BN - 1) / k8::BN;
   a.supertile = (a.tiles_m % 16 == 0 && a.tiles_n % 16 == 0) ? 1 : 0;
   const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch;
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k8::gemm_fp8_nt, dim3((unsigned)nblocks), dim3(k8::NTHREADS), 0, stream, a);
+  if (variant == 1)
+    hipLaunchKernelGGL(k8::gemm_fp8_w4<0>, dim3((unsigned)nblocks), dim3(k8::NT4), 0, stream, a);
+  else if (variant == 9)
+    hipLaunchKernelGGL(k8::gemm_fp8_w4<1>, dim3((unsigned)nblocks), dim3(k8::NT4), 0, stream, a);
+  else if (variant == 10)
+    hipLaunchKernelGGL(k8::gemm_fp8_w4<2>, dim3((unsigned)nblocks), dim3(k8::NT4), 0, stream, a);
+  else if (variant == 11)
+    hipLaunchKernelGGL(k8::gemm_fp8_w4<3>, dim3((unsigned)nblocks), dim3(k8::NT4), 0, stream, a);
+  else
+    hipLaunchKernelGGL(k8::gemm_fp8_nt, dim3((unsigned)nblocks), dim3(k8::NTHREADS), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -30,9 +30,13 @@ def main():
     dt = getattr(torch, a.dtype)
     for n in a.sizes:
         torch.manual_seed(0)
-        A = torch.randn(n, n, device="cuda", dtype=dt)
-        B = torch.randn(n, n, device="cuda", dtype=dt)
-        C = torch.empty(n, n, device="cuda", dtype=dt)
+        if dt == torch.float8_e4m3fn:  # e4m3 operands (scale 1), B column-major, bf16 C
+            A, _ = gemm.fp8_quantize(torch.randn(n, n, device="cuda"))
+            B, _ = gemm.fp8_quantize(torch.randn(n, n, device="cuda"), colmajor=True)
+        else:
+            A = torch.randn(n, n, device="cuda", dtype=dt)
+            B = torch.randn(n, n, device="cuda", dtype=dt)
+        C = torch.empty(n, n, device="cuda", dtype=gemm.out_dtype(dt))
         ref = gemm.matmul(A, B, kernel=ks[0])
         R = torch.matmul(A.float(), B.float())
         res = {k: [] for k in ks}

@@ -24,12 +24,13 @@ def _relerr(x, ref):
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 256), (1000, 1052, 384),
-                                   (300, 200, 128), (2304, 2048, 1024)])
+                                   (300, 200, 128), (2304, 2048, 1024), (256, 512, 256),
+                                   (768, 256, 640)])
 def test_fp8_exact_small_integers(M, N, K):
     g = torch.Generator(device="cuda").manual_seed(M + 7 * N + K)
     Af, Bf = _ints((M, K), g), _ints((K, N), g)
     A8, B8 = Af.to(FP8), _colmajor(Bf.to(FP8))
-    assert gemm.kernel_for(A8, B8) == "pdmb_fp8_256_nt"
+    assert gemm.kernel_for(A8, B8) == "pdmb_fp8_w4_nt"
     C = gemm.matmul(A8, B8)
     assert C.dtype == torch.bfloat16 and C.shape == (M, N)
     ref = (Af.double() @ Bf.double()).to(torch.bfloat16)
@@ -84,13 +85,25 @@ def test_fp8_batched_and_column_shards():
         assert torch.equal(C, ref)
 
 
-def test_fp8_race_screen():
+@pytest.mark.parametrize("kernel", ["fp8_w4", "fp8"])
+def test_fp8_race_screen(kernel):
     torch.manual_seed(11)
     A8, sa = gemm.fp8_quantize(torch.randn(4096, 4096, device="cuda"))
     B8, sb = gemm.fp8_quantize(torch.randn(4096, 4096, device="cuda"), colmajor=True)
-    ref = gemm.matmul(A8, B8, alpha=sa * sb)
+    ref = gemm.matmul(A8, B8, alpha=sa * sb, kernel=kernel)
+    assert _relerr(ref, (A8.double() * sa) @ (B8.double() * sb)) < 8e-3
     for _ in range(20):
-        assert torch.equal(gemm.matmul(A8, B8, alpha=sa * sb), ref)
+        assert torch.equal(gemm.matmul(A8, B8, alpha=sa * sb, kernel=kernel), ref)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (1000, 1052, 384), (2304, 2048, 1024),
+                                   (512, 512, 384)])
+def test_fp8_8wave_kernel_exact(M, N, K):
+    """The 8-wave SCHED-3 fp8 kernel (kept for A/B) on the exact-integer cases."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    Af, Bf = _ints((M, K), g), _ints((K, N), g)
+    C = gemm.matmul(Af.to(FP8), _colmajor(Bf.to(FP8)), kernel="fp8")
+    assert torch.equal(C, (Af.double() @ Bf.double()).to(torch.bfloat16))
 
 
 def test_fp8_unsupported_shape_fails_loudly():
