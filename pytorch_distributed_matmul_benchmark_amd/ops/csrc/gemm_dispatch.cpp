@@ -22,6 +22,8 @@ bool gemm_f32_256_supported(const GemmArgs& a, size_t align_a, size_t align_b, s
 hipError_t gemm_f32_256_launch(GemmArgs a, int variant, hipStream_t stream);
 bool gemm_fp8_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream);
+bool gemm_w4_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
+hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream);
 
 static unsigned long long* g_debug_buffer = nullptr;
 
@@ -71,7 +73,12 @@ int resolve_kernel(const Problem& p, int kernel) {
   const bool fast = gemm256_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   const bool f32fast = p.dtype == kF32 &&
                        gemm_f32_256_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
-  if (kernel == kAuto) return fast ? kMfma256d : (f32fast ? kF32_256s : kGeneric);
+  // Auto: the 4-wave kernel where the tiles are whole (M, N % 256; +4.5 % over
+  // SCHED 3 at 16k, profiles/r1_s4_w4_ab.jsonl), SCHED 3 for edge tiles.
+  if (kernel == kAuto) {
+    if (fast && gemm_w4_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C)) return kMfmaW4;
+    return fast ? kMfma256d : (f32fast ? kF32_256s : kGeneric);
+  }
   if (kernel == kF32_256) return f32fast ? kF32_256 : -1;
   if (kernel >= kMfma256X1 && kernel <= kMfma256X4)
     return (fast && p.dtype == kBF16) ? kernel : -1;
@@ -81,6 +88,8 @@ int resolve_kernel(const Problem& p, int kernel) {
   if (kernel == kMfma256b) return fast ? kMfma256b : -1;
   if (kernel == kMfma256c) return fast ? kMfma256c : -1;
   if (kernel == kMfma256d) return fast ? kMfma256d : -1;
+  if (kernel == kMfmaW4)
+    return gemm_w4_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C) ? kMfmaW4 : -1;
   if (kernel == kMfma256Stamp) return (fast && p.dtype == kBF16) ? kMfma256Stamp : -1;
   if (kernel == kGeneric) return kGeneric;
   return -1;
@@ -229,7 +238,9 @@ static hipError_t gemm_padded(const Problem& p, hipStream_t stream, int* used) {
   if (used) *used = k;
   if (k == kGeneric || k < 0) return hipErrorInvalidValue;  // cannot happen: q is aligned
   GemmArgs a = to_args(q);
-  e = k == kF32_256s ? gemm_f32_256_launch(a, 1, stream) : gemm256_launch(q.dtype, a, 4, stream);
+  e = k == kF32_256s  ? gemm_f32_256_launch(a, 1, stream)
+      : k == kMfmaW4 ? gemm_w4_launch(q.dtype, a, stream)
+                     : gemm256_launch(q.dtype, a, 4, stream);
   if (e != hipSuccess) return e;
   for (int b = 0; b < batch; ++b) {
     char* C = (char*)p.C + (size_t)b * p.sC * es;
@@ -267,6 +278,7 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
   if (k == kMfma256b) return gemm256_launch(p.dtype, a, 1, stream);
   if (k == kMfma256c) return gemm256_launch(p.dtype, a, 2, stream);
   if (k == kMfma256d) return gemm256_launch(p.dtype, a, 4, stream);
+  if (k == kMfmaW4) return gemm_w4_launch(p.dtype, a, stream);
   if (k == kMfma256Stamp) return gemm256_launch(p.dtype, a, 3, stream);
   if (k == kF32_256) return gemm_f32_256_launch(a, 0, stream);
   if (k >= kMfma256X1 && k <= kMfma256X4) return gemm256_launch(p.dtype, a, 10 + (k - kMfma256X1 + 1), stream);
@@ -345,6 +357,8 @@ const char* kernel_name(int kernel) {
       return "pdmb_fp8_256_nt";
     case kFp8W4:
       return "pdmb_fp8_w4_nt";
+    case kMfmaW4:
+      return "pdmb_w4_nn";
     default:
       return "auto";
   }

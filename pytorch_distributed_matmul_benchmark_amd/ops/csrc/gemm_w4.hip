@@ -1,0 +1,333 @@
+// gemm_w4.hip — bf16 / fp16 C = A @ B (row-major NN, fp32 accumulate) with
+// 4 waves per workgroup, one per SIMD, each owning a 128x128 output block
+// (256 fp32 accumulators per lane in AGPRs).
+//
+// Same job as gemm_mfma256.hip (the GEMM behind the reference's torch.matmul /
+// torch.bmm, matmul_scaling_benchmark.py:79,92,120,142,188,211), with the
+// structure that took the fp8 kernel from 3079 to 3217 TF (gemm_fp8.hip
+// "W4"): the 8-wave kernel reads 192 KiB of LDS fragments per 256x256x64
+// K-tile (every A fragment by 4 waves, every B fragment by 2); with 128x128
+// per wave a workgroup reads 128 KiB (each by 2). On random bf16 data the
+// chip is power-bound (profiles/r1_pmc_sched3.md: 1.75 GHz at 77 % MFMA
+// utilisation), so LDS energy is clock.
+//
+// The LDS images are the 8-wave kernel's, byte for byte (A: [256 rows][128 B]
+// with 16-B chunk c at c ^ ((row>>1)&7); B: two halves [64 k][256 B] with
+// 32-B unit u at u ^ ((k&3) | ((k>>3)&1)<<2), read by ds_read_b64_tr_b16), so
+// the conflict-free read patterns carry over. Only the DMA split (16 pieces of
+// 1 KiB per wave per K-tile) and the per-wave fragment offsets change.
+//
+// Schedule (per K-tile t from stage S, tile t+1 in S^1; gemm_fp8.hip ktile_w4):
+//   Bar0: B(t+1) landed (vmcnt 16), every wave done reading A(t) (lgkmcnt 0).
+//   m-blocks 0-3: 64 MFMAs | read B(t+1) fragments | DMA A(t+2) -> S.A
+//   Bar_mid: A(t+1) landed, every wave done reading B(t+1) from S^1.B.
+//   m-blocks 4-7: 64 MFMAs | read A(t+1) fragments | DMA B(t+3) -> S^1.B
+// Every load sits in the shadow of an MFMA (one item per 16-cycle
+// v_mfma_f32_16x16x32 gap at most, kItems), and each operand half gets
+// ~1.5 K-tiles of DMA flight.
+//
+// Fast-path constraints (host-checked; otherwise the 8-wave kernel): M and N
+// multiples of 256 (interior tiles only: no edge masking, no out-of-extent
+// DMA), K % 64 == 0, lda / ldb % 8 == 0, ldc % 4 == 0, 16-B aligned A / B,
+// 8-B aligned C.
+#include "common.h"
+
+namespace pdmb {
+namespace kw4 {
+
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int NT = 256;
+constexpr int A_BYTES = BM * BK * 2;         // 32 KiB
+constexpr int BH_BYTES = BK * (BN / 2) * 2;  // 16 KiB per B half
+constexpr int STAGE = A_BYTES + 2 * BH_BYTES;  // 64 KiB
+
+// 16 fp32 accumulators x K = 32 per lane, operands swapped (B fragment
+// first) so the accumulator holds C^T and a lane owns 4 consecutive columns.
+template <int DT>
+__device__ __forceinline__ void mfma_acc(f32x4& acc, const s16x8& b, const s16x8& a);
+template <>
+__device__ __forceinline__ void mfma_acc<kBF16>(f32x4& acc, const s16x8& b, const s16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+}
+template <>
+__device__ __forceinline__ void mfma_acc<kF16>(f32x4& acc, const s16x8& b, const s16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+}
+
+// LDS-DMA with a scalar offset; M0 is clobbered (declared), not saved.
+__device__ __forceinline__ void dma16_m0(u32x4 rsrc, uint32_t voff, uint32_t soff, uint32_t lds) {
+  asm volatile(
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %0, %1, %2 offen lds"
+      :
+      : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds)
+      : "memory", "m0");
+}
+
+struct Frag {  // one 16-row (A) or 16-column (B) block of a K-tile: k 0..31 and 32..63
+  s16x8 k[2];
+};
+
+struct Ctx {
+  u32x4 ra;             // A descriptor at K = 0
+  const char* Bb;       // B at row 0, column n0
+  long long b_bytes;    // bytes from Bb to the end of B's extent
+  int lda2, ldb2, nk;   // leading dims in bytes, K / 64
+  uint32_t voffA, voffB;  // per-lane DMA offsets of piece 0
+  // Per-lane LDS fragment offsets, one VGPR per stage so every read is
+  // ds_read off:imm with no address add (the immediate stops at 64 KiB).
+  uint32_t aoff[2][2];  // [stage][ks]
+  uint32_t boff[2][4];  // [stage][jj]: B block j uses jj = 2 * (j >> 2) + (j & 1)
+  int wu;
+  uint32_t lds0;
+};
+
+// DMA piece h (0..15) of tile `tile` into the stage at byte offset `so`.
+// h < 8: A rows h*32 + wu*8 + [0,8) (8 x 128 B). h >= 8: B half nq = (h-8)>>2,
+// k rows kb*16 + wu*4 + [0,4) with kb = (h-8)&3 (4 x 256 B). B's swizzle
+// depends on k & 11 only, which kb*16 leaves alone, so one per-lane offset
+// serves all pieces; nq shifts the source by 32 columns (64 B).
+__device__ __forceinline__ void issue_piece(const Ctx& c, u32x4 rb, int so, int tile, int h) {
+  if (h < 8) {
+    dma16_m0(c.ra, c.voffA, (uint32_t)tile * (BK * 2) + (uint32_t)(h * 32 * c.lda2),
+             c.lds0 + so + (h * 32 + c.wu * 8) * 128);
+  } else {
+    const int nq = (h - 8) >> 2, kb = (h - 8) & 3;
+    dma16_m0(rb, c.voffB, (uint32_t)(kb * 16 * c.ldb2 + nq * 64),
+             c.lds0 + so + A_BYTES + nq * BH_BYTES + (kb * 16 + c.wu * 4) * 256);
+  }
+}
+
+__device__ __forceinline__ u32x4 b_rsrc(const Ctx& c, int tile) {
+  const long long off = (long long)tile * BK * c.ldb2;
+  return make_rsrc(c.Bb + off, c.b_bytes - off);
+}
+
+// A fragment half ks of block m (rows 16m..16m+15 of this wave's 128).
+__device__ __forceinline__ s16x8 frag_a(const char* smem, uint32_t off, int m) {
+  return *(const lds_s16x8*)(smem + m * 16 * 128 + off);
+}
+
+// B fragment half ks of block j (16 output columns): two transposed reads.
+__device__ __forceinline__ s16x8 frag_b(const char* smem, uint32_t off, int j, int ks) {
+  const char* p = smem + A_BYTES + ((j >> 1) & 1) * BH_BYTES + ks * 32 * 256 + off;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p + 4 * 256));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// What a wave issues after MFMA `gap` (0..15: ks*8 + ni) of m-block `blk`.
+// 0: nothing; 1: next DMA piece (blocks 0-3: A of t+2, blocks 4-7: B of
+// t+3); 100 + 2s + ks: half ks of B fragment s of tile t+1; 200 + 2m + ks:
+// half ks of A fragment m of tile t+1 (m = 7: into the second A7 set).
+// A fragment m of t+1 is written only after block m of t is done with it.
+constexpr int kItems[8][16] = {
+    {100, 0, 101, 0, 1, 0, 102, 0, 103, 0, 1, 0, 0, 0, 0, 0},
+    {104, 0, 105, 0, 1, 0, 106, 0, 107, 0, 1, 0, 0, 0, 0, 0},
+    {108, 0, 109, 0, 1, 0, 110, 0, 111, 0, 1, 0, 0, 0, 0, 0},
+    {112, 0, 113, 0, 1, 0, 114, 0, 115, 0, 1, 0, 0, 0, 0, 0},
+    {200, 0, 201, 0, 1, 0, 202, 0, 203, 0, 1, 0, 0, 0, 0, 0},
+    {204, 0, 205, 0, 1, 0, 206, 0, 207, 0, 1, 0, 0, 0, 0, 0},
+    {208, 0, 209, 0, 1, 0, 210, 0, 211, 0, 1, 0, 214, 0, 215, 0},
+    {212, 0, 213, 0, 1, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0}};
+
+constexpr int piece_of(int blk, int gap) {  // running index of a DMA item (0..15)
+  int n = 0;
+  for (int b = 0; b < 8; ++b)
+    for (int g = 0; g < 16; ++g) {
+      if (b == blk && g == gap) return n;
+      if (kItems[b][g] == 1) ++n;
+    }
+  return n;
+}
+
+template <int DT, int SO>
+__device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, f32x4 (&acc)[8][8],
+                                      Frag (&A)[8], Frag& A7c, Frag& A7n, Frag (&Bc)[8],
+                                      Frag (&Bn)[8]) {
+  constexpr int SN = STAGE - SO;  // stage of tile t+1
+  constexpr int sn = SN / STAGE;
+  const int ta = t + 2 < c.nk ? t + 2 : c.nk - 1;  // clamped tail DMAs (harmless re-reads)
+  const int tb = t + 3 < c.nk ? t + 3 : c.nk - 1;
+  const u32x4 rb = b_rsrc(c, tb);
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    if (mi == 0 || mi == 4) {
+      asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int gap = 0; gap < 16; ++gap) {
+      const int ks = gap >> 3, ni = gap & 7;
+      mfma_acc<DT>(acc[mi][ni], Bc[ni].k[ks], mi == 7 ? A7c.k[ks] : A[mi].k[ks]);
+      const int it = kItems[mi][gap];
+      if (it == 1) {
+        const int h = piece_of(mi, gap);  // 0..7: A of t+2 into S; 8..15: B of t+3 into S^1
+        if (h < 8)
+          issue_piece(c, rb, SO, ta, h);
+        else
+          issue_piece(c, rb, SN, tb, h);
+      } else if (it >= 100 && it < 200) {
+        const int s = (it - 100) >> 1, h = (it - 100) & 1;
+        Bn[s].k[h] = frag_b(smem, c.boff[sn][2 * (s >> 2) + (s & 1)], s, h);
+      } else if (it >= 214) {
+        const int h = it - 214;
+        A7n.k[h] = frag_a(smem, c.aoff[sn][h], 7);
+      } else if (it >= 200) {
+        const int m = (it - 200) >> 1, h = (it - 200) & 1;
+        A[m].k[h] = frag_a(smem, c.aoff[sn][h], m);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(NT, 1) gemm_w4_nn(GemmArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  int bz, tm, tn;
+  map_tile(a, blockIdx.x, bz, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int lane = threadIdx.x & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wu >> 1, wc = wu & 1;
+  const int l16 = lane & 15, g = lane >> 4;
+
+  Ctx c;
+  c.wu = wu;
+  c.lds0 = (uint32_t)(size_t)((lds_void*)smem);
+  c.lda2 = a.lda * 2;
+  c.ldb2 = a.ldb * 2;
+  c.nk = a.K / BK;
+  const char* Ab = (const char*)a.A + ((long long)bz * a.sA + (long long)m0 * a.lda) * 2;
+  c.ra = make_rsrc(Ab, ((long long)(a.M - m0 - 1) * a.lda + a.K) * 2);
+  c.Bb = (const char*)a.B + ((long long)bz * a.sB + n0) * 2;
+  c.b_bytes = ((long long)(a.K - 1) * a.ldb + (a.N - n0)) * 2;
+  {
+    const int r = wu * 8 + (lane >> 3), lc8 = lane & 7;  // row of A piece 0
+    c.voffA = (uint32_t)(r * c.lda2 + ((lc8 ^ ((r >> 1) & 7)) * 16));
+    const int lr16 = lane >> 4, lc16 = lane & 15;
+    const int k = wu * 4 + lr16;  // k row of B piece 0 (kb = 0)
+    const int s = (k & 3) | (((k >> 3) & 1) << 2);
+    const int p = ((lc16 >> 1) ^ s) * 16 + (lc16 & 1) * 8;
+    const int n = (p >> 5) * 64 + (p & 31);  // nq = 0; nq = 1 adds 32 columns via soffset
+    c.voffB = (uint32_t)(k * c.ldb2 + n * 2);
+    const int swA = (l16 >> 1) & 7;
+    const int q4 = l16 >> 2, p4 = l16 & 3;
+    const int sB = q4 | ((g & 1) << 2);
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        uint32_t ao = (uint32_t)(st * STAGE + (wr * 128 + l16) * 128 + (((4 * ks + g) ^ swA) * 16));
+        asm volatile("" : "+v"(ao));  // opaque: keep each as its own base VGPR
+        c.aoff[st][ks] = ao;
+      }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int u = 4 * wc + jj;  // 32-B unit of the B half: columns (u>>1)*64 + nq*32 + (u&1)*16
+        uint32_t bo = (uint32_t)(st * STAGE + (8 * g + q4) * 256 + ((u ^ sB) * 32) + p4 * 8);
+        asm volatile("" : "+v"(bo));
+        c.boff[st][jj] = bo;
+      }
+    }
+  }
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Prologue, in the DMA order the loop's counted waits assume:
+  // A(0), B(0) -> stage 0; B(1), A(1) -> stage 1; tile 0's fragments to
+  // registers; then B(2) -> stage 0.B (the loop's "Bar_mid(-1)" issue).
+  const int nk = c.nk;
+  const int t1 = nk > 1 ? 1 : 0, t2 = nk > 2 ? 2 : nk - 1;
+  {
+    const u32x4 rb0 = b_rsrc(c, 0), rb1 = b_rsrc(c, t1);
+#pragma unroll
+    for (int h = 0; h < 16; ++h) issue_piece(c, rb0, 0, 0, h);
+#pragma unroll
+    for (int h = 8; h < 16; ++h) issue_piece(c, rb1, STAGE, t1, h);
+#pragma unroll
+    for (int h = 0; h < 8; ++h) issue_piece(c, rb1, STAGE, t1, h);
+  }
+  asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");  // tile 0 landed everywhere
+  Frag A[8], A7a, A7b, B0[8], B1[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      A[i].k[ks] = frag_a(smem, c.aoff[0][ks], i);
+      B0[i].k[ks] = frag_b(smem, c.boff[0][2 * (i >> 2) + (i & 1)], i, ks);
+    }
+  A7a = A[7];
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // stage 0.B read by all
+  {
+    const u32x4 rb2 = b_rsrc(c, t2);
+#pragma unroll
+    for (int h = 8; h < 16; ++h) issue_piece(c, rb2, 0, t2, h);
+  }
+  int t = 0;
+  for (; t + 1 < nk; t += 2) {  // branch-free body: B0/B1 and A7a/A7b swap roles every K-tile
+    ktile<DT, 0>(c, smem, t, acc, A, A7a, A7b, B0, B1);
+    ktile<DT, STAGE>(c, smem, t + 1, acc, A, A7b, A7a, B1, B0);
+  }
+  if (t < nk) ktile<DT, 0>(c, smem, t, acc, A, A7a, A7b, B0, B1);  // odd count
+  // Drain the tail DMAs and give the last MFMAs time to write their AGPRs
+  // (asm MFMAs are invisible to hipcc's hazard recognizer).
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+
+  // Epilogue: acc[i][j] holds C^T of a 16x16 tile: lane owns row l16 and
+  // columns 4g..4g+3 (interior tiles only: no masks).
+  char* Cb = (char*)a.C + (long long)bz * a.sC * 2;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = m0 + wr * 128 + i * 16 + l16;
+    char* crow = Cb + (long long)row * a.ldc * 2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = n0 + wc * 128 + j * 16 + 4 * g;
+      u32x2 v;
+      v.x = pack2<DT>(acc[i][j].x, acc[i][j].y);
+      v.y = pack2<DT>(acc[i][j].z, acc[i][j].w);
+      *(u32x2*)(crow + col * 2) = v;
+    }
+  }
+}
+
+}  // namespace kw4
+
+bool gemm_w4_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c) {
+  if (dt != kBF16 && dt != kF16) return false;
+  if (a.M <= 0 || a.N <= 0 || a.K <= 0) return false;
+  if (a.M % 256 || a.N % 256 || a.K % 64) return false;
+  if (a.lda % 8 || a.ldb % 8 || a.ldc % 4) return false;
+  if (a.lda < a.K || a.ldb < a.N || a.ldc < a.N) return false;
+  if (a.batch > 1 && (a.sA % 8 || a.sB % 8 || a.sC % 4)) return false;
+  if (align_a % 16 || align_b % 16 || align_c % 8) return false;
+  // 32-bit offsets: A rows up to 255 * lda (+ K bytes of the tile offset),
+  // B rows up to 63 * ldb (+ 64 B of the half offset).
+  if ((long long)256 * a.lda * 2 + (long long)a.K * 2 >= (1LL << 31)) return false;
+  if ((long long)64 * a.ldb * 2 + 64 >= (1LL << 31)) return false;
+  return true;
+}
+
+hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream) {
+  a.tiles_m = a.M / kw4::BM;
+  a.tiles_n = a.N / kw4::BN;
+  a.supertile = (a.tiles_m % 16 == 0 && a.tiles_n % 16 == 0) ? 1 : 0;
+  const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch;
+  if (nblocks <= 0) return hipSuccess;
+  if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
+  if (dt == kBF16)
+    hipLaunchKernelGGL(kw4::gemm_w4_nn<kBF16>, dim3((unsigned)nblocks), dim3(kw4::NT), 0, stream, a);
+  else
+    hipLaunchKernelGGL(kw4::gemm_w4_nn<kF16>, dim3((unsigned)nblocks), dim3(kw4::NT), 0, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace pdmb

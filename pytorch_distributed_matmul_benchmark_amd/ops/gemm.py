@@ -20,13 +20,13 @@ import torch
 
 from . import _native
 
-KERNELS = {"auto": 0, "mfma256": 1, "generic": 2, "mfma256b": 3, "mfma256c": 4, "mfma256d": 9,
+KERNELS = {"auto": 0, "mfma256": 1, "generic": 2, "mfma256b": 3, "mfma256c": 4, "mfma256d": 9, "w4": 21,
            "mfma256c_stamp": 5, "f32_256": 6,
            "f32_256s": 7, "fp8": 15, "fp8_w4": 16, "diag_fp8_w4_nowait": 17, "diag_fp8_w4_nosync": 18, "diag_fp8_w4_mfma_only": 19, "diag_f32_nodma": 20, "x_clusterprio": 10, "x_staticprio": 11, "x_tall": 13}
 KERNEL_NAMES = {0: "auto", 1: "pdmb_mfma256_nn", 2: "pdmb_generic_nn", 3: "pdmb_mfma256b_nn", 4: "pdmb_mfma256c_nn",
                 9: "pdmb_mfma256d_nn",
                 5: "pdmb_mfma256c_stamp", 6: "pdmb_f32_256_nn",
-                7: "pdmb_f32_256s_nn", 15: "pdmb_fp8_256_nt", 16: "pdmb_fp8_w4_nt",
+                7: "pdmb_f32_256s_nn", 15: "pdmb_fp8_256_nt", 16: "pdmb_fp8_w4_nt", 21: "pdmb_w4_nn",
                 -1: "unsupported"}
 SUPPORTED_DTYPES = (torch.float32, torch.float16, torch.bfloat16)
 FP8 = torch.float8_e4m3fn  # OCP e4m3 (gfx950), bf16 output, column-major B
@@ -131,7 +131,10 @@ def padded_kernel_for(A: torch.Tensor, B: torch.Tensor) -> Optional[str]:
     batch = max(A.shape[0] if A.dim() == 3 else 1, B.shape[0] if B.dim() == 3 else 1)
     if 2.0 * M * N * K * batch < PAD_MIN_FLOPS or kernel_for(A, B) != "pdmb_generic_nn":
         return None
-    return "pdmb_f32_256s_nn" if A.dtype == torch.float32 else "pdmb_mfma256d_nn"
+    if A.dtype == torch.float32:
+        return "pdmb_f32_256s_nn"
+    # gemm_dispatch.cpp: M is never padded, N is rounded up to 8; whole 256-tiles -> W4
+    return "pdmb_w4_nn" if M % 256 == 0 and (N + 7) // 8 * 8 % 256 == 0 else "pdmb_mfma256d_nn"
 
 
 def bmm(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,

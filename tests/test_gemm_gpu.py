@@ -260,3 +260,43 @@ def test_padded_path_misaligned_views_and_batches():
     out = torch.empty(1100, 1500, device="cuda", dtype=torch.bfloat16)
     ms = gemm.bench_matmul(A, B, out, iters=3, warmup=1)  # native loop takes the padded path too
     assert ms > 0 and _relerr(out, _ref(A, B)) < TOL[torch.bfloat16]
+
+
+# ---- W4: 4 waves x 128x128 per wave (gemm_w4.hip), the auto kernel for whole 256-tiles ----
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+@pytest.mark.parametrize("b,M,N,K,pad", [(1, 256, 256, 64, 0), (1, 1024, 512, 192, 0),
+                                         (3, 512, 768, 256, 0), (1, 768, 1280, 320, 64),
+                                         (1, 2304, 2048, 1024, 0)])
+def test_w4_exact_small_integers(dtype, b, M, N, K, pad):
+    """Integer operands keep every fp32 partial sum exact: C == fp64 product rounded once."""
+    dt = DT[dtype]
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
+    A = torch.randint(-3, 4, (b, M, K + pad), device="cuda", generator=g).to(dt)[..., :K]
+    B = torch.randint(-3, 4, (b, K, N + pad), device="cuda", generator=g).to(dt)[..., :N]
+    if b == 1:
+        A, B = A[0], B[0]
+    assert gemm.kernel_for(A, B) == "pdmb_w4_nn"  # auto picks W4 for whole tiles
+    C = gemm.matmul(A, B, kernel="w4")
+    assert torch.equal(C, (A.double() @ B.double()).to(dt))
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+def test_w4_random_matches_sched3(dtype):
+    dt = DT[dtype]
+    torch.manual_seed(5)
+    A = torch.randn(4096, 4096, device="cuda", dtype=dt)
+    B = torch.randn(4096, 4096, device="cuda", dtype=dt)
+    C = gemm.matmul(A, B, kernel="w4")
+    assert _relerr(C, _ref(A, B)) < TOL[dt]
+    # same fp32 accumulation order per output as the 8-wave kernel: bitwise equal
+    assert torch.equal(C, gemm.matmul(A, B, kernel="mfma256d"))
+
+
+def test_w4_rejects_edge_tiles_and_auto_falls_back():
+    A = torch.randn(300, 256, device="cuda", dtype=torch.bfloat16)
+    B = torch.randn(256, 512, device="cuda", dtype=torch.bfloat16)
+    assert gemm.kernel_for(A, B, kernel="w4") == "unsupported"
+    assert gemm.kernel_for(A, B) == "pdmb_mfma256d_nn"
+    with pytest.raises(RuntimeError):
+        gemm.matmul(A, B, kernel="w4")

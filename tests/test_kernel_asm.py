@@ -71,3 +71,21 @@ def test_bf16_two_quadrant_schedule(tmp_path):
     assert len(re.findall(r"s_waitcnt vmcnt\(0\)", b)) == 1
     assert len(re.findall(r"s_waitcnt vmcnt\(6\)", b)) >= 4
     assert len(re.findall(r"v_mfma_f32_16x16x32_bf16", b)) == 128
+
+
+def test_w4_kernel_agpr_accumulators_and_counted_waits(tmp_path):
+    """gemm_w4.hip: 256 AGPR accumulators, no spills, 128 KiB LDS (1 workgroup/CU),
+    counted vmcnt(16) waits at the two barriers of each K-tile and one vmcnt(0) drain."""
+    ks = _kernels("gemm_w4.hip", tmp_path)
+    for dt, mfma in (("ILi2E", "v_mfma_f32_16x16x32_bf16"), ("ILi1E", "v_mfma_f32_16x16x32_f16")):
+        name = [k for k in ks if "gemm_w4_nn" in k and dt in k]
+        assert name, sorted(ks)
+        k = ks[name[0]]
+        b = k["body"]
+        assert k["spill"] == 0 and k["lds"] == 2 * 65536
+        assert re.search(r"v_mfma_f32_16x16x32_\w+ a\[", b)  # accumulators live in AGPRs
+        assert len(re.findall(r"s_waitcnt vmcnt\(0\)", b)) == 1
+        assert len(re.findall(r"s_waitcnt vmcnt\(16\) lgkmcnt\(0\)", b)) >= 4
+        # loop body: 2 K-tiles x 8 blocks x 16 MFMAs, plus one odd tail K-tile
+        assert len(re.findall(mfma, b)) == 3 * 128
+        assert len(re.findall(r"buffer_load_dwordx4 .* lds", b)) >= 3 * 16
