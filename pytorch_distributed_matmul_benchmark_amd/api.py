@@ -18,6 +18,9 @@ event-ordered comm streams) and keeps the reference's return conventions
   backup/matmul_overlap_benchmark.py:36-278
                                       benchmark_no_overlap, benchmark_overlap,
                                       benchmark_pipeline (pipeline_depth)
+  MI355X addition (no reference counterpart)
+                                      benchmark_ring_parallel (all-gather-GEMM
+                                      over the ring, models/ring_parallel.py)
 """
 from __future__ import annotations
 
@@ -33,6 +36,7 @@ from .models import independent as _ind
 from .models import matrix_parallel as _mp
 from .models import model_parallel as _mdp
 from .models import overlap as _ov
+from .models import ring_parallel as _rp
 from .models.common import Workload
 from .models.common import validate_result as _validate
 from .parallel import dist as _dist
@@ -155,6 +159,16 @@ def benchmark_overlap(matrix_size: int, dtype: torch.dtype, device: str, rank: i
     r = _ov.run(_w(matrix_size, dtype, num_iterations, warmup_iterations), _ctx(device, rank),
                 mode="overlap")
     return r.avg_ms / 1e3, r.compute_only_tflops or 0.0, (r.comm_ms or 0.0) / 1e3
+
+
+def benchmark_ring_parallel(matrix_size: int, dtype: torch.dtype, device: str, rank: int,
+                            world_size: int, num_iterations: int = 50,
+                            warmup_iterations: int = 10) -> Tuple[float, float]:
+    """Ring all-gather-GEMM, same return convention as benchmark_matrix_parallel
+    (seconds, TFLOPS = 2N³ / t / ws)."""
+    r = _rp.run(_w(matrix_size, dtype, num_iterations, warmup_iterations),
+                _ctx(device, rank, world_size))
+    return r.avg_ms / 1e3, r.tflops
 
 
 def benchmark_pipeline(matrix_size: int, dtype: torch.dtype, device: str, rank: int,

@@ -2,6 +2,7 @@
 
 ``MODES`` maps every mode name of every reference script to its runner:
   * matmul_scaling_benchmark.py: independent | batch_parallel | matrix_parallel
+    (+ ring_parallel, an MI355X addition: all-gather-GEMM over the xGMI ring)
   * backup/matmul_distributed_benchmark.py: independent | data_parallel | model_parallel
   * backup/matmul_overlap_benchmark.py: no_overlap | overlap | pipeline
 """
@@ -10,13 +11,15 @@ from __future__ import annotations
 from enum import Enum
 from functools import partial
 
-from . import batch_parallel, data_parallel, independent, matrix_parallel, model_parallel, overlap
+from . import (batch_parallel, data_parallel, independent, matrix_parallel, model_parallel, overlap,
+               ring_parallel)
 from .common import ModeResult, Workload
 
 MODES = {
     "independent": independent.run,
     "batch_parallel": batch_parallel.run,
     "matrix_parallel": matrix_parallel.run,
+    "ring_parallel": ring_parallel.run,
     "data_parallel": data_parallel.run,
     "model_parallel": model_parallel.run,
     "no_overlap": partial(overlap.run, mode="no_overlap"),
@@ -25,6 +28,8 @@ MODES = {
 }
 
 SCALING_MODES = ("independent", "batch_parallel", "matrix_parallel")
+# Selectable in matmul_scaling_benchmark.py beyond the reference's three.
+EXTRA_SCALING_MODES = ("ring_parallel",)
 
 
 class ScalingMode(Enum):
@@ -58,5 +63,5 @@ def run_mode(name, w: Workload, ctx) -> ModeResult:
     return fn(w, ctx)
 
 
-__all__ = ["MODES", "SCALING_MODES", "DISTRIBUTED_MODES", "OVERLAP_MODES", "ModeResult",
+__all__ = ["MODES", "SCALING_MODES", "EXTRA_SCALING_MODES", "DISTRIBUTED_MODES", "OVERLAP_MODES", "ModeResult",
            "Workload", "run_mode", "ScalingMode", "BenchmarkMode"]

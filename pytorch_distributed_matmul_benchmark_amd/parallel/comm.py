@@ -101,6 +101,30 @@ class CommStream:
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor, after=None, done=None):
         return self.collective(dist.all_gather_into_tensor, out, inp, after=after, done=done)
 
+    def exchange(self, send: torch.Tensor, dst: int, recv: torch.Tensor, src: int,
+                 after=None, done=None):
+        """One ring hop on the comm stream: ``send`` → rank ``dst`` while ``recv``
+        ← rank ``src`` (global ranks), issued as one batched P2P group so RCCL
+        runs both directions of the hop concurrently."""
+        with stream_ctx(self.stream):
+            if after is not None:
+                self.wait_event(after)
+            # gloo P2P takes host memory only: GPU tensors of a gloo rehearsal
+            # (ranks sharing one GPU) hop through host copies on this stream.
+            staged = send.is_cuda and dist.get_backend(self.group) == "gloo"
+            s_t, r_t = (send.cpu(), torch.empty(recv.shape, dtype=recv.dtype)) if staged \
+                else (send, recv)
+            ops = [dist.P2POp(dist.isend, s_t, dst, group=self.group),
+                   dist.P2POp(dist.irecv, r_t, src, group=self.group)]
+            works = dist.batch_isend_irecv(ops)
+            for wk in works:
+                wk.wait()
+            if staged:
+                recv.copy_(r_t)
+            if done is not None:
+                done.record(self.stream)
+        return works
+
     def synchronize(self) -> None:
         if self.stream is not None:
             self.stream.synchronize()

@@ -27,7 +27,8 @@ from typing import Dict, List, Optional
 
 import torch
 
-from .models import DISTRIBUTED_MODES, OVERLAP_MODES, SCALING_MODES, ModeResult, Workload, run_mode
+from .models import (DISTRIBUTED_MODES, EXTRA_SCALING_MODES, OVERLAP_MODES, SCALING_MODES,
+                     ModeResult, Workload, run_mode)
 from .models.common import tolerance
 from .ops.gemm import out_dtype as _gemm_out_dtype
 from .parallel.dist import (DistContext, all_ok, barrier, cleanup_distributed, reduce_scalar,
@@ -43,7 +44,7 @@ KINDS = {
                   default_mode="independent",
                   desc="Distributed PyTorch Matrix Multiplication Benchmark (MI355X)"),
     "scaling": dict(title="Matrix Multiplication Scaling Benchmark", width=70,
-                    modes=SCALING_MODES, default_mode="independent",
+                    modes=SCALING_MODES + EXTRA_SCALING_MODES, default_mode="independent",
                     desc="Matrix Multiplication Scaling Benchmark (MI355X)"),
     "distributed": dict(title="Distributed Matrix Multiplication Benchmark", width=70,
                         modes=DISTRIBUTED_MODES, default_mode="data_parallel",
@@ -207,7 +208,8 @@ def _print_results(kind: str, mode: str, rep: Reporter, ctx: DistContext, n: int
             rep.line(f"  - Each GPU processes 1/{ws} of the matrix")
         total_flops = {"independent": square_flops(n, ws),
                        "batch_parallel": square_flops(n, r.extra.get("global_batch", 4)),
-                       "matrix_parallel": square_flops(n)}[mode]
+                       "matrix_parallel": square_flops(n),
+                       "ring_parallel": square_flops(n)}[mode]
         actual = tflops_from(total_flops, agg["avg_ms"] / 1e3)
         extra["actual_tflops"] = actual
         rep.line(f"  - Actual TFLOPS (total FLOPs / time): {actual:.2f}")
@@ -250,7 +252,8 @@ def _print_results(kind: str, mode: str, rep: Reporter, ctx: DistContext, n: int
         extra["scaling_efficiency_vs_1gpu"] = eff
         rep.line(f"  - Scaling efficiency vs 1 GPU: {eff:.1f}%")
     if kind != "basic":
-        pct = percent_of_peak(r.tflops if mode != "matrix_parallel" else r.compute_only_tflops or 0.0,
+        pct = percent_of_peak(r.tflops if mode not in ("matrix_parallel", "ring_parallel")
+                              else r.compute_only_tflops or 0.0,
                               peak, dtype)
         if pct is not None:
             extra["pct_peak"] = pct

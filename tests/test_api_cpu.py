@@ -14,6 +14,8 @@ def test_signatures_and_returns_cpu():
     assert t > 0 and tf > 0
     t, tf = api.benchmark_matrix_parallel(96, torch.float32, "cpu", 0, 1, 2, 1)
     assert t > 0 and tf > 0
+    t, tf = api.benchmark_ring_parallel(96, torch.float32, "cpu", 0, 1, 2, 1)
+    assert t > 0 and tf > 0
     for f in (api.benchmark_data_parallel, api.benchmark_no_overlap, api.benchmark_overlap):
         t, tf, tc = f(96, torch.float32, "cpu", 0, 2, 1)
         assert t > 0 and tf > 0 and tc >= 0

@@ -42,7 +42,8 @@ def test_basic_cpu_fp32(tmp_path):
     assert recs[0]["tflops_rank0"] > 0
 
 
-@pytest.mark.parametrize("mode", ["independent", "batch_parallel", "matrix_parallel"])
+@pytest.mark.parametrize("mode", ["independent", "batch_parallel", "matrix_parallel",
+                                  "ring_parallel"])
 def test_scaling_single_process(mode):
     out = _run([sys.executable, os.path.join(ROOT, "matmul_scaling_benchmark.py"), "--device",
                 "cpu", "--sizes", "200", "--iterations", "2", "--warmup", "1", "--dtype",
@@ -69,6 +70,21 @@ def test_scaling_torchrun_gloo(mode, extra, tmp_path):
         assert rec["global_batch"] == 4 and rec["local_batch"] == 2
     if mode == "matrix_parallel":
         assert rec["shard_cols"] == 152
+
+
+@pytest.mark.parametrize("ws,n", [(2, 300), (3, 520)])
+def test_ring_parallel_gloo(ws, n, tmp_path):
+    """All-gather-GEMM over the ring: A row-sharded (256-row blocks, zero-padded),
+    each rank's C[:, S_r] checked against the float64 product of the global A."""
+    js = tmp_path / "r.jsonl"
+    out = _torchrun(ws, "matmul_scaling_benchmark.py", "--device", "cpu", "--sizes", str(n),
+                    "--iterations", "2", "--warmup", "1", "--dtype", "float32", "--mode",
+                    "ring_parallel", "--check", "--json", str(js))
+    assert f"Results for {n}x{n}" in out
+    assert "PASS" in out and "FAIL" not in out and "ERROR" not in out
+    rec = json.loads(js.read_text().splitlines()[-1])
+    assert rec["mode"] == "ring_parallel" and rec["world_size"] == ws
+    assert rec["hops"] == ws - 1 and rec["shard_rows"] == 256
 
 
 def test_batch_parallel_ws3_reports_real_batch(tmp_path):

@@ -27,7 +27,8 @@ def _run(nproc, script, *args, port=None):
 
 @pytest.mark.parametrize("mode,extra", [("batch_parallel", []), ("batch_parallel", ["--overlap"]),
                                         ("matrix_parallel", []),
-                                        ("matrix_parallel", ["--overlap", "--chunks", "2"])])
+                                        ("matrix_parallel", ["--overlap", "--chunks", "2"]),
+                                        ("ring_parallel", [])])
 def test_two_ranks_share_gpu_scaling_modes(mode, extra):
     out = _run(2, "matmul_scaling_benchmark.py", "--sizes", "2048", "4608", "--iterations", "3",
                "--warmup", "1", "--mode", mode, "--check", *extra)
