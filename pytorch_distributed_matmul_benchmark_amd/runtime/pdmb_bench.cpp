@@ -2,7 +2,7 @@
 //
 // The same workloads as matmul_scaling_benchmark.py (independent |
 // batch_parallel | matrix_parallel, reference matmul_scaling_benchmark.py:
-// 69-238) driven entirely from C++: one host thread per GPU in one process,
+// 69-238, plus ring_parallel, models/ring_parallel.py) driven entirely from C++: one host thread per GPU in one process,
 // RCCL communicators from ncclCommInitAll over xGMI, the gfx950 MFMA GEMM
 // library of ops/csrc (pdmb::gemm), hipEvents for timing and an
 // event-ordered comm stream for the --overlap variants. No PyTorch, no Python:
@@ -48,7 +48,7 @@ namespace {
       throw std::runtime_error(std::string(#x) + ": " + ncclGetErrorString(r_));         \
   } while (0)
 
-enum Mode { kIndependent, kBatchParallel, kMatrixParallel };
+enum Mode { kIndependent, kBatchParallel, kMatrixParallel, kRingParallel };
 
 struct Opts {
   int gpus = 1;
@@ -62,7 +62,10 @@ struct Opts {
 };
 
 const char* mode_name(Mode m) {
-  return m == kIndependent ? "independent" : m == kBatchParallel ? "batch_parallel" : "matrix_parallel";
+  return m == kIndependent      ? "independent"
+         : m == kBatchParallel  ? "batch_parallel"
+         : m == kMatrixParallel ? "matrix_parallel"
+                                : "ring_parallel";
 }
 const char* dtype_name(int d) { return d == 0 ? "float32" : d == 1 ? "float16" : "bfloat16"; }
 size_t esize(int d) { return d == 0 ? 4 : 2; }
@@ -382,6 +385,86 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     res.flops_total = flop * gb;
     if (o.check)  // C[0] = sum over ranks of A_r[0] @ B_r[0]: partial refs are summed on the host
       check_rows(dt, A.p, B.p, C.p, n, n, n, n, n, n, st, res.ref, res.got);
+  } else if (o.mode == kRingParallel) {
+    // All-gather-GEMM over the ring (models/ring_parallel.py): A row-sharded in
+    // blocks of rp rows, B column-sharded. Hop s multiplies the A block of rank
+    // (r - s) mod ws into rows of C[:, S_r] while the comm stream forwards it to
+    // r+1 and receives the next block from r-1 (ncclSend + ncclRecv in one group).
+    const int shard = ceil_div(ceil_div(n, ws), 8) * 8;
+    const int c0 = std::min(rank * shard, n), width = std::max(0, std::min(n, c0 + shard) - c0);
+    const int rp = ceil_div(n, ws);
+    auto rows_of = [&](int j) { return std::max(0, std::min(n, (j + 1) * rp) - j * rp); };
+    res.shard = shard;
+    const size_t blk = (size_t)rp * n;
+    Buf Ag((size_t)n * n * es), Bg((size_t)n * n * es), Bl((size_t)n * shard * es);
+    Buf Cl((size_t)n * shard * es), Al(blk * es), R0(blk * es), R1(blk * es);
+    fill(Ag.p, (long long)n * n, dt, 1000, st);
+    fill(Bg.p, (long long)n * n, dt, 1001, st);
+    HIP_OK(hipMemsetAsync(Bl.p, 0, Bl.bytes, st));
+    if (width)
+      HIP_OK(hipMemcpy2DAsync(Bl.p, shard * es, (char*)Bg.p + c0 * es, n * es, width * es, n,
+                              hipMemcpyDeviceToDevice, st));
+    HIP_OK(hipMemsetAsync(Al.p, 0, Al.bytes, st));
+    if (rows_of(rank))
+      HIP_OK(hipMemcpyAsync(Al.p, (char*)Ag.p + (size_t)rank * rp * n * es,
+                            (size_t)rows_of(rank) * n * es, hipMemcpyDeviceToDevice, st));
+    res.kernel = pdmb::kernel_name(
+        pdmb::resolve_kernel(problem(dt, Al.p, Bl.p, Cl.p, rp, shard, n, n, shard, shard), o.kernel));
+    char* R[2] = {(char*)R0.p, (char*)R1.p};
+    std::vector<hipEvent_t> gdone, rdone;
+    for (int s = 0; s < ws; ++s) gdone.push_back(event());
+    for (int s = 0; s + 1 < ws; ++s) rdone.push_back(event());
+    hipEvent_t last = nullptr;  // most recently issued GEMM (across iterations)
+    auto block_gemm = [&](const char* a, int j) {
+      if (rows_of(j))
+        gemm(problem(dt, a, Bl.p, (char*)Cl.p + (size_t)j * rp * shard * es, rows_of(j), shard, n,
+                     n, shard, shard),
+             o.kernel, st);
+    };
+    auto iter = [&]() {
+      char* cur = (char*)Al.p;
+      for (int s = 0; s < ws; ++s) {
+        if (s > 0) HIP_OK(hipStreamWaitEvent(st, rdone[s - 1], 0));
+        char* nb = R[(s + 1) % 2];
+        if (s + 1 < ws) {
+          if (last) HIP_OK(hipStreamWaitEvent(cs, last, 0));  // nb's last reader is done
+          NCCL_OK(ncclGroupStart());
+          NCCL_OK(ncclSend(cur, blk, nccl_type(dt), (rank + 1) % ws, comm, cs));
+          NCCL_OK(ncclRecv(nb, blk, nccl_type(dt), (rank + ws - 1) % ws, comm, cs));
+          NCCL_OK(ncclGroupEnd());
+          HIP_OK(hipEventRecord(rdone[s], cs));
+        }
+        block_gemm(cur, (rank - s + ws) % ws);
+        HIP_OK(hipEventRecord(gdone[s], st));
+        last = gdone[s];
+        cur = nb;
+      }
+    };
+    for (int i = 0; i < o.warmup; ++i) iter();
+    HIP_OK(hipStreamSynchronize(st));
+    {
+      hipEvent_t q0 = event(), q1 = event();
+      const int k = std::max(1, std::min(o.iters, 10));
+      HIP_OK(hipEventRecord(q0, st));
+      for (int i = 0; i < k; ++i)
+        for (int j = 0; j < ws; ++j) block_gemm((const char*)Al.p, j);
+      HIP_OK(hipEventRecord(q1, st));
+      HIP_OK(hipEventSynchronize(q1));
+      res.comp_ms = elapsed(q0, q1) / k;
+    }
+    bar.wait();
+    hipEvent_t m0 = event(), m1 = event();
+    HIP_OK(hipEventRecord(m0, st));
+    for (int i = 0; i < o.iters; ++i) iter();
+    HIP_OK(hipEventRecord(m1, st));
+    HIP_OK(hipEventSynchronize(m1));
+    HIP_OK(hipStreamSynchronize(cs));
+    res.avg_ms = elapsed(m0, m1) / std::max(o.iters, 1);
+    res.comm_ms = std::max(0.0, res.avg_ms - res.comp_ms);
+    res.flops_local = 2.0 * n * (double)shard * n;
+    res.flops_total = flop;
+    // Cl is C[:, S_r] exactly (blocks are contiguous, unpadded): sampled rows vs A @ B_local.
+    if (o.check) check_rows(dt, Ag.p, Bl.p, Cl.p, n, shard, n, n, shard, shard, st, res.ref, res.got);
   } else {  // matrix_parallel: replicated A, padded column shard of one global B
     const int shard = ceil_div(ceil_div(n, ws), 8) * 8;
     const int c0 = std::min(rank * shard, n), width = std::max(0, std::min(n, c0 + shard) - c0);
@@ -518,7 +601,7 @@ double norm_relerr(const std::vector<double>& got, const std::vector<double>& re
 void usage() {
   std::printf(
       "pdmb_bench [--gpus N] [--sizes N ...] [--iterations I] [--warmup W]\n"
-      "           [--dtype bfloat16|float16|float32] [--mode independent|batch_parallel|matrix_parallel]\n"
+      "           [--dtype bfloat16|float16|float32] [--mode independent|batch_parallel|matrix_parallel|ring_parallel]\n"
       "           [--batch B] [--overlap] [--chunks C] [--kernel ID] [--check] [--json FILE]\n");
 }
 
@@ -548,6 +631,7 @@ Opts parse(int argc, char** argv) {
       if (m == "independent") o.mode = kIndependent;
       else if (m == "batch_parallel") o.mode = kBatchParallel;
       else if (m == "matrix_parallel") o.mode = kMatrixParallel;
+      else if (m == "ring_parallel") o.mode = kRingParallel;
       else throw std::runtime_error("bad --mode " + m);
     } else if (a == "--sizes") {
       o.sizes.clear();
@@ -640,7 +724,8 @@ int main(int argc, char** argv) {
     if (o.mode == kBatchParallel)
       std::printf("  - Processing %d total batches across %d GPU(s) (%d per GPU)\n", r0.global_batch,
                   o.gpus, r0.local_batch);
-    std::printf("  - Total system TFLOPS: %.2f\n", o.mode == kMatrixParallel ? actual : per_gpu * o.gpus);
+    const bool sharded = o.mode == kMatrixParallel || o.mode == kRingParallel;
+    std::printf("  - Total system TFLOPS: %.2f\n", sharded ? actual : per_gpu * o.gpus);
     std::printf("  - Actual TFLOPS (total FLOPs / time): %.2f\n", actual);
     std::printf("  - Node TFLOPS (all FLOPs / slowest rank): %.2f\n", node);
     std::printf("  - Kernel: %s\n", r0.kernel.c_str());

@@ -11,7 +11,7 @@ mkdir -p "$(dirname "$OUT")"
 export HSA_ENABLE_IPC_MODE_LEGACY=${HSA_ENABLE_IPC_MODE_LEGACY:-0}
 PORT=29800
 for n in $COUNTS; do
-  for spec in "independent" "batch_parallel" "batch_parallel --overlap" "matrix_parallel" "matrix_parallel --overlap"; do
+  for spec in "independent" "batch_parallel" "batch_parallel --overlap" "matrix_parallel" "matrix_parallel --overlap" "ring_parallel"; do
     PORT=$((PORT + 1))
     # shellcheck disable=SC2086
     timeout -k 10 900 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node="$n" \

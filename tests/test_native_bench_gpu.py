@@ -22,7 +22,8 @@ def exe():
 @pytest.mark.parametrize("mode,extra", [("independent", []), ("batch_parallel", []),
                                         ("batch_parallel", ["--overlap"]),
                                         ("matrix_parallel", []),
-                                        ("matrix_parallel", ["--overlap"])])
+                                        ("matrix_parallel", ["--overlap"]),
+                                        ("ring_parallel", [])])
 @pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
 def test_native_executor_modes(exe, mode, extra, dtype, tmp_path):
     js = tmp_path / "r.jsonl"
