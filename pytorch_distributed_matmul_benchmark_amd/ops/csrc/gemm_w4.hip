@@ -183,12 +183,13 @@ __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, f32
   }
 }
 
-template <int DT>
+// TALL: XCD sub-block 8 (M) x 4 (N) instead of 4 x 8 (A/B experiment, kMfmaW4Tall).
+template <int DT, bool TALL = false>
 __global__ void __launch_bounds__(NT, 1) gemm_w4_nn(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
 
   int bz, tm, tn;
-  map_tile(a, blockIdx.x, bz, tm, tn);
+  map_tile(a, blockIdx.x, bz, tm, tn, TALL);
   const int m0 = tm * BM, n0 = tn * BN;
   const int lane = threadIdx.x & 63;
   const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -316,14 +317,17 @@ bool gemm_w4_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b
   return true;
 }
 
-hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream) {
+hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, bool tall) {
   a.tiles_m = a.M / kw4::BM;
   a.tiles_n = a.N / kw4::BN;
   a.supertile = (a.tiles_m % 16 == 0 && a.tiles_n % 16 == 0) ? 1 : 0;
   const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch;
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
-  if (dt == kBF16)
+  if (dt == kBF16 && tall)
+    hipLaunchKernelGGL((kw4::gemm_w4_nn<kBF16, true>), dim3((unsigned)nblocks), dim3(kw4::NT), 0,
+                       stream, a);
+  else if (dt == kBF16)
     hipLaunchKernelGGL(kw4::gemm_w4_nn<kBF16>, dim3((unsigned)nblocks), dim3(kw4::NT), 0, stream, a);
   else
     hipLaunchKernelGGL(kw4::gemm_w4_nn<kF16>, dim3((unsigned)nblocks), dim3(kw4::NT), 0, stream, a);
