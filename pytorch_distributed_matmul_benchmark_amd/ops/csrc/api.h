@@ -26,6 +26,7 @@ enum Kernel : int {
   kFp8W4Diag3 = 19,  // diagnostic: kFp8W4 MFMAs + barriers only (no loads)
   kMfmaW4 = 21,   // gemm_w4.hip: bf16/fp16 NN, 4 waves x 128x128, AGPR accumulators (M, N % 256)
   kMfmaW4Tall = 22,  // experiment (A/B only): kMfmaW4 (bf16) with the 8x4 XCD sub-block
+  kMfmaW4Wide = 23,  // experiment (A/B only): kMfmaW4 (bf16) with the 2x16 XCD sub-block
   kFp8 = 15,      // gemm_fp8.hip: e4m3 A [M,K] x column-major B, block-scaled MFMA 16x16x128, bf16 out
 };
 

@@ -136,8 +136,9 @@ __device__ __forceinline__ void dma16(u32x4 rsrc, uint32_t voff, uint32_t lds_ba
 // whole chip touches 32 panels per K-step (shared through Infinity Cache).
 // Super-tiles sweep N fastest so A panels stay Infinity-Cache resident.
 // Otherwise: grouped order with 16 tile-rows per group (chip-wide locality).
+// sub: XCD sub-block shape, 0 = 4 (M) x 8 (N), 1 = 8 x 4 ("tall"), 2 = 2 x 16 ("wide").
 __device__ __forceinline__ void map_tile(const GemmArgs& a, int b, int& bz, int& tm, int& tn,
-                                         bool tall = false) {
+                                         int sub = 0) {
   const int tpb = a.tiles_m * a.tiles_n;
   if (a.supertile) {
     const int x = b & 7, j = b >> 3;
@@ -147,7 +148,10 @@ __device__ __forceinline__ void map_tile(const GemmArgs& a, int b, int& bz, int&
     bz = round / st_per_b;
     const int s = round - bz * st_per_b;
     const int sr = s / st_n, sc = s - sr * st_n;
-    if (tall) {  // XCD sub-block 8 (M) x 4 (N)
+    if (sub == 2) {  // XCD sub-block 2 (M) x 16 (N)
+      tm = (sr << 4) + (x << 1) + (i >> 4);
+      tn = (sc << 4) + (i & 15);
+    } else if (sub == 1) {  // XCD sub-block 8 (M) x 4 (N)
       tm = (sr << 4) + ((x & 1) << 3) + (i >> 2);
       tn = (sc << 4) + ((x >> 1) << 2) + (i & 3);
     } else {     // XCD sub-block 4 (M) x 8 (N)

@@ -23,7 +23,7 @@ hipError_t gemm_f32_256_launch(GemmArgs a, int variant, hipStream_t stream);
 bool gemm_fp8_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream);
 bool gemm_w4_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
-hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, bool tall = false);
+hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub = 0);
 
 static unsigned long long* g_debug_buffer = nullptr;
 
@@ -90,9 +90,9 @@ int resolve_kernel(const Problem& p, int kernel) {
   if (kernel == kMfma256d) return fast ? kMfma256d : -1;
   if (kernel == kMfmaW4)
     return gemm_w4_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C) ? kMfmaW4 : -1;
-  if (kernel == kMfmaW4Tall)
+  if (kernel == kMfmaW4Tall || kernel == kMfmaW4Wide)
     return (p.dtype == kBF16 && gemm_w4_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C))
-               ? kMfmaW4Tall : -1;
+               ? kernel : -1;
   if (kernel == kMfma256Stamp) return (fast && p.dtype == kBF16) ? kMfma256Stamp : -1;
   if (kernel == kGeneric) return kGeneric;
   return -1;
@@ -282,7 +282,8 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
   if (k == kMfma256c) return gemm256_launch(p.dtype, a, 2, stream);
   if (k == kMfma256d) return gemm256_launch(p.dtype, a, 4, stream);
   if (k == kMfmaW4) return gemm_w4_launch(p.dtype, a, stream);
-  if (k == kMfmaW4Tall) return gemm_w4_launch(p.dtype, a, stream, true);
+  if (k == kMfmaW4Tall) return gemm_w4_launch(p.dtype, a, stream, 1);
+  if (k == kMfmaW4Wide) return gemm_w4_launch(p.dtype, a, stream, 2);
   if (k == kMfma256Stamp) return gemm256_launch(p.dtype, a, 3, stream);
   if (k == kF32_256) return gemm_f32_256_launch(a, 0, stream);
   if (k >= kMfma256X1 && k <= kMfma256X4) return gemm256_launch(p.dtype, a, 10 + (k - kMfma256X1 + 1), stream);
@@ -365,6 +366,8 @@ const char* kernel_name(int kernel) {
       return "pdmb_w4_nn";
     case kMfmaW4Tall:
       return "pdmb_w4_nn_tall";
+    case kMfmaW4Wide:
+      return "pdmb_w4_nn_wide";
     default:
       return "auto";
   }

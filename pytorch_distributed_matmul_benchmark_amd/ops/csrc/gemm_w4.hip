@@ -183,13 +183,14 @@ __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, f32
   }
 }
 
-// TALL: XCD sub-block 8 (M) x 4 (N) instead of 4 x 8 (A/B experiment, kMfmaW4Tall).
-template <int DT, bool TALL = false>
+// SUB: XCD sub-block shape (map_tile): 0 = 4 x 8 (default), 1 = 8 x 4
+// (kMfmaW4Tall), 2 = 2 x 16 (kMfmaW4Wide); 1 and 2 are A/B experiments.
+template <int DT, int SUB = 0>
 __global__ void __launch_bounds__(NT, 1) gemm_w4_nn(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
 
   int bz, tm, tn;
-  map_tile(a, blockIdx.x, bz, tm, tn, TALL);
+  map_tile(a, blockIdx.x, bz, tm, tn, SUB);
   const int m0 = tm * BM, n0 = tn * BN;
   const int lane = threadIdx.x & 63;
   const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -317,15 +318,18 @@ bool gemm_w4_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b
   return true;
 }
 
-hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, bool tall) {
+hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
   a.tiles_m = a.M / kw4::BM;
   a.tiles_n = a.N / kw4::BN;
   a.supertile = (a.tiles_m % 16 == 0 && a.tiles_n % 16 == 0) ? 1 : 0;
   const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch;
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
-  if (dt == kBF16 && tall)
-    hipLaunchKernelGGL((kw4::gemm_w4_nn<kBF16, true>), dim3((unsigned)nblocks), dim3(kw4::NT), 0,
+  if (dt == kBF16 && sub == 1)
+    hipLaunchKernelGGL((kw4::gemm_w4_nn<kBF16, 1>), dim3((unsigned)nblocks), dim3(kw4::NT), 0,
+                       stream, a);
+  else if (dt == kBF16 && sub == 2)
+    hipLaunchKernelGGL((kw4::gemm_w4_nn<kBF16, 2>), dim3((unsigned)nblocks), dim3(kw4::NT), 0,
                        stream, a);
   else if (dt == kBF16)
     hipLaunchKernelGGL(kw4::gemm_w4_nn<kBF16>, dim3((unsigned)nblocks), dim3(kw4::NT), 0, stream, a);
