@@ -27,6 +27,8 @@ enum Kernel : int {
   kMfmaW4 = 21,   // gemm_w4.hip: bf16/fp16 NN, 4 waves x 128x128, AGPR accumulators (M, N % 256)
   kMfmaW4Tall = 22,  // experiment (A/B only): kMfmaW4 (bf16) with the 8x4 XCD sub-block
   kMfmaW4Wide = 23,  // experiment (A/B only): kMfmaW4 (bf16) with the 2x16 XCD sub-block
+  kFp8W4Tall = 24,   // experiment (A/B only): kFp8W4 with the 8x4 XCD sub-block
+  kFp8W4Wide = 25,   // experiment (A/B only): kFp8W4 with the 2x16 XCD sub-block
   kFp8 = 15,      // gemm_fp8.hip: e4m3 A [M,K] x column-major B, block-scaled MFMA 16x16x128, bf16 out
 };
 

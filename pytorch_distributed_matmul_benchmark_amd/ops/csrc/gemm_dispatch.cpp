@@ -63,12 +63,13 @@ int resolve_kernel(const Problem& p, int kernel) {
   const GemmArgs a = to_args(p);
   if (p.dtype == kFP8)  // one kernel, no generic / padded fallback
     return (kernel == kAuto || kernel == kFp8 || kernel == kFp8W4 || kernel == kFp8W4Diag ||
-                    kernel == kFp8W4Diag2 || kernel == kFp8W4Diag3) &&
+                    kernel == kFp8W4Diag2 || kernel == kFp8W4Diag3 || kernel == kFp8W4Tall ||
+                    kernel == kFp8W4Wide) &&
                    gemm_fp8_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C)
                ? (kernel == kAuto ? kFp8W4 : kernel)
                : -1;
   if (kernel == kFp8 || kernel == kFp8W4 || kernel == kFp8W4Diag || kernel == kFp8W4Diag2 ||
-      kernel == kFp8W4Diag3)
+      kernel == kFp8W4Diag3 || kernel == kFp8W4Tall || kernel == kFp8W4Wide)
     return -1;
   const bool fast = gemm256_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   const bool f32fast = p.dtype == kF32 &&
@@ -277,6 +278,8 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
   if (k == kFp8W4Diag) return gemm_fp8_launch(a, 9, stream);
   if (k == kFp8W4Diag2) return gemm_fp8_launch(a, 10, stream);
   if (k == kFp8W4Diag3) return gemm_fp8_launch(a, 11, stream);
+  if (k == kFp8W4Tall) return gemm_fp8_launch(a, 12, stream);
+  if (k == kFp8W4Wide) return gemm_fp8_launch(a, 13, stream);
   if (k == kMfma256) return gemm256_launch(p.dtype, a, 0, stream);
   if (k == kMfma256b) return gemm256_launch(p.dtype, a, 1, stream);
   if (k == kMfma256c) return gemm256_launch(p.dtype, a, 2, stream);
@@ -368,6 +371,10 @@ const char* kernel_name(int kernel) {
       return "pdmb_w4_nn_tall";
     case kMfmaW4Wide:
       return "pdmb_w4_nn_wide";
+    case kFp8W4Tall:
+      return "pdmb_fp8_w4_nt_tall";
+    case kFp8W4Wide:
+      return "pdmb_fp8_w4_nt_wide";
     default:
       return "auto";
   }

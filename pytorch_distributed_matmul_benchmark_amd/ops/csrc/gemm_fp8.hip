@@ -426,12 +426,13 @@ __device__ __forceinline__ void ktile_w4(const Ctx4& c, const char* smem, int t,
   }
 }
 
-template <int DIAG_NOWAIT>
+// SUB: XCD sub-block shape (map_tile); 1 (8x4) and 2 (2x16) are A/B experiments.
+template <int DIAG_NOWAIT, int SUB = 0>
 __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE4];
 
   int bz, tm, tn;
-  map_tile(a, blockIdx.x, bz, tm, tn);
+  map_tile(a, blockIdx.x, bz, tm, tn, SUB);
   const int m0 = tm * BM, n0 = tn * BN;
   const int lane = threadIdx.x & 63;
   const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -555,6 +556,10 @@ hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream) {
     hipLaunchKernelGGL(k8::gemm_fp8_w4<2>, dim3((unsigned)nblocks), dim3(k8::NT4), 0, stream, a);
   else if (variant == 11)
     hipLaunchKernelGGL(k8::gemm_fp8_w4<3>, dim3((unsigned)nblocks), dim3(k8::NT4), 0, stream, a);
+  else if (variant == 12)
+    hipLaunchKernelGGL((k8::gemm_fp8_w4<0, 1>), dim3((unsigned)nblocks), dim3(k8::NT4), 0, stream, a);
+  else if (variant == 13)
+    hipLaunchKernelGGL((k8::gemm_fp8_w4<0, 2>), dim3((unsigned)nblocks), dim3(k8::NT4), 0, stream, a);
   else
     hipLaunchKernelGGL(k8::gemm_fp8_nt, dim3((unsigned)nblocks), dim3(k8::NTHREADS), 0, stream, a);
   return hipGetLastError();

@@ -22,7 +22,7 @@ from . import _native
 
 KERNELS = {"auto": 0, "mfma256": 1, "generic": 2, "mfma256b": 3, "mfma256c": 4, "mfma256d": 9, "w4": 21,
            "mfma256c_stamp": 5, "f32_256": 6,
-           "f32_256s": 7, "fp8": 15, "fp8_w4": 16, "diag_fp8_w4_nowait": 17, "diag_fp8_w4_nosync": 18, "diag_fp8_w4_mfma_only": 19, "diag_f32_nodma": 20, "x_clusterprio": 10, "x_staticprio": 11, "x_tall": 13, "x_w4_tall": 22, "x_w4_wide": 23}
+           "f32_256s": 7, "fp8": 15, "fp8_w4": 16, "diag_fp8_w4_nowait": 17, "diag_fp8_w4_nosync": 18, "diag_fp8_w4_mfma_only": 19, "diag_f32_nodma": 20, "x_clusterprio": 10, "x_staticprio": 11, "x_tall": 13, "x_w4_tall": 22, "x_w4_wide": 23, "x_fp8_w4_tall": 24, "x_fp8_w4_wide": 25}
 KERNEL_NAMES = {0: "auto", 1: "pdmb_mfma256_nn", 2: "pdmb_generic_nn", 3: "pdmb_mfma256b_nn", 4: "pdmb_mfma256c_nn",
                 9: "pdmb_mfma256d_nn",
                 5: "pdmb_mfma256c_stamp", 6: "pdmb_f32_256_nn",
