@@ -87,6 +87,19 @@ def test_ring_parallel_gloo(ws, n, tmp_path):
     assert rec["hops"] == ws - 1 and rec["shard_rows"] == 256
 
 
+@pytest.mark.parametrize("ws,mode,extra", [(4, "batch_parallel", ["--overlap", "--chunks", "2"]),
+                                           (4, "matrix_parallel", ["--overlap", "--chunks", "2"]),
+                                           (4, "ring_parallel", []),
+                                           (8, "ring_parallel", [])])
+def test_scaling_gloo_more_ranks(ws, mode, extra):
+    """verify_collectives + float64-checked results at ws = 4 / 8."""
+    out = _torchrun(ws, "matmul_scaling_benchmark.py", "--device", "cpu", "--sizes", "520",
+                    "--iterations", "1", "--warmup", "1", "--dtype", "float32", "--mode", mode,
+                    "--check", *extra)
+    assert f"Collective operations verified successfully across {ws}" in out
+    assert "PASS" in out and "FAIL" not in out and "ERROR" not in out
+
+
 def test_batch_parallel_ws3_reports_real_batch(tmp_path):
     out = _torchrun(3, "matmul_scaling_benchmark.py", "--device", "cpu", "--sizes", "128",
                     "--iterations", "1", "--warmup", "1", "--dtype", "float32", "--mode",
