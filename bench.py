@@ -148,6 +148,44 @@ class Workload:
                         dist.all_gather_into_tensor(gathered, Cl)
             self.flops = flop_gemm
             self.global_batch, self.parallelism = 1, f"tp{ws}"
+        elif mode == "ring_parallel":
+            # Opt-in (not timed by default): all-gather-GEMM over the ring,
+            # models/ring_parallel.py. A row blocks rotate by P2P behind each hop's GEMM.
+            rs, sh = column_shard(n, ws, ctx.rank, align=256), column_shard(n, ws, ctx.rank, align=8)
+            A = self._rnd(n, n, seed=10_000)
+            Al = torch.zeros(rs.padded, n, device=dev, dtype=dt)
+            Al[:rs.width].copy_(A[rs.start:rs.stop])
+            del A
+            Bg = self._rnd(n, n, seed=10_001, b=True)
+            Bl = (torch.zeros(sh.padded, n, device=dev, dtype=dt).t() if dt == gemm.FP8
+                  else torch.zeros(n, sh.padded, device=dev, dtype=dt))
+            Bl[:, :sh.width].copy_(Bg[:, sh.start:sh.stop])
+            del Bg
+            rp = rs.padded
+            Cl = torch.empty(ws * rp, sh.padded, device=dev, dtype=odt)
+            R = [torch.empty_like(Al), torch.empty_like(Al)]
+            self.kernel = self._label(Al, Bl, Cl[:rp])
+            cs = CommStream(dev)
+            gdone = [new_event(dev) for _ in range(ws)]
+            rdone = [new_event(dev) for _ in range(max(ws - 1, 0))]
+            last = [None]
+            nxt, prv = (ctx.rank + 1) % ws, (ctx.rank - 1) % ws
+
+            def step():
+                cur = Al
+                for s in range(ws):
+                    if s > 0 and self.cuda:
+                        comp.wait_event(rdone[s - 1])
+                    if s < ws - 1:
+                        cs.exchange(cur, nxt, R[(s + 1) % 2], prv, after=last[0], done=rdone[s])
+                    j = (ctx.rank - s) % ws
+                    self._mm(cur, Bl, Cl[j * rp:(j + 1) * rp])
+                    gdone[s].record(comp)
+                    last[0] = gdone[s]
+                    if s < ws - 1:
+                        cur = R[(s + 1) % 2]
+            self.flops = flop_gemm
+            self.global_batch, self.parallelism = 1, f"ring{ws}"
         else:
             raise ValueError(mode)
         self.step = step
@@ -216,7 +254,7 @@ def main() -> int:
     ap.add_argument("--size", type=int, default=16384)
     ap.add_argument("--dtype", default="bfloat16", choices=list(DTYPES))
     ap.add_argument("--mode", default="independent",
-                    choices=["independent", "batch_parallel", "matrix_parallel"])
+                    choices=["independent", "batch_parallel", "matrix_parallel", "ring_parallel"])
     ap.add_argument("--overlap", action="store_true",
                     help="batch/matrix_parallel: hide the collective behind the GEMM chunks")
     ap.add_argument("--chunks", type=int, default=4)
@@ -239,7 +277,7 @@ def main() -> int:
     headline16k = dt == torch.bfloat16 and a.size == 16384 and cuda
 
     def vs_base(mode, value):
-        base = BASELINE_TFLOPS[mode].get(ws) if headline16k else None
+        base = BASELINE_TFLOPS.get(mode, {}).get(ws) if headline16k else None
         return round(value / base, 3) if base else None
 
     # Headline: the metric BASELINE.json names, measured first on a quiet node.
@@ -275,7 +313,7 @@ def main() -> int:
             "metric": METRIC, "value": round(value, 4), "unit": "TFLOPS",
             "n_gpus": ws, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms_step, 4), "higher_is_better": True,
-            "scaling": "strong" if a.mode == "matrix_parallel" else "weak",
+            "scaling": "strong" if a.mode in ("matrix_parallel", "ring_parallel") else "weak",
             "vs_baseline": vs_base(a.mode, value),
             "dtype": {"bfloat16": "bf16", "float16": "fp16", "float32": "fp32",
                       "float8_e4m3fn": "fp8_e4m3"}[a.dtype],
@@ -285,7 +323,8 @@ def main() -> int:
                        "global_batch": head["global_batch"], "seq_len": a.size,
                        "parallelism": head["parallelism"], "mode": a.mode,
                        "overlap": bool(a.overlap), "backend": a.backend, "kernel": head["kernel"]},
-            "per_gpu_tflops": round(value / ws, 2) if a.mode != "matrix_parallel" else None,
+            "per_gpu_tflops": (round(value / ws, 2)
+                               if a.mode not in ("matrix_parallel", "ring_parallel") else None),
             "vs_reference_1gpu_linear": round(value / (140.0 * ws), 3),
             "modes": modes,
         }

@@ -44,6 +44,16 @@ def test_bench_two_ranks(mode, extra, scaling, gb):
     assert d["value"] == pytest.approx(flops / (d["ms_per_step"] / 1e3) / 1e12, rel=0.02, abs=1e-4)
 
 
+@pytest.mark.parametrize("nproc", [2, 3])
+def test_bench_ring_parallel_opt_in(nproc):
+    d = _bench(nproc, "--size", "256", "--steps", "2", "--warmup", "1", "--mode", "ring_parallel",
+               "--extra-steps", "0")
+    assert d["config"]["parallelism"] == f"ring{nproc}" and d["scaling"] == "strong"
+    assert d["value"] == pytest.approx(2.0 * 256 ** 3 / (d["ms_per_step"] / 1e3) / 1e12,
+                                       rel=0.02, abs=1e-4)
+    assert d["vs_baseline"] is None and d["modes"] == {}
+
+
 def test_bench_four_ranks_batch_never_empty():
     d = _bench(4, "--size", "128", "--steps", "2", "--warmup", "1", "--mode", "batch_parallel",
                )

@@ -58,3 +58,10 @@ def test_two_ranks_share_gpu_bench_json():
     # the secondary modes ran on the same ranks: the other three scaling variants
     assert set(d["modes"]) == {"batch_parallel", "matrix_parallel", "matrix_parallel+overlap"}
     assert all(m["value"] > 0 for m in d["modes"].values())
+
+
+def test_two_ranks_share_gpu_bench_ring():
+    out = _run(2, "bench.py", "--gpus", "2", "--size", "2048", "--steps", "3", "--warmup", "1",
+               "--mode", "ring_parallel", "--extra-steps", "0")
+    d = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["parallelism"] == "ring2"
