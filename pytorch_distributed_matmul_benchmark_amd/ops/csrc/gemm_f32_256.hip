@@ -197,7 +197,7 @@ bool gemm_f32_256_supported(const GemmArgs& a, size_t align_a, size_t align_b, s
 hipError_t gemm_f32_256_launch(GemmArgs a, int variant, hipStream_t stream) {
   a.tiles_m = (a.M + kf32::BM - 1) / kf32::BM;
   a.tiles_n = (a.N + kf32::BN - 1) / kf32::BN;
-  a.supertile = (a.tiles_m % 16 == 0 && a.tiles_n % 16 == 0) ? 1 : 0;
+  a.supertile = choose_supertile(a.tiles_m, a.tiles_n);
   const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch;
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;

@@ -544,7 +544,7 @@ bool gemm_fp8_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_
 hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream) {
   a.tiles_m = (a.M + k8::BM - 1) / k8::BM;
   a.tiles_n = (a.N + k8::BN - 1) / k8::BN;
-  a.supertile = (a.tiles_m % 16 == 0 && a.tiles_n % 16 == 0) ? 1 : 0;
+  a.supertile = choose_supertile(a.tiles_m, a.tiles_n);
   const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch;
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;

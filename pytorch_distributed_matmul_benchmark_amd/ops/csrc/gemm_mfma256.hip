@@ -506,7 +506,7 @@ bool gemm256_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b
 hipError_t gemm256_launch(int dt, GemmArgs a, int sched, hipStream_t stream) {
   a.tiles_m = (a.M + k256::BM - 1) / k256::BM;
   a.tiles_n = (a.N + k256::BN - 1) / k256::BN;
-  a.supertile = (a.tiles_m % 16 == 0 && a.tiles_n % 16 == 0) ? 1 : 0;
+  a.supertile = choose_supertile(a.tiles_m, a.tiles_n);
   const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch;
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;

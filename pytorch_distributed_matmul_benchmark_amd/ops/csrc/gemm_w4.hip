@@ -321,7 +321,7 @@ bool gemm_w4_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b
 hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
   a.tiles_m = a.M / kw4::BM;
   a.tiles_n = a.N / kw4::BN;
-  a.supertile = (a.tiles_m % 16 == 0 && a.tiles_n % 16 == 0) ? 1 : 0;
+  a.supertile = choose_supertile(a.tiles_m, a.tiles_n);
   const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch;
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;

@@ -25,7 +25,8 @@ def _relerr(x, ref):
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 256), (1000, 1052, 384),
                                    (300, 200, 128), (2304, 2048, 1024), (256, 512, 256),
-                                   (768, 256, 640)])
+                                   (768, 256, 640),
+                                   (2048, 8192, 256), (8192, 2048, 256)])  # thin-grid super-tiles
 def test_fp8_exact_small_integers(M, N, K):
     g = torch.Generator(device="cuda").manual_seed(M + 7 * N + K)
     Af, Bf = _ints((M, K), g), _ints((K, N), g)

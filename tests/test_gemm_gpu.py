@@ -300,3 +300,25 @@ def test_w4_rejects_edge_tiles_and_auto_falls_back():
     assert gemm.kernel_for(A, B) == "pdmb_mfma256d_nn"
     with pytest.raises(RuntimeError):
         gemm.matmul(A, B, kernel="w4")
+
+
+# ---- thin grids: 8x32 / 32x8-tile super-tile rounds (map_tile supertile 2 / 3) ----
+
+@pytest.mark.parametrize("M,N,batch", [(2048, 8192, 1), (8192, 2048, 1), (2048, 8192, 2),
+                                       (8192, 2048, 3), (4096, 2048, 1)])
+@pytest.mark.parametrize("kernel,dtype", [("w4", "bfloat16"), ("w4", "float16"),
+                                          ("mfma256d", "bfloat16"), ("f32_256", "float32")])
+def test_thin_grid_supertiles_exact(M, N, batch, kernel, dtype):
+    """Every output tile is written exactly once under the thin-grid block->tile
+    maps (a mis-mapping leaves stale tiles or duplicates): integer data, exact
+    result. Shapes: row chunks of an overlap GEMM, ws=8 column shards."""
+    dt, K = DT[dtype], 256
+    g = torch.Generator(device="cuda").manual_seed(M + N + batch)
+    A = torch.randint(-3, 4, (batch, M, K), device="cuda", generator=g).to(dt)
+    B = torch.randint(-3, 4, (batch, K, N), device="cuda", generator=g).to(dt)
+    if batch == 1:
+        A, B = A[0], B[0]
+    C = torch.full(torch.broadcast_shapes(A.shape[:-1] + (N,)), float("nan"), device="cuda",
+                   dtype=dt)
+    gemm.matmul(A, B, out=C, kernel=kernel)
+    assert torch.equal(C, (A.double() @ B.double()).to(dt))
