@@ -85,7 +85,7 @@ struct GemmArgs {
   long long sA, sB, sC;
   int batch;
   int tiles_m, tiles_n;  // output tiles per batch element
-  int supertile;         // 1: XCD-aware 16x16 super-tile order, 2: 8x32, 3: 32x8, 0: grouped
+  int supertile;         // XCD-aware round order: 1 = 16x16 tiles, 2-5 thin rounds (map_tile), 0: grouped
   float alpha;           // fp8 only: C = alpha * (A @ B) (per-tensor scales folded)
   unsigned long long* dbg;  // diagnostic builds only (in-kernel stamps); nullptr otherwise
 };
@@ -137,14 +137,17 @@ __device__ __forceinline__ void dma16(u32x4 rsrc, uint32_t voff, uint32_t lds_ba
 // Super-tiles sweep N fastest so A panels stay Infinity-Cache resident.
 // Otherwise: grouped order with 16 tile-rows per group (chip-wide locality).
 // Thin grids (a row chunk of an overlap GEMM, a ws=8 column shard) keep the
-// 32-workgroup XCD blocks with a 256-tile round of another shape: supertile 2
-// = 8 x 32 tiles (XCDs 2 x 4 of 4x8 blocks), 3 = 32 x 8 (XCDs 4 x 2 of 8x4).
-// sub: XCD sub-block shape in 16x16 rounds, 0 = 4 (M) x 8 (N), 1 = 8 x 4
-// ("tall"), 2 = 2 x 16 ("wide").
+// 32-workgroup XCD blocks with a 256-tile round of another shape, given as
+// (XCD grid xm x xn) x (block bm x bn): supertile 2 = 8 x 32 tiles (2x4 of
+// 4x8), 3 = 32 x 8 (4x2 of 8x4), 4 = 4 x 64 (1x8 of 4x8), 5 = 64 x 4 (8x1 of
+// 8x4). sub: XCD sub-block shape in 16x16 rounds, 0 = 4 (M) x 8 (N),
+// 1 = 8 x 4 ("tall"), 2 = 2 x 16 ("wide").
 inline int choose_supertile(int tiles_m, int tiles_n) {
   if (tiles_m % 16 == 0 && tiles_n % 16 == 0) return 1;
   if (tiles_m % 8 == 0 && tiles_n % 32 == 0) return 2;
   if (tiles_m % 32 == 0 && tiles_n % 8 == 0) return 3;
+  if (tiles_m % 4 == 0 && tiles_n % 64 == 0) return 4;
+  if (tiles_m % 64 == 0 && tiles_n % 4 == 0) return 5;
   return 0;
 }
 
@@ -154,19 +157,17 @@ __device__ __forceinline__ void map_tile(const GemmArgs& a, int b, int& bz, int&
   if (a.supertile >= 2) {
     const int x = b & 7, j = b >> 3;
     const int round = j >> 5, i = j & 31;
-    const bool wide = a.supertile == 2;
-    const int st_n = a.tiles_n / (wide ? 32 : 8);
-    const int st_per_b = (a.tiles_m / (wide ? 8 : 32)) * st_n;
+    const int st = a.supertile;
+    const int xn = st == 2 ? 4 : st == 3 ? 2 : st == 4 ? 8 : 1;  // XCD grid columns
+    const int bn = (st == 2 || st == 4) ? 8 : 4, bm = 32 / bn;  // XCD block
+    const int SM = (8 / xn) * bm, SN = xn * bn;                   // round shape in tiles
+    const int st_n = a.tiles_n / SN;
+    const int st_per_b = (a.tiles_m / SM) * st_n;
     bz = round / st_per_b;
     const int s = round - bz * st_per_b;
     const int sr = s / st_n, sc = s - sr * st_n;
-    if (wide) {
-      tm = sr * 8 + (x >> 2) * 4 + (i >> 3);
-      tn = sc * 32 + (x & 3) * 8 + (i & 7);
-    } else {
-      tm = sr * 32 + (x >> 1) * 8 + (i >> 2);
-      tn = sc * 8 + (x & 1) * 4 + (i & 3);
-    }
+    tm = sr * SM + (x / xn) * bm + i / bn;
+    tn = sc * SN + (x % xn) * bn + i % bn;
   } else if (a.supertile) {
     const int x = b & 7, j = b >> 3;
     const int round = j >> 5, i = j & 31;
