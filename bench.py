@@ -25,6 +25,16 @@ BASELINE configs 3-5 (``--extra-steps 0`` skips them).
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
+
+``--gpus N > 1`` without torchrun self-launches N ranks (a child
+``torch.distributed.run``, started before anything touches the GPU) and exits
+with its code; under torchrun, ``WORLD_SIZE != --gpus`` is an error. At N > 1
+the job also times the headline GEMM on rank 0 alone (others at a barrier)
+and reports ``scaling_efficiency = value / (N x single_gpu_tflops)`` — the
+1 -> N curve's efficiency from one launch. Every mode's setup is agreed
+across ranks (a setup failure becomes an ``"error"`` entry, no hang); a
+failure inside a timed region exits that rank at once, so torchrun tears the
+job down in seconds (fault injection: ``PDMB_BENCH_FAULT=rank:mode:phase``).
 """
 from __future__ import annotations
 
@@ -41,12 +51,14 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from pytorch_distributed_matmul_benchmark_amd.ops import gemm  # noqa: E402
-from pytorch_distributed_matmul_benchmark_amd.parallel.comm import (CommStream,  # noqa: E402
-                                                                   new_event)
+from pytorch_distributed_matmul_benchmark_amd.parallel.comm import (  # noqa: E402
+    CommStream, new_event, stream_ctx)
+from pytorch_distributed_matmul_benchmark_amd.parallel.overlap import (  # noqa: E402
+    GatherOverlap, ReduceOverlap, compute_stream, gemm_chunks)
 from pytorch_distributed_matmul_benchmark_amd.parallel.dist import (  # noqa: E402
-    barrier, cleanup_distributed, setup_distributed)
+    DistContext, all_ok, barrier, cleanup_distributed, reduce_scalar, setup_distributed)
 from pytorch_distributed_matmul_benchmark_amd.parallel.partition import (  # noqa: E402
-    column_shard, effective_chunks, global_batch, local_batch, row_chunks)
+    column_shard, global_batch, local_batch)
 
 # Reference numbers (README.md:43-46): whole-system TFLOPS at 16k bf16.
 BASELINE_TFLOPS = {"independent": {1: 140.0, 2: 294.0},
@@ -69,8 +81,13 @@ class Workload:
         odt = gemm.out_dtype(dt)  # fp8 operands write a bf16 C
         self._g = torch.Generator(device=dev)
         flop_gemm = 2.0 * n * n * n
-        comp = torch.cuda.current_stream(dev) if self.cuda else None
         overlap = overlap and ws > 1
+        comp = torch.cuda.current_stream(dev) if self.cuda else None
+        self._mask = None
+        if overlap and self.cuda and a.comm_cus > 0:
+            # GEMM chunks on a CU-masked stream, RCCL gets the free CUs at once
+            comp, self._mask = compute_stream(dev, a.comm_cus)
+        self.comp = comp
 
         if mode == "independent":
             A, B = self._rnd(n, n, seed=2 * ctx.rank), self._rnd(n, n, seed=2 * ctx.rank + 1, b=True)
@@ -88,22 +105,12 @@ class Workload:
             C = torch.empty(lb, n, n, device=dev, dtype=odt)
             self.kernel = self._label(A, B, C)
             if overlap:
-                cs = CommStream(dev)
-                ch = effective_chunks(n, n, a.chunks) if self.cuda else a.chunks
-                units = [(b, s, e) for b in range(lb) for (s, e) in row_chunks(n, ch)]
-                ready = [new_event(dev) for _ in units]
-                done = [new_event(dev) for _ in units]
+                ov = ReduceOverlap(lb, gemm_chunks(n, n, a.chunks, dt, dev), dev)
 
                 def step():
-                    for u, (b, s, e) in enumerate(units):
-                        if self.cuda:
-                            comp.wait_event(done[u])
-                        self._mm(A[b, s:e], B[b], C[b, s:e])
-                        ready[u].record(comp)
-                        cs.all_reduce(C[b, s:e], after=ready[u], done=done[u])
-                    if self.cuda:
-                        for d in done:
-                            comp.wait_event(d)
+                    with stream_ctx(self.comp):
+                        ov.step(self._mm, A, B, C, self.comp)
+                    self._join()
             else:
                 def step():
                     self._mm(A, B, C)
@@ -122,23 +129,14 @@ class Workload:
             Cl = torch.empty(n, sh.padded, device=dev, dtype=odt)
             self.kernel = self._label(A, Bl, Cl)
             if overlap:
-                cs = CommStream(dev)
-                rc = row_chunks(n, effective_chunks(n, sh.padded, a.chunks) if self.cuda
-                                else a.chunks)
-                bufs = [torch.empty(ws * (e - s), sh.padded, device=dev, dtype=odt) for s, e in rc]
-                ready = [new_event(dev) for _ in rc]
-                done = [new_event(dev) for _ in rc]
+                ov = GatherOverlap(n, sh.padded, ws, dev, odt,
+                                   gemm_chunks(n, sh.padded, a.chunks, dt, dev),
+                                   pieces=a.comm_chunks, requested=a.chunks)
 
                 def step():
-                    for j, (s, e) in enumerate(rc):
-                        if self.cuda:
-                            comp.wait_event(done[j])
-                        self._mm(A[s:e], Bl, Cl[s:e])
-                        ready[j].record(comp)
-                        cs.all_gather_into(bufs[j], Cl[s:e], after=ready[j], done=done[j])
-                    if self.cuda:
-                        for d in done:
-                            comp.wait_event(d)
+                    with stream_ctx(self.comp):
+                        ov.step(self._mm, A, Bl, Cl, self.comp)
+                    self._join()
             else:
                 gathered = torch.empty(ws * n, sh.padded, device=dev, dtype=odt)
 
@@ -175,7 +173,7 @@ class Workload:
                 cur = Al
                 for s in range(ws):
                     if s > 0 and self.cuda:
-                        comp.wait_event(rdone[s - 1])
+                        self.comp.wait_event(rdone[s - 1])
                     if s < ws - 1:
                         cs.exchange(cur, nxt, R[(s + 1) % 2], prv, after=last[0], done=rdone[s])
                     j = (ctx.rank - s) % ws
@@ -208,6 +206,11 @@ class Workload:
         if (self.backend == "torch" or not self.cuda) and self.dt != gemm.FP8:
             return torch.matmul(A, B, out=out)
         return gemm.matmul(A, B, out=out)
+
+    def _join(self):
+        """The timing (current) stream waits for the masked compute stream."""
+        if self._mask is not None:
+            torch.cuda.current_stream(self.ctx.device).wait_stream(self.comp)
 
     def _label(self, A, B, C):
         if not self.cuda:
@@ -246,6 +249,116 @@ def _free(ctx) -> None:
         torch.cuda.empty_cache()
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _self_launch(a) -> int:
+    """``--gpus N > 1`` outside torchrun: start N ranks as a child
+    ``torch.distributed.run`` (the reference's launcher pattern,
+    run_scaling_benchmark.sh:23-31) and exit with its code. Nothing here has
+    touched the GPU (``import torch`` does not initialise HIP), so the child
+    ranks own their devices from scratch; the parent only waits."""
+    import subprocess
+
+    if a.device == "cuda" and a.dist_backend in ("auto", "nccl"):
+        ndev = torch.cuda.device_count()  # does not initialise HIP on this image
+        if ndev < a.gpus:
+            print(f"bench.py: --gpus {a.gpus} but only {ndev} GPU(s) visible; RCCL needs one GPU "
+                  f"per rank (use --dist-backend gloo to rehearse more ranks than GPUs)",
+                  file=sys.stderr, flush=True)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={a.master_port or _free_port()}", os.path.abspath(__file__),
+           *sys.argv[1:]]
+    env = dict(os.environ, PDMB_BENCH_CHILD="1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def _fault(ctx, key: str, phase: str) -> None:
+    """Fault injection for the failure-agreement tests: ``PDMB_BENCH_FAULT=
+    rank:mode:phase`` (mode ``*`` = any; phase ``setup`` | ``timed``) raises
+    on that rank at that point."""
+    spec = os.environ.get("PDMB_BENCH_FAULT")
+    if not spec:
+        return
+    r, m, p = spec.split(":")
+    if int(r) == ctx.rank and m in (key, "*") and p == phase:
+        raise RuntimeError(f"injected fault (rank {ctx.rank}, {key}, {phase})")
+
+
+def _die(ctx, key: str, exc: BaseException) -> None:
+    """A failure inside a timed region cannot be agreed on (the other ranks are
+    already blocked in a collective this rank will never join): report it and
+    exit at once, so torchrun's agent tears the job down in seconds instead of
+    every peer waiting out the process-group timeout."""
+    import traceback
+
+    print(f"[rank {ctx.rank}] {key} failed in the timed region: {exc!r}", file=sys.stderr,
+          flush=True)
+    traceback.print_exc(file=sys.stderr)
+    sys.stderr.flush()
+    sys.stdout.flush()
+    os._exit(1)
+
+
+def _measure(a, ctx, mode: str, overlap: bool, warmup: int, steps: int, key: str):
+    """Build (agreed across ranks) and time one workload. Returns
+    ``(tflops, seconds, workload_info)`` or ``(None, None, error_string)``."""
+    w, err = None, None
+    try:
+        _fault(ctx, key, "setup")
+        w = Workload(a, ctx, mode, overlap)
+    except Exception as e:  # OOM, unsupported shape, ...: every rank skips together
+        err = f"{type(e).__name__}: {e}"
+        print(f"[rank {ctx.rank}] {key} setup failed: {err}", file=sys.stderr, flush=True)
+    if not all_ok(ctx, err is None):
+        del w
+        _free(ctx)
+        return None, None, err or "failed on another rank"
+    try:
+        _fault(ctx, key, "timed")
+        el = w.timed(warmup, steps)
+    except Exception as e:
+        _die(ctx, key, e)
+    v = w.flops * steps / el / 1e12 if el > 0 else 0.0
+    info = dict(global_batch=w.global_batch, parallelism=w.parallelism, kernel=w.kernel)
+    del w
+    _free(ctx)
+    return v, el, info
+
+
+def _single_gpu_tflops(a, ctx):
+    """The '1 GPU' denominator of the scaling efficiency: the headline GEMM
+    timed on rank 0 alone (same K/W, same device) while every other rank
+    waits at a barrier — measured in the same job, so the 1 -> N curve needs
+    no second launch. The reference's own "Scaling efficiency" is rank
+    imbalance, not scaling (matmul_scaling_benchmark.py:315)."""
+    val = 0.0
+    barrier(ctx)
+    if ctx.rank == 0:
+        try:
+            one = DistContext(rank=0, world_size=1, local_rank=ctx.local_rank, device=ctx.device)
+            w = Workload(a, one, "independent", False)
+            el = w.timed(a.warmup, a.steps)
+            val = w.flops * a.steps / el / 1e12 if el > 0 else 0.0
+            del w
+        except Exception as e:  # a failed reference is "no efficiency", never a hang
+            print(f"[rank 0] single-GPU reference failed: {e!r}", file=sys.stderr, flush=True)
+            val = 0.0
+        _free(ctx)
+    barrier(ctx)
+    v = reduce_scalar(ctx, val, "sum")
+    return v if v > 0 else None
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -257,39 +370,66 @@ def main() -> int:
                     choices=["independent", "batch_parallel", "matrix_parallel", "ring_parallel"])
     ap.add_argument("--overlap", action="store_true",
                     help="batch/matrix_parallel: hide the collective behind the GEMM chunks")
-    ap.add_argument("--chunks", type=int, default=4)
+    ap.add_argument("--chunks", type=int, default=4,
+                    help="overlap: GEMM row chunks (capped so each chunk fills the chip)")
+    ap.add_argument("--comm-chunks", type=int, default=0,
+                    help="matrix_parallel --overlap: all-gather pieces per GEMM chunk "
+                         "(0: enough pieces for --chunks in total)")
+    ap.add_argument("--comm-cus", type=int, default=0,
+                    help="overlap: CUs kept free of GEMM workgroups for RCCL (CU-masked "
+                         "compute stream; 0 = no mask)")
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: torch.matmul + gloo, to exercise the multi-rank path without a GPU")
     ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"])
+    ap.add_argument("--master-port", type=int, default=0,
+                    help="self-launch rendezvous port (0: a free one)")
     ap.add_argument("--extra-steps", type=int, default=10,
                     help="timed steps for each secondary mode reported under \"modes\" "
                          "(batch_parallel / matrix_parallel, serialized and overlapped); 0: skip")
     ap.add_argument("--extra-warmup", type=int, default=3)
+    ap.add_argument("--no-scaling-ref", action="store_true",
+                    help="N > 1: skip the in-job 1-GPU reference (scaling_efficiency = null)")
     a = ap.parse_args()
 
-    ctx = setup_distributed(a.device, backend=None if a.dist_backend == "auto" else a.dist_backend)
+    if "WORLD_SIZE" not in os.environ:
+        if a.gpus > 1:
+            return _self_launch(a)
+    elif int(os.environ["WORLD_SIZE"]) != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}",
+              file=sys.stderr, flush=True)
+        return 2
+
+    ctx = setup_distributed(a.device, timeout_s=float(os.environ.get("PDMB_PG_TIMEOUT", "300")),
+                            backend=None if a.dist_backend == "auto" else a.dist_backend)
     cuda = ctx.device.type == "cuda"
     ws = ctx.world_size
-    if ws != a.gpus and ctx.is_main:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={ws}; using {ws}", file=sys.stderr)
     dt = DTYPES[a.dtype]
     headline16k = dt == torch.bfloat16 and a.size == 16384 and cuda
 
     def vs_base(mode, value):
         base = BASELINE_TFLOPS.get(mode, {}).get(ws) if headline16k else None
-        return round(value / base, 3) if base else None
+        return round(value / base, 3) if base and value is not None else None
 
     # Headline: the metric BASELINE.json names, measured first on a quiet node.
-    w = Workload(a, ctx, a.mode, a.overlap)
-    elapsed = w.timed(a.warmup, a.steps)
+    value, elapsed, head = _measure(a, ctx, a.mode, a.overlap, a.warmup, a.steps, a.mode)
+    if value is None:
+        if ctx.is_main:
+            print(f"bench.py: headline {a.mode} failed: {head}", file=sys.stderr, flush=True)
+        cleanup_distributed()
+        return 1
     ms_step = elapsed / max(a.steps, 1) * 1e3
-    value = w.flops * a.steps / elapsed / 1e12 if elapsed > 0 else 0.0
-    head = dict(global_batch=w.global_batch, parallelism=w.parallelism, kernel=w.kernel)
-    del w
-    _free(ctx)
+
+    single = value if ws == 1 and a.mode == "independent" else None
+    if ws > 1 and not a.no_scaling_ref:
+        single = _single_gpu_tflops(a, ctx)
+
+    def eff(v):
+        return round(v / (ws * single), 4) if single and v is not None else None
 
     # Secondary modes (BASELINE configs 4-5): same operands' shapes and dtype, own timing.
+    # At ws = 1 there is no collective to overlap: those entries are null, not a
+    # second copy of the serialized number.
     modes = {}
     if a.extra_steps > 0:
         for mode, ov in (("batch_parallel", False), ("batch_parallel", True),
@@ -297,16 +437,19 @@ def main() -> int:
             if mode == a.mode and ov == a.overlap:
                 continue
             key = mode + ("+overlap" if ov else "")
-            w = Workload(a, ctx, mode, ov)
-            el = w.timed(a.extra_warmup, a.extra_steps)
-            v = w.flops * a.extra_steps / el / 1e12 if el > 0 else 0.0
+            if ov and ws == 1:
+                modes[key] = None
+                continue
+            v, el, info = _measure(a, ctx, mode, ov, a.extra_warmup, a.extra_steps, key)
+            if v is None:
+                modes[key] = {"error": info}
+                continue
             modes[key] = {"value": round(v, 4), "ms_per_step": round(el / a.extra_steps * 1e3, 4),
                           "steps": a.extra_steps, "warmup": a.extra_warmup,
-                          "global_batch": w.global_batch, "parallelism": w.parallelism,
+                          "global_batch": info["global_batch"], "parallelism": info["parallelism"],
                           "scaling": "strong" if mode == "matrix_parallel" else "weak",
-                          "vs_baseline": vs_base(mode, v), "kernel": w.kernel}
-            del w
-            _free(ctx)
+                          "vs_baseline": vs_base(mode, v), "scaling_efficiency": eff(v),
+                          "kernel": info["kernel"]}
 
     if ctx.is_main:
         out = {
@@ -315,6 +458,8 @@ def main() -> int:
             "ms_per_step": round(ms_step, 4), "higher_is_better": True,
             "scaling": "strong" if a.mode in ("matrix_parallel", "ring_parallel") else "weak",
             "vs_baseline": vs_base(a.mode, value),
+            "scaling_efficiency": eff(value),
+            "single_gpu_tflops": round(single, 4) if single else None,
             "dtype": {"bfloat16": "bf16", "float16": "fp16", "float32": "fp32",
                       "float8_e4m3fn": "fp8_e4m3"}[a.dtype],
             "data": "synthetic (torch.randn N(0,1) operands, seeded per rank)",

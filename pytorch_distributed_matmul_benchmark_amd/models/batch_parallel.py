@@ -24,9 +24,10 @@ from __future__ import annotations
 
 import torch
 
-from ..parallel.comm import CommStream, current_stream, new_event
+from ..parallel.comm import current_stream, stream_ctx
+from ..parallel.overlap import ReduceOverlap, compute_stream, gemm_chunks
 from ..parallel.dist import DistContext
-from ..parallel.partition import effective_chunks, global_batch, local_batch, row_chunks
+from ..parallel.partition import global_batch, local_batch
 from ..utils.metrics import gemm_flops, tflops_from
 from ..utils.timing import SegmentTimer, Stopwatch, synchronize, time_loop_ms
 import torch.distributed as dist
@@ -34,14 +35,6 @@ import torch.distributed as dist
 from .common import (ModeResult, Workload, align_ranks, allreduced_relerr, gemm_fn, kernel_label,
                      out_dtype, randn, warmup)
 
-
-def _units(lb: int, n: int, chunks: int):
-    """(batch index, row start, row stop) overlap units."""
-    out = []
-    for b in range(lb):
-        for (s, e) in row_chunks(n, chunks):
-            out.append((b, s, e))
-    return out
 
 
 def run(w: Workload, ctx: DistContext) -> ModeResult:
@@ -87,26 +80,16 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
                          compute_only_tflops=tflops_from(flops, comp / 1e3), kernel=label,
                          extra=extra)
     else:
-        units = _units(lb, n, effective_chunks(n, n, w.chunks) if dev.type == "cuda" else w.chunks)
-        extra["units"] = len(units)
-        comm = CommStream(dev)
-        ready = [new_event(dev) for _ in units]
-        done = [new_event(dev) for _ in units]
-        started = [False] * len(units)
-        compute = current_stream(dev)
+        ov = ReduceOverlap(lb, gemm_chunks(n, n, w.chunks, w.dtype, dev), dev)
+        extra["units"] = len(ov.units)
+        compute, owner = compute_stream(dev, w.comm_cus)
+        extra["comm_cus"] = w.comm_cus
 
         def step():
-            for u, (b, s, e) in enumerate(units):
-                if started[u] and compute is not None:
-                    compute.wait_event(done[u])
-                mm(A[b, s:e], B[b], C[b, s:e])
-                ready[u].record(compute)
-                comm.all_reduce(C[b, s:e], after=ready[u], done=done[u])
-                started[u] = True
-            # close the iteration: compute stream joins the comm stream
-            if compute is not None:
-                for d in done:
-                    compute.wait_event(d)
+            with stream_ctx(compute):
+                ov.step(mm, A, B, C, compute)
+            if compute is not None:  # the timing stream joins the (masked) compute stream
+                current_stream(dev).wait_stream(compute)
 
         warmup(step, w, ctx)
         # compute-only reference time (reference: 10 GEMM-only iterations), taken
@@ -116,10 +99,10 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         comp = time_loop_ms(lambda: mm(A, B, C), k, 0, dev) / k
         align_ranks(ctx)
         sw = Stopwatch(dev)
-        sw.start(compute)
+        sw.start(current_stream(dev))
         for _ in range(w.iters):
             step()
-        sw.stop(compute)
+        sw.stop(current_stream(dev))
         avg = sw.elapsed_ms() / max(w.iters, 1)
         res = ModeResult(mode="batch_parallel", n=n, world_size=ws, avg_ms=avg,
                          flops_local=flops, flops_total=flops * ws,

@@ -35,6 +35,8 @@ class Workload:
     batch: int = 4              # batch_parallel requested global batch (rounded up to a multiple of ws)
     overlap: bool = False       # comm/compute overlap on a second stream
     chunks: int = 4             # overlap granularity (row chunks per GEMM)
+    comm_chunks: int = 0        # matrix_parallel overlap: all-gather pieces per GEMM chunk (0: auto)
+    comm_cus: int = 0           # overlap: CUs kept free of GEMM workgroups for RCCL (CU-masked stream)
     graph: bool = False         # independent: replay the timed loop as one hipGraph
     check: bool = False         # verify the result against a float64 reference
     min_warmup_ms: float = 0.0  # extend the warm-up until this much GPU time has run (DVFS)

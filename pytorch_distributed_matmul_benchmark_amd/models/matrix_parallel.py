@@ -16,18 +16,22 @@ Differences:
     ``[ws*N, shard]`` filled by ``all_gather_into_tensor`` (block r =
     C[:, r*shard:(r+1)*shard]); no per-iteration allocation and no list
     copy-out.
-  * ``overlap=True``: C_local is computed in row chunks; chunk j is
-    all-gathered on the high-priority comm stream while chunk j+1 is
-    computed (event-ordered). Gather layout: per chunk ``[ws*rows_j, shard]``.
+  * ``overlap=True``: C_local is computed in row chunks (``gemm_chunks``:
+    as many as still fill the chip, split-K included); chunk j is
+    all-gathered in ``comm_chunks`` pieces on the high-priority comm stream
+    while chunk j+1 is computed (event-ordered, parallel/overlap.py), the
+    GEMM optionally on a CU-masked stream (``comm_cus``). Gather layout: per
+    piece ``[ws*rows_p, shard]``.
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
 
-from ..parallel.comm import CommStream, current_stream, new_event
+from ..parallel.comm import current_stream, stream_ctx
+from ..parallel.overlap import GatherOverlap, compute_stream, gemm_chunks
 from ..parallel.dist import DistContext
-from ..parallel.partition import column_shard, effective_chunks, row_chunks
+from ..parallel.partition import column_shard
 from ..utils.metrics import gemm_flops, tflops_from
 from ..utils.timing import SegmentTimer, Stopwatch, synchronize, time_loop_ms
 from . import independent
@@ -103,37 +107,33 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         avg = comp + cm
         full = (lambda: assemble(gathered, n, ws))
     else:
-        rc = row_chunks(n, effective_chunks(n, sh.padded, w.chunks) if dev.type == "cuda"
-                        else w.chunks)
-        extra["chunks"] = len(rc)
-        bufs = [torch.empty((ws * (e - s), sh.padded), device=dev, dtype=out_dtype(w)) for s, e in rc]
-        cs = CommStream(dev)
-        ready = [new_event(dev) for _ in rc]
-        done = [new_event(dev) for _ in rc]
-        compute = current_stream(dev)
+        ov = GatherOverlap(n, sh.padded, ws, dev, out_dtype(w),
+                           gemm_chunks(n, sh.padded, w.chunks, w.dtype, dev),
+                           pieces=w.comm_chunks, requested=w.chunks)
+        extra["chunks"] = len(ov.chunks)
+        extra["comm_pieces"] = ov.n_pieces
+        extra["comm_cus"] = w.comm_cus
+        compute, owner = compute_stream(dev, w.comm_cus)
 
         def step():
-            for j, (s, e) in enumerate(rc):
-                mm(A[s:e], B_local, C_local[s:e])
-                ready[j].record(compute)
-                cs.all_gather_into(bufs[j], C_local[s:e], after=ready[j], done=done[j])
-            if compute is not None:
-                for d in done:
-                    compute.wait_event(d)
+            with stream_ctx(compute):
+                ov.step(mm, A, B_local, C_local, compute)
+            if compute is not None:  # the timing stream joins the (masked) compute stream
+                current_stream(dev).wait_stream(compute)
 
         warmup(step, w, ctx)
         align_ranks(ctx)
         sw = Stopwatch(dev)
-        sw.start(compute)
+        sw.start(current_stream(dev))
         for _ in range(w.iters):
             step()
-        sw.stop(compute)
+        sw.stop(current_stream(dev))
         avg = sw.elapsed_ms() / max(w.iters, 1)
         synchronize(dev)
         k = max(1, min(w.iters, 10))
         comp = time_loop_ms(lambda: mm(A, B_local, C_local), k, 1, dev) / k
         cm = max(avg - comp, 0.0)
-        full = (lambda: assemble(bufs, n, ws))
+        full = (lambda: assemble(ov.gathered(), n, ws))
 
     res = ModeResult(mode="matrix_parallel", n=n, world_size=ws, avg_ms=avg,
                      flops_local=flops_local, flops_total=flops_total,

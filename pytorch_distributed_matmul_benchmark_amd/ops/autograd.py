@@ -26,6 +26,8 @@ class _NativeMatmul(torch.autograd.Function):
         dA = dB = None
         if ctx.needs_input_grad[0]:
             dA = gemm.matmul(dC, B.transpose(-1, -2).contiguous())
+            if A.dim() == 2 and dA.dim() == 3:  # A broadcast over B's batch
+                dA = dA.sum(0)
         if ctx.needs_input_grad[1]:
             if A.dim() == 3:
                 dB = gemm.matmul(A.transpose(-1, -2).contiguous(), dC)

@@ -60,6 +60,43 @@ def _needs_build(out: Path, deps) -> bool:
     return any(Path(d).stat().st_mtime > t for d in deps)
 
 
+def experiments() -> bool:
+    """``PDMB_EXPERIMENTS=1``: also compile the A/B and timing-only diagnostic
+    kernels (api.h ``ExperimentKernel``). The default build ships without them."""
+    return os.environ.get("PDMB_EXPERIMENTS", "0") == "1"
+
+
+def source_files():
+    return ([CSRC / s for s in HIP_SOURCES + HOST_SOURCES] + sorted(CSRC.glob("*.h"))
+            + [Path(__file__)])
+
+
+def source_digest() -> str:
+    """Content hash of every source the extension is built from plus the build
+    flags. Stored next to the library (``stamp_path``) at build time and
+    compared by ``_native.load`` — content, not mtimes, so a copied tree
+    (gpurun snapshot, git checkout) is judged correctly."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for p in source_files():
+        h.update(p.name.encode())
+        h.update(p.read_bytes())
+    h.update(f"arch={ARCH};experiments={int(experiments())}".encode())
+    return h.hexdigest()
+
+
+def stamp_path() -> Path:
+    return HERE / f"{EXT_NAME}.sources.sha256"
+
+
+def is_stale() -> bool:
+    """True if the built library is missing or was built from other sources / flags."""
+    if not lib_path().exists() or not stamp_path().exists():
+        return True
+    return stamp_path().read_text().strip() != source_digest()
+
+
 def _run(cmd, verbose):
     if verbose:
         print(" ".join(str(c) for c in cmd), flush=True)
@@ -102,10 +139,15 @@ def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -
     """Compile every HIP/C++ source for gfx950 and link ``_C``. Returns the .so path."""
     headers = sorted(CSRC.glob("*.h"))
     out = lib_path()
-    all_src = [CSRC / s for s in HIP_SOURCES + HOST_SOURCES]
-    if not force and not _needs_build(out, all_src + headers + [Path(__file__)]):
+    digest = source_digest()
+    if not force and not is_stale():
         return out
     BUILD.mkdir(exist_ok=True)
+    # a flag change (PDMB_EXPERIMENTS) invalidates every object
+    flags_file = BUILD / "flags.txt"
+    flags = f"arch={ARCH};experiments={int(experiments())}"
+    if not flags_file.exists() or flags_file.read_text() != flags:
+        force = True
     inc, libdirs = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
     import torch
@@ -113,6 +155,8 @@ def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
     hip_flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
                  "-Wno-unused-result", "-munsafe-fp-atomics", f"-I{CSRC}"]
+    if experiments():
+        hip_flags.append("-DPDMB_EXPERIMENTS=1")
     host_flags = ["-O2", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
                   f"-DTORCH_EXTENSION_NAME={EXT_NAME}", "-DTORCH_API_INCLUDE_EXTENSION_H",
                   "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", f"-I{CSRC}",
@@ -144,6 +188,8 @@ def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -
         f"-L{torch_lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
         "-ltorch_python", "-lamdhip64", f"-Wl,-rpath,{torch_lib}"]
     _run(link, verbose)
+    flags_file.write_text(flags)
+    stamp_path().write_text(digest + "\n")
     return out
 
 

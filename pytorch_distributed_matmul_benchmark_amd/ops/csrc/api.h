@@ -6,31 +6,41 @@
 
 namespace pdmb {
 
+// Shipping kernels (the public `kernel=` surface of ops/gemm.py).
 enum Kernel : int {
   kAuto = 0,      // fastest kernel that supports the problem
-  kMfma256 = 1,   // gemm_mfma256.hip (LDS-DMA, 256x256, ping-pong)
   kGeneric = 2,   // gemm_generic.hip (any shape)
-  kMfma256b = 3,  // gemm_mfma256.hip, DMA issued in the read slot (SCHED 1)
-  kMfma256c = 4,  // SCHED 1 + fragment reads balanced over the read slots (SCHED 2)
-  kMfma256d = 9,  // SCHED 3: two quadrants (32 MFMAs) per compute slot, 4 barriers per K-tile
-  kF32_256 = 6,   // gemm_f32_256.hip: exact-fp32 MFMA, 256x256 LDS-DMA tile
-  kF32_256s = 7,  // same, DMA issue staggered between the two waves of a SIMD
-  kF32NoDma = 20,  // diagnostic: f32 K-loop without loads (timing only, wrong results)
-  kMfma256X1 = 10,  // SCHED 2 experiment builds (A/B only): 10 = per-cluster setprio,
-  kMfma256X2 = 11,  //   11 = static priority of waves 4..7,
-  kMfma256X4 = 13,  //   13 = XCD sub-block 8x4 (12 unused)
-  kMfma256Stamp = 5,  // diagnostic: SCHED 2 with in-kernel barrier-wait stamps (needs a debug buffer)
-  kFp8W4 = 16,    // gemm_fp8.hip experiment: 4 waves x 128x128, AGPR accumulators via asm MFMA
-  kFp8W4Diag = 17,  // diagnostic: kFp8W4 without the DMA wait (timing only, wrong results)
-  kFp8W4Diag2 = 18,  // diagnostic: kFp8W4 with no wait at all before the barrier
-  kFp8W4Diag3 = 19,  // diagnostic: kFp8W4 MFMAs + barriers only (no loads)
-  kMfmaW4 = 21,   // gemm_w4.hip: bf16/fp16 NN, 4 waves x 128x128, AGPR accumulators (M, N % 256)
-  kMfmaW4Tall = 22,  // experiment (A/B only): kMfmaW4 (bf16) with the 8x4 XCD sub-block
-  kMfmaW4Wide = 23,  // experiment (A/B only): kMfmaW4 (bf16) with the 2x16 XCD sub-block
-  kFp8W4Tall = 24,   // experiment (A/B only): kFp8W4 with the 8x4 XCD sub-block
-  kFp8W4Wide = 25,   // experiment (A/B only): kFp8W4 with the 2x16 XCD sub-block
-  kFp8 = 15,      // gemm_fp8.hip: e4m3 A [M,K] x column-major B, block-scaled MFMA 16x16x128, bf16 out
+  kF32_256s = 7,  // gemm_f32_256.hip: exact-fp32 MFMA, 256x256 LDS-DMA tile, staggered DMA
+  kMfma256d = 9,  // gemm_mfma256.hip SCHED 3: 8 waves, 256x256, edge tiles (any M, N % 8)
+  kFp8W4 = 16,    // gemm_fp8.hip: e4m3 A x column-major B, 4 waves x 128x128, bf16 out
+  kMfmaW4 = 21,   // gemm_w4.hip: bf16/fp16 NN, 4 waves x 128x128, AGPR acc, split-K (M, N % 256)
 };
+
+// Experiment / diagnostic ids (A/B and timing-only builds). Compiled and
+// dispatched only when the library is built with PDMB_EXPERIMENTS=1
+// (ops/build.py); the default build resolves every one of them to -1.
+enum ExperimentKernel : int {
+  kMfma256 = 1,       // SCHED 0 (ping-pong)
+  kMfma256b = 3,      // SCHED 1: DMA issued in the read slot
+  kMfma256c = 4,      // SCHED 2: fragment reads balanced over the read slots
+  kMfma256Stamp = 5,  // SCHED 2 with in-kernel barrier-wait stamps (needs a debug buffer)
+  kF32_256 = 6,       // exact-fp32 256x256 without the staggered DMA
+  kMfma256X1 = 10,    // SCHED 2 + per-cluster setprio
+  kMfma256X2 = 11,    // SCHED 2 + static priority of waves 4..7
+  kMfma256X4 = 13,    // SCHED 2 + XCD sub-block 8x4
+  kFp8 = 15,          // fp8 8-wave 256x256 (block-scaled MFMA 16x16x128)
+  kFp8W4Diag = 17,    // timing only (wrong results): kFp8W4 without the DMA wait
+  kFp8W4Diag2 = 18,   // timing only: no wait at all before the barrier
+  kFp8W4Diag3 = 19,   // timing only: MFMAs + barriers, no loads
+  kF32NoDma = 20,     // timing only: f32 K-loop without loads
+  kMfmaW4Tall = 22,   // kMfmaW4 (bf16) with the 8x4 XCD sub-block
+  kMfmaW4Wide = 23,   // kMfmaW4 (bf16) with the 2x16 XCD sub-block
+  kFp8W4Tall = 24,    // kFp8W4 with the 8x4 XCD sub-block
+  kFp8W4Wide = 25,    // kFp8W4 with the 2x16 XCD sub-block
+};
+
+// True iff this library was built with the experiment kernels.
+bool experiments_built();
 
 // dtype kFP8: A, B are OCP fp8 e4m3, B is COLUMN-major (ldb = distance between
 // columns, i.e. B is stored as Bt [N,K]), C is bf16 and C = alpha * (A @ B).
@@ -44,7 +54,26 @@ struct Problem {
   long long sA, sB, sC;
   int batch;
   float alpha = 1.0f;
+  // W4 split-K: K slices per output tile (0 = auto: split only under-filled
+  // grids, see choose_splitk; 1 = off). Ignored by the other kernels.
+  int splitk = 0;
+  // Caller-owned scratch of at least gemm_workspace_bytes(p, kernel) bytes
+  // (padded-path copies, split-K partials), stream-ordered with the launch.
+  void* workspace = nullptr;
+  size_t workspace_bytes = 0;
 };
+
+// Split-K arrival counters are a library resource: one zeroed block per
+// (device, stream), created on first use and left zeroed by every launch
+// (launches on one stream never overlap). kMaxSplitTiles bounds the tiles of
+// one split-K launch.
+constexpr int kMaxSplitTiles = 4096;
+
+// Scratch bytes `gemm(p, kernel, ...)` needs in p.workspace (0 if none).
+size_t gemm_workspace_bytes(const Problem& p, int kernel);
+
+// K slices the W4 kernel would use for this problem (1 = no split).
+int choose_splitk(const Problem& p);
 
 // Which kernel `kernel` (kAuto allowed) resolves to for this problem;
 // -1 if the requested kernel cannot run it.

@@ -65,12 +65,19 @@ pdmb::Problem make_problem(const at::Tensor& A, const at::Tensor& B, const at::T
   TORCH_CHECK(inner_ok(A) && (fp8 ? colmajor_ok(B) : inner_ok(B)) && inner_ok(C),
               fp8 ? "pdmb: fp8 needs row-major A / C and column-major B"
                   : "pdmb: innermost dim must be contiguous");
-  auto ld = [](const at::Tensor& t) {
-    int64_t l = t.stride(-2);
-    return std::max<int64_t>(l, std::max<int64_t>(t.size(-1), 1));
+  // Leading dimension = the real row stride. A row stride below the row
+  // length (expanded / overlapping views) would make the kernels address
+  // memory outside the tensor, so it is refused (ops/gemm.py makes such
+  // inputs contiguous first; an overlapping `out` is an error).
+  auto ld = [](const at::Tensor& t, const char* what) {
+    const int64_t rows = t.size(-2), cols = t.size(-1);
+    if (rows <= 1) return std::max<int64_t>(cols, 1);
+    TORCH_CHECK(t.stride(-2) >= cols, "pdmb: ", what, " row stride ", t.stride(-2),
+                " < row length ", cols, " (overlapping or expanded view)");
+    return t.stride(-2);
   };
-  TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31) && batch < (1LL << 31),
-              "pdmb: dimension too large");
+  TORCH_CHECK(!batched || C.size(0) <= 1 || C.stride(0) >= C.size(-2) * ld(C, "out"),
+              "pdmb: out batch stride overlaps (expanded or aliased output)");
   pdmb::Problem p{};
   p.dtype = dtype_code(A.scalar_type());
   p.A = A.data_ptr();
@@ -79,15 +86,16 @@ pdmb::Problem make_problem(const at::Tensor& A, const at::Tensor& B, const at::T
   p.M = (int)M;
   p.N = (int)N;
   p.K = (int)K;
-  p.lda = (int)ld(A);
+  p.lda = (int)ld(A, "A");
   if (fp8) {
+    TORCH_CHECK(N <= 1 || B.stride(-1) >= K, "pdmb: fp8 B column stride < K (overlapping view)");
     const int64_t lb = std::max<int64_t>(B.stride(-1), std::max<int64_t>(K, 1));
     p.ldb = (int)lb;  // distance between columns (Bt row stride)
   } else {
-    p.ldb = (int)ld(B);
+    p.ldb = (int)ld(B, "B");
   }
   p.alpha = (float)alpha;
-  p.ldc = (int)ld(C);
+  p.ldc = (int)ld(C, "out");
   p.sA = (batched && A.dim() == 3) ? A.stride(0) : 0;
   p.sB = (batched && B.dim() == 3) ? B.stride(0) : 0;
   p.sC = batched ? C.stride(0) : 0;
@@ -104,12 +112,26 @@ at::Tensor alloc_out(const at::Tensor& A, const at::Tensor& B) {
   return at::empty(shape, A.options().dtype(fp8 ? at::kBFloat16 : A.scalar_type()));
 }
 
+// Scratch for one launch from PyTorch's caching allocator on the launch
+// stream (padded copies, split-K partials): stream-ordered reuse, safe under
+// concurrent streams and torch.cuda.graph capture, never shared.
+at::Tensor workspace_for(pdmb::Problem& p, int kernel, const at::Tensor& like) {
+  const size_t need = pdmb::gemm_workspace_bytes(p, kernel);
+  if (!need) return at::Tensor();
+  at::Tensor ws = at::empty({(int64_t)need}, like.options().dtype(at::kByte));
+  p.workspace = ws.data_ptr();
+  p.workspace_bytes = need;
+  return ws;
+}
+
 at::Tensor matmul(const at::Tensor& A, const at::Tensor& B, c10::optional<at::Tensor> out,
-                  int64_t kernel, double alpha) {
+                  int64_t kernel, double alpha, int64_t splitk) {
   at::Tensor C = out.has_value() ? *out : alloc_out(A, B);
   pdmb::Problem p = make_problem(A, B, C, alpha);
+  p.splitk = (int)splitk;
   c10::hip::HIPGuard guard(A.device().index());
   hipStream_t s = c10::hip::getCurrentHIPStream(A.device().index()).stream();
+  at::Tensor ws = workspace_for(p, (int)kernel, A);
   int used = -1;
   hipError_t e = pdmb::gemm(p, (int)kernel, s, &used);
   TORCH_CHECK(used >= 0, "pdmb: kernel ", kernel, " cannot run this problem");
@@ -121,16 +143,64 @@ int64_t resolve(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, i
   return pdmb::resolve_kernel(make_problem(A, B, C), (int)kernel);
 }
 
+// K slices the W4 kernel would use (1 = no split; 0 if W4 does not run it).
+int64_t splitk_for(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t kernel,
+                   int64_t splitk) {
+  pdmb::Problem p = make_problem(A, B, C);
+  p.splitk = (int)splitk;
+  if (pdmb::resolve_kernel(p, (int)kernel) != pdmb::kMfmaW4) return 0;
+  return pdmb::choose_splitk(p);
+}
+
 // Total milliseconds for `iters` timed launches (after `warmup`).
 double bench(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t iters,
-             int64_t warmup, bool graph, int64_t kernel) {
+             int64_t warmup, bool graph, int64_t kernel, int64_t splitk) {
   pdmb::Problem p = make_problem(A, B, C);
+  p.splitk = (int)splitk;
   TORCH_CHECK(pdmb::resolve_kernel(p, (int)kernel) >= 0, "pdmb: kernel cannot run this problem");
   c10::hip::HIPGuard guard(A.device().index());
   hipStream_t s = c10::hip::getCurrentHIPStream(A.device().index()).stream();
+  at::Tensor ws = workspace_for(p, (int)kernel, A);  // lives across every timed launch
   float ms = 0.f;
   check_hip(pdmb::bench_gemm(p, (int)kernel, (int)iters, (int)warmup, graph, s, &ms), "bench_gemm");
   return (double)ms;
+}
+
+// A stream whose kernels may use only the CUs NOT in `excluded` (the GEMM
+// side of a comm/compute overlap: RCCL's workgroups get those CUs at once
+// instead of waiting for GEMM workgroups to retire). Bit i of the HIP CU mask
+// is CU i of the device's enumeration; `excluded` are those indices. Returns
+// the raw handle (wrap with torch.cuda.ExternalStream; free with
+// destroy_stream).
+int64_t create_cu_masked_stream(int64_t device, std::vector<int64_t> excluded) {
+  c10::hip::HIPGuard guard((c10::DeviceIndex)device);
+  hipDeviceProp_t prop;
+  check_hip(hipGetDeviceProperties(&prop, (int)device), "hipGetDeviceProperties");
+  const int ncu = prop.multiProcessorCount;
+  std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+  for (int i = 0; i < ncu; ++i) mask[i / 32] |= 1u << (i % 32);
+  for (int64_t i : excluded) {
+    TORCH_CHECK(i >= 0 && i < ncu, "pdmb: CU index ", i, " outside [0, ", ncu, ")");
+    mask[i / 32] &= ~(1u << (i % 32));
+  }
+  hipStream_t s = nullptr;
+  check_hip(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()),
+            "hipExtStreamCreateWithCUMask");
+  return (int64_t)(uintptr_t)s;
+}
+
+std::vector<int64_t> stream_cu_mask(int64_t stream, int64_t device) {
+  c10::hip::HIPGuard guard((c10::DeviceIndex)device);
+  hipDeviceProp_t prop;
+  check_hip(hipGetDeviceProperties(&prop, (int)device), "hipGetDeviceProperties");
+  std::vector<uint32_t> mask((prop.multiProcessorCount + 31) / 32, 0u);
+  check_hip(hipExtStreamGetCUMask((hipStream_t)(uintptr_t)stream, (uint32_t)mask.size(), mask.data()),
+            "hipExtStreamGetCUMask");
+  return std::vector<int64_t>(mask.begin(), mask.end());
+}
+
+void destroy_stream(int64_t stream) {
+  check_hip(hipStreamDestroy((hipStream_t)(uintptr_t)stream), "hipStreamDestroy");
 }
 
 std::string kernel_name(int64_t k) { return pdmb::kernel_name((int)k); }
@@ -152,20 +222,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) native GEMM kernels and timing loop";
   m.def("matmul", &matmul, "C = A @ B on gfx950 MFMA (fp8: C = alpha * A @ B, bf16 out)",
         py::arg("A"), py::arg("B"), py::arg("out") = py::none(), py::arg("kernel") = 0,
-        py::arg("alpha") = 1.0);
+        py::arg("alpha") = 1.0, py::arg("splitk") = 0);
   m.def("resolve", &resolve, "kernel id that would run (or -1)", py::arg("A"), py::arg("B"),
         py::arg("out"), py::arg("kernel") = 0);
+  m.def("splitk_for", &splitk_for, "W4 K slices for this problem (0: not W4)", py::arg("A"),
+        py::arg("B"), py::arg("out"), py::arg("kernel") = 0, py::arg("splitk") = 0);
   m.def("bench", &bench, "native hipEvent timing loop; returns total ms", py::arg("A"),
         py::arg("B"), py::arg("out"), py::arg("iters"), py::arg("warmup"),
-        py::arg("graph") = false, py::arg("kernel") = 0);
+        py::arg("graph") = false, py::arg("kernel") = 0, py::arg("splitk") = 0);
   m.def("kernel_name", &kernel_name);
   m.def("set_debug_buffer", &set_debug_buffer, py::arg("buf") = py::none());
-  m.attr("KERNEL_AUTO") = (int)pdmb::kAuto;
-  m.attr("KERNEL_MFMA256") = (int)pdmb::kMfma256;
-  m.attr("KERNEL_GENERIC") = (int)pdmb::kGeneric;
-  m.attr("KERNEL_MFMA256B") = (int)pdmb::kMfma256b;
-  m.attr("KERNEL_MFMA256C") = (int)pdmb::kMfma256c;
-  m.attr("KERNEL_MFMA256_STAMP") = (int)pdmb::kMfma256Stamp;
-  m.attr("KERNEL_F32_256") = (int)pdmb::kF32_256;
+  m.def("create_cu_masked_stream", &create_cu_masked_stream, py::arg("device"),
+        py::arg("excluded"));
+  m.def("stream_cu_mask", &stream_cu_mask, py::arg("stream"), py::arg("device"));
+  m.def("destroy_stream", &destroy_stream, py::arg("stream"));
+  m.attr("EXPERIMENTS") = pdmb::experiments_built();
+  m.attr("MAX_SPLIT_TILES") = pdmb::kMaxSplitTiles;
   m.attr("ARCH") = "gfx950";
 }

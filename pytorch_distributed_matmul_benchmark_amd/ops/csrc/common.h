@@ -88,6 +88,12 @@ struct GemmArgs {
   int supertile;         // XCD-aware round order: 1 = 16x16 tiles, 2-5 thin rounds (map_tile), 0: grouped
   float alpha;           // fp8 only: C = alpha * (A @ B) (per-tensor scales folded)
   unsigned long long* dbg;  // diagnostic builds only (in-kernel stamps); nullptr otherwise
+  // Split-K (W4 only; splitk <= 1 = off): K-tile range [slice * kt_per, +kt_per)
+  // per workgroup; the S slices of one output tile meet in `part` (fp32, S
+  // tile images: one slot per slice) and `flags` (2 counters per tile, zero between launches).
+  int splitk, kt_per;
+  float* part;
+  unsigned* flags;
 };
 
 // ---- LDS-DMA helpers (shared by the LDS-DMA kernels) ----------------------

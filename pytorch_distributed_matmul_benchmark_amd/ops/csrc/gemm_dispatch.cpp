@@ -59,44 +59,150 @@ static bool generic_vec_ok(const Problem& p) {
   return true;
 }
 
+bool experiments_built() {
+#ifdef PDMB_EXPERIMENTS
+  return true;
+#else
+  return false;
+#endif
+}
+
+static bool is_fp8_kernel(int k) {
+  return k == kFp8W4 || k == kFp8 || k == kFp8W4Diag || k == kFp8W4Diag2 || k == kFp8W4Diag3 ||
+         k == kFp8W4Tall || k == kFp8W4Wide;
+}
+
+static bool is_experiment(int k) {
+  switch (k) {
+    case kMfma256: case kMfma256b: case kMfma256c: case kMfma256Stamp: case kF32_256:
+    case kMfma256X1: case kMfma256X2: case kMfma256X4: case kFp8: case kFp8W4Diag:
+    case kFp8W4Diag2: case kFp8W4Diag3: case kF32NoDma: case kMfmaW4Tall: case kMfmaW4Wide:
+    case kFp8W4Tall: case kFp8W4Wide:
+      return true;
+    default:
+      return false;
+  }
+}
+
 int resolve_kernel(const Problem& p, int kernel) {
+  if (is_experiment(kernel) && !experiments_built()) return -1;
   const GemmArgs a = to_args(p);
-  if (p.dtype == kFP8)  // one kernel, no generic / padded fallback
-    return (kernel == kAuto || kernel == kFp8 || kernel == kFp8W4 || kernel == kFp8W4Diag ||
-                    kernel == kFp8W4Diag2 || kernel == kFp8W4Diag3 || kernel == kFp8W4Tall ||
-                    kernel == kFp8W4Wide) &&
+  if (p.dtype == kFP8)  // fp8 kernels only; no generic / padded fallback
+    return (kernel == kAuto || is_fp8_kernel(kernel)) &&
                    gemm_fp8_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C)
                ? (kernel == kAuto ? kFp8W4 : kernel)
                : -1;
-  if (kernel == kFp8 || kernel == kFp8W4 || kernel == kFp8W4Diag || kernel == kFp8W4Diag2 ||
-      kernel == kFp8W4Diag3 || kernel == kFp8W4Tall || kernel == kFp8W4Wide)
-    return -1;
+  if (is_fp8_kernel(kernel)) return -1;
   const bool fast = gemm256_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
+  const bool w4 = gemm_w4_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   const bool f32fast = p.dtype == kF32 &&
                        gemm_f32_256_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
-  // Auto: the 4-wave kernel where the tiles are whole (M, N % 256; +4.5 % over
-  // SCHED 3 at 16k, profiles/r1_s4_w4_ab.jsonl), SCHED 3 for edge tiles.
-  if (kernel == kAuto) {
-    if (fast && gemm_w4_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C)) return kMfmaW4;
-    return fast ? kMfma256d : (f32fast ? kF32_256s : kGeneric);
+  switch (kernel) {
+    // Auto: the 4-wave kernel where the tiles are whole (M, N % 256; +4.5 %
+    // over SCHED 3 at 16k, profiles/r1_s4_w4_ab.jsonl), SCHED 3 for edge tiles.
+    case kAuto: return (fast && w4) ? kMfmaW4 : fast ? kMfma256d : f32fast ? kF32_256s : kGeneric;
+    case kGeneric: return kGeneric;
+    case kMfma256d: return fast ? kMfma256d : -1;
+    case kMfmaW4: return w4 ? kMfmaW4 : -1;
+    case kF32_256s: return f32fast ? kF32_256s : -1;
+#ifdef PDMB_EXPERIMENTS
+    case kF32_256: case kF32NoDma: return f32fast ? kernel : -1;
+    case kMfma256: case kMfma256b: case kMfma256c: return fast ? kernel : -1;
+    case kMfma256X1: case kMfma256X2: case kMfma256X4: case kMfma256Stamp:
+      return (fast && p.dtype == kBF16) ? kernel : -1;
+    case kMfmaW4Tall: case kMfmaW4Wide: return (p.dtype == kBF16 && w4) ? kernel : -1;
+#endif
+    default: return -1;
   }
-  if (kernel == kF32_256) return f32fast ? kF32_256 : -1;
-  if (kernel >= kMfma256X1 && kernel <= kMfma256X4)
-    return (fast && p.dtype == kBF16) ? kernel : -1;
-  if (kernel == kF32_256s) return f32fast ? kF32_256s : -1;
-  if (kernel == kF32NoDma) return f32fast ? kF32NoDma : -1;
-  if (kernel == kMfma256) return fast ? kMfma256 : -1;
-  if (kernel == kMfma256b) return fast ? kMfma256b : -1;
-  if (kernel == kMfma256c) return fast ? kMfma256c : -1;
-  if (kernel == kMfma256d) return fast ? kMfma256d : -1;
-  if (kernel == kMfmaW4)
-    return gemm_w4_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C) ? kMfmaW4 : -1;
-  if (kernel == kMfmaW4Tall || kernel == kMfmaW4Wide)
-    return (p.dtype == kBF16 && gemm_w4_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C))
-               ? kernel : -1;
-  if (kernel == kMfma256Stamp) return (fast && p.dtype == kBF16) ? kMfma256Stamp : -1;
-  if (kernel == kGeneric) return kGeneric;
-  return -1;
+}
+
+// ---- split-K (W4) -------------------------------------------------------
+// A grid of T 256x256 tiles fills the 256 CUs (1 workgroup / CU) only if T is
+// a multiple of 256: the matrix_parallel column shards at ws >= 4 for the
+// reference's default sizes (matmul_scaling_benchmark.py:179-188, :351) have
+// T = 32 / 128 (4k / 8k at ws = 8), so one workgroup per tile leaves 1/8 or
+// 1/2 of the chip idle. Splitting K over S workgroups per tile multiplies the
+// grid by S. Model, in K-tile times of one workgroup: a launch costs
+//   waves(T * S) * (ceil(nk / S) + kFixed + kMeet * (S - 1) [S > 1])
+// (kMeet: the last slice's read of one 256 KiB fp32 slot, kFixed: prologue
+// + epilogue); pick the cheapest S in {1, 2, 4, 8} with >= kMinKt K-tiles per
+// slice. Measured constants: profiles/r2_splitk_*.
+static constexpr double kFixed = 2.0, kMeet = 1.5;
+static constexpr int kMinKt = 4;
+
+int choose_splitk(const Problem& p) {
+  if (p.M % 256 || p.N % 256 || p.K % 64 || p.K <= 0) return 1;
+  const long long T = (long long)(p.M / 256) * (p.N / 256) * (p.batch < 1 ? 1 : p.batch);
+  const int nk = p.K / 64;
+  if (p.splitk > 0) return p.splitk;
+  if (T <= 0 || T > kMaxSplitTiles) return 1;
+  auto cost = [&](int S) {
+    const long long waves = (T * S + 255) / 256;
+    const int per = (nk + S - 1) / S;
+    return (double)waves * (per + kFixed + (S > 1 ? kMeet * (S - 1) : 0.0));
+  };
+  int best = 1;
+  double bc = cost(1);
+  for (int S = 2; S <= 8; S *= 2) {
+    const int per = (nk + S - 1) / S;
+    if (per < kMinKt || (S - 1) * per >= nk) break;
+    const double c = cost(S);
+    if (c < bc * 0.97) {  // split only for a clear win
+      best = S;
+      bc = c;
+    }
+  }
+  return best;
+}
+
+static size_t splitk_bytes(const Problem& p, int S) {
+  if (S <= 1) return 0;
+  const long long T = (long long)(p.M / 256) * (p.N / 256) * (p.batch < 1 ? 1 : p.batch);
+  return (size_t)T * S * 256 * 256 * sizeof(float);  // one slot per slice (the last's unused)
+}
+
+// Per-(device, stream) split-K counters (2 per tile), zeroed once on the
+// stream before first use; never freed (64 KiB each). Returns nullptr if the
+// stream is being captured and has none yet (hipMalloc is not capturable):
+// the caller then runs unsplit.
+static unsigned* stream_counters(hipStream_t s) {
+  static std::mutex mu;
+  static std::unordered_map<unsigned long long, unsigned*>* map =
+      new std::unordered_map<unsigned long long, unsigned*>();  // leaked on purpose
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  const unsigned long long key = ((unsigned long long)(uintptr_t)s << 8) ^ (unsigned)dev;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = map->find(key);
+  if (it != map->end()) return it->second;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+  unsigned* c = nullptr;
+  const size_t bytes = 2 * sizeof(unsigned) * kMaxSplitTiles;
+  if (hipMalloc(&c, bytes) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(c, 0, bytes, s) != hipSuccess) {
+    (void)hipFree(c);
+    return nullptr;
+  }
+  (*map)[key] = c;
+  return c;
+}
+
+static hipError_t w4_launch(const Problem& p, GemmArgs a, void* part, size_t part_bytes,
+                            hipStream_t stream, int sub = 0) {
+  int S = choose_splitk(p);
+  if (S > 1) {
+    unsigned* flags = stream_counters(stream);
+    if (!flags || part_bytes < splitk_bytes(p, S) || !part) {
+      if (p.splitk > 1) return hipErrorInvalidValue;  // explicitly requested: no silent change
+      S = 1;
+    } else {
+      a.part = (float*)part;
+      a.flags = flags;
+    }
+  }
+  a.splitk = S;
+  return gemm_w4_launch(p.dtype, a, stream, sub);
 }
 
 // ---- padded fast path -------------------------------------------------------
@@ -105,42 +211,14 @@ int resolve_kernel(const Problem& p, int kernel) {
 // dimension / base is misaligned is copied into zero-padded, aligned
 // workspace operands and run on the fast kernel (exact: the padding only adds
 // zero products). The copies are O(MK + KN + MN) against O(MNK) of MFMA work.
+// The workspace is the caller's (Problem::workspace, sized by
+// gemm_workspace_bytes), so concurrent streams and graph captures never share
+// or reallocate it.
 static constexpr double kPadMinFlops = 2147483648.0;  // 2^31
 
 static int pad_k(int dt) { return dt == kF32 ? 32 : 64; }
 static int pad_n(int dt) { return dt == kF32 ? 4 : 8; }
 static long long round_up(long long x, long long m) { return (x + m - 1) / m * m; }
-
-struct Workspace {
-  void* ptr = nullptr;
-  size_t bytes = 0;
-};
-
-// One growing workspace per device, reused across calls (stream-ordered use
-// only; growing synchronises the device, which never happens inside a
-// steady-state timed loop because warm-up calls size it first).
-static hipError_t workspace(size_t bytes, void** out) {
-  static std::mutex mu;
-  static std::unordered_map<int, Workspace> ws;
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  std::lock_guard<std::mutex> lk(mu);
-  Workspace& w = ws[dev];
-  if (w.bytes < bytes) {
-    if (w.ptr) {
-      if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
-      (void)hipFree(w.ptr);
-      w.ptr = nullptr;
-      w.bytes = 0;
-    }
-    const size_t want = (size_t)round_up((long long)bytes, 1 << 21);
-    if ((e = hipMalloc(&w.ptr, want)) != hipSuccess) return e;
-    w.bytes = want;
-  }
-  *out = w.ptr;
-  return hipSuccess;
-}
 
 // dst[r][c] = (r < rows && c < cols) ? src[r][c] : 0 for r < drows, c < dcols.
 // dst rows are 16-B aligned (ldd % VEC == 0); each thread writes one 16-B
@@ -199,56 +277,93 @@ static bool wants_padding(const Problem& p, int kernel) {
   return resolve_kernel(p, kAuto) == kGeneric;
 }
 
-static hipError_t gemm_padded(const Problem& p, hipStream_t stream, int* used) {
+// The zero-padded problem `gemm_padded` runs (operands in the workspace).
+struct Padded {
+  Problem q;
+  size_t a_bytes, b_bytes, c_bytes, a_el, b_el, c_el;
+};
+
+static Padded padded_problem(const Problem& p, char* w) {
+  Padded d{};
   const size_t es = p.dtype == kF32 ? 4 : 2;
   const int batch = p.batch < 1 ? 1 : p.batch;
   const long long Kp = round_up(p.K, pad_k(p.dtype)), Np = round_up(p.N, pad_n(p.dtype));
-  const size_t a_el = (size_t)p.M * Kp, b_el = (size_t)Kp * Np, c_el = (size_t)p.M * Np;
-  const size_t a_bytes = round_up(a_el * es * batch, 256), b_bytes = round_up(b_el * es * batch, 256);
-  const size_t c_bytes = round_up(c_el * es * batch, 256);
-  void* w = nullptr;
-  hipError_t e = workspace(a_bytes + b_bytes + c_bytes, &w);
-  if (e != hipSuccess) return e;
-  char* Ap = (char*)w;
-  char* Bp = Ap + a_bytes;
-  char* Cp = Bp + b_bytes;
-  const bool f32 = p.dtype == kF32;
-  for (int b = 0; b < batch; ++b) {
-    const char* A = (const char*)p.A + (size_t)b * p.sA * es;
-    const char* B = (const char*)p.B + (size_t)b * p.sB * es;
-    char* Ad = Ap + b * a_el * es;
-    char* Bd = Bp + b * b_el * es;
-    e = f32 ? pad_copy_launch<float>(A, p.lda, p.M, p.K, Ad, Kp, p.M, (int)Kp, stream)
-            : pad_copy_launch<unsigned short>(A, p.lda, p.M, p.K, Ad, Kp, p.M, (int)Kp, stream);
-    if (e != hipSuccess) return e;
-    e = f32 ? pad_copy_launch<float>(B, p.ldb, p.K, p.N, Bd, Np, (int)Kp, (int)Np, stream)
-            : pad_copy_launch<unsigned short>(B, p.ldb, p.K, p.N, Bd, Np, (int)Kp, (int)Np, stream);
-    if (e != hipSuccess) return e;
+  d.a_el = (size_t)p.M * Kp;
+  d.b_el = (size_t)Kp * Np;
+  d.c_el = (size_t)p.M * Np;
+  d.a_bytes = round_up(d.a_el * es * batch, 256);
+  d.b_bytes = round_up(d.b_el * es * batch, 256);
+  d.c_bytes = round_up(d.c_el * es * batch, 256);
+  Problem& q = d.q;
+  q = p;
+  q.A = w;
+  q.B = w ? w + d.a_bytes : nullptr;
+  q.C = w ? w + d.a_bytes + d.b_bytes : nullptr;
+  if (!w) {  // sizing only: any 256-B aligned stand-in passes the alignment checks
+    q.A = q.B = q.C = (void*)(uintptr_t)256;
   }
-  Problem q = p;
-  q.A = Ap;
-  q.B = Bp;
-  q.C = Cp;
   q.K = (int)Kp;
   q.N = (int)Np;
   q.lda = (int)Kp;
   q.ldb = (int)Np;
   q.ldc = (int)Np;
-  q.sA = (long long)a_el;
-  q.sB = (long long)b_el;
-  q.sC = (long long)c_el;
+  q.sA = (long long)d.a_el;
+  q.sB = (long long)d.b_el;
+  q.sC = (long long)d.c_el;
   q.batch = batch;
+  q.workspace = nullptr;
+  q.workspace_bytes = 0;
+  return d;
+}
+
+size_t gemm_workspace_bytes(const Problem& p, int kernel) {
+  if (wants_padding(p, kernel)) {
+    const Padded d = padded_problem(p, nullptr);
+    const size_t copies = d.a_bytes + d.b_bytes + d.c_bytes;
+    return copies + (resolve_kernel(d.q, kAuto) == kMfmaW4 ? splitk_bytes(d.q, choose_splitk(d.q)) : 0);
+  }
+  if (resolve_kernel(p, kernel) == kMfmaW4 || (kernel == kMfmaW4Tall || kernel == kMfmaW4Wide))
+    return splitk_bytes(p, choose_splitk(p));
+  return 0;
+}
+
+static hipError_t gemm_padded(const Problem& p, hipStream_t stream, int* used) {
+  if (!p.workspace || p.workspace_bytes < gemm_workspace_bytes(p, kAuto)) return hipErrorInvalidValue;
+  const size_t es = p.dtype == kF32 ? 4 : 2;
+  const Padded d = padded_problem(p, (char*)p.workspace);
+  const Problem& q = d.q;
+  char* Ap = (char*)q.A;
+  char* Bp = (char*)q.B;
+  char* Cp = (char*)q.C;
+  const int batch = q.batch;
+  const int Kp = q.K, Np = q.N;
+  const bool f32 = p.dtype == kF32;
+  hipError_t e;
+  for (int b = 0; b < batch; ++b) {
+    const char* A = (const char*)p.A + (size_t)b * p.sA * es;
+    const char* B = (const char*)p.B + (size_t)b * p.sB * es;
+    char* Ad = Ap + b * d.a_el * es;
+    char* Bd = Bp + b * d.b_el * es;
+    e = f32 ? pad_copy_launch<float>(A, p.lda, p.M, p.K, Ad, Kp, p.M, Kp, stream)
+            : pad_copy_launch<unsigned short>(A, p.lda, p.M, p.K, Ad, Kp, p.M, Kp, stream);
+    if (e != hipSuccess) return e;
+    e = f32 ? pad_copy_launch<float>(B, p.ldb, p.K, p.N, Bd, Np, Kp, Np, stream)
+            : pad_copy_launch<unsigned short>(B, p.ldb, p.K, p.N, Bd, Np, Kp, Np, stream);
+    if (e != hipSuccess) return e;
+  }
   const int k = resolve_kernel(q, kAuto);
   if (used) *used = k;
   if (k == kGeneric || k < 0) return hipErrorInvalidValue;  // cannot happen: q is aligned
   GemmArgs a = to_args(q);
+  char* part = Cp + d.c_bytes;
+  const size_t part_bytes = p.workspace_bytes - (d.a_bytes + d.b_bytes + d.c_bytes);
   e = k == kF32_256s  ? gemm_f32_256_launch(a, 1, stream)
-      : k == kMfmaW4 ? gemm_w4_launch(q.dtype, a, stream)
+      : k == kMfmaW4 ? w4_launch(q, a, part, part_bytes, stream)
                      : gemm256_launch(q.dtype, a, 4, stream);
   if (e != hipSuccess) return e;
   for (int b = 0; b < batch; ++b) {
     char* C = (char*)p.C + (size_t)b * p.sC * es;
-    const char* Cs = Cp + b * c_el * es;
+    const char* Cs = Cp + b * d.c_el * es;
     e = f32 ? unpad_copy_launch<float>(Cs, Np, p.M, p.N, C, p.ldc, stream)
             : unpad_copy_launch<unsigned short>(Cs, Np, p.M, p.N, C, p.ldc, stream);
     if (e != hipSuccess) return e;
@@ -273,26 +388,31 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     }
     return hipSuccess;
   }
-  if (k == kFp8) return gemm_fp8_launch(a, 0, stream);
-  if (k == kFp8W4) return gemm_fp8_launch(a, 1, stream);
-  if (k == kFp8W4Diag) return gemm_fp8_launch(a, 9, stream);
-  if (k == kFp8W4Diag2) return gemm_fp8_launch(a, 10, stream);
-  if (k == kFp8W4Diag3) return gemm_fp8_launch(a, 11, stream);
-  if (k == kFp8W4Tall) return gemm_fp8_launch(a, 12, stream);
-  if (k == kFp8W4Wide) return gemm_fp8_launch(a, 13, stream);
-  if (k == kMfma256) return gemm256_launch(p.dtype, a, 0, stream);
-  if (k == kMfma256b) return gemm256_launch(p.dtype, a, 1, stream);
-  if (k == kMfma256c) return gemm256_launch(p.dtype, a, 2, stream);
-  if (k == kMfma256d) return gemm256_launch(p.dtype, a, 4, stream);
-  if (k == kMfmaW4) return gemm_w4_launch(p.dtype, a, stream);
-  if (k == kMfmaW4Tall) return gemm_w4_launch(p.dtype, a, stream, 1);
-  if (k == kMfmaW4Wide) return gemm_w4_launch(p.dtype, a, stream, 2);
-  if (k == kMfma256Stamp) return gemm256_launch(p.dtype, a, 3, stream);
-  if (k == kF32_256) return gemm_f32_256_launch(a, 0, stream);
-  if (k >= kMfma256X1 && k <= kMfma256X4) return gemm256_launch(p.dtype, a, 10 + (k - kMfma256X1 + 1), stream);
-  if (k == kF32_256s) return gemm_f32_256_launch(a, 1, stream);
-  if (k == kF32NoDma) return gemm_f32_256_launch(a, 9, stream);
-  return gemm_generic_launch(p.dtype, a, generic_vec_ok(p), stream);
+  switch (k) {
+    case kFp8W4: return gemm_fp8_launch(a, 1, stream);
+    case kMfma256d: return gemm256_launch(p.dtype, a, 4, stream);
+    case kMfmaW4: return w4_launch(p, a, p.workspace, p.workspace_bytes, stream);
+    case kF32_256s: return gemm_f32_256_launch(a, 1, stream);
+#ifdef PDMB_EXPERIMENTS
+    case kFp8: return gemm_fp8_launch(a, 0, stream);
+    case kFp8W4Diag: return gemm_fp8_launch(a, 9, stream);
+    case kFp8W4Diag2: return gemm_fp8_launch(a, 10, stream);
+    case kFp8W4Diag3: return gemm_fp8_launch(a, 11, stream);
+    case kFp8W4Tall: return gemm_fp8_launch(a, 12, stream);
+    case kFp8W4Wide: return gemm_fp8_launch(a, 13, stream);
+    case kMfma256: return gemm256_launch(p.dtype, a, 0, stream);
+    case kMfma256b: return gemm256_launch(p.dtype, a, 1, stream);
+    case kMfma256c: return gemm256_launch(p.dtype, a, 2, stream);
+    case kMfma256Stamp: return gemm256_launch(p.dtype, a, 3, stream);
+    case kMfmaW4Tall: return w4_launch(p, a, p.workspace, p.workspace_bytes, stream, 1);
+    case kMfmaW4Wide: return w4_launch(p, a, p.workspace, p.workspace_bytes, stream, 2);
+    case kF32_256: return gemm_f32_256_launch(a, 0, stream);
+    case kF32NoDma: return gemm_f32_256_launch(a, 9, stream);
+    case kMfma256X1: case kMfma256X2: case kMfma256X4:
+      return gemm256_launch(p.dtype, a, 10 + (k - kMfma256X1 + 1), stream);
+#endif
+    default: return gemm_generic_launch(p.dtype, a, generic_vec_ok(p), stream);
+  }
 }
 
 hipError_t bench_gemm(const Problem& p, int kernel, int iters, int warmup, bool use_graph,
@@ -308,6 +428,9 @@ hipError_t bench_gemm(const Problem& p, int kernel, int iters, int warmup, bool 
     // capture mode (other libraries may enqueue on it concurrently).
     hipStream_t cap;
     if ((e = hipStreamCreateWithFlags(&cap, hipStreamNonBlocking)) != hipSuccess) return e;
+    // Split-K counters cannot be created inside a capture: make them now.
+    (void)stream_counters(cap);
+    if ((e = hipStreamSynchronize(cap)) != hipSuccess) return e;
     e = hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal);
     if (e == hipSuccess) {
       for (int i = 0; i < iters && e == hipSuccess; ++i) e = gemm(p, kernel, cap, nullptr);
@@ -345,38 +468,22 @@ hipError_t bench_gemm(const Problem& p, int kernel, int iters, int warmup, bool 
 
 const char* kernel_name(int kernel) {
   switch (kernel) {
-    case kMfma256:
-      return "pdmb_mfma256_nn";
-    case kGeneric:
-      return "pdmb_generic_nn";
-    case kMfma256b:
-      return "pdmb_mfma256b_nn";
-    case kMfma256c:
-      return "pdmb_mfma256c_nn";
-    case kMfma256d:
-      return "pdmb_mfma256d_nn";
-    case kMfma256Stamp:
-      return "pdmb_mfma256c_stamp";
-    case kF32_256:
-      return "pdmb_f32_256_nn";
-    case kF32_256s:
-      return "pdmb_f32_256s_nn";
-    case kFp8:
-      return "pdmb_fp8_256_nt";
-    case kFp8W4:
-      return "pdmb_fp8_w4_nt";
-    case kMfmaW4:
-      return "pdmb_w4_nn";
-    case kMfmaW4Tall:
-      return "pdmb_w4_nn_tall";
-    case kMfmaW4Wide:
-      return "pdmb_w4_nn_wide";
-    case kFp8W4Tall:
-      return "pdmb_fp8_w4_nt_tall";
-    case kFp8W4Wide:
-      return "pdmb_fp8_w4_nt_wide";
-    default:
-      return "auto";
+    case kGeneric: return "pdmb_generic_nn";
+    case kMfma256d: return "pdmb_mfma256d_nn";
+    case kF32_256s: return "pdmb_f32_256s_nn";
+    case kFp8W4: return "pdmb_fp8_w4_nt";
+    case kMfmaW4: return "pdmb_w4_nn";
+    case kMfma256: return "pdmb_mfma256_nn";
+    case kMfma256b: return "pdmb_mfma256b_nn";
+    case kMfma256c: return "pdmb_mfma256c_nn";
+    case kMfma256Stamp: return "pdmb_mfma256c_stamp";
+    case kF32_256: return "pdmb_f32_256_nn";
+    case kFp8: return "pdmb_fp8_256_nt";
+    case kMfmaW4Tall: return "pdmb_w4_nn_tall";
+    case kMfmaW4Wide: return "pdmb_w4_nn_wide";
+    case kFp8W4Tall: return "pdmb_fp8_w4_nt_tall";
+    case kFp8W4Wide: return "pdmb_fp8_w4_nt_wide";
+    default: return "auto";
   }
 }
 

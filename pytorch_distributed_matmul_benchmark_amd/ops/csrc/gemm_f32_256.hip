@@ -202,13 +202,19 @@ hipError_t gemm_f32_256_launch(GemmArgs a, int variant, hipStream_t stream) {
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
   const dim3 grid((unsigned)nblocks), block(kf32::NT);
+  if (variant == 1) {  // the shipping exact-fp32 kernel (kF32_256s)
+    hipLaunchKernelGGL(kf32::gemm_f32_256<true>, grid, block, 0, stream, a);
+    return hipGetLastError();
+  }
+#ifdef PDMB_EXPERIMENTS
   if (variant == 9)
     hipLaunchKernelGGL((kf32::gemm_f32_256<false, true>), grid, block, 0, stream, a);
-  else if (variant == 1)
-    hipLaunchKernelGGL(kf32::gemm_f32_256<true>, grid, block, 0, stream, a);
   else
     hipLaunchKernelGGL(kf32::gemm_f32_256<false>, grid, block, 0, stream, a);
   return hipGetLastError();
+#else
+  return hipErrorInvalidValue;  // experiment variants are not built
+#endif
 }
 
 }  // namespace pdmb

@@ -176,6 +176,7 @@ __device__ __forceinline__ void tile_body(const Ctx& c, char* smem, int t, f32x4
   PDMB8_BARRIER();
 }
 
+#ifdef PDMB_EXPERIMENTS  // the 8-wave kernel: an A/B build only (kFp8)
 __global__ void __launch_bounds__(NTHREADS, 2) gemm_fp8_nt(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
@@ -271,6 +272,7 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_fp8_nt(GemmArgs a) {
     }
   }
 }
+#endif
 
 
 // ---- W4 (default): 4 waves, one per SIMD, 128x128 output per wave --------
@@ -548,20 +550,27 @@ hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream) {
   const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch;
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
-  if (variant == 1)
-    hipLaunchKernelGGL(k8::gemm_fp8_w4<0>, dim3((unsigned)nblocks), dim3(k8::NT4), 0, stream, a);
-  else if (variant == 9)
-    hipLaunchKernelGGL(k8::gemm_fp8_w4<1>, dim3((unsigned)nblocks), dim3(k8::NT4), 0, stream, a);
+  const dim3 grid((unsigned)nblocks);
+  if (variant == 1) {  // the shipping fp8 kernel (kFp8W4)
+    hipLaunchKernelGGL(k8::gemm_fp8_w4<0>, grid, dim3(k8::NT4), 0, stream, a);
+    return hipGetLastError();
+  }
+#ifdef PDMB_EXPERIMENTS
+  if (variant == 9)
+    hipLaunchKernelGGL(k8::gemm_fp8_w4<1>, grid, dim3(k8::NT4), 0, stream, a);
   else if (variant == 10)
-    hipLaunchKernelGGL(k8::gemm_fp8_w4<2>, dim3((unsigned)nblocks), dim3(k8::NT4), 0, stream, a);
+    hipLaunchKernelGGL(k8::gemm_fp8_w4<2>, grid, dim3(k8::NT4), 0, stream, a);
   else if (variant == 11)
-    hipLaunchKernelGGL(k8::gemm_fp8_w4<3>, dim3((unsigned)nblocks), dim3(k8::NT4), 0, stream, a);
+    hipLaunchKernelGGL(k8::gemm_fp8_w4<3>, grid, dim3(k8::NT4), 0, stream, a);
   else if (variant == 12)
-    hipLaunchKernelGGL((k8::gemm_fp8_w4<0, 1>), dim3((unsigned)nblocks), dim3(k8::NT4), 0, stream, a);
+    hipLaunchKernelGGL((k8::gemm_fp8_w4<0, 1>), grid, dim3(k8::NT4), 0, stream, a);
   else if (variant == 13)
-    hipLaunchKernelGGL((k8::gemm_fp8_w4<0, 2>), dim3((unsigned)nblocks), dim3(k8::NT4), 0, stream, a);
+    hipLaunchKernelGGL((k8::gemm_fp8_w4<0, 2>), grid, dim3(k8::NT4), 0, stream, a);
   else
-    hipLaunchKernelGGL(k8::gemm_fp8_nt, dim3((unsigned)nblocks), dim3(k8::NTHREADS), 0, stream, a);
+    hipLaunchKernelGGL(k8::gemm_fp8_nt, grid, dim3(k8::NTHREADS), 0, stream, a);
+#else
+  return hipErrorInvalidValue;  // experiment variants are not built
+#endif
   return hipGetLastError();
 }
 

@@ -512,6 +512,12 @@ hipError_t gemm256_launch(int dt, GemmArgs a, int sched, hipStream_t stream) {
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
   dim3 grid((unsigned)nblocks), block(k256::NTHREADS);
 #define PDMB_LAUNCH256(D, S) hipLaunchKernelGGL((k256::gemm256_nn<D, S>), grid, block, 0, stream, a)
+  if (sched == 4) {  // SCHED 3: the shipping schedule (kMfma256d)
+    if (dt == kBF16) PDMB_LAUNCH256(kBF16, 3);
+    else PDMB_LAUNCH256(kF16, 3);
+    return hipGetLastError();
+  }
+#ifdef PDMB_EXPERIMENTS
   if (sched >= 10) {  // SCHED 2 experiment flags (bf16 only, A/B builds)
     if (dt != kBF16) return hipErrorInvalidValue;
     switch (sched - 10) {
@@ -528,18 +534,19 @@ hipError_t gemm256_launch(int dt, GemmArgs a, int sched, hipStream_t stream) {
     return hipGetLastError();
   }
   if (dt == kBF16) {
-    if (sched == 4) PDMB_LAUNCH256(kBF16, 3);
-    else if (sched == 2) PDMB_LAUNCH256(kBF16, 2);
+    if (sched == 2) PDMB_LAUNCH256(kBF16, 2);
     else if (sched == 1) PDMB_LAUNCH256(kBF16, 1);
     else PDMB_LAUNCH256(kBF16, 0);
   } else {
-    if (sched == 4) PDMB_LAUNCH256(kF16, 3);
-    else if (sched == 2) PDMB_LAUNCH256(kF16, 2);
+    if (sched == 2) PDMB_LAUNCH256(kF16, 2);
     else if (sched == 1) PDMB_LAUNCH256(kF16, 1);
     else PDMB_LAUNCH256(kF16, 0);
   }
-#undef PDMB_LAUNCH256
   return hipGetLastError();
+#else
+  return hipErrorInvalidValue;  // experiment schedules are not built
+#endif
+#undef PDMB_LAUNCH256
 }
 
 }  // namespace pdmb

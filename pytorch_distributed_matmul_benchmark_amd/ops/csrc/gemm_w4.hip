@@ -30,6 +30,7 @@
 // multiples of 256 (interior tiles only: no edge masking, no out-of-extent
 // DMA), K % 64 == 0, lda / ldb % 8 == 0, ldc % 4 == 0, 16-B aligned A / B,
 // 8-B aligned C.
+#include "api.h"
 #include "common.h"
 
 namespace pdmb {
@@ -183,6 +184,63 @@ __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, f32
   }
 }
 
+// Split-K meeting point of the S workgroups of one output tile, fused into
+// the epilogue (no second kernel, no memset). The first S-1 to arrive each
+// park their fp32 accumulators in their slice's slot of `part`; the last to
+// arrive gets the slots back (nullptr for the others) and writes C as
+// slot 0 + slot 1 + ... in slice order with its own registers in its own
+// place, so the result is bitwise reproducible whoever arrives last. Arrival
+// order comes from a per-tile counter, so no workgroup ever waits for one
+// that has not started: the last waits only for slots whose owners have
+// already arrived, i.e. are resident and past their K-loop, and finish their
+// stores unconditionally (no co-residency assumption, safe next to RCCL or
+// under a CU mask). The last workgroup re-zeroes both counters, so they are
+// zero between launches on a stream (which never overlap).
+//
+// Slot layout follows the accumulator registers (f32x4 (i, j) of thread t at
+// ((i * 8 + j) * 256 + t) * 16 B): every store and load is a fully coalesced
+// 1 KiB wave access, and no index math depends on the MFMA layout.
+// Memory order: stores -> release fence -> `done` increment; `done` load ->
+// acquire fence in every thread -> slot loads. The agent-scope fences write
+// back / invalidate the XCD-private L2s, so the slices may sit on any XCDs.
+template <int N8>
+__device__ __forceinline__ const f32x4* splitk_meet(const GemmArgs& a, char* smem, int bz, int tm,
+                                                    int tn, int slice, f32x4 (&acc)[N8][8]) {
+  const int S = a.splitk;
+  const long long tile = ((long long)bz * a.tiles_m + tm) * a.tiles_n + tn;
+  unsigned* arrive = a.flags + 2 * tile;
+  unsigned* done = arrive + 1;
+  int* bcast = (int*)smem;
+  __syncthreads();  // every wave is past its last LDS read before smem is reused
+  if (threadIdx.x == 0)
+    bcast[0] = (int)__hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int ord = bcast[0];
+  const int t = threadIdx.x;
+  f32x4* slots = (f32x4*)(a.part + tile * (long long)S * (N8 * 8 * 4 * NT));
+  if (ord < S - 1) {
+    f32x4* p = slots + (long long)slice * (N8 * 8 * NT);
+#pragma unroll
+    for (int i = 0; i < N8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) p[(i * 8 + j) * NT + t] = acc[i][j];
+    __threadfence();
+    __syncthreads();
+    if (t == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return nullptr;
+  }
+  if (t == 0) {
+    while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(S - 1))
+      __builtin_amdgcn_s_sleep(1);
+    // Nobody else touches this tile's counters in this launch any more.
+    __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  __threadfence();
+  return slots + t;  // slot s, block (i, j): [(s * N8 * 8 + i * 8 + j) * NT] (own slot unused)
+}
+
 // SUB: XCD sub-block shape (map_tile): 0 = 4 x 8 (default), 1 = 8 x 4
 // (kMfmaW4Tall), 2 = 2 x 16 (kMfmaW4Wide); 1 and 2 are A/B experiments.
 template <int DT, int SUB = 0>
@@ -191,6 +249,15 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4_nn(GemmArgs a) {
 
   int bz, tm, tn;
   map_tile(a, blockIdx.x, bz, tm, tn, SUB);
+  // Split-K: the grid's "batch" is batch x S with the slice innermost, so
+  // one slice of every tile is a contiguous block range (map_tile's grouped
+  // order) and each workgroup runs K-tiles [kt0, kt0 + nk) of its tile.
+  int slice = 0;
+  if (a.splitk > 1) {
+    slice = bz % a.splitk;
+    bz /= a.splitk;
+  }
+  const int kt0 = slice * a.kt_per;
   const int m0 = tm * BM, n0 = tn * BN;
   const int lane = threadIdx.x & 63;
   const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -202,11 +269,15 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4_nn(GemmArgs a) {
   c.lds0 = (uint32_t)(size_t)((lds_void*)smem);
   c.lda2 = a.lda * 2;
   c.ldb2 = a.ldb * 2;
-  c.nk = a.K / BK;
-  const char* Ab = (const char*)a.A + ((long long)bz * a.sA + (long long)m0 * a.lda) * 2;
-  c.ra = make_rsrc(Ab, ((long long)(a.M - m0 - 1) * a.lda + a.K) * 2);
-  c.Bb = (const char*)a.B + ((long long)bz * a.sB + n0) * 2;
-  c.b_bytes = ((long long)(a.K - 1) * a.ldb + (a.N - n0)) * 2;
+  {
+    const int nk_all = a.K / BK;
+    c.nk = a.splitk > 1 ? min(a.kt_per, nk_all - kt0) : nk_all;
+  }
+  const int k0 = kt0 * BK;
+  const char* Ab = (const char*)a.A + ((long long)bz * a.sA + (long long)m0 * a.lda + k0) * 2;
+  c.ra = make_rsrc(Ab, ((long long)(a.M - m0 - 1) * a.lda + (a.K - k0)) * 2);
+  c.Bb = (const char*)a.B + ((long long)bz * a.sB + (long long)k0 * a.ldb + n0) * 2;
+  c.b_bytes = ((long long)(a.K - k0 - 1) * a.ldb + (a.N - n0)) * 2;
   {
     const int r = wu * 8 + (lane >> 3), lc8 = lane & 7;  // row of A piece 0
     c.voffA = (uint32_t)(r * c.lda2 + ((lc8 ^ ((r >> 1) & 7)) * 16));
@@ -283,20 +354,53 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4_nn(GemmArgs a) {
   // (asm MFMAs are invisible to hipcc's hazard recognizer).
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
 
+  // Split-K: only the last slice of a tile to arrive gets here with `red`
+  // (the other slices' fp32 slots); it adds them block row by block row
+  // while storing, so no more than 2 x 8 fragments are live in VGPRs.
+  const f32x4* red = nullptr;
+  if (a.splitk > 1) {
+    red = splitk_meet(a, smem, bz, tm, tn, slice, acc);
+    if (!red) return;
+  }
+
   // Epilogue: acc[i][j] holds C^T of a 16x16 tile: lane owns row l16 and
   // columns 4g..4g+3 (interior tiles only: no masks).
   char* Cb = (char*)a.C + (long long)bz * a.sC * 2;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
+    f32x4 v[8];
+    if (!red) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = acc[i][j];
+    } else {  // sum over slices in slice order (bitwise reproducible)
+      for (int s = 0; s < a.splitk; ++s) {
+        f32x4 q[8];
+        if (s == slice) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) q[j] = acc[i][j];
+        } else {
+          const f32x4* p = red + (long long)(s * 64 + i * 8) * NT;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) q[j] = p[j * NT];
+        }
+        if (s == 0) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = q[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] += q[j];
+        }
+      }
+    }
     const int row = m0 + wr * 128 + i * 16 + l16;
     char* crow = Cb + (long long)row * a.ldc * 2;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int col = n0 + wc * 128 + j * 16 + 4 * g;
-      u32x2 v;
-      v.x = pack2<DT>(acc[i][j].x, acc[i][j].y);
-      v.y = pack2<DT>(acc[i][j].z, acc[i][j].w);
-      *(u32x2*)(crow + col * 2) = v;
+      u32x2 w;
+      w.x = pack2<DT>(v[j].x, v[j].y);
+      w.y = pack2<DT>(v[j].z, v[j].w);
+      *(u32x2*)(crow + col * 2) = w;
     }
   }
 }
@@ -321,20 +425,38 @@ bool gemm_w4_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b
 hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
   a.tiles_m = a.M / kw4::BM;
   a.tiles_n = a.N / kw4::BN;
+  const int S = a.splitk > 1 ? a.splitk : 1;
+  if (S > 1) {
+    const int nk = a.K / kw4::BK;
+    a.kt_per = (nk + S - 1) / S;
+    if ((S - 1) * a.kt_per >= nk || !a.part || !a.flags ||
+        (long long)a.tiles_m * a.tiles_n * a.batch > kMaxSplitTiles)
+      return hipErrorInvalidValue;  // every slice must own >= 1 K-tile
+  } else {
+    a.splitk = 1;
+  }
+  // The grid's batch is batch x S (slice innermost); the XCD-aware order is
+  // chosen from the per-element tile grid as before.
   a.supertile = choose_supertile(a.tiles_m, a.tiles_n);
-  const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch;
+  const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch * S;
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
-  if (dt == kBF16 && sub == 1)
-    hipLaunchKernelGGL((kw4::gemm_w4_nn<kBF16, 1>), dim3((unsigned)nblocks), dim3(kw4::NT), 0,
-                       stream, a);
-  else if (dt == kBF16 && sub == 2)
-    hipLaunchKernelGGL((kw4::gemm_w4_nn<kBF16, 2>), dim3((unsigned)nblocks), dim3(kw4::NT), 0,
-                       stream, a);
-  else if (dt == kBF16)
-    hipLaunchKernelGGL(kw4::gemm_w4_nn<kBF16>, dim3((unsigned)nblocks), dim3(kw4::NT), 0, stream, a);
+  const dim3 grid((unsigned)nblocks), block(kw4::NT);
+#ifdef PDMB_EXPERIMENTS
+  if (dt == kBF16 && sub == 1) {
+    hipLaunchKernelGGL((kw4::gemm_w4_nn<kBF16, 1>), grid, block, 0, stream, a);
+    return hipGetLastError();
+  }
+  if (dt == kBF16 && sub == 2) {
+    hipLaunchKernelGGL((kw4::gemm_w4_nn<kBF16, 2>), grid, block, 0, stream, a);
+    return hipGetLastError();
+  }
+#endif
+  if (sub != 0) return hipErrorInvalidValue;
+  if (dt == kBF16)
+    hipLaunchKernelGGL(kw4::gemm_w4_nn<kBF16>, grid, block, 0, stream, a);
   else
-    hipLaunchKernelGGL(kw4::gemm_w4_nn<kF16>, dim3((unsigned)nblocks), dim3(kw4::NT), 0, stream, a);
+    hipLaunchKernelGGL(kw4::gemm_w4_nn<kF16>, grid, block, 0, stream, a);
   return hipGetLastError();
 }
 

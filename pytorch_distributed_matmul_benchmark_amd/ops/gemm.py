@@ -20,25 +20,43 @@ import torch
 
 from . import _native
 
-KERNELS = {"auto": 0, "mfma256": 1, "generic": 2, "mfma256b": 3, "mfma256c": 4, "mfma256d": 9, "w4": 21,
-           "mfma256c_stamp": 5, "f32_256": 6,
-           "f32_256s": 7, "fp8": 15, "fp8_w4": 16, "diag_fp8_w4_nowait": 17, "diag_fp8_w4_nosync": 18, "diag_fp8_w4_mfma_only": 19, "diag_f32_nodma": 20, "x_clusterprio": 10, "x_staticprio": 11, "x_tall": 13, "x_w4_tall": 22, "x_w4_wide": 23, "x_fp8_w4_tall": 24, "x_fp8_w4_wide": 25}
-KERNEL_NAMES = {0: "auto", 1: "pdmb_mfma256_nn", 2: "pdmb_generic_nn", 3: "pdmb_mfma256b_nn", 4: "pdmb_mfma256c_nn",
-                9: "pdmb_mfma256d_nn",
-                5: "pdmb_mfma256c_stamp", 6: "pdmb_f32_256_nn",
-                7: "pdmb_f32_256s_nn", 15: "pdmb_fp8_256_nt", 16: "pdmb_fp8_w4_nt", 21: "pdmb_w4_nn",
-                -1: "unsupported"}
+# The shipping kernels: the public ``kernel=`` surface (api.h ``Kernel``).
+KERNELS = {"auto": 0, "generic": 2, "f32_256s": 7, "mfma256d": 9, "fp8_w4": 16, "w4": 21}
+# A/B and timing-only diagnostic kernels (api.h ``ExperimentKernel``): accepted
+# only by a library built with ``PDMB_EXPERIMENTS=1``; ``diag_*`` ones skip waits
+# or data movement on purpose and compute WRONG results.
+EXPERIMENT_KERNELS = {"mfma256": 1, "mfma256b": 3, "mfma256c": 4, "mfma256c_stamp": 5,
+                      "f32_256": 6, "x_clusterprio": 10, "x_staticprio": 11, "x_tall": 13,
+                      "fp8": 15, "diag_fp8_w4_nowait": 17, "diag_fp8_w4_nosync": 18,
+                      "diag_fp8_w4_mfma_only": 19, "diag_f32_nodma": 20, "x_w4_tall": 22,
+                      "x_w4_wide": 23, "x_fp8_w4_tall": 24, "x_fp8_w4_wide": 25}
+KERNEL_NAMES = {0: "auto", 2: "pdmb_generic_nn", 7: "pdmb_f32_256s_nn", 9: "pdmb_mfma256d_nn",
+                16: "pdmb_fp8_w4_nt", 21: "pdmb_w4_nn", 1: "pdmb_mfma256_nn",
+                3: "pdmb_mfma256b_nn", 4: "pdmb_mfma256c_nn", 5: "pdmb_mfma256c_stamp",
+                6: "pdmb_f32_256_nn", 15: "pdmb_fp8_256_nt", -1: "unsupported"}
 SUPPORTED_DTYPES = (torch.float32, torch.float16, torch.bfloat16)
 FP8 = torch.float8_e4m3fn  # OCP e4m3 (gfx950), bf16 output, column-major B
 
 
+def experiments_built() -> bool:
+    """True iff the loaded library carries the experiment kernels."""
+    return bool(getattr(_native.load(), "EXPERIMENTS", False))
+
+
 def _kid(kernel) -> int:
     if isinstance(kernel, int):
-        return kernel
-    try:
+        if kernel in KERNELS.values() or (kernel in EXPERIMENT_KERNELS.values()
+                                          and experiments_built()):
+            return kernel
+        raise ValueError(f"kernel id {kernel} is not a shipping kernel of this build")
+    if kernel in KERNELS:
         return KERNELS[kernel]
-    except KeyError:
-        raise ValueError(f"unknown kernel {kernel!r}; choose from {sorted(KERNELS)}") from None
+    if kernel in EXPERIMENT_KERNELS:
+        if not experiments_built():
+            raise ValueError(f"kernel {kernel!r} is an experiment/diagnostic kernel, not built by "
+                             "default (rebuild with PDMB_EXPERIMENTS=1 to A/B it)")
+        return EXPERIMENT_KERNELS[kernel]
+    raise ValueError(f"unknown kernel {kernel!r}; choose from {sorted(KERNELS)}")
 
 
 def _out_shape(A: torch.Tensor, B: torch.Tensor):
@@ -49,15 +67,18 @@ def _out_shape(A: torch.Tensor, B: torch.Tensor):
 
 
 def _prep(t: torch.Tensor) -> torch.Tensor:
-    # Kernels need a unit innermost stride; leading dims may be strided.
+    # Kernels need a unit innermost stride and a row stride of at least the row
+    # length (no expanded / overlapping rows); leading dims may be strided.
     if t.dim() >= 1 and t.shape[-1] > 1 and t.stride(-1) != 1:
+        return t.contiguous()
+    if t.dim() >= 2 and t.shape[-2] > 1 and t.stride(-2) < t.shape[-1]:
         return t.contiguous()
     return t
 
 
 def _prep_colmajor(t: torch.Tensor) -> torch.Tensor:
     # fp8 B operand: unit stride along K (column-major [K,N], i.e. a row-major Bt [N,K]).
-    if t.shape[-2] > 1 and t.stride(-2) != 1:
+    if (t.shape[-2] > 1 and t.stride(-2) != 1) or (t.shape[-1] > 1 and t.stride(-1) < t.shape[-2]):
         return t.transpose(-1, -2).contiguous().transpose(-1, -2)
     return t
 
@@ -85,8 +106,11 @@ def fp8_quantize(x: torch.Tensor, colmajor: bool = False):
 
 
 def matmul(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
-           kernel="auto", alpha: float = 1.0) -> torch.Tensor:
+           kernel="auto", alpha: float = 1.0, splitk: int = 0) -> torch.Tensor:
     """``out = A @ B`` for 2-D/3-D row-major operands (3-D = batched).
+
+    ``splitk`` (W4 only): K slices per output tile, 0 = auto (split only grids
+    that under-fill the 256 CUs, ``splitk_for``), 1 = never.
 
     float8_e4m3fn operands: ``out = alpha * (A @ B)`` in bfloat16 on the
     block-scaled fp8 MFMA (B is used column-major; a row-major B is copied).
@@ -116,7 +140,7 @@ def matmul(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
     if out is None:
         out = torch.empty(_out_shape(A, B), dtype=out_dtype(A.dtype), device=A.device)
     # auto: odd K/N/alignment padded onto the fast path (C++; not for fp8)
-    C.matmul(A, B, out, _kid(kernel), float(alpha))
+    C.matmul(A, B, out, _kid(kernel), float(alpha), int(splitk))
     return out
 
 
@@ -159,8 +183,20 @@ def kernel_for(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = N
     return KERNEL_NAMES[int(C.resolve(A, B, out, _kid(kernel)))]
 
 
+def splitk_for(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
+               kernel="auto", splitk: int = 0) -> int:
+    """K slices the W4 kernel uses for these operands (1: unsplit, 0: not W4)."""
+    if A.device.type != "cuda":
+        return 0
+    C = _native.load()
+    if out is None:
+        out = torch.empty(_out_shape(A, B), dtype=out_dtype(A.dtype), device=A.device)
+    A, B = _prep_pair(A, B)
+    return int(C.splitk_for(A, B, out, _kid(kernel), int(splitk)))
+
+
 def bench_matmul(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, iters: int,
-                 warmup: int, graph: bool = False, kernel="auto") -> float:
+                 warmup: int, graph: bool = False, kernel="auto", splitk: int = 0) -> float:
     """Native timing loop (hipEvents around ``iters`` launches). Returns TOTAL ms."""
     if A.device.type != "cuda":
         import time
@@ -173,4 +209,5 @@ def bench_matmul(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, iters: int
         return (time.perf_counter() - t0) * 1e3
     C = _native.load()
     A, B = _prep_pair(A, B)
-    return float(C.bench(A, B, out, int(iters), int(warmup), bool(graph), _kid(kernel)))
+    return float(C.bench(A, B, out, int(iters), int(warmup), bool(graph), _kid(kernel),
+                         int(splitk)))

@@ -1,0 +1,156 @@
+"""Overlap schedules shared by ``bench.py`` and ``models/``: chunked GEMM on a
+(possibly CU-masked) compute stream, collective pieces on the comm stream.
+
+Reference: backup/matmul_overlap_benchmark.py:93-180 (two streams, double
+buffer, the collective issued with no dependency on its producer — SURVEY Q7)
+and matmul_scaling_benchmark.py:167-238 (matrix_parallel, serialized). Here:
+
+* ``gemm_chunks`` — how many row chunks the GEMM is cut into. A chunk is
+  worth having only if its GEMM still fills the chip: with W4 split-K
+  (gemm_w4.hip) a chunk of >= 64 256x256 tiles does (S = 4 slices), so the
+  8k ws=8 shard (128 tiles) now overlaps in 2 chunks instead of running
+  serialized (round 1 required >= 256 tiles per chunk).
+* ``GatherOverlap`` — matrix_parallel: GEMM chunk j, then its rows are
+  all-gathered in ``pieces`` RCCL calls (independent of the GEMM chunking),
+  each on the comm stream after an event recorded behind chunk j; the step
+  ends with the compute stream waiting for every piece (the timed region
+  includes the last collective).
+* ``ReduceOverlap`` — batch_parallel: (batch element, row chunk) units, each
+  all-reduced behind its GEMM.
+* ``compute_stream(device, comm_cus)`` — a HIP stream whose kernels may not
+  use ``comm_cus`` CUs (hipExtStreamCreateWithCUMask, spread evenly over the
+  8 XCDs), so RCCL's workgroups start on those CUs at once instead of waiting
+  for a 1-workgroup-per-CU GEMM wave to retire.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from .comm import CommStream, new_event
+from .partition import ceil_div, effective_chunks, row_chunks
+
+# 256x256 output tiles a GEMM chunk needs to fill the chip (ops/gemm.py
+# min_chunk_tiles): 64 for the split-K W4 kernel (bf16/fp16), a full wave of
+# 256 for the others.
+_SPLITK_MIN_TILES = 64
+
+
+def min_chunk_tiles(dtype: torch.dtype, device: torch.device) -> int:
+    if device.type != "cuda":
+        return 1
+    return _SPLITK_MIN_TILES if dtype in (torch.bfloat16, torch.float16) else 256
+
+
+def gemm_chunks(m: int, n: int, requested: int, dtype: torch.dtype,
+                device: torch.device) -> List[Tuple[int, int]]:
+    """Row chunks [start, stop) of an [m, n] GEMM output for an overlap schedule."""
+    if device.type != "cuda":
+        return row_chunks(m, requested)
+    return row_chunks(m, effective_chunks(m, n, requested,
+                                          min_tiles=min_chunk_tiles(dtype, device)))
+
+
+def _xcd_spread(ncu: int, k: int, nxcd: int = 8) -> List[int]:
+    """k CU indices spread evenly over the XCDs (HIP CU-mask bit i lands on
+    XCD i % nxcd on multi-XCD parts): the first k indices do exactly that."""
+    return list(range(min(max(k, 0), ncu)))
+
+
+class MaskedStream:
+    """A CU-masked HIP stream (owned; destroyed with the object)."""
+
+    def __init__(self, device: torch.device, comm_cus: int):
+        from ..ops import _native
+
+        self._C = _native.load()
+        ncu = torch.cuda.get_device_properties(device).multi_processor_count
+        self.excluded = _xcd_spread(ncu, comm_cus)
+        self.handle = int(self._C.create_cu_masked_stream(device.index, self.excluded))
+        self.stream = torch.cuda.ExternalStream(self.handle, device=device)
+        self.device = device
+
+    def active_cus(self) -> int:
+        mask = self._C.stream_cu_mask(self.handle, self.device.index)
+        return sum(bin(int(w) & 0xFFFFFFFF).count("1") for w in mask)
+
+    def close(self) -> None:
+        if self.handle:
+            torch.cuda.synchronize(self.device)
+            self._C.destroy_stream(self.handle)
+            self.handle = 0
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def compute_stream(device: torch.device, comm_cus: int = 0):
+    """(stream, owner): the current stream (comm_cus == 0) or a CU-masked one."""
+    if device.type != "cuda":
+        return None, None
+    if comm_cus <= 0:
+        return torch.cuda.current_stream(device), None
+    ms = MaskedStream(device, comm_cus)
+    return ms.stream, ms
+
+
+class GatherOverlap:
+    """matrix_parallel overlap: C_local rows in GEMM chunks, each all-gathered in pieces."""
+
+    def __init__(self, n_rows: int, shard: int, ws: int, device: torch.device,
+                 out_dtype: torch.dtype, chunks: Sequence[Tuple[int, int]], pieces: int = 0,
+                 requested: int = 4, comm: Optional[CommStream] = None):
+        self.chunks = list(chunks)
+        per = pieces if pieces > 0 else max(1, ceil_div(max(requested, 1), len(self.chunks)))
+        self.pieces = []
+        for s, e in self.chunks:
+            self.pieces.append([(s + ps, s + pe) for ps, pe in row_chunks(e - s, per, align=8)])
+        self.bufs = [[torch.empty((ws * (pe - ps), shard), device=device, dtype=out_dtype)
+                      for ps, pe in pcs] for pcs in self.pieces]
+        self.ready = [new_event(device) for _ in self.chunks]
+        self.done = [[new_event(device) for _ in pcs] for pcs in self.pieces]
+        self.cs = comm or CommStream(device)
+        self.device = device
+
+    @property
+    def n_pieces(self) -> int:
+        return sum(len(p) for p in self.pieces)
+
+    def step(self, mm, A, B_local, C_local, compute) -> None:
+        for j, (s, e) in enumerate(self.chunks):
+            mm(A[s:e], B_local, C_local[s:e])
+            self.ready[j].record(compute)
+            for p, (ps, pe) in enumerate(self.pieces[j]):
+                self.cs.all_gather_into(self.bufs[j][p], C_local[ps:pe],
+                                        after=self.ready[j] if p == 0 else None,
+                                        done=self.done[j][p])
+        if compute is not None:
+            for dj in self.done:
+                compute.wait_event(dj[-1])  # comm stream is in order: last piece => all
+
+    def gathered(self) -> List[torch.Tensor]:
+        """Gather buffers in row order (models.matrix_parallel.assemble)."""
+        return [b for bj in self.bufs for b in bj]
+
+
+class ReduceOverlap:
+    """batch_parallel overlap: per (batch element, row chunk) GEMM, then all-reduce."""
+
+    def __init__(self, local_batch: int, chunks: Sequence[Tuple[int, int]],
+                 device: torch.device, comm: Optional[CommStream] = None):
+        self.units = [(b, s, e) for b in range(local_batch) for (s, e) in chunks]
+        self.ready = [new_event(device) for _ in self.units]
+        self.done = [new_event(device) for _ in self.units]
+        self.cs = comm or CommStream(device)
+
+    def step(self, mm, A, B, C, compute) -> None:
+        for u, (b, s, e) in enumerate(self.units):
+            mm(A[b, s:e], B[b], C[b, s:e])
+            self.ready[u].record(compute)
+            self.cs.all_reduce(C[b, s:e], after=self.ready[u], done=self.done[u])
+        if compute is not None and self.done:
+            compute.wait_event(self.done[-1])

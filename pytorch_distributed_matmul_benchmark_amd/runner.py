@@ -77,13 +77,20 @@ def build_parser(kind: str) -> argparse.ArgumentParser:
     g.add_argument("--backend", default="native", choices=["native", "torch"],
                    help="GEMM implementation on GPU: native gfx950 MFMA kernels (default) or "
                         "torch.matmul/hipBLASLt for A/B comparison")
-    g.add_argument("--kernel", default="auto", choices=["auto", "mfma256", "generic"],
-                   help="native kernel selection")
+    g.add_argument("--kernel", default="auto",
+                   choices=["auto", "w4", "mfma256d", "generic", "f32_256s", "fp8_w4"],
+                   help="native kernel selection (shipping kernels; A/B kernels need a "
+                        "PDMB_EXPERIMENTS=1 build and scripts/ab_kernels.py)")
     g.add_argument("--batch", type=int, default=4,
                    help="batch_parallel global batch (rounded up to a multiple of the world size)")
     g.add_argument("--overlap", action="store_true",
                    help="batch/matrix_parallel: overlap the collective with the GEMM on a second stream")
     g.add_argument("--chunks", type=int, default=4, help="overlap granularity (row chunks per GEMM)")
+    g.add_argument("--comm-chunks", type=int, default=0,
+                   help="matrix_parallel --overlap: all-gather pieces per GEMM chunk (0: auto)")
+    g.add_argument("--comm-cus", type=int, default=0,
+                   help="--overlap: CUs kept free of GEMM workgroups for RCCL (CU-masked "
+                        "compute stream, spread over the 8 XCDs; 0 = no mask)")
     g.add_argument("--graph", action="store_true",
                    help="independent: replay the timed loop as one hipGraph")
     g.add_argument("--check", action="store_true",
@@ -119,7 +126,8 @@ def _mode_of(kind: str, args) -> str:
 def _workload(args, n: int, dtype: torch.dtype) -> Workload:
     return Workload(n=n, dtype=dtype, iters=args.iterations, warmup=args.warmup, seed=args.seed,
                     backend=args.backend, kernel=args.kernel, batch=args.batch,
-                    overlap=args.overlap, chunks=args.chunks, graph=args.graph, check=args.check,
+                    overlap=args.overlap, chunks=args.chunks, comm_chunks=args.comm_chunks,
+                    comm_cus=args.comm_cus, graph=args.graph, check=args.check,
                     min_warmup_ms=args.min_warmup_ms)
 
 

@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -164,6 +165,16 @@ struct Buf {
   Buf(const Buf&) = delete;
   Buf& operator=(const Buf&) = delete;
   Buf(Buf&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; }
+  Buf& operator=(Buf&& o) noexcept {
+    if (this != &o) {
+      if (p) (void)hipFree(p);
+      p = o.p;
+      bytes = o.bytes;
+      o.p = nullptr;
+      o.bytes = 0;
+    }
+    return *this;
+  }
   template <class T>
   T* as() const { return (T*)p; }
 };
@@ -194,7 +205,25 @@ pdmb::Problem problem(int dt, const void* A, const void* B, void* C, int M, int 
   return p;
 }
 
-void gemm(const pdmb::Problem& p, int kernel, hipStream_t s) {
+// Launch scratch (padded copies / split-K partials), one growing buffer per
+// stream. Growing waits for the stream first; it happens in warm-up only.
+void* scratch(hipStream_t s, size_t bytes) {
+  static std::map<hipStream_t, Buf>* m = new std::map<hipStream_t, Buf>();
+  Buf& b = (*m)[s];
+  if (b.bytes < bytes) {
+    HIP_OK(hipStreamSynchronize(s));
+    b = Buf(bytes);
+  }
+  return b.p;
+}
+
+void gemm(const pdmb::Problem& p0, int kernel, hipStream_t s) {
+  pdmb::Problem p = p0;
+  const size_t need = pdmb::gemm_workspace_bytes(p, kernel);
+  if (need) {
+    p.workspace = scratch(s, need);
+    p.workspace_bytes = need;
+  }
   int used = -1;
   HIP_OK(pdmb::gemm(p, kernel, s, &used));
   if (used < 0) throw std::runtime_error("requested kernel cannot run this problem");

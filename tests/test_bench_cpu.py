@@ -78,3 +78,78 @@ def test_bench_reports_secondary_modes():
     d0 = _bench(2, "--size", "128", "--steps", "1", "--warmup", "0", "--extra-steps", "0",
                 "--mode", "batch_parallel")
     assert d0["modes"] == {}
+
+
+def _plain(*args, env_extra=None, timeout=300):
+    """bench.py run WITHOUT torchrun (the driver's 1-GPU form; --gpus N self-launches)."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", **(env_extra or {}))
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu",
+                           *args], capture_output=True, text=True, timeout=timeout, cwd="/tmp",
+                          env=env)
+
+
+def _line(r):
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout + r.stderr[-3000:]
+    return json.loads(lines[0])
+
+
+def test_bench_self_launches_n_ranks():
+    """--gpus 4 with no torchrun: bench.py starts 4 ranks itself, one JSON line,
+    whole-job value, and an in-job scaling efficiency vs rank 0 alone."""
+    r = _plain("--gpus", "4", "--size", "256", "--steps", "3", "--warmup", "1",
+               "--extra-steps", "1", "--extra-warmup", "0")
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r)
+    assert d["n_gpus"] == 4 and d["config"]["parallelism"] == "independent4"
+    assert d["single_gpu_tflops"] > 0
+    assert d["scaling_efficiency"] == pytest.approx(d["value"] / (4 * d["single_gpu_tflops"]),
+                                                    rel=1e-3)
+    for key, m in d["modes"].items():
+        assert m["scaling_efficiency"] is not None, key
+
+
+def test_bench_ws1_overlap_modes_are_null():
+    d = _line(_plain("--size", "128", "--steps", "1", "--warmup", "0", "--extra-steps", "1",
+                     "--extra-warmup", "0"))
+    assert d["n_gpus"] == 1 and d["scaling_efficiency"] == 1.0
+    assert d["modes"]["batch_parallel+overlap"] is None
+    assert d["modes"]["matrix_parallel+overlap"] is None
+    assert d["modes"]["batch_parallel"]["value"] > 0
+
+
+def test_bench_world_size_mismatch_is_an_error():
+    env = dict(os.environ, RANK="0", WORLD_SIZE="2", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu",
+                        "--gpus", "4", "--size", "64"], capture_output=True, text=True,
+                       timeout=120, cwd="/tmp", env=env)
+    assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
+
+
+def test_bench_setup_failure_on_one_rank_is_agreed():
+    """A secondary mode that fails to set up on rank 1 only becomes an "error"
+    entry on rank 0's line; the headline and the other modes still report."""
+    r = _plain("--gpus", "2", "--size", "128", "--steps", "1", "--warmup", "0",
+               "--extra-steps", "1", "--extra-warmup", "0",
+               env_extra={"PDMB_BENCH_FAULT": "1:matrix_parallel:setup"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r)
+    assert "error" in d["modes"]["matrix_parallel"]
+    assert d["modes"]["batch_parallel"]["value"] > 0 and d["value"] > 0
+
+
+@pytest.mark.parametrize("spec", ["1:batch_parallel:timed", "1:independent:setup"])
+def test_bench_fault_exits_fast(spec):
+    """A timed-region fault on one rank (peers blocked in a collective) or a failed
+    headline ends the whole job non-zero within seconds, not at the PG timeout."""
+    import time
+
+    t0 = time.time()
+    r = _plain("--gpus", "2", "--size", "128", "--steps", "2", "--warmup", "1",
+               "--extra-steps", "2", "--extra-warmup", "1",
+               env_extra={"PDMB_BENCH_FAULT": spec, "PDMB_PG_TIMEOUT": "600"}, timeout=240)
+    assert r.returncode != 0
+    assert time.time() - t0 < 90
+    assert "injected fault" in r.stderr

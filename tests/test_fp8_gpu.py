@@ -88,6 +88,8 @@ def test_fp8_batched_and_column_shards():
 
 @pytest.mark.parametrize("kernel", ["fp8_w4", "fp8"])
 def test_fp8_race_screen(kernel):
+    if kernel in gemm.EXPERIMENT_KERNELS and not gemm.experiments_built():
+        pytest.skip("8-wave fp8 kernel: PDMB_EXPERIMENTS=1 build only")
     torch.manual_seed(11)
     A8, sa = gemm.fp8_quantize(torch.randn(4096, 4096, device="cuda"))
     B8, sb = gemm.fp8_quantize(torch.randn(4096, 4096, device="cuda"), colmajor=True)
@@ -101,6 +103,8 @@ def test_fp8_race_screen(kernel):
                                    (512, 512, 384)])
 def test_fp8_8wave_kernel_exact(M, N, K):
     """The 8-wave SCHED-3 fp8 kernel (kept for A/B) on the exact-integer cases."""
+    if not gemm.experiments_built():
+        pytest.skip("8-wave fp8 kernel: PDMB_EXPERIMENTS=1 build only")
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     Af, Bf = _ints((M, K), g), _ints((K, N), g)
     C = gemm.matmul(Af.to(FP8), _colmajor(Bf.to(FP8)), kernel="fp8")
@@ -122,3 +126,20 @@ def test_fp8_bench_loop():
     ms = gemm.bench_matmul(A8, B8, C, 10, 3) / 10
     tflops = 2 * 8192 ** 3 / ms / 1e9
     assert tflops > 1500, tflops  # above any bf16 rate: the fp8 MFMA path really runs
+
+
+@pytest.mark.parametrize("M,N,batch", [(1024, 16384, 1), (16384, 1024, 1), (1024, 16384, 2)])
+def test_fp8_thin_supertiles_exact(M, N, batch):
+    """4 x 64 / 64 x 4-tile rounds (map_tile supertiles 4 / 5): every tile written once."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + batch)
+    K = 256
+    Af = torch.stack([_ints((M, K), g) for _ in range(batch)])
+    Bf = torch.stack([_ints((K, N), g) for _ in range(batch)])
+    A8 = Af.to(FP8)
+    B8 = Bf.transpose(-1, -2).contiguous().to(FP8).transpose(-1, -2)
+    if batch == 1:
+        A8, B8, Af, Bf = A8[0], B8[0], Af[0], Bf[0]
+    C = torch.full(torch.broadcast_shapes(Af.shape[:-1] + (N,)), float("nan"), device="cuda",
+                   dtype=torch.bfloat16)
+    gemm.matmul(A8, B8, out=C)
+    assert torch.equal(C, (Af.double() @ Bf.double()).to(torch.bfloat16))

@@ -27,7 +27,17 @@ def test_native_extension_is_loaded():
     assert mod.__file__.endswith(".so")
 
 
-FAST = ["mfma256", "mfma256b", "mfma256c", "mfma256d"]
+# shipping LDS-DMA kernels + the 8-wave A/B schedules (those run only on a
+# PDMB_EXPERIMENTS=1 build; the default build must refuse them)
+FAST = ["mfma256d", "mfma256", "mfma256b", "mfma256c"]
+
+
+def _need(kernel):
+    """Skip an experiment-kernel case on the default (shipping) build."""
+    if kernel in gemm.EXPERIMENT_KERNELS and not gemm.experiments_built():
+        with pytest.raises(ValueError):
+            gemm._kid(kernel)
+        pytest.skip(f"{kernel} is an experiment kernel (PDMB_EXPERIMENTS=1 build)")
 
 
 @pytest.mark.parametrize("kernel", FAST)
@@ -35,11 +45,12 @@ FAST = ["mfma256", "mfma256b", "mfma256c", "mfma256d"]
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 128), (1000, 1048, 320),
                                    (300, 200, 128), (4352, 4352, 448)])
 def test_mfma256_exact_small_integers(dtype, M, N, K, kernel):
+    _need(kernel)
     dt = DT[dtype]
     g = torch.Generator(device="cuda").manual_seed(M * 7 + N)
     A = torch.randint(-1, 2, (M, K), device="cuda", generator=g).to(dt)
     B = torch.randint(-1, 2, (K, N), device="cuda", generator=g).to(dt)
-    assert gemm.kernel_for(A, B, kernel=kernel) == gemm.KERNEL_NAMES[gemm.KERNELS[kernel]]
+    assert gemm.kernel_for(A, B, kernel=kernel) == gemm.KERNEL_NAMES[gemm._kid(kernel)]
     C = gemm.matmul(A, B, kernel=kernel)
     R = _ref(A, B)  # |R| <= K <= 448: exact in fp16; bf16 rounds > 256 only
     if dt == torch.float16 or K <= 256:
@@ -65,6 +76,7 @@ def test_mfma256_identity_asymmetric(dtype):
 @pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
 @pytest.mark.parametrize("n", [2048, 4096])
 def test_mfma256_random(dtype, n, kernel):
+    _need(kernel)
     dt = DT[dtype]
     torch.manual_seed(0)
     A = torch.randn(n, n, device="cuda", dtype=dt)
@@ -76,6 +88,7 @@ def test_mfma256_random(dtype, n, kernel):
 
 @pytest.mark.parametrize("kernel", FAST)
 def test_mfma256_batched_and_broadcast(kernel):
+    _need(kernel)
     dt = torch.bfloat16
     torch.manual_seed(1)
     A = torch.randn(3, 512, 320, device="cuda", dtype=dt)
@@ -172,6 +185,7 @@ def test_native_bench_loop(graph):
 def test_race_screen_repeated_runs(kernel):
     """LDS-DMA pipeline race screen: identical outputs over many launches at several
     sizes, including one big enough to keep every CU busy for many rounds."""
+    _need(kernel)
     for n in (768, 2048, 2560, 8192):
         torch.manual_seed(n)
         A = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
@@ -187,6 +201,7 @@ def test_race_screen_repeated_runs(kernel):
                                    (300, 200, 64), (2304, 2048, 1024)])
 @pytest.mark.parametrize("kernel", ["f32_256", "f32_256s"])
 def test_f32_256_exact_and_random(M, N, K, kernel):
+    _need(kernel)
     g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
     A = torch.randint(-3, 4, (M, K), device="cuda", generator=g).float()
     B = torch.randint(-3, 4, (K, N), device="cuda", generator=g).float()
@@ -218,6 +233,7 @@ def test_f32_256_identity_batched_and_shards():
 
 @pytest.mark.parametrize("kernel", ["f32_256", "f32_256s"])
 def test_f32_256_race_screen(kernel):
+    _need(kernel)
     torch.manual_seed(11)
     A = torch.randn(4096, 4096, device="cuda")
     B = torch.randn(4096, 4096, device="cuda")
@@ -305,13 +321,15 @@ def test_w4_rejects_edge_tiles_and_auto_falls_back():
 # ---- thin grids: 8x32 / 32x8-tile super-tile rounds (map_tile supertile 2 / 3) ----
 
 @pytest.mark.parametrize("M,N,batch", [(2048, 8192, 1), (8192, 2048, 1), (2048, 8192, 2),
-                                       (8192, 2048, 3), (4096, 2048, 1)])
+                                       (8192, 2048, 3), (4096, 2048, 1),
+                                       (1024, 16384, 1), (16384, 1024, 1), (1024, 16384, 2)])
 @pytest.mark.parametrize("kernel,dtype", [("w4", "bfloat16"), ("w4", "float16"),
-                                          ("mfma256d", "bfloat16"), ("f32_256", "float32")])
+                                          ("mfma256d", "bfloat16"), ("f32_256s", "float32")])
 def test_thin_grid_supertiles_exact(M, N, batch, kernel, dtype):
     """Every output tile is written exactly once under the thin-grid block->tile
     maps (a mis-mapping leaves stale tiles or duplicates): integer data, exact
-    result. Shapes: row chunks of an overlap GEMM, ws=8 column shards."""
+    result. Shapes: row chunks of an overlap GEMM, ws=8 column shards; 1024 x 16384
+    and 16384 x 1024 are the 4 x 64 / 64 x 4-tile rounds (supertiles 4 / 5)."""
     dt, K = DT[dtype], 256
     g = torch.Generator(device="cuda").manual_seed(M + N + batch)
     A = torch.randint(-3, 4, (batch, M, K), device="cuda", generator=g).to(dt)
@@ -322,3 +340,122 @@ def test_thin_grid_supertiles_exact(M, N, batch, kernel, dtype):
                    dtype=dt)
     gemm.matmul(A, B, out=C, kernel=kernel)
     assert torch.equal(C, (A.double() @ B.double()).to(dt))
+
+
+# ---- W4 split-K: under-filled grids (matrix_parallel column shards at ws >= 4) ----
+
+@pytest.mark.parametrize("M,N,K,b,splitk", [
+    (2048, 2048, 2048, 1, 0), (4096, 512, 4096, 1, 8), (8192, 1024, 8192, 1, 2),
+    (1024, 1024, 4096, 1, 2), (1024, 1024, 4096, 1, 4), (1024, 1024, 4096, 1, 8),
+    (512, 512, 2048, 2, 4), (1024, 768, 832, 1, 4), (4096, 512, 4096, 1, 0)])
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+def test_w4_splitk_exact(M, N, K, b, splitk, dtype):
+    """Integer data keeps every fp32 slice partial and their sum exact: the split
+    result equals the fp64 product rounded once (K = 832 leaves the last of 4
+    slices one K-tile)."""
+    dt = DT[dtype]
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + splitk)
+    A = torch.randint(-3, 4, (b, M, K), device="cuda", generator=g).to(dt)
+    B = torch.randint(-3, 4, (b, K, N), device="cuda", generator=g).to(dt)
+    if b == 1:
+        A, B = A[0], B[0]
+    S = gemm.splitk_for(A, B, splitk=splitk)
+    assert S == splitk if splitk else S > 1
+    C = torch.full(torch.broadcast_shapes(A.shape[:-1] + (N,)), float("nan"), device="cuda",
+                   dtype=dt)
+    gemm.matmul(A, B, out=C, kernel="w4", splitk=splitk)
+    assert torch.equal(C, (A.double() @ B.double()).to(dt))
+
+
+def test_w4_splitk_choice_for_shard_shapes():
+    """Auto split only where the grid under-fills the 256 CUs."""
+    def S(M, N, K):
+        A = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
+        B = torch.empty(K, N, device="cuda", dtype=torch.bfloat16)
+        return gemm.splitk_for(A, B)
+    assert S(16384, 16384, 16384) == 1 and S(16384, 2048, 16384) == 1
+    assert S(8192, 1024, 8192) >= 2 and S(4096, 512, 4096) >= 4 and S(2048, 2048, 2048) >= 2
+    assert S(16384, 1024, 256) == 1  # too little K to split
+
+
+@pytest.mark.parametrize("M,N,K,splitk", [(8192, 1024, 8192, 0), (2048, 2048, 2048, 0),
+                                          (4096, 512, 4096, 8)])
+def test_w4_splitk_random_and_bitwise_repeatable(M, N, K, splitk):
+    """Random data vs fp64, and a race screen: the slices meet in a fixed order, so
+    every launch is bitwise identical whichever slice arrives last."""
+    torch.manual_seed(M + N)
+    A = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    B = torch.randn(K, N, device="cuda", dtype=torch.bfloat16)
+    ref = gemm.matmul(A, B, splitk=splitk)
+    assert _relerr(ref, _ref(A, B)) < TOL[torch.bfloat16]
+    for _ in range(30):
+        assert torch.equal(gemm.matmul(A, B, splitk=splitk), ref)
+    # unsplit W4 differs only by fp32 summation order
+    assert _relerr(gemm.matmul(A, B, splitk=1), ref.double()) < 1e-2
+
+
+def test_w4_splitk_concurrent_streams_and_graph():
+    """Per-stream counters: split-K GEMMs on two streams at once stay exact; a
+    torch.cuda.graph capture of one replays exactly (counters re-zeroed by
+    every launch)."""
+    g = torch.Generator(device="cuda").manual_seed(3)
+    A = torch.randint(-3, 4, (2048, 4096), device="cuda", generator=g).to(torch.bfloat16)
+    B = torch.randint(-3, 4, (4096, 1024), device="cuda", generator=g).to(torch.bfloat16)
+    R = (A.double() @ B.double()).to(torch.bfloat16)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = [torch.empty_like(R) for _ in range(8)]
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        with torch.cuda.stream(s1 if i % 2 else s2):
+            gemm.matmul(A, B, out=o, splitk=4)
+    torch.cuda.synchronize()
+    assert all(torch.equal(o, R) for o in outs)
+    s = torch.cuda.Stream()
+    out = torch.empty_like(R)
+    with torch.cuda.stream(s):
+        gemm.matmul(A, B, out=out, splitk=4)  # counters for s exist before capture
+    s.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        gemm.matmul(A, B, out=out, splitk=4)
+    for _ in range(3):
+        out.fill_(float("nan"))
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, R)
+
+
+def test_w4_splitk_native_bench_loop_graph():
+    A = torch.randn(2048, 2048, device="cuda", dtype=torch.bfloat16)
+    B = torch.randn(2048, 2048, device="cuda", dtype=torch.bfloat16)
+    out = torch.empty(2048, 2048, device="cuda", dtype=torch.bfloat16)
+    assert gemm.splitk_for(A, B) > 1
+    for graph in (False, True):
+        out.zero_()
+        assert gemm.bench_matmul(A, B, out, iters=5, warmup=0, graph=graph) > 0
+        assert _relerr(out, _ref(A, B)) < TOL[torch.bfloat16]
+
+
+def test_overlapping_views_are_refused_or_copied():
+    """An expanded / overlapping-row input is made contiguous; an overlapping
+    output is refused (never silently treated as contiguous)."""
+    x = torch.randn(512, device="cuda", dtype=torch.bfloat16)
+    A = x[None].expand(256, 512)  # stride(0) == 0
+    B = torch.randn(512, 256, device="cuda", dtype=torch.bfloat16)
+    assert _relerr(gemm.matmul(A, B), _ref(A, B)) < TOL[torch.bfloat16]
+    bad = torch.empty(256, device="cuda", dtype=torch.bfloat16)[None].expand(256, 256)
+    with pytest.raises(RuntimeError):
+        gemm.matmul(A.contiguous(), B, out=bad)
+    C3 = torch.empty(256, 256, device="cuda", dtype=torch.bfloat16)[None].expand(2, 256, 256)
+    with pytest.raises(RuntimeError):
+        gemm.matmul(torch.randn(2, 256, 512, device="cuda", dtype=torch.bfloat16), B, out=C3)
+
+
+def test_shipping_surface_refuses_diagnostics():
+    if gemm.experiments_built():
+        pytest.skip("experiment build")
+    A = torch.randn(256, 256, device="cuda", dtype=torch.bfloat16)
+    for k in ("diag_f32_nodma", "diag_fp8_w4_nowait", "mfma256c_stamp", "x_w4_tall"):
+        with pytest.raises(ValueError):
+            gemm.matmul(A, A, kernel=k)
+    assert _native.load().resolve(A, A, torch.empty_like(A), 20) == -1  # raw id, C++ side

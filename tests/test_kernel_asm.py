@@ -17,8 +17,10 @@ HIPCC = "/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else shut
 pytestmark = pytest.mark.skipif(HIPCC is None, reason="hipcc not available")
 
 
-def _kernels(src, tmp_path):
-    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{CSRC}", "-c",
+def _kernels(src, tmp_path, experiments=False):
+    """Compile ``src`` (default build, or with the A/B experiment kernels)."""
+    defs = ["-DPDMB_EXPERIMENTS=1"] if experiments else []
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{CSRC}", *defs, "-c",
                     os.path.join(CSRC, src), "-o", str(tmp_path / "k.o"), "-save-temps"],
                    cwd=tmp_path, check=True, capture_output=True, timeout=600)
     s = next(tmp_path.glob("*gfx950*.s")).read_text()
@@ -36,7 +38,7 @@ def _kernels(src, tmp_path):
 
 
 def test_bf16_lds_dma_kernel_stays_pipelined(tmp_path):
-    ks = _kernels("gemm_mfma256.hip", tmp_path)
+    ks = _kernels("gemm_mfma256.hip", tmp_path, experiments=True)  # SCHED 2 is an A/B build
     main = [k for k in ks if "gemm256_nn" in k and "ILi2ELi2ELb0E" in k]
     assert main, sorted(ks)
     k = ks[main[0]]
@@ -52,7 +54,7 @@ def test_bf16_lds_dma_kernel_stays_pipelined(tmp_path):
 
 
 def test_f32_kernel_no_spill(tmp_path):
-    ks = _kernels("gemm_f32_256.hip", tmp_path)
+    ks = _kernels("gemm_f32_256.hip", tmp_path, experiments=True)
     assert ks
     for name, k in ks.items():
         assert k["spill"] == 0 and "scratch_" not in k["body"], name
@@ -84,8 +86,20 @@ def test_w4_kernel_agpr_accumulators_and_counted_waits(tmp_path):
         b = k["body"]
         assert k["spill"] == 0 and k["lds"] == 2 * 65536
         assert re.search(r"v_mfma_f32_16x16x32_\w+ a\[", b)  # accumulators live in AGPRs
-        assert len(re.findall(r"s_waitcnt vmcnt\(0\)", b)) == 1
+        assert k["vgpr"] <= 256
+        loop = b[:b.find("global_atomic")]  # K-loop + drain; the split-K epilogue follows
+        assert "global_atomic" in b  # the fused split-K meeting point is compiled in
+        assert len(re.findall(r"s_waitcnt vmcnt\(0\)", loop)) == 1
         assert len(re.findall(r"s_waitcnt vmcnt\(16\) lgkmcnt\(0\)", b)) >= 4
         # loop body: 2 K-tiles x 8 blocks x 16 MFMAs, plus one odd tail K-tile
         assert len(re.findall(mfma, b)) == 3 * 128
         assert len(re.findall(r"buffer_load_dwordx4 .* lds", b)) >= 3 * 16
+
+
+def test_default_build_has_no_experiment_kernels(tmp_path):
+    """The shipping library instantiates only the shipping schedules."""
+    ks = _kernels("gemm_mfma256.hip", tmp_path)
+    assert ks and all("ELi3ELb0ELi0EE" in k for k in ks), sorted(ks)  # SCHED 3 only
+    (tmp_path / "fp8").mkdir()
+    ks = _kernels("gemm_fp8.hip", tmp_path / "fp8")
+    assert ks and all("gemm_fp8_w4ILi0ELi0E" in k for k in ks), sorted(ks)
