@@ -51,10 +51,9 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from pytorch_distributed_matmul_benchmark_amd.ops import gemm  # noqa: E402
-from pytorch_distributed_matmul_benchmark_amd.parallel.comm import (  # noqa: E402
-    CommStream, new_event, stream_ctx)
+from pytorch_distributed_matmul_benchmark_amd.parallel.comm import stream_ctx  # noqa: E402
 from pytorch_distributed_matmul_benchmark_amd.parallel.overlap import (  # noqa: E402
-    GatherOverlap, ReduceOverlap, compute_stream, gemm_chunks)
+    BidirRing, GatherOverlap, ReduceOverlap, compute_stream, gemm_chunks)
 from pytorch_distributed_matmul_benchmark_amd.parallel.dist import (  # noqa: E402
     DistContext, all_ok, barrier, cleanup_distributed, reduce_scalar, setup_distributed)
 from pytorch_distributed_matmul_benchmark_amd.parallel.partition import (  # noqa: E402
@@ -147,9 +146,10 @@ class Workload:
             self.flops = flop_gemm
             self.global_batch, self.parallelism = 1, f"tp{ws}"
         elif mode == "ring_parallel":
-            # Opt-in (not timed by default): all-gather-GEMM over the ring,
-            # models/ring_parallel.py. A row blocks rotate by P2P behind each hop's GEMM.
-            rs, sh = column_shard(n, ws, ctx.rank, align=256), column_shard(n, ws, ctx.rank, align=8)
+            # Opt-in (not timed by default): all-gather-GEMM over both ring
+            # directions, models/ring_parallel.py. A half-blocks rotate by P2P
+            # behind each hop's GEMMs.
+            rs, sh = column_shard(n, ws, ctx.rank, align=512), column_shard(n, ws, ctx.rank, align=8)
             A = self._rnd(n, n, seed=10_000)
             Al = torch.zeros(rs.padded, n, device=dev, dtype=dt)
             Al[:rs.width].copy_(A[rs.start:rs.stop])
@@ -161,27 +161,11 @@ class Workload:
             del Bg
             rp = rs.padded
             Cl = torch.empty(ws * rp, sh.padded, device=dev, dtype=odt)
-            R = [torch.empty_like(Al), torch.empty_like(Al)]
-            self.kernel = self._label(Al, Bl, Cl[:rp])
-            cs = CommStream(dev)
-            gdone = [new_event(dev) for _ in range(ws)]
-            rdone = [new_event(dev) for _ in range(max(ws - 1, 0))]
-            last = [None]
-            nxt, prv = (ctx.rank + 1) % ws, (ctx.rank - 1) % ws
+            self.kernel = self._label(Al[:rp // 2], Bl, Cl[:rp // 2])
+            ring = BidirRing(Al, rp, ctx.rank, ws, dev)
 
             def step():
-                cur = Al
-                for s in range(ws):
-                    if s > 0 and self.cuda:
-                        self.comp.wait_event(rdone[s - 1])
-                    if s < ws - 1:
-                        cs.exchange(cur, nxt, R[(s + 1) % 2], prv, after=last[0], done=rdone[s])
-                    j = (ctx.rank - s) % ws
-                    self._mm(cur, Bl, Cl[j * rp:(j + 1) * rp])
-                    gdone[s].record(comp)
-                    last[0] = gdone[s]
-                    if s < ws - 1:
-                        cur = R[(s + 1) % 2]
+                ring.step(self._mm, Bl, Cl, self.comp)
             self.flops = flop_gemm
             self.global_batch, self.parallelism = 1, f"ring{ws}"
         else:

@@ -11,24 +11,29 @@ Here A is not replicated; it is row-sharded like a sequence shard:
     every hop's GEMM is whole 256-row tiles) and B columns ``S_r``
     (matrix_parallel's column shard);
   * it computes C[:, S_r] = A @ B[:, S_r] — matrix_parallel's local product —
-    in ws row blocks. At hop s it multiplies the A block of rank (r - s) mod ws
-    while, on the high-priority comm stream, it forwards that block to
-    rank r+1 and receives the next one from rank r-1 (one batched
-    isend/irecv per hop);
-  * so compute of hop s overlaps the transfer for hop s+1, and each hop moves
-    N²/ws elements over the single xGMI link to the ring neighbour. A and C
-    stay sharded (N²/ws elements each per rank), so the per-rank memory does
-    not grow with N² as matrix_parallel's replicated A and gathered C do.
+    in ws row blocks, using BOTH directions of the ring: each A block is cut
+    into a top and a bottom half; tops travel clockwise (r -> r+1), bottoms
+    counter-clockwise (r -> r-1). At hop s the rank multiplies the top half
+    of rank (r - s)'s block and the bottom half of rank (r + s)'s block while,
+    on the high-priority comm stream, it forwards both halves and receives
+    the next two (one batched isend/irecv group of 4 transfers per hop);
+  * so compute of hop s overlaps the transfers for hop s+1, and each hop
+    moves N²/(2 ws) elements over EACH of the two xGMI links to the ring
+    neighbours (a one-directional ring moves N²/ws over one link: per-link
+    bound). A and C stay sharded (N²/ws elements each per rank),
+    so per-rank memory does not grow with N² as matrix_parallel's
+    replicated A and gathered C do.
 
-Event protocol (two receive buffers R0/R1; hop 0 reads the rank's own block):
+Event protocol (two receive buffers per direction; hop 0 reads the rank's
+own block):
 
-    comm hop s : wait(last GEMM issued) → send cur_s → r+1, recv R[(s+1)%2] ← r-1
-                 → record(recv_done[s])
-    compute s+1: wait(recv_done[s]) → GEMM(R[(s+1)%2])
+    comm hop s : wait(last GEMM issued) → send top_s → r+1, recv Rt[(s+1)%2] ← r-1,
+                 send bot_s → r-1, recv Rb[(s+1)%2] ← r+1 → record(recv_done[s])
+    compute s+1: wait(recv_done[s]) → GEMM(Rt[(s+1)%2]), GEMM(Rb[(s+1)%2])
 
 Waiting for the most recently issued GEMM before each hop guarantees that
-the buffer being overwritten (read by GEMM s-1) is no longer in use; the
-GEMM of hop s itself runs concurrently with the hop's transfer.
+the buffers being overwritten (read by hop s-1's GEMMs) are no longer in
+use; the GEMMs of hop s run concurrently with the hop's transfers.
 
 TFLOPS follows matrix_parallel: "portion" = 2N³ / t / ws per rank, system =
 AVG of that, Actual = 2N³ / t.
@@ -37,7 +42,8 @@ from __future__ import annotations
 
 import torch
 
-from ..parallel.comm import CommStream, current_stream, new_event
+from ..parallel.comm import current_stream
+from ..parallel.overlap import BidirRing
 from ..parallel.dist import DistContext
 from ..parallel.partition import column_shard
 from ..utils.metrics import gemm_flops, tflops_from
@@ -46,7 +52,7 @@ from . import independent
 from .common import (ModeResult, Workload, align_ranks, gemm_fn, kernel_label, out_dtype, randn,
                      sampled_relerr, warmup, zeros_b)
 
-ROW_ALIGN = 256  # one GEMM tile: every hop's product is whole tiles
+ROW_ALIGN = 512  # two GEMM tiles: each half-block product is whole 256-row tiles
 
 
 def make_operands(w: Workload, ctx: DistContext):
@@ -87,30 +93,13 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     A_local, B_local, rs, csh = make_operands(w, ctx)
     rp = rs.padded
     C_local = torch.empty((ws * rp, csh.padded), device=dev, dtype=out_dtype(w))
-    R = [torch.empty_like(A_local), torch.empty_like(A_local)]
     mm = gemm_fn(w, dev)
-    label = kernel_label(w, A_local, B_local, C_local[:rp])
-    nxt, prv = (r + 1) % ws, (r - 1) % ws
-    cs = CommStream(dev)
+    label = kernel_label(w, A_local[:rp // 2], B_local, C_local[:rp // 2])
     compute = current_stream(dev)
-    gemm_done = [new_event(dev) for _ in range(ws)]
-    recv_done = [new_event(dev) for _ in range(ws - 1)]
-    last = [None]  # event after the most recently issued GEMM (across iterations)
+    ring = BidirRing(A_local, rp, r, ws, dev)
 
     def step():
-        cur = A_local
-        for s in range(ws):
-            if s > 0 and compute is not None:
-                compute.wait_event(recv_done[s - 1])
-            if s < ws - 1:
-                # Forward this hop's block and receive the next one while it is multiplied.
-                cs.exchange(cur, nxt, R[(s + 1) % 2], prv, after=last[0], done=recv_done[s])
-            j = (r - s) % ws  # whose A rows ``cur`` holds
-            mm(cur, B_local, C_local[j * rp:(j + 1) * rp])
-            gemm_done[s].record(compute)
-            last[0] = gemm_done[s]
-            if s < ws - 1:
-                cur = R[(s + 1) % 2]
+        ring.step(mm, B_local, C_local, compute)
 
     warmup(step, w, ctx)
     align_ranks(ctx)
@@ -138,7 +127,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
                      compute_ms=comp, comm_ms=cm,
                      compute_only_tflops=tflops_from(flops_local, comp / 1e3),
                      kernel=label,
-                     extra={"shard_rows": rp, "shard_cols": csh.padded, "hops": ws - 1,
+                     extra={"shard_rows": rp, "shard_cols": csh.padded, "hops": ws - 1, "directions": 2,
                             "overlap": True})
     if w.check:
         synchronize(dev)

@@ -14,6 +14,7 @@ enum Kernel : int {
   kMfma256d = 9,  // gemm_mfma256.hip SCHED 3: 8 waves, 256x256, edge tiles (any M, N % 8)
   kFp8W4 = 16,    // gemm_fp8.hip: e4m3 A x column-major B, 4 waves x 128x128, bf16 out
   kMfmaW4 = 21,   // gemm_w4.hip: bf16/fp16 NN, 4 waves x 128x128, AGPR acc, split-K (M, N % 256)
+  kT128 = 26,     // gemm_t128.hip: bf16/fp16 NN, 128x128 tile, 4 waves x 64x64, split-K (M, N % 128)
 };
 
 // Experiment / diagnostic ids (A/B and timing-only builds). Compiled and
@@ -54,8 +55,8 @@ struct Problem {
   long long sA, sB, sC;
   int batch;
   float alpha = 1.0f;
-  // W4 split-K: K slices per output tile (0 = auto: split only under-filled
-  // grids, see choose_splitk; 1 = off). Ignored by the other kernels.
+  // W4 / T128 split-K: K slices per output tile (0 = auto: split only
+  // under-filled grids, see choose_splitk; 1 = off). Ignored by the others.
   int splitk = 0;
   // Caller-owned scratch of at least gemm_workspace_bytes(p, kernel) bytes
   // (padded-path copies, split-K partials), stream-ordered with the launch.
@@ -69,11 +70,16 @@ struct Problem {
 // one split-K launch.
 constexpr int kMaxSplitTiles = 4096;
 
+// Kernel an `auto` call runs through zero-padded workspace copies (the
+// padded fast path), or -1 if `auto` runs the problem as it is.
+int resolve_padded(const Problem& p);
+
 // Scratch bytes `gemm(p, kernel, ...)` needs in p.workspace (0 if none).
 size_t gemm_workspace_bytes(const Problem& p, int kernel);
 
-// K slices the W4 kernel would use for this problem (1 = no split).
-int choose_splitk(const Problem& p);
+// K slices the W4 / T128 kernel that `kernel` resolves to would use for this
+// problem (1 = no split; 0 = neither runs it, or p.splitk is not possible).
+int choose_splitk(const Problem& p, int kernel);
 
 // Which kernel `kernel` (kAuto allowed) resolves to for this problem;
 // -1 if the requested kernel cannot run it.

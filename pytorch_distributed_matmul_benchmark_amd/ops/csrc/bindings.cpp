@@ -143,13 +143,16 @@ int64_t resolve(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, i
   return pdmb::resolve_kernel(make_problem(A, B, C), (int)kernel);
 }
 
-// K slices the W4 kernel would use (1 = no split; 0 if W4 does not run it).
+int64_t resolve_padded(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C) {
+  return pdmb::resolve_padded(make_problem(A, B, C));
+}
+
+// K slices the W4 / T128 kernel would use (1 = no split; 0 if neither runs it).
 int64_t splitk_for(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t kernel,
                    int64_t splitk) {
   pdmb::Problem p = make_problem(A, B, C);
   p.splitk = (int)splitk;
-  if (pdmb::resolve_kernel(p, (int)kernel) != pdmb::kMfmaW4) return 0;
-  return pdmb::choose_splitk(p);
+  return pdmb::choose_splitk(p, (int)kernel);
 }
 
 // Total milliseconds for `iters` timed launches (after `warmup`).
@@ -225,6 +228,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("alpha") = 1.0, py::arg("splitk") = 0);
   m.def("resolve", &resolve, "kernel id that would run (or -1)", py::arg("A"), py::arg("B"),
         py::arg("out"), py::arg("kernel") = 0);
+  m.def("resolve_padded", &resolve_padded, "kernel the padded fast path runs (or -1)",
+        py::arg("A"), py::arg("B"), py::arg("out"));
   m.def("splitk_for", &splitk_for, "W4 K slices for this problem (0: not W4)", py::arg("A"),
         py::arg("B"), py::arg("out"), py::arg("kernel") = 0, py::arg("splitk") = 0);
   m.def("bench", &bench, "native hipEvent timing loop; returns total ms", py::arg("A"),

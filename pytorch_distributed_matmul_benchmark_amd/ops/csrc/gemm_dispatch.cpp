@@ -24,6 +24,8 @@ bool gemm_fp8_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_
 hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream);
 bool gemm_w4_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub = 0);
+bool gemm_t128_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
+hipError_t gemm_t128_launch(int dt, GemmArgs a, hipStream_t stream);
 
 static unsigned long long* g_debug_buffer = nullptr;
 
@@ -84,6 +86,12 @@ static bool is_experiment(int k) {
   }
 }
 
+struct Plan {
+  int kernel;  // kMfmaW4 | kT128 | -1
+  int splitk;
+};
+static Plan plan(const Problem& p, int kernel);
+
 int resolve_kernel(const Problem& p, int kernel) {
   if (is_experiment(kernel) && !experiments_built()) return -1;
   const GemmArgs a = to_args(p);
@@ -95,15 +103,22 @@ int resolve_kernel(const Problem& p, int kernel) {
   if (is_fp8_kernel(kernel)) return -1;
   const bool fast = gemm256_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   const bool w4 = gemm_w4_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
+  const bool t128 = gemm_t128_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   const bool f32fast = p.dtype == kF32 &&
                        gemm_f32_256_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   switch (kernel) {
     // Auto: the 4-wave kernel where the tiles are whole (M, N % 256; +4.5 %
     // over SCHED 3 at 16k, profiles/r1_s4_w4_ab.jsonl), SCHED 3 for edge tiles.
-    case kAuto: return (fast && w4) ? kMfmaW4 : fast ? kMfma256d : f32fast ? kF32_256s : kGeneric;
+    // Auto: the whole-tile kernels where the tiles are whole (W4 for grids
+    // that fill the chip, T128 for under-filled ones: plan()), SCHED 3 for
+    // edge tiles.
+    case kAuto:
+      if (w4 || t128) return plan(p, kAuto).kernel;
+      return fast ? kMfma256d : f32fast ? kF32_256s : kGeneric;
     case kGeneric: return kGeneric;
     case kMfma256d: return fast ? kMfma256d : -1;
     case kMfmaW4: return w4 ? kMfmaW4 : -1;
+    case kT128: return t128 ? kT128 : -1;
     case kF32_256s: return f32fast ? kF32_256s : -1;
 #ifdef PDMB_EXPERIMENTS
     case kF32_256: case kF32NoDma: return f32fast ? kernel : -1;
@@ -116,49 +131,87 @@ int resolve_kernel(const Problem& p, int kernel) {
   }
 }
 
-// ---- split-K (W4) -------------------------------------------------------
-// A grid of T 256x256 tiles fills the 256 CUs (1 workgroup / CU) only if T is
+// ---- tile size and split-K (W4 / T128) -------------------------------
+// A grid of T output tiles fills the 256 CUs (1 workgroup / CU) only if T is
 // a multiple of 256: the matrix_parallel column shards at ws >= 4 for the
 // reference's default sizes (matmul_scaling_benchmark.py:179-188, :351) have
-// T = 32 / 128 (4k / 8k at ws = 8), so one workgroup per tile leaves 1/8 or
-// 1/2 of the chip idle. Splitting K over S workgroups per tile multiplies the
-// grid by S. Model, in K-tile times of one workgroup: a launch costs
-//   waves(T * S) * (ceil(nk / S) + kFixed + kMeet * (S - 1) [S > 1])
-// (kMeet: the last slice's read of one 256 KiB fp32 slot, kFixed: prologue
-// + epilogue); pick the cheapest S in {1, 2, 4, 8} with >= kMinKt K-tiles per
-// slice. Measured constants: profiles/r2_splitk_*.
-static constexpr double kFixed = 2.0, kMeet = 1.5;
-static constexpr int kMinKt = 4;
+// T = 32 / 128 256x256 tiles (4k / 8k at ws = 8). Two levers: the 128x128
+// tile (T128, 4x the workgroups, each K-tile ~kT128Kt of a W4 K-tile) and
+// splitting K over S workgroups per tile (each extra slice costs the last one
+// a serial read of one fp32 slab: 256 KiB for W4, 64 KiB for T128). Model, in
+// W4 K-tile times (~1.2 us on MI355X):
+//   cost = waves(T * S) * (ceil(nk / S) * kt + fixed + meet * (S - 1))
+// over W4 x S in {1, 2} and T128 x S in {1, 2, 4}; the cheapest wins, W4 on
+// ties (its tile is the more efficient one at full occupancy). Constants from
+// profiles/r2_splitk_sweep.jsonl / r2_t128_sweep.jsonl.
+static constexpr double kT128Kt = 0.30;   // T128 K-tile / W4 K-tile
+static constexpr double kFixed = 1.0;     // launch + prologue + epilogue
+static constexpr double kMeetW4 = 3.0;    // 256 KiB slab
+static constexpr double kMeetT128 = 0.8;  // 64 KiB slab
+static constexpr int kMinKt = 4;          // K-tiles per slice, at least
 
-int choose_splitk(const Problem& p) {
-  if (p.M % 256 || p.N % 256 || p.K % 64 || p.K <= 0) return 1;
-  const long long T = (long long)(p.M / 256) * (p.N / 256) * (p.batch < 1 ? 1 : p.batch);
+static long long tiles_of(const Problem& p, int tile) {
+  return (long long)(p.M / tile) * (p.N / tile) * (p.batch < 1 ? 1 : p.batch);
+}
+
+static double plan_cost(const Problem& p, int kernel, int S) {
+  const int tile = kernel == kT128 ? 128 : 256;
+  const long long T = tiles_of(p, tile);
   const int nk = p.K / 64;
-  if (p.splitk > 0) return p.splitk;
-  if (T <= 0 || T > kMaxSplitTiles) return 1;
-  auto cost = [&](int S) {
-    const long long waves = (T * S + 255) / 256;
-    const int per = (nk + S - 1) / S;
-    return (double)waves * (per + kFixed + (S > 1 ? kMeet * (S - 1) : 0.0));
-  };
-  int best = 1;
-  double bc = cost(1);
-  for (int S = 2; S <= 8; S *= 2) {
-    const int per = (nk + S - 1) / S;
-    if (per < kMinKt || (S - 1) * per >= nk) break;
-    const double c = cost(S);
-    if (c < bc * 0.97) {  // split only for a clear win
-      best = S;
+  const int per = (nk + S - 1) / S;
+  const double kt = kernel == kT128 ? kT128Kt : 1.0;
+  const double meet = kernel == kT128 ? kMeetT128 : kMeetW4;
+  return (double)((T * S + 255) / 256) * (per * kt + kFixed + meet * (S - 1));
+}
+
+static bool split_ok(const Problem& p, int kernel, int S) {
+  if (S == 1) return true;
+  const int nk = p.K / 64;
+  const int per = (nk + S - 1) / S;
+  const int tile = kernel == kT128 ? 128 : 256;
+  return per >= kMinKt && (S - 1) * per < nk && tiles_of(p, tile) <= kMaxSplitTiles;
+}
+
+// `kernel`: kAuto (choose), kMfmaW4 or kT128 (choose only the split).
+// p.splitk > 0 fixes the split.
+static Plan plan(const Problem& p, int kernel) {
+  const GemmArgs a = to_args(p);
+  const bool w4 = (kernel == kAuto || kernel == kMfmaW4) &&
+                  gemm_w4_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
+  const bool t128 = (kernel == kAuto || kernel == kT128) &&
+                    gemm_t128_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
+  Plan best{-1, 1};
+  double bc = 1e300;
+  auto consider = [&](int k, int S) {
+    if (p.splitk > 0 && S != p.splitk) return;
+    if (!split_ok(p, k, S)) return;
+    const double c = plan_cost(p, k, S);
+    if (c < bc * 0.97) {  // a different choice only for a clear win
       bc = c;
+      best = Plan{k, S};
     }
-  }
+  };
+  static const int kS[] = {1, 2, 4, 8};
+  if (w4)
+    for (int S : kS)
+      if (S <= 2 || p.splitk == S) consider(kMfmaW4, S);
+  if (t128)
+    for (int S : kS)
+      if (S <= 4 || p.splitk == S) consider(kT128, S);
+  if (best.kernel < 0 && (w4 || t128)) best = Plan{w4 ? kMfmaW4 : kT128, 0};  // invalid split
   return best;
 }
 
-static size_t splitk_bytes(const Problem& p, int S) {
+int choose_splitk(const Problem& p, int kernel) {
+  const int k = resolve_kernel(p, kernel);
+  if (k != kMfmaW4 && k != kT128) return 0;
+  return plan(p, k).splitk;
+}
+
+static size_t splitk_bytes(const Problem& p, int kernel, int S) {
   if (S <= 1) return 0;
-  const long long T = (long long)(p.M / 256) * (p.N / 256) * (p.batch < 1 ? 1 : p.batch);
-  return (size_t)T * S * 256 * 256 * sizeof(float);  // one slot per slice (the last's unused)
+  const int tile = kernel == kT128 ? 128 : 256;
+  return (size_t)tiles_of(p, tile) * S * tile * tile * sizeof(float);  // one slot per slice
 }
 
 // Per-(device, stream) split-K counters (2 per tile), zeroed once on the
@@ -188,12 +241,14 @@ static unsigned* stream_counters(hipStream_t s) {
   return c;
 }
 
-static hipError_t w4_launch(const Problem& p, GemmArgs a, void* part, size_t part_bytes,
-                            hipStream_t stream, int sub = 0) {
-  int S = choose_splitk(p);
+// Launch W4 or T128 (kernel k, already resolved) with its planned split.
+static hipError_t tiled_launch(const Problem& p, int k, GemmArgs a, void* part, size_t part_bytes,
+                               hipStream_t stream, int sub = 0) {
+  int S = plan(p, k == kT128 ? kT128 : kMfmaW4).splitk;
+  if (S < 1) return hipErrorInvalidValue;  // requested split not possible for this K
   if (S > 1) {
     unsigned* flags = stream_counters(stream);
-    if (!flags || part_bytes < splitk_bytes(p, S) || !part) {
+    if (!flags || part_bytes < splitk_bytes(p, k, S) || !part) {
       if (p.splitk > 1) return hipErrorInvalidValue;  // explicitly requested: no silent change
       S = 1;
     } else {
@@ -202,7 +257,7 @@ static hipError_t w4_launch(const Problem& p, GemmArgs a, void* part, size_t par
     }
   }
   a.splitk = S;
-  return gemm_w4_launch(p.dtype, a, stream, sub);
+  return k == kT128 ? gemm_t128_launch(p.dtype, a, stream) : gemm_w4_launch(p.dtype, a, stream, sub);
 }
 
 // ---- padded fast path -------------------------------------------------------
@@ -316,14 +371,21 @@ static Padded padded_problem(const Problem& p, char* w) {
   return d;
 }
 
+int resolve_padded(const Problem& p) {
+  if (!wants_padding(p, kAuto)) return -1;
+  return resolve_kernel(padded_problem(p, nullptr).q, kAuto);
+}
+
 size_t gemm_workspace_bytes(const Problem& p, int kernel) {
   if (wants_padding(p, kernel)) {
     const Padded d = padded_problem(p, nullptr);
     const size_t copies = d.a_bytes + d.b_bytes + d.c_bytes;
-    return copies + (resolve_kernel(d.q, kAuto) == kMfmaW4 ? splitk_bytes(d.q, choose_splitk(d.q)) : 0);
+    const int k = resolve_kernel(d.q, kAuto);
+    return copies + ((k == kMfmaW4 || k == kT128) ? splitk_bytes(d.q, k, plan(d.q, k).splitk) : 0);
   }
-  if (resolve_kernel(p, kernel) == kMfmaW4 || (kernel == kMfmaW4Tall || kernel == kMfmaW4Wide))
-    return splitk_bytes(p, choose_splitk(p));
+  const int k = resolve_kernel(p, kernel);
+  if (k == kMfmaW4 || k == kT128) return splitk_bytes(p, k, plan(p, k).splitk);
+  if (k == kMfmaW4Tall || k == kMfmaW4Wide) return splitk_bytes(p, kMfmaW4, plan(p, kMfmaW4).splitk);
   return 0;
 }
 
@@ -358,7 +420,7 @@ static hipError_t gemm_padded(const Problem& p, hipStream_t stream, int* used) {
   char* part = Cp + d.c_bytes;
   const size_t part_bytes = p.workspace_bytes - (d.a_bytes + d.b_bytes + d.c_bytes);
   e = k == kF32_256s  ? gemm_f32_256_launch(a, 1, stream)
-      : k == kMfmaW4 ? w4_launch(q, a, part, part_bytes, stream)
+      : (k == kMfmaW4 || k == kT128) ? tiled_launch(q, k, a, part, part_bytes, stream)
                      : gemm256_launch(q.dtype, a, 4, stream);
   if (e != hipSuccess) return e;
   for (int b = 0; b < batch; ++b) {
@@ -391,7 +453,8 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
   switch (k) {
     case kFp8W4: return gemm_fp8_launch(a, 1, stream);
     case kMfma256d: return gemm256_launch(p.dtype, a, 4, stream);
-    case kMfmaW4: return w4_launch(p, a, p.workspace, p.workspace_bytes, stream);
+    case kMfmaW4:
+    case kT128: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream);
     case kF32_256s: return gemm_f32_256_launch(a, 1, stream);
 #ifdef PDMB_EXPERIMENTS
     case kFp8: return gemm_fp8_launch(a, 0, stream);
@@ -404,8 +467,8 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kMfma256b: return gemm256_launch(p.dtype, a, 1, stream);
     case kMfma256c: return gemm256_launch(p.dtype, a, 2, stream);
     case kMfma256Stamp: return gemm256_launch(p.dtype, a, 3, stream);
-    case kMfmaW4Tall: return w4_launch(p, a, p.workspace, p.workspace_bytes, stream, 1);
-    case kMfmaW4Wide: return w4_launch(p, a, p.workspace, p.workspace_bytes, stream, 2);
+    case kMfmaW4Tall: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 1);
+    case kMfmaW4Wide: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 2);
     case kF32_256: return gemm_f32_256_launch(a, 0, stream);
     case kF32NoDma: return gemm_f32_256_launch(a, 9, stream);
     case kMfma256X1: case kMfma256X2: case kMfma256X4:
@@ -473,6 +536,7 @@ const char* kernel_name(int kernel) {
     case kF32_256s: return "pdmb_f32_256s_nn";
     case kFp8W4: return "pdmb_fp8_w4_nt";
     case kMfmaW4: return "pdmb_w4_nn";
+    case kT128: return "pdmb_t128_nn";
     case kMfma256: return "pdmb_mfma256_nn";
     case kMfma256b: return "pdmb_mfma256b_nn";
     case kMfma256c: return "pdmb_mfma256c_nn";

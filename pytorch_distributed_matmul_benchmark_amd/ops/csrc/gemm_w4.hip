@@ -32,6 +32,7 @@
 // 8-B aligned C.
 #include "api.h"
 #include "common.h"
+#include "splitk.h"
 
 namespace pdmb {
 namespace kw4 {
@@ -184,63 +185,6 @@ __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, f32
   }
 }
 
-// Split-K meeting point of the S workgroups of one output tile, fused into
-// the epilogue (no second kernel, no memset). The first S-1 to arrive each
-// park their fp32 accumulators in their slice's slot of `part`; the last to
-// arrive gets the slots back (nullptr for the others) and writes C as
-// slot 0 + slot 1 + ... in slice order with its own registers in its own
-// place, so the result is bitwise reproducible whoever arrives last. Arrival
-// order comes from a per-tile counter, so no workgroup ever waits for one
-// that has not started: the last waits only for slots whose owners have
-// already arrived, i.e. are resident and past their K-loop, and finish their
-// stores unconditionally (no co-residency assumption, safe next to RCCL or
-// under a CU mask). The last workgroup re-zeroes both counters, so they are
-// zero between launches on a stream (which never overlap).
-//
-// Slot layout follows the accumulator registers (f32x4 (i, j) of thread t at
-// ((i * 8 + j) * 256 + t) * 16 B): every store and load is a fully coalesced
-// 1 KiB wave access, and no index math depends on the MFMA layout.
-// Memory order: stores -> release fence -> `done` increment; `done` load ->
-// acquire fence in every thread -> slot loads. The agent-scope fences write
-// back / invalidate the XCD-private L2s, so the slices may sit on any XCDs.
-template <int N8>
-__device__ __forceinline__ const f32x4* splitk_meet(const GemmArgs& a, char* smem, int bz, int tm,
-                                                    int tn, int slice, f32x4 (&acc)[N8][8]) {
-  const int S = a.splitk;
-  const long long tile = ((long long)bz * a.tiles_m + tm) * a.tiles_n + tn;
-  unsigned* arrive = a.flags + 2 * tile;
-  unsigned* done = arrive + 1;
-  int* bcast = (int*)smem;
-  __syncthreads();  // every wave is past its last LDS read before smem is reused
-  if (threadIdx.x == 0)
-    bcast[0] = (int)__hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  const int ord = bcast[0];
-  const int t = threadIdx.x;
-  f32x4* slots = (f32x4*)(a.part + tile * (long long)S * (N8 * 8 * 4 * NT));
-  if (ord < S - 1) {
-    f32x4* p = slots + (long long)slice * (N8 * 8 * NT);
-#pragma unroll
-    for (int i = 0; i < N8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) p[(i * 8 + j) * NT + t] = acc[i][j];
-    __threadfence();
-    __syncthreads();
-    if (t == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return nullptr;
-  }
-  if (t == 0) {
-    while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(S - 1))
-      __builtin_amdgcn_s_sleep(1);
-    // Nobody else touches this tile's counters in this launch any more.
-    __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  __threadfence();
-  return slots + t;  // slot s, block (i, j): [(s * N8 * 8 + i * 8 + j) * NT] (own slot unused)
-}
-
 // SUB: XCD sub-block shape (map_tile): 0 = 4 x 8 (default), 1 = 8 x 4
 // (kMfmaW4Tall), 2 = 2 x 16 (kMfmaW4Wide); 1 and 2 are A/B experiments.
 template <int DT, int SUB = 0>
@@ -354,14 +298,14 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4_nn(GemmArgs a) {
   // (asm MFMAs are invisible to hipcc's hazard recognizer).
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
 
-  // Split-K: only the last slice of a tile to arrive gets here with `red`
-  // (the other slices' fp32 slots); it adds them block row by block row
-  // while storing, so no more than 2 x 8 fragments are live in VGPRs.
-  const f32x4* red = nullptr;
-  if (a.splitk > 1) {
-    red = splitk_meet(a, smem, bz, tm, tn, slice, acc);
-    if (!red) return;
-  }
+  // Split-K: only the last slice of a tile to arrive writes C, adding the
+  // other slices' fp32 slots block row by block row while storing, so no
+  // more than 2 x 8 fragments are live in VGPRs (splitk.h).
+  SplitSlots sl;
+  const bool split = a.splitk > 1;
+  if (split && !splitk_meet<8, 8, NT>(a, smem, ((long long)bz * a.tiles_m + tm) * a.tiles_n + tn,
+                                      slice, acc, sl))
+    return;
 
   // Epilogue: acc[i][j] holds C^T of a 16x16 tile: lane owns row l16 and
   // columns 4g..4g+3 (interior tiles only: no masks).
@@ -369,28 +313,11 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4_nn(GemmArgs a) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     f32x4 v[8];
-    if (!red) {
+    if (!split) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = acc[i][j];
-    } else {  // sum over slices in slice order (bitwise reproducible)
-      for (int s = 0; s < a.splitk; ++s) {
-        f32x4 q[8];
-        if (s == slice) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) q[j] = acc[i][j];
-        } else {
-          const f32x4* p = red + (long long)(s * 64 + i * 8) * NT;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) q[j] = p[j * NT];
-        }
-        if (s == 0) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = q[j];
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] += q[j];
-        }
-      }
+    } else {
+      splitk_row<8, 8, NT>(a, sl, slice, i, acc, v);
     }
     const int row = m0 + wr * 128 + i * 16 + l16;
     char* crow = Cb + (long long)row * a.ldc * 2;

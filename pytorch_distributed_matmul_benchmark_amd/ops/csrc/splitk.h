@@ -1,0 +1,118 @@
+// In-launch split-K combine shared by the W4 (256x256) and T128 (128x128)
+// kernels: the S workgroups of one output tile meet in the epilogue (no
+// second kernel, no memset, no fences).
+//
+// Hand-off (cdna_hip_programming.md Guideline 16, "sc1" form; MI355X_MICROARCH
+// § visibility, Valid forms row 1): the first S-1 slices to arrive (arrival
+// ticket from the per-tile `arrive` counter) store their fp32 accumulators
+// WRITE-THROUGH (buffer_store_dwordx4 ... sc1) into their slice's slot, every
+// storing wave drains (s_waitcnt vmcnt(0)), the workgroup meets at a barrier,
+// and one lane adds to the tile's `done` counter (relaxed, agent scope). The
+// last to arrive polls `done` (relaxed agent loads = sc1, s_sleep between)
+// until S-1, then EVERY load of the slots is an sc1 load, so no acquire fence
+// is needed and none of the ~3.5 us __threadfence() pairs of round 1's
+// version are paid. The last slice sums slot 0 + slot 1 + ... in slice order
+// with its own registers in its own place: bitwise reproducible whoever
+// arrives last. It never waits for a workgroup that has not started (only for
+// slots whose owners already took a ticket, i.e. are resident and past their
+// K-loop), so no co-residency is assumed (safe beside RCCL / under a CU mask).
+// The last slice re-zeroes both counters, which are therefore zero between
+// launches on a stream (launches on one stream never overlap; the counters
+// are zeroed once per stream when created, gemm_dispatch.cpp).
+//
+// Slot layout follows the accumulator registers: f32x4 block b of thread t at
+// ((slice * NBLK + b) * NT + t) * 16 B, so every access is a coalesced 1 KiB
+// wave access and no index math depends on the MFMA layout.
+#pragma once
+
+#include "common.h"
+
+namespace pdmb {
+
+struct SplitSlots {
+  __amdgpu_buffer_rsrc_t rs;  // this tile's S slots (valid for the reducer)
+  int t;                      // thread index
+};
+
+template <int NBLK, int NT>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t splitk_rsrc(const GemmArgs& a, long long tile) {
+  constexpr long long slot_floats = (long long)NBLK * NT * 4;
+  return __builtin_amdgcn_make_buffer_rsrc(a.part + tile * a.splitk * slot_floats, 0,
+                                           (int)(a.splitk * slot_floats * 4), 0x00020000);
+}
+
+// Returns true in the workgroup that must write C (the last slice); `out`
+// then addresses the slots. `smem` is the kernel's one LDS array (reused for
+// the broadcast after a barrier: a second __shared__ object can de-pipeline
+// the LDS-DMA loop, cdna_hip_programming.md trap 4(a)).
+template <int MB, int NB, int NT>
+__device__ __forceinline__ bool splitk_meet(const GemmArgs& a, char* smem, long long tile, int slice,
+                                            f32x4 (&acc)[MB][NB], SplitSlots& out) {
+  constexpr int NBLK = MB * NB;
+  const int S = a.splitk;
+  unsigned* arrive = a.flags + 2 * tile;
+  unsigned* done = arrive + 1;
+  int* bcast = (int*)smem;
+  const int t = threadIdx.x;
+  __syncthreads();  // every wave is past its last LDS read before smem is reused
+  if (t == 0)
+    bcast[0] = (int)__hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int ord = bcast[0];
+  const __amdgpu_buffer_rsrc_t rs = splitk_rsrc<NBLK, NT>(a, tile);
+  if (ord < S - 1) {
+#pragma unroll
+    for (int i = 0; i < MB; ++i)
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(u32x4, acc[i][j]), rs,
+            ((slice * NBLK + i * NB + j) * NT + t) * 16, 0, 16 /* sc1: write-through */);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains
+    __syncthreads();
+    if (t == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
+  }
+  if (t == 0) {
+    while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(S - 1))
+      __builtin_amdgcn_s_sleep(1);
+    // Nobody touches this tile's counters again in this launch.
+    __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // Compiler-only ordering: keep the sc1 slot loads below the poll.
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __syncthreads();
+  out.rs = rs;
+  out.t = t;
+  return true;
+}
+
+// Block row i of the tile's sum over slices, in slice order (the reducer).
+template <int MB, int NB, int NT>
+__device__ __forceinline__ void splitk_row(const GemmArgs& a, const SplitSlots& sl, int slice, int i,
+                                           const f32x4 (&acc)[MB][NB], f32x4 (&v)[NB]) {
+  constexpr int NBLK = MB * NB;
+  for (int s = 0; s < a.splitk; ++s) {
+    f32x4 q[NB];
+    if (s == slice) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) q[j] = acc[i][j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        q[j] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                       sl.rs, ((s * NBLK + i * NB + j) * NT + sl.t) * 16, 0, 16 /* sc1 */));
+    }
+    if (s == 0) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) v[j] = q[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) v[j] += q[j];
+    }
+  }
+}
+
+}  // namespace pdmb

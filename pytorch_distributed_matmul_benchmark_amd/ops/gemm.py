@@ -21,7 +21,8 @@ import torch
 from . import _native
 
 # The shipping kernels: the public ``kernel=`` surface (api.h ``Kernel``).
-KERNELS = {"auto": 0, "generic": 2, "f32_256s": 7, "mfma256d": 9, "fp8_w4": 16, "w4": 21}
+KERNELS = {"auto": 0, "generic": 2, "f32_256s": 7, "mfma256d": 9, "fp8_w4": 16, "w4": 21,
+           "t128": 26}
 # A/B and timing-only diagnostic kernels (api.h ``ExperimentKernel``): accepted
 # only by a library built with ``PDMB_EXPERIMENTS=1``; ``diag_*`` ones skip waits
 # or data movement on purpose and compute WRONG results.
@@ -31,7 +32,7 @@ EXPERIMENT_KERNELS = {"mfma256": 1, "mfma256b": 3, "mfma256c": 4, "mfma256c_stam
                       "diag_fp8_w4_mfma_only": 19, "diag_f32_nodma": 20, "x_w4_tall": 22,
                       "x_w4_wide": 23, "x_fp8_w4_tall": 24, "x_fp8_w4_wide": 25}
 KERNEL_NAMES = {0: "auto", 2: "pdmb_generic_nn", 7: "pdmb_f32_256s_nn", 9: "pdmb_mfma256d_nn",
-                16: "pdmb_fp8_w4_nt", 21: "pdmb_w4_nn", 1: "pdmb_mfma256_nn",
+                16: "pdmb_fp8_w4_nt", 21: "pdmb_w4_nn", 26: "pdmb_t128_nn", 1: "pdmb_mfma256_nn",
                 3: "pdmb_mfma256b_nn", 4: "pdmb_mfma256c_nn", 5: "pdmb_mfma256c_stamp",
                 6: "pdmb_f32_256_nn", 15: "pdmb_fp8_256_nt", -1: "unsupported"}
 SUPPORTED_DTYPES = (torch.float32, torch.float16, torch.bfloat16)
@@ -109,8 +110,8 @@ def matmul(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
            kernel="auto", alpha: float = 1.0, splitk: int = 0) -> torch.Tensor:
     """``out = A @ B`` for 2-D/3-D row-major operands (3-D = batched).
 
-    ``splitk`` (W4 only): K slices per output tile, 0 = auto (split only grids
-    that under-fill the 256 CUs, ``splitk_for``), 1 = never.
+    ``splitk`` (W4 / T128 only): K slices per output tile, 0 = auto (split only
+    grids that under-fill the 256 CUs, ``splitk_for``), 1 = never.
 
     float8_e4m3fn operands: ``out = alpha * (A @ B)`` in bfloat16 on the
     block-scaled fp8 MFMA (B is used column-major; a row-major B is copied).
@@ -151,14 +152,11 @@ def padded_kernel_for(A: torch.Tensor, B: torch.Tensor) -> Optional[str]:
     """Fast kernel an ``auto`` call runs through zero-padded copies, or None."""
     if A.device.type != "cuda" or A.dtype not in SUPPORTED_DTYPES:
         return None
-    M, K, N = A.shape[-2], A.shape[-1], B.shape[-1]
-    batch = max(A.shape[0] if A.dim() == 3 else 1, B.shape[0] if B.dim() == 3 else 1)
-    if 2.0 * M * N * K * batch < PAD_MIN_FLOPS or kernel_for(A, B) != "pdmb_generic_nn":
-        return None
-    if A.dtype == torch.float32:
-        return "pdmb_f32_256s_nn"
-    # gemm_dispatch.cpp: M is never padded, N is rounded up to 8; whole 256-tiles -> W4
-    return "pdmb_w4_nn" if M % 256 == 0 and (N + 7) // 8 * 8 % 256 == 0 else "pdmb_mfma256d_nn"
+    C = _native.load()
+    out = torch.empty(_out_shape(A, B), dtype=out_dtype(A.dtype), device=A.device)
+    A, B = _prep_pair(A, B)
+    k = int(C.resolve_padded(A, B, out))
+    return KERNEL_NAMES[k] if k >= 0 else None
 
 
 def bmm(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
@@ -185,7 +183,7 @@ def kernel_for(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = N
 
 def splitk_for(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
                kernel="auto", splitk: int = 0) -> int:
-    """K slices the W4 kernel uses for these operands (1: unsplit, 0: not W4)."""
+    """K slices the W4 / T128 kernel uses for these operands (1: unsplit, 0: neither)."""
     if A.device.type != "cuda":
         return 0
     C = _native.load()

@@ -106,21 +106,39 @@ class CommStream:
         """One ring hop on the comm stream: ``send`` → rank ``dst`` while ``recv``
         ← rank ``src`` (global ranks), issued as one batched P2P group so RCCL
         runs both directions of the hop concurrently."""
+        return self.exchange_multi([(send, dst)], [(recv, src)], after=after, done=done)
+
+    def exchange_multi(self, sends, recvs, after=None, done=None):
+        """Several point-to-point transfers as ONE batched group on the comm
+        stream (``sends``: [(tensor, dst)], ``recvs``: [(tensor, src)]). The
+        bidirectional ring sends half a block to each neighbour this way, so
+        every hop drives two xGMI links (one per direction) instead of one.
+        Transfer i carries tag i (gloo matches on it; RCCL matches in issue
+        order, which is the same list order on every rank), so two transfers
+        between the same pair (ws = 2) never cross."""
         with stream_ctx(self.stream):
             if after is not None:
                 self.wait_event(after)
             # gloo P2P takes host memory only: GPU tensors of a gloo rehearsal
             # (ranks sharing one GPU) hop through host copies on this stream.
-            staged = send.is_cuda and dist.get_backend(self.group) == "gloo"
-            s_t, r_t = (send.cpu(), torch.empty(recv.shape, dtype=recv.dtype)) if staged \
-                else (send, recv)
-            ops = [dist.P2POp(dist.isend, s_t, dst, group=self.group),
-                   dist.P2POp(dist.irecv, r_t, src, group=self.group)]
+            staged = bool(sends) and sends[0][0].is_cuda and dist.get_backend(self.group) == "gloo"
+            ops, landing = [], []
+            for i in range(max(len(sends), len(recvs))):
+                if i < len(sends):
+                    t, dst = sends[i]
+                    ops.append(dist.P2POp(dist.isend, t.cpu() if staged else t, dst,
+                                          group=self.group, tag=i))
+                if i < len(recvs):
+                    t, src = recvs[i]
+                    r_t = torch.empty(t.shape, dtype=t.dtype) if staged else t
+                    landing.append((t, r_t))
+                    ops.append(dist.P2POp(dist.irecv, r_t, src, group=self.group, tag=i))
             works = dist.batch_isend_irecv(ops)
             for wk in works:
                 wk.wait()
             if staged:
-                recv.copy_(r_t)
+                for t, r_t in landing:
+                    t.copy_(r_t)
             if done is not None:
                 done.record(self.stream)
         return works

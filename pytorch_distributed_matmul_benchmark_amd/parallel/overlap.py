@@ -154,3 +154,42 @@ class ReduceOverlap:
             self.cs.all_reduce(C[b, s:e], after=self.ready[u], done=self.done[u])
         if compute is not None and self.done:
             compute.wait_event(self.done[-1])
+
+
+class BidirRing:
+    """ring_parallel (models/ring_parallel.py): all-gather-GEMM over both ring
+    directions. Rank r's A block (``rp`` rows) is cut into a top and a bottom
+    half; tops rotate clockwise (r -> r+1), bottoms counter-clockwise, so each
+    hop drives the links to BOTH neighbours. Hop s multiplies the top of rank
+    (r - s)'s block and the bottom of rank (r + s)'s block into
+    ``C_local[j * rp : (j + 1) * rp]`` while the next halves move."""
+
+    def __init__(self, A_local: torch.Tensor, rp: int, rank: int, ws: int,
+                 device: torch.device, comm: Optional[CommStream] = None):
+        self.A, self.rp, self.h, self.r, self.ws = A_local, rp, rp // 2, rank, ws
+        self.Rt = [torch.empty_like(A_local[:self.h]) for _ in range(2)]
+        self.Rb = [torch.empty_like(A_local[self.h:]) for _ in range(2)]
+        self.cs = comm or CommStream(device)
+        self.gemm_done = [new_event(device) for _ in range(ws)]
+        self.recv_done = [new_event(device) for _ in range(max(ws - 1, 0))]
+        self.last = None  # event after the most recently issued GEMM (across steps)
+
+    def step(self, mm, B_local, C_local, compute) -> None:
+        r, ws, rp, h = self.r, self.ws, self.rp, self.h
+        nxt, prv = (r + 1) % ws, (r - 1) % ws
+        top, bot = self.A[:h], self.A[h:]
+        for s in range(ws):
+            if s > 0 and compute is not None:
+                compute.wait_event(self.recv_done[s - 1])
+            if s < ws - 1:
+                # forward both halves, receive the next two while these multiply
+                self.cs.exchange_multi([(top, nxt), (bot, prv)],
+                                       [(self.Rt[(s + 1) % 2], prv), (self.Rb[(s + 1) % 2], nxt)],
+                                       after=self.last, done=self.recv_done[s])
+            jt, jb = (r - s) % ws, (r + s) % ws  # whose A rows each half holds
+            mm(top, B_local, C_local[jt * rp:jt * rp + h])
+            mm(bot, B_local, C_local[jb * rp + h:(jb + 1) * rp])
+            self.gemm_done[s].record(compute)
+            self.last = self.gemm_done[s]
+            if s < ws - 1:
+                top, bot = self.Rt[(s + 1) % 2], self.Rb[(s + 1) % 2]

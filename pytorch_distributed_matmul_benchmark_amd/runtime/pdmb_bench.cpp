@@ -273,9 +273,14 @@ void check_rows(int dt, const void* A, const void* B, const void* C, int M, int 
   HIP_OK(hipStreamSynchronize(s));
 }
 
-int effective_chunks(int m, int n, int chunks) {
+// Row chunks of an overlapped GEMM: as many as still fill the chip. With the
+// 128x128 T128 tiles and split-K (bf16 / fp16) a chunk of 64 256x256-tile
+// equivalents does; the fp32 kernel needs a full wave of 256 (as
+// parallel/overlap.py gemm_chunks).
+int effective_chunks(int m, int n, int chunks, int dt) {
   const long long tiles = (long long)ceil_div(m, 256) * ceil_div(n, 256);
-  return std::max(1, (int)std::min<long long>(chunks, tiles / 256));
+  const long long min_tiles = dt == 0 ? 256 : 64;  // dt 0 = float32
+  return std::max(1, (int)std::min<long long>(chunks, tiles / min_tiles));
 }
 
 std::vector<std::pair<int, int>> row_chunks(int m, int chunks) {
@@ -337,7 +342,7 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     res.kernel = pdmb::kernel_name(pdmb::resolve_kernel(p, o.kernel));
     struct Unit { int b, r0, r1; };
     std::vector<Unit> units;
-    const int ch = o.overlap ? effective_chunks(n, n, o.chunks) : 1;
+    const int ch = o.overlap ? effective_chunks(n, n, o.chunks, dt) : 1;
     for (int b = 0; b < lb; ++b)
       for (auto rc : row_chunks(n, ch)) units.push_back({b, rc.first, rc.second});
     res.chunks = ch;
@@ -415,18 +420,23 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     if (o.check)  // C[0] = sum over ranks of A_r[0] @ B_r[0]: partial refs are summed on the host
       check_rows(dt, A.p, B.p, C.p, n, n, n, n, n, n, st, res.ref, res.got);
   } else if (o.mode == kRingParallel) {
-    // All-gather-GEMM over the ring (models/ring_parallel.py): A row-sharded in
-    // blocks of rp rows, B column-sharded. Hop s multiplies the A block of rank
-    // (r - s) mod ws into rows of C[:, S_r] while the comm stream forwards it to
-    // r+1 and receives the next block from r-1 (ncclSend + ncclRecv in one group).
+    // All-gather-GEMM over BOTH ring directions (models/ring_parallel.py): A
+    // row-sharded in blocks of rp rows, B column-sharded. Each block is cut
+    // into a top (ht rows, 256-aligned) and a bottom half; tops travel r -> r+1,
+    // bottoms r -> r-1, so every hop drives the links to both neighbours. Hop s
+    // multiplies the top of rank (r - s)'s block and the bottom of rank
+    // (r + s)'s block while the comm stream moves the next two halves (two
+    // ncclSend + two ncclRecv in one group).
     const int shard = ceil_div(ceil_div(n, ws), 8) * 8;
     const int c0 = std::min(rank * shard, n), width = std::max(0, std::min(n, c0 + shard) - c0);
     const int rp = ceil_div(n, ws);
+    const int ht = std::min(rp, ceil_div(ceil_div(rp, 2), 256) * 256), hb = rp - ht;
     auto rows_of = [&](int j) { return std::max(0, std::min(n, (j + 1) * rp) - j * rp); };
     res.shard = shard;
-    const size_t blk = (size_t)rp * n;
+    const size_t blk = (size_t)rp * n, blt = (size_t)ht * n, blb = (size_t)hb * n;
     Buf Ag((size_t)n * n * es), Bg((size_t)n * n * es), Bl((size_t)n * shard * es);
-    Buf Cl((size_t)n * shard * es), Al(blk * es), R0(blk * es), R1(blk * es);
+    Buf Cl((size_t)n * shard * es), Al(blk * es), Rt0(blt * es), Rt1(blt * es), Rb0(blb * es),
+        Rb1(blb * es);
     fill(Ag.p, (long long)n * n, dt, 1000, st);
     fill(Bg.p, (long long)n * n, dt, 1001, st);
     HIP_OK(hipMemsetAsync(Bl.p, 0, Bl.bytes, st));
@@ -438,35 +448,47 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
       HIP_OK(hipMemcpyAsync(Al.p, (char*)Ag.p + (size_t)rank * rp * n * es,
                             (size_t)rows_of(rank) * n * es, hipMemcpyDeviceToDevice, st));
     res.kernel = pdmb::kernel_name(
-        pdmb::resolve_kernel(problem(dt, Al.p, Bl.p, Cl.p, rp, shard, n, n, shard, shard), o.kernel));
-    char* R[2] = {(char*)R0.p, (char*)R1.p};
+        pdmb::resolve_kernel(problem(dt, Al.p, Bl.p, Cl.p, ht, shard, n, n, shard, shard), o.kernel));
+    char* Rt[2] = {(char*)Rt0.p, (char*)Rt1.p};
+    char* Rb[2] = {(char*)Rb0.p, (char*)Rb1.p};
     std::vector<hipEvent_t> gdone, rdone;
     for (int s = 0; s < ws; ++s) gdone.push_back(event());
     for (int s = 0; s + 1 < ws; ++s) rdone.push_back(event());
     hipEvent_t last = nullptr;  // most recently issued GEMM (across iterations)
-    auto block_gemm = [&](const char* a, int j) {
-      if (rows_of(j))
-        gemm(problem(dt, a, Bl.p, (char*)Cl.p + (size_t)j * rp * shard * es, rows_of(j), shard, n,
-                     n, shard, shard),
+    // rows [r0, r1) of block j (held in `a` from its row r0) -> C rows j*rp + r0 ..
+    auto part_gemm = [&](const char* a, int j, int r0, int r1) {
+      r1 = std::min(r1, rows_of(j));
+      if (r1 > r0)
+        gemm(problem(dt, a, Bl.p, (char*)Cl.p + ((size_t)j * rp + r0) * shard * es, r1 - r0, shard,
+                     n, n, shard, shard),
              o.kernel, st);
     };
+    auto block_gemm = [&](const char* a, int j) { part_gemm(a, j, 0, rp); };
     auto iter = [&]() {
-      char* cur = (char*)Al.p;
+      char* top = (char*)Al.p;
+      char* bot = (char*)Al.p + blt * es;
       for (int s = 0; s < ws; ++s) {
         if (s > 0) HIP_OK(hipStreamWaitEvent(st, rdone[s - 1], 0));
-        char* nb = R[(s + 1) % 2];
+        char* nt = Rt[(s + 1) % 2];
+        char* nb = Rb[(s + 1) % 2];
         if (s + 1 < ws) {
-          if (last) HIP_OK(hipStreamWaitEvent(cs, last, 0));  // nb's last reader is done
+          if (last) HIP_OK(hipStreamWaitEvent(cs, last, 0));  // nt / nb's last readers are done
           NCCL_OK(ncclGroupStart());
-          NCCL_OK(ncclSend(cur, blk, nccl_type(dt), (rank + 1) % ws, comm, cs));
-          NCCL_OK(ncclRecv(nb, blk, nccl_type(dt), (rank + ws - 1) % ws, comm, cs));
+          NCCL_OK(ncclSend(top, blt, nccl_type(dt), (rank + 1) % ws, comm, cs));
+          NCCL_OK(ncclRecv(nt, blt, nccl_type(dt), (rank + ws - 1) % ws, comm, cs));
+          if (blb) {
+            NCCL_OK(ncclSend(bot, blb, nccl_type(dt), (rank + ws - 1) % ws, comm, cs));
+            NCCL_OK(ncclRecv(nb, blb, nccl_type(dt), (rank + 1) % ws, comm, cs));
+          }
           NCCL_OK(ncclGroupEnd());
           HIP_OK(hipEventRecord(rdone[s], cs));
         }
-        block_gemm(cur, (rank - s + ws) % ws);
+        part_gemm(top, (rank - s + ws) % ws, 0, ht);
+        part_gemm(bot, (rank + s) % ws, ht, rp);  // bot holds the block's rows ht .. rp
         HIP_OK(hipEventRecord(gdone[s], st));
         last = gdone[s];
-        cur = nb;
+        top = nt;
+        bot = nb;
       }
     };
     for (int i = 0; i < o.warmup; ++i) iter();
@@ -508,7 +530,7 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
                               hipMemcpyDeviceToDevice, st));
     const pdmb::Problem p = problem(dt, A.p, Bl.p, Cl.p, n, shard, n, n, shard, shard);
     res.kernel = pdmb::kernel_name(pdmb::resolve_kernel(p, o.kernel));
-    const int ch = o.overlap ? effective_chunks(n, shard, o.chunks) : 1;
+    const int ch = o.overlap ? effective_chunks(n, shard, o.chunks, dt) : 1;
     res.chunks = ch;
     const auto rcs = row_chunks(n, ch);
     // per-chunk gather buffers [ws * rows, shard] carved out of G

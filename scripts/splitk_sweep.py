@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Under-filled-grid GEMMs: W4 split-K (S = 1/2/4/8/auto) vs hipBLASLt, interleaved.
+"""Under-filled-grid GEMMs: W4 / T128 x split-K (and auto) vs hipBLASLt, interleaved.
 
 Shapes default to the per-rank matrix_parallel shards of the reference's default
 sizes (matmul_scaling_benchmark.py:179-188 at :351-352) plus 2048^3. Both arms
@@ -52,7 +52,9 @@ def main():
     ap.add_argument("--dtype", default="bfloat16", choices=["bfloat16", "float16"])
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--min-ms", type=float, default=20.0, help="GPU time per timed graph")
-    ap.add_argument("--splits", type=int, nargs="+", default=[0, 1, 2, 4, 8])
+    ap.add_argument("--arms", nargs="+",
+                    default=["auto", "w4:1", "w4:2", "t128:1", "t128:2", "t128:4"],
+                    help="kernel:splitk (auto = the dispatcher's plan)")
     a = ap.parse_args()
     dt = getattr(torch, a.dtype)
     for shp in a.shapes:
@@ -66,17 +68,20 @@ def main():
         iters = max(5, int(a.min_ms * 1e-3 / (flops / 1.0e15)))  # ~min_ms at 1 PF
         arms = {}
         tiles = (m // 256) * (n // 256)
-        for S in a.splits:
+        for arm in a.arms:
+            kern, _, sk = arm.partition(":")
+            S = int(sk or 0)
             if S > 1 and tiles > 1024:
                 continue  # a full grid: split-K only adds partial traffic
             try:
-                real = gemm.splitk_for(A, B, splitk=S)
-                gemm.matmul(A, B, out=out, splitk=S)
-            except Exception as e:  # noqa: BLE001 (S not valid for this K)
-                print(json.dumps({"shape": shp, "splitk": S, "skipped": str(e)[:120]}), flush=True)
+                name = gemm.kernel_for(A, B, kernel=kern)
+                real = gemm.splitk_for(A, B, kernel=kern, splitk=S)
+                gemm.matmul(A, B, out=out, kernel=kern, splitk=S)
+            except Exception as e:  # noqa: BLE001 (S not valid for this K / shape)
+                print(json.dumps({"shape": shp, "arm": arm, "skipped": str(e)[:120]}), flush=True)
                 continue
             err = ((out.float() - R).norm() / R.norm()).item()
-            arms[f"w4_s{S}"] = dict(S=S, real=real, err=err)
+            arms[arm] = dict(kernel=kern, S=S, name=name, real=real, err=err)
         arms["hipblaslt"] = dict()
         best = {k_: float("inf") for k_ in arms}
         for _ in range(a.rounds):
@@ -85,14 +90,14 @@ def main():
                     ms = torch_graph_ms(A, B, out, iters)
                 else:
                     ms = gemm.bench_matmul(A, B, out, iters=iters, warmup=2, graph=True,
-                                           splitk=info["S"])
+                                           kernel=info["kernel"], splitk=info["S"])
                 best[name] = min(best[name], ms / iters)
         for name, info in arms.items():
             rec = {"shape": shp, "arm": name, "us": round(best[name] * 1e3, 2),
                    "tflops": round(flops / (best[name] * 1e-3) / 1e12, 1), "iters": iters,
                    "rounds": a.rounds, "dtype": a.dtype}
             if name != "hipblaslt":
-                rec.update(splitk_requested=info["S"], splitk=info["real"],
+                rec.update(kernel=info["name"], splitk_requested=info["S"], splitk=info["real"],
                            relerr=round(info["err"], 6))
             print(json.dumps(rec), flush=True)
         del A, B, out, R

@@ -74,7 +74,8 @@ def test_scaling_torchrun_gloo(mode, extra, tmp_path):
 
 @pytest.mark.parametrize("ws,n", [(2, 300), (3, 520)])
 def test_ring_parallel_gloo(ws, n, tmp_path):
-    """All-gather-GEMM over the ring: A row-sharded (256-row blocks, zero-padded),
+    """All-gather-GEMM over both ring directions: A row-sharded (512-row blocks,
+    zero-padded; top halves travel clockwise, bottom halves counter-clockwise),
     each rank's C[:, S_r] checked against the float64 product of the global A."""
     js = tmp_path / "r.jsonl"
     out = _torchrun(ws, "matmul_scaling_benchmark.py", "--device", "cpu", "--sizes", str(n),
@@ -84,7 +85,7 @@ def test_ring_parallel_gloo(ws, n, tmp_path):
     assert "PASS" in out and "FAIL" not in out and "ERROR" not in out
     rec = json.loads(js.read_text().splitlines()[-1])
     assert rec["mode"] == "ring_parallel" and rec["world_size"] == ws
-    assert rec["hops"] == ws - 1 and rec["shard_rows"] == 256
+    assert rec["hops"] == ws - 1 and rec["shard_rows"] == 512 and rec["directions"] == 2
 
 
 @pytest.mark.parametrize("ws,mode,extra", [(4, "batch_parallel", ["--overlap", "--chunks", "2"]),

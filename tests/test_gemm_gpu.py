@@ -292,7 +292,8 @@ def test_w4_exact_small_integers(dtype, b, M, N, K, pad):
     B = torch.randint(-3, 4, (b, K, N + pad), device="cuda", generator=g).to(dt)[..., :N]
     if b == 1:
         A, B = A[0], B[0]
-    assert gemm.kernel_for(A, B) == "pdmb_w4_nn"  # auto picks W4 for whole tiles
+    # auto picks a whole-tile kernel (W4, or T128 for these under-filled grids)
+    assert gemm.kernel_for(A, B) in ("pdmb_w4_nn", "pdmb_t128_nn")
     C = gemm.matmul(A, B, kernel="w4")
     assert torch.equal(C, (A.double() @ B.double()).to(dt))
 
@@ -342,59 +343,80 @@ def test_thin_grid_supertiles_exact(M, N, batch, kernel, dtype):
     assert torch.equal(C, (A.double() @ B.double()).to(dt))
 
 
-# ---- W4 split-K: under-filled grids (matrix_parallel column shards at ws >= 4) ----
+# ---- under-filled grids: T128 (128x128 tiles) and W4 / T128 split-K ----
+# (matrix_parallel column shards at ws >= 4: 4096 x 512, 8192 x 1024; 2048^3)
 
+@pytest.mark.parametrize("kernel", ["w4", "t128"])
 @pytest.mark.parametrize("M,N,K,b,splitk", [
-    (2048, 2048, 2048, 1, 0), (4096, 512, 4096, 1, 8), (8192, 1024, 8192, 1, 2),
+    (2048, 2048, 2048, 1, 0), (4096, 512, 4096, 1, 0), (8192, 1024, 8192, 1, 2),
     (1024, 1024, 4096, 1, 2), (1024, 1024, 4096, 1, 4), (1024, 1024, 4096, 1, 8),
-    (512, 512, 2048, 2, 4), (1024, 768, 832, 1, 4), (4096, 512, 4096, 1, 0)])
+    (512, 512, 2048, 2, 4), (1024, 768, 832, 1, 4), (4096, 512, 4096, 1, 1),
+    (256, 256, 64, 1, 0), (512, 768, 320, 3, 0)])
 @pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
-def test_w4_splitk_exact(M, N, K, b, splitk, dtype):
-    """Integer data keeps every fp32 slice partial and their sum exact: the split
-    result equals the fp64 product rounded once (K = 832 leaves the last of 4
-    slices one K-tile)."""
+def test_whole_tile_kernels_exact(kernel, M, N, K, b, splitk, dtype):
+    """Integer data keeps every fp32 slice partial and their sum exact: the
+    (split) result equals the fp64 product rounded once (K = 832 leaves the
+    last of 4 slices one K-tile; K = 64 is a one-K-tile prologue/tail)."""
+    if kernel == "w4" and (M % 256 or N % 256):
+        pytest.skip("W4 needs M, N % 256")
     dt = DT[dtype]
     g = torch.Generator(device="cuda").manual_seed(M + N + K + splitk)
     A = torch.randint(-3, 4, (b, M, K), device="cuda", generator=g).to(dt)
     B = torch.randint(-3, 4, (b, K, N), device="cuda", generator=g).to(dt)
     if b == 1:
         A, B = A[0], B[0]
-    S = gemm.splitk_for(A, B, splitk=splitk)
-    assert S == splitk if splitk else S > 1
+    assert gemm.kernel_for(A, B, kernel=kernel) == f"pdmb_{kernel}_nn"
+    S = gemm.splitk_for(A, B, kernel=kernel, splitk=splitk)
+    assert S == splitk if splitk else S >= 1
     C = torch.full(torch.broadcast_shapes(A.shape[:-1] + (N,)), float("nan"), device="cuda",
                    dtype=dt)
-    gemm.matmul(A, B, out=C, kernel="w4", splitk=splitk)
+    gemm.matmul(A, B, out=C, kernel=kernel, splitk=splitk)
     assert torch.equal(C, (A.double() @ B.double()).to(dt))
 
 
-def test_w4_splitk_choice_for_shard_shapes():
-    """Auto split only where the grid under-fills the 256 CUs."""
-    def S(M, N, K):
+def test_auto_plan_for_shard_shapes():
+    """Auto: W4 where 256x256 tiles fill the chip, T128 for the under-filled
+    matrix_parallel shards (and 2048^3)."""
+    def plan(M, N, K):
         A = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
         B = torch.empty(K, N, device="cuda", dtype=torch.bfloat16)
-        return gemm.splitk_for(A, B)
-    assert S(16384, 16384, 16384) == 1 and S(16384, 2048, 16384) == 1
-    assert S(8192, 1024, 8192) >= 2 and S(4096, 512, 4096) >= 4 and S(2048, 2048, 2048) >= 2
-    assert S(16384, 1024, 256) == 1  # too little K to split
+        return gemm.kernel_for(A, B), gemm.splitk_for(A, B)
+    assert plan(16384, 16384, 16384) == ("pdmb_w4_nn", 1)
+    assert plan(16384, 2048, 16384) == ("pdmb_w4_nn", 1)
+    for shape in ((8192, 1024, 8192), (4096, 512, 4096), (2048, 2048, 2048)):
+        assert plan(*shape)[0] == "pdmb_t128_nn", shape
+    assert plan(16384, 1024, 256)[1] == 1  # too little K to split
 
 
-@pytest.mark.parametrize("M,N,K,splitk", [(8192, 1024, 8192, 0), (2048, 2048, 2048, 0),
-                                          (4096, 512, 4096, 8)])
-def test_w4_splitk_random_and_bitwise_repeatable(M, N, K, splitk):
-    """Random data vs fp64, and a race screen: the slices meet in a fixed order, so
-    every launch is bitwise identical whichever slice arrives last."""
+@pytest.mark.parametrize("kernel,M,N,K,splitk", [
+    ("auto", 8192, 1024, 8192, 0), ("auto", 2048, 2048, 2048, 0), ("t128", 4096, 512, 4096, 2),
+    ("w4", 4096, 512, 4096, 8), ("t128", 4096, 4096, 4096, 1)])
+def test_tiled_random_and_bitwise_repeatable(kernel, M, N, K, splitk):
+    """Random data vs fp64, and a race screen for the LDS-DMA ring and the
+    split-K meeting: the slices meet in a fixed order, so every launch is
+    bitwise identical whichever slice arrives last."""
     torch.manual_seed(M + N)
     A = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     B = torch.randn(K, N, device="cuda", dtype=torch.bfloat16)
-    ref = gemm.matmul(A, B, splitk=splitk)
+    ref = gemm.matmul(A, B, kernel=kernel, splitk=splitk)
     assert _relerr(ref, _ref(A, B)) < TOL[torch.bfloat16]
     for _ in range(30):
-        assert torch.equal(gemm.matmul(A, B, splitk=splitk), ref)
-    # unsplit W4 differs only by fp32 summation order
-    assert _relerr(gemm.matmul(A, B, splitk=1), ref.double()) < 1e-2
+        assert torch.equal(gemm.matmul(A, B, kernel=kernel, splitk=splitk), ref)
+    # W4 unsplit differs only by fp32 summation order
+    assert _relerr(gemm.matmul(A, B, kernel="w4", splitk=1), ref.double()) < 1e-2
 
 
-def test_w4_splitk_concurrent_streams_and_graph():
+def test_t128_matches_w4_bitwise_unsplit():
+    """Same per-output fp32 accumulation order (K-tiles ascending, 16x16x32 MFMA
+    steps): the 128x128 and 256x256 kernels agree bitwise."""
+    torch.manual_seed(4)
+    A = torch.randn(2048, 3072, device="cuda", dtype=torch.bfloat16)
+    B = torch.randn(3072, 1536, device="cuda", dtype=torch.bfloat16)
+    assert torch.equal(gemm.matmul(A, B, kernel="t128", splitk=1),
+                       gemm.matmul(A, B, kernel="w4", splitk=1))
+
+
+def test_splitk_concurrent_streams_and_graph():
     """Per-stream counters: split-K GEMMs on two streams at once stay exact; a
     torch.cuda.graph capture of one replays exactly (counters re-zeroed by
     every launch)."""
@@ -402,38 +424,40 @@ def test_w4_splitk_concurrent_streams_and_graph():
     A = torch.randint(-3, 4, (2048, 4096), device="cuda", generator=g).to(torch.bfloat16)
     B = torch.randint(-3, 4, (4096, 1024), device="cuda", generator=g).to(torch.bfloat16)
     R = (A.double() @ B.double()).to(torch.bfloat16)
-    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
-    outs = [torch.empty_like(R) for _ in range(8)]
-    torch.cuda.synchronize()
-    for i, o in enumerate(outs):
-        with torch.cuda.stream(s1 if i % 2 else s2):
-            gemm.matmul(A, B, out=o, splitk=4)
-    torch.cuda.synchronize()
-    assert all(torch.equal(o, R) for o in outs)
-    s = torch.cuda.Stream()
-    out = torch.empty_like(R)
-    with torch.cuda.stream(s):
-        gemm.matmul(A, B, out=out, splitk=4)  # counters for s exist before capture
-    s.synchronize()
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph, stream=s):
-        gemm.matmul(A, B, out=out, splitk=4)
-    for _ in range(3):
-        out.fill_(float("nan"))
-        graph.replay()
+    for kernel in ("w4", "t128"):
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        outs = [torch.empty_like(R) for _ in range(8)]
         torch.cuda.synchronize()
-        assert torch.equal(out, R)
+        for i, o in enumerate(outs):
+            with torch.cuda.stream(s1 if i % 2 else s2):
+                gemm.matmul(A, B, out=o, kernel=kernel, splitk=4)
+        torch.cuda.synchronize()
+        assert all(torch.equal(o, R) for o in outs)
+        s = torch.cuda.Stream()
+        out = torch.empty_like(R)
+        with torch.cuda.stream(s):
+            gemm.matmul(A, B, out=out, kernel=kernel, splitk=4)  # counters for s exist first
+        s.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=s):
+            gemm.matmul(A, B, out=out, kernel=kernel, splitk=4)
+        for _ in range(3):
+            out.fill_(float("nan"))
+            graph.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(out, R)
 
 
-def test_w4_splitk_native_bench_loop_graph():
+def test_splitk_native_bench_loop_graph():
     A = torch.randn(2048, 2048, device="cuda", dtype=torch.bfloat16)
     B = torch.randn(2048, 2048, device="cuda", dtype=torch.bfloat16)
     out = torch.empty(2048, 2048, device="cuda", dtype=torch.bfloat16)
-    assert gemm.splitk_for(A, B) > 1
-    for graph in (False, True):
-        out.zero_()
-        assert gemm.bench_matmul(A, B, out, iters=5, warmup=0, graph=graph) > 0
-        assert _relerr(out, _ref(A, B)) < TOL[torch.bfloat16]
+    for kernel in ("w4", "t128"):
+        for graph in (False, True):
+            out.zero_()
+            assert gemm.bench_matmul(A, B, out, iters=5, warmup=0, graph=graph, kernel=kernel,
+                                     splitk=2) > 0
+            assert _relerr(out, _ref(A, B)) < TOL[torch.bfloat16]
 
 
 def test_overlapping_views_are_refused_or_copied():

@@ -103,3 +103,23 @@ def test_default_build_has_no_experiment_kernels(tmp_path):
     (tmp_path / "fp8").mkdir()
     ks = _kernels("gemm_fp8.hip", tmp_path / "fp8")
     assert ks and all("gemm_fp8_w4ILi0ELi0E" in k for k in ks), sorted(ks)
+
+
+def test_t128_kernel_pipelined(tmp_path):
+    """gemm_t128.hip: no spills, 64 AGPR accumulators, 4-stage ring (128 KiB LDS),
+    one vmcnt(16)-counted barrier per K-tile and one vmcnt(0) drain before the
+    split-K epilogue."""
+    ks = _kernels("gemm_t128.hip", tmp_path)
+    for dt, mfma in (("ILi2E", "v_mfma_f32_16x16x32_bf16"), ("ILi1E", "v_mfma_f32_16x16x32_f16")):
+        name = [k for k in ks if "gemm_t128_nn" in k and dt in k]
+        assert name, sorted(ks)
+        k = ks[name[0]]
+        b = k["body"]
+        assert k["spill"] == 0 and k["lds"] == 4 * 32768 and k["vgpr"] <= 256
+        assert re.search(r"v_mfma_f32_16x16x32_\w+ a\[", b)
+        loop = b[:b.find("global_atomic")]
+        assert len(re.findall(r"s_waitcnt vmcnt\(0\)", loop)) == 1
+        assert len(re.findall(r"s_waitcnt vmcnt\(16\) lgkmcnt\(0\)", b)) == 3
+        assert len(re.findall(mfma, b)) == 3 * 32  # 2 unrolled K-tiles + the odd tail
+        assert len(re.findall(r"buffer_load_dwordx4 .* lds", b)) == 4 * 8 + 3 * 8
+        assert len(re.findall(r"buffer_store_dwordx4 .* sc1", b)) == 16  # split-K slots

@@ -70,7 +70,7 @@ def test_torchrun_rccl_single_rank(mode, extra):
                 "--check", *extra])
     assert "Results for 2048x2048" in out and "PASS" in out
     assert "FAIL" not in out and "ERROR" not in out
-    assert "pdmb_w4_nn" in out or "pdmb_mfma256" in out
+    assert "pdmb_w4_nn" in out or "pdmb_t128_nn" in out or "pdmb_mfma256" in out
 
 
 def test_bench_json_contract():
@@ -81,7 +81,7 @@ def test_bench_json_contract():
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in d, k
     assert d["n_gpus"] == 1 and d["steps"] == 4 and d["value"] > 0
-    assert d["config"]["kernel"] == "pdmb_w4_nn"
+    assert d["config"]["kernel"] in ("pdmb_w4_nn", "pdmb_t128_nn")  # 2048^3: 64 W4 tiles -> T128
 
 
 def test_smoke_hook():
