@@ -384,7 +384,8 @@ def test_auto_plan_for_shard_shapes():
     assert plan(16384, 16384, 16384) == ("pdmb_w4_nn", 1)
     assert plan(16384, 2048, 16384) == ("pdmb_w4_nn", 1)
     for shape in ((8192, 1024, 8192), (4096, 512, 4096), (2048, 2048, 2048)):
-        assert plan(*shape)[0] == "pdmb_t128_nn", shape
+        k, S = plan(*shape)  # more workgroups than 256x256 tiles: T128, or a split W4
+        assert k == "pdmb_t128_nn" or (k == "pdmb_w4_nn" and S > 1), (shape, k, S)
     assert plan(16384, 1024, 256)[1] == 1  # too little K to split
 
 

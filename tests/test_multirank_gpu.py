@@ -65,3 +65,32 @@ def test_two_ranks_share_gpu_bench_ring():
                "--mode", "ring_parallel", "--extra-steps", "0")
     d = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["parallelism"] == "ring2"
+
+
+@pytest.mark.parametrize("mode,extra", [
+    ("matrix_parallel", ["--overlap", "--chunks", "4", "--comm-chunks", "3", "--comm-cus", "16"]),
+    ("batch_parallel", ["--overlap", "--chunks", "2", "--comm-cus", "32"]),
+    ("matrix_parallel", ["--overlap", "--chunks", "1", "--comm-chunks", "4"])])
+def test_two_ranks_cu_masked_overlap_checked(mode, extra):
+    """GEMM chunks on a CU-masked stream, collectives in pieces decoupled from the
+    GEMM chunking: the float64 Σ-over-ranks / gathered-C checks still pass."""
+    out = _run(2, "matmul_scaling_benchmark.py", "--sizes", "2048", "--iterations", "3",
+               "--warmup", "1", "--mode", mode, "--check", *extra)
+    assert "PASS" in out and "FAIL" not in out and "ERROR" not in out
+
+
+def test_two_ranks_self_launch_through_bench():
+    """bench.py --gpus 2 with no torchrun starts both ranks itself (gloo: they share
+    the one GPU) and reports a scaling efficiency against rank 0 alone."""
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--dist-backend", "gloo",
+                        "--size", "2048", "--steps", "3", "--warmup", "1", "--extra-steps", "2",
+                        "--extra-warmup", "1", "--comm-cus", "16"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["single_gpu_tflops"] > 0
+    assert d["scaling_efficiency"] is not None
+    assert d["modes"]["matrix_parallel+overlap"]["value"] > 0
