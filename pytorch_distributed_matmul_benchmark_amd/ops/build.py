@@ -135,6 +135,22 @@ def build_bench(verbose: bool = False, force: bool = False) -> Path:
     return out
 
 
+PROBE_SRC = RUNTIME / "mfma_probe.hip"
+
+
+def probe_path() -> Path:
+    return RUNTIME / "mfma_probe"
+
+
+def build_probe(verbose: bool = False, force: bool = False) -> Path:
+    """The stand-alone MFMA-shape probe (runtime/mfma_probe.hip): 16x16x32 vs
+    32x32x16 bf16 FLOP rate on random operands (scripts/gpu_r2c.sh)."""
+    out = probe_path()
+    if force or _needs_build(out, [PROBE_SRC]):
+        _run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", PROBE_SRC, "-o", out], verbose)
+    return out
+
+
 def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -> Path:
     """Compile every HIP/C++ source for gfx950 and link ``_C``. Returns the .so path."""
     headers = sorted(CSRC.glob("*.h"))
@@ -205,6 +221,7 @@ def main(argv=None):
     print(p)
     if not a.no_bench:
         print(build_bench(verbose=a.verbose))
+        print(build_probe(verbose=a.verbose))
 
 
 if __name__ == "__main__":
