@@ -143,8 +143,8 @@ int resolve_kernel(const Problem& p, int kernel) {
 //   cost = waves(T * S) * (ceil(nk / S) * kt + fixed + meet * (S - 1))
 // over W4 x S in {1, 2} and T128 x S in {1, 2, 4}; the cheapest wins, W4 on
 // ties (its tile is the more efficient one at full occupancy). Constants from
-// profiles/r2_splitk_sweep.jsonl / r2_t128_sweep.jsonl.
-static constexpr double kT128Kt = 0.30;   // T128 K-tile / W4 K-tile
+// profiles/r2_t128_splitk_sweep.jsonl (interleaved vs hipBLASLt).
+static constexpr double kT128Kt = 0.40;   // T128 K-tile / W4 K-tile (16k: 952 vs 1507 TF)
 static constexpr double kFixed = 1.0;     // launch + prologue + epilogue
 static constexpr double kMeetW4 = 3.0;    // 256 KiB slab
 static constexpr double kMeetT128 = 0.8;  // 64 KiB slab

@@ -28,7 +28,7 @@ def test_mode_single_gpu(mode, dtype):
     r = run_mode(mode, w, _ctx())
     assert r.relerr is not None and r.relerr < tolerance(dtype), r.relerr
     assert r.avg_ms > 0 and r.tflops > 0
-    assert r.kernel.startswith("pdmb_fp8" if dtype == torch.float8_e4m3fn else ("pdmb_w4", "pdmb_mfma256"))
+    assert r.kernel.startswith("pdmb_fp8" if dtype == torch.float8_e4m3fn else ("pdmb_w4", "pdmb_t128", "pdmb_mfma256"))
 
 
 def test_fp32_independent_uses_exact_mfma():
