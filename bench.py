@@ -51,9 +51,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from pytorch_distributed_matmul_benchmark_amd.ops import gemm  # noqa: E402
-from pytorch_distributed_matmul_benchmark_amd.parallel.comm import stream_ctx  # noqa: E402
 from pytorch_distributed_matmul_benchmark_amd.parallel.overlap import (  # noqa: E402
-    BidirRing, GatherOverlap, ReduceOverlap, compute_stream, gemm_chunks)
+    BidirRing, GatherOverlap, ReduceOverlap, compute_ctx, compute_stream, gemm_chunks)
 from pytorch_distributed_matmul_benchmark_amd.parallel.dist import (  # noqa: E402
     DistContext, all_ok, barrier, cleanup_distributed, reduce_scalar, setup_distributed)
 from pytorch_distributed_matmul_benchmark_amd.parallel.partition import (  # noqa: E402
@@ -107,7 +106,7 @@ class Workload:
                 ov = ReduceOverlap(lb, gemm_chunks(n, n, a.chunks, dt, dev), dev)
 
                 def step():
-                    with stream_ctx(self.comp):
+                    with compute_ctx(self.comp, self._mask):
                         ov.step(self._mm, A, B, C, self.comp)
                     self._join()
             else:
@@ -133,7 +132,7 @@ class Workload:
                                    pieces=a.comm_chunks, requested=a.chunks)
 
                 def step():
-                    with stream_ctx(self.comp):
+                    with compute_ctx(self.comp, self._mask):
                         ov.step(self._mm, A, Bl, Cl, self.comp)
                     self._join()
             else:

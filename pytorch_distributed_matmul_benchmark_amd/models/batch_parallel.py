@@ -24,8 +24,8 @@ from __future__ import annotations
 
 import torch
 
-from ..parallel.comm import current_stream, stream_ctx
-from ..parallel.overlap import ReduceOverlap, compute_stream, gemm_chunks
+from ..parallel.comm import current_stream
+from ..parallel.overlap import ReduceOverlap, compute_ctx, compute_stream, gemm_chunks
 from ..parallel.dist import DistContext
 from ..parallel.partition import global_batch, local_batch
 from ..utils.metrics import gemm_flops, tflops_from
@@ -86,7 +86,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         extra["comm_cus"] = w.comm_cus
 
         def step():
-            with stream_ctx(compute):
+            with compute_ctx(compute, owner):
                 ov.step(mm, A, B, C, compute)
             if compute is not None:  # the timing stream joins the (masked) compute stream
                 current_stream(dev).wait_stream(compute)

@@ -28,8 +28,8 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
-from ..parallel.comm import current_stream, stream_ctx
-from ..parallel.overlap import GatherOverlap, compute_stream, gemm_chunks
+from ..parallel.comm import current_stream
+from ..parallel.overlap import GatherOverlap, compute_ctx, compute_stream, gemm_chunks
 from ..parallel.dist import DistContext
 from ..parallel.partition import column_shard
 from ..utils.metrics import gemm_flops, tflops_from
@@ -116,7 +116,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         compute, owner = compute_stream(dev, w.comm_cus)
 
         def step():
-            with stream_ctx(compute):
+            with compute_ctx(compute, owner):
                 ov.step(mm, A, B_local, C_local, compute)
             if compute is not None:  # the timing stream joins the (masked) compute stream
                 current_stream(dev).wait_stream(compute)

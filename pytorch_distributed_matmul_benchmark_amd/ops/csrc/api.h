@@ -58,6 +58,10 @@ struct Problem {
   // W4 / T128 split-K: K slices per output tile (0 = auto: split only
   // under-filled grids, see choose_splitk; 1 = off). Ignored by the others.
   int splitk = 0;
+  // CUs the launch stream may use (a CU-masked stream: parallel/overlap.py
+  // MaskedStream); 0 = every CU of the device. The W4 / T128 planner sizes
+  // grids for it (a 256-workgroup wave on 248 CUs is two waves).
+  int cus = 0;
   // Caller-owned scratch of at least gemm_workspace_bytes(p, kernel) bytes
   // (padded-path copies, split-K partials), stream-ordered with the launch.
   void* workspace = nullptr;
@@ -99,6 +103,11 @@ hipError_t bench_gemm(const Problem& p, int kernel, int iters, int warmup, bool 
                       hipStream_t stream, float* ms);
 
 const char* kernel_name(int kernel);
+
+// Comm proxy for overlap experiments (scripts/cu_mask_overlap.py): copy
+// `bytes` (multiple of 16) from src to dst with exactly `blocks` 256-thread
+// workgroups, the footprint of an RCCL collective's channels.
+hipError_t comm_proxy(void* dst, const void* src, size_t bytes, int blocks, hipStream_t stream);
 
 // Diagnostic builds write per-wave stamps here (device memory; nullptr = off).
 void set_debug_buffer(void* p);

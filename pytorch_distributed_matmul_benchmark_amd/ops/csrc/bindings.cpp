@@ -125,10 +125,11 @@ at::Tensor workspace_for(pdmb::Problem& p, int kernel, const at::Tensor& like) {
 }
 
 at::Tensor matmul(const at::Tensor& A, const at::Tensor& B, c10::optional<at::Tensor> out,
-                  int64_t kernel, double alpha, int64_t splitk) {
+                  int64_t kernel, double alpha, int64_t splitk, int64_t cus) {
   at::Tensor C = out.has_value() ? *out : alloc_out(A, B);
   pdmb::Problem p = make_problem(A, B, C, alpha);
   p.splitk = (int)splitk;
+  p.cus = (int)cus;
   c10::hip::HIPGuard guard(A.device().index());
   hipStream_t s = c10::hip::getCurrentHIPStream(A.device().index()).stream();
   at::Tensor ws = workspace_for(p, (int)kernel, A);
@@ -139,8 +140,11 @@ at::Tensor matmul(const at::Tensor& A, const at::Tensor& B, c10::optional<at::Te
   return C;
 }
 
-int64_t resolve(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t kernel) {
-  return pdmb::resolve_kernel(make_problem(A, B, C), (int)kernel);
+int64_t resolve(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t kernel,
+                int64_t cus) {
+  pdmb::Problem p = make_problem(A, B, C);
+  p.cus = (int)cus;
+  return pdmb::resolve_kernel(p, (int)kernel);
 }
 
 int64_t resolve_padded(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C) {
@@ -149,9 +153,10 @@ int64_t resolve_padded(const at::Tensor& A, const at::Tensor& B, const at::Tenso
 
 // K slices the W4 / T128 kernel would use (1 = no split; 0 if neither runs it).
 int64_t splitk_for(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t kernel,
-                   int64_t splitk) {
+                   int64_t splitk, int64_t cus) {
   pdmb::Problem p = make_problem(A, B, C);
   p.splitk = (int)splitk;
+  p.cus = (int)cus;
   return pdmb::choose_splitk(p, (int)kernel);
 }
 
@@ -208,6 +213,18 @@ void destroy_stream(int64_t stream) {
 
 std::string kernel_name(int64_t k) { return pdmb::kernel_name((int)k); }
 
+// Comm proxy (overlap experiments): copy src -> dst with `blocks` workgroups
+// on the current stream.
+void comm_proxy(const at::Tensor& dst, const at::Tensor& src, int64_t blocks) {
+  TORCH_CHECK(dst.is_cuda() && src.is_cuda() && dst.is_contiguous() && src.is_contiguous() &&
+                  dst.nbytes() == src.nbytes() && dst.nbytes() % 16 == 0,
+              "pdmb: comm_proxy needs equal-size contiguous GPU tensors (bytes % 16 == 0)");
+  c10::hip::HIPGuard guard(dst.device().index());
+  hipStream_t s = c10::hip::getCurrentHIPStream(dst.device().index()).stream();
+  check_hip(pdmb::comm_proxy(dst.data_ptr(), src.data_ptr(), dst.nbytes(), (int)blocks, s),
+            "comm_proxy");
+}
+
 // Diagnostic: set (or clear, with None) the device buffer the stamp kernel writes.
 void set_debug_buffer(c10::optional<at::Tensor> buf) {
   if (buf.has_value()) {
@@ -225,17 +242,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) native GEMM kernels and timing loop";
   m.def("matmul", &matmul, "C = A @ B on gfx950 MFMA (fp8: C = alpha * A @ B, bf16 out)",
         py::arg("A"), py::arg("B"), py::arg("out") = py::none(), py::arg("kernel") = 0,
-        py::arg("alpha") = 1.0, py::arg("splitk") = 0);
+        py::arg("alpha") = 1.0, py::arg("splitk") = 0, py::arg("cus") = 0);
   m.def("resolve", &resolve, "kernel id that would run (or -1)", py::arg("A"), py::arg("B"),
-        py::arg("out"), py::arg("kernel") = 0);
+        py::arg("out"), py::arg("kernel") = 0, py::arg("cus") = 0);
   m.def("resolve_padded", &resolve_padded, "kernel the padded fast path runs (or -1)",
         py::arg("A"), py::arg("B"), py::arg("out"));
   m.def("splitk_for", &splitk_for, "W4 K slices for this problem (0: not W4)", py::arg("A"),
-        py::arg("B"), py::arg("out"), py::arg("kernel") = 0, py::arg("splitk") = 0);
+        py::arg("B"), py::arg("out"), py::arg("kernel") = 0, py::arg("splitk") = 0,
+        py::arg("cus") = 0);
   m.def("bench", &bench, "native hipEvent timing loop; returns total ms", py::arg("A"),
         py::arg("B"), py::arg("out"), py::arg("iters"), py::arg("warmup"),
         py::arg("graph") = false, py::arg("kernel") = 0, py::arg("splitk") = 0);
   m.def("kernel_name", &kernel_name);
+  m.def("comm_proxy", &comm_proxy, py::arg("dst"), py::arg("src"), py::arg("blocks"));
   m.def("set_debug_buffer", &set_debug_buffer, py::arg("buf") = py::none());
   m.def("create_cu_masked_stream", &create_cu_masked_stream, py::arg("device"),
         py::arg("excluded"));

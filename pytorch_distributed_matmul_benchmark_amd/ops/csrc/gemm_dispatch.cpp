@@ -141,7 +141,8 @@ int resolve_kernel(const Problem& p, int kernel) {
 // a serial read of one fp32 slab: 256 KiB for W4, 64 KiB for T128). Model, in
 // W4 K-tile times (~1.2 us on MI355X):
 //   cost = waves(T * S) * (ceil(nk / S) * kt + fixed + meet * (S - 1))
-// over W4 x S in {1, 2} and T128 x S in {1, 2, 4}; the cheapest wins, W4 on
+// (waves over the CUs the stream may use, Problem::cus) over W4 x S in
+// {1, 2, 4} and T128 x S in {1, 2, 4}; the cheapest wins, W4 on
 // ties (its tile is the more efficient one at full occupancy). Constants from
 // profiles/r2_t128_splitk_sweep.jsonl (interleaved vs hipBLASLt).
 static constexpr double kT128Kt = 0.40;   // T128 K-tile / W4 K-tile (16k: 952 vs 1507 TF)
@@ -154,6 +155,19 @@ static long long tiles_of(const Problem& p, int tile) {
   return (long long)(p.M / tile) * (p.N / tile) * (p.batch < 1 ? 1 : p.batch);
 }
 
+static int device_cus() {
+  static int n[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!n[dev]) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    n[dev] = v;
+  }
+  return n[dev];
+}
+
 static double plan_cost(const Problem& p, int kernel, int S) {
   const int tile = kernel == kT128 ? 128 : 256;
   const long long T = tiles_of(p, tile);
@@ -161,7 +175,8 @@ static double plan_cost(const Problem& p, int kernel, int S) {
   const int per = (nk + S - 1) / S;
   const double kt = kernel == kT128 ? kT128Kt : 1.0;
   const double meet = kernel == kT128 ? kMeetT128 : kMeetW4;
-  return (double)((T * S + 255) / 256) * (per * kt + kFixed + meet * (S - 1));
+  const long long cus = p.cus > 0 ? p.cus : device_cus();  // 1 workgroup per CU
+  return (double)((T * S + cus - 1) / cus) * (per * kt + kFixed + meet * (S - 1));
 }
 
 static bool split_ok(const Problem& p, int kernel, int S) {
@@ -194,7 +209,7 @@ static Plan plan(const Problem& p, int kernel) {
   static const int kS[] = {1, 2, 4, 8};
   if (w4)
     for (int S : kS)
-      if (S <= 2 || p.splitk == S) consider(kMfmaW4, S);
+      if (S <= 4 || p.splitk == S) consider(kMfmaW4, S);
   if (t128)
     for (int S : kS)
       if (S <= 4 || p.splitk == S) consider(kT128, S);
@@ -527,6 +542,21 @@ hipError_t bench_gemm(const Problem& p, int kernel, int iters, int warmup, bool 
   if (exec) hipGraphExecDestroy(exec);
   if (graph) hipGraphDestroy(graph);
   return e;
+}
+
+// ---- comm proxy ------------------------------------------------------------
+__global__ void __launch_bounds__(256) proxy_copy(uint4* __restrict__ dst,
+                                                  const uint4* __restrict__ src, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
+hipError_t comm_proxy(void* dst, const void* src, size_t bytes, int blocks, hipStream_t stream) {
+  if (bytes % 16 || blocks <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(proxy_copy, dim3(blocks), dim3(256), 0, stream, (uint4*)dst, (const uint4*)src,
+                     bytes / 16);
+  return hipGetLastError();
 }
 
 const char* kernel_name(int kernel) {

@@ -14,6 +14,8 @@ and is enqueued on the current HIP stream, so it composes with
 """
 from __future__ import annotations
 
+import contextlib
+import threading
 from typing import Optional
 
 import torch
@@ -37,6 +39,26 @@ KERNEL_NAMES = {0: "auto", 2: "pdmb_generic_nn", 7: "pdmb_f32_256s_nn", 9: "pdmb
                 6: "pdmb_f32_256_nn", 15: "pdmb_fp8_256_nt", -1: "unsupported"}
 SUPPORTED_DTYPES = (torch.float32, torch.float16, torch.bfloat16)
 FP8 = torch.float8_e4m3fn  # OCP e4m3 (gfx950), bf16 output, column-major B
+
+
+_budget = threading.local()
+
+
+@contextlib.contextmanager
+def cu_budget(cus: int):
+    """GEMMs issued in this block (this thread) run on a stream that may use
+    only ``cus`` CUs (a CU-masked stream, parallel/overlap.py): the W4 / T128
+    planner sizes their grids for that many CUs instead of the whole device."""
+    prev = getattr(_budget, "cus", 0)
+    _budget.cus = int(cus)
+    try:
+        yield
+    finally:
+        _budget.cus = prev
+
+
+def _cus() -> int:
+    return getattr(_budget, "cus", 0)
 
 
 def experiments_built() -> bool:
@@ -141,7 +163,7 @@ def matmul(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
     if out is None:
         out = torch.empty(_out_shape(A, B), dtype=out_dtype(A.dtype), device=A.device)
     # auto: odd K/N/alignment padded onto the fast path (C++; not for fp8)
-    C.matmul(A, B, out, _kid(kernel), float(alpha), int(splitk))
+    C.matmul(A, B, out, _kid(kernel), float(alpha), int(splitk), _cus())
     return out
 
 
@@ -178,7 +200,7 @@ def kernel_for(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = N
     if out is None:
         out = torch.empty(_out_shape(A, B), dtype=out_dtype(A.dtype), device=A.device)
     A, B = _prep_pair(A, B)
-    return KERNEL_NAMES[int(C.resolve(A, B, out, _kid(kernel)))]
+    return KERNEL_NAMES[int(C.resolve(A, B, out, _kid(kernel), _cus()))]
 
 
 def splitk_for(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
@@ -190,7 +212,7 @@ def splitk_for(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = N
     if out is None:
         out = torch.empty(_out_shape(A, B), dtype=out_dtype(A.dtype), device=A.device)
     A, B = _prep_pair(A, B)
-    return int(C.splitk_for(A, B, out, _kid(kernel), int(splitk)))
+    return int(C.splitk_for(A, B, out, _kid(kernel), int(splitk), _cus()))
 
 
 def bench_matmul(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, iters: int,
@@ -209,3 +231,10 @@ def bench_matmul(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, iters: int
     A, B = _prep_pair(A, B)
     return float(C.bench(A, B, out, int(iters), int(warmup), bool(graph), _kid(kernel),
                          int(splitk)))
+
+
+def comm_proxy(dst: torch.Tensor, src: torch.Tensor, blocks: int = 32) -> None:
+    """Copy ``src`` into ``dst`` on the current stream with exactly ``blocks``
+    256-thread workgroups: the CU footprint of an RCCL collective's channels,
+    for single-GPU overlap experiments (scripts/cu_mask_overlap.py)."""
+    _native.load().comm_proxy(dst, src, int(blocks))

@@ -28,7 +28,7 @@ from typing import List, Optional, Sequence, Tuple
 
 import torch
 
-from .comm import CommStream, new_event
+from .comm import CommStream, new_event, stream_ctx
 from .partition import ceil_div, effective_chunks, row_chunks
 
 # 256x256 output tiles a GEMM chunk needs to fill the chip (ops/gemm.py
@@ -59,7 +59,9 @@ def _xcd_spread(ncu: int, k: int, nxcd: int = 8) -> List[int]:
 
 
 class MaskedStream:
-    """A CU-masked HIP stream (owned; destroyed with the object)."""
+    """A CU-masked HIP stream (owned; destroyed with the object). GEMMs issued
+    on it should run under ``ops.gemm.cu_budget(self.cus)`` (``budget()``) so
+    their grids are planned for the CUs they may use."""
 
     def __init__(self, device: torch.device, comm_cus: int):
         from ..ops import _native
@@ -70,6 +72,12 @@ class MaskedStream:
         self.handle = int(self._C.create_cu_masked_stream(device.index, self.excluded))
         self.stream = torch.cuda.ExternalStream(self.handle, device=device)
         self.device = device
+        self.cus = ncu - len(self.excluded)
+
+    def budget(self):
+        from ..ops import gemm
+
+        return gemm.cu_budget(self.cus)
 
     def active_cus(self) -> int:
         mask = self._C.stream_cu_mask(self.handle, self.device.index)
@@ -86,6 +94,19 @@ class MaskedStream:
             self.close()
         except Exception:
             pass
+
+
+def compute_ctx(stream, owner):
+    """Context for issuing GEMMs on a compute stream from ``compute_stream``:
+    the stream, plus the CU budget when it is a masked one."""
+    import contextlib
+
+    if owner is None:
+        return stream_ctx(stream)
+    st = contextlib.ExitStack()
+    st.enter_context(stream_ctx(stream))
+    st.enter_context(owner.budget())
+    return st
 
 
 def compute_stream(device: torch.device, comm_cus: int = 0):
