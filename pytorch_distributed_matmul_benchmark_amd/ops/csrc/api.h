@@ -15,6 +15,7 @@ enum Kernel : int {
   kFp8W4 = 16,    // gemm_fp8.hip: e4m3 A x column-major B, 4 waves x 128x128, bf16 out
   kMfmaW4 = 21,   // gemm_w4.hip: bf16/fp16 NN, 4 waves x 128x128, AGPR acc, split-K (M, N % 256)
   kT128 = 26,     // gemm_t128.hip: bf16/fp16 NN, 128x128 tile, 4 waves x 64x64, split-K (M, N % 128)
+  kT128x2 = 27,   // gemm_t128.hip with a 2-stage ring, 2 workgroups per CU (A/B vs kT128)
 };
 
 // Experiment / diagnostic ids (A/B and timing-only builds). Compiled and

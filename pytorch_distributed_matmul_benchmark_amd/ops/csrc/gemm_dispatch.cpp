@@ -25,7 +25,7 @@ hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream);
 bool gemm_w4_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub = 0);
 bool gemm_t128_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
-hipError_t gemm_t128_launch(int dt, GemmArgs a, hipStream_t stream);
+hipError_t gemm_t128_launch(int dt, GemmArgs a, hipStream_t stream, int stages = 4);
 
 static unsigned long long* g_debug_buffer = nullptr;
 
@@ -119,6 +119,7 @@ int resolve_kernel(const Problem& p, int kernel) {
     case kMfma256d: return fast ? kMfma256d : -1;
     case kMfmaW4: return w4 ? kMfmaW4 : -1;
     case kT128: return t128 ? kT128 : -1;
+    case kT128x2: return t128 ? kT128x2 : -1;
     case kF32_256s: return f32fast ? kF32_256s : -1;
 #ifdef PDMB_EXPERIMENTS
     case kF32_256: case kF32NoDma: return f32fast ? kernel : -1;
@@ -218,7 +219,8 @@ static Plan plan(const Problem& p, int kernel) {
 }
 
 int choose_splitk(const Problem& p, int kernel) {
-  const int k = resolve_kernel(p, kernel);
+  int k = resolve_kernel(p, kernel);
+  if (k == kT128x2) k = kT128;
   if (k != kMfmaW4 && k != kT128) return 0;
   return plan(p, k).splitk;
 }
@@ -272,7 +274,8 @@ static hipError_t tiled_launch(const Problem& p, int k, GemmArgs a, void* part, 
     }
   }
   a.splitk = S;
-  return k == kT128 ? gemm_t128_launch(p.dtype, a, stream) : gemm_w4_launch(p.dtype, a, stream, sub);
+  return k == kT128 ? gemm_t128_launch(p.dtype, a, stream, sub == 2 ? 2 : 4)
+                    : gemm_w4_launch(p.dtype, a, stream, sub);
 }
 
 // ---- padded fast path -------------------------------------------------------
@@ -400,6 +403,7 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel) {
   }
   const int k = resolve_kernel(p, kernel);
   if (k == kMfmaW4 || k == kT128) return splitk_bytes(p, k, plan(p, k).splitk);
+  if (k == kT128x2) return splitk_bytes(p, kT128, plan(p, kT128).splitk);
   if (k == kMfmaW4Tall || k == kMfmaW4Wide) return splitk_bytes(p, kMfmaW4, plan(p, kMfmaW4).splitk);
   return 0;
 }
@@ -470,6 +474,7 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kMfma256d: return gemm256_launch(p.dtype, a, 4, stream);
     case kMfmaW4:
     case kT128: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream);
+    case kT128x2: return tiled_launch(p, kT128, a, p.workspace, p.workspace_bytes, stream, 2);
     case kF32_256s: return gemm_f32_256_launch(a, 1, stream);
 #ifdef PDMB_EXPERIMENTS
     case kFp8: return gemm_fp8_launch(a, 0, stream);
@@ -567,6 +572,7 @@ const char* kernel_name(int kernel) {
     case kFp8W4: return "pdmb_fp8_w4_nt";
     case kMfmaW4: return "pdmb_w4_nn";
     case kT128: return "pdmb_t128_nn";
+    case kT128x2: return "pdmb_t128x2_nn";
     case kMfma256: return "pdmb_mfma256_nn";
     case kMfma256b: return "pdmb_mfma256b_nn";
     case kMfma256c: return "pdmb_mfma256c_nn";

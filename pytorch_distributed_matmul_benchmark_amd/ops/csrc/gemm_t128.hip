@@ -21,7 +21,8 @@
 //    (the NN B operand, no transposed copy). Both are W4's conflict-free
 //    layouts (A: W4's image at half the rows; B: one W4 half without the
 //    column interleave).
-//  * NS = 4 stage ring (4 x 32 KiB = 128 KiB, 1 workgroup per CU) filled by
+//  * NS = 4 stage ring (4 x 32 KiB = 128 KiB, 1 workgroup per CU; kT128x2:
+//    NS = 2, 64 KiB, 2 workgroups per CU) filled by
 //    LDS-DMA (buffer_load ... lds): during K-tile t the workgroup issues tile
 //    t + 4 into t's stage, so each tile has ~3 K-tiles of flight (a 128x128
 //    K-tile is 1/4 of W4's MFMA time, so the ring is deeper instead).
@@ -48,10 +49,33 @@ namespace kt128 {
 
 constexpr int BM = 128, BN = 128, BK = 64;
 constexpr int NT = 256;
-constexpr int NS = 4;                        // LDS stages
+constexpr int NS4 = 4;                       // LDS stages (default: 1 workgroup / CU)
 constexpr int A_BYTES = BM * BK * 2;         // 16 KiB
 constexpr int B_BYTES = BK * BN * 2;         // 16 KiB
 constexpr int STAGE = A_BYTES + B_BYTES;     // 32 KiB
+
+// Top-of-K-tile wait: the pieces issued after tile t+1's are those of tiles
+// t+2 .. t+NS-1 (8 per tile per wave).
+template <int NS>
+__device__ __forceinline__ void wait_next_and_barrier() {
+  if constexpr (NS == 4)
+    asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (NS == 3)
+    asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Prologue wait: tile 0 landed, tiles 1 .. NS-1 may still be in flight.
+template <int NS>
+__device__ __forceinline__ void wait_first_and_barrier() {
+  if constexpr (NS == 4)
+    asm volatile("s_waitcnt vmcnt(24)\n\ts_barrier" ::: "memory");
+  else if constexpr (NS == 3)
+    asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+}
 constexpr int NPIECE = 8;                    // DMA pieces per wave per K-tile (4 A + 4 B)
 
 template <int DT>
@@ -143,13 +167,14 @@ constexpr int piece_of(int gap) {
 
 // One K-tile: 32 MFMAs on (Ac, Bc) = fragments of tile t, reading tile t+1's
 // fragments into (An, Bn) from stage sn, DMA of tile t + NS into stage sc.
-template <int DT>
+template <int DT, int NS>
 __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, uint32_t sc,
                                       uint32_t sn, f32x4 (&acc)[4][4], Frag (&Ac)[4],
                                       Frag (&Bc)[4], Frag (&An)[4], Frag (&Bn)[4]) {
   const int td = t + NS < c.nk ? t + NS : c.nk - 1;  // clamped tail DMAs (harmless re-reads)
+  static_assert(NS >= 2 && NS <= 4, "T128 ring depth");
   const u32x4 rb = b_rsrc(c, td);
-  asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  wait_next_and_barrier<NS>();
   __builtin_amdgcn_sched_barrier(0);
   uint32_t ao[2], bo[4];
 #pragma unroll
@@ -174,8 +199,10 @@ __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, uin
   }
 }
 
-template <int DT>
-__global__ void __launch_bounds__(NT, 1) gemm_t128_nn(GemmArgs a) {
+// NS = 4: 128 KiB ring, 1 workgroup per CU (default). NS = 2: 64 KiB, 2
+// workgroups per CU (kT128x2: the other workgroup hides DMA latency).
+template <int DT, int NS>
+__global__ void __launch_bounds__(NT, NS == 2 ? 2 : 1) gemm_t128_nn(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
 
   int bz, tm, tn;
@@ -250,7 +277,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_t128_nn(GemmArgs a) {
 #pragma unroll
     for (int h = 0; h < NPIECE; ++h) issue_piece(c, rb, st * STAGE, tl, h);
   }
-  asm volatile("s_waitcnt vmcnt(24)\n\ts_barrier" ::: "memory");  // tile 0 landed everywhere
+  wait_first_and_barrier<NS>();  // tile 0 landed everywhere
   Frag A0[4], B0[4], A1[4], B1[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -265,14 +292,14 @@ __global__ void __launch_bounds__(NT, 1) gemm_t128_nn(GemmArgs a) {
   // t+2 .. t+NS-1 = 16 pieces (the prologue issued t+NS-1 = 3 for t = 0).
   int t = 0;
   for (; t + 1 < nk; t += 2) {
-    ktile<DT>(c, smem, t, (uint32_t)((t % NS) * STAGE), (uint32_t)(((t + 1) % NS) * STAGE), acc,
-              A0, B0, A1, B1);
-    ktile<DT>(c, smem, t + 1, (uint32_t)(((t + 1) % NS) * STAGE),
+    ktile<DT, NS>(c, smem, t, (uint32_t)((t % NS) * STAGE), (uint32_t)(((t + 1) % NS) * STAGE),
+                  acc, A0, B0, A1, B1);
+    ktile<DT, NS>(c, smem, t + 1, (uint32_t)(((t + 1) % NS) * STAGE),
               (uint32_t)(((t + 2) % NS) * STAGE), acc, A1, B1, A0, B0);
   }
   if (t < nk)  // odd count: the last tile's "next" reads are clamped re-reads
-    ktile<DT>(c, smem, t, (uint32_t)((t % NS) * STAGE), (uint32_t)((t % NS) * STAGE), acc, A0,
-              B0, A1, B1);
+    ktile<DT, NS>(c, smem, t, (uint32_t)((t % NS) * STAGE), (uint32_t)((t % NS) * STAGE), acc, A0,
+                  B0, A1, B1);
   // Drain the tail DMAs and give the last MFMAs time to write their AGPRs
   // (asm MFMAs are invisible to hipcc's hazard recognizer).
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
@@ -325,7 +352,7 @@ bool gemm_t128_supported(int dt, const GemmArgs& a, size_t align_a, size_t align
   return true;
 }
 
-hipError_t gemm_t128_launch(int dt, GemmArgs a, hipStream_t stream) {
+hipError_t gemm_t128_launch(int dt, GemmArgs a, hipStream_t stream, int stages) {
   a.tiles_m = a.M / kt128::BM;
   a.tiles_n = a.N / kt128::BN;
   const int S = a.splitk > 1 ? a.splitk : 1;
@@ -343,10 +370,17 @@ hipError_t gemm_t128_launch(int dt, GemmArgs a, hipStream_t stream) {
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
   const dim3 grid((unsigned)nblocks), block(kt128::NT);
-  if (dt == kBF16)
-    hipLaunchKernelGGL(kt128::gemm_t128_nn<kBF16>, grid, block, 0, stream, a);
-  else
-    hipLaunchKernelGGL(kt128::gemm_t128_nn<kF16>, grid, block, 0, stream, a);
+  if (stages == 2) {
+    if (dt == kBF16)
+      hipLaunchKernelGGL((kt128::gemm_t128_nn<kBF16, 2>), grid, block, 0, stream, a);
+    else
+      hipLaunchKernelGGL((kt128::gemm_t128_nn<kF16, 2>), grid, block, 0, stream, a);
+  } else {
+    if (dt == kBF16)
+      hipLaunchKernelGGL((kt128::gemm_t128_nn<kBF16, kt128::NS4>), grid, block, 0, stream, a);
+    else
+      hipLaunchKernelGGL((kt128::gemm_t128_nn<kF16, kt128::NS4>), grid, block, 0, stream, a);
+  }
   return hipGetLastError();
 }
 

@@ -346,7 +346,7 @@ def test_thin_grid_supertiles_exact(M, N, batch, kernel, dtype):
 # ---- under-filled grids: T128 (128x128 tiles) and W4 / T128 split-K ----
 # (matrix_parallel column shards at ws >= 4: 4096 x 512, 8192 x 1024; 2048^3)
 
-@pytest.mark.parametrize("kernel", ["w4", "t128"])
+@pytest.mark.parametrize("kernel", ["w4", "t128", "t128x2"])
 @pytest.mark.parametrize("M,N,K,b,splitk", [
     (2048, 2048, 2048, 1, 0), (4096, 512, 4096, 1, 0), (8192, 1024, 8192, 1, 2),
     (1024, 1024, 4096, 1, 2), (1024, 1024, 4096, 1, 4), (1024, 1024, 4096, 1, 8),
