@@ -14,8 +14,9 @@ enum Kernel : int {
   kMfma256d = 9,  // gemm_mfma256.hip SCHED 3: 8 waves, 256x256, edge tiles (any M, N % 8)
   kFp8W4 = 16,    // gemm_fp8.hip: e4m3 A x column-major B, 4 waves x 128x128, bf16 out
   kMfmaW4 = 21,   // gemm_w4.hip: bf16/fp16 NN, 4 waves x 128x128, AGPR acc, split-K (M, N % 256)
-  kT128 = 26,     // gemm_t128.hip: bf16/fp16 NN, 128x128 tile, 4 waves x 64x64, split-K (M, N % 128)
-  kT128x2 = 27,   // gemm_t128.hip with a 2-stage ring, 2 workgroups per CU (A/B vs kT128)
+  kT128 = 26,     // gemm_tile.hip: bf16/fp16 NN, 128x128 tile, 4 waves x 64x64, split-K (M, N % 128)
+  kT128x2 = 27,   // gemm_tile.hip 128x128 with a 2-stage ring, 2 workgroups per CU (A/B vs kT128)
+  kT256x128 = 28, // gemm_tile.hip: 256x128 tile, 4 waves x 128x64, 3-stage ring (M % 256, N % 128)
 };
 
 // Experiment / diagnostic ids (A/B and timing-only builds). Compiled and

@@ -24,8 +24,9 @@ bool gemm_fp8_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_
 hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream);
 bool gemm_w4_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub = 0);
-bool gemm_t128_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
-hipError_t gemm_t128_launch(int dt, GemmArgs a, hipStream_t stream, int stages = 4);
+bool gemm_tile_supported(int dt, int bm, const GemmArgs& a, size_t align_a, size_t align_b,
+                         size_t align_c);
+hipError_t gemm_tile_launch(int kernel, int dt, GemmArgs a, hipStream_t stream);
 
 static unsigned long long* g_debug_buffer = nullptr;
 
@@ -103,7 +104,8 @@ int resolve_kernel(const Problem& p, int kernel) {
   if (is_fp8_kernel(kernel)) return -1;
   const bool fast = gemm256_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   const bool w4 = gemm_w4_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
-  const bool t128 = gemm_t128_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
+  const bool t128 = gemm_tile_supported(p.dtype, 128, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
+  const bool t256 = gemm_tile_supported(p.dtype, 256, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   const bool f32fast = p.dtype == kF32 &&
                        gemm_f32_256_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   switch (kernel) {
@@ -113,13 +115,14 @@ int resolve_kernel(const Problem& p, int kernel) {
     // that fill the chip, T128 for under-filled ones: plan()), SCHED 3 for
     // edge tiles.
     case kAuto:
-      if (w4 || t128) return plan(p, kAuto).kernel;
+      if (w4 || t128 || t256) return plan(p, kAuto).kernel;
       return fast ? kMfma256d : f32fast ? kF32_256s : kGeneric;
     case kGeneric: return kGeneric;
     case kMfma256d: return fast ? kMfma256d : -1;
     case kMfmaW4: return w4 ? kMfmaW4 : -1;
     case kT128: return t128 ? kT128 : -1;
-    case kT128x2: return t128 ? kT128x2 : -1;
+    case kT128x2: return t128 ? kT128x2 : -1;  // shares T128's constraints
+    case kT256x128: return t256 ? kT256x128 : -1;
     case kF32_256s: return f32fast ? kF32_256s : -1;
 #ifdef PDMB_EXPERIMENTS
     case kF32_256: case kF32NoDma: return f32fast ? kernel : -1;
@@ -132,28 +135,50 @@ int resolve_kernel(const Problem& p, int kernel) {
   }
 }
 
-// ---- tile size and split-K (W4 / T128) -------------------------------
+// ---- tile size and split-K (W4 / tile family) ------------------------------
 // A grid of T output tiles fills the 256 CUs (1 workgroup / CU) only if T is
-// a multiple of 256: the matrix_parallel column shards at ws >= 4 for the
-// reference's default sizes (matmul_scaling_benchmark.py:179-188, :351) have
-// T = 32 / 128 256x256 tiles (4k / 8k at ws = 8). Two levers: the 128x128
-// tile (T128, 4x the workgroups, each K-tile ~kT128Kt of a W4 K-tile) and
-// splitting K over S workgroups per tile (each extra slice costs the last one
-// a serial read of one fp32 slab: 256 KiB for W4, 64 KiB for T128). Model, in
-// W4 K-tile times (~1.2 us on MI355X):
-//   cost = waves(T * S) * (ceil(nk / S) * kt + fixed + meet * (S - 1))
-// (waves over the CUs the stream may use, Problem::cus) over W4 x S in
-// {1, 2, 4} and T128 x S in {1, 2, 4}; the cheapest wins, W4 on
-// ties (its tile is the more efficient one at full occupancy). Constants from
-// profiles/r2_t128_splitk_sweep.jsonl (interleaved vs hipBLASLt).
-static constexpr double kT128Kt = 0.40;   // T128 K-tile / W4 K-tile (16k: 952 vs 1507 TF)
-static constexpr double kFixed = 1.0;     // launch + prologue + epilogue
-static constexpr double kMeetW4 = 3.0;    // 256 KiB slab
-static constexpr double kMeetT128 = 0.8;  // 64 KiB slab
+// a multiple of 256: the matrix_parallel column shards for the reference's
+// default sizes (matmul_scaling_benchmark.py:179-188, :351) have T = 32 / 128
+// 256x256 tiles (4k / 8k at ws = 8; 4k at ws = 2 too). Two levers: smaller
+// tiles (gemm_tile.hip: T256x128 = 2x, T128 = 4x the workgroups; T128x2 runs
+// two of them per CU) and splitting K over S workgroups per tile. The planner
+// prices every (kernel, S) in microseconds and takes the cheapest (W4 unless
+// another is >= 3 % cheaper):
+//   waves = ceil(units / (CUs the stream may use x workgroups per CU))
+//   t     = waves * (ceil(nk / S) * kt * boost(busy) + kFixedUs) + meet
+//   boost = 0.62 + 0.38 * busy: a K-tile runs faster while part of the chip
+//           idles (power headroom: W4's K-tile is 1.16 us at 128 workgroups,
+//           1.42 us at 256+)
+//   meet  = split-K combine, chip-bandwidth bound: every slice but one
+//           writes and the last reads back an fp32 tile slab,
+//           T * (S-1) * 2 * BM * BN * 4 B / kSlabBw + kMeetUs.
+// kt per K-tile at full occupancy (us, random bf16, profiles/r2_*sweep*.jsonl):
+// W4 1.42, T128 0.46, T128x2 0.86 per pair of co-resident workgroups. The fit
+// reproduces the measured times of the shard shapes within ~10 %.
+struct KernelModel {
+  int kernel, bm, bn, occ;
+  double kt;
+};
+static constexpr KernelModel kModels[] = {
+    {kMfmaW4, 256, 256, 1, 1.42},
+    {kT256x128, 256, 128, 1, 0.78},
+    {kT128, 128, 128, 1, 0.46},
+    {kT128x2, 128, 128, 2, 0.86},
+};
+static constexpr double kFixedUs = 4.0;   // launch + prologue + epilogue
+static constexpr double kMeetUs = 4.0;    // combine latency (poll, serial slab read)
+static constexpr double kSlabBw = 4.0e6;  // bytes per us of slab traffic, chip-wide
 static constexpr int kMinKt = 4;          // K-tiles per slice, at least
 
-static long long tiles_of(const Problem& p, int tile) {
-  return (long long)(p.M / tile) * (p.N / tile) * (p.batch < 1 ? 1 : p.batch);
+static const KernelModel& model_of(int kernel) {
+  for (const KernelModel& m : kModels)
+    if (m.kernel == kernel) return m;
+  return kModels[0];
+}
+
+static long long tiles_of(const Problem& p, int kernel) {
+  const KernelModel& m = model_of(kernel);
+  return (long long)(p.M / m.bm) * (p.N / m.bn) * (p.batch < 1 ? 1 : p.batch);
 }
 
 static int device_cus() {
@@ -170,65 +195,72 @@ static int device_cus() {
 }
 
 static double plan_cost(const Problem& p, int kernel, int S) {
-  const int tile = kernel == kT128 ? 128 : 256;
-  const long long T = tiles_of(p, tile);
+  const KernelModel& m = model_of(kernel);
+  const long long T = tiles_of(p, kernel);
   const int nk = p.K / 64;
   const int per = (nk + S - 1) / S;
-  const double kt = kernel == kT128 ? kT128Kt : 1.0;
-  const double meet = kernel == kT128 ? kMeetT128 : kMeetW4;
-  const long long cus = p.cus > 0 ? p.cus : device_cus();  // 1 workgroup per CU
-  return (double)((T * S + cus - 1) / cus) * (per * kt + kFixed + meet * (S - 1));
+  const long long slots = (long long)(p.cus > 0 ? p.cus : device_cus()) * m.occ;
+  const long long units = T * S;
+  const long long waves = (units + slots - 1) / slots;
+  const double busy = (double)units / (double)(waves * slots);
+  double t = (double)waves * (per * m.kt * (0.62 + 0.38 * busy) + kFixedUs);
+  if (S > 1) t += (double)T * (S - 1) * 2.0 * m.bm * m.bn * 4.0 / kSlabBw + kMeetUs;
+  return t;
 }
 
 static bool split_ok(const Problem& p, int kernel, int S) {
   if (S == 1) return true;
   const int nk = p.K / 64;
   const int per = (nk + S - 1) / S;
-  const int tile = kernel == kT128 ? 128 : 256;
-  return per >= kMinKt && (S - 1) * per < nk && tiles_of(p, tile) <= kMaxSplitTiles;
+  return per >= kMinKt && (S - 1) * per < nk && tiles_of(p, kernel) <= kMaxSplitTiles;
 }
 
-// `kernel`: kAuto (choose), kMfmaW4 or kT128 (choose only the split).
-// p.splitk > 0 fixes the split.
-static Plan plan(const Problem& p, int kernel) {
+static bool supports(const Problem& p, int kernel) {
   const GemmArgs a = to_args(p);
-  const bool w4 = (kernel == kAuto || kernel == kMfmaW4) &&
-                  gemm_w4_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
-  const bool t128 = (kernel == kAuto || kernel == kT128) &&
-                    gemm_t128_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
+  if (kernel == kMfmaW4) return gemm_w4_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
+  return gemm_tile_supported(p.dtype, model_of(kernel).bm, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
+}
+
+// `kernel`: kAuto (choose), or one of kMfmaW4 / kT256x128 / kT128 / kT128x2
+// (choose only the split). p.splitk > 0 fixes the split.
+static Plan plan(const Problem& p, int kernel) {
   Plan best{-1, 1};
   double bc = 1e300;
-  auto consider = [&](int k, int S) {
-    if (p.splitk > 0 && S != p.splitk) return;
-    if (!split_ok(p, k, S)) return;
-    const double c = plan_cost(p, k, S);
-    if (c < bc * 0.97) {  // a different choice only for a clear win
-      bc = c;
-      best = Plan{k, S};
-    }
-  };
+  bool any = false;
   static const int kS[] = {1, 2, 4, 8};
-  if (w4)
-    for (int S : kS)
-      if (S <= 4 || p.splitk == S) consider(kMfmaW4, S);
-  if (t128)
-    for (int S : kS)
-      if (S <= 4 || p.splitk == S) consider(kT128, S);
-  if (best.kernel < 0 && (w4 || t128)) best = Plan{w4 ? kMfmaW4 : kT128, 0};  // invalid split
+  for (const KernelModel& m : kModels) {
+    if (kernel != kAuto && kernel != m.kernel) continue;
+    if (!supports(p, m.kernel)) continue;
+    any = true;
+    for (int S : kS) {
+      if (S > 4 && p.splitk != S) continue;
+      if (p.splitk > 0 && S != p.splitk) continue;
+      if (!split_ok(p, m.kernel, S)) continue;
+      const double c = plan_cost(p, m.kernel, S);
+      if (c < bc * 0.97) {  // a different choice only for a clear win
+        bc = c;
+        best = Plan{m.kernel, S};
+      }
+    }
+  }
+  if (best.kernel < 0 && any)  // the requested split is impossible for this K
+    for (const KernelModel& m : kModels)
+      if ((kernel == kAuto || kernel == m.kernel) && supports(p, m.kernel)) return Plan{m.kernel, 0};
   return best;
 }
 
+static bool is_tiled(int k) { return k == kMfmaW4 || k == kT128 || k == kT128x2 || k == kT256x128; }
+
 int choose_splitk(const Problem& p, int kernel) {
-  int k = resolve_kernel(p, kernel);
-  if (k == kT128x2) k = kT128;
-  if (k != kMfmaW4 && k != kT128) return 0;
+  const int k = resolve_kernel(p, kernel);
+  if (!is_tiled(k)) return 0;
   return plan(p, k).splitk;
 }
 
 static size_t splitk_bytes(const Problem& p, int kernel, int S) {
   if (S <= 1) return 0;
-  const int tile = kernel == kT128 ? 128 : 256;
-  return (size_t)tiles_of(p, tile) * S * tile * tile * sizeof(float);  // one slot per slice
+  const KernelModel& m = model_of(kernel);
+  return (size_t)tiles_of(p, m.kernel) * S * m.bm * m.bn * sizeof(float);  // one slot per slice
 }
 
 // Per-(device, stream) split-K counters (2 per tile), zeroed once on the
@@ -258,10 +290,10 @@ static unsigned* stream_counters(hipStream_t s) {
   return c;
 }
 
-// Launch W4 or T128 (kernel k, already resolved) with its planned split.
+// Launch W4 or a tile-family kernel (k, already resolved) with its planned split.
 static hipError_t tiled_launch(const Problem& p, int k, GemmArgs a, void* part, size_t part_bytes,
                                hipStream_t stream, int sub = 0) {
-  int S = plan(p, k == kT128 ? kT128 : kMfmaW4).splitk;
+  int S = plan(p, k).splitk;
   if (S < 1) return hipErrorInvalidValue;  // requested split not possible for this K
   if (S > 1) {
     unsigned* flags = stream_counters(stream);
@@ -274,8 +306,7 @@ static hipError_t tiled_launch(const Problem& p, int k, GemmArgs a, void* part, 
     }
   }
   a.splitk = S;
-  return k == kT128 ? gemm_t128_launch(p.dtype, a, stream, sub == 2 ? 2 : 4)
-                    : gemm_w4_launch(p.dtype, a, stream, sub);
+  return k == kMfmaW4 ? gemm_w4_launch(p.dtype, a, stream, sub) : gemm_tile_launch(k, p.dtype, a, stream);
 }
 
 // ---- padded fast path -------------------------------------------------------
@@ -399,11 +430,10 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel) {
     const Padded d = padded_problem(p, nullptr);
     const size_t copies = d.a_bytes + d.b_bytes + d.c_bytes;
     const int k = resolve_kernel(d.q, kAuto);
-    return copies + ((k == kMfmaW4 || k == kT128) ? splitk_bytes(d.q, k, plan(d.q, k).splitk) : 0);
+    return copies + (is_tiled(k) ? splitk_bytes(d.q, k, plan(d.q, k).splitk) : 0);
   }
   const int k = resolve_kernel(p, kernel);
-  if (k == kMfmaW4 || k == kT128) return splitk_bytes(p, k, plan(p, k).splitk);
-  if (k == kT128x2) return splitk_bytes(p, kT128, plan(p, kT128).splitk);
+  if (is_tiled(k)) return splitk_bytes(p, k, plan(p, k).splitk);
   if (k == kMfmaW4Tall || k == kMfmaW4Wide) return splitk_bytes(p, kMfmaW4, plan(p, kMfmaW4).splitk);
   return 0;
 }
@@ -439,7 +469,7 @@ static hipError_t gemm_padded(const Problem& p, hipStream_t stream, int* used) {
   char* part = Cp + d.c_bytes;
   const size_t part_bytes = p.workspace_bytes - (d.a_bytes + d.b_bytes + d.c_bytes);
   e = k == kF32_256s  ? gemm_f32_256_launch(a, 1, stream)
-      : (k == kMfmaW4 || k == kT128) ? tiled_launch(q, k, a, part, part_bytes, stream)
+      : is_tiled(k) ? tiled_launch(q, k, a, part, part_bytes, stream)
                      : gemm256_launch(q.dtype, a, 4, stream);
   if (e != hipSuccess) return e;
   for (int b = 0; b < batch; ++b) {
@@ -473,8 +503,9 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kFp8W4: return gemm_fp8_launch(a, 1, stream);
     case kMfma256d: return gemm256_launch(p.dtype, a, 4, stream);
     case kMfmaW4:
-    case kT128: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream);
-    case kT128x2: return tiled_launch(p, kT128, a, p.workspace, p.workspace_bytes, stream, 2);
+    case kT128:
+    case kT128x2:
+    case kT256x128: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream);
     case kF32_256s: return gemm_f32_256_launch(a, 1, stream);
 #ifdef PDMB_EXPERIMENTS
     case kFp8: return gemm_fp8_launch(a, 0, stream);
@@ -573,6 +604,7 @@ const char* kernel_name(int kernel) {
     case kMfmaW4: return "pdmb_w4_nn";
     case kT128: return "pdmb_t128_nn";
     case kT128x2: return "pdmb_t128x2_nn";
+    case kT256x128: return "pdmb_t256x128_nn";
     case kMfma256: return "pdmb_mfma256_nn";
     case kMfma256b: return "pdmb_mfma256b_nn";
     case kMfma256c: return "pdmb_mfma256c_nn";

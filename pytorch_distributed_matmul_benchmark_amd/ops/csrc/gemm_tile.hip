@@ -1,0 +1,413 @@
+// gemm_tile.hip — bf16 / fp16 C = A @ B (row-major NN, fp32 accumulate): the
+// one-barrier LDS-DMA tile family for grids that under-fill the 256 CUs with
+// W4's 256x256 tiles. Members (Cfg<BM, BN, NS>):
+//   T128      128 x 128, 4-stage ring, 1 workgroup / CU
+//   T128x2    128 x 128, 2-stage ring, 2 workgroups / CU (A/B)
+//   T256x128  256 x 128, 3-stage ring, 1 workgroup / CU
+//
+// Why: matrix_parallel's per-rank column shards at ws >= 2 of the reference's
+// default sizes (matmul_scaling_benchmark.py:179-188 at :351-352) include
+// [4096^2] @ [4096 x 512] (32 256x256 tiles), [8192^2] @ [8192 x 1024] and
+// [4096^2] @ [4096 x 2048] (128 each); 2048^3 has 64. W4 (gemm_w4.hip) leaves
+// most CUs idle there, and splitting K over 256x256 tiles costs a 256 KiB
+// fp32 slab per slice to combine (profiles/r2_t128_splitk_sweep.jsonl). The
+// smaller tiles give 2x / 4x the workgroups with the same LDS images and MFMA
+// idiom, and smaller split-K slabs.
+//
+// Structure (W4's idioms, one barrier per K-tile):
+//  * 4 waves, one per SIMD, as 2 x 2, each owning a (BM/2) x 64 output block
+//    (MB x NB MFMA 16x16x32 blocks, MB = BM/32, NB = 4; fp32 accumulators in
+//    AGPRs; operands swapped so the accumulator holds C^T).
+//  * LDS images per stage: A [BM rows][128 B] with 16-B chunk c at
+//    c ^ ((row >> 1) & 7); B [64 k][256 B] with 32-B unit u (16 columns) at
+//    u ^ ((k & 3) | ((k >> 3) & 1) << 2), read transposed by ds_read_b64_tr_b16
+//    (the NN B operand, no transposed copy). Both are W4's conflict-free
+//    layouts (A: W4's image at BM rows; B: one W4 B half without its column
+//    interleave).
+//  * NS-stage ring filled by LDS-DMA (buffer_load ... lds): during K-tile t
+//    the workgroup refills t's stage with tile t + NS, so each tile has
+//    ~NS-1 K-tiles of flight.
+//  * One barrier per K-tile: s_waitcnt vmcnt(P * (NS-2)) (tile t+1 landed;
+//    later tiles may be in flight; P DMA pieces per wave per K-tile)
+//    lgkmcnt(0) (this wave's reads of tile t's fragments done) then
+//    s_barrier; after it t's stage is free and t+1's readable. Fragments of
+//    t+1 are read during t's MFMAs into a second register set.
+//  * Every load sits in an MFMA gap (Sched: B fragments, A fragments and DMA
+//    pieces spread over the K-tile's MFMA gaps, at most one per gap).
+//  * Optional split-K over K-tile ranges with the in-launch combine of
+//    splitk.h.
+//
+// Fast-path constraints (host-checked): M % BM == 0, N % BN == 0 (interior
+// tiles only), K % 64 == 0, lda / ldb % 8 == 0, ldc % 4 == 0, 16-B aligned
+// A / B, 8-B aligned C.
+#include "api.h"
+#include "common.h"
+#include "splitk.h"
+
+namespace pdmb {
+namespace ktile {
+
+constexpr int BK = 64;
+constexpr int NT = 256;
+
+template <int BM_, int BN_, int NS_, int OCC_>
+struct Cfg {
+  static constexpr int BM = BM_, BN = BN_, NS = NS_, OCC = OCC_;
+  static_assert(BN == 128, "B image: one 256-B row of 128 columns per k");
+  static_assert(BM == 128 || BM == 256, "A image rows");
+  static_assert(NS >= 2 && NS <= 4, "ring depth");
+  static constexpr int MB = BM / 32, NB = BN / 32;       // 16x16 blocks per wave (2 x 2 waves)
+  static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BK * BN * 2;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int PA = A_BYTES / 4096, PB = B_BYTES / 4096;  // 1 KiB pieces per wave
+  static constexpr int P = PA + PB;
+  static constexpr int G = MB * NB * 2;                  // MFMAs (gaps) per K-tile per wave
+  static_assert(NS * STAGE <= 160 * 1024 / OCC, "LDS");
+};
+
+using CfgT128 = Cfg<128, 128, 4, 1>;
+using CfgT128x2 = Cfg<128, 128, 2, 2>;
+using CfgT256x128 = Cfg<256, 128, 3, 1>;
+
+// Item schedule of one K-tile: which load follows MFMA `gap`. Three classes —
+// B fragment halves (2 NB, each two ds_read_b64_tr_b16), A fragment halves
+// (2 MB, ds_read_b128) and DMA pieces (P) — are spread Bresenham-style so each
+// class stays within one item of its even share of the gaps; at most one item
+// per gap. Encoding: 0 none; 1 + piece; 100 + (2j + half) B; 200 + (2m + half) A.
+template <class C>
+struct Sched {
+  int item[C::G];
+  constexpr Sched() : item() {
+    const int T[3] = {2 * C::NB, 2 * C::MB, C::P};
+    int n[3] = {0, 0, 0};
+    for (int g = 0; g < C::G; ++g) {
+      int best = -1, bd = 0;
+      for (int k = 0; k < 3; ++k) {
+        const int d = T[k] * (g + 1) - n[k] * C::G;  // deficit vs the even share (x G)
+        if (n[k] < T[k] && d > bd) {
+          bd = d;
+          best = k;
+        }
+      }
+      if (best == 0) item[g] = 100 + n[0]++;
+      else if (best == 1) item[g] = 200 + n[1]++;
+      else if (best == 2) item[g] = 1 + n[2]++;
+      else item[g] = 0;
+    }
+  }
+  constexpr int issued(int base, int lo, int hi) const {
+    int c = 0;
+    for (int g = 0; g < C::G; ++g) c += (item[g] >= lo && item[g] < hi) ? 1 : 0;
+    return c + base;
+  }
+};
+
+template <int DT>
+__device__ __forceinline__ void mfma_acc(f32x4& acc, const s16x8& b, const s16x8& a);
+template <>
+__device__ __forceinline__ void mfma_acc<kBF16>(f32x4& acc, const s16x8& b, const s16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+}
+template <>
+__device__ __forceinline__ void mfma_acc<kF16>(f32x4& acc, const s16x8& b, const s16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+}
+
+// LDS-DMA with a scalar offset; M0 is clobbered (declared), not saved.
+__device__ __forceinline__ void dma16_m0(u32x4 rsrc, uint32_t voff, uint32_t soff, uint32_t lds) {
+  asm volatile(
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %0, %1, %2 offen lds"
+      :
+      : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds)
+      : "memory", "m0");
+}
+
+// Top-of-K-tile wait (N = P * (NS - 2): pieces of tiles t+2 .. t+NS-1 may be in
+// flight, tile t+1's have landed) and the prologue's (N = P * (NS - 1)).
+template <int N>
+__device__ __forceinline__ void wait_lgkm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+struct Frag {  // one 16-row (A) or 16-column (B) block of a K-tile: k 0..31 and 32..63
+  s16x8 k[2];
+};
+
+template <class C>
+struct Ctx {
+  u32x4 ra;               // A descriptor at this slice's first K
+  const char* Bb;         // B at this slice's first K row, column n0
+  long long b_bytes;      // bytes from Bb to the end of B's extent
+  int lda2, ldb2, nk;     // leading dims in bytes, K-tiles of this slice
+  uint32_t voffA, voffB;  // per-lane DMA offsets of piece 0
+  uint32_t aoff[2];       // per-lane A fragment offsets in stage 0, [ks]
+  uint32_t boff[C::NB];   // per-lane B fragment offsets in stage 0, [block j]
+  int wu;
+  uint32_t lds0;
+};
+
+template <class C>
+__device__ __forceinline__ u32x4 b_rsrc(const Ctx<C>& c, int tile) {
+  const long long off = (long long)tile * BK * c.ldb2;
+  return make_rsrc(c.Bb + off, c.b_bytes - off);
+}
+
+// DMA piece h (0 .. P-1) of K-tile `tile` into the stage at byte offset `so`.
+// h < PA: A rows h*32 + wu*8 + [0,8) (8 x 128 B); else B k rows
+// (h-PA)*16 + wu*4 + [0,4) (4 x 256 B). The swizzles depend on (row >> 1) & 7
+// (A) and k & 11 (B) only, which those row offsets leave alone, so one
+// per-lane offset serves every piece.
+template <class C>
+__device__ __forceinline__ void issue_piece(const Ctx<C>& c, u32x4 rb, uint32_t so, int tile, int h) {
+  if (h < C::PA) {
+    dma16_m0(c.ra, c.voffA, (uint32_t)tile * (BK * 2) + (uint32_t)(h * 32 * c.lda2),
+             c.lds0 + so + (h * 32 + c.wu * 8) * 128);
+  } else {
+    const int kb = h - C::PA;
+    dma16_m0(rb, c.voffB, (uint32_t)(kb * 16 * c.ldb2),
+             c.lds0 + so + C::A_BYTES + (kb * 16 + c.wu * 4) * 256);
+  }
+}
+
+// A fragment half ks of block m (rows 16m..16m+15 of this wave's BM/2).
+__device__ __forceinline__ s16x8 frag_a(const char* smem, uint32_t off, int m) {
+  return *(const lds_s16x8*)(smem + m * 16 * 128 + off);
+}
+
+// B fragment half ks of block j (16 output columns): two transposed reads.
+template <class C>
+__device__ __forceinline__ s16x8 frag_b(const char* smem, uint32_t off, int ks) {
+  const char* p = smem + C::A_BYTES + ks * 32 * 256 + off;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p + 4 * 256));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// One K-tile: G MFMAs on (Ac, Bc) = fragments of tile t, reading tile t+1's
+// fragments into (An, Bn) from stage sn, DMA of tile t + NS into stage sc.
+template <int DT, class C>
+__device__ __forceinline__ void ktile(const Ctx<C>& c, const char* smem, int t, uint32_t sc,
+                                      uint32_t sn, f32x4 (&acc)[C::MB][C::NB], Frag (&Ac)[C::MB],
+                                      Frag (&Bc)[C::NB], Frag (&An)[C::MB], Frag (&Bn)[C::NB]) {
+  constexpr Sched<C> S{};
+  const int td = t + C::NS < c.nk ? t + C::NS : c.nk - 1;  // clamped tail DMAs (harmless re-reads)
+  const u32x4 rb = b_rsrc(c, td);
+  wait_lgkm_barrier<C::P * (C::NS - 2)>();
+  __builtin_amdgcn_sched_barrier(0);
+  uint32_t ao[2], bo[C::NB];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) ao[ks] = c.aoff[ks] + sn;
+#pragma unroll
+  for (int j = 0; j < C::NB; ++j) bo[j] = c.boff[j] + sn;
+#pragma unroll
+  for (int gap = 0; gap < C::G; ++gap) {
+    constexpr int MN = C::MB * C::NB;
+    const int ks = gap / MN, mi = (gap % MN) / C::NB, ni = gap % C::NB;
+    mfma_acc<DT>(acc[mi][ni], Bc[ni].k[ks], Ac[mi].k[ks]);
+    const int it = S.item[gap];
+    if (it >= 200) {
+      const int m = (it - 200) >> 1, h = (it - 200) & 1;
+      An[m].k[h] = frag_a(smem, ao[h], m);
+    } else if (it >= 100) {
+      const int j = (it - 100) >> 1, h = (it - 100) & 1;
+      Bn[j].k[h] = frag_b<C>(smem, bo[j], h);
+    } else if (it >= 1) {
+      issue_piece<C>(c, rb, sc, td, it - 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int DT, class C>
+__global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[C::NS * C::STAGE];
+  constexpr int MB = C::MB, NB = C::NB, NS = C::NS;
+
+  int bz, tm, tn;
+  map_tile(a, blockIdx.x, bz, tm, tn);
+  int slice = 0;  // split-K: grid batch = batch x S, slice innermost (as W4)
+  if (a.splitk > 1) {
+    slice = bz % a.splitk;
+    bz /= a.splitk;
+  }
+  const int kt0 = slice * a.kt_per;
+  const int m0 = tm * C::BM, n0 = tn * C::BN;
+  const int lane = threadIdx.x & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wu >> 1, wc = wu & 1;
+  const int l16 = lane & 15, g = lane >> 4;
+
+  Ctx<C> c;
+  c.wu = wu;
+  c.lds0 = (uint32_t)(size_t)((lds_void*)smem);
+  c.lda2 = a.lda * 2;
+  c.ldb2 = a.ldb * 2;
+  {
+    const int nk_all = a.K / BK;
+    c.nk = a.splitk > 1 ? min(a.kt_per, nk_all - kt0) : nk_all;
+  }
+  const int k0 = kt0 * BK;
+  const char* Ab = (const char*)a.A + ((long long)bz * a.sA + (long long)m0 * a.lda + k0) * 2;
+  c.ra = make_rsrc(Ab, ((long long)(a.M - m0 - 1) * a.lda + (a.K - k0)) * 2);
+  c.Bb = (const char*)a.B + ((long long)bz * a.sB + (long long)k0 * a.ldb + n0) * 2;
+  c.b_bytes = ((long long)(a.K - k0 - 1) * a.ldb + (a.N - n0)) * 2;
+  {
+    const int r = wu * 8 + (lane >> 3), lc8 = lane & 7;  // row of A piece 0
+    c.voffA = (uint32_t)(r * c.lda2 + ((lc8 ^ ((r >> 1) & 7)) * 16));
+    const int lr16 = lane >> 4, lc16 = lane & 15;
+    const int k = wu * 4 + lr16;  // k row of B piece 0
+    const int s = (k & 3) | (((k >> 3) & 1) << 2);
+    const int n = ((lc16 >> 1) ^ s) * 16 + (lc16 & 1) * 8;  // column of this lane's 16 B
+    c.voffB = (uint32_t)(k * c.ldb2 + n * 2);
+    const int swA = (l16 >> 1) & 7;
+    const int q4 = l16 >> 2, p4 = l16 & 3;
+    const int sB = q4 | ((g & 1) << 2);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint32_t ao = (uint32_t)((wr * (C::BM / 2) + l16) * 128 + (((4 * ks + g) ^ swA) * 16));
+      asm volatile("" : "+v"(ao));  // opaque: one base VGPR each
+      c.aoff[ks] = ao;
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int u = NB * wc + j;  // 32-B unit = columns 16u .. 16u+15 of the tile
+      uint32_t bo = (uint32_t)((8 * g + q4) * 256 + ((u ^ sB) * 32) + p4 * 8);
+      asm volatile("" : "+v"(bo));
+      c.boff[j] = bo;
+    }
+  }
+
+  f32x4 acc[MB][NB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Prologue: tiles 0 .. NS-1 into stages 0 .. NS-1 (clamped), wait for tile
+  // 0 everywhere (tiles 1 .. NS-1 may still fly), read its fragments.
+  const int nk = c.nk;
+#pragma unroll
+  for (int st = 0; st < NS; ++st) {
+    const int tl = st < nk ? st : nk - 1;
+    const u32x4 rb = b_rsrc(c, tl);
+#pragma unroll
+    for (int h = 0; h < C::P; ++h) issue_piece<C>(c, rb, st * C::STAGE, tl, h);
+  }
+  wait_barrier<C::P * (NS - 1)>();
+  Frag A0[MB], B0[NB], A1[MB], B1[NB];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+    for (int i = 0; i < MB; ++i) A0[i].k[ks] = frag_a(smem, c.aoff[ks], i);
+#pragma unroll
+    for (int j = 0; j < NB; ++j) B0[j].k[ks] = frag_b<C>(smem, c.boff[j], ks);
+  }
+  // Steady state: K-tile t computes from set (t & 1), reads t+1 into the
+  // other set from stage (t+1) % NS, refills stage t % NS with tile t + NS.
+  int t = 0;
+  for (; t + 1 < nk; t += 2) {
+    ktile<DT, C>(c, smem, t, (uint32_t)((t % NS) * C::STAGE), (uint32_t)(((t + 1) % NS) * C::STAGE),
+                 acc, A0, B0, A1, B1);
+    ktile<DT, C>(c, smem, t + 1, (uint32_t)(((t + 1) % NS) * C::STAGE),
+                 (uint32_t)(((t + 2) % NS) * C::STAGE), acc, A1, B1, A0, B0);
+  }
+  if (t < nk)  // odd count: the last tile's "next" reads are clamped re-reads
+    ktile<DT, C>(c, smem, t, (uint32_t)((t % NS) * C::STAGE), (uint32_t)((t % NS) * C::STAGE), acc,
+                 A0, B0, A1, B1);
+  // Drain the tail DMAs and give the last MFMAs time to write their AGPRs
+  // (asm MFMAs are invisible to hipcc's hazard recognizer).
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+
+  SplitSlots sl;
+  const bool split = a.splitk > 1;
+  if (split && !splitk_meet<MB, NB, NT>(a, smem, ((long long)bz * a.tiles_m + tm) * a.tiles_n + tn,
+                                        slice, acc, sl))
+    return;
+
+  // Epilogue: acc[i][j] holds C^T of a 16x16 block: lane owns row l16 and
+  // columns 4g..4g+3 (interior tiles only: no masks).
+  char* Cb = (char*)a.C + (long long)bz * a.sC * 2;
+#pragma unroll
+  for (int i = 0; i < MB; ++i) {
+    f32x4 v[NB];
+    if (!split) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) v[j] = acc[i][j];
+    } else {
+      splitk_row<MB, NB, NT>(a, sl, slice, i, acc, v);
+    }
+    const int row = m0 + wr * (C::BM / 2) + i * 16 + l16;
+    char* crow = Cb + (long long)row * a.ldc * 2;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int col = n0 + wc * (C::BN / 2) + j * 16 + 4 * g;
+      u32x2 w;
+      w.x = pack2<DT>(v[j].x, v[j].y);
+      w.y = pack2<DT>(v[j].z, v[j].w);
+      *(u32x2*)(crow + col * 2) = w;
+    }
+  }
+}
+
+template <class C>
+hipError_t launch(int dt, GemmArgs a, hipStream_t stream) {
+  a.tiles_m = a.M / C::BM;
+  a.tiles_n = a.N / C::BN;
+  const int S = a.splitk > 1 ? a.splitk : 1;
+  if (S > 1) {
+    const int nk = a.K / BK;
+    a.kt_per = (nk + S - 1) / S;
+    if ((S - 1) * a.kt_per >= nk || !a.part || !a.flags ||
+        (long long)a.tiles_m * a.tiles_n * a.batch > kMaxSplitTiles)
+      return hipErrorInvalidValue;  // every slice must own >= 1 K-tile
+  } else {
+    a.splitk = 1;
+  }
+  a.supertile = choose_supertile(a.tiles_m, a.tiles_n);
+  const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch * S;
+  if (nblocks <= 0) return hipSuccess;
+  if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)nblocks), block(NT);
+  if (dt == kBF16)
+    hipLaunchKernelGGL((gemm_tile_nn<kBF16, C>), grid, block, 0, stream, a);
+  else
+    hipLaunchKernelGGL((gemm_tile_nn<kF16, C>), grid, block, 0, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace ktile
+
+// bm x 128 tiles (bm = 128 or 256).
+bool gemm_tile_supported(int dt, int bm, const GemmArgs& a, size_t align_a, size_t align_b,
+                         size_t align_c) {
+  if (dt != kBF16 && dt != kF16) return false;
+  if (a.M <= 0 || a.N <= 0 || a.K <= 0) return false;
+  if (a.M % bm || a.N % 128 || a.K % 64) return false;
+  if (a.lda % 8 || a.ldb % 8 || a.ldc % 4) return false;
+  if (a.lda < a.K || a.ldb < a.N || a.ldc < a.N) return false;
+  if (a.batch > 1 && (a.sA % 8 || a.sB % 8 || a.sC % 4)) return false;
+  if (align_a % 16 || align_b % 16 || align_c % 8) return false;
+  // 32-bit offsets: A rows up to bm-1 * lda (+ K bytes of the tile offset),
+  // B rows up to 63 * ldb.
+  if ((long long)bm * a.lda * 2 + (long long)a.K * 2 >= (1LL << 31)) return false;
+  if ((long long)64 * a.ldb * 2 + 64 >= (1LL << 31)) return false;
+  return true;
+}
+
+// kernel: kT128 | kT128x2 | kT256x128
+hipError_t gemm_tile_launch(int kernel, int dt, GemmArgs a, hipStream_t stream) {
+  switch (kernel) {
+    case kT128: return ktile::launch<ktile::CfgT128>(dt, a, stream);
+    case kT128x2: return ktile::launch<ktile::CfgT128x2>(dt, a, stream);
+    case kT256x128: return ktile::launch<ktile::CfgT256x128>(dt, a, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace pdmb

@@ -346,7 +346,7 @@ def test_thin_grid_supertiles_exact(M, N, batch, kernel, dtype):
 # ---- under-filled grids: T128 (128x128 tiles) and W4 / T128 split-K ----
 # (matrix_parallel column shards at ws >= 4: 4096 x 512, 8192 x 1024; 2048^3)
 
-@pytest.mark.parametrize("kernel", ["w4", "t128", "t128x2"])
+@pytest.mark.parametrize("kernel", ["w4", "t256x128", "t128", "t128x2"])
 @pytest.mark.parametrize("M,N,K,b,splitk", [
     (2048, 2048, 2048, 1, 0), (4096, 512, 4096, 1, 0), (8192, 1024, 8192, 1, 2),
     (1024, 1024, 4096, 1, 2), (1024, 1024, 4096, 1, 4), (1024, 1024, 4096, 1, 8),
@@ -359,6 +359,8 @@ def test_whole_tile_kernels_exact(kernel, M, N, K, b, splitk, dtype):
     last of 4 slices one K-tile; K = 64 is a one-K-tile prologue/tail)."""
     if kernel == "w4" and (M % 256 or N % 256):
         pytest.skip("W4 needs M, N % 256")
+    if kernel == "t256x128" and M % 256:
+        pytest.skip("T256x128 needs M % 256")
     dt = DT[dtype]
     g = torch.Generator(device="cuda").manual_seed(M + N + K + splitk)
     A = torch.randint(-3, 4, (b, M, K), device="cuda", generator=g).to(dt)
@@ -383,15 +385,17 @@ def test_auto_plan_for_shard_shapes():
         return gemm.kernel_for(A, B), gemm.splitk_for(A, B)
     assert plan(16384, 16384, 16384) == ("pdmb_w4_nn", 1)
     assert plan(16384, 2048, 16384) == ("pdmb_w4_nn", 1)
-    for shape in ((8192, 1024, 8192), (4096, 512, 4096), (2048, 2048, 2048)):
-        k, S = plan(*shape)  # more workgroups than 256x256 tiles: T128, or a split W4
-        assert k == "pdmb_t128_nn" or (k == "pdmb_w4_nn" and S > 1), (shape, k, S)
+    for shape in ((8192, 1024, 8192), (4096, 512, 4096), (2048, 2048, 2048), (4096, 2048, 4096)):
+        k, S = plan(*shape)  # more workgroups than 256x256 tiles: a smaller tile or a split W4
+        assert k in ("pdmb_t128_nn", "pdmb_t256x128_nn") or (k == "pdmb_w4_nn" and S > 1), \
+            (shape, k, S)
     assert plan(16384, 1024, 256)[1] == 1  # too little K to split
 
 
 @pytest.mark.parametrize("kernel,M,N,K,splitk", [
     ("auto", 8192, 1024, 8192, 0), ("auto", 2048, 2048, 2048, 0), ("t128", 4096, 512, 4096, 2),
-    ("w4", 4096, 512, 4096, 8), ("t128", 4096, 4096, 4096, 1)])
+    ("w4", 4096, 512, 4096, 8), ("t128", 4096, 4096, 4096, 1), ("t256x128", 4096, 2048, 4096, 1),
+    ("t256x128", 2048, 1024, 8192, 4)])
 def test_tiled_random_and_bitwise_repeatable(kernel, M, N, K, splitk):
     """Random data vs fp64, and a race screen for the LDS-DMA ring and the
     split-K meeting: the slices meet in a fixed order, so every launch is
@@ -407,14 +411,15 @@ def test_tiled_random_and_bitwise_repeatable(kernel, M, N, K, splitk):
     assert _relerr(gemm.matmul(A, B, kernel="w4", splitk=1), ref.double()) < 1e-2
 
 
-def test_t128_matches_w4_bitwise_unsplit():
+def test_tile_family_matches_w4_bitwise_unsplit():
     """Same per-output fp32 accumulation order (K-tiles ascending, 16x16x32 MFMA
-    steps): the 128x128 and 256x256 kernels agree bitwise."""
+    steps): the 128x128, 256x128 and 256x256 kernels agree bitwise."""
     torch.manual_seed(4)
     A = torch.randn(2048, 3072, device="cuda", dtype=torch.bfloat16)
     B = torch.randn(3072, 1536, device="cuda", dtype=torch.bfloat16)
-    assert torch.equal(gemm.matmul(A, B, kernel="t128", splitk=1),
-                       gemm.matmul(A, B, kernel="w4", splitk=1))
+    ref = gemm.matmul(A, B, kernel="w4", splitk=1)
+    for k in ("t128", "t128x2", "t256x128"):
+        assert torch.equal(gemm.matmul(A, B, kernel=k, splitk=1), ref), k
 
 
 def test_splitk_concurrent_streams_and_graph():
@@ -425,7 +430,7 @@ def test_splitk_concurrent_streams_and_graph():
     A = torch.randint(-3, 4, (2048, 4096), device="cuda", generator=g).to(torch.bfloat16)
     B = torch.randint(-3, 4, (4096, 1024), device="cuda", generator=g).to(torch.bfloat16)
     R = (A.double() @ B.double()).to(torch.bfloat16)
-    for kernel in ("w4", "t128"):
+    for kernel in ("w4", "t256x128", "t128"):
         s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
         outs = [torch.empty_like(R) for _ in range(8)]
         torch.cuda.synchronize()

@@ -105,21 +105,37 @@ def test_default_build_has_no_experiment_kernels(tmp_path):
     assert ks and all("gemm_fp8_w4ILi0ELi0E" in k for k in ks), sorted(ks)
 
 
-def test_t128_kernel_pipelined(tmp_path):
-    """gemm_t128.hip: no spills, 64 AGPR accumulators, 4-stage ring (128 KiB LDS),
-    one vmcnt(16)-counted barrier per K-tile and one vmcnt(0) drain before the
-    split-K epilogue."""
-    ks = _kernels("gemm_t128.hip", tmp_path)
+@pytest.mark.parametrize("cfg,lds,waitn,mfma_per_kt,pieces", [
+    ("Li128ELi128ELi4ELi1E", 4 * 32768, 16, 32, 8),    # T128: 4-stage ring
+    ("Li256ELi128ELi3ELi1E", 3 * 49152, 12, 64, 12),   # T256x128: 3-stage ring
+])
+def test_tile_family_pipelined(tmp_path, cfg, lds, waitn, mfma_per_kt, pieces):
+    """gemm_tile.hip (1 workgroup / CU members): no spills, AGPR accumulators,
+    one vmcnt(P*(NS-2))-counted barrier per K-tile, one vmcnt(0) drain before the
+    split-K epilogue, prologue + 3 unrolled K-tiles of DMA pieces, sc1 slots."""
+    ks = _kernels("gemm_tile.hip", tmp_path)
     for dt, mfma in (("ILi2E", "v_mfma_f32_16x16x32_bf16"), ("ILi1E", "v_mfma_f32_16x16x32_f16")):
-        name = [k for k in ks if "gemm_t128_nn" in k and dt in k]
+        name = [k for k in ks if "gemm_tile_nn" + dt in k and cfg in k]
         assert name, sorted(ks)
         k = ks[name[0]]
         b = k["body"]
-        assert k["spill"] == 0 and k["lds"] == 4 * 32768 and k["vgpr"] <= 256
+        assert k["spill"] == 0 and k["lds"] == lds and k["vgpr"] <= 256
         assert re.search(r"v_mfma_f32_16x16x32_\w+ a\[", b)
         loop = b[:b.find("global_atomic")]
         assert len(re.findall(r"s_waitcnt vmcnt\(0\)", loop)) == 1
-        assert len(re.findall(r"s_waitcnt vmcnt\(16\) lgkmcnt\(0\)", b)) == 3
-        assert len(re.findall(mfma, b)) == 3 * 32  # 2 unrolled K-tiles + the odd tail
-        assert len(re.findall(r"buffer_load_dwordx4 .* lds", b)) == 4 * 8 + 3 * 8
-        assert len(re.findall(r"buffer_store_dwordx4 .* sc1", b)) == 16  # split-K slots
+        assert len(re.findall(rf"s_waitcnt vmcnt\({waitn}\) lgkmcnt\(0\)", b)) == 3
+        assert len(re.findall(mfma, b)) == 3 * mfma_per_kt  # 2 unrolled K-tiles + the odd tail
+        stages = lds // (lds // {16: 4, 12: 3}[waitn])
+        assert len(re.findall(r"buffer_load_dwordx4 .* lds", b)) == (stages + 3) * pieces
+        assert len(re.findall(r"buffer_store_dwordx4 .* sc1", b)) == mfma_per_kt // 2  # slots
+
+
+def test_t128x2_two_workgroups_per_cu(tmp_path):
+    """The 2-stage T128 variant: 64 KiB LDS and <= 256 VGPR + AGPR per wave, so two
+    256-thread workgroups fit on a CU; its loop waits vmcnt(0) at every K-tile top."""
+    ks = _kernels("gemm_tile.hip", tmp_path)
+    name = [k for k in ks if "gemm_tile_nnILi2E" in k and "Li128ELi128ELi2ELi2E" in k]
+    assert name, sorted(ks)
+    k = ks[name[0]]
+    assert k["spill"] == 0 and k["lds"] == 2 * 32768 and k["vgpr"] <= 128
+    assert len(re.findall(r"s_waitcnt vmcnt\(0\) lgkmcnt\(0\)", k["body"])) == 3

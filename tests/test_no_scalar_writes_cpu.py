@@ -17,7 +17,7 @@ FORBIDDEN = re.compile(r"\b(s_store_\w+|s_atomic_\w+|s_buffer_store\w*|s_buffer_
 
 
 @pytest.mark.skipif(HIPCC is None, reason="hipcc not available")
-@pytest.mark.parametrize("src", ["gemm_w4.hip", "gemm_t128.hip", "gemm_mfma256.hip", "gemm_fp8.hip",
+@pytest.mark.parametrize("src", ["gemm_w4.hip", "gemm_tile.hip", "gemm_mfma256.hip", "gemm_fp8.hip",
                                  "gemm_f32_256.hip", "gemm_generic.hip", "gemm_dispatch.cpp"])
 def test_no_scalar_cache_writes(src, tmp_path):
     lang = ["-x", "hip"] if src.endswith(".cpp") else []
