@@ -52,7 +52,8 @@ import torch.distributed as dist  # noqa: E402
 
 from pytorch_distributed_matmul_benchmark_amd.ops import gemm  # noqa: E402
 from pytorch_distributed_matmul_benchmark_amd.parallel.overlap import (  # noqa: E402
-    BidirRing, GatherOverlap, ReduceOverlap, compute_ctx, compute_stream, gemm_chunks)
+    BidirRing, GatherOverlap, ReduceOverlap, all_gather_now, compute_ctx, compute_stream, gemm_chunks)
+from pytorch_distributed_matmul_benchmark_amd.parallel.comm import CommStream  # noqa: E402
 from pytorch_distributed_matmul_benchmark_amd.parallel.dist import (  # noqa: E402
     DistContext, all_ok, barrier, cleanup_distributed, reduce_scalar, setup_distributed)
 from pytorch_distributed_matmul_benchmark_amd.parallel.partition import (  # noqa: E402
@@ -129,7 +130,7 @@ class Workload:
             if overlap:
                 ov = GatherOverlap(n, sh.padded, ws, dev, odt,
                                    gemm_chunks(n, sh.padded, a.chunks, dt, dev),
-                                   pieces=a.comm_chunks, requested=a.chunks)
+                                   pieces=a.comm_chunks, requested=a.chunks, impl=a.allgather)
 
                 def step():
                     with compute_ctx(self.comp, self._mask):
@@ -137,11 +138,12 @@ class Workload:
                     self._join()
             else:
                 gathered = torch.empty(ws * n, sh.padded, device=dev, dtype=odt)
+                cs = CommStream(dev) if a.allgather == "direct" else None
 
                 def step():
                     self._mm(A, Bl, Cl)
                     if ws > 1:
-                        dist.all_gather_into_tensor(gathered, Cl)
+                        all_gather_now(gathered, Cl, a.allgather, cs)
             self.flops = flop_gemm
             self.global_batch, self.parallelism = 1, f"tp{ws}"
         elif mode == "ring_parallel":
@@ -361,6 +363,8 @@ def main() -> int:
     ap.add_argument("--comm-cus", type=int, default=0,
                     help="overlap: CUs kept free of GEMM workgroups for RCCL (CU-masked "
                          "compute stream; 0 = no mask)")
+    ap.add_argument("--allgather", default="rccl", choices=["rccl", "direct"],
+                    help="matrix_parallel all-gather: RCCL, or direct P2P to every peer at once")
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: torch.matmul + gloo, to exercise the multi-rank path without a GPU")

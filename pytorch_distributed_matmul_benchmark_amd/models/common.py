@@ -37,6 +37,7 @@ class Workload:
     chunks: int = 4             # overlap granularity (row chunks per GEMM)
     comm_chunks: int = 0        # matrix_parallel overlap: all-gather pieces per GEMM chunk (0: auto)
     comm_cus: int = 0           # overlap: CUs kept free of GEMM workgroups for RCCL (CU-masked stream)
+    allgather: str = "rccl"     # matrix_parallel all-gather: rccl | direct (P2P to every peer at once)
     graph: bool = False         # independent: replay the timed loop as one hipGraph
     check: bool = False         # verify the result against a float64 reference
     min_warmup_ms: float = 0.0  # extend the warm-up until this much GPU time has run (DVFS)

@@ -29,7 +29,9 @@ import torch
 import torch.distributed as dist
 
 from ..parallel.comm import current_stream
-from ..parallel.overlap import GatherOverlap, compute_ctx, compute_stream, gemm_chunks
+from ..parallel.comm import CommStream
+from ..parallel.overlap import (GatherOverlap, all_gather_now, compute_ctx, compute_stream,
+                                gemm_chunks)
 from ..parallel.dist import DistContext
 from ..parallel.partition import column_shard
 from ..utils.metrics import gemm_flops, tflops_from
@@ -77,15 +79,17 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     label = kernel_label(w, A, B_local, C_local)
     flops_local = gemm_flops(n, sh.padded, n)
     flops_total = gemm_flops(n, n, n)
-    extra = {"shard_cols": sh.padded, "overlap": bool(w.overlap)}
+    extra = {"shard_cols": sh.padded, "overlap": bool(w.overlap), "allgather": w.allgather}
 
     if not w.overlap:
         # dim-0 concatenation [ws*N, shard] (the layout both gloo and RCCL accept);
         # block r = gathered.view(ws, N, shard)[r] = C[:, r*shard:(r+1)*shard].
         gathered = torch.empty((ws * n, sh.padded), device=dev, dtype=out_dtype(w))
 
+        cs = CommStream(dev) if w.allgather == "direct" else None
+
         def comm():
-            dist.all_gather_into_tensor(gathered, C_local)
+            all_gather_now(gathered, C_local, w.allgather, cs)
 
         def serial_step():
             mm(A, B_local, C_local)
@@ -109,7 +113,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     else:
         ov = GatherOverlap(n, sh.padded, ws, dev, out_dtype(w),
                            gemm_chunks(n, sh.padded, w.chunks, w.dtype, dev),
-                           pieces=w.comm_chunks, requested=w.chunks)
+                           pieces=w.comm_chunks, requested=w.chunks, impl=w.allgather)
         extra["chunks"] = len(ov.chunks)
         extra["comm_pieces"] = ov.n_pieces
         extra["comm_cus"] = w.comm_cus

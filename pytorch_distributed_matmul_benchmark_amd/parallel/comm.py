@@ -143,6 +143,29 @@ class CommStream:
                 done.record(self.stream)
         return works
 
+    def all_gather_direct(self, out: torch.Tensor, inp: torch.Tensor, after=None, done=None):
+        """All-gather as ONE batched group of point-to-point transfers: this
+        rank's ``inp`` goes straight to every other rank and every other
+        rank's block lands straight in its slot of ``out`` ([ws * rows, ...],
+        block r = rank r's ``inp``). On a fully connected 8 x MI355X node each
+        of the ws-1 transfers has its own xGMI link, so all 7 links carry
+        data at once with no forwarding hop (RCCL's ring all-gather forwards
+        every block ws-1 times). Selected with ``--allgather direct``."""
+        group_ws = dist.get_world_size(self.group)
+        me = dist.get_rank(self.group)
+        rows = inp.shape[0]
+        blocks = [out[r * rows:(r + 1) * rows] for r in range(group_ws)]
+        with stream_ctx(self.stream):
+            if after is not None:
+                self.wait_event(after)
+            blocks[me].copy_(inp)
+        peers = [(me + d) % group_ws for d in range(1, group_ws)]
+        g = lambda r: dist.get_global_rank(self.group, r) if self.group is not None else r  # noqa: E731
+        return self.exchange_multi([(inp, g(p)) for p in peers],
+                                   [(blocks[(me - d) % group_ws], g((me - d) % group_ws))
+                                    for d in range(1, group_ws)],
+                                   after=None, done=done)
+
     def synchronize(self) -> None:
         if self.stream is not None:
             self.stream.synchronize()

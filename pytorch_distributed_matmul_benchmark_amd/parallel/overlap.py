@@ -11,7 +11,8 @@ and matmul_scaling_benchmark.py:167-238 (matrix_parallel, serialized). Here:
   8k ws=8 shard (128 tiles) now overlaps in 2 chunks instead of running
   serialized (round 1 required >= 256 tiles per chunk).
 * ``GatherOverlap`` — matrix_parallel: GEMM chunk j, then its rows are
-  all-gathered in ``pieces`` RCCL calls (independent of the GEMM chunking),
+  all-gathered in ``pieces`` calls (independent of the GEMM chunking; RCCL's
+  all_gather_into_tensor or the direct P2P all-gather, ``impl``),
   each on the comm stream after an event recorded behind chunk j; the step
   ends with the compute stream waiting for every piece (the timed region
   includes the last collective).
@@ -124,7 +125,10 @@ class GatherOverlap:
 
     def __init__(self, n_rows: int, shard: int, ws: int, device: torch.device,
                  out_dtype: torch.dtype, chunks: Sequence[Tuple[int, int]], pieces: int = 0,
-                 requested: int = 4, comm: Optional[CommStream] = None):
+                 requested: int = 4, comm: Optional[CommStream] = None, impl: str = "rccl"):
+        if impl not in ("rccl", "direct"):
+            raise ValueError(f"all-gather impl {impl!r}: rccl | direct")
+        self.impl = impl
         self.chunks = list(chunks)
         per = pieces if pieces > 0 else max(1, ceil_div(max(requested, 1), len(self.chunks)))
         self.pieces = []
@@ -145,10 +149,10 @@ class GatherOverlap:
         for j, (s, e) in enumerate(self.chunks):
             mm(A[s:e], B_local, C_local[s:e])
             self.ready[j].record(compute)
+            gather = self.cs.all_gather_direct if self.impl == "direct" else self.cs.all_gather_into
             for p, (ps, pe) in enumerate(self.pieces[j]):
-                self.cs.all_gather_into(self.bufs[j][p], C_local[ps:pe],
-                                        after=self.ready[j] if p == 0 else None,
-                                        done=self.done[j][p])
+                gather(self.bufs[j][p], C_local[ps:pe], after=self.ready[j] if p == 0 else None,
+                       done=self.done[j][p])
         if compute is not None:
             for dj in self.done:
                 compute.wait_event(dj[-1])  # comm stream is in order: last piece => all
@@ -214,3 +218,22 @@ class BidirRing:
             self.last = self.gemm_done[s]
             if s < ws - 1:
                 top, bot = self.Rt[(s + 1) % 2], self.Rb[(s + 1) % 2]
+
+
+def all_gather_now(out: torch.Tensor, inp: torch.Tensor, impl: str = "rccl",
+                   comm: Optional[CommStream] = None) -> None:
+    """Serialized all-gather on the current stream: RCCL's
+    ``all_gather_into_tensor``, or the direct P2P all-gather (every block over
+    its own link) on ``comm`` with the current stream joined behind it."""
+    import torch.distributed as dist
+
+    if impl == "rccl":
+        dist.all_gather_into_tensor(out, inp)
+        return
+    dev = inp.device
+    cur = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
+    ready, done = new_event(dev), new_event(dev)
+    ready.record(cur)
+    comm.all_gather_direct(out, inp, after=ready, done=done)
+    if cur is not None:
+        cur.wait_event(done)

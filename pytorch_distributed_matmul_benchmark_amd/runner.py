@@ -88,6 +88,10 @@ def build_parser(kind: str) -> argparse.ArgumentParser:
     g.add_argument("--chunks", type=int, default=4, help="overlap granularity (row chunks per GEMM)")
     g.add_argument("--comm-chunks", type=int, default=0,
                    help="matrix_parallel --overlap: all-gather pieces per GEMM chunk (0: auto)")
+    g.add_argument("--allgather", default="rccl", choices=["rccl", "direct"],
+                   help="matrix_parallel all-gather: RCCL's all_gather_into_tensor, or direct: one "
+                        "batched P2P group sending this rank's shard to every peer at once (each "
+                        "over its own xGMI link on a fully connected node)")
     g.add_argument("--comm-cus", type=int, default=0,
                    help="--overlap: CUs kept free of GEMM workgroups for RCCL (CU-masked "
                         "compute stream, spread over the 8 XCDs; 0 = no mask)")
@@ -127,7 +131,8 @@ def _workload(args, n: int, dtype: torch.dtype) -> Workload:
     return Workload(n=n, dtype=dtype, iters=args.iterations, warmup=args.warmup, seed=args.seed,
                     backend=args.backend, kernel=args.kernel, batch=args.batch,
                     overlap=args.overlap, chunks=args.chunks, comm_chunks=args.comm_chunks,
-                    comm_cus=args.comm_cus, graph=args.graph, check=args.check,
+                    comm_cus=args.comm_cus, allgather=args.allgather, graph=args.graph,
+                    check=args.check,
                     min_warmup_ms=args.min_warmup_ms)
 
 

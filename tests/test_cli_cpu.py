@@ -191,3 +191,15 @@ def test_fp8_cli_cpu_and_gloo(tmp_path):
                         "--iterations", "2", "--warmup", "1", "--dtype", "float8_e4m3fn",
                         "--mode", mode, "--overlap", "--chunks", "2", "--check")
         assert out.count("PASS") == 1 and "FAIL" not in out and "ERROR" not in out
+
+
+@pytest.mark.parametrize("ws,extra", [(2, []), (3, ["--overlap", "--chunks", "2", "--comm-chunks", "2"]),
+                                      (4, ["--overlap", "--chunks", "3"])])
+def test_matrix_parallel_direct_allgather(ws, extra):
+    """--allgather direct: the shard goes to every peer in one batched P2P group
+    (each over its own link on a fully connected node); the gathered C is checked
+    against the float64 product, serialized and overlapped."""
+    out = _torchrun(ws, "matmul_scaling_benchmark.py", "--device", "cpu", "--sizes", "300",
+                    "--iterations", "2", "--warmup", "1", "--dtype", "float32", "--mode",
+                    "matrix_parallel", "--allgather", "direct", "--check", *extra)
+    assert "PASS" in out and "FAIL" not in out and "ERROR" not in out

@@ -32,6 +32,9 @@ def test_native_extension_is_loaded():
 FAST = ["mfma256d", "mfma256", "mfma256b", "mfma256c"]
 
 
+TILED = ("pdmb_w4_nn", "pdmb_t256x128_nn", "pdmb_t128_nn", "pdmb_t128x2_nn")
+
+
 def _need(kernel):
     """Skip an experiment-kernel case on the default (shipping) build."""
     if kernel in gemm.EXPERIMENT_KERNELS and not gemm.experiments_built():
@@ -292,8 +295,8 @@ def test_w4_exact_small_integers(dtype, b, M, N, K, pad):
     B = torch.randint(-3, 4, (b, K, N + pad), device="cuda", generator=g).to(dt)[..., :N]
     if b == 1:
         A, B = A[0], B[0]
-    # auto picks a whole-tile kernel (W4, or T128 for these under-filled grids)
-    assert gemm.kernel_for(A, B) in ("pdmb_w4_nn", "pdmb_t128_nn")
+    # auto picks a whole-tile kernel (W4, or a smaller tile for these under-filled grids)
+    assert gemm.kernel_for(A, B) in TILED
     C = gemm.matmul(A, B, kernel="w4")
     assert torch.equal(C, (A.double() @ B.double()).to(dt))
 
@@ -387,8 +390,7 @@ def test_auto_plan_for_shard_shapes():
     assert plan(16384, 2048, 16384) == ("pdmb_w4_nn", 1)
     for shape in ((8192, 1024, 8192), (4096, 512, 4096), (2048, 2048, 2048), (4096, 2048, 4096)):
         k, S = plan(*shape)  # more workgroups than 256x256 tiles: a smaller tile or a split W4
-        assert k in ("pdmb_t128_nn", "pdmb_t256x128_nn") or (k == "pdmb_w4_nn" and S > 1), \
-            (shape, k, S)
+        assert k in TILED[1:] or (k == "pdmb_w4_nn" and S > 1), (shape, k, S)
     assert plan(16384, 1024, 256)[1] == 1  # too little K to split
 
 
