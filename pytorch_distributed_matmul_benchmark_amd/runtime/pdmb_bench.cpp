@@ -59,6 +59,7 @@ struct Opts {
   Mode mode = kIndependent;
   int batch = 4, chunks = 4, kernel = 0;
   bool overlap = false, check = false;
+  bool direct = false;  // --allgather direct: P2P to every peer in one group (own link each)
   std::string json;
 };
 
@@ -546,11 +547,31 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
       done.push_back(event());
     }
     std::vector<bool> used(rcs.size(), false);
+    // All-gather `count` elements per rank from `send` into `recv` (rank-major):
+    // RCCL's ring/channel algorithm, or --allgather direct: this rank's block
+    // sent straight to every peer and every peer's block received straight
+    // into its slot, all in one group (on a fully connected node each
+    // transfer has its own xGMI link; no forwarding hops).
+    auto allgather = [&](const void* send, char* recv, size_t count, hipStream_t s) {
+      if (!o.direct) {
+        NCCL_OK(ncclAllGather(send, recv, count, nccl_type(dt), comm, s));
+        return;
+      }
+      const size_t bytes = count * es;
+      HIP_OK(hipMemcpyAsync(recv + (size_t)rank * bytes, send, bytes, hipMemcpyDeviceToDevice, s));
+      NCCL_OK(ncclGroupStart());
+      for (int d = 1; d < ws; ++d) {
+        const int to = (rank + d) % ws, from = (rank - d + ws) % ws;
+        NCCL_OK(ncclSend(send, count, nccl_type(dt), to, comm, s));
+        NCCL_OK(ncclRecv(recv + (size_t)from * bytes, count, nccl_type(dt), from, comm, s));
+      }
+      NCCL_OK(ncclGroupEnd());
+    };
     auto iter = [&](hipEvent_t em) {
       if (!o.overlap) {
         gemm(p, o.kernel, st);
         if (em) HIP_OK(hipEventRecord(em, st));
-        NCCL_OK(ncclAllGather(Cl.p, G.p, (size_t)n * shard, nccl_type(dt), comm, st));
+        allgather(Cl.p, (char*)G.p, (size_t)n * shard, st);
         return;
       }
       for (size_t j = 0; j < rcs.size(); ++j) {
@@ -561,7 +582,7 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
         gemm(problem(dt, a, Bl.p, c, r1 - r0, shard, n, n, shard, shard), o.kernel, st);
         HIP_OK(hipEventRecord(ready[j], st));
         HIP_OK(hipStreamWaitEvent(cs, ready[j], 0));
-        NCCL_OK(ncclAllGather(c, gb[j], (size_t)(r1 - r0) * shard, nccl_type(dt), comm, cs));
+        allgather(c, gb[j], (size_t)(r1 - r0) * shard, cs);
         HIP_OK(hipEventRecord(done[j], cs));
         used[j] = true;
       }
@@ -653,7 +674,8 @@ void usage() {
   std::printf(
       "pdmb_bench [--gpus N] [--sizes N ...] [--iterations I] [--warmup W]\n"
       "           [--dtype bfloat16|float16|float32] [--mode independent|batch_parallel|matrix_parallel|ring_parallel]\n"
-      "           [--batch B] [--overlap] [--chunks C] [--kernel ID] [--check] [--json FILE]\n");
+      "           [--batch B] [--overlap] [--chunks C] [--allgather rccl|direct] [--kernel ID]\n"
+      "           [--check] [--json FILE]\n");
 }
 
 Opts parse(int argc, char** argv) {
@@ -671,6 +693,7 @@ Opts parse(int argc, char** argv) {
     else if (a == "--chunks") o.chunks = std::stoi(next());
     else if (a == "--kernel") o.kernel = std::stoi(next());
     else if (a == "--overlap") o.overlap = true;
+    else if (a == "--allgather") o.direct = next() == "direct";
     else if (a == "--check") o.check = true;
     else if (a == "--json") o.json = next();
     else if (a == "--dtype") {

@@ -70,7 +70,9 @@ def test_two_ranks_share_gpu_bench_ring():
 @pytest.mark.parametrize("mode,extra", [
     ("matrix_parallel", ["--overlap", "--chunks", "4", "--comm-chunks", "3", "--comm-cus", "16"]),
     ("batch_parallel", ["--overlap", "--chunks", "2", "--comm-cus", "32"]),
-    ("matrix_parallel", ["--overlap", "--chunks", "1", "--comm-chunks", "4"])])
+    ("matrix_parallel", ["--overlap", "--chunks", "1", "--comm-chunks", "4"]),
+    ("matrix_parallel", ["--allgather", "direct"]),
+    ("matrix_parallel", ["--allgather", "direct", "--overlap", "--chunks", "2", "--comm-chunks", "2"])])
 def test_two_ranks_cu_masked_overlap_checked(mode, extra):
     """GEMM chunks on a CU-masked stream, collectives in pieces decoupled from the
     GEMM chunking: the float64 Σ-over-ranks / gathered-C checks still pass."""

@@ -23,6 +23,8 @@ def exe():
                                         ("batch_parallel", ["--overlap"]),
                                         ("matrix_parallel", []),
                                         ("matrix_parallel", ["--overlap"]),
+                                        ("matrix_parallel", ["--allgather", "direct"]),
+                                        ("matrix_parallel", ["--overlap", "--allgather", "direct"]),
                                         ("ring_parallel", [])])
 @pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
 def test_native_executor_modes(exe, mode, extra, dtype, tmp_path):
