@@ -20,6 +20,7 @@ hipError_t gemm256_launch(int dt, GemmArgs a, int sched, hipStream_t stream);
 hipError_t gemm_generic_launch(int dt, GemmArgs a, bool vec, hipStream_t stream);
 bool gemm_f32_256_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 hipError_t gemm_f32_256_launch(GemmArgs a, int variant, hipStream_t stream);
+hipError_t gemm_f32_w4_launch(GemmArgs a, hipStream_t stream);
 bool gemm_fp8_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream);
 bool gemm_w4_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
@@ -124,6 +125,7 @@ int resolve_kernel(const Problem& p, int kernel) {
     case kT128x2: return t128 ? kT128x2 : -1;  // shares T128's constraints
     case kT256x128: return t256 ? kT256x128 : -1;
     case kF32_256s: return f32fast ? kF32_256s : -1;
+    case kF32W4: return f32fast ? kF32W4 : -1;  // same constraints as f32_256
 #ifdef PDMB_EXPERIMENTS
     case kF32_256: case kF32NoDma: return f32fast ? kernel : -1;
     case kMfma256: case kMfma256b: case kMfma256c: return fast ? kernel : -1;
@@ -507,6 +509,7 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kT128x2:
     case kT256x128: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream);
     case kF32_256s: return gemm_f32_256_launch(a, 1, stream);
+    case kF32W4: return gemm_f32_w4_launch(a, stream);
 #ifdef PDMB_EXPERIMENTS
     case kFp8: return gemm_fp8_launch(a, 0, stream);
     case kFp8W4Diag: return gemm_fp8_launch(a, 9, stream);
@@ -605,6 +608,7 @@ const char* kernel_name(int kernel) {
     case kT128: return "pdmb_t128_nn";
     case kT128x2: return "pdmb_t128x2_nn";
     case kT256x128: return "pdmb_t256x128_nn";
+    case kF32W4: return "pdmb_f32_w4_nn";
     case kMfma256: return "pdmb_mfma256_nn";
     case kMfma256b: return "pdmb_mfma256b_nn";
     case kMfma256c: return "pdmb_mfma256c_nn";

@@ -1,0 +1,231 @@
+// gemm_f32_w4.hip — exact-fp32 C = A @ B (row-major NN) on v_mfma_f32_16x16x4_f32
+// with W4's structure: 4 waves per 256x256 workgroup, one per SIMD, each
+// owning 128x128 outputs in 256 AGPR accumulators.
+//
+// Why: gemm_f32_256.hip (8 waves x 128x64, 2 waves per SIMD) reaches 148 TF at
+// 16k, 95 % MFMA busy at 2.38 GHz — fp32 MFMA is not power-bound — while
+// hipBLASLt's one-wave-per-SIMD 128x128-per-wave kernel is 98.7 % busy
+// (154 TF, profiles/r1_fp32_ablation.md). Round 1 could not build that shape:
+// hipcc spilled and broke the accumulator chains. Here, as in gemm_w4.hip,
+// the MFMAs are inline asm on "+a" accumulator operands, so the 256
+// accumulators stay in AGPRs and the operands in VGPRs.
+//
+// Layout (gemm_f32_256.hip's conflict-free images, unchanged):
+//  * A [256 rows][32 fp32 = 128 B], 16-B chunk c of row r at c ^ ((r >> 1) & 7);
+//    one ds_read_b128 gives a lane 4 consecutive k of its row, so MFMA e of a
+//    16-k block uses k = 16 kb + 4 g + e in lane group g (a k-permutation).
+//  * B [32 k][260 fp32] (1040-B rows; the pad puts k-rows 4 apart on opposite
+//    bank halves): the matching B element is ds_read_b32 of B[16 kb + 4 g + e][col].
+//  * 2 stages x 66,048 B, filled by LDS-DMA (buffer_load ... lds): per K-tile
+//    32 A pieces (8 rows x 128 B) + 32 B pieces (one k-row) = 16 per wave.
+// Schedule per K-tile t (stage s = t & 1):
+//    s_waitcnt vmcnt(0) lgkmcnt(0); s_barrier   (t landed; t-1's stage free)
+//    read half 0's fragments (8 b128 + 32 b32) from s
+//    512 MFMAs (2 halves x 4 e x 8 m x 8 n, 32 cycles each = ~7 us) with, in
+//    their gaps, the 16 DMA pieces of tile t+1 into s ^ 1 (all in the first
+//    quarter, so they land long before the next barrier) and half 1's
+//    fragment reads (during half 0).
+// Operands swapped (B element as the MFMA's A) so each lane owns 4
+// consecutive output columns -> 16-B stores. Edges: the DMA descriptors'
+// extents read zeros past M / N / K, the stores are masked, so any M and
+// N % 4 == 0 runs here (the host checks K % 32, alignment).
+#include "common.h"
+
+namespace pdmb {
+namespace kf32w4 {
+
+constexpr int BM = 256, BN = 256, BK = 32, NT = 256;
+constexpr int A_BYTES = BM * BK * 4;      // 32 KiB
+constexpr int B_PITCH = (BN + 4) * 4;     // 1040 B per k-row
+constexpr int B_BYTES = BK * B_PITCH;     // 33,280 B
+constexpr int STAGE = A_BYTES + B_BYTES;  // 66,048 B (16-B multiple)
+constexpr int LDS_BYTES = 2 * STAGE;      // 132,096 B
+
+__device__ __forceinline__ void mfma(f32x4& acc, float b, float a) {
+  asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+}
+
+// LDS-DMA with a scalar offset; M0 is clobbered (declared), not saved.
+__device__ __forceinline__ void dma16_m0(u32x4 rsrc, uint32_t voff, uint32_t soff, uint32_t lds) {
+  asm volatile(
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %0, %1, %2 offen lds"
+      :
+      : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds)
+      : "memory", "m0");
+}
+
+struct Ctx {
+  const char* Ab;
+  const char* Bb;
+  long long a_bytes, b_bytes;
+  int lda4, ldb4, nk, wu;
+  uint32_t voffA, voffB;
+  uint32_t lds0;
+};
+
+struct Half {  // fragments of one 16-k block: A rows (4 k each) and B elements
+  f32x4 a[8];
+  float b[8][4];
+};
+
+// DMA piece h (0..15) of K-tile `tile` into stage `stg`: h < 8: A rows
+// (h*4 + wu)*8 + [0,8) (8 x 128 B); h >= 8: B k-row (h-8)*4 + wu (1 KiB).
+// A's swizzle depends on (r >> 1) & 7, which the h*32-row offset keeps.
+__device__ __forceinline__ void issue_piece(const Ctx& c, u32x4 ra, u32x4 rb, int stg, int h) {
+  if (h < 8) {
+    dma16_m0(ra, c.voffA, (uint32_t)(h * 32 * c.lda4),
+             c.lds0 + stg * STAGE + ((h * 4 + c.wu) * 8) * 128);
+  } else {
+    const int kr = (h - 8) * 4 + c.wu;
+    dma16_m0(rb, c.voffB, (uint32_t)((h - 8) * 4 * c.ldb4), c.lds0 + stg * STAGE + A_BYTES + kr * B_PITCH);
+  }
+}
+
+// Fragment reads of 16-k block kb from stage stg. mi / ni index the wave's
+// 8 row blocks / 8 column blocks; each is issued separately so the schedule
+// can place it in an MFMA gap.
+__device__ __forceinline__ f32x4 read_a(const char* smem, int stg, int kb, int mi, int wr, int l16,
+                                        int g) {
+  const int r = wr * 128 + mi * 16 + l16;
+  const int ch = (kb * 4 + g) ^ ((r >> 1) & 7);
+  return *(const f32x4*)(smem + stg * STAGE + r * 128 + ch * 16);
+}
+__device__ __forceinline__ float read_b(const char* smem, int stg, int kb, int ni, int e, int wc,
+                                        int l16, int g) {
+  const int k = kb * 16 + 4 * g + e;
+  const int col = wc * 128 + ni * 16 + l16;
+  return *(const float*)(smem + stg * STAGE + A_BYTES + k * B_PITCH + col * 4);
+}
+
+// One 16-k half: 256 MFMAs from `cur`; in their gaps read the other half's
+// fragments into `nxt` (kb_next >= 0) and issue DMA pieces [p0, p0 + np) of
+// the next tile (one per 4 MFMAs from the start).
+__device__ __forceinline__ void half_step(const Ctx& c, const char* smem, f32x4 (&acc)[8][8],
+                                          const Half& cur, Half& nxt, int stg_rd, int kb_next,
+                                          int wr, int wc, int l16, int g, u32x4 ra, u32x4 rb,
+                                          int stg_dma, int p0, int np) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 8; ++ni) {
+        const int gap = (e * 8 + mi) * 8 + ni;  // 0..255
+        mfma(acc[mi][ni], cur.b[ni][e], cur.a[mi][e]);
+        if (gap % 4 == 3 && gap / 4 < np) {
+          issue_piece(c, ra, rb, stg_dma, p0 + gap / 4);
+        } else if (kb_next >= 0 && gap % 4 == 1 && gap / 4 < 40) {
+          // 40 reads: 8 A rows (b128) then 32 B elements (b32), one per 4 MFMAs
+          const int q = gap / 4;
+          if (q < 8) {
+            nxt.a[q] = read_a(smem, stg_rd, kb_next, q, wr, l16, g);
+          } else {
+            const int e2 = (q - 8) >> 3, ni2 = (q - 8) & 7;
+            nxt.b[ni2][e2] = read_b(smem, stg_rd, kb_next, ni2, e2, wc, l16, g);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+}
+
+__global__ void __launch_bounds__(NT, 1) gemm_f32_w4(GemmArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+
+  int bz, tm, tn;
+  map_tile(a, blockIdx.x, bz, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int lane = threadIdx.x & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wu >> 1, wc = wu & 1;
+  const int l16 = lane & 15, g = lane >> 4;
+
+  Ctx c;
+  c.wu = wu;
+  c.lds0 = (uint32_t)(size_t)((lds_void*)smem);
+  c.lda4 = a.lda * 4;
+  c.ldb4 = a.ldb * 4;
+  c.nk = a.K / BK;
+  c.Ab = (const char*)a.A + ((long long)bz * a.sA + (long long)m0 * a.lda) * 4;
+  c.Bb = (const char*)a.B + ((long long)bz * a.sB + n0) * 4;
+  c.a_bytes = ((long long)(a.M - m0 - 1) * a.lda + a.K) * 4;
+  c.b_bytes = ((long long)(a.K - 1) * a.ldb + (a.N - n0)) * 4;
+  {
+    const int r = wu * 8 + (lane >> 3);  // row of A piece 0
+    c.voffA = (uint32_t)(r * c.lda4 + (((lane & 7) ^ ((r >> 1) & 7)) * 16));
+    c.voffB = (uint32_t)(wu * c.ldb4 + lane * 16);  // k-row wu of piece 8
+  }
+  auto rsrc_a = [&](int tile) {
+    const long long off = (long long)tile * BK * 4;
+    return make_rsrc(c.Ab + off, c.a_bytes - off);
+  };
+  auto rsrc_b = [&](int tile) {
+    const long long off = (long long)tile * BK * c.ldb4;
+    return make_rsrc(c.Bb + off, c.b_bytes - off);
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = c.nk;
+  {
+    const u32x4 ra = rsrc_a(0), rb = rsrc_b(0);
+#pragma unroll
+    for (int h = 0; h < 16; ++h) issue_piece(c, ra, rb, 0, h);
+  }
+  Half h0, h1;
+  for (int t = 0; t < nk; ++t) {
+    const int s = t & 1;
+    // Tile t landed (its DMA is the only one outstanding); every wave is done
+    // reading stage s ^ 1 (tile t-1), which tile t+1 now refills.
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) h0.a[mi] = read_a(smem, s, 0, mi, wr, l16, g);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)  // in the order the MFMAs consume them
+#pragma unroll
+      for (int ni = 0; ni < 8; ++ni) h0.b[ni][e] = read_b(smem, s, 0, ni, e, wc, l16, g);
+    const bool more = t + 1 < nk;
+    const int tn1 = more ? t + 1 : t;  // the last tile issues nothing (np = 0)
+    const u32x4 ra = rsrc_a(tn1), rb = rsrc_b(tn1);
+    half_step(c, smem, acc, h0, h1, s, 1, wr, wc, l16, g, ra, rb, s ^ 1, 0, more ? 16 : 0);
+    half_step(c, smem, acc, h1, h0, s, -1, wr, wc, l16, g, ra, rb, s ^ 1, 0, 0);
+  }
+  // Give the last MFMAs time to write their AGPRs (asm MFMAs are invisible to
+  // hipcc's hazard recognizer).
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+
+  float* Cb = (float*)a.C + (long long)bz * a.sC;
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    const int row = m0 + wr * 128 + mi * 16 + l16;
+    if (row < a.M) {
+      float* crow = Cb + (long long)row * a.ldc;
+#pragma unroll
+      for (int ni = 0; ni < 8; ++ni) {
+        const int col = n0 + wc * 128 + ni * 16 + 4 * g;
+        if (col < a.N) *(f32x4*)(crow + col) = acc[mi][ni];
+      }
+    }
+  }
+}
+
+}  // namespace kf32w4
+
+hipError_t gemm_f32_w4_launch(GemmArgs a, hipStream_t stream) {
+  a.tiles_m = (a.M + kf32w4::BM - 1) / kf32w4::BM;
+  a.tiles_n = (a.N + kf32w4::BN - 1) / kf32w4::BN;
+  a.supertile = choose_supertile(a.tiles_m, a.tiles_n);
+  const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch;
+  if (nblocks <= 0) return hipSuccess;
+  if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(kf32w4::gemm_f32_w4, dim3((unsigned)nblocks), dim3(kf32w4::NT), 0, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace pdmb

@@ -202,13 +202,13 @@ def test_race_screen_repeated_runs(kernel):
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 32), (512, 768, 96), (1000, 1052, 320),
                                    (300, 200, 64), (2304, 2048, 1024)])
-@pytest.mark.parametrize("kernel", ["f32_256", "f32_256s"])
+@pytest.mark.parametrize("kernel", ["f32_256", "f32_256s", "f32_w4"])
 def test_f32_256_exact_and_random(M, N, K, kernel):
     _need(kernel)
     g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
     A = torch.randint(-3, 4, (M, K), device="cuda", generator=g).float()
     B = torch.randint(-3, 4, (K, N), device="cuda", generator=g).float()
-    assert gemm.kernel_for(A, B, kernel=kernel).startswith("pdmb_f32_256")
+    assert gemm.kernel_for(A, B, kernel=kernel).startswith(("pdmb_f32_256", "pdmb_f32_w4"))
     C = gemm.matmul(A, B, kernel=kernel)
     assert torch.equal(C.double(), _ref(A, B))  # small integers: exact in fp32
     A = torch.randn(M, K, device="cuda", generator=g)
@@ -234,7 +234,7 @@ def test_f32_256_identity_batched_and_shards():
         assert _relerr(gemm.matmul(Af, Bs), _ref(Af, Bs)) < TOL[torch.float32]
 
 
-@pytest.mark.parametrize("kernel", ["f32_256", "f32_256s"])
+@pytest.mark.parametrize("kernel", ["f32_256", "f32_256s", "f32_w4"])
 def test_f32_256_race_screen(kernel):
     _need(kernel)
     torch.manual_seed(11)
@@ -328,7 +328,8 @@ def test_w4_rejects_edge_tiles_and_auto_falls_back():
                                        (8192, 2048, 3), (4096, 2048, 1),
                                        (1024, 16384, 1), (16384, 1024, 1), (1024, 16384, 2)])
 @pytest.mark.parametrize("kernel,dtype", [("w4", "bfloat16"), ("w4", "float16"),
-                                          ("mfma256d", "bfloat16"), ("f32_256s", "float32")])
+                                          ("mfma256d", "bfloat16"), ("f32_256s", "float32"),
+                                          ("f32_w4", "float32")])
 def test_thin_grid_supertiles_exact(M, N, batch, kernel, dtype):
     """Every output tile is written exactly once under the thin-grid block->tile
     maps (a mis-mapping leaves stale tiles or duplicates): integer data, exact
