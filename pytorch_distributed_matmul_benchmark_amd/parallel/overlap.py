@@ -104,6 +104,9 @@ def compute_ctx(stream, owner):
 
     if owner is None:
         return stream_ctx(stream)
+    # the masked stream starts behind everything already queued on the
+    # caller's stream (operand initialisation, the previous step's join)
+    stream.wait_stream(torch.cuda.current_stream(owner.device))
     st = contextlib.ExitStack()
     st.enter_context(stream_ctx(stream))
     st.enter_context(owner.budget())
