@@ -155,7 +155,8 @@ int resolve_kernel(const Problem& p, int kernel) {
 //           writes and the last reads back an fp32 tile slab,
 //           T * (S-1) * 2 * BM * BN * 4 B / kSlabBw + kMeetUs.
 // kt per K-tile at full occupancy (us, random bf16, profiles/r2_*sweep*.jsonl):
-// W4 1.42, T128 0.46, T128x2 0.86 per pair of co-resident workgroups. The fit
+// W4 1.42, T256x128 0.87 (16k: 1187 vs 1438 TF for W4 on one box), T128 0.46,
+// T128x2 0.86 per pair of co-resident workgroups. The fit
 // reproduces the measured times of the shard shapes within ~10 %.
 struct KernelModel {
   int kernel, bm, bn, occ;
@@ -163,7 +164,7 @@ struct KernelModel {
 };
 static constexpr KernelModel kModels[] = {
     {kMfmaW4, 256, 256, 1, 1.42},
-    {kT256x128, 256, 128, 1, 0.78},
+    {kT256x128, 256, 128, 1, 0.87},
     {kT128, 128, 128, 1, 0.46},
     {kT128x2, 128, 128, 2, 0.86},
 };

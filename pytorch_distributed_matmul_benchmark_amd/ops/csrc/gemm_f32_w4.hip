@@ -18,13 +18,14 @@
 //    bank halves): the matching B element is ds_read_b32 of B[16 kb + 4 g + e][col].
 //  * 2 stages x 66,048 B, filled by LDS-DMA (buffer_load ... lds): per K-tile
 //    32 A pieces (8 rows x 128 B) + 32 B pieces (one k-row) = 16 per wave.
-// Schedule per K-tile t (stage s = t & 1):
-//    s_waitcnt vmcnt(0) lgkmcnt(0); s_barrier   (t landed; t-1's stage free)
-//    read half 0's fragments (8 b128 + 32 b32) from s
-//    512 MFMAs (2 halves x 4 e x 8 m x 8 n, 32 cycles each = ~7 us) with, in
-//    their gaps, the 16 DMA pieces of tile t+1 into s ^ 1 (all in the first
-//    quarter, so they land long before the next barrier) and half 1's
-//    fragment reads (during half 0).
+// Schedule per K-tile t (stage s = t & 1): 512 MFMAs (2 halves x 4 e x 8 m
+// x 8 n, 32 cycles each = ~7 us) from registers; during half 0 the wave
+// reads half 1's fragments of t; then ONE barrier mid-tile (vmcnt(0): tile
+// t+1 landed; lgkmcnt(0): done reading s); during half 1 it refills s with
+// tile t+2 (16 DMA pieces, so each tile has a whole tile of flight) and reads
+// half 0 of tile t+1 from s ^ 1. No wave waits at a tile boundary and no LDS
+// read latency is exposed (round 2's first version waited at the top of each
+// tile and ran 1 % behind f32_256s).
 // Operands swapped (B element as the MFMA's A) so each lane owns 4
 // consecutive output columns -> 16-B stores. Edges: the DMA descriptors'
 // extents read zeros past M / N / K, the stores are masked, so any M and
@@ -171,30 +172,47 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4(GemmArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // Prologue: tiles 0 and 1 into stages 0 and 1; tile 0 landed everywhere;
+  // half 0 of tile 0 to registers.
   const int nk = c.nk;
   {
     const u32x4 ra = rsrc_a(0), rb = rsrc_b(0);
 #pragma unroll
     for (int h = 0; h < 16; ++h) issue_piece(c, ra, rb, 0, h);
   }
+  if (nk > 1) {
+    const u32x4 ra = rsrc_a(1), rb = rsrc_b(1);
+#pragma unroll
+    for (int h = 0; h < 16; ++h) issue_piece(c, ra, rb, 1, h);
+    asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
   Half h0, h1;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {  // in the order the MFMAs consume them
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+      if (e == 0) h0.a[mi] = read_a(smem, 0, 0, mi, wr, l16, g);
+#pragma unroll
+    for (int ni = 0; ni < 8; ++ni) h0.b[ni][e] = read_b(smem, 0, 0, ni, e, wc, l16, g);
+  }
+  // K-tile t (stage s = t & 1; tile t+1 in s ^ 1 was issued a tile ago):
+  //   half 0: MFMAs from h0 | read half 1 of t from s into h1
+  //   mid-tile: vmcnt(0) (t+1 landed) lgkmcnt(0) (this wave done reading s),
+  //             s_barrier — so nobody waits at the top of a tile
+  //   half 1: MFMAs from h1 | DMA tile t+2 into s | read half 0 of t+1 from
+  //           s ^ 1 into h0
   for (int t = 0; t < nk; ++t) {
     const int s = t & 1;
-    // Tile t landed (its DMA is the only one outstanding); every wave is done
-    // reading stage s ^ 1 (tile t-1), which tile t+1 now refills.
+    const bool more = t + 1 < nk, more2 = t + 2 < nk;
+    const int td = more2 ? t + 2 : t;  // the last two tiles issue no DMA (np = 0)
+    const u32x4 ra = rsrc_a(td), rb = rsrc_b(td);
+    half_step(c, smem, acc, h0, h1, s, 1, wr, wc, l16, g, ra, rb, s, 0, 0);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi) h0.a[mi] = read_a(smem, s, 0, mi, wr, l16, g);
-#pragma unroll
-    for (int e = 0; e < 4; ++e)  // in the order the MFMAs consume them
-#pragma unroll
-      for (int ni = 0; ni < 8; ++ni) h0.b[ni][e] = read_b(smem, s, 0, ni, e, wc, l16, g);
-    const bool more = t + 1 < nk;
-    const int tn1 = more ? t + 1 : t;  // the last tile issues nothing (np = 0)
-    const u32x4 ra = rsrc_a(tn1), rb = rsrc_b(tn1);
-    half_step(c, smem, acc, h0, h1, s, 1, wr, wc, l16, g, ra, rb, s ^ 1, 0, more ? 16 : 0);
-    half_step(c, smem, acc, h1, h0, s, -1, wr, wc, l16, g, ra, rb, s ^ 1, 0, 0);
+    half_step(c, smem, acc, h1, h0, s ^ 1, more ? 0 : -1, wr, wc, l16, g, ra, rb, s,
+              0, more2 ? 16 : 0);
   }
   // Give the last MFMAs time to write their AGPRs (asm MFMAs are invisible to
   // hipcc's hazard recognizer).
