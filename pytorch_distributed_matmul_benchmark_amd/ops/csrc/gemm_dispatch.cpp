@@ -117,7 +117,9 @@ int resolve_kernel(const Problem& p, int kernel) {
     // edge tiles.
     case kAuto:
       if (w4 || t128 || t256) return plan(p, kAuto).kernel;
-      return fast ? kMfma256d : f32fast ? kF32_256s : kGeneric;
+      // fp32: the 4-wave kernel (150.4 vs 150.1 TF for f32_256s at 16k,
+      // profiles/r2_f32_w4_ab_v2.jsonl; hipBLASLt 154.4).
+      return fast ? kMfma256d : f32fast ? kF32W4 : kGeneric;
     case kGeneric: return kGeneric;
     case kMfma256d: return fast ? kMfma256d : -1;
     case kMfmaW4: return w4 ? kMfmaW4 : -1;
@@ -471,7 +473,8 @@ static hipError_t gemm_padded(const Problem& p, hipStream_t stream, int* used) {
   GemmArgs a = to_args(q);
   char* part = Cp + d.c_bytes;
   const size_t part_bytes = p.workspace_bytes - (d.a_bytes + d.b_bytes + d.c_bytes);
-  e = k == kF32_256s  ? gemm_f32_256_launch(a, 1, stream)
+  e = k == kF32W4     ? gemm_f32_w4_launch(a, stream)
+      : k == kF32_256s ? gemm_f32_256_launch(a, 1, stream)
       : is_tiled(k) ? tiled_launch(q, k, a, part, part_bytes, stream)
                      : gemm256_launch(q.dtype, a, 4, stream);
   if (e != hipSuccess) return e;

@@ -160,8 +160,8 @@ def test_fp32_exact_mfma_path():
     torch.manual_seed(3)
     A = torch.randn(512, 512, device="cuda", dtype=torch.float32)
     B = torch.randn(512, 512, device="cuda", dtype=torch.float32)
-    assert gemm.kernel_for(A, B) == "pdmb_f32_256s_nn"
-    for k in ("auto", "generic"):
+    assert gemm.kernel_for(A, B) == "pdmb_f32_w4_nn"
+    for k in ("auto", "generic", "f32_256s"):
         C = gemm.matmul(A, B, kernel=k)
         assert _relerr(C, _ref(A, B)) < TOL[torch.float32]
 
@@ -225,7 +225,7 @@ def test_f32_256_identity_batched_and_shards():
     torch.manual_seed(7)
     A3 = torch.randn(3, 384, 256, device="cuda")
     B3 = torch.randn(3, 256, 640, device="cuda")
-    assert gemm.kernel_for(A3, B3) == "pdmb_f32_256s_nn"
+    assert gemm.kernel_for(A3, B3) == "pdmb_f32_w4_nn"
     assert _relerr(gemm.bmm(A3, B3), torch.bmm(A3.double(), B3.double())) < TOL[torch.float32]
     Bf = torch.randn(1024, 1024, device="cuda")
     Af = torch.randn(1024, 1024, device="cuda")
@@ -256,7 +256,7 @@ def test_odd_sizes_padded_to_fast_path(dtype, M, N, K):
     A = torch.randn(M, K, device="cuda", dtype=dt)
     B = torch.randn(K, N, device="cuda", dtype=dt)
     assert gemm.kernel_for(A, B) == "pdmb_generic_nn"  # unpadded, only generic could run it
-    assert gemm.padded_kernel_for(A, B) in ("pdmb_mfma256d_nn", "pdmb_f32_256s_nn")
+    assert gemm.padded_kernel_for(A, B) in ("pdmb_mfma256d_nn", "pdmb_f32_w4_nn")
     C = gemm.matmul(A, B)
     assert C.shape == (M, N)
     assert _relerr(C, _ref(A, B)) < TOL[dt]
