@@ -23,6 +23,7 @@ Differences:
 from __future__ import annotations
 
 import torch
+import torch.distributed as dist
 
 from ..parallel.comm import current_stream
 from ..parallel.overlap import ReduceOverlap, compute_ctx, compute_stream, gemm_chunks
@@ -30,11 +31,8 @@ from ..parallel.dist import DistContext
 from ..parallel.partition import global_batch, local_batch
 from ..utils.metrics import gemm_flops, tflops_from
 from ..utils.timing import SegmentTimer, Stopwatch, synchronize, time_loop_ms
-import torch.distributed as dist
-
 from .common import (ModeResult, Workload, align_ranks, allreduced_relerr, gemm_fn, kernel_label,
                      out_dtype, randn, warmup)
-
 
 
 def run(w: Workload, ctx: DistContext) -> ModeResult:

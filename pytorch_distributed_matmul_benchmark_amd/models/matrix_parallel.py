@@ -26,10 +26,8 @@ Differences:
 from __future__ import annotations
 
 import torch
-import torch.distributed as dist
 
-from ..parallel.comm import current_stream
-from ..parallel.comm import CommStream
+from ..parallel.comm import CommStream, current_stream
 from ..parallel.overlap import (GatherOverlap, all_gather_now, compute_ctx, compute_stream,
                                 gemm_chunks)
 from ..parallel.dist import DistContext
