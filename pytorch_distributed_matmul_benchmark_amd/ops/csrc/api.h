@@ -41,6 +41,7 @@ enum ExperimentKernel : int {
   kMfmaW4Wide = 23,   // kMfmaW4 (bf16) with the 2x16 XCD sub-block
   kFp8W4Tall = 24,    // kFp8W4 with the 8x4 XCD sub-block
   kFp8W4Wide = 25,    // kFp8W4 with the 2x16 XCD sub-block
+  kMfmaW4Il32 = 30,   // kMfmaW4 (bf16) with the 8-wave kernel's 32-column B-half interleave
 };
 
 // True iff this library was built with the experiment kernels.

@@ -80,7 +80,7 @@ static bool is_experiment(int k) {
   switch (k) {
     case kMfma256: case kMfma256b: case kMfma256c: case kMfma256Stamp: case kF32_256:
     case kMfma256X1: case kMfma256X2: case kMfma256X4: case kFp8: case kFp8W4Diag:
-    case kFp8W4Diag2: case kFp8W4Diag3: case kF32NoDma: case kMfmaW4Tall: case kMfmaW4Wide:
+    case kFp8W4Diag2: case kFp8W4Diag3: case kF32NoDma: case kMfmaW4Tall: case kMfmaW4Wide: case kMfmaW4Il32:
     case kFp8W4Tall: case kFp8W4Wide:
       return true;
     default:
@@ -133,7 +133,7 @@ int resolve_kernel(const Problem& p, int kernel) {
     case kMfma256: case kMfma256b: case kMfma256c: return fast ? kernel : -1;
     case kMfma256X1: case kMfma256X2: case kMfma256X4: case kMfma256Stamp:
       return (fast && p.dtype == kBF16) ? kernel : -1;
-    case kMfmaW4Tall: case kMfmaW4Wide: return (p.dtype == kBF16 && w4) ? kernel : -1;
+    case kMfmaW4Tall: case kMfmaW4Wide: case kMfmaW4Il32: return (p.dtype == kBF16 && w4) ? kernel : -1;
 #endif
     default: return -1;
   }
@@ -439,7 +439,7 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel) {
   }
   const int k = resolve_kernel(p, kernel);
   if (is_tiled(k)) return splitk_bytes(p, k, plan(p, k).splitk);
-  if (k == kMfmaW4Tall || k == kMfmaW4Wide) return splitk_bytes(p, kMfmaW4, plan(p, kMfmaW4).splitk);
+  if (k == kMfmaW4Tall || k == kMfmaW4Wide || k == kMfmaW4Il32) return splitk_bytes(p, kMfmaW4, plan(p, kMfmaW4).splitk);
   return 0;
 }
 
@@ -527,6 +527,7 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kMfma256Stamp: return gemm256_launch(p.dtype, a, 3, stream);
     case kMfmaW4Tall: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 1);
     case kMfmaW4Wide: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 2);
+    case kMfmaW4Il32: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 3);
     case kF32_256: return gemm_f32_256_launch(a, 0, stream);
     case kF32NoDma: return gemm_f32_256_launch(a, 9, stream);
     case kMfma256X1: case kMfma256X2: case kMfma256X4:
@@ -621,6 +622,7 @@ const char* kernel_name(int kernel) {
     case kFp8: return "pdmb_fp8_256_nt";
     case kMfmaW4Tall: return "pdmb_w4_nn_tall";
     case kMfmaW4Wide: return "pdmb_w4_nn_wide";
+    case kMfmaW4Il32: return "pdmb_w4_nn_il32";
     case kFp8W4Tall: return "pdmb_fp8_w4_nt_tall";
     case kFp8W4Wide: return "pdmb_fp8_w4_nt_wide";
     default: return "auto";

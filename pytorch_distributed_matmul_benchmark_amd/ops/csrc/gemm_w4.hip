@@ -17,6 +17,15 @@
 // the conflict-free read patterns carry over. Only the DMA split (16 pieces of
 // 1 KiB per wave per K-tile) and the per-wave fragment offsets change.
 //
+// B halves and L2 requests (round 2): which 128 columns of the 256-wide tile
+// a B half holds is free — the LDS image and every read pattern stay the same.
+// The 8-wave kernel's choice (IL = 32: half nq = the four 32-column runs
+// [64i + 32nq, +32)) makes each k-row of a half four 64-B segments, so every
+// 128-B line of B is fetched as two half-line requests (PMC at 8192^3: W4
+// 8.43e7 L2 requests vs hipBLASLt 6.92e7; the A+B minimum is 6.7e7). IL = 64
+// (the default: half nq = [128i + 64nq, +64)) fetches whole lines; a wave
+// still owns 128 contiguous output columns, 64 from each half.
+//
 // Schedule (per K-tile t from stage S, tile t+1 in S^1; gemm_fp8.hip ktile_w4):
 //   Bar0: B(t+1) landed (vmcnt 16), every wave done reading A(t) (lgkmcnt 0).
 //   m-blocks 0-3: 64 MFMAs | read B(t+1) fragments | DMA A(t+2) -> S.A
@@ -80,23 +89,31 @@ struct Ctx {
   // Per-lane LDS fragment offsets, one VGPR per stage so every read is
   // ds_read off:imm with no address add (the immediate stops at 64 KiB).
   uint32_t aoff[2][2];  // [stage][ks]
-  uint32_t boff[2][4];  // [stage][jj]: B block j uses jj = 2 * (j >> 2) + (j & 1)
+  uint32_t boff[2][4];  // [stage][jj]: B block j uses jj = bjj<IL>(j)
   int wu;
   uint32_t lds0;
 };
+
+// B block j (16 output columns wc*128 + 16j of the wave) lives in half bhalf
+// at 32-B unit 4 wc + bjj of it (see "B halves" above).
+template <int IL>
+__device__ __forceinline__ constexpr int bhalf(int j) { return IL == 64 ? j >> 2 : (j >> 1) & 1; }
+template <int IL>
+__device__ __forceinline__ constexpr int bjj(int j) { return IL == 64 ? j & 3 : 2 * (j >> 2) + (j & 1); }
 
 // DMA piece h (0..15) of tile `tile` into the stage at byte offset `so`.
 // h < 8: A rows h*32 + wu*8 + [0,8) (8 x 128 B). h >= 8: B half nq = (h-8)>>2,
 // k rows kb*16 + wu*4 + [0,4) with kb = (h-8)&3 (4 x 256 B). B's swizzle
 // depends on k & 11 only, which kb*16 leaves alone, so one per-lane offset
-// serves all pieces; nq shifts the source by 32 columns (64 B).
+// serves all pieces; nq shifts the source by IL columns.
+template <int IL>
 __device__ __forceinline__ void issue_piece(const Ctx& c, u32x4 rb, int so, int tile, int h) {
   if (h < 8) {
     dma16_m0(c.ra, c.voffA, (uint32_t)tile * (BK * 2) + (uint32_t)(h * 32 * c.lda2),
              c.lds0 + so + (h * 32 + c.wu * 8) * 128);
   } else {
     const int nq = (h - 8) >> 2, kb = (h - 8) & 3;
-    dma16_m0(rb, c.voffB, (uint32_t)(kb * 16 * c.ldb2 + nq * 64),
+    dma16_m0(rb, c.voffB, (uint32_t)(kb * 16 * c.ldb2 + nq * IL * 2),
              c.lds0 + so + A_BYTES + nq * BH_BYTES + (kb * 16 + c.wu * 4) * 256);
   }
 }
@@ -112,8 +129,9 @@ __device__ __forceinline__ s16x8 frag_a(const char* smem, uint32_t off, int m) {
 }
 
 // B fragment half ks of block j (16 output columns): two transposed reads.
+template <int IL>
 __device__ __forceinline__ s16x8 frag_b(const char* smem, uint32_t off, int j, int ks) {
-  const char* p = smem + A_BYTES + ((j >> 1) & 1) * BH_BYTES + ks * 32 * 256 + off;
+  const char* p = smem + A_BYTES + bhalf<IL>(j) * BH_BYTES + ks * 32 * 256 + off;
   s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
   s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p + 4 * 256));
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
@@ -144,7 +162,7 @@ constexpr int piece_of(int blk, int gap) {  // running index of a DMA item (0..1
   return n;
 }
 
-template <int DT, int SO>
+template <int DT, int IL, int SO>
 __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, f32x4 (&acc)[8][8],
                                       Frag (&A)[8], Frag& A7c, Frag& A7n, Frag (&Bc)[8],
                                       Frag (&Bn)[8]) {
@@ -167,12 +185,12 @@ __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, f32
       if (it == 1) {
         const int h = piece_of(mi, gap);  // 0..7: A of t+2 into S; 8..15: B of t+3 into S^1
         if (h < 8)
-          issue_piece(c, rb, SO, ta, h);
+          issue_piece<IL>(c, rb, SO, ta, h);
         else
-          issue_piece(c, rb, SN, tb, h);
+          issue_piece<IL>(c, rb, SN, tb, h);
       } else if (it >= 100 && it < 200) {
         const int s = (it - 100) >> 1, h = (it - 100) & 1;
-        Bn[s].k[h] = frag_b(smem, c.boff[sn][2 * (s >> 2) + (s & 1)], s, h);
+        Bn[s].k[h] = frag_b<IL>(smem, c.boff[sn][bjj<IL>(s)], s, h);
       } else if (it >= 214) {
         const int h = it - 214;
         A7n.k[h] = frag_a(smem, c.aoff[sn][h], 7);
@@ -187,7 +205,8 @@ __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, f32
 
 // SUB: XCD sub-block shape (map_tile): 0 = 4 x 8 (default), 1 = 8 x 4
 // (kMfmaW4Tall), 2 = 2 x 16 (kMfmaW4Wide); 1 and 2 are A/B experiments.
-template <int DT, int SUB = 0>
+// IL: B half interleave in columns (64 default; 32 = kMfmaW4Il32, A/B only).
+template <int DT, int SUB = 0, int IL = 64>
 __global__ void __launch_bounds__(NT, 1) gemm_w4_nn(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
 
@@ -229,7 +248,8 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4_nn(GemmArgs a) {
     const int k = wu * 4 + lr16;  // k row of B piece 0 (kb = 0)
     const int s = (k & 3) | (((k >> 3) & 1) << 2);
     const int p = ((lc16 >> 1) ^ s) * 16 + (lc16 & 1) * 8;
-    const int n = (p >> 5) * 64 + (p & 31);  // nq = 0; nq = 1 adds 32 columns via soffset
+    // unit u = p >> 4 holds columns (u / (IL/16)) * 2 IL + (u % (IL/16)) * 16 (+ nq IL via soffset)
+    const int n = (p / IL) * 2 * IL + (p % IL);
     c.voffB = (uint32_t)(k * c.ldb2 + n * 2);
     const int swA = (l16 >> 1) & 7;
     const int q4 = l16 >> 2, p4 = l16 & 3;
@@ -244,7 +264,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4_nn(GemmArgs a) {
       }
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
-        const int u = 4 * wc + jj;  // 32-B unit of the B half: columns (u>>1)*64 + nq*32 + (u&1)*16
+        const int u = 4 * wc + jj;  // 32-B unit of the B half
         uint32_t bo = (uint32_t)(st * STAGE + (8 * g + q4) * 256 + ((u ^ sB) * 32) + p4 * 8);
         asm volatile("" : "+v"(bo));
         c.boff[st][jj] = bo;
@@ -266,11 +286,11 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4_nn(GemmArgs a) {
   {
     const u32x4 rb0 = b_rsrc(c, 0), rb1 = b_rsrc(c, t1);
 #pragma unroll
-    for (int h = 0; h < 16; ++h) issue_piece(c, rb0, 0, 0, h);
+    for (int h = 0; h < 16; ++h) issue_piece<IL>(c, rb0, 0, 0, h);
 #pragma unroll
-    for (int h = 8; h < 16; ++h) issue_piece(c, rb1, STAGE, t1, h);
+    for (int h = 8; h < 16; ++h) issue_piece<IL>(c, rb1, STAGE, t1, h);
 #pragma unroll
-    for (int h = 0; h < 8; ++h) issue_piece(c, rb1, STAGE, t1, h);
+    for (int h = 0; h < 8; ++h) issue_piece<IL>(c, rb1, STAGE, t1, h);
   }
   asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");  // tile 0 landed everywhere
   Frag A[8], A7a, A7b, B0[8], B1[8];
@@ -279,21 +299,21 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4_nn(GemmArgs a) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       A[i].k[ks] = frag_a(smem, c.aoff[0][ks], i);
-      B0[i].k[ks] = frag_b(smem, c.boff[0][2 * (i >> 2) + (i & 1)], i, ks);
+      B0[i].k[ks] = frag_b<IL>(smem, c.boff[0][bjj<IL>(i)], i, ks);
     }
   A7a = A[7];
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // stage 0.B read by all
   {
     const u32x4 rb2 = b_rsrc(c, t2);
 #pragma unroll
-    for (int h = 8; h < 16; ++h) issue_piece(c, rb2, 0, t2, h);
+    for (int h = 8; h < 16; ++h) issue_piece<IL>(c, rb2, 0, t2, h);
   }
   int t = 0;
   for (; t + 1 < nk; t += 2) {  // branch-free body: B0/B1 and A7a/A7b swap roles every K-tile
-    ktile<DT, 0>(c, smem, t, acc, A, A7a, A7b, B0, B1);
-    ktile<DT, STAGE>(c, smem, t + 1, acc, A, A7b, A7a, B1, B0);
+    ktile<DT, IL, 0>(c, smem, t, acc, A, A7a, A7b, B0, B1);
+    ktile<DT, IL, STAGE>(c, smem, t + 1, acc, A, A7b, A7a, B1, B0);
   }
-  if (t < nk) ktile<DT, 0>(c, smem, t, acc, A, A7a, A7b, B0, B1);  // odd count
+  if (t < nk) ktile<DT, IL, 0>(c, smem, t, acc, A, A7a, A7b, B0, B1);  // odd count
   // Drain the tail DMAs and give the last MFMAs time to write their AGPRs
   // (asm MFMAs are invisible to hipcc's hazard recognizer).
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
@@ -343,9 +363,9 @@ bool gemm_w4_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b
   if (a.batch > 1 && (a.sA % 8 || a.sB % 8 || a.sC % 4)) return false;
   if (align_a % 16 || align_b % 16 || align_c % 8) return false;
   // 32-bit offsets: A rows up to 255 * lda (+ K bytes of the tile offset),
-  // B rows up to 63 * ldb (+ 64 B of the half offset).
+  // B rows up to 63 * ldb (+ 128 B of the half offset).
   if ((long long)256 * a.lda * 2 + (long long)a.K * 2 >= (1LL << 31)) return false;
-  if ((long long)64 * a.ldb * 2 + 64 >= (1LL << 31)) return false;
+  if ((long long)64 * a.ldb * 2 + 128 >= (1LL << 31)) return false;
   return true;
 }
 
@@ -376,6 +396,10 @@ hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
   }
   if (dt == kBF16 && sub == 2) {
     hipLaunchKernelGGL((kw4::gemm_w4_nn<kBF16, 2>), grid, block, 0, stream, a);
+    return hipGetLastError();
+  }
+  if (dt == kBF16 && sub == 3) {
+    hipLaunchKernelGGL((kw4::gemm_w4_nn<kBF16, 0, 32>), grid, block, 0, stream, a);
     return hipGetLastError();
   }
 #endif

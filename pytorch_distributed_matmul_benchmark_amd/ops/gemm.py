@@ -32,7 +32,8 @@ EXPERIMENT_KERNELS = {"mfma256": 1, "mfma256b": 3, "mfma256c": 4, "mfma256c_stam
                       "f32_256": 6, "x_clusterprio": 10, "x_staticprio": 11, "x_tall": 13,
                       "fp8": 15, "diag_fp8_w4_nowait": 17, "diag_fp8_w4_nosync": 18,
                       "diag_fp8_w4_mfma_only": 19, "diag_f32_nodma": 20, "x_w4_tall": 22,
-                      "x_w4_wide": 23, "x_fp8_w4_tall": 24, "x_fp8_w4_wide": 25}
+                      "x_w4_wide": 23, "x_fp8_w4_tall": 24, "x_fp8_w4_wide": 25,
+                      "x_w4_il32": 30}
 KERNEL_NAMES = {0: "auto", 2: "pdmb_generic_nn", 7: "pdmb_f32_256s_nn", 9: "pdmb_mfma256d_nn",
                 16: "pdmb_fp8_w4_nt", 21: "pdmb_w4_nn", 26: "pdmb_t128_nn",
                 27: "pdmb_t128x2_nn", 28: "pdmb_t256x128_nn", 29: "pdmb_f32_w4_nn", 1: "pdmb_mfma256_nn",
