@@ -41,6 +41,11 @@ enum ExperimentKernel : int {
   kMfmaW4Wide = 23,   // kMfmaW4 (bf16) with the 2x16 XCD sub-block
   kFp8W4Tall = 24,    // kFp8W4 with the 8x4 XCD sub-block
   kFp8W4Wide = 25,    // kFp8W4 with the 2x16 XCD sub-block
+  kFp8W4Scaled = 31,  // kFp8W4 on the block-scaled MFMA form (scales 1)
+  kMfmaW4Trace = 32,  // kMfmaW4 (bf16) writing the tile timeline into the debug buffer
+  kFp8W4Trace = 33,   // kFp8W4 writing the tile timeline into the debug buffer
+  kMfmaW4Pers = 34,   // persistent W4 (one workgroup per CU, per-XCD work queues)
+  kMfmaW4PersTrace = 35,  // kMfmaW4Pers writing the tile timeline
   kMfmaW4Il32 = 30,   // kMfmaW4 (bf16) with the 8-wave kernel's 32-column B-half interleave
 };
 

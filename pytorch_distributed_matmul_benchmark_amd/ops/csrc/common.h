@@ -25,6 +25,8 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 typedef __attribute__((address_space(3))) s16x8 lds_s16x8;
+typedef __attribute__((address_space(3))) u32x2 lds_u32x2;
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4_t;
 
 // Data-type tags shared by host and device code. Values are part of the
 // binding ABI (ops/gemm.py mirrors them).
@@ -94,7 +96,99 @@ struct GemmArgs {
   int splitk, kt_per;
   float* part;
   unsigned* flags;
+  // Persistent kernels: per-XCD tile queues (8 tickets + 1 exit counter,
+  // zero at launch) and the grid (one workgroup per usable CU).
+  unsigned* queue;
+  int pers_grid;
 };
+
+// ---- C epilogue through LDS (W4 bf16/fp16, W4 fp8) --------------------------
+// After the K-loop a wave holds 128 columns of 16-row blocks as C^T MFMA
+// tiles: for block row i, lane (l16, g) owns row l16 and columns 16j + 4g ..
+// +3 of each 16-column block j — 8-byte pieces. Stored directly, every store
+// instruction writes 16 rows x 32 B: a 256x256 tile is 4096 partial-line
+// write requests, and the 256 CUs, which run in lock-step, issue them at the
+// same moment (the tile timeline, scripts/tile_timeline.py: 7-8 us per tile
+// at 16k, a third of W4's per-tile fixed cost). Staged through a wave-private
+// LDS buffer, each 16-row block leaves as 4 dwordx4 stores of 4 whole 256-B
+// rows: a quarter of the requests, all of them whole lines.
+// Buffer rows are 264 B (256 + 8): the b64 writes (16 lanes = 16 rows, 2
+// banks each) and the b128 reads (16 lanes = one row) are conflict-free.
+constexpr int kEpiPitch = 264;
+constexpr int kEpiBuf = 16 * kEpiPitch;  // one 16-row block, 4224 B
+
+// Store block row v (v[j] = the fp32 C^T tile j, scaled by `alpha`) of a
+// wave's 16 x 128 output at (row0, col0) of C (row stride ldc_b bytes)
+// through `buf` (kEpiBuf bytes of LDS owned by this wave). MASK: rows >= M
+// are skipped, column chunks are cut at N (N % 4 == 0: a chunk is all, half
+// or none). SCALE: multiply by alpha (fp8's folded scales).
+template <int DT, bool MASK, bool SCALE>
+__device__ __forceinline__ void store_block16(char* buf, const f32x4 (&v)[8], float alpha, char* C,
+                                              long long ldc_b, int row0, int col0, int M, int N,
+                                              int lane) {
+  const int l16 = lane & 15, g = lane >> 4;
+  lds_void* lb = (lds_void*)buf;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    u32x2 w;
+    if constexpr (SCALE) {
+      w.x = pack2<DT>(v[j].x * alpha, v[j].y * alpha);
+      w.y = pack2<DT>(v[j].z * alpha, v[j].w * alpha);
+    } else {
+      w.x = pack2<DT>(v[j].x, v[j].y);
+      w.y = pack2<DT>(v[j].z, v[j].w);
+    }
+    *(lds_u32x2*)((__attribute__((address_space(3))) char*)lb + l16 * kEpiPitch + (j * 16 + 4 * g) * 2) = w;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const u32x4 x = *(lds_u32x4_t*)((__attribute__((address_space(3))) char*)lb + (4 * r + g) * kEpiPitch + l16 * 16);
+    const int row = row0 + 4 * r + g, col = col0 + 8 * l16;
+    char* p = C + (long long)row * ldc_b + (long long)col * 2;
+    if constexpr (MASK) {
+      if (row < M) {
+        if (col + 8 <= N)
+          *(u32x4*)p = x;
+        else if (col + 4 <= N)
+          *(u32x2*)p = u32x2{x.x, x.y};
+      }
+    } else {
+      *(u32x4*)p = x;
+    }
+  }
+}
+
+// ---- Tile timeline trace (diagnostic kernel ids; a.dbg != nullptr) --------
+// Per tile 8 u64 at dbg[row * 8] (row = the tile's virtual block): [0] start, [1] first K-tile's
+// fragments in registers, [2] K-loop done, [3] C stored and drained
+// (vmcnt 0), all s_memrealtime (the chip-wide 100 MHz clock, so stamps of
+// different CUs compare); [4] HW_ID (CU / SH / SE), [5] XCC_ID, [6] tm << 32 | tn.
+// One lane writes them with vector stores (scripts/tile_timeline.py reads them).
+__device__ __forceinline__ unsigned long long tile_clock() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
+struct TileTrace {
+  unsigned long long t[4];
+};
+
+__device__ __forceinline__ void tile_trace_write(const GemmArgs& a, const TileTrace& tr, int row, int tm,
+                                                 int tn) {
+  unsigned hw, xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  if (threadIdx.x == 0 && a.dbg) {
+    unsigned long long* d = a.dbg + (size_t)row * 8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d[i] = tr.t[i];
+    d[4] = hw;
+    d[5] = xcc;
+    d[6] = ((unsigned long long)(unsigned)tm << 32) | (unsigned)tn;
+    d[7] = 0;
+  }
+}
 
 // ---- LDS-DMA helpers (shared by the LDS-DMA kernels) ----------------------
 // Raw buffer descriptor (gfx950 dword3 = 0x00020000: 32-bit data format,

@@ -73,7 +73,7 @@ bool experiments_built() {
 
 static bool is_fp8_kernel(int k) {
   return k == kFp8W4 || k == kFp8 || k == kFp8W4Diag || k == kFp8W4Diag2 || k == kFp8W4Diag3 ||
-         k == kFp8W4Tall || k == kFp8W4Wide;
+         k == kFp8W4Tall || k == kFp8W4Wide || k == kFp8W4Scaled || k == kFp8W4Trace;
 }
 
 static bool is_experiment(int k) {
@@ -81,7 +81,7 @@ static bool is_experiment(int k) {
     case kMfma256: case kMfma256b: case kMfma256c: case kMfma256Stamp: case kF32_256:
     case kMfma256X1: case kMfma256X2: case kMfma256X4: case kFp8: case kFp8W4Diag:
     case kFp8W4Diag2: case kFp8W4Diag3: case kF32NoDma: case kMfmaW4Tall: case kMfmaW4Wide: case kMfmaW4Il32:
-    case kFp8W4Tall: case kFp8W4Wide:
+    case kMfmaW4Pers: case kMfmaW4PersTrace: case kFp8W4Tall: case kFp8W4Wide: case kFp8W4Scaled: case kFp8W4Trace: case kMfmaW4Trace:
       return true;
     default:
       return false;
@@ -133,7 +133,9 @@ int resolve_kernel(const Problem& p, int kernel) {
     case kMfma256: case kMfma256b: case kMfma256c: return fast ? kernel : -1;
     case kMfma256X1: case kMfma256X2: case kMfma256X4: case kMfma256Stamp:
       return (fast && p.dtype == kBF16) ? kernel : -1;
-    case kMfmaW4Tall: case kMfmaW4Wide: case kMfmaW4Il32: return (p.dtype == kBF16 && w4) ? kernel : -1;
+    case kMfmaW4Tall: case kMfmaW4Wide: case kMfmaW4Il32: case kMfmaW4Trace:
+    case kMfmaW4Pers: case kMfmaW4PersTrace:
+      return (p.dtype == kBF16 && w4) ? kernel : -1;
 #endif
     default: return -1;
   }
@@ -268,10 +270,13 @@ static size_t splitk_bytes(const Problem& p, int kernel, int S) {
   return (size_t)tiles_of(p, m.kernel) * S * m.bm * m.bn * sizeof(float);  // one slot per slice
 }
 
-// Per-(device, stream) split-K counters (2 per tile), zeroed once on the
-// stream before first use; never freed (64 KiB each). Returns nullptr if the
+// Per-(device, stream) counters, zeroed once on the stream before first use,
+// never freed (~32 KiB each): split-K (2 per tile, kMaxSplitTiles tiles),
+// then the persistent kernels' work queues (kQueueWords). Returns nullptr if the
 // stream is being captured and has none yet (hipMalloc is not capturable):
 // the caller then runs unsplit.
+static constexpr int kQueueWords = 16;  // 8 XCD ticket counters + exit counter (+ pad)
+
 static unsigned* stream_counters(hipStream_t s) {
   static std::mutex mu;
   static std::unordered_map<unsigned long long, unsigned*>* map =
@@ -285,7 +290,7 @@ static unsigned* stream_counters(hipStream_t s) {
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
   unsigned* c = nullptr;
-  const size_t bytes = 2 * sizeof(unsigned) * kMaxSplitTiles;
+  const size_t bytes = sizeof(unsigned) * (2 * kMaxSplitTiles + kQueueWords);
   if (hipMalloc(&c, bytes) != hipSuccess) return nullptr;
   if (hipMemsetAsync(c, 0, bytes, s) != hipSuccess) {
     (void)hipFree(c);
@@ -311,6 +316,15 @@ static hipError_t tiled_launch(const Problem& p, int k, GemmArgs a, void* part, 
     }
   }
   a.splitk = S;
+  if (sub == 5 || sub == 6) {  // persistent W4: unsplit, needs the stream's queue
+    unsigned* c = S > 1 ? nullptr : stream_counters(stream);
+    if (!c) {
+      sub = sub == 6 ? 4 : 0;
+    } else {
+      a.queue = c + 2 * kMaxSplitTiles;
+      a.pers_grid = p.cus > 0 ? p.cus : device_cus();
+    }
+  }
   return k == kMfmaW4 ? gemm_w4_launch(p.dtype, a, stream, sub) : gemm_tile_launch(k, p.dtype, a, stream);
 }
 
@@ -439,7 +453,9 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel) {
   }
   const int k = resolve_kernel(p, kernel);
   if (is_tiled(k)) return splitk_bytes(p, k, plan(p, k).splitk);
-  if (k == kMfmaW4Tall || k == kMfmaW4Wide || k == kMfmaW4Il32) return splitk_bytes(p, kMfmaW4, plan(p, kMfmaW4).splitk);
+  if (k == kMfmaW4Tall || k == kMfmaW4Wide || k == kMfmaW4Il32 || k == kMfmaW4Trace ||
+      k == kMfmaW4Pers || k == kMfmaW4PersTrace)
+    return splitk_bytes(p, kMfmaW4, plan(p, kMfmaW4).splitk);
   return 0;
 }
 
@@ -521,6 +537,8 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kFp8W4Diag3: return gemm_fp8_launch(a, 11, stream);
     case kFp8W4Tall: return gemm_fp8_launch(a, 12, stream);
     case kFp8W4Wide: return gemm_fp8_launch(a, 13, stream);
+    case kFp8W4Scaled: return gemm_fp8_launch(a, 14, stream);
+    case kFp8W4Trace: return gemm_fp8_launch(a, 15, stream);
     case kMfma256: return gemm256_launch(p.dtype, a, 0, stream);
     case kMfma256b: return gemm256_launch(p.dtype, a, 1, stream);
     case kMfma256c: return gemm256_launch(p.dtype, a, 2, stream);
@@ -528,6 +546,9 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kMfmaW4Tall: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 1);
     case kMfmaW4Wide: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 2);
     case kMfmaW4Il32: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 3);
+    case kMfmaW4Trace: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 4);
+    case kMfmaW4Pers: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 5);
+    case kMfmaW4PersTrace: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 6);
     case kF32_256: return gemm_f32_256_launch(a, 0, stream);
     case kF32NoDma: return gemm_f32_256_launch(a, 9, stream);
     case kMfma256X1: case kMfma256X2: case kMfma256X4:
@@ -625,6 +646,11 @@ const char* kernel_name(int kernel) {
     case kMfmaW4Il32: return "pdmb_w4_nn_il32";
     case kFp8W4Tall: return "pdmb_fp8_w4_nt_tall";
     case kFp8W4Wide: return "pdmb_fp8_w4_nt_wide";
+    case kFp8W4Scaled: return "pdmb_fp8_w4_nt_scaled";
+    case kMfmaW4Trace: return "pdmb_w4_nn_trace";
+    case kMfmaW4Pers: return "pdmb_w4_pers";
+    case kMfmaW4PersTrace: return "pdmb_w4_pers_trace";
+    case kFp8W4Trace: return "pdmb_fp8_w4_nt_trace";
     default: return "auto";
   }
 }

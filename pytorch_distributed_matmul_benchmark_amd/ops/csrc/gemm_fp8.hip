@@ -296,10 +296,19 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_fp8_nt(GemmArgs a) {
 constexpr int NT4 = 256;
 constexpr int STAGE4 = 2 * A_BYTES;  // A [256][128 B] + Bt [256][128 B]
 
+// SCALED = 0 (default): the unscaled v_mfma_f32_16x16x128_f8f6f4 (e4m3 x e4m3,
+// same rate as the block-scaled form, scale 1). SCALED = 1: the block-scaled
+// form with both scales 2^0 — identical results, but it assembles to TWO
+// instructions (a v_mfma_ld_scale_b32 prefix + the MFMA, 16 bytes), an extra
+// issue slot in every MFMA gap of a one-wave-per-SIMD schedule (A/B only).
+template <int SCALED>
 __device__ __forceinline__ void mfma_f8_acc(f32x4& acc, const i32x8& a, const i32x8& b, int sc) {
-  asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0]"
-               : "+a"(acc)
-               : "v"(a), "v"(b), "v"(sc));
+  if constexpr (SCALED)
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0]"
+                 : "+a"(acc)
+                 : "v"(a), "v"(b), "v"(sc));
+  else
+    asm volatile("v_mfma_f32_16x16x128_f8f6f4 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
 // LDS-DMA with a scalar offset (the 8 pieces of one operand differ by 32 rows).
@@ -386,7 +395,7 @@ constexpr int w4_piece(int blk, int gap) {  // running index of a DMA item (0..1
 //   blocks 4-7: MFMAs | read A(t+1) from S^1.A | DMA B(t+3) -> S^1.B
 // Each operand half thus gets ~1.5 K-tiles of DMA flight (one K-tile was not
 // enough: the same kernel without the DMA wait ran 17 % faster).
-template <int SO, int DIAG_NOWAIT = 0>
+template <int SO, int DIAG_NOWAIT = 0, int SCALED = 0>
 __device__ __forceinline__ void ktile_w4(const Ctx4& c, const char* smem, int t, f32x4 (&acc)[8][8],
                                          i32x8 (&A)[8], i32x8& A7c, i32x8& A7n, i32x8 (&Bc)[8],
                                          i32x8 (&Bn)[8], int sc) {
@@ -406,7 +415,7 @@ __device__ __forceinline__ void ktile_w4(const Ctx4& c, const char* smem, int t,
     }
 #pragma unroll
     for (int ni = 0; ni < 8; ++ni) {
-      mfma_f8_acc(acc[mi][ni], Bc[ni], mi == 7 ? A7c : A[mi], sc);
+      mfma_f8_acc<SCALED>(acc[mi][ni], Bc[ni], mi == 7 ? A7c : A[mi], sc);
       if constexpr (DIAG_NOWAIT != 3) {  // 3: timing-only, MFMAs + barriers alone
         const int it = kW4Items[mi][ni];
         if (it == 1) {
@@ -429,9 +438,13 @@ __device__ __forceinline__ void ktile_w4(const Ctx4& c, const char* smem, int t,
 }
 
 // SUB: XCD sub-block shape (map_tile); 1 (8x4) and 2 (2x16) are A/B experiments.
-template <int DIAG_NOWAIT, int SUB = 0>
+// SCALED: see mfma_f8_acc (1 = kFp8W4Scaled, A/B only).
+// TRACE: write the tile timeline (common.h tile_trace_write; kFp8W4Trace).
+template <int DIAG_NOWAIT, int SUB = 0, int SCALED = 0, int TRACE = 0>
 __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE4];
+  TileTrace tr;
+  if constexpr (TRACE) tr.t[0] = tile_clock();
 
   int bz, tm, tn;
   map_tile(a, blockIdx.x, bz, tm, tn, SUB);
@@ -497,36 +510,44 @@ __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4(GemmArgs a) {
   }
   A7a = A[7];
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // stage 0.B read by all
+  if constexpr (TRACE) tr.t[1] = tile_clock();
 #pragma unroll
   for (int h = 8; h < 16; ++h) issue_piece(c, 0, t2, h);
   int t = 0;
   for (; t + 1 < nk; t += 2) {  // branch-free body: B0/B1 and A7a/A7b swap roles every K-tile
-    ktile_w4<0, DIAG_NOWAIT>(c, smem, t, acc, A, A7a, A7b, B0, B1, sc);
-    ktile_w4<STAGE4, DIAG_NOWAIT>(c, smem, t + 1, acc, A, A7b, A7a, B1, B0, sc);
+    ktile_w4<0, DIAG_NOWAIT, SCALED>(c, smem, t, acc, A, A7a, A7b, B0, B1, sc);
+    ktile_w4<STAGE4, DIAG_NOWAIT, SCALED>(c, smem, t + 1, acc, A, A7b, A7a, B1, B0, sc);
   }
-  if (t < nk) ktile_w4<0, DIAG_NOWAIT>(c, smem, t, acc, A, A7a, A7b, B0, B1, sc);  // odd count
+  if (t < nk) ktile_w4<0, DIAG_NOWAIT, SCALED>(c, smem, t, acc, A, A7a, A7b, B0, B1, sc);  // odd count
   // Drain the tail DMAs and give the last MFMAs time to write their AGPRs
   // (asm MFMAs are invisible to hipcc's hazard recognizer).
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  if constexpr (TRACE) tr.t[2] = tile_clock();
 
+  // Epilogue through LDS as whole rows (common.h store_block16), masked at
+  // M / N; every DMA landed and every fragment read done before any wave
+  // writes its staging buffers.
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   const float alpha = a.alpha;
   char* Cb = (char*)a.C + (long long)bz * a.sC * 2;
+  char* ebuf = smem + wu * 2 * kEpiBuf;
+  if (m0 + BM <= a.M && n0 + BN <= a.N) {  // interior tile: no masks
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int row = m0 + wr * 128 + i * 16 + l16;
-    if (row < a.M) {
-      char* crow = Cb + (long long)row * a.ldc * 2;
+    for (int i = 0; i < 8; ++i)
+      store_block16<kBF16, false, true>(ebuf + (i & 1) * kEpiBuf, acc[i], alpha, Cb,
+                                        (long long)a.ldc * 2, m0 + wr * 128 + i * 16,
+                                        n0 + wc * 128, a.M, a.N, lane);
+  } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int col = n0 + wc * 128 + j * 16 + 4 * g;
-        if (col < a.N) {
-          u32x2 v;
-          v.x = pack2<kBF16>(acc[i][j].x * alpha, acc[i][j].y * alpha);
-          v.y = pack2<kBF16>(acc[i][j].z * alpha, acc[i][j].w * alpha);
-          *(u32x2*)(crow + col * 2) = v;
-        }
-      }
-    }
+    for (int i = 0; i < 8; ++i)
+      store_block16<kBF16, true, true>(ebuf + (i & 1) * kEpiBuf, acc[i], alpha, Cb,
+                                       (long long)a.ldc * 2, m0 + wr * 128 + i * 16,
+                                       n0 + wc * 128, a.M, a.N, lane);
+  }
+  if constexpr (TRACE) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tr.t[3] = tile_clock();
+    tile_trace_write(a, tr, blockIdx.x, tm, tn);
   }
 }
 
@@ -566,6 +587,10 @@ hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream) {
     hipLaunchKernelGGL((k8::gemm_fp8_w4<0, 1>), grid, dim3(k8::NT4), 0, stream, a);
   else if (variant == 13)
     hipLaunchKernelGGL((k8::gemm_fp8_w4<0, 2>), grid, dim3(k8::NT4), 0, stream, a);
+  else if (variant == 14)
+    hipLaunchKernelGGL((k8::gemm_fp8_w4<0, 0, 1>), grid, dim3(k8::NT4), 0, stream, a);
+  else if (variant == 15)
+    hipLaunchKernelGGL((k8::gemm_fp8_w4<0, 0, 0, 1>), grid, dim3(k8::NT4), 0, stream, a);
   else
     hipLaunchKernelGGL(k8::gemm_fp8_nt, grid, dim3(k8::NTHREADS), 0, stream, a);
 #else

@@ -206,24 +206,43 @@ __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, f32
 // SUB: XCD sub-block shape (map_tile): 0 = 4 x 8 (default), 1 = 8 x 4
 // (kMfmaW4Tall), 2 = 2 x 16 (kMfmaW4Wide); 1 and 2 are A/B experiments.
 // IL: B half interleave in columns (64 default; 32 = kMfmaW4Il32, A/B only).
-template <int DT, int SUB = 0, int IL = 64>
-__global__ void __launch_bounds__(NT, 1) gemm_w4_nn(GemmArgs a) {
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+// TRACE: write the tile timeline (common.h tile_trace_write; kMfmaW4Trace).
+// One output tile: virtual block vb (map_tile's order). PERS (persistent
+// kernel; no split-K): thread 0 takes the next ticket of its XCD's queue
+// `qpre` as the tile starts and returns it; it is first read after the
+// K-loop's vmcnt(0), so the atomic's latency hides behind the tile.
+template <int DT, int SUB, int IL, int TRACE, bool PERS>
+__device__ __forceinline__ unsigned w4_tile(const GemmArgs& a, char* smem, int vb, unsigned* qpre) {
+  TileTrace tr;
+  if constexpr (TRACE) tr.t[0] = tile_clock();
+  // PERS: an opaque thread id, so nothing lane-derived is hoisted out of the
+  // persistent tile loop (live across the epilogue, it spilled).
+  int tid = threadIdx.x;
+  if constexpr (PERS) asm volatile("" : "+v"(tid));
+  unsigned pre = 0;
+  if constexpr (PERS) {
+    // A per-lane (opaque) address keeps this a plain returning atomic: the
+    // compiler's wave-aggregation rewrite would read the result at once and
+    // wait for it here instead of after the K-loop.
+    unsigned z = 0;
+    asm volatile("" : "+v"(z));
+    if (tid == 0) pre = __hip_atomic_fetch_add(qpre + z, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 
   int bz, tm, tn;
-  map_tile(a, blockIdx.x, bz, tm, tn, SUB);
+  map_tile(a, vb, bz, tm, tn, SUB);
   // Split-K: the grid's "batch" is batch x S with the slice innermost, so
   // one slice of every tile is a contiguous block range (map_tile's grouped
   // order) and each workgroup runs K-tiles [kt0, kt0 + nk) of its tile.
   int slice = 0;
-  if (a.splitk > 1) {
+  if (!PERS && a.splitk > 1) {
     slice = bz % a.splitk;
     bz /= a.splitk;
   }
   const int kt0 = slice * a.kt_per;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int lane = threadIdx.x & 63;
-  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = tid & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wu >> 1, wc = wu & 1;
   const int l16 = lane & 15, g = lane >> 4;
 
@@ -234,7 +253,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4_nn(GemmArgs a) {
   c.ldb2 = a.ldb * 2;
   {
     const int nk_all = a.K / BK;
-    c.nk = a.splitk > 1 ? min(a.kt_per, nk_all - kt0) : nk_all;
+    c.nk = !PERS && a.splitk > 1 ? min(a.kt_per, nk_all - kt0) : nk_all;
   }
   const int k0 = kt0 * BK;
   const char* Ab = (const char*)a.A + ((long long)bz * a.sA + (long long)m0 * a.lda + k0) * 2;
@@ -303,6 +322,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4_nn(GemmArgs a) {
     }
   A7a = A[7];
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // stage 0.B read by all
+  if constexpr (TRACE) tr.t[1] = tile_clock();
   {
     const u32x4 rb2 = b_rsrc(c, t2);
 #pragma unroll
@@ -317,38 +337,98 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4_nn(GemmArgs a) {
   // Drain the tail DMAs and give the last MFMAs time to write their AGPRs
   // (asm MFMAs are invisible to hipcc's hazard recognizer).
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  if constexpr (TRACE) tr.t[2] = tile_clock();
 
   // Split-K: only the last slice of a tile to arrive writes C, adding the
   // other slices' fp32 slots block row by block row while storing, so no
   // more than 2 x 8 fragments are live in VGPRs (splitk.h).
   SplitSlots sl;
-  const bool split = a.splitk > 1;
+  const bool split = !PERS && a.splitk > 1;
   if (split && !splitk_meet<8, 8, NT>(a, smem, ((long long)bz * a.tiles_m + tm) * a.tiles_n + tn,
                                       slice, acc, sl))
-    return;
+    return pre;
 
-  // Epilogue: acc[i][j] holds C^T of a 16x16 tile: lane owns row l16 and
-  // columns 4g..4g+3 (interior tiles only: no masks).
+  // Epilogue: acc[i][j] holds C^T of a 16x16 tile (lane: row l16, columns
+  // 4g..4g+3), stored through LDS as whole rows (common.h store_block16;
+  // interior tiles only: no masks). Every wave's DMAs have landed and every
+  // fragment read is done before any wave writes its staging buffers.
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   char* Cb = (char*)a.C + (long long)bz * a.sC * 2;
+  char* ebuf = smem + 1024 + wu * 2 * kEpiBuf;  // past splitk_meet's ticket word
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     f32x4 v[8];
     if (!split) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = acc[i][j];
-    } else {
+    } else if constexpr (!PERS) {
       splitk_row<8, 8, NT>(a, sl, slice, i, acc, v);
     }
-    const int row = m0 + wr * 128 + i * 16 + l16;
-    char* crow = Cb + (long long)row * a.ldc * 2;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int col = n0 + wc * 128 + j * 16 + 4 * g;
-      u32x2 w;
-      w.x = pack2<DT>(v[j].x, v[j].y);
-      w.y = pack2<DT>(v[j].z, v[j].w);
-      *(u32x2*)(crow + col * 2) = w;
+    store_block16<DT, false, false>(ebuf + (i & 1) * kEpiBuf, v, 1.0f, Cb, (long long)a.ldc * 2,
+                             m0 + wr * 128 + i * 16, n0 + wc * 128, a.M, a.N, lane);
+  }
+  if constexpr (TRACE) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tr.t[3] = tile_clock();
+    tile_trace_write(a, tr, vb, tm, tn);
+  }
+  return pre;
+}
+
+template <int DT, int SUB = 0, int IL = 64, int TRACE = 0>
+__global__ void __launch_bounds__(NT, 1) gemm_w4_nn(GemmArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  (void)w4_tile<DT, SUB, IL, TRACE, false>(a, smem, blockIdx.x, nullptr);
+}
+
+// Persistent W4: one workgroup per CU, tiles from per-XCD queues. The tile
+// timeline (scripts/tile_timeline.py) shows the XCDs running at different
+// speeds (16k bf16: 331.9 to 349.3 us per tile) while hardware dispatch
+// gives each exactly 1/8 of the tiles, so the fast ones idle at the end (~2 %
+// of the kernel). Here XCD x (its real XCC_ID) takes the virtual blocks
+// vb = x + 8 i from queue x — map_tile's XCD-local tile sets, so L2 reuse is
+// unchanged — and a workgroup whose queue is empty steals from the others.
+// a.queue: 8 ticket counters + 1 exit counter, zero at launch; the last
+// workgroup to exit re-zeroes them (stream-ordered, like the split-K flags).
+// Every workgroup exits when no queue has a tile left.
+template <int DT, int TRACE = 0>
+__global__ void __launch_bounds__(NT, 1) gemm_w4_pers(GemmArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 16];
+  volatile int* qword = (volatile int*)(smem + 2 * STAGE);
+  unsigned* q = a.queue;
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  xcc &= 7;
+  const int T = a.tiles_m * a.tiles_n * a.batch;
+  auto count = [&](int x) { return T > x ? (T - x + 7) / 8 : 0; };
+  auto take = [&](unsigned own) -> int {  // thread 0: own ticket, else steal
+    if ((int)own < count(xcc)) return (int)xcc + 8 * (int)own;
+    for (int y = 1; y < 8; ++y) {
+      const int x = (xcc + y) & 7;
+      if (count(x) == 0) continue;
+      const unsigned i = __hip_atomic_fetch_add(&q[x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((int)i < count(x)) return x + 8 * (int)i;
     }
+    return -1;
+  };
+  if (threadIdx.x == 0)
+    *qword = take(__hip_atomic_fetch_add(&q[xcc], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  __syncthreads();
+  int vb = __builtin_amdgcn_readfirstlane(*qword);  // uniform: tile math stays scalar
+  while (vb >= 0) {
+    const unsigned pre = w4_tile<DT, 0, 64, TRACE, true>(a, smem, vb, &q[xcc]);
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    if (tid == 0) *qword = take(pre);
+    // every wave is done with its epilogue staging (lgkmcnt) before the next
+    // tile's DMAs land, and sees the next ticket
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    vb = __builtin_amdgcn_readfirstlane(*qword);
+  }
+  if (threadIdx.x == 0) {
+    const unsigned d = __hip_atomic_fetch_add(&q[8], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == gridDim.x - 1)  // every other workgroup has taken its last ticket
+      for (int i = 0; i < 9; ++i) __hip_atomic_store(&q[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -402,7 +482,26 @@ hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
     hipLaunchKernelGGL((kw4::gemm_w4_nn<kBF16, 0, 32>), grid, block, 0, stream, a);
     return hipGetLastError();
   }
+  if (dt == kBF16 && sub == 4) {
+    hipLaunchKernelGGL((kw4::gemm_w4_nn<kBF16, 0, 64, 1>), grid, block, 0, stream, a);
+    return hipGetLastError();
+  }
+  if (dt == kBF16 && sub == 6) {  // persistent + tile timeline
+    if (S > 1 || !a.queue) return hipErrorInvalidValue;
+    const unsigned g = (unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid);
+    hipLaunchKernelGGL((kw4::gemm_w4_pers<kBF16, 1>), dim3(g), block, 0, stream, a);
+    return hipGetLastError();
+  }
 #endif
+  if (sub == 5) {  // persistent (per-XCD work queues), unsplit only
+    if (S > 1 || !a.queue || a.pers_grid <= 0) return hipErrorInvalidValue;
+    const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
+    if (dt == kBF16)
+      hipLaunchKernelGGL((kw4::gemm_w4_pers<kBF16>), pg, block, 0, stream, a);
+    else
+      hipLaunchKernelGGL((kw4::gemm_w4_pers<kF16>), pg, block, 0, stream, a);
+    return hipGetLastError();
+  }
   if (sub != 0) return hipErrorInvalidValue;
   if (dt == kBF16)
     hipLaunchKernelGGL(kw4::gemm_w4_nn<kBF16>, grid, block, 0, stream, a);

@@ -33,7 +33,8 @@ EXPERIMENT_KERNELS = {"mfma256": 1, "mfma256b": 3, "mfma256c": 4, "mfma256c_stam
                       "fp8": 15, "diag_fp8_w4_nowait": 17, "diag_fp8_w4_nosync": 18,
                       "diag_fp8_w4_mfma_only": 19, "diag_f32_nodma": 20, "x_w4_tall": 22,
                       "x_w4_wide": 23, "x_fp8_w4_tall": 24, "x_fp8_w4_wide": 25,
-                      "x_w4_il32": 30}
+                      "x_w4_il32": 30, "x_fp8_w4_scaled": 31, "diag_w4_trace": 32,
+                      "diag_fp8_w4_trace": 33, "x_w4_pers": 34, "diag_w4_pers_trace": 35}
 KERNEL_NAMES = {0: "auto", 2: "pdmb_generic_nn", 7: "pdmb_f32_256s_nn", 9: "pdmb_mfma256d_nn",
                 16: "pdmb_fp8_w4_nt", 21: "pdmb_w4_nn", 26: "pdmb_t128_nn",
                 27: "pdmb_t128x2_nn", 28: "pdmb_t256x128_nn", 29: "pdmb_f32_w4_nn", 1: "pdmb_mfma256_nn",
@@ -240,3 +241,28 @@ def comm_proxy(dst: torch.Tensor, src: torch.Tensor, blocks: int = 32) -> None:
     256-thread workgroups: the CU footprint of an RCCL collective's channels,
     for single-GPU overlap experiments (scripts/cu_mask_overlap.py)."""
     _native.load().comm_proxy(dst, src, int(blocks))
+
+
+TRACE_KERNELS = {"w4": "diag_w4_trace", "fp8_w4": "diag_fp8_w4_trace", "x_w4_pers": "diag_w4_pers_trace"}
+
+
+def tile_trace(A: torch.Tensor, B: torch.Tensor, kernel: str = "w4") -> torch.Tensor:
+    """Run one launch of ``kernel``'s tile-timeline build (experiment builds
+    only) and return its trace: int64 [workgroups, 8] = start, first K-tile
+    in registers, K-loop done, C drained (s_memrealtime, 100 MHz), HW_ID,
+    XCC_ID, tm << 32 | tn, 0 (common.h tile_trace_write). Row = blockIdx.x."""
+    C = _native.load()
+    kid = _kid(TRACE_KERNELS.get(kernel, kernel))
+    A, B = _prep_pair(A, B)
+    out = torch.empty(_out_shape(A, B), dtype=out_dtype(A.dtype), device=A.device)
+    M, N = out.shape[-2], out.shape[-1]
+    batch = out.numel() // (M * N)
+    blocks = -(-M // 256) * -(-N // 256) * batch
+    buf = torch.zeros(blocks, 8, dtype=torch.int64, device=A.device)
+    C.set_debug_buffer(buf)
+    try:
+        C.matmul(A, B, out, kid, 1.0, 0, _cus())
+        torch.cuda.synchronize(A.device)
+    finally:
+        C.set_debug_buffer(None)
+    return buf.cpu()

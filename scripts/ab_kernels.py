@@ -1,9 +1,13 @@
 #!/usr/bin/env python3
 """Interleaved A/B of native GEMM kernel variants in ONE process (cdna rule 24):
 N rounds × K kernels on the same random operands; prints median/min TFLOPS per
-kernel and checks every variant against the first one's output.
+kernel, its error vs an fp32 torch reference and whether its output is bitwise
+equal to the first kernel's. The arm ``torch`` is the vendor library
+(hipBLASLt: torch.matmul, or torch._scaled_mm for fp8) in the same rounds.
 
     python scripts/ab_kernels.py --kernels mfma256c,x_noprio --sizes 8192 16384 --rounds 5
+    python scripts/ab_kernels.py --kernels fp8_w4,torch --dtype float8_e4m3fn \
+        --shapes 16384,16384,2048 16384,16384,16384      # M,N,K (K sweeps: per-tile overhead)
 """
 import argparse
 import json
@@ -22,39 +26,67 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kernels", required=True)
     ap.add_argument("--sizes", type=int, nargs="+", default=[8192, 16384])
+    ap.add_argument("--shapes", nargs="+", default=None, help="M,N,K triples (instead of --sizes)")
     ap.add_argument("--dtype", default="bfloat16")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
     a = ap.parse_args()
     ks = a.kernels.split(",")
     dt = getattr(torch, a.dtype)
-    for n in a.sizes:
+    shapes = ([tuple(int(v) for v in s.split(",")) for s in a.shapes] if a.shapes
+              else [(n, n, n) for n in a.sizes])
+    for m, n, kk in shapes:
         torch.manual_seed(0)
         if dt == torch.float8_e4m3fn:  # e4m3 operands (scale 1), B column-major, bf16 C
-            A, _ = gemm.fp8_quantize(torch.randn(n, n, device="cuda"))
-            B, _ = gemm.fp8_quantize(torch.randn(n, n, device="cuda"), colmajor=True)
+            A, _ = gemm.fp8_quantize(torch.randn(m, kk, device="cuda"))
+            B, _ = gemm.fp8_quantize(torch.randn(kk, n, device="cuda"), colmajor=True)
         else:
-            A = torch.randn(n, n, device="cuda", dtype=dt)
-            B = torch.randn(n, n, device="cuda", dtype=dt)
-        C = torch.empty(n, n, device="cuda", dtype=gemm.out_dtype(dt))
-        ref = gemm.matmul(A, B, kernel=ks[0])
+            A = torch.randn(m, kk, device="cuda", dtype=dt)
+            B = torch.randn(kk, n, device="cuda", dtype=dt)
+        C = torch.empty(m, n, device="cuda", dtype=gemm.out_dtype(dt))
+        flops = 2.0 * m * n * kk
+        one = torch.ones((), device="cuda")
+
+        def vendor(out=None):
+            if dt == torch.float8_e4m3fn:
+                return torch._scaled_mm(A, B, one, one, out_dtype=torch.bfloat16, out=out)
+            return torch.matmul(A, B, out=out)
+
+        def run(k):
+            return vendor() if k == "torch" else gemm.matmul(A, B, kernel=k)
+
+        def bench(k, iters):
+            if k != "torch":
+                return gemm.bench_matmul(A, B, C, iters, 2, kernel=k) / iters
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            vendor(C)
+            e0.record()
+            for _ in range(iters):
+                vendor(C)
+            e1.record()
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / iters
+
+        ref = run(ks[0])
         R = torch.matmul(A.float(), B.float())
         res = {k: [] for k in ks}
-        errs = {}
+        errs, same = {}, {}
         for k in ks:
-            out = gemm.matmul(A, B, kernel=k)
+            out = run(k)
             errs[k] = ((out.float() - R).norm() / R.norm()).item()  # diag_* builds are timing-only
+            same[k] = bool(torch.equal(out, ref))
         for _ in range(2):  # warm clocks
             for k in ks:
-                gemm.bench_matmul(A, B, C, 5, 2, kernel=k)
+                bench(k, 5)
         for _ in range(a.rounds):
             for k in ks:
-                ms = gemm.bench_matmul(A, B, C, a.iters, 2, kernel=k) / a.iters
-                res[k].append(2.0 * n ** 3 / ms / 1e9)
+                res[k].append(flops / bench(k, a.iters) / 1e9)
         for k in ks:
-            print(json.dumps({"n": n, "kernel": k, "median_tflops": round(statistics.median(res[k]), 1),
+            med = statistics.median(res[k])
+            print(json.dumps({"n": n, **({"m": m, "k": kk} if a.shapes else {}), "kernel": k,
+                              "median_tflops": round(med, 1), "median_us": round(flops / med / 1e6, 1),
                               "min": round(min(res[k]), 1), "max": round(max(res[k]), 1),
-                              "relerr": errs[k]}), flush=True)
+                              "relerr": errs[k], "bitwise_eq_first": same[k]}), flush=True)
         del A, B, C, ref, R
         torch.cuda.empty_cache()
 

@@ -425,6 +425,69 @@ def test_tile_family_matches_w4_bitwise_unsplit():
         assert torch.equal(gemm.matmul(A, B, kernel=k, splitk=1), ref), k
 
 
+@pytest.mark.parametrize("b,M,N,K", [(1, 256, 256, 64), (1, 256, 512, 128), (1, 2304, 1280, 192),
+                                     (3, 1024, 768, 256), (1, 4096, 4096, 512), (1, 8192, 2048, 128)])
+def test_persistent_w4_matches_w4_bitwise(b, M, N, K):
+    """Persistent W4 (per-XCD work queues, stealing): same tiles, same
+    accumulation order, so bitwise equal to W4 — for grids smaller than the
+    chip, than 8 (XCDs with empty queues steal), and batched. Three launches
+    each: the queue counters must be back at zero after every one."""
+    _need("x_w4_pers")
+    g = torch.Generator(device="cuda").manual_seed(b * 7 + M + N + K)
+    shape = (b,) if b > 1 else ()
+    A = torch.randn(*shape, M, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    B = torch.randn(*shape, K, N, device="cuda", dtype=torch.bfloat16, generator=g)
+    ref = gemm.matmul(A, B, kernel="w4", splitk=1)
+    for _ in range(3):
+        out = torch.full_like(ref, float("nan"))
+        gemm.matmul(A, B, out=out, kernel="x_w4_pers")
+        assert torch.equal(out, ref)
+    assert _relerr(ref, _ref(A, B)) < TOL[torch.bfloat16]
+
+
+def test_persistent_w4_streams_graph_and_cu_budget():
+    """Queues are per stream: persistent launches on two streams at once stay
+    exact; a graph replays exactly; a CU-masked stream (fewer workgroups than
+    CUs) still covers every tile."""
+    _need("x_w4_pers")
+    from pytorch_distributed_matmul_benchmark_amd.parallel.overlap import MaskedStream
+
+    g = torch.Generator(device="cuda").manual_seed(11)
+    A = torch.randint(-3, 4, (4096, 2048), device="cuda", generator=g).to(torch.bfloat16)
+    B = torch.randint(-3, 4, (2048, 4096), device="cuda", generator=g).to(torch.bfloat16)
+    R = (A.double() @ B.double()).to(torch.bfloat16)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = [torch.empty_like(R) for _ in range(6)]
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        with torch.cuda.stream(s1 if i % 2 else s2):
+            gemm.matmul(A, B, out=o, kernel="x_w4_pers")
+    torch.cuda.synchronize()
+    assert all(torch.equal(o, R) for o in outs)
+    s = torch.cuda.Stream()
+    out = torch.empty_like(R)
+    with torch.cuda.stream(s):
+        gemm.matmul(A, B, out=out, kernel="x_w4_pers")  # the stream's queue exists first
+    s.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        gemm.matmul(A, B, out=out, kernel="x_w4_pers")
+    for _ in range(3):
+        out.fill_(float("nan"))
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, R)
+    ms = MaskedStream(torch.device("cuda", 0), 24)
+    try:
+        out.fill_(float("nan"))
+        with torch.cuda.stream(ms.stream), ms.budget():
+            gemm.matmul(A, B, out=out, kernel="x_w4_pers")
+        torch.cuda.synchronize()
+        assert torch.equal(out, R)
+    finally:
+        ms.close()
+
+
 def test_splitk_concurrent_streams_and_graph():
     """Per-stream counters: split-K GEMMs on two streams at once stay exact; a
     torch.cuda.graph capture of one replays exactly (counters re-zeroed by
