@@ -39,6 +39,7 @@ job down in seconds (fault injection: ``PDMB_BENCH_FAULT=rank:mode:phase``).
 from __future__ import annotations
 
 import argparse
+import contextlib
 import gc
 import json
 import os
@@ -105,6 +106,8 @@ class Workload:
             self.kernel = self._label(A, B, C)
             if overlap:
                 ov = ReduceOverlap(lb, gemm_chunks(n, n, a.chunks, dt, dev), dev)
+                _, s0, e0 = ov.units[0]  # what a chunk runs beside the reductions
+                self.kernel = self._label(A[0, s0:e0], B[0], C[0, s0:e0], shared=True)
 
                 def step():
                     with compute_ctx(self.comp, self._mask):
@@ -131,6 +134,8 @@ class Workload:
                 ov = GatherOverlap(n, sh.padded, ws, dev, odt,
                                    gemm_chunks(n, sh.padded, a.chunks, dt, dev),
                                    pieces=a.comm_chunks, requested=a.chunks, impl=a.allgather)
+                s0, e0 = ov.chunks[0]  # what a chunk runs beside the gathers
+                self.kernel = self._label(A[s0:e0], Bl, Cl[s0:e0], shared=True)
 
                 def step():
                     with compute_ctx(self.comp, self._mask):
@@ -162,11 +167,12 @@ class Workload:
             del Bg
             rp = rs.padded
             Cl = torch.empty(ws * rp, sh.padded, device=dev, dtype=odt)
-            self.kernel = self._label(Al[:rp // 2], Bl, Cl[:rp // 2])
+            self.kernel = self._label(Al[:rp // 2], Bl, Cl[:rp // 2], shared=True)
             ring = BidirRing(Al, rp, ctx.rank, ws, dev)
 
             def step():
-                ring.step(self._mm, Bl, Cl, self.comp)
+                with gemm.shared_device():  # the hops' transfers run beside these GEMMs
+                    ring.step(self._mm, Bl, Cl, self.comp)
             self.flops = flop_gemm
             self.global_batch, self.parallelism = 1, f"ring{ws}"
         else:
@@ -197,10 +203,15 @@ class Workload:
         if self._mask is not None:
             torch.cuda.current_stream(self.ctx.device).wait_stream(self.comp)
 
-    def _label(self, A, B, C):
+    def _label(self, A, B, C, shared=False):
+        """The kernel the step's GEMMs run (shared: beside collectives, as
+        compute_ctx / the ring issue them, under gemm.shared_device)."""
         if not self.cuda:
             return "torch.matmul(cpu)"
-        return gemm.kernel_for(A, B, C) if self.backend == "native" else "hipBLASLt"
+        if self.backend != "native":
+            return "hipBLASLt"
+        with (gemm.shared_device() if shared else contextlib.nullcontext()):
+            return gemm.kernel_for(A, B, C)
 
     def _sync(self):
         if self.cuda:

@@ -80,6 +80,8 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     else:
         ov = ReduceOverlap(lb, gemm_chunks(n, n, w.chunks, w.dtype, dev), dev)
         extra["units"] = len(ov.units)
+        _, s0, e0 = ov.units[0]  # what a chunk runs beside the reductions
+        label = kernel_label(w, A[0, s0:e0], B[0], C[0, s0:e0], shared=True)
         compute, owner = compute_stream(dev, w.comm_cus)
         extra["comm_cus"] = w.comm_cus
 

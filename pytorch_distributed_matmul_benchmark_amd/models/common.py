@@ -13,6 +13,7 @@ new C — and a new gather list — every iteration).
 """
 from __future__ import annotations
 
+import contextlib
 from dataclasses import dataclass, field
 from typing import Callable, Dict, Optional
 
@@ -91,16 +92,20 @@ def gemm_fn(w: Workload, device: torch.device) -> Callable:
     return mm
 
 
-def kernel_label(w: Workload, A, B, out) -> str:
+def kernel_label(w: Workload, A, B, out, shared: bool = False) -> str:
+    """The kernel ``gemm_fn`` runs for this problem; ``shared``: as issued
+    beside collectives (under ``ops.gemm.shared_device``, like the overlap
+    schedules' GEMMs)."""
     if A.device.type != "cuda":
         return "torch.matmul(cpu)"
     if w.backend == "torch":
         return "torch._scaled_mm(hipBLASLt)" if w.dtype == _gemm.FP8 else "torch.matmul(hipBLASLt)"
-    if w.kernel == "auto":
-        padded = _gemm.padded_kernel_for(A, B)
-        if padded:
-            return f"{padded} (zero-padded K/N)"
-    return _gemm.kernel_for(A, B, out, kernel=w.kernel)
+    with (_gemm.shared_device() if shared else contextlib.nullcontext()):
+        if w.kernel == "auto":
+            padded = _gemm.padded_kernel_for(A, B)
+            if padded:
+                return f"{padded} (zero-padded K/N)"
+        return _gemm.kernel_for(A, B, out, kernel=w.kernel)
 
 
 def generator(device: torch.device, seed: int) -> torch.Generator:

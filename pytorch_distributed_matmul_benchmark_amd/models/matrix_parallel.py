@@ -113,6 +113,8 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
                            gemm_chunks(n, sh.padded, w.chunks, w.dtype, dev),
                            pieces=w.comm_chunks, requested=w.chunks, impl=w.allgather)
         extra["chunks"] = len(ov.chunks)
+        s0, e0 = ov.chunks[0]  # what a chunk runs beside the gathers
+        label = kernel_label(w, A[s0:e0], B_local, C_local[s0:e0], shared=True)
         extra["comm_pieces"] = ov.n_pieces
         extra["comm_cus"] = w.comm_cus
         compute, owner = compute_stream(dev, w.comm_cus)

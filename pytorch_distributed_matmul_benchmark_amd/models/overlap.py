@@ -31,6 +31,7 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from ..ops import gemm
 from ..parallel.comm import CommStream, current_stream, new_event
 from ..parallel.dist import DistContext
 from ..utils.metrics import gemm_flops, tflops_from
@@ -52,8 +53,8 @@ def run(w: Workload, ctx: DistContext, mode: str = "overlap", depth: int = None)
     Bs = [randn((n, n), w, dev, seed=100 * (w.seed + ctx.rank) + 2 * i + 1, operand="B") for i in range(depth)]
     Cs = [torch.empty((n, n), device=dev, dtype=out_dtype(w)) for _ in range(depth)]
     mm = gemm_fn(w, dev)
-    label = kernel_label(w, As[0], Bs[0], Cs[0])
     distributed = ctx.is_distributed
+    label = kernel_label(w, As[0], Bs[0], Cs[0], shared=depth > 1 and distributed)
     compute = current_stream(dev)
 
     used = [True] + [False] * (depth - 1)
@@ -77,7 +78,8 @@ def run(w: Workload, ctx: DistContext, mode: str = "overlap", depth: int = None)
                 counter[0] += 1
                 if used[i] and compute is not None:
                     compute.wait_event(done[i])   # WAR: buffer's previous reduce finished
-                mm(As[i], Bs[i], Cs[i])
+                with gemm.shared_device():  # earlier buffers' all-reduces run beside it
+                    mm(As[i], Bs[i], Cs[i])
                 ready[i].record(compute)
                 cs.all_reduce(Cs[i], after=ready[i], done=done[i])
                 used[i] = True

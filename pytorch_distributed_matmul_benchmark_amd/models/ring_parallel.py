@@ -42,6 +42,7 @@ from __future__ import annotations
 
 import torch
 
+from ..ops import gemm
 from ..parallel.comm import current_stream
 from ..parallel.overlap import BidirRing
 from ..parallel.dist import DistContext
@@ -94,12 +95,13 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     rp = rs.padded
     C_local = torch.empty((ws * rp, csh.padded), device=dev, dtype=out_dtype(w))
     mm = gemm_fn(w, dev)
-    label = kernel_label(w, A_local[:rp // 2], B_local, C_local[:rp // 2])
+    label = kernel_label(w, A_local[:rp // 2], B_local, C_local[:rp // 2], shared=True)
     compute = current_stream(dev)
     ring = BidirRing(A_local, rp, r, ws, dev)
 
     def step():
-        ring.step(mm, B_local, C_local, compute)
+        with gemm.shared_device():  # the hops' transfers run beside these GEMMs
+            ring.step(mm, B_local, C_local, compute)
 
     warmup(step, w, ctx)
     align_ranks(ctx)

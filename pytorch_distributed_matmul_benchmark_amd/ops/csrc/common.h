@@ -197,8 +197,11 @@ __device__ __forceinline__ void tile_trace_write(const GemmArgs& a, const TileTr
 // clamped with 32-bit scalar logic (SALU has no 64-bit less-than).
 __device__ __forceinline__ u32x4 make_rsrc(const char* base, long long bytes) {
   const unsigned long long p = (unsigned long long)base;
-  const unsigned int hi = (unsigned int)((unsigned long long)bytes >> 32);
-  const unsigned int lo = (unsigned int)bytes;
+  unsigned int hi = (unsigned int)((unsigned long long)bytes >> 32);
+  unsigned int lo = (unsigned int)bytes;
+  // opaque halves: otherwise hipcc folds the clamp back into a 64-bit compare,
+  // which SALU lacks, and keeps its constant in a VGPR pair
+  asm("" : "+s"(hi), "+s"(lo));
   const unsigned int nr = (hi & 0x80000000u) ? 0u : (hi ? 0xffffffffu : lo);
   u32x4 r;
   r.x = (unsigned int)p;

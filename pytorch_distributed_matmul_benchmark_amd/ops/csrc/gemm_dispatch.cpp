@@ -88,6 +88,9 @@ static bool is_experiment(int k) {
   }
 }
 
+static bool w4s_fits(const Problem& p);
+static bool w4s_auto(const Problem& p);
+
 struct Plan {
   int kernel;  // kMfmaW4 | kT128 | -1
   int splitk;
@@ -116,13 +119,17 @@ int resolve_kernel(const Problem& p, int kernel) {
     // that fill the chip, T128 for under-filled ones: plan()), SCHED 3 for
     // edge tiles.
     case kAuto:
-      if (w4 || t128 || t256) return plan(p, kAuto).kernel;
+      if (w4 || t128 || t256) {
+        const Plan pl = plan(p, kAuto);
+        return pl.kernel == kMfmaW4 && pl.splitk == 1 && w4s_auto(p) ? kMfmaW4S : pl.kernel;
+      }
       // fp32: the 4-wave kernel (150.4 vs 150.1 TF for f32_256s at 16k,
       // profiles/r2_f32_w4_ab_v2.jsonl; hipBLASLt 154.4).
       return fast ? kMfma256d : f32fast ? kF32W4 : kGeneric;
     case kGeneric: return kGeneric;
     case kMfma256d: return fast ? kMfma256d : -1;
     case kMfmaW4: return w4 ? kMfmaW4 : -1;
+    case kMfmaW4S: return w4 && w4s_fits(p) ? kMfmaW4S : -1;
     case kT128: return t128 ? kT128 : -1;
     case kT128x2: return t128 ? kT128x2 : -1;  // shares T128's constraints
     case kT256x128: return t256 ? kT256x128 : -1;
@@ -134,8 +141,9 @@ int resolve_kernel(const Problem& p, int kernel) {
     case kMfma256X1: case kMfma256X2: case kMfma256X4: case kMfma256Stamp:
       return (fast && p.dtype == kBF16) ? kernel : -1;
     case kMfmaW4Tall: case kMfmaW4Wide: case kMfmaW4Il32: case kMfmaW4Trace:
-    case kMfmaW4Pers: case kMfmaW4PersTrace:
+    case kMfmaW4PersTrace:
       return (p.dtype == kBF16 && w4) ? kernel : -1;
+    case kMfmaW4Pers: return w4 ? kernel : -1;  // bf16 and fp16
 #endif
     default: return -1;
   }
@@ -201,6 +209,22 @@ static int device_cus() {
   return n[dev];
 }
 
+// W4S (gemm_w4.hip): an even number (>= 6) of K-tiles and a grid of whole
+// 8-XCD rounds. Auto picks it over W4 for >= 2 tiles per CU on a device the
+// GEMM has to itself (p.cus == 0): its tiles are assigned statically, so a CU
+// held by a concurrent kernel (an RCCL collective of an overlap schedule:
+// gemm.shared_device, Problem::cus < 0) would hold back a whole tile
+// sequence; there, and on CU-masked streams, the dispatch-balanced W4 runs.
+// Measured (profiles/r2_w4s_ab.jsonl): +3.1 % at 16384^2 x 2048, +2.8 % at
+// K = 4096, +2.2 % on the 16384 x 2048 x 16384 ws=8 shard, +0.1 % at 16k.
+static bool w4s_fits(const Problem& p) {
+  const int nk = p.K / 64;
+  return (p.dtype == kBF16 || p.dtype == kF16) && nk % 2 == 0 && nk >= 6 && device_cus() % 8 == 0;
+}
+static bool w4s_auto(const Problem& p) {
+  return p.cus == 0 && w4s_fits(p) && tiles_of(p, kMfmaW4) >= 2LL * device_cus();
+}
+
 static double plan_cost(const Problem& p, int kernel, int S) {
   const KernelModel& m = model_of(kernel);
   const long long T = tiles_of(p, kernel);
@@ -260,6 +284,7 @@ static bool is_tiled(int k) { return k == kMfmaW4 || k == kT128 || k == kT128x2 
 
 int choose_splitk(const Problem& p, int kernel) {
   const int k = resolve_kernel(p, kernel);
+  if (k == kMfmaW4S) return 1;
   if (!is_tiled(k)) return 0;
   return plan(p, k).splitk;
 }
@@ -316,6 +341,13 @@ static hipError_t tiled_launch(const Problem& p, int k, GemmArgs a, void* part, 
     }
   }
   a.splitk = S;
+  if (sub == 7) {  // W4S: unsplit, one workgroup per usable CU (a multiple of 8)
+    if (S > 1) {
+      sub = 0;
+    } else {
+      a.pers_grid = ((p.cus > 0 ? p.cus : device_cus()) / 8) * 8;
+    }
+  }
   if (sub == 5 || sub == 6) {  // persistent W4: unsplit, needs the stream's queue
     unsigned* c = S > 1 ? nullptr : stream_counters(stream);
     if (!c) {
@@ -528,6 +560,7 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kT128:
     case kT128x2:
     case kT256x128: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream);
+    case kMfmaW4S: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 7);
     case kF32_256s: return gemm_f32_256_launch(a, 1, stream);
     case kF32W4: return gemm_f32_w4_launch(a, stream);
 #ifdef PDMB_EXPERIMENTS
@@ -631,6 +664,7 @@ const char* kernel_name(int kernel) {
     case kF32_256s: return "pdmb_f32_256s_nn";
     case kFp8W4: return "pdmb_fp8_w4_nt";
     case kMfmaW4: return "pdmb_w4_nn";
+    case kMfmaW4S: return "pdmb_w4s";
     case kT128: return "pdmb_t128_nn";
     case kT128x2: return "pdmb_t128x2_nn";
     case kT256x128: return "pdmb_t256x128_nn";

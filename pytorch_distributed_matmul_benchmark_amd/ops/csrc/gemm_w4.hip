@@ -64,6 +64,17 @@ template <>
 __device__ __forceinline__ void mfma_acc<kF16>(f32x4& acc, const s16x8& b, const s16x8& a) {
   asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
 }
+// acc = B * A with C = 0: starts an accumulator without zeroing it first.
+template <int DT>
+__device__ __forceinline__ void mfma_zero(f32x4& acc, const s16x8& b, const s16x8& a);
+template <>
+__device__ __forceinline__ void mfma_zero<kBF16>(f32x4& acc, const s16x8& b, const s16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&a"(acc) : "v"(b), "v"(a));
+}
+template <>
+__device__ __forceinline__ void mfma_zero<kF16>(f32x4& acc, const s16x8& b, const s16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=&a"(acc) : "v"(b), "v"(a));
+}
 
 // LDS-DMA with a scalar offset; M0 is clobbered (declared), not saved.
 __device__ __forceinline__ void dma16_m0(u32x4 rsrc, uint32_t voff, uint32_t soff, uint32_t lds) {
@@ -74,6 +85,20 @@ __device__ __forceinline__ void dma16_m0(u32x4 rsrc, uint32_t voff, uint32_t sof
       :
       : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds)
       : "memory", "m0");
+}
+
+// LDS-DMA to M0 = lds0w + OFF, OFF an immediate (known once the K-tile's
+// item loop is unrolled): M0 is formed by the one SALU add that replaces
+// the s_mov, instead of from ~32 precomputed addresses held in SGPRs.
+__device__ __forceinline__ void dma16_at(u32x4 rsrc, uint32_t voff, uint32_t soff, uint32_t lds0w,
+                                         uint32_t off) {
+  asm volatile(
+      "s_add_u32 m0, %3, %4\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %0, %1, %2 offen lds"
+      :
+      : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds0w), "i"(off)
+      : "memory", "m0", "scc");
 }
 
 struct Frag {  // one 16-row (A) or 16-column (B) block of a K-tile: k 0..31 and 32..63
@@ -92,6 +117,7 @@ struct Ctx {
   uint32_t boff[2][4];  // [stage][jj]: B block j uses jj = bjj<IL>(j)
   int wu;
   uint32_t lds0;
+  uint32_t lds0w;  // lds0 + wu * 1 KiB: every DMA piece's per-wave LDS offset
 };
 
 // B block j (16 output columns wc*128 + 16j of the wave) lives in half bhalf
@@ -108,13 +134,14 @@ __device__ __forceinline__ constexpr int bjj(int j) { return IL == 64 ? j & 3 : 
 // serves all pieces; nq shifts the source by IL columns.
 template <int IL>
 __device__ __forceinline__ void issue_piece(const Ctx& c, u32x4 rb, int so, int tile, int h) {
+  // per-wave part (A: wu * 8 rows * 128 B, B: wu * 4 k-rows * 256 B) in lds0w
   if (h < 8) {
-    dma16_m0(c.ra, c.voffA, (uint32_t)tile * (BK * 2) + (uint32_t)(h * 32 * c.lda2),
-             c.lds0 + so + (h * 32 + c.wu * 8) * 128);
+    dma16_at(c.ra, c.voffA, (uint32_t)tile * (BK * 2) + (uint32_t)(h * 32 * c.lda2), c.lds0w,
+             so + h * 32 * 128);
   } else {
     const int nq = (h - 8) >> 2, kb = (h - 8) & 3;
-    dma16_m0(rb, c.voffB, (uint32_t)(kb * 16 * c.ldb2 + nq * IL * 2),
-             c.lds0 + so + A_BYTES + nq * BH_BYTES + (kb * 16 + c.wu * 4) * 256);
+    dma16_at(rb, c.voffB, (uint32_t)(kb * 16 * c.ldb2 + nq * IL * 2), c.lds0w,
+             so + A_BYTES + nq * BH_BYTES + kb * 16 * 256);
   }
 }
 
@@ -249,6 +276,7 @@ __device__ __forceinline__ unsigned w4_tile(const GemmArgs& a, char* smem, int v
   Ctx c;
   c.wu = wu;
   c.lds0 = (uint32_t)(size_t)((lds_void*)smem);
+  c.lds0w = c.lds0 + wu * 1024;
   c.lda2 = a.lda * 2;
   c.ldb2 = a.ldb * 2;
   {
@@ -432,6 +460,305 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4_pers(GemmArgs a) {
   }
 }
 
+// ---- W4S: streaming persistent W4 -----------------------------------------
+// The tile timeline (profiles/r2_tile_timeline_*.jsonl) puts ~7.4 us of a
+// 16k tile outside its K-loop: the first DMA latency (prologue, 2.2), the C
+// epilogue (4.9) and the dispatch gap (0.3-0.7) — ~2 % at K = 16384, ~8 % at
+// K = 4096 — and with one workgroup per CU (W4 holds all 512 registers of
+// every SIMD) nothing else on the CU can hide them. W4S runs a CU's tiles as
+// ONE K-tile stream: the DMA items that would fetch K-tiles nk, nk+1, nk+2
+// of the current tile fetch K-tiles 0, 1, 2 of the CU's next tile instead,
+// the last K-tile reads the next tile's first fragments as usual, and the
+// epilogue goes out through its own LDS region (past the two stages) while
+// those land. Its 32 stores per wave are not drained: vmcnt counts loads,
+// stores and LDS-DMA together in issue order, so the first two K-tiles of
+// the next tile wait with vmcnt(16 + 32) where they would wait vmcnt(16).
+// Tiles are assigned statically (workgroup b: tiles b, b + G, b + 2G, ...,
+// G = grid, a multiple of 8 so a tile stays on map_tile's XCD): every
+// workgroup must be resident at once (one per CU) — the host launches it only
+// for grids of >= 2 tiles per workgroup on an unmasked device.
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+struct Src {  // one output tile's operand sources
+  u32x4 ra;           // A at row m0, K = 0
+  const char* Bb;     // B at row 0, column n0
+  long long b_bytes;  // bytes from Bb to the end of B's extent
+};
+
+__device__ __forceinline__ Src tile_src(const GemmArgs& a, int bz, int tm, int tn) {
+  const int m0 = tm * BM, n0 = tn * BN;
+  Src s;
+  s.ra = make_rsrc((const char*)a.A + ((long long)bz * a.sA + (long long)m0 * a.lda) * 2,
+                   ((long long)(a.M - m0 - 1) * a.lda + a.K) * 2);
+  s.Bb = (const char*)a.B + ((long long)bz * a.sB + n0) * 2;
+  s.b_bytes = ((long long)(a.K - 1) * a.ldb + (a.N - n0)) * 2;
+  return s;
+}
+
+__device__ __forceinline__ u32x4 src_b(const Src& s, int kt, int ldb2) {
+  const long long off = (long long)kt * BK * ldb2;
+  return make_rsrc(s.Bb + off, s.b_bytes - off);
+}
+
+// ktile with explicit DMA targets (A of the item "t+2": descriptor raT at K
+// byte offset kaT; B of "t+3": descriptor rbT at its K-tile) and wait counts
+// (W0 at Bar0, W1 at Bar_mid); otherwise ktile<DT, 64, SO> item for item.
+// ZERO (K-tile 0 of a tile): the first MFMA of every accumulator takes C = 0.
+template <int DT, int SO, int W0, int W1, bool ZERO = false>
+__device__ __forceinline__ void ktile_s(const Ctx& c, const char* smem, u32x4 raT, uint32_t kaT,
+                                        u32x4 rbT, f32x4 (&acc)[8][8], Frag (&A)[8], Frag& A7c,
+                                        Frag& A7n, Frag (&Bc)[8], Frag (&Bn)[8]) {
+  constexpr int IL = 64;
+  constexpr int SN = STAGE - SO;
+  constexpr int sn = SN / STAGE;
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    if (mi == 0) {
+      wait_vm_lgkm_barrier<W0>();
+      __builtin_amdgcn_sched_barrier(0);
+    } else if (mi == 4) {
+      wait_vm_lgkm_barrier<W1>();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int gap = 0; gap < 16; ++gap) {
+      const int ks = gap >> 3, ni = gap & 7;
+      if (ZERO && ks == 0)
+        mfma_zero<DT>(acc[mi][ni], Bc[ni].k[ks], mi == 7 ? A7c.k[ks] : A[mi].k[ks]);
+      else
+        mfma_acc<DT>(acc[mi][ni], Bc[ni].k[ks], mi == 7 ? A7c.k[ks] : A[mi].k[ks]);
+      const int it = kItems[mi][gap];
+      if (it == 1) {
+        const int h = piece_of(mi, gap);
+        if (h < 8) {
+          dma16_at(raT, c.voffA, kaT + (uint32_t)(h * 32 * c.lda2), c.lds0w, SO + h * 32 * 128);
+        } else {
+          const int nq = (h - 8) >> 2, kb = (h - 8) & 3;
+          dma16_at(rbT, c.voffB, (uint32_t)(kb * 16 * c.ldb2 + nq * IL * 2), c.lds0w,
+                   SN + A_BYTES + nq * BH_BYTES + kb * 16 * 256);
+        }
+      } else if (it >= 100 && it < 200) {
+        const int s = (it - 100) >> 1, h = (it - 100) & 1;
+        Bn[s].k[h] = frag_b<IL>(smem, c.boff[sn][bjj<IL>(s)], s, h);
+      } else if (it >= 214) {
+        const int h = it - 214;
+        A7n.k[h] = frag_a(smem, c.aoff[sn][h], 7);
+      } else if (it >= 200) {
+        const int m = (it - 200) >> 1, h = (it - 200) & 1;
+        A[m].k[h] = frag_a(smem, c.aoff[sn][h], m);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(NT, 1) gemm_w4s(GemmArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 4 * kEpiBuf];
+  constexpr int IL = 64;
+  const int T = a.tiles_m * a.tiles_n * a.batch;
+  const int G = gridDim.x;
+  int vb = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wu >> 1, wc = wu & 1;
+  const int l16 = lane & 15, g = lane >> 4;
+
+  Ctx c;
+  c.wu = wu;
+  c.lds0 = (uint32_t)(size_t)((lds_void*)smem);
+  c.lds0w = c.lds0 + wu * 1024;
+  c.lda2 = a.lda * 2;
+  c.ldb2 = a.ldb * 2;
+  c.nk = a.K / BK;
+  {
+    const int r = wu * 8 + (lane >> 3), lc8 = lane & 7;
+    c.voffA = (uint32_t)(r * c.lda2 + ((lc8 ^ ((r >> 1) & 7)) * 16));
+    const int lr16 = lane >> 4, lc16 = lane & 15;
+    const int k = wu * 4 + lr16;
+    const int s = (k & 3) | (((k >> 3) & 1) << 2);
+    const int p = ((lc16 >> 1) ^ s) * 16 + (lc16 & 1) * 8;
+    const int n = (p / IL) * 2 * IL + (p % IL);
+    c.voffB = (uint32_t)(k * c.ldb2 + n * 2);
+    const int swA = (l16 >> 1) & 7;
+    const int q4 = l16 >> 2, p4 = l16 & 3;
+    const int sB = q4 | ((g & 1) << 2);
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        uint32_t ao = (uint32_t)(st * STAGE + (wr * 128 + l16) * 128 + (((4 * ks + g) ^ swA) * 16));
+        asm volatile("" : "+v"(ao));
+        c.aoff[st][ks] = ao;
+      }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int u = 4 * wc + jj;
+        uint32_t bo = (uint32_t)(st * STAGE + (8 * g + q4) * 256 + ((u ^ sB) * 32) + p4 * 8);
+        asm volatile("" : "+v"(bo));
+        c.boff[st][jj] = bo;
+      }
+    }
+  }
+  const int nk = c.nk;
+
+  int bz, tm, tn;
+  map_tile(a, vb, bz, tm, tn);
+  Src cur = tile_src(a, bz, tm, tn);
+  int nvb = vb + G, nbz = bz, ntm = tm, ntn = tn;
+  Src nxt = cur;
+  if (nvb < T) {
+    map_tile(a, nvb, nbz, ntm, ntn);
+    nxt = tile_src(a, nbz, ntm, ntn);
+  }
+
+  f32x4 acc[8][8];  // started by each tile's K-tile 0 (ktile_s ZERO)
+
+  // Prologue of the first tile, as W4's: A(0), B(0) -> stage 0; B(1), A(1)
+  // -> stage 1; fragments of K-tile 0; then B(2) -> stage 0.B.
+  auto dma_a = [&](const u32x4& ra, uint32_t ka, int so, int h) {
+    dma16_at(ra, c.voffA, ka + (uint32_t)(h * 32 * c.lda2), c.lds0w, so + h * 32 * 128);
+  };
+  auto dma_b = [&](const u32x4& rb, int so, int h) {
+    const int nq = (h - 8) >> 2, kb = (h - 8) & 3;
+    dma16_at(rb, c.voffB, (uint32_t)(kb * 16 * c.ldb2 + nq * IL * 2), c.lds0w,
+             so + A_BYTES + nq * BH_BYTES + kb * 16 * 256);
+  };
+  {
+    const u32x4 rb0 = src_b(cur, 0, c.ldb2), rb1 = src_b(cur, 1, c.ldb2);
+#pragma unroll
+    for (int h = 0; h < 16; ++h) {
+      if (h < 8)
+        dma_a(cur.ra, 0u, 0, h);
+      else
+        dma_b(rb0, 0, h);
+    }
+#pragma unroll
+    for (int h = 8; h < 16; ++h) dma_b(rb1, STAGE, h);
+#pragma unroll
+    for (int h = 0; h < 8; ++h) dma_a(cur.ra, BK * 2, STAGE, h);
+  }
+  asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+  Frag A[8], A7a, A7b, B0[8], B1[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      A[i].k[ks] = frag_a(smem, c.aoff[0][ks], i);
+      B0[i].k[ks] = frag_b<IL>(smem, c.boff[0][bjj<IL>(i)], i, ks);
+    }
+  A7a = A[7];
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  {
+    const u32x4 rb2 = src_b(cur, 2, c.ldb2);
+#pragma unroll
+    for (int h = 8; h < 16; ++h) dma_b(rb2, 0, h);
+  }
+
+  char* ebuf = smem + 2 * STAGE + wu * kEpiBuf;
+  // 32 out-of-range LDS-DMA loads (num_records 0: no memory access; zeros
+  // into this wave's epilogue buffer) in the place of the 32 epilogue stores
+  // that precede every later tile's first K-tile: every tile, the first one
+  // included, then runs the same code with the same vmcnt counts.
+  {
+    u32x4 nul;
+    nul.x = 0u;
+    nul.y = 0u;
+    nul.z = 0u;
+    nul.w = 0x00020000u;
+    const uint32_t eb = c.lds0 + 2 * STAGE + wu * kEpiBuf;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) dma16_m0(nul, 0u, 0u, eb);
+  }
+  for (;;) {
+    const bool more = nvb < T;
+    // DMA targets of item "kt" (A: t+2, B: t+3): this tile, the next, or
+    // (last tile) a harmless re-read of this tile's last K-tile. Scalar
+    // selects, then one descriptor: no branch in the MFMA stream.
+    // 32-bit bitwise selects (m = all ones: this tile) stay on the SALU
+    auto sel = [](uint32_t m, uint32_t x, uint32_t y) { return (x & m) | (y & ~m); };
+    auto tgt_a = [&](int kt, u32x4& r, uint32_t& ka) {
+      const uint32_t m = (kt < nk || !more) ? ~0u : 0u;
+      const int k = kt < nk ? kt : (more ? kt - nk : nk - 1);
+      r.x = sel(m, cur.ra.x, nxt.ra.x);
+      r.y = sel(m, cur.ra.y, nxt.ra.y);
+      r.z = sel(m, cur.ra.z, nxt.ra.z);
+      r.w = cur.ra.w;
+      ka = (uint32_t)k * (BK * 2);
+    };
+    auto tgt_b = [&](int kt) -> u32x4 {
+      const uint32_t m = (kt < nk || !more) ? ~0u : 0u;
+      const int k = kt < nk ? kt : (more ? kt - nk : nk - 1);
+      const unsigned long long pc = (unsigned long long)cur.Bb, pn = (unsigned long long)nxt.Bb;
+      const unsigned long long bc = (unsigned long long)cur.b_bytes, bn = (unsigned long long)nxt.b_bytes;
+      const unsigned long long p = ((unsigned long long)sel(m, (uint32_t)(pc >> 32), (uint32_t)(pn >> 32)) << 32) |
+                                   sel(m, (uint32_t)pc, (uint32_t)pn);
+      const long long bytes = (long long)(((unsigned long long)sel(m, (uint32_t)(bc >> 32), (uint32_t)(bn >> 32)) << 32) |
+                                          sel(m, (uint32_t)bc, (uint32_t)bn));
+      const long long off = (long long)k * BK * c.ldb2;
+      return make_rsrc((const char*)p + off, bytes - off);
+    };
+    // K-tiles 0 and 1 (32 stores or dummies per wave are younger than the
+    // DMAs they wait for), then pairs whose DMA targets stay in this tile
+    // (W4's instruction mix: no selects), then the last two pairs, whose
+    // targets cross into the next tile (nk >= 6: host-checked).
+    ktile_s<DT, 0, 48, 48, true>(c, smem, cur.ra, 2 * (BK * 2), src_b(cur, 3, c.ldb2), acc, A, A7a,
+                                 A7b, B0, B1);
+    ktile_s<DT, STAGE, 48, 16>(c, smem, cur.ra, 3 * (BK * 2), src_b(cur, 4, c.ldb2), acc, A, A7b, A7a,
+                               B1, B0);
+    int t = 2;
+    for (; t + 4 < nk; t += 2) {
+      ktile_s<DT, 0, 16, 16>(c, smem, cur.ra, (uint32_t)(t + 2) * (BK * 2), src_b(cur, t + 3, c.ldb2),
+                             acc, A, A7a, A7b, B0, B1);
+      ktile_s<DT, STAGE, 16, 16>(c, smem, cur.ra, (uint32_t)(t + 3) * (BK * 2),
+                                 src_b(cur, t + 4, c.ldb2), acc, A, A7b, A7a, B1, B0);
+    }
+    for (; t < nk; t += 2) {
+      u32x4 ra;
+      uint32_t ka;
+      tgt_a(t + 2, ra, ka);
+      ktile_s<DT, 0, 16, 16>(c, smem, ra, ka, tgt_b(t + 3), acc, A, A7a, A7b, B0, B1);
+      tgt_a(t + 3, ra, ka);
+      ktile_s<DT, STAGE, 16, 16>(c, smem, ra, ka, tgt_b(t + 4), acc, A, A7b, A7a, B1, B0);
+    }
+    // The last MFMAs write their AGPRs before the epilogue reads them (asm
+    // MFMAs are invisible to hipcc's hazard recognizer).
+    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    char* Cb = (char*)a.C + (long long)bz * a.sC * 2;
+    // lane id from v_mbcnt (no live-in): the store offsets are formed here
+    // instead of being kept live through the K-loop (where they spilled)
+    unsigned all = ~0u;
+    asm volatile("" : "+s"(all));  // per tile, so the mbcnt is not hoisted either
+    const int eln = (int)__builtin_amdgcn_mbcnt_hi(all, __builtin_amdgcn_mbcnt_lo(all, 0u));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      f32x4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = acc[i][j];
+      store_block16<DT, false, false>(ebuf, v, 1.0f, Cb, (long long)a.ldc * 2,
+                                      tm * BM + wr * 128 + i * 16, tn * BN + wc * 128, a.M, a.N, eln);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (!more) break;
+    vb = nvb;
+    bz = nbz;
+    tm = ntm;
+    tn = ntn;
+    cur = nxt;
+    nvb = vb + G;
+    if (nvb < T) {
+      map_tile(a, nvb, nbz, ntm, ntn);
+      nxt = tile_src(a, nbz, ntm, ntn);
+    }
+  }
+  // No LDS-DMA may still be writing when this workgroup's LDS is handed on.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 }  // namespace kw4
 
 bool gemm_w4_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c) {
@@ -493,6 +820,17 @@ hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
     return hipGetLastError();
   }
 #endif
+  if (sub == 7) {  // W4S: streaming persistent, static tiles (nk even, >= 6)
+    if (S > 1 || a.pers_grid <= 0 || a.pers_grid % 8 || (a.K / kw4::BK) % 2 || a.K / kw4::BK < 6)
+      return hipErrorInvalidValue;
+    const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
+    if (dt == kBF16)
+      hipLaunchKernelGGL((kw4::gemm_w4s<kBF16>), pg, block, 0, stream, a);
+    else
+      hipLaunchKernelGGL((kw4::gemm_w4s<kF16>), pg, block, 0, stream, a);
+    return hipGetLastError();
+  }
+#ifdef PDMB_EXPERIMENTS
   if (sub == 5) {  // persistent (per-XCD work queues), unsplit only
     if (S > 1 || !a.queue || a.pers_grid <= 0) return hipErrorInvalidValue;
     const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
@@ -502,6 +840,7 @@ hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
       hipLaunchKernelGGL((kw4::gemm_w4_pers<kF16>), pg, block, 0, stream, a);
     return hipGetLastError();
   }
+#endif
   if (sub != 0) return hipErrorInvalidValue;
   if (dt == kBF16)
     hipLaunchKernelGGL(kw4::gemm_w4_nn<kBF16>, grid, block, 0, stream, a);

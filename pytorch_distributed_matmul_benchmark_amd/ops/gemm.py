@@ -24,7 +24,7 @@ from . import _native
 
 # The shipping kernels: the public ``kernel=`` surface (api.h ``Kernel``).
 KERNELS = {"auto": 0, "generic": 2, "f32_256s": 7, "mfma256d": 9, "fp8_w4": 16, "w4": 21,
-           "t128": 26, "t128x2": 27, "t256x128": 28, "f32_w4": 29}
+           "t128": 26, "t128x2": 27, "t256x128": 28, "f32_w4": 29, "w4s": 36}
 # A/B and timing-only diagnostic kernels (api.h ``ExperimentKernel``): accepted
 # only by a library built with ``PDMB_EXPERIMENTS=1``; ``diag_*`` ones skip waits
 # or data movement on purpose and compute WRONG results.
@@ -37,7 +37,8 @@ EXPERIMENT_KERNELS = {"mfma256": 1, "mfma256b": 3, "mfma256c": 4, "mfma256c_stam
                       "diag_fp8_w4_trace": 33, "x_w4_pers": 34, "diag_w4_pers_trace": 35}
 KERNEL_NAMES = {0: "auto", 2: "pdmb_generic_nn", 7: "pdmb_f32_256s_nn", 9: "pdmb_mfma256d_nn",
                 16: "pdmb_fp8_w4_nt", 21: "pdmb_w4_nn", 26: "pdmb_t128_nn",
-                27: "pdmb_t128x2_nn", 28: "pdmb_t256x128_nn", 29: "pdmb_f32_w4_nn", 1: "pdmb_mfma256_nn",
+                27: "pdmb_t128x2_nn", 28: "pdmb_t256x128_nn", 29: "pdmb_f32_w4_nn", 36: "pdmb_w4s",
+                1: "pdmb_mfma256_nn",
                 3: "pdmb_mfma256b_nn", 4: "pdmb_mfma256c_nn", 5: "pdmb_mfma256c_stamp",
                 6: "pdmb_f32_256_nn", 15: "pdmb_fp8_256_nt", -1: "unsupported"}
 SUPPORTED_DTYPES = (torch.float32, torch.float16, torch.bfloat16)
@@ -60,8 +61,27 @@ def cu_budget(cus: int):
         _budget.cus = prev
 
 
+@contextlib.contextmanager
+def shared_device():
+    """GEMMs issued in this block (this thread) share the device with
+    concurrent kernels (the RCCL collectives of an overlap schedule): the
+    planner then keeps to kernels whose tiles the hardware dispatches as CUs
+    free up, never a persistent one (W4S) that assumes every CU is its own."""
+    prev = getattr(_budget, "shared", False)
+    _budget.shared = True
+    try:
+        yield
+    finally:
+        _budget.shared = prev
+
+
 def _cus() -> int:
-    return getattr(_budget, "cus", 0)
+    """CU budget for the C++ planner: > 0 a masked stream's CUs, 0 the whole
+    device to itself, -1 the whole device shared (shared_device)."""
+    cus = getattr(_budget, "cus", 0)
+    if cus == 0 and getattr(_budget, "shared", False):
+        return -1
+    return cus
 
 
 def experiments_built() -> bool:

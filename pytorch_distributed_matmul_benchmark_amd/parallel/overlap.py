@@ -98,16 +98,22 @@ class MaskedStream:
 
 
 def compute_ctx(stream, owner):
-    """Context for issuing GEMMs on a compute stream from ``compute_stream``:
-    the stream, plus the CU budget when it is a masked one."""
+    """Context for issuing GEMMs on a compute stream from ``compute_stream``
+    while collectives run beside them: the stream, the shared-device flag
+    (``ops.gemm.shared_device``: no persistent GEMM kernel that assumes every
+    CU is its own), plus the CU budget when the stream is a masked one."""
     import contextlib
 
+    from ..ops import gemm
+
+    st = contextlib.ExitStack()
+    st.enter_context(gemm.shared_device())
     if owner is None:
-        return stream_ctx(stream)
+        st.enter_context(stream_ctx(stream))
+        return st
     # the masked stream starts behind everything already queued on the
     # caller's stream (operand initialisation, the previous step's join)
     stream.wait_stream(torch.cuda.current_stream(owner.device))
-    st = contextlib.ExitStack()
     st.enter_context(stream_ctx(stream))
     st.enter_context(owner.budget())
     return st

@@ -218,8 +218,14 @@ void* scratch(hipStream_t s, size_t bytes) {
   return b.p;
 }
 
+// --overlap and ring_parallel run collectives beside the GEMMs: the planner
+// then keeps to dispatch-balanced kernels (Problem::cus = -1: no persistent
+// W4S, whose static tile assignment assumes every CU is its own).
+static bool g_shared_device = false;
+
 void gemm(const pdmb::Problem& p0, int kernel, hipStream_t s) {
   pdmb::Problem p = p0;
+  if (g_shared_device && p.cus == 0) p.cus = -1;
   const size_t need = pdmb::gemm_workspace_bytes(p, kernel);
   if (need) {
     p.workspace = scratch(s, need);
@@ -736,6 +742,7 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "error: %d GPU(s) requested, %d visible\n", o.gpus, ndev);
     return 2;
   }
+  g_shared_device = o.overlap || o.mode == kRingParallel;
   hipDeviceProp_t prop;
   (void)hipGetDeviceProperties(&prop, 0);
   std::printf("pdmb_bench (native HIP + RCCL executor)\n  GPU 0: %s (%s), %d CUs\n", prop.name,

@@ -32,7 +32,7 @@ def test_native_extension_is_loaded():
 FAST = ["mfma256d", "mfma256", "mfma256b", "mfma256c"]
 
 
-TILED = ("pdmb_w4_nn", "pdmb_t256x128_nn", "pdmb_t128_nn", "pdmb_t128x2_nn")
+TILED = ("pdmb_w4_nn", "pdmb_t256x128_nn", "pdmb_t128_nn", "pdmb_t128x2_nn", "pdmb_w4s")
 
 
 def _need(kernel):
@@ -387,8 +387,12 @@ def test_auto_plan_for_shard_shapes():
         A = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
         B = torch.empty(K, N, device="cuda", dtype=torch.bfloat16)
         return gemm.kernel_for(A, B), gemm.splitk_for(A, B)
-    assert plan(16384, 16384, 16384) == ("pdmb_w4_nn", 1)
-    assert plan(16384, 2048, 16384) == ("pdmb_w4_nn", 1)
+    # >= 2 tiles per CU, K / 64 even: the streaming W4S; shared device: W4
+    assert plan(16384, 16384, 16384) == ("pdmb_w4s", 1)
+    assert plan(16384, 2048, 16384) == ("pdmb_w4s", 1)
+    with gemm.shared_device():
+        assert plan(16384, 16384, 16384) == ("pdmb_w4_nn", 1)
+    assert plan(8192, 8192, 8192) == ("pdmb_w4s", 1)
     for shape in ((8192, 1024, 8192), (4096, 512, 4096), (2048, 2048, 2048), (4096, 2048, 4096)):
         k, S = plan(*shape)  # more workgroups than 256x256 tiles: a smaller tile or a split W4
         assert k in TILED[1:] or (k == "pdmb_w4_nn" and S > 1), (shape, k, S)
@@ -443,6 +447,34 @@ def test_persistent_w4_matches_w4_bitwise(b, M, N, K):
         gemm.matmul(A, B, out=out, kernel="x_w4_pers")
         assert torch.equal(out, ref)
     assert _relerr(ref, _ref(A, B)) < TOL[torch.bfloat16]
+
+
+@pytest.mark.parametrize("b,M,N,K", [(1, 256, 256, 384), (1, 2304, 1280, 384), (3, 1024, 768, 512),
+                                     (1, 4096, 4096, 512), (1, 8192, 2048, 1024), (1, 16384, 8192, 384),
+                                     (1, 4096, 4096, 640)])
+def test_streaming_w4s_matches_w4_bitwise(b, M, N, K):
+    """W4S (one K-tile stream per CU, overlapped epilogue): bitwise equal to W4
+    for one tile per workgroup, several, uneven counts (T not a multiple of the
+    grid) and batches."""
+    g = torch.Generator(device="cuda").manual_seed(b * 5 + M + N + K)
+    shape = (b,) if b > 1 else ()
+    A = torch.randn(*shape, M, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    B = torch.randn(*shape, K, N, device="cuda", dtype=torch.bfloat16, generator=g)
+    ref = gemm.matmul(A, B, kernel="w4", splitk=1)
+    for _ in range(2):
+        out = torch.full_like(ref, float("nan"))
+        gemm.matmul(A, B, out=out, kernel="w4s")
+        assert torch.equal(out, ref)
+
+
+def test_streaming_w4s_fp16_exact():
+    g = torch.Generator(device="cuda").manual_seed(5)
+    A = torch.randint(-3, 4, (2048, 1024), device="cuda", generator=g).to(torch.float16)
+    B = torch.randint(-3, 4, (1024, 4096), device="cuda", generator=g).to(torch.float16)
+    R = (A.double() @ B.double()).to(torch.float16)
+    assert torch.equal(gemm.matmul(A, B, kernel="w4s"), R)
+    with pytest.raises(RuntimeError):  # K / 64 odd: W4S cannot stream it
+        gemm.matmul(A[:, :960], B[:960], kernel="w4s")
 
 
 def test_persistent_w4_streams_graph_and_cu_budget():
