@@ -112,24 +112,33 @@ struct GemmArgs {
 // at 16k, a third of W4's per-tile fixed cost). Staged through a wave-private
 // LDS buffer, each 16-row block leaves as 4 dwordx4 stores of 4 whole 256-B
 // rows: a quarter of the requests, all of them whole lines.
-// Buffer rows are 264 B (256 + 8): the b64 writes (16 lanes = 16 rows, 2
-// banks each) and the b128 reads (16 lanes = one row) are conflict-free.
-constexpr int kEpiPitch = 264;
-constexpr int kEpiBuf = 16 * kEpiPitch;  // one 16-row block, 4224 B
+// Buffer rows are NB * 32 + 8 bytes (W4: 264): the b64 writes (16 lanes =
+// 16 rows, 2 banks each) and the b128 reads (16 B chunks of whole rows)
+// are conflict-free for NB = 8 and NB = 4.
+template <int NB>
+constexpr int epi_pitch() { return NB * 32 + 8; }
+template <int NB = 8>
+constexpr int epi_buf() { return 16 * epi_pitch<NB>(); }
+constexpr int kEpiPitch = epi_pitch<8>();
+constexpr int kEpiBuf = epi_buf<8>();  // one 16-row block of W4, 4224 B
 
-// Store block row v (v[j] = the fp32 C^T tile j, scaled by `alpha`) of a
-// wave's 16 x 128 output at (row0, col0) of C (row stride ldc_b bytes)
-// through `buf` (kEpiBuf bytes of LDS owned by this wave). MASK: rows >= M
-// are skipped, column chunks are cut at N (N % 4 == 0: a chunk is all, half
-// or none). SCALE: multiply by alpha (fp8's folded scales).
-template <int DT, bool MASK, bool SCALE>
-__device__ __forceinline__ void store_block16(char* buf, const f32x4 (&v)[8], float alpha, char* C,
+// Store block row v (v[j] = the fp32 C^T tile j, scaled by `alpha` if
+// SCALE) of a wave's 16 x (NB * 16) output at (row0, col0) of C (row stride
+// ldc_b bytes) through `buf` (epi_buf<NB>() bytes of LDS owned by this
+// wave). MASK: rows >= M are skipped, column chunks are cut at N (N % 4 ==
+// 0: a chunk is all, half or none).
+template <int DT, bool MASK, bool SCALE, int NB = 8>
+__device__ __forceinline__ void store_block16(char* buf, const f32x4 (&v)[NB], float alpha, char* C,
                                               long long ldc_b, int row0, int col0, int M, int N,
                                               int lane) {
+  constexpr int P = epi_pitch<NB>();
+  constexpr int CPR = NB * 2;    // 16-B chunks per row
+  constexpr int RPI = 64 / CPR;  // rows per read instruction
   const int l16 = lane & 15, g = lane >> 4;
-  lds_void* lb = (lds_void*)buf;
+  typedef __attribute__((address_space(3))) char lds_char;
+  lds_char* lb = (lds_char*)(lds_void*)buf;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
+  for (int j = 0; j < NB; ++j) {
     u32x2 w;
     if constexpr (SCALE) {
       w.x = pack2<DT>(v[j].x * alpha, v[j].y * alpha);
@@ -138,12 +147,13 @@ __device__ __forceinline__ void store_block16(char* buf, const f32x4 (&v)[8], fl
       w.x = pack2<DT>(v[j].x, v[j].y);
       w.y = pack2<DT>(v[j].z, v[j].w);
     }
-    *(lds_u32x2*)((__attribute__((address_space(3))) char*)lb + l16 * kEpiPitch + (j * 16 + 4 * g) * 2) = w;
+    *(lds_u32x2*)(lb + l16 * P + (j * 16 + 4 * g) * 2) = w;
   }
+  const int rl = lane / CPR, ch = lane % CPR;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const u32x4 x = *(lds_u32x4_t*)((__attribute__((address_space(3))) char*)lb + (4 * r + g) * kEpiPitch + l16 * 16);
-    const int row = row0 + 4 * r + g, col = col0 + 8 * l16;
+  for (int r = 0; r < 16 / RPI; ++r) {
+    const u32x4 x = *(lds_u32x4_t*)(lb + (RPI * r + rl) * P + ch * 16);
+    const int row = row0 + RPI * r + rl, col = col0 + 8 * ch;
     char* p = C + (long long)row * ldc_b + (long long)col * 2;
     if constexpr (MASK) {
       if (row < M) {

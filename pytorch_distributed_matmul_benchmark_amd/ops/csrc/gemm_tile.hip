@@ -330,9 +330,13 @@ __global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
                                         slice, acc, sl))
     return;
 
-  // Epilogue: acc[i][j] holds C^T of a 16x16 block: lane owns row l16 and
-  // columns 4g..4g+3 (interior tiles only: no masks).
+  // Epilogue: acc[i][j] holds C^T of a 16x16 block (lane: row l16, columns
+  // 4g..4g+3), stored through LDS as whole rows (common.h store_block16;
+  // interior tiles only: no masks) once every wave's DMAs have landed and
+  // every fragment read is done.
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   char* Cb = (char*)a.C + (long long)bz * a.sC * 2;
+  char* ebuf = smem + 1024 + wu * 2 * epi_buf<NB>();  // past splitk_meet's ticket word
 #pragma unroll
   for (int i = 0; i < MB; ++i) {
     f32x4 v[NB];
@@ -342,16 +346,9 @@ __global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
     } else {
       splitk_row<MB, NB, NT>(a, sl, slice, i, acc, v);
     }
-    const int row = m0 + wr * (C::BM / 2) + i * 16 + l16;
-    char* crow = Cb + (long long)row * a.ldc * 2;
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const int col = n0 + wc * (C::BN / 2) + j * 16 + 4 * g;
-      u32x2 w;
-      w.x = pack2<DT>(v[j].x, v[j].y);
-      w.y = pack2<DT>(v[j].z, v[j].w);
-      *(u32x2*)(crow + col * 2) = w;
-    }
+    store_block16<DT, false, false, NB>(ebuf + (i & 1) * epi_buf<NB>(), v, 1.0f, Cb,
+                                        (long long)a.ldc * 2, m0 + wr * (C::BM / 2) + i * 16,
+                                        n0 + wc * (C::BN / 2), a.M, a.N, lane);
   }
 }
 
