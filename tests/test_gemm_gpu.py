@@ -451,11 +451,13 @@ def test_persistent_w4_matches_w4_bitwise(b, M, N, K):
 
 @pytest.mark.parametrize("b,M,N,K", [(1, 256, 256, 384), (1, 2304, 1280, 384), (3, 1024, 768, 512),
                                      (1, 4096, 4096, 512), (1, 8192, 2048, 1024), (1, 16384, 8192, 384),
-                                     (1, 4096, 4096, 640)])
+                                     (1, 4096, 4096, 640), (1, 2048, 16384, 384), (1, 16384, 2048, 384),
+                                     (1, 1024, 32768, 384), (1, 32768, 1024, 384)])
 def test_streaming_w4s_matches_w4_bitwise(b, M, N, K):
     """W4S (one K-tile stream per CU, overlapped epilogue): bitwise equal to W4
     for one tile per workgroup, several, uneven counts (T not a multiple of the
-    grid) and batches."""
+    grid), batches, and >= 2 tiles per CU under every thin-grid block->tile map
+    (supertiles 2-5: 8x64, 64x8, 4x128 and 128x4 tile grids)."""
     g = torch.Generator(device="cuda").manual_seed(b * 5 + M + N + K)
     shape = (b,) if b > 1 else ()
     A = torch.randn(*shape, M, K, device="cuda", dtype=torch.bfloat16, generator=g)
