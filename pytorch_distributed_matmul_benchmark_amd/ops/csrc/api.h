@@ -19,6 +19,7 @@ enum Kernel : int {
   kT256x128 = 28, // gemm_tile.hip: 256x128 tile, 4 waves x 128x64, 3-stage ring (M % 256, N % 128)
   kF32W4 = 29,    // gemm_f32_w4.hip: exact fp32, 4 waves x 128x128, AGPR acc (fp32 auto)
   kMfmaW4S = 36,  // gemm_w4.hip W4S: W4 as one K-tile stream per CU (persistent, static tiles)
+  kFp8W4S = 37,   // gemm_fp8.hip: the fp8 W4 kernel as one K-tile stream per CU (interior tiles)
 };
 
 // Experiment / diagnostic ids (A/B and timing-only builds). Compiled and

@@ -240,6 +240,21 @@ __device__ __forceinline__ void dma16(u32x4 rsrc, uint32_t voff, uint32_t lds_ba
       : "memory");
 }
 
+// LDS-DMA with a scalar source offset to M0 = lds0w + OFF, OFF an immediate
+// (known once a K-tile's item loop is unrolled): M0 is formed by the one
+// SALU add that replaces an s_mov, instead of from ~32 precomputed addresses
+// held in SGPRs (W4: 96 -> 67 SGPRs; what made W4S fit). M0 is clobbered.
+__device__ __forceinline__ void dma16_at(u32x4 rsrc, uint32_t voff, uint32_t soff, uint32_t lds0w,
+                                         uint32_t off) {
+  asm volatile(
+      "s_add_u32 m0, %3, %4\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %0, %1, %2 offen lds"
+      :
+      : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds0w), "i"(off)
+      : "memory", "m0", "scc");
+}
+
 // ---- block -> output tile mapping -------------------------------------
 // Speed only (never correctness): workgroups are dealt round-robin over the
 // 8 XCDs (blocks b and b+8 share an XCD). In super-tile mode every "round"

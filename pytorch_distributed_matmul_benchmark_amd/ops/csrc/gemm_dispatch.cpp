@@ -23,6 +23,7 @@ hipError_t gemm_f32_256_launch(GemmArgs a, int variant, hipStream_t stream);
 hipError_t gemm_f32_w4_launch(GemmArgs a, hipStream_t stream);
 bool gemm_fp8_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream);
+bool gemm_fp8_w4s_fits(const GemmArgs& a);
 bool gemm_w4_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub = 0);
 bool gemm_tile_supported(int dt, int bm, const GemmArgs& a, size_t align_a, size_t align_b,
@@ -72,7 +73,7 @@ bool experiments_built() {
 }
 
 static bool is_fp8_kernel(int k) {
-  return k == kFp8W4 || k == kFp8 || k == kFp8W4Diag || k == kFp8W4Diag2 || k == kFp8W4Diag3 ||
+  return k == kFp8W4 || k == kFp8W4S || k == kFp8 || k == kFp8W4Diag || k == kFp8W4Diag2 || k == kFp8W4Diag3 ||
          k == kFp8W4Tall || k == kFp8W4Wide || k == kFp8W4Scaled || k == kFp8W4Trace;
 }
 
@@ -88,6 +89,7 @@ static bool is_experiment(int k) {
   }
 }
 
+static int device_cus();
 static bool w4s_fits(const Problem& p);
 static bool w4s_auto(const Problem& p);
 
@@ -100,11 +102,17 @@ static Plan plan(const Problem& p, int kernel);
 int resolve_kernel(const Problem& p, int kernel) {
   if (is_experiment(kernel) && !experiments_built()) return -1;
   const GemmArgs a = to_args(p);
-  if (p.dtype == kFP8)  // fp8 kernels only; no generic / padded fallback
-    return (kernel == kAuto || is_fp8_kernel(kernel)) &&
-                   gemm_fp8_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C)
-               ? (kernel == kAuto ? kFp8W4 : kernel)
-               : -1;
+  if (p.dtype == kFP8) {  // fp8 kernels only; no generic / padded fallback
+    if (!(kernel == kAuto || is_fp8_kernel(kernel)) ||
+        !gemm_fp8_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C))
+      return -1;
+    const bool s_fits = gemm_fp8_w4s_fits(a) && device_cus() % 8 == 0;
+    if (kernel == kFp8W4S) return s_fits ? kFp8W4S : -1;
+    if (kernel != kAuto) return kernel;
+    // the streaming kernel on a device of its own with >= 2 tiles per CU (as W4S)
+    const long long T = (long long)(p.M / 256) * (p.N / 256) * (p.batch < 1 ? 1 : p.batch);
+    return s_fits && p.cus == 0 && T >= 2LL * device_cus() ? kFp8W4S : kFp8W4;
+  }
   if (is_fp8_kernel(kernel)) return -1;
   const bool fast = gemm256_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   const bool w4 = gemm_w4_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
@@ -555,6 +563,11 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
   }
   switch (k) {
     case kFp8W4: return gemm_fp8_launch(a, 1, stream);
+    case kFp8W4S: {
+      GemmArgs s = a;
+      s.pers_grid = ((p.cus > 0 ? p.cus : device_cus()) / 8) * 8;
+      return gemm_fp8_launch(s, 2, stream);
+    }
     case kMfma256d: return gemm256_launch(p.dtype, a, 4, stream);
     case kMfmaW4:
     case kT128:
@@ -663,6 +676,7 @@ const char* kernel_name(int kernel) {
     case kMfma256d: return "pdmb_mfma256d_nn";
     case kF32_256s: return "pdmb_f32_256s_nn";
     case kFp8W4: return "pdmb_fp8_w4_nt";
+    case kFp8W4S: return "pdmb_fp8_w4s";
     case kMfmaW4: return "pdmb_w4_nn";
     case kMfmaW4S: return "pdmb_w4s";
     case kT128: return "pdmb_t128_nn";

@@ -1,6 +1,7 @@
 // gemm_fp8.hip — C = alpha * (A @ B) with A, B in OCP fp8 e4m3 (gfx950's
-// float8_e4m3fn, not MI300's fnuz), fp32 accumulate, bf16 out, on the
-// block-scaled MFMA v_mfma_scale_f32_16x16x128_f8f6f4.
+// float8_e4m3fn, not MI300's fnuz), fp32 accumulate, bf16 out, on the fp8
+// MFMA v_mfma_f32_16x16x128_f8f6f4 (the W4 kernels; the 8-wave A/B kernel
+// keeps the block-scaled form with unit scales).
 //
 // An MI355X extension beyond the reference's float32/float16/bfloat16
 // (matmul_benchmark.py:163-174): the fp8 MFMA with K = 128 runs at twice the
@@ -551,7 +552,232 @@ __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4(GemmArgs a) {
   }
 }
 
+// ---- fp8 W4S: the W4 fp8 kernel as one K-tile stream per CU --------------
+// gemm_w4.hip's W4S carried over (its comment has the why): the DMA items of
+// K-tiles nk .. nk+2 fetch the next tile's K-tiles 0 .. 2, the epilogue
+// (alpha, bf16) goes out through its own LDS region without a drain, the
+// next tile's first two K-tiles wait vmcnt(16 + 32), the first tile issues
+// 32 out-of-range LDS-DMA loads in the stores' place, and every MFMA of
+// K-tile 0 (one per accumulator: K = 128 per MFMA) starts from C = 0.
+// Interior tiles only (M, N % 256), K % 256 == 0, K >= 768; static tiles
+// b, b + G, ... (G = grid, a multiple of 8) on a device the GEMM has to itself.
+__device__ __forceinline__ void mfma_f8_zero(f32x4& acc, const i32x8& a, const i32x8& b) {
+  asm volatile("v_mfma_f32_16x16x128_f8f6f4 %0, %1, %2, 0" : "=&a"(acc) : "v"(a), "v"(b));
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm_barrier8() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+struct Src8 {  // one output tile's operand descriptors (K = 0)
+  u32x4 ra, rb;
+};
+
+__device__ __forceinline__ Src8 tile_src8(const GemmArgs& a, int bz, int tm, int tn) {
+  const int m0 = tm * BM, n0 = tn * BN;
+  Src8 s;
+  s.ra = make_rsrc((const char*)a.A + (long long)bz * a.sA + (long long)m0 * a.lda,
+                   (long long)(a.M - m0 - 1) * a.lda + a.K);
+  s.rb = make_rsrc((const char*)a.B + (long long)bz * a.sB + (long long)n0 * a.ldb,
+                   (long long)(a.N - n0 - 1) * a.ldb + a.K);
+  return s;
+}
+
+// ktile_w4 with explicit DMA targets: A of item "t+2" (descriptor raT at K
+// byte offset kaT), B of "t+3" (rbT at kbT), wait counts W0 / W1, ZERO.
+template <int SO, int W0, int W1, bool ZERO>
+__device__ __forceinline__ void ktile_w4s(const Ctx4& c, const char* smem, u32x4 raT, uint32_t kaT,
+                                          u32x4 rbT, uint32_t kbT, uint32_t lds0w,
+                                          f32x4 (&acc)[8][8], i32x8 (&A)[8], i32x8& A7c,
+                                          i32x8& A7n, i32x8 (&Bc)[8], i32x8 (&Bn)[8]) {
+  constexpr int SN = STAGE4 - SO;
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    if (mi == 0) {
+      wait_vm_lgkm_barrier8<W0>();
+      __builtin_amdgcn_sched_barrier(0);
+    } else if (mi == 4) {
+      wait_vm_lgkm_barrier8<W1>();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int ni = 0; ni < 8; ++ni) {
+      if constexpr (ZERO)
+        mfma_f8_zero(acc[mi][ni], Bc[ni], mi == 7 ? A7c : A[mi]);
+      else
+        mfma_f8_acc<0>(acc[mi][ni], Bc[ni], mi == 7 ? A7c : A[mi], 0);
+      const int it = kW4Items[mi][ni];
+      if (it == 1) {
+        const int h = w4_piece(mi, ni);
+        if (h < 8)  // A of t+2 into S.A: rows (h*4 + wu)*8 + [0,8)
+          dma16_at(raT, c.voffA, kaT + (uint32_t)(h * 32 * c.lda), lds0w, SO + h * 4 * 8 * BK);
+        else  // B of t+3 into S^1.B
+          dma16_at(rbT, c.voffB, kbT + (uint32_t)((h - 8) * 32 * c.ldb), lds0w,
+                   SN + A_BYTES + (h - 8) * 4 * 8 * BK);
+      } else if (it >= 10 && it < 20) {
+        Bn[it - 10] = frag(smem + (it - 10) * 16 * BK, c.boff[SN / STAGE4]);
+      } else if (it == 27) {
+        A7n = frag(smem + 7 * 16 * BK, c.aoff[SN / STAGE4]);
+      } else if (it >= 20) {
+        A[it - 20] = frag(smem + (it - 20) * 16 * BK, c.aoff[SN / STAGE4]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4s(GemmArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE4 + 4 * kEpiBuf];
+  const int T = a.tiles_m * a.tiles_n * a.batch;
+  const int G = gridDim.x;
+  int vb = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wu >> 1, wc = wu & 1;
+  const int l16 = lane & 15, g = lane >> 4;
+
+  Ctx4 c;
+  c.wu = wu;
+  c.lds0 = (uint32_t)(size_t)((lds_void*)smem);
+  const uint32_t lds0w = c.lds0 + wu * 8 * BK;  // every piece's per-wave LDS rows
+  c.lda = a.lda;
+  c.ldb = a.ldb;
+  c.nk = a.K / BK;
+  {
+    const int r = wu * 8 + (lane >> 3), lc8 = lane & 7;
+    c.voffA = (uint32_t)(r * a.lda + ((lc8 ^ swz(r)) * 16));
+    c.voffB = (uint32_t)(r * a.ldb + ((lc8 ^ swz(r)) * 16));
+    const int sw = swz(l16);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        uint32_t ao = (uint32_t)(st * STAGE4 + (wr * 128 + l16) * BK + (((2 * g + h) ^ sw) * 16));
+        uint32_t bo = (uint32_t)(st * STAGE4 + A_BYTES + (wc * 128 + l16) * BK +
+                                 (((2 * g + h) ^ sw) * 16));
+        asm volatile("" : "+v"(ao), "+v"(bo));
+        c.aoff[st][h] = ao;
+        c.boff[st][h] = bo;
+      }
+    }
+  }
+  const int nk = c.nk;
+  int bz, tm, tn;
+  map_tile(a, vb, bz, tm, tn);
+  Src8 cur = tile_src8(a, bz, tm, tn);
+  int nvb = vb + G, nbz = bz, ntm = tm, ntn = tn;
+  Src8 nxt = cur;
+  if (nvb < T) {
+    map_tile(a, nvb, nbz, ntm, ntn);
+    nxt = tile_src8(a, nbz, ntm, ntn);
+  }
+  f32x4 acc[8][8];  // started by each tile's K-tile 0 (ZERO)
+
+  // Prologue of the first tile, as gemm_fp8_w4's: A(0), B(0) -> stage 0;
+  // B(1), A(1) -> stage 1; fragments of K-tile 0; B(2) -> stage 0.B.
+  auto dma_a = [&](const u32x4& r, uint32_t ka, int so, int h) {
+    dma16_at(r, c.voffA, ka + (uint32_t)(h * 32 * c.lda), lds0w, so + h * 4 * 8 * BK);
+  };
+  auto dma_b = [&](const u32x4& r, uint32_t kb, int so, int h) {
+    dma16_at(r, c.voffB, kb + (uint32_t)((h - 8) * 32 * c.ldb), lds0w, so + A_BYTES + (h - 8) * 4 * 8 * BK);
+  };
+#pragma unroll
+  for (int h = 0; h < 8; ++h) dma_a(cur.ra, 0u, 0, h);
+#pragma unroll
+  for (int h = 8; h < 16; ++h) dma_b(cur.rb, 0u, 0, h);
+#pragma unroll
+  for (int h = 8; h < 16; ++h) dma_b(cur.rb, BK, STAGE4, h);
+#pragma unroll
+  for (int h = 0; h < 8; ++h) dma_a(cur.ra, BK, STAGE4, h);
+  asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+  i32x8 A[8], A7a, A7b, B0[8], B1[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    A[i] = frag(smem + i * 16 * BK, c.aoff[0]);
+    B0[i] = frag(smem + i * 16 * BK, c.boff[0]);
+  }
+  A7a = A[7];
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+  for (int h = 8; h < 16; ++h) dma_b(cur.rb, 2 * BK, 0, h);
+  char* ebuf = smem + 2 * STAGE4 + wu * kEpiBuf;
+  {  // 32 dummy LDS-DMA loads in the place of the epilogue stores (see above)
+    u32x4 nul;
+    nul.x = 0u;
+    nul.y = 0u;
+    nul.z = 0u;
+    nul.w = 0x00020000u;
+    const uint32_t eb = c.lds0 + 2 * STAGE4 + wu * kEpiBuf;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) dma16_m0(nul, 0u, 0u, eb);
+  }
+  for (;;) {
+    const bool more = nvb < T;
+    auto sel = [](uint32_t m, uint32_t x, uint32_t y) { return (x & m) | (y & ~m); };
+    // descriptor and K offset of item "kt": this tile, the next, or (last
+    // tile) a harmless re-read of this tile's last K-tile
+    auto tgt = [&](int kt, const u32x4& rc, const u32x4& rn, u32x4& r, uint32_t& ko) {
+      const uint32_t m = (kt < nk || !more) ? ~0u : 0u;
+      const int k = kt < nk ? kt : (more ? kt - nk : nk - 1);
+      r.x = sel(m, rc.x, rn.x);
+      r.y = sel(m, rc.y, rn.y);
+      r.z = sel(m, rc.z, rn.z);
+      r.w = rc.w;
+      ko = (uint32_t)k * BK;
+    };
+    ktile_w4s<0, 48, 48, true>(c, smem, cur.ra, 2 * BK, cur.rb, 3 * BK, lds0w, acc, A, A7a, A7b, B0, B1);
+    ktile_w4s<STAGE4, 48, 16, false>(c, smem, cur.ra, 3 * BK, cur.rb, 4 * BK, lds0w, acc, A, A7b, A7a,
+                                     B1, B0);
+    int t = 2;
+    for (; t + 4 < nk; t += 2) {
+      ktile_w4s<0, 16, 16, false>(c, smem, cur.ra, (uint32_t)(t + 2) * BK, cur.rb, (uint32_t)(t + 3) * BK,
+                                  lds0w, acc, A, A7a, A7b, B0, B1);
+      ktile_w4s<STAGE4, 16, 16, false>(c, smem, cur.ra, (uint32_t)(t + 3) * BK, cur.rb,
+                                       (uint32_t)(t + 4) * BK, lds0w, acc, A, A7b, A7a, B1, B0);
+    }
+    for (; t < nk; t += 2) {
+      u32x4 ra, rb;
+      uint32_t ka, kb;
+      tgt(t + 2, cur.ra, nxt.ra, ra, ka);
+      tgt(t + 3, cur.rb, nxt.rb, rb, kb);
+      ktile_w4s<0, 16, 16, false>(c, smem, ra, ka, rb, kb, lds0w, acc, A, A7a, A7b, B0, B1);
+      tgt(t + 3, cur.ra, nxt.ra, ra, ka);
+      tgt(t + 4, cur.rb, nxt.rb, rb, kb);
+      ktile_w4s<STAGE4, 16, 16, false>(c, smem, ra, ka, rb, kb, lds0w, acc, A, A7b, A7a, B1, B0);
+    }
+    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    char* Cb = (char*)a.C + (long long)bz * a.sC * 2;
+    unsigned all = ~0u;
+    asm volatile("" : "+s"(all));  // per tile: lane offsets formed here, not kept live
+    const int eln = (int)__builtin_amdgcn_mbcnt_hi(all, __builtin_amdgcn_mbcnt_lo(all, 0u));
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      store_block16<kBF16, false, true>(ebuf, acc[i], a.alpha, Cb, (long long)a.ldc * 2,
+                                        tm * BM + wr * 128 + i * 16, tn * BN + wc * 128, a.M, a.N, eln);
+    __builtin_amdgcn_sched_barrier(0);
+    if (!more) break;
+    vb = nvb;
+    bz = nbz;
+    tm = ntm;
+    tn = ntn;
+    cur = nxt;
+    nvb = vb + G;
+    if (nvb < T) {
+      map_tile(a, nvb, nbz, ntm, ntn);
+      nxt = tile_src8(a, nbz, ntm, ntn);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA in flight at exit
+}
+
 }  // namespace k8
+
+bool gemm_fp8_w4s_fits(const GemmArgs& a) {
+  const int nk = a.K / k8::BK;
+  return a.M % k8::BM == 0 && a.N % k8::BN == 0 && a.K % (2 * k8::BK) == 0 && nk >= 6;
+}
 
 bool gemm_fp8_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c) {
   if (a.K % 128 != 0 || a.K <= 0 || a.N % 4 != 0 || a.M <= 0 || a.N <= 0) return false;
@@ -574,6 +800,12 @@ hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream) {
   const dim3 grid((unsigned)nblocks);
   if (variant == 1) {  // the shipping fp8 kernel (kFp8W4)
     hipLaunchKernelGGL(k8::gemm_fp8_w4<0>, grid, dim3(k8::NT4), 0, stream, a);
+    return hipGetLastError();
+  }
+  if (variant == 2) {  // kFp8W4S: streaming persistent (host: gemm_fp8_w4s_fits, pers_grid % 8 == 0)
+    if (!gemm_fp8_w4s_fits(a) || a.pers_grid <= 0 || a.pers_grid % 8) return hipErrorInvalidValue;
+    const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
+    hipLaunchKernelGGL(k8::gemm_fp8_w4s, pg, dim3(k8::NT4), 0, stream, a);
     return hipGetLastError();
   }
 #ifdef PDMB_EXPERIMENTS

@@ -87,20 +87,6 @@ __device__ __forceinline__ void dma16_m0(u32x4 rsrc, uint32_t voff, uint32_t sof
       : "memory", "m0");
 }
 
-// LDS-DMA to M0 = lds0w + OFF, OFF an immediate (known once the K-tile's
-// item loop is unrolled): M0 is formed by the one SALU add that replaces
-// the s_mov, instead of from ~32 precomputed addresses held in SGPRs.
-__device__ __forceinline__ void dma16_at(u32x4 rsrc, uint32_t voff, uint32_t soff, uint32_t lds0w,
-                                         uint32_t off) {
-  asm volatile(
-      "s_add_u32 m0, %3, %4\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %0, %1, %2 offen lds"
-      :
-      : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds0w), "i"(off)
-      : "memory", "m0", "scc");
-}
-
 struct Frag {  // one 16-row (A) or 16-column (B) block of a K-tile: k 0..31 and 32..63
   s16x8 k[2];
 };

@@ -143,3 +143,44 @@ def test_fp8_thin_supertiles_exact(M, N, batch):
                    dtype=torch.bfloat16)
     gemm.matmul(A8, B8, out=C)
     assert torch.equal(C, (Af.double() @ Bf.double()).to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("batch,M,N,K", [(1, 256, 256, 768), (1, 1024, 2048, 1024), (1, 4096, 4096, 768),
+                                         (1, 8192, 4096, 1024), (2, 2048, 2048, 768), (1, 16384, 2048, 768),
+                                         (1, 2048, 16384, 768)])
+def test_fp8_streaming_w4s_matches_w4_bitwise(batch, M, N, K):
+    """fp8 W4S (one K-tile stream per CU, epilogue overlapped with the next
+    tile's first DMAs, C = 0 MFMA starts): the same accumulation order as the
+    W4 fp8 kernel, so bitwise equal, for one and several tiles per CU, uneven
+    tile counts, thin grids and batches."""
+    g = torch.Generator(device="cuda").manual_seed(batch + M + 3 * N + K)
+    A = torch.randn(batch, M, K, device="cuda", generator=g).to(FP8)
+    B = _colmajor(torch.randn(batch, K, N, device="cuda", generator=g).to(FP8))
+    if batch == 1:
+        A, B = A[0], B[0]
+    ref = gemm.matmul(A, B, kernel="fp8_w4", alpha=0.5)
+    for _ in range(2):
+        out = torch.full_like(ref, float("nan"))
+        gemm.matmul(A, B, out=out, kernel="fp8_w4s", alpha=0.5)
+        assert torch.equal(out, ref)
+
+
+def test_fp8_w4s_plan_and_refusals():
+    g = torch.Generator(device="cuda").manual_seed(9)
+
+    def ops(M, N, K):
+        return (torch.randn(M, K, device="cuda", generator=g).to(FP8),
+                _colmajor(torch.randn(K, N, device="cuda", generator=g).to(FP8)))
+
+    A, B = ops(8192, 8192, 1024)  # 1024 tiles, K / 128 even: auto streams
+    assert gemm.kernel_for(A, B) == "pdmb_fp8_w4s"
+    with gemm.shared_device():
+        assert gemm.kernel_for(A, B) == "pdmb_fp8_w4_nt"
+    A, B = ops(8000, 8192, 1024)  # edge tiles: W4 fp8 only
+    assert gemm.kernel_for(A, B) == "pdmb_fp8_w4_nt"
+    with pytest.raises(RuntimeError):
+        gemm.matmul(A, B, kernel="fp8_w4s")
+    A, B = ops(8192, 8192, 640)  # K / 128 odd
+    assert gemm.kernel_for(A, B) == "pdmb_fp8_w4_nt"
+    with pytest.raises(RuntimeError):
+        gemm.matmul(A, B, kernel="fp8_w4s")
