@@ -102,7 +102,33 @@ def test_default_build_has_no_experiment_kernels(tmp_path):
     assert ks and all("ELi3ELb0ELi0EE" in k for k in ks), sorted(ks)  # SCHED 3 only
     (tmp_path / "fp8").mkdir()
     ks = _kernels("gemm_fp8.hip", tmp_path / "fp8")
-    assert ks and all("gemm_fp8_w4ILi0ELi0E" in k for k in ks), sorted(ks)
+    assert ks and all("gemm_fp8_w4ILi0ELi0E" in k or "gemm_fp8_w4s" in k for k in ks), sorted(ks)
+
+
+@pytest.mark.parametrize("src,pat,dts,zero_per_kt", [
+    ("gemm_w4.hip", "gemm_w4s", ("ILi2E", "ILi1E"), 64),   # bf16 / fp16: C = 0 on ks = 0 only
+    ("gemm_fp8.hip", "gemm_fp8_w4s", ("",), 64),           # fp8: one MFMA per accumulator
+])
+def test_streaming_kernels_structure(tmp_path, src, pat, dts, zero_per_kt):
+    """W4S / fp8 W4S: no scratch, AGPR accumulators, the boundary's counted
+    waits vmcnt(48) (32 epilogue stores younger than the awaited DMAs), each
+    tile started by C = 0 MFMAs (no zeroing), 32 placeholder LDS-DMA loads,
+    and exactly one vmcnt(0) drain (at exit): no compiler-inserted wait may
+    drain the stream."""
+    ks = _kernels(src, tmp_path)
+    for dt in dts:
+        name = [k for k in ks if pat + dt in k]
+        assert name, sorted(ks)
+        k = ks[name[0]]
+        b = k["body"]
+        assert k["spill"] == 0 and "scratch_" not in b, name
+        assert k["lds"] == 2 * 65536 + 4 * 4224
+        assert re.search(r"v_mfma_f32_16x16x\d+_\w+ a\[", b)
+        assert len(re.findall(r"s_waitcnt vmcnt\(48\) lgkmcnt\(0\)", b)) == 3
+        assert len(re.findall(r"v_mfma_f32_16x16x\d+_\w+ a\[\d+:\d+\], v\[\d+:\d+\], v\[\d+:\d+\], 0$",
+                              b, re.M)) == zero_per_kt
+        assert len(re.findall(r"s_waitcnt vmcnt\(0\)", b)) == 1
+        assert len(re.findall(r"global_store_dwordx4", b)) == 32
 
 
 @pytest.mark.parametrize("cfg,lds,waitn,mfma_per_kt,pieces", [
@@ -132,10 +158,11 @@ def test_tile_family_pipelined(tmp_path, cfg, lds, waitn, mfma_per_kt, pieces):
 
 def test_t128x2_two_workgroups_per_cu(tmp_path):
     """The 2-stage T128 variant: 64 KiB LDS and <= 256 VGPR + AGPR per wave, so two
-    256-thread workgroups fit on a CU; its loop waits vmcnt(0) at every K-tile top."""
+    256-thread workgroups fit on a CU; its loop waits vmcnt(0) at every K-tile top
+    (+1: the barrier before the LDS-staged epilogue)."""
     ks = _kernels("gemm_tile.hip", tmp_path)
     name = [k for k in ks if "gemm_tile_nnILi2E" in k and "Li128ELi128ELi2ELi2E" in k]
     assert name, sorted(ks)
     k = ks[name[0]]
     assert k["spill"] == 0 and k["lds"] == 2 * 32768 and k["vgpr"] <= 128
-    assert len(re.findall(r"s_waitcnt vmcnt\(0\) lgkmcnt\(0\)", k["body"])) == 3
+    assert len(re.findall(r"s_waitcnt vmcnt\(0\) lgkmcnt\(0\)", k["body"])) == 4
