@@ -48,6 +48,7 @@ enum ExperimentKernel : int {
   kFp8W4Trace = 33,   // kFp8W4 writing the tile timeline into the debug buffer
   kMfmaW4Pers = 34,   // persistent W4 (one workgroup per CU, per-XCD work queues)
   kMfmaW4PersTrace = 35,  // kMfmaW4Pers writing the tile timeline
+  kMfmaW4STrace = 38,  // W4S writing per-workgroup start / end stamps
   kMfmaW4Il32 = 30,   // kMfmaW4 (bf16) with the 8-wave kernel's 32-column B-half interleave
 };
 

@@ -541,9 +541,13 @@ __device__ __forceinline__ void ktile_s(const Ctx& c, const char* smem, u32x4 ra
   }
 }
 
-template <int DT>
+// TRACE (kMfmaW4STrace): each workgroup stamps its start and end (after the
+// final drain) into the tile-trace row blockIdx.x, for the per-XCD tail.
+template <int DT, int TRACE = 0>
 __global__ void __launch_bounds__(NT, 1) gemm_w4s(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 4 * kEpiBuf];
+  TileTrace tr;
+  if constexpr (TRACE) tr.t[0] = tile_clock();
   constexpr int IL = 64;
   const int T = a.tiles_m * a.tiles_n * a.batch;
   const int G = gridDim.x;
@@ -743,6 +747,10 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4s(GemmArgs a) {
   }
   // No LDS-DMA may still be writing when this workgroup's LDS is handed on.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (TRACE) {
+    tr.t[1] = tr.t[2] = tr.t[3] = tile_clock();
+    tile_trace_write(a, tr, blockIdx.x, 0, 0);
+  }
 }
 
 }  // namespace kw4
@@ -803,6 +811,15 @@ hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
     if (S > 1 || !a.queue) return hipErrorInvalidValue;
     const unsigned g = (unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid);
     hipLaunchKernelGGL((kw4::gemm_w4_pers<kBF16, 1>), dim3(g), block, 0, stream, a);
+    return hipGetLastError();
+  }
+#endif
+#ifdef PDMB_EXPERIMENTS
+  if (sub == 8) {  // W4S with per-workgroup start / end stamps
+    if (S > 1 || a.pers_grid <= 0 || a.pers_grid % 8 || (a.K / kw4::BK) % 2 || a.K / kw4::BK < 6)
+      return hipErrorInvalidValue;
+    const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
+    hipLaunchKernelGGL((kw4::gemm_w4s<kBF16, 1>), pg, block, 0, stream, a);
     return hipGetLastError();
   }
 #endif

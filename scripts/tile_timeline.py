@@ -19,6 +19,8 @@ tile_trace_write). Per (kernel, shape) this prints, in microseconds:
 
     python scripts/tile_timeline.py --kernels w4 --shapes 16384,16384,1024 16384,16384,16384
     python scripts/tile_timeline.py --kernels fp8_w4 --dtype float8_e4m3fn --shapes ...
+    python scripts/tile_timeline.py --kernels w4s ...   # W4S: one row per workgroup
+                                                       # (start, end), so loop / epilogue read 0
 """
 import argparse
 import json
@@ -62,6 +64,10 @@ def analyse(tr: torch.Tensor) -> dict:
         ends.append(wgs[-1][3])
         loop_sum += sum(r[2] - r[1] for r in wgs)
     first_starts = sorted(min(r[0] for r in w) for w in per_cu.values())
+    per_xcd = {}
+    for r in rows:
+        per_xcd.setdefault(r[5] & 0xF, []).append(r[3])
+    xcd_end = {x: statistics.median(v) - t0 for x, v in sorted(per_xcd.items())}
 
     def us(x):
         return round(x * TICK_US, 2)
@@ -76,6 +82,10 @@ def analyse(tr: torch.Tensor) -> dict:
         "first_start_spread_us": us(first_starts[-1] - first_starts[0]),
         "loop_frac": round(loop_sum / (len(per_cu) * span), 4),
         "tail_us": us(max(ends) - statistics.median(ends)),
+        # median end of each XCD's workgroups: XCDs that run faster idle at the end
+        "xcd_end_us": [us(v) for v in xcd_end.values()],
+        "xcd_idle_frac": round(sum(max(xcd_end.values()) - v for v in xcd_end.values())
+                               / (len(xcd_end) * max(xcd_end.values())), 4),
     }
 
 
