@@ -78,7 +78,8 @@ def build_parser(kind: str) -> argparse.ArgumentParser:
                    help="GEMM implementation on GPU: native gfx950 MFMA kernels (default) or "
                         "torch.matmul/hipBLASLt for A/B comparison")
     g.add_argument("--kernel", default="auto",
-                   choices=["auto", "w4", "mfma256d", "generic", "f32_256s", "fp8_w4"],
+                   choices=["auto", "w4", "w4s", "t128", "t128x2", "t256x128", "mfma256d", "generic",
+                            "f32_w4", "f32_256s", "fp8_w4", "fp8_w4s"],
                    help="native kernel selection (shipping kernels; A/B kernels need a "
                         "PDMB_EXPERIMENTS=1 build and scripts/ab_kernels.py)")
     g.add_argument("--batch", type=int, default=4,
