@@ -90,6 +90,7 @@ static bool is_experiment(int k) {
 }
 
 static int device_cus();
+static int fp8_split(const Problem& p);
 static bool w4s_fits(const Problem& p);
 static bool w4s_auto(const Problem& p);
 
@@ -293,9 +294,33 @@ static bool is_tiled(int k) { return k == kMfmaW4 || k == kT128 || k == kT128x2 
 
 int choose_splitk(const Problem& p, int kernel) {
   const int k = resolve_kernel(p, kernel);
-  if (k == kMfmaW4S) return 1;
+  if (k == kMfmaW4S || k == kFp8W4S) return 1;
+  if (k == kFp8W4) return fp8_split(p);
   if (!is_tiled(k)) return 0;
   return plan(p, k).splitk;
+}
+
+// fp8 W4 split-K (gemm_fp8.hip): grids of 256x256 tiles that fill at most
+// half the CUs are split 2 or 4 ways along K while every slice keeps >= 16
+// K-tiles (128 deep) and the split grid still fits the CUs the stream may
+// use; p.splitk > 0 fixes it (1 = never). Measured (profiles/
+// r2_fp8_splitk_ab.jsonl): 8192x1024x8192 S=2 2237 vs 1844 TF unsplit;
+// slices of 8 K-tiles lose (4096x1024x4096 S=4 787 vs 878; 2048^3 S=2 563
+// vs 694): the meet's slot traffic and latency outweigh the extra CUs.
+static int fp8_split(const Problem& p) {
+  if (p.splitk > 0) return p.splitk;
+  const long long T = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256) * (p.batch < 1 ? 1 : p.batch);
+  const int nk = p.K / 128;
+  const long long cus = p.cus > 0 ? p.cus : device_cus();
+  int S = 1;
+  for (int s : {2, 4})
+    if (T * s <= cus && nk / s >= 16 && T <= kMaxSplitTiles) S = s;
+  return S;
+}
+static size_t fp8_split_bytes(const Problem& p, int S) {
+  if (S <= 1) return 0;
+  const long long T = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256) * (p.batch < 1 ? 1 : p.batch);
+  return (size_t)T * S * 256 * 256 * sizeof(float);
 }
 
 static size_t splitk_bytes(const Problem& p, int kernel, int S) {
@@ -494,6 +519,7 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel) {
   }
   const int k = resolve_kernel(p, kernel);
   if (is_tiled(k)) return splitk_bytes(p, k, plan(p, k).splitk);
+  if (k == kFp8W4) return fp8_split_bytes(p, fp8_split(p));
   if (k == kMfmaW4Tall || k == kMfmaW4Wide || k == kMfmaW4Il32 || k == kMfmaW4Trace ||
       k == kMfmaW4Pers || k == kMfmaW4PersTrace)
     return splitk_bytes(p, kMfmaW4, plan(p, kMfmaW4).splitk);
@@ -563,7 +589,22 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     return hipSuccess;
   }
   switch (k) {
-    case kFp8W4: return gemm_fp8_launch(a, 1, stream);
+    case kFp8W4: {
+      GemmArgs s = a;
+      s.splitk = 1;
+      const int S = fp8_split(p);
+      if (S > 1) {
+        unsigned* flags = stream_counters(stream);
+        if (flags && p.workspace && p.workspace_bytes >= fp8_split_bytes(p, S)) {
+          s.splitk = S;
+          s.part = (float*)p.workspace;
+          s.flags = flags;
+        } else if (p.splitk > 1) {
+          return hipErrorInvalidValue;  // explicitly requested: no silent change
+        }
+      }
+      return gemm_fp8_launch(s, 1, stream);
+    }
     case kFp8W4S: {
       GemmArgs s = a;
       s.pers_grid = ((p.cus > 0 ? p.cus : device_cus()) / 8) * 8;

@@ -33,7 +33,9 @@
 // N % 4 == 0, lda / ldb % 16 == 0 (16-B rows), ldc % 4 == 0, 16-B aligned
 // A / B, 8-B aligned C. M and N edges read zeros through the buffer
 // descriptor's extent and are masked at the store.
+#include "api.h"
 #include "common.h"
+#include "splitk.h"
 
 namespace pdmb {
 namespace k8 {
@@ -449,6 +451,15 @@ __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4(GemmArgs a) {
 
   int bz, tm, tn;
   map_tile(a, blockIdx.x, bz, tm, tn, SUB);
+  // Split-K (grids that under-fill the CUs): the grid's "batch" is batch x S
+  // with the slice innermost, as in gemm_w4.hip; slice s runs K-tiles
+  // [s * kt_per, +kt_per) and the slices meet in the epilogue (splitk.h).
+  int slice = 0;
+  if (a.splitk > 1) {
+    slice = bz % a.splitk;
+    bz /= a.splitk;
+  }
+  const int kt0 = slice * a.kt_per;
   const int m0 = tm * BM, n0 = tn * BN;
   const int lane = threadIdx.x & 63;
   const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -460,11 +471,12 @@ __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4(GemmArgs a) {
   c.lds0 = (uint32_t)(size_t)((lds_void*)smem);
   c.lda = a.lda;
   c.ldb = a.ldb;
-  c.nk = a.K / BK;
-  const char* Ab = (const char*)a.A + (long long)bz * a.sA + (long long)m0 * a.lda;
-  const char* Bb = (const char*)a.B + (long long)bz * a.sB + (long long)n0 * a.ldb;
-  c.ra = make_rsrc(Ab, (long long)(a.M - m0 - 1) * a.lda + a.K);
-  c.rb = make_rsrc(Bb, (long long)(a.N - n0 - 1) * a.ldb + a.K);
+  c.nk = a.splitk > 1 ? min(a.kt_per, a.K / BK - kt0) : a.K / BK;
+  const long long k0 = (long long)kt0 * BK;  // bytes: fp8 rows are K-contiguous
+  const char* Ab = (const char*)a.A + (long long)bz * a.sA + (long long)m0 * a.lda + k0;
+  const char* Bb = (const char*)a.B + (long long)bz * a.sB + (long long)n0 * a.ldb + k0;
+  c.ra = make_rsrc(Ab, (long long)(a.M - m0 - 1) * a.lda + a.K - k0);
+  c.rb = make_rsrc(Bb, (long long)(a.N - n0 - 1) * a.ldb + a.K - k0);
   {
     const int r = wu * 8 + (lane >> 3), lc8 = lane & 7;  // row of piece 0 (swz(r + 32h) = swz(r))
     c.voffA = (uint32_t)(r * a.lda + ((lc8 ^ swz(r)) * 16));
@@ -525,25 +537,36 @@ __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4(GemmArgs a) {
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
   if constexpr (TRACE) tr.t[2] = tile_clock();
 
+  // Split-K: only the last slice of a tile to arrive writes C, summing the
+  // slices' fp32 slots (unscaled) block row by block row (splitk.h).
+  SplitSlots sl;
+  const bool split = a.splitk > 1;
+  if (split && !splitk_meet<8, 8, NT4>(a, smem, ((long long)bz * a.tiles_m + tm) * a.tiles_n + tn,
+                                       slice, acc, sl))
+    return;
   // Epilogue through LDS as whole rows (common.h store_block16), masked at
   // M / N; every DMA landed and every fragment read done before any wave
   // writes its staging buffers.
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   const float alpha = a.alpha;
   char* Cb = (char*)a.C + (long long)bz * a.sC * 2;
-  char* ebuf = smem + wu * 2 * kEpiBuf;
-  if (m0 + BM <= a.M && n0 + BN <= a.N) {  // interior tile: no masks
+  char* ebuf = smem + 1024 + wu * 2 * kEpiBuf;  // past splitk_meet's ticket word
+  const bool interior = m0 + BM <= a.M && n0 + BN <= a.N;
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-      store_block16<kBF16, false, true>(ebuf + (i & 1) * kEpiBuf, acc[i], alpha, Cb,
-                                        (long long)a.ldc * 2, m0 + wr * 128 + i * 16,
-                                        n0 + wc * 128, a.M, a.N, lane);
-  } else {
+  for (int i = 0; i < 8; ++i) {
+    f32x4 v[8];
+    if (!split) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-      store_block16<kBF16, true, true>(ebuf + (i & 1) * kEpiBuf, acc[i], alpha, Cb,
-                                       (long long)a.ldc * 2, m0 + wr * 128 + i * 16,
-                                       n0 + wc * 128, a.M, a.N, lane);
+      for (int j = 0; j < 8; ++j) v[j] = acc[i][j];
+    } else {
+      splitk_row<8, 8, NT4>(a, sl, slice, i, acc, v);
+    }
+    if (interior)
+      store_block16<kBF16, false, true>(ebuf + (i & 1) * kEpiBuf, v, alpha, Cb, (long long)a.ldc * 2,
+                                        m0 + wr * 128 + i * 16, n0 + wc * 128, a.M, a.N, lane);
+    else
+      store_block16<kBF16, true, true>(ebuf + (i & 1) * kEpiBuf, v, alpha, Cb, (long long)a.ldc * 2,
+                                       m0 + wr * 128 + i * 16, n0 + wc * 128, a.M, a.N, lane);
   }
   if constexpr (TRACE) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -794,7 +817,17 @@ hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream) {
   a.tiles_m = (a.M + k8::BM - 1) / k8::BM;
   a.tiles_n = (a.N + k8::BN - 1) / k8::BN;
   a.supertile = choose_supertile(a.tiles_m, a.tiles_n);
-  const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch;
+  const int S = variant == 1 && a.splitk > 1 ? a.splitk : 1;  // split-K: the W4 kernel only
+  if (S > 1) {
+    const int nk = a.K / k8::BK;
+    a.kt_per = (nk + S - 1) / S;
+    if ((S - 1) * a.kt_per >= nk || !a.part || !a.flags ||
+        (long long)a.tiles_m * a.tiles_n * a.batch > kMaxSplitTiles)
+      return hipErrorInvalidValue;  // every slice must own >= 1 K-tile
+  } else {
+    a.splitk = 1;
+  }
+  const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch * S;
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
   const dim3 grid((unsigned)nblocks);

@@ -6,6 +6,7 @@ equal to the first kernel's. The arm ``torch`` is the vendor library
 (hipBLASLt: torch.matmul, or torch._scaled_mm for fp8) in the same rounds.
 
     python scripts/ab_kernels.py --kernels mfma256c,x_noprio --sizes 8192 16384 --rounds 5
+    python scripts/ab_kernels.py --kernels auto,auto:1,torch ...    # "kernel:S": split-K S (1 = off)
     python scripts/ab_kernels.py --kernels fp8_w4,torch --dtype float8_e4m3fn \
         --shapes 16384,16384,2048 16384,16384,16384      # M,N,K (K sweeps: per-tile overhead)
 """
@@ -52,12 +53,18 @@ def main():
                 return torch._scaled_mm(A, B, one, one, out_dtype=torch.bfloat16, out=out)
             return torch.matmul(A, B, out=out)
 
+        def arm(k):  # "kernel" or "kernel:S" (S = K slices: split-K forced / off with 1)
+            name, _, S = k.partition(":")
+            return name, int(S or 0)
+
         def run(k):
-            return vendor() if k == "torch" else gemm.matmul(A, B, kernel=k)
+            name, S = arm(k)
+            return vendor() if k == "torch" else gemm.matmul(A, B, kernel=name, splitk=S)
 
         def bench(k, iters):
             if k != "torch":
-                return gemm.bench_matmul(A, B, C, iters, 2, kernel=k) / iters
+                name, S = arm(k)
+                return gemm.bench_matmul(A, B, C, iters, 2, kernel=name, splitk=S) / iters
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             vendor(C)
             e0.record()

@@ -184,3 +184,20 @@ def test_fp8_w4s_plan_and_refusals():
     assert gemm.kernel_for(A, B) == "pdmb_fp8_w4_nt"
     with pytest.raises(RuntimeError):
         gemm.matmul(A, B, kernel="fp8_w4s")
+
+
+@pytest.mark.parametrize("M,N,K,splitk", [(8192, 1024, 8192, 0), (4096, 512, 4096, 0), (4096, 1024, 4096, 2),
+                                          (2048, 2048, 2048, 4), (1000, 1052, 4096, 0)])
+def test_fp8_splitk_exact(M, N, K, splitk):
+    """fp8 W4 split-K (auto for grids that fill <= half the CUs, or forced):
+    slices meet in-launch (splitk.h), alpha applied after the slot sum; exact
+    on small integers, edge tiles included."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + splitk)
+    Af, Bf = _ints((M, K), g, -2, 3), _ints((K, N), g, -2, 3)
+    A8, B8 = Af.to(FP8), _colmajor(Bf.to(FP8))
+    S = gemm.splitk_for(A8, B8) if splitk == 0 else splitk
+    if splitk == 0:
+        assert S > 1, (M, N, K, S)  # these grids fill at most half the chip, >= 16 K-tiles / slice
+    for _ in range(2):  # counters re-zeroed by every launch
+        C = gemm.matmul(A8, B8, splitk=splitk, alpha=0.5)
+        assert torch.equal(C, (0.5 * (Af.double() @ Bf.double())).to(torch.bfloat16))
