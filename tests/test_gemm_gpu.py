@@ -589,3 +589,35 @@ def test_shipping_surface_refuses_diagnostics():
         with pytest.raises(ValueError):
             gemm.matmul(A, A, kernel=k)
     assert _native.load().resolve(A, A, torch.empty_like(A), 20) == -1  # raw id, C++ side
+
+
+def test_streaming_kernels_in_graphs():
+    """W4S and fp8 W4S (persistent, no workspace or counters) capture and
+    replay exactly: the native loop's hipGraph mode and torch.cuda.graph."""
+    g = torch.Generator(device="cuda").manual_seed(21)
+    A = torch.randint(-3, 4, (8192, 1024), device="cuda", generator=g).to(torch.bfloat16)
+    B = torch.randint(-3, 4, (1024, 8192), device="cuda", generator=g).to(torch.bfloat16)
+    assert gemm.kernel_for(A, B) == "pdmb_w4s"
+    R = (A.double() @ B.double()).to(torch.bfloat16)
+    out = torch.empty_like(R)
+    assert gemm.bench_matmul(A, B, out, iters=3, warmup=1, graph=True) > 0
+    assert torch.equal(out, R)
+    s = torch.cuda.Stream()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        gemm.matmul(A, B, out=out)
+    for _ in range(2):
+        out.fill_(float("nan"))
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, R)
+    A8 = A.to(torch.float8_e4m3fn)
+    B8 = B.t().contiguous().to(torch.float8_e4m3fn).t()
+    assert gemm.kernel_for(A8, B8) == "pdmb_fp8_w4s"
+    out8 = torch.empty_like(R)
+    graph8 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph8, stream=s):
+        gemm.matmul(A8, B8, out=out8)
+    graph8.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out8, R)
