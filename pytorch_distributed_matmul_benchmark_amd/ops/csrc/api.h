@@ -49,6 +49,8 @@ enum ExperimentKernel : int {
   kMfmaW4Pers = 34,   // persistent W4 (one workgroup per CU, per-XCD work queues)
   kMfmaW4PersTrace = 35,  // kMfmaW4Pers writing the tile timeline
   kMfmaW4STrace = 38,  // W4S writing per-workgroup start / end stamps
+  kMfmaW4SRot = 39,    // W4S with the per-round rotating XCD block map (supertile 6)
+  kMfmaW4SRotTrace = 40,  // kMfmaW4SRot with per-workgroup start / end stamps
   kMfmaW4Il32 = 30,   // kMfmaW4 (bf16) with the 8-wave kernel's 32-column B-half interleave
 };
 

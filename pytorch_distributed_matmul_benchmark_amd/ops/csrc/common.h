@@ -279,10 +279,10 @@ inline int choose_supertile(int tiles_m, int tiles_n) {
   return 0;
 }
 
-__device__ __forceinline__ void map_tile(const GemmArgs& a, int b, int& bz, int& tm, int& tn,
-                                         int sub = 0) {
+__host__ __device__ __forceinline__ void map_tile(const GemmArgs& a, int b, int& bz, int& tm, int& tn,
+                                                  int sub = 0) {
   const int tpb = a.tiles_m * a.tiles_n;
-  if (a.supertile >= 2) {
+  if (a.supertile >= 2 && a.supertile <= 5) {
     const int x = b & 7, j = b >> 3;
     const int round = j >> 5, i = j & 31;
     const int st = a.supertile;
@@ -297,8 +297,11 @@ __device__ __forceinline__ void map_tile(const GemmArgs& a, int b, int& bz, int&
     tm = sr * SM + (x / xn) * bm + i / bn;
     tn = sc * SN + (x % xn) * bn + i % bn;
   } else if (a.supertile) {
-    const int x = b & 7, j = b >> 3;
+    const int j = b >> 3;
     const int round = j >> 5, i = j & 31;
+    // supertile 6: mode 1 with the XCD -> block position rotated by one per
+    // round, so every XCD visits every position of the 16 x 16 round (A/B)
+    const int x = a.supertile == 6 ? ((b & 7) + round) & 7 : b & 7;
     const int st_n = a.tiles_n >> 4;
     const int st_per_b = (a.tiles_m >> 4) * st_n;
     bz = round / st_per_b;

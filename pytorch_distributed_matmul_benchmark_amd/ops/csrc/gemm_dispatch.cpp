@@ -82,7 +82,8 @@ static bool is_experiment(int k) {
     case kMfma256: case kMfma256b: case kMfma256c: case kMfma256Stamp: case kF32_256:
     case kMfma256X1: case kMfma256X2: case kMfma256X4: case kFp8: case kFp8W4Diag:
     case kFp8W4Diag2: case kFp8W4Diag3: case kF32NoDma: case kMfmaW4Tall: case kMfmaW4Wide: case kMfmaW4Il32:
-    case kMfmaW4Pers: case kMfmaW4PersTrace: case kMfmaW4STrace: case kFp8W4Tall: case kFp8W4Wide: case kFp8W4Scaled: case kFp8W4Trace: case kMfmaW4Trace:
+    case kMfmaW4Pers: case kMfmaW4PersTrace: case kMfmaW4STrace: case kMfmaW4SRot: case kMfmaW4SRotTrace:
+    case kFp8W4Tall: case kFp8W4Wide: case kFp8W4Scaled: case kFp8W4Trace: case kMfmaW4Trace:
       return true;
     default:
       return false;
@@ -152,7 +153,8 @@ int resolve_kernel(const Problem& p, int kernel) {
     case kMfmaW4Tall: case kMfmaW4Wide: case kMfmaW4Il32: case kMfmaW4Trace:
     case kMfmaW4PersTrace:
       return (p.dtype == kBF16 && w4) ? kernel : -1;
-    case kMfmaW4STrace: return (p.dtype == kBF16 && w4 && w4s_fits(p)) ? kernel : -1;
+    case kMfmaW4STrace: case kMfmaW4SRot: case kMfmaW4SRotTrace:
+      return (p.dtype == kBF16 && w4 && w4s_fits(p)) ? kernel : -1;
     case kMfmaW4Pers: return w4 ? kernel : -1;  // bf16 and fp16
 #endif
     default: return -1;
@@ -375,7 +377,7 @@ static hipError_t tiled_launch(const Problem& p, int k, GemmArgs a, void* part, 
     }
   }
   a.splitk = S;
-  if (sub == 7 || sub == 8) {  // W4S: unsplit, one workgroup per usable CU (a multiple of 8)
+  if (sub >= 7 && sub <= 10) {  // W4S: unsplit, one workgroup per usable CU (a multiple of 8)
     if (S > 1) {
       sub = 0;
     } else {
@@ -638,6 +640,8 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kMfmaW4Pers: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 5);
     case kMfmaW4PersTrace: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 6);
     case kMfmaW4STrace: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 8);
+    case kMfmaW4SRot: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 9);
+    case kMfmaW4SRotTrace: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 10);
     case kF32_256: return gemm_f32_256_launch(a, 0, stream);
     case kF32NoDma: return gemm_f32_256_launch(a, 9, stream);
     case kMfma256X1: case kMfma256X2: case kMfma256X4:
@@ -742,6 +746,8 @@ const char* kernel_name(int kernel) {
     case kMfmaW4Pers: return "pdmb_w4_pers";
     case kMfmaW4PersTrace: return "pdmb_w4_pers_trace";
     case kMfmaW4STrace: return "pdmb_w4s_trace";
+    case kMfmaW4SRot: return "pdmb_w4s_rot";
+    case kMfmaW4SRotTrace: return "pdmb_w4s_rot_trace";
     case kFp8W4Trace: return "pdmb_fp8_w4_nt_trace";
     default: return "auto";
   }

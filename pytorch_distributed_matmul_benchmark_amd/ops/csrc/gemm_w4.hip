@@ -815,6 +815,22 @@ hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
   }
 #endif
 #ifdef PDMB_EXPERIMENTS
+  if (sub == 9) {  // W4S with the per-round rotating XCD block map (supertile 6)
+    if (S > 1 || a.pers_grid <= 0 || a.pers_grid % 8 || (a.K / kw4::BK) % 2 || a.K / kw4::BK < 6)
+      return hipErrorInvalidValue;
+    if (a.supertile == 1) a.supertile = 6;
+    const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
+    hipLaunchKernelGGL((kw4::gemm_w4s<kBF16>), pg, block, 0, stream, a);
+    return hipGetLastError();
+  }
+  if (sub == 10) {  // the same with per-workgroup start / end stamps
+    if (S > 1 || a.pers_grid <= 0 || a.pers_grid % 8 || (a.K / kw4::BK) % 2 || a.K / kw4::BK < 6)
+      return hipErrorInvalidValue;
+    if (a.supertile == 1) a.supertile = 6;
+    const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
+    hipLaunchKernelGGL((kw4::gemm_w4s<kBF16, 1>), pg, block, 0, stream, a);
+    return hipGetLastError();
+  }
   if (sub == 8) {  // W4S with per-workgroup start / end stamps
     if (S > 1 || a.pers_grid <= 0 || a.pers_grid % 8 || (a.K / kw4::BK) % 2 || a.K / kw4::BK < 6)
       return hipErrorInvalidValue;
