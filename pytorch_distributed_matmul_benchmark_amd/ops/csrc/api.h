@@ -20,6 +20,8 @@ enum Kernel : int {
   kF32W4 = 29,    // gemm_f32_w4.hip: exact fp32, 4 waves x 128x128, AGPR acc (fp32 auto)
   kMfmaW4S = 36,  // gemm_w4.hip W4S: W4 as one K-tile stream per CU (persistent, static tiles)
   kFp8W4S = 37,   // gemm_fp8.hip: the fp8 W4 kernel as one K-tile stream per CU (interior tiles)
+  kFp8T128 = 41,      // gemm_tile.hip fp8: 128x128 tile, 4 waves x 64x64, split-K (M, N % 128)
+  kFp8T256x128 = 42,  // gemm_tile.hip fp8: 256x128 tile, 4 waves x 128x64, split-K (M % 256, N % 128)
 };
 
 // Experiment / diagnostic ids (A/B and timing-only builds). Compiled and

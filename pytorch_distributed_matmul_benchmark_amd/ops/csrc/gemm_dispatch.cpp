@@ -73,7 +73,7 @@ bool experiments_built() {
 }
 
 static bool is_fp8_kernel(int k) {
-  return k == kFp8W4 || k == kFp8W4S || k == kFp8 || k == kFp8W4Diag || k == kFp8W4Diag2 || k == kFp8W4Diag3 ||
+  return k == kFp8W4 || k == kFp8W4S || k == kFp8T128 || k == kFp8T256x128 || k == kFp8 || k == kFp8W4Diag || k == kFp8W4Diag2 || k == kFp8W4Diag3 ||
          k == kFp8W4Tall || k == kFp8W4Wide || k == kFp8W4Scaled || k == kFp8W4Trace;
 }
 
@@ -94,6 +94,7 @@ static int device_cus();
 static int fp8_split(const Problem& p);
 static bool w4s_fits(const Problem& p);
 static bool w4s_auto(const Problem& p);
+static bool supports(const Problem& p, int kernel);
 
 struct Plan {
   int kernel;  // kMfmaW4 | kT128 | -1
@@ -110,10 +111,14 @@ int resolve_kernel(const Problem& p, int kernel) {
       return -1;
     const bool s_fits = gemm_fp8_w4s_fits(a) && device_cus() % 8 == 0;
     if (kernel == kFp8W4S) return s_fits ? kFp8W4S : -1;
+    if (kernel == kFp8T128 || kernel == kFp8T256x128) return supports(p, kernel) ? kernel : -1;
     if (kernel != kAuto) return kernel;
     // the streaming kernel on a device of its own with >= 2 tiles per CU (as W4S)
     const long long T = (long long)(p.M / 256) * (p.N / 256) * (p.batch < 1 ? 1 : p.batch);
-    return s_fits && p.cus == 0 && T >= 2LL * device_cus() ? kFp8W4S : kFp8W4;
+    if (s_fits && p.cus == 0 && T >= 2LL * device_cus()) return kFp8W4S;
+    // otherwise the planner: fp8 W4 (edge tiles too) or the fp8 tile family
+    const Plan pl = plan(p, kAuto);
+    return pl.kernel >= 0 ? pl.kernel : kFp8W4;
   }
   if (is_fp8_kernel(kernel)) return -1;
   const bool fast = gemm256_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
@@ -182,15 +187,23 @@ int resolve_kernel(const Problem& p, int kernel) {
 // W4 1.42, T256x128 0.87 (16k: 1187 vs 1438 TF for W4 on one box), T128 0.46,
 // T128x2 0.86 per pair of co-resident workgroups. The fit
 // reproduces the measured times of the shard shapes within ~10 %.
+//
+// fp8 (one K-tile = 128 e4m3: the same bytes per row and MFMA cycles as a
+// bf16 K-tile of 64) is planned over its own models: fp8 W4 (edge tiles too;
+// its split stays fp8_split's measured rule) and the fp8 tile family.
 struct KernelModel {
   int kernel, bm, bn, occ;
   double kt;
+  bool fp8;
 };
 static constexpr KernelModel kModels[] = {
-    {kMfmaW4, 256, 256, 1, 1.42},
-    {kT256x128, 256, 128, 1, 0.87},
-    {kT128, 128, 128, 1, 0.46},
-    {kT128x2, 128, 128, 2, 0.86},
+    {kMfmaW4, 256, 256, 1, 1.42, false},
+    {kT256x128, 256, 128, 1, 0.87, false},
+    {kT128, 128, 128, 1, 0.46, false},
+    {kT128x2, 128, 128, 2, 0.86, false},
+    {kFp8W4, 256, 256, 1, 1.30, true},
+    {kFp8T256x128, 256, 128, 1, 0.80, true},
+    {kFp8T128, 128, 128, 1, 0.42, true},
 };
 static constexpr double kFixedUs = 4.0;   // launch + prologue + epilogue
 static constexpr double kMeetUs = 4.0;    // combine latency (poll, serial slab read)
@@ -203,10 +216,12 @@ static const KernelModel& model_of(int kernel) {
   return kModels[0];
 }
 
-static long long tiles_of(const Problem& p, int kernel) {
+static long long tiles_of(const Problem& p, int kernel) {  // ceil: fp8 W4 runs edge tiles
   const KernelModel& m = model_of(kernel);
-  return (long long)(p.M / m.bm) * (p.N / m.bn) * (p.batch < 1 ? 1 : p.batch);
+  return (long long)((p.M + m.bm - 1) / m.bm) * ((p.N + m.bn - 1) / m.bn) * (p.batch < 1 ? 1 : p.batch);
 }
+
+static int ktiles(const Problem& p) { return p.K / (p.dtype == kFP8 ? 128 : 64); }
 
 static int device_cus() {
   static int n[64] = {0};
@@ -240,7 +255,7 @@ static bool w4s_auto(const Problem& p) {
 static double plan_cost(const Problem& p, int kernel, int S) {
   const KernelModel& m = model_of(kernel);
   const long long T = tiles_of(p, kernel);
-  const int nk = p.K / 64;
+  const int nk = ktiles(p);
   const int per = (nk + S - 1) / S;
   const long long slots = (long long)(p.cus > 0 ? p.cus : device_cus()) * m.occ;
   const long long units = T * S;
@@ -252,8 +267,9 @@ static double plan_cost(const Problem& p, int kernel, int S) {
 }
 
 static bool split_ok(const Problem& p, int kernel, int S) {
+  if (kernel == kFp8W4) return S == fp8_split(p);  // its measured rule (fp8_split)
   if (S == 1) return true;
-  const int nk = p.K / 64;
+  const int nk = ktiles(p);
   const int per = (nk + S - 1) / S;
   return per >= kMinKt && (S - 1) * per < nk && tiles_of(p, kernel) <= kMaxSplitTiles;
 }
@@ -261,6 +277,7 @@ static bool split_ok(const Problem& p, int kernel, int S) {
 static bool supports(const Problem& p, int kernel) {
   const GemmArgs a = to_args(p);
   if (kernel == kMfmaW4) return gemm_w4_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
+  if (kernel == kFp8W4) return gemm_fp8_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   return gemm_tile_supported(p.dtype, model_of(kernel).bm, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
 }
 
@@ -273,7 +290,7 @@ static Plan plan(const Problem& p, int kernel) {
   static const int kS[] = {1, 2, 4, 8};
   for (const KernelModel& m : kModels) {
     if (kernel != kAuto && kernel != m.kernel) continue;
-    if (!supports(p, m.kernel)) continue;
+    if (m.fp8 != (p.dtype == kFP8) || !supports(p, m.kernel)) continue;
     any = true;
     for (int S : kS) {
       if (S > 4 && p.splitk != S) continue;
@@ -288,11 +305,14 @@ static Plan plan(const Problem& p, int kernel) {
   }
   if (best.kernel < 0 && any)  // the requested split is impossible for this K
     for (const KernelModel& m : kModels)
-      if ((kernel == kAuto || kernel == m.kernel) && supports(p, m.kernel)) return Plan{m.kernel, 0};
+      if ((kernel == kAuto || kernel == m.kernel) && m.fp8 == (p.dtype == kFP8) && supports(p, m.kernel))
+        return Plan{m.kernel, 0};
   return best;
 }
 
-static bool is_tiled(int k) { return k == kMfmaW4 || k == kT128 || k == kT128x2 || k == kT256x128; }
+static bool is_tiled(int k) {
+  return k == kMfmaW4 || k == kT128 || k == kT128x2 || k == kT256x128 || k == kFp8T128 || k == kFp8T256x128;
+}
 
 int choose_splitk(const Problem& p, int kernel) {
   const int k = resolve_kernel(p, kernel);
@@ -616,7 +636,9 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kMfmaW4:
     case kT128:
     case kT128x2:
-    case kT256x128: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream);
+    case kT256x128:
+    case kFp8T128:
+    case kFp8T256x128: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream);
     case kMfmaW4S: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 7);
     case kF32_256s: return gemm_f32_256_launch(a, 1, stream);
     case kF32W4: return gemm_f32_w4_launch(a, stream);
@@ -724,6 +746,8 @@ const char* kernel_name(int kernel) {
     case kF32_256s: return "pdmb_f32_256s_nn";
     case kFp8W4: return "pdmb_fp8_w4_nt";
     case kFp8W4S: return "pdmb_fp8_w4s";
+    case kFp8T128: return "pdmb_fp8_t128_nt";
+    case kFp8T256x128: return "pdmb_fp8_t256x128_nt";
     case kMfmaW4: return "pdmb_w4_nn";
     case kMfmaW4S: return "pdmb_w4s";
     case kT128: return "pdmb_t128_nn";

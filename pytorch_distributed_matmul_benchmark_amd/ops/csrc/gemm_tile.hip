@@ -1,4 +1,5 @@
-// gemm_tile.hip — bf16 / fp16 C = A @ B (row-major NN, fp32 accumulate): the
+// gemm_tile.hip — bf16 / fp16 C = A @ B (row-major NN, fp32 accumulate) and
+// fp8 e4m3 C = alpha * (A @ B) (A row-major, B column-major, bf16 out): the
 // one-barrier LDS-DMA tile family for grids that under-fill the 256 CUs with
 // W4's 256x256 tiles. Members (Cfg<BM, BN, NS>):
 //   T128      128 x 128, 4-stage ring, 1 workgroup / CU
@@ -37,9 +38,18 @@
 //  * Optional split-K over K-tile ranges with the in-launch combine of
 //    splitk.h.
 //
+// fp8 (DT = kFP8; kFp8T128 / kFp8T256x128): a K-tile is 128 e4m3 = 128 B per
+// row, so the A image is byte for byte the bf16 one and B (column-major, Bt
+// [N,K] rows) is a second A-like image of BN rows; both use gemm_fp8.hip's
+// swizzle swz8 (conflict-free for the fp8 fragment: chunks 2g, 2g+1 of a row)
+// and ds_read_b128, no transposed read. One v_mfma_f32_16x16x128_f8f6f4 per
+// block per K-tile (twice the cycles of the bf16 pair it replaces), so the
+// same item schedule runs with the MFMA at every other gap: 16 MFMAs and 24
+// loads per K-tile per wave, as many cycles as the bf16 kernel's 32 + 24.
+//
 // Fast-path constraints (host-checked): M % BM == 0, N % BN == 0 (interior
-// tiles only), K % 64 == 0, lda / ldb % 8 == 0, ldc % 4 == 0, 16-B aligned
-// A / B, 8-B aligned C.
+// tiles only), K % 64 == 0 (fp8: K % 128), lda / ldb % 8 == 0 (fp8: % 16),
+// ldc % 4 == 0, 16-B aligned A / B, 8-B aligned C.
 #include "api.h"
 #include "common.h"
 #include "splitk.h"
@@ -113,6 +123,20 @@ __device__ __forceinline__ void mfma_acc<kF16>(f32x4& acc, const s16x8& b, const
   asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
 }
 
+// fp8: one 16x16x128 e4m3 MFMA on a block's whole fragment (k[0] | k[1]).
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void mfma_acc_f8(f32x4& acc, const s16x8 (&b)[2], const s16x8 (&a)[2]) {
+  const s16x8 bv[2] = {b[0], b[1]}, av[2] = {a[0], a[1]};
+  const i32x8 bb = __builtin_bit_cast(i32x8, bv), aa = __builtin_bit_cast(i32x8, av);
+  asm volatile("v_mfma_f32_16x16x128_f8f6f4 %0, %1, %2, %0" : "+a"(acc) : "v"(bb), "v"(aa));
+}
+
+// fp8 row swizzle (gemm_fp8.hip swz): 16-B chunk c of 128-B row r at c ^ swz8(r);
+// depends on r & 15 only.
+__host__ __device__ __forceinline__ int swz8(int r) {
+  return ((r >> 1) & 7) ^ ((((r & 15) - 4) & 15) < 8 ? 2 : 0);
+}
+
 // LDS-DMA with a scalar offset; M0 is clobbered (declared), not saved.
 __device__ __forceinline__ void dma16_m0(u32x4 rsrc, uint32_t voff, uint32_t soff, uint32_t lds) {
   asm volatile(
@@ -142,12 +166,13 @@ struct Frag {  // one 16-row (A) or 16-column (B) block of a K-tile: k 0..31 and
 template <class C>
 struct Ctx {
   u32x4 ra;               // A descriptor at this slice's first K
+  u32x4 rb;               // fp8: Bt descriptor at this slice's first K (row n0)
   const char* Bb;         // B at this slice's first K row, column n0
   long long b_bytes;      // bytes from Bb to the end of B's extent
   int lda2, ldb2, nk;     // leading dims in bytes, K-tiles of this slice
   uint32_t voffA, voffB;  // per-lane DMA offsets of piece 0
   uint32_t aoff[2];       // per-lane A fragment offsets in stage 0, [ks]
-  uint32_t boff[C::NB];   // per-lane B fragment offsets in stage 0, [block j]
+  uint32_t boff[C::NB];   // per-lane B fragment offsets in stage 0, [block j] (fp8: [half])
   int wu;
   uint32_t lds0;
 };
@@ -163,9 +188,16 @@ __device__ __forceinline__ u32x4 b_rsrc(const Ctx<C>& c, int tile) {
 // (h-PA)*16 + wu*4 + [0,4) (4 x 256 B). The swizzles depend on (row >> 1) & 7
 // (A) and k & 11 (B) only, which those row offsets leave alone, so one
 // per-lane offset serves every piece.
-template <class C>
+template <int DT, class C>
 __device__ __forceinline__ void issue_piece(const Ctx<C>& c, u32x4 rb, uint32_t so, int tile, int h) {
-  if (h < C::PA) {
+  if constexpr (DT == kFP8) {  // A / Bt rows h' * 32 + wu * 8 + [0,8), K at tile * 128 B
+    if (h < C::PA)
+      dma16_m0(c.ra, c.voffA, (uint32_t)tile * 128 + (uint32_t)(h * 32 * c.lda2),
+               c.lds0 + so + (h * 32 + c.wu * 8) * 128);
+    else
+      dma16_m0(c.rb, c.voffB, (uint32_t)tile * 128 + (uint32_t)((h - C::PA) * 32 * c.ldb2),
+               c.lds0 + so + C::A_BYTES + ((h - C::PA) * 32 + c.wu * 8) * 128);
+  } else if (h < C::PA) {
     dma16_m0(c.ra, c.voffA, (uint32_t)tile * (BK * 2) + (uint32_t)(h * 32 * c.lda2),
              c.lds0 + so + (h * 32 + c.wu * 8) * 128);
   } else {
@@ -189,6 +221,12 @@ __device__ __forceinline__ s16x8 frag_b(const char* smem, uint32_t off, int ks) 
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+// fp8 B fragment half h of block j (16 output columns = 16 Bt rows).
+template <class C>
+__device__ __forceinline__ s16x8 frag_b8(const char* smem, uint32_t off, int j) {
+  return *(const lds_s16x8*)(smem + C::A_BYTES + j * 16 * 128 + off);
+}
+
 // One K-tile: G MFMAs on (Ac, Bc) = fragments of tile t, reading tile t+1's
 // fragments into (An, Bn) from stage sn, DMA of tile t + NS into stage sc.
 template <int DT, class C>
@@ -197,7 +235,9 @@ __device__ __forceinline__ void ktile(const Ctx<C>& c, const char* smem, int t, 
                                       Frag (&Bc)[C::NB], Frag (&An)[C::MB], Frag (&Bn)[C::NB]) {
   constexpr Sched<C> S{};
   const int td = t + C::NS < c.nk ? t + C::NS : c.nk - 1;  // clamped tail DMAs (harmless re-reads)
-  const u32x4 rb = b_rsrc(c, td);
+  u32x4 rb;
+  if constexpr (DT == kFP8) rb = c.rb;
+  else rb = b_rsrc(c, td);
   wait_lgkm_barrier<C::P * (C::NS - 2)>();
   __builtin_amdgcn_sched_barrier(0);
   uint32_t ao[2], bo[C::NB];
@@ -208,17 +248,25 @@ __device__ __forceinline__ void ktile(const Ctx<C>& c, const char* smem, int t, 
 #pragma unroll
   for (int gap = 0; gap < C::G; ++gap) {
     constexpr int MN = C::MB * C::NB;
-    const int ks = gap / MN, mi = (gap % MN) / C::NB, ni = gap % C::NB;
-    mfma_acc<DT>(acc[mi][ni], Bc[ni].k[ks], Ac[mi].k[ks]);
+    if constexpr (DT == kFP8) {  // one MFMA per block, at every other gap
+      if ((gap & 1) == 0) {
+        const int b = gap >> 1, mi = b / C::NB, ni = b % C::NB;
+        mfma_acc_f8(acc[mi][ni], Bc[ni].k, Ac[mi].k);
+      }
+    } else {
+      const int ks = gap / MN, mi = (gap % MN) / C::NB, ni = gap % C::NB;
+      mfma_acc<DT>(acc[mi][ni], Bc[ni].k[ks], Ac[mi].k[ks]);
+    }
     const int it = S.item[gap];
     if (it >= 200) {
       const int m = (it - 200) >> 1, h = (it - 200) & 1;
       An[m].k[h] = frag_a(smem, ao[h], m);
     } else if (it >= 100) {
       const int j = (it - 100) >> 1, h = (it - 100) & 1;
-      Bn[j].k[h] = frag_b<C>(smem, bo[j], h);
+      if constexpr (DT == kFP8) Bn[j].k[h] = frag_b8<C>(smem, bo[h], j);
+      else Bn[j].k[h] = frag_b<C>(smem, bo[j], h);
     } else if (it >= 1) {
-      issue_piece<C>(c, rb, sc, td, it - 1);
+      issue_piece<DT, C>(c, rb, sc, td, it - 1);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -246,18 +294,40 @@ __global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
   Ctx<C> c;
   c.wu = wu;
   c.lds0 = (uint32_t)(size_t)((lds_void*)smem);
-  c.lda2 = a.lda * 2;
-  c.ldb2 = a.ldb * 2;
+  constexpr int ES = DT == kFP8 ? 1 : 2;       // bytes per element
+  constexpr int BKE = DT == kFP8 ? 128 : BK;   // K per K-tile (128 B per row either way)
+  c.lda2 = a.lda * ES;
+  c.ldb2 = a.ldb * ES;
   {
-    const int nk_all = a.K / BK;
+    const int nk_all = a.K / BKE;
     c.nk = a.splitk > 1 ? min(a.kt_per, nk_all - kt0) : nk_all;
   }
-  const int k0 = kt0 * BK;
-  const char* Ab = (const char*)a.A + ((long long)bz * a.sA + (long long)m0 * a.lda + k0) * 2;
-  c.ra = make_rsrc(Ab, ((long long)(a.M - m0 - 1) * a.lda + (a.K - k0)) * 2);
-  c.Bb = (const char*)a.B + ((long long)bz * a.sB + (long long)k0 * a.ldb + n0) * 2;
-  c.b_bytes = ((long long)(a.K - k0 - 1) * a.ldb + (a.N - n0)) * 2;
-  {
+  const int k0 = kt0 * BKE;
+  const char* Ab = (const char*)a.A + ((long long)bz * a.sA + (long long)m0 * a.lda + k0) * ES;
+  c.ra = make_rsrc(Ab, ((long long)(a.M - m0 - 1) * a.lda + (a.K - k0)) * ES);
+  if constexpr (DT == kFP8) {  // Bt [N,K]: rows n0 .., K-contiguous
+    const char* Bt = (const char*)a.B + (long long)bz * a.sB + (long long)n0 * a.ldb + k0;
+    c.rb = make_rsrc(Bt, (long long)(a.N - n0 - 1) * a.ldb + (a.K - k0));
+    c.Bb = Bt;
+    c.b_bytes = 0;
+    const int r = wu * 8 + (lane >> 3), lc8 = lane & 7;  // row of piece 0 (swz8(r + 32h) = swz8(r))
+    c.voffA = (uint32_t)(r * c.lda2 + ((lc8 ^ swz8(r)) * 16));
+    c.voffB = (uint32_t)(r * c.ldb2 + ((lc8 ^ swz8(r)) * 16));
+    const int sw = swz8(l16);  // fragment rows are 16-aligned bases + l16
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint32_t ao = (uint32_t)((wr * (C::BM / 2) + l16) * 128 + (((2 * g + h) ^ sw) * 16));
+      uint32_t bo = (uint32_t)((wc * (C::BN / 2) + l16) * 128 + (((2 * g + h) ^ sw) * 16));
+      asm volatile("" : "+v"(ao), "+v"(bo));  // opaque: one base VGPR each
+      c.aoff[h] = ao;
+      c.boff[h] = bo;
+    }
+#pragma unroll
+    for (int j = 2; j < NB; ++j) c.boff[j] = 0u;  // unused by the fp8 reads
+  } else {
+    c.rb = c.ra;
+    c.Bb = (const char*)a.B + ((long long)bz * a.sB + (long long)k0 * a.ldb + n0) * 2;
+    c.b_bytes = ((long long)(a.K - k0 - 1) * a.ldb + (a.N - n0)) * 2;
     const int r = wu * 8 + (lane >> 3), lc8 = lane & 7;  // row of A piece 0
     c.voffA = (uint32_t)(r * c.lda2 + ((lc8 ^ ((r >> 1) & 7)) * 16));
     const int lr16 = lane >> 4, lc16 = lane & 15;
@@ -295,9 +365,11 @@ __global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
 #pragma unroll
   for (int st = 0; st < NS; ++st) {
     const int tl = st < nk ? st : nk - 1;
-    const u32x4 rb = b_rsrc(c, tl);
+    u32x4 rb;
+    if constexpr (DT == kFP8) rb = c.rb;
+    else rb = b_rsrc(c, tl);
 #pragma unroll
-    for (int h = 0; h < C::P; ++h) issue_piece<C>(c, rb, st * C::STAGE, tl, h);
+    for (int h = 0; h < C::P; ++h) issue_piece<DT, C>(c, rb, st * C::STAGE, tl, h);
   }
   wait_barrier<C::P * (NS - 1)>();
   Frag A0[MB], B0[NB], A1[MB], B1[NB];
@@ -306,7 +378,10 @@ __global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
 #pragma unroll
     for (int i = 0; i < MB; ++i) A0[i].k[ks] = frag_a(smem, c.aoff[ks], i);
 #pragma unroll
-    for (int j = 0; j < NB; ++j) B0[j].k[ks] = frag_b<C>(smem, c.boff[j], ks);
+    for (int j = 0; j < NB; ++j) {
+      if constexpr (DT == kFP8) B0[j].k[ks] = frag_b8<C>(smem, c.boff[ks], j);
+      else B0[j].k[ks] = frag_b<C>(smem, c.boff[j], ks);
+    }
   }
   // Steady state: K-tile t computes from set (t & 1), reads t+1 into the
   // other set from stage (t+1) % NS, refills stage t % NS with tile t + NS.
@@ -346,9 +421,14 @@ __global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
     } else {
       splitk_row<MB, NB, NT>(a, sl, slice, i, acc, v);
     }
-    store_block16<DT, false, false, NB>(ebuf + (i & 1) * epi_buf<NB>(), v, 1.0f, Cb,
-                                        (long long)a.ldc * 2, m0 + wr * (C::BM / 2) + i * 16,
-                                        n0 + wc * (C::BN / 2), a.M, a.N, lane);
+    if constexpr (DT == kFP8)  // alpha (the per-tensor scales), bf16 out
+      store_block16<kBF16, false, true, NB>(ebuf + (i & 1) * epi_buf<NB>(), v, a.alpha, Cb,
+                                            (long long)a.ldc * 2, m0 + wr * (C::BM / 2) + i * 16,
+                                            n0 + wc * (C::BN / 2), a.M, a.N, lane);
+    else
+      store_block16<DT, false, false, NB>(ebuf + (i & 1) * epi_buf<NB>(), v, 1.0f, Cb,
+                                          (long long)a.ldc * 2, m0 + wr * (C::BM / 2) + i * 16,
+                                          n0 + wc * (C::BN / 2), a.M, a.N, lane);
   }
 }
 
@@ -358,7 +438,7 @@ hipError_t launch(int dt, GemmArgs a, hipStream_t stream) {
   a.tiles_n = a.N / C::BN;
   const int S = a.splitk > 1 ? a.splitk : 1;
   if (S > 1) {
-    const int nk = a.K / BK;
+    const int nk = a.K / (dt == kFP8 ? 128 : BK);
     a.kt_per = (nk + S - 1) / S;
     if ((S - 1) * a.kt_per >= nk || !a.part || !a.flags ||
         (long long)a.tiles_m * a.tiles_n * a.batch > kMaxSplitTiles)
@@ -371,10 +451,16 @@ hipError_t launch(int dt, GemmArgs a, hipStream_t stream) {
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
   const dim3 grid((unsigned)nblocks), block(NT);
-  if (dt == kBF16)
+  if (dt == kBF16) {
     hipLaunchKernelGGL((gemm_tile_nn<kBF16, C>), grid, block, 0, stream, a);
-  else
+  } else if (dt == kF16) {
     hipLaunchKernelGGL((gemm_tile_nn<kF16, C>), grid, block, 0, stream, a);
+  } else {
+    if constexpr (C::OCC == 1)  // fp8: T128, T256x128
+      hipLaunchKernelGGL((gemm_tile_nn<kFP8, C>), grid, block, 0, stream, a);
+    else
+      return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
@@ -383,6 +469,18 @@ hipError_t launch(int dt, GemmArgs a, hipStream_t stream) {
 // bm x 128 tiles (bm = 128 or 256).
 bool gemm_tile_supported(int dt, int bm, const GemmArgs& a, size_t align_a, size_t align_b,
                          size_t align_c) {
+  if (dt == kFP8) {  // A [M,K] row-major, Bt [N,K] row-major, bf16 C
+    if (a.M <= 0 || a.N <= 0 || a.K <= 0) return false;
+    if (a.M % bm || a.N % 128 || a.K % 128) return false;
+    if (a.lda % 16 || a.ldb % 16 || a.ldc % 4) return false;
+    if (a.lda < a.K || a.ldb < a.K || a.ldc < a.N) return false;
+    if (a.batch > 1 && (a.sA % 16 || a.sB % 16 || a.sC % 4)) return false;
+    if (align_a % 16 || align_b % 16 || align_c % 8) return false;
+    // 32-bit offsets: rows up to bm-1 (A) / 127 (Bt) plus the K byte offset.
+    if ((long long)bm * a.lda + a.K >= (1LL << 31) || (long long)128 * a.ldb + a.K >= (1LL << 31))
+      return false;
+    return true;
+  }
   if (dt != kBF16 && dt != kF16) return false;
   if (a.M <= 0 || a.N <= 0 || a.K <= 0) return false;
   if (a.M % bm || a.N % 128 || a.K % 64) return false;
@@ -397,9 +495,12 @@ bool gemm_tile_supported(int dt, int bm, const GemmArgs& a, size_t align_a, size
   return true;
 }
 
-// kernel: kT128 | kT128x2 | kT256x128
+// kernel: kT128 | kT128x2 | kT256x128 (bf16 / fp16), kFp8T128 | kFp8T256x128 (fp8)
 hipError_t gemm_tile_launch(int kernel, int dt, GemmArgs a, hipStream_t stream) {
+  if ((dt == kFP8) != (kernel == kFp8T128 || kernel == kFp8T256x128)) return hipErrorInvalidValue;
   switch (kernel) {
+    case kFp8T128: return ktile::launch<ktile::CfgT128>(dt, a, stream);
+    case kFp8T256x128: return ktile::launch<ktile::CfgT256x128>(dt, a, stream);
     case kT128: return ktile::launch<ktile::CfgT128>(dt, a, stream);
     case kT128x2: return ktile::launch<ktile::CfgT128x2>(dt, a, stream);
     case kT256x128: return ktile::launch<ktile::CfgT256x128>(dt, a, stream);

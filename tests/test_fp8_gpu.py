@@ -8,6 +8,7 @@ from pytorch_distributed_matmul_benchmark_amd.ops import gemm
 
 pytestmark = pytest.mark.gpu
 FP8 = torch.float8_e4m3fn
+FP8_KERNELS = ("pdmb_fp8_w4_nt", "pdmb_fp8_w4s", "pdmb_fp8_t128_nt", "pdmb_fp8_t256x128_nt")
 
 
 def _ints(shape, g, lo=-3, hi=4):
@@ -31,10 +32,12 @@ def test_fp8_exact_small_integers(M, N, K):
     g = torch.Generator(device="cuda").manual_seed(M + 7 * N + K)
     Af, Bf = _ints((M, K), g), _ints((K, N), g)
     A8, B8 = Af.to(FP8), _colmajor(Bf.to(FP8))
-    assert gemm.kernel_for(A8, B8) == "pdmb_fp8_w4_nt"
+    assert gemm.kernel_for(A8, B8) in FP8_KERNELS
+    ref = (Af.double() @ Bf.double()).to(torch.bfloat16)
     C = gemm.matmul(A8, B8)
     assert C.dtype == torch.bfloat16 and C.shape == (M, N)
-    ref = (Af.double() @ Bf.double()).to(torch.bfloat16)
+    assert torch.equal(C, ref)
+    C = gemm.matmul(A8, B8, kernel="fp8_w4")  # W4 handles every shape (edge tiles)
     assert torch.equal(C, ref)
 
 
@@ -195,9 +198,58 @@ def test_fp8_splitk_exact(M, N, K, splitk):
     g = torch.Generator(device="cuda").manual_seed(M + N + K + splitk)
     Af, Bf = _ints((M, K), g, -2, 3), _ints((K, N), g, -2, 3)
     A8, B8 = Af.to(FP8), _colmajor(Bf.to(FP8))
-    S = gemm.splitk_for(A8, B8) if splitk == 0 else splitk
+    S = gemm.splitk_for(A8, B8, kernel="fp8_w4") if splitk == 0 else splitk
     if splitk == 0:
         assert S > 1, (M, N, K, S)  # these grids fill at most half the chip, >= 16 K-tiles / slice
     for _ in range(2):  # counters re-zeroed by every launch
-        C = gemm.matmul(A8, B8, splitk=splitk, alpha=0.5)
+        C = gemm.matmul(A8, B8, splitk=splitk, alpha=0.5, kernel="fp8_w4")
         assert torch.equal(C, (0.5 * (Af.double() @ Bf.double())).to(torch.bfloat16))
+
+
+# ---- fp8 tile family (gemm_tile.hip, DT = kFP8): under-filled fp8 grids ----
+@pytest.mark.parametrize("kernel", ["fp8_t128", "fp8_t256x128"])
+@pytest.mark.parametrize("M,N,K,splitk", [(256, 128, 128, 1), (512, 384, 256, 1), (2048, 2048, 2048, 1),
+                                          (4096, 512, 4096, 0), (4096, 512, 4096, 2), (2048, 1024, 4096, 4),
+                                          (1024, 16384, 256, 1), (16384, 1024, 256, 1), (768, 640, 1152, 2)])
+def test_fp8_tile_family_exact(kernel, M, N, K, splitk):
+    """fp8 T128 / T256x128 (A / Bt images with the fp8 swizzle, one 16x16x128
+    MFMA per block per K-tile, alpha in the LDS-staged epilogue) on exact small
+    integers: unsplit, auto and forced split-K (odd K-tile counts too), and
+    thin grids (map_tile supertiles 4 / 5 at 128-row tiles)."""
+    if kernel == "fp8_t256x128" and M % 256:
+        pytest.skip("T256x128: M % 256")
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K + splitk)
+    Af, Bf = _ints((M, K), g, -2, 3), _ints((K, N), g, -2, 3)
+    A8, B8 = Af.to(FP8), _colmajor(Bf.to(FP8))
+    assert gemm.kernel_for(A8, B8, kernel=kernel) == f"pdmb_{kernel}_nt"
+    ref = (0.5 * (Af.double() @ Bf.double())).to(torch.bfloat16)
+    for _ in range(2):  # split-K counters re-zeroed by every launch
+        C = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+        gemm.matmul(A8, B8, out=C, kernel=kernel, splitk=splitk, alpha=0.5)
+        assert torch.equal(C, ref)
+
+
+@pytest.mark.parametrize("kernel", ["fp8_t128", "fp8_t256x128"])
+def test_fp8_tile_family_matches_w4_bitwise(kernel):
+    """Unsplit, a block's K-tiles go through the same one-MFMA-per-128-K chain
+    as in fp8 W4: bitwise equal on random operands, batched too."""
+    g = torch.Generator(device="cuda").manual_seed(21)
+    A = torch.randn(2, 1024, 2048, device="cuda", generator=g).to(FP8)
+    B = _colmajor(torch.randn(2, 2048, 768, device="cuda", generator=g).to(FP8))
+    ref = gemm.matmul(A, B, kernel="fp8_w4", alpha=0.25, splitk=1)
+    out = gemm.matmul(A, B, kernel=kernel, alpha=0.25, splitk=1)
+    assert torch.equal(out, ref)
+
+
+def test_fp8_tile_family_refusals_and_race_screen():
+    g = torch.Generator(device="cuda").manual_seed(4)
+    A = torch.randn(1000, 512, device="cuda", generator=g).to(FP8)  # M % 128 != 0
+    B = _colmajor(torch.randn(512, 512, device="cuda", generator=g).to(FP8))
+    assert gemm.kernel_for(A, B, kernel="fp8_t128") == "unsupported"
+    assert gemm.kernel_for(A, B) == "pdmb_fp8_w4_nt"  # auto: edge tiles on W4
+    A8, sa = gemm.fp8_quantize(torch.randn(4096, 4096, device="cuda", generator=g))
+    B8, sb = gemm.fp8_quantize(torch.randn(4096, 512, device="cuda", generator=g), colmajor=True)
+    ref = gemm.matmul(A8, B8, alpha=sa * sb, kernel="fp8_t128")
+    assert _relerr(ref, (A8.double() * sa) @ (B8.double() * sb)) < 8e-3
+    for _ in range(20):
+        assert torch.equal(gemm.matmul(A8, B8, alpha=sa * sb, kernel="fp8_t128"), ref)
