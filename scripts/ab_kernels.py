@@ -27,7 +27,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kernels", required=True)
     ap.add_argument("--sizes", type=int, nargs="+", default=[8192, 16384])
-    ap.add_argument("--shapes", nargs="+", default=None, help="M,N,K triples (instead of --sizes)")
+    ap.add_argument("--shapes", nargs="+", default=None,
+                    help="M,N,K triples or M,N,K,batch (instead of --sizes)")
     ap.add_argument("--dtype", default="bfloat16")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
@@ -36,16 +37,19 @@ def main():
     dt = getattr(torch, a.dtype)
     shapes = ([tuple(int(v) for v in s.split(",")) for s in a.shapes] if a.shapes
               else [(n, n, n) for n in a.sizes])
-    for m, n, kk in shapes:
+    for shp in shapes:
+        m, n, kk = shp[:3]
+        bt = shp[3] if len(shp) > 3 else 0  # 0: 2-D operands
+        lead = (bt,) if bt else ()
         torch.manual_seed(0)
         if dt == torch.float8_e4m3fn:  # e4m3 operands (scale 1), B column-major, bf16 C
-            A, _ = gemm.fp8_quantize(torch.randn(m, kk, device="cuda"))
-            B, _ = gemm.fp8_quantize(torch.randn(kk, n, device="cuda"), colmajor=True)
+            A, _ = gemm.fp8_quantize(torch.randn(*lead, m, kk, device="cuda"))
+            B, _ = gemm.fp8_quantize(torch.randn(*lead, kk, n, device="cuda"), colmajor=True)
         else:
-            A = torch.randn(m, kk, device="cuda", dtype=dt)
-            B = torch.randn(kk, n, device="cuda", dtype=dt)
-        C = torch.empty(m, n, device="cuda", dtype=gemm.out_dtype(dt))
-        flops = 2.0 * m * n * kk
+            A = torch.randn(*lead, m, kk, device="cuda", dtype=dt)
+            B = torch.randn(*lead, kk, n, device="cuda", dtype=dt)
+        C = torch.empty(*lead, m, n, device="cuda", dtype=gemm.out_dtype(dt))
+        flops = 2.0 * m * n * kk * max(bt, 1)
         one = torch.ones((), device="cuda")
 
         def vendor(out=None):
@@ -90,7 +94,8 @@ def main():
                 res[k].append(flops / bench(k, a.iters) / 1e9)
         for k in ks:
             med = statistics.median(res[k])
-            print(json.dumps({"n": n, **({"m": m, "k": kk} if a.shapes else {}), "kernel": k,
+            print(json.dumps({"n": n, **({"m": m, "k": kk} if a.shapes else {}),
+                              **({"batch": bt} if bt else {}), "kernel": k,
                               "median_tflops": round(med, 1), "median_us": round(flops / med / 1e6, 1),
                               "min": round(min(res[k]), 1), "max": round(max(res[k]), 1),
                               "relerr": errs[k], "bitwise_eq_first": same[k]}), flush=True)
