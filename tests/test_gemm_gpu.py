@@ -469,6 +469,24 @@ def test_streaming_w4s_matches_w4_bitwise(b, M, N, K):
         assert torch.equal(out, ref)
 
 
+@pytest.mark.parametrize("b,M,N,K", [(1, 4096, 4096, 512), (2, 4096, 8192, 384), (1, 8192, 8192, 384),
+                                     (1, 16384, 2048, 384)])
+def test_streaming_w4s_rot_matches_w4_bitwise(b, M, N, K):
+    """A/B kernel x_w4s_rot (W4S with the XCD -> block position rotated per
+    round, map_tile supertile 6; thin grids keep their own maps): every tile
+    once, bitwise equal to W4."""
+    if not gemm.experiments_built():
+        pytest.skip("x_w4s_rot: PDMB_EXPERIMENTS=1 build only")
+    g = torch.Generator(device="cuda").manual_seed(b * 7 + M + N + K)
+    shape = (b,) if b > 1 else ()
+    A = torch.randn(*shape, M, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    B = torch.randn(*shape, K, N, device="cuda", dtype=torch.bfloat16, generator=g)
+    ref = gemm.matmul(A, B, kernel="w4", splitk=1)
+    out = torch.full_like(ref, float("nan"))
+    gemm.matmul(A, B, out=out, kernel="x_w4s_rot")
+    assert torch.equal(out, ref)
+
+
 def test_streaming_w4s_fp16_exact():
     g = torch.Generator(device="cuda").manual_seed(5)
     A = torch.randint(-3, 4, (2048, 1024), device="cuda", generator=g).to(torch.float16)
