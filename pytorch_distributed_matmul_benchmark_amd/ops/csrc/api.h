@@ -54,6 +54,9 @@ enum ExperimentKernel : int {
   kMfmaW4SRot = 39,    // W4S with the per-round rotating XCD block map (supertile 6)
   kMfmaW4SRotTrace = 40,  // kMfmaW4SRot with per-workgroup start / end stamps
   kMfmaW4Il32 = 30,   // kMfmaW4 (bf16) with the 8-wave kernel's 32-column B-half interleave
+  kFp8W4TS = 43,      // kFp8W4 with plain (temporal) C stores (shipping: non-temporal)
+  kFp8W4STS = 44,     // kFp8W4S with plain C stores
+  kMfmaW4STS = 45,    // kMfmaW4S (bf16) with plain C stores
 };
 
 // True iff this library was built with the experiment kernels.

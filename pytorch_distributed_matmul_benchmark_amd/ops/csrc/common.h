@@ -127,7 +127,12 @@ constexpr int kEpiBuf = epi_buf<8>();  // one 16-row block of W4, 4224 B
 // ldc_b bytes) through `buf` (epi_buf<NB>() bytes of LDS owned by this
 // wave). MASK: rows >= M are skipped, column chunks are cut at N (N % 4 ==
 // 0: a chunk is all, half or none).
-template <int DT, bool MASK, bool SCALE, int NB = 8>
+// NTS (default): non-temporal C stores (global_store ... nt). C is written
+// once and never read back by the kernel; hipBLASLt's fp8 kernels store it
+// the same way ("NTD"). Measured vs plain stores (profiles/
+// r2_ntstore_ab.jsonl): fp8 W4 4096^3 2538 -> 2760 TF, fp8 W4S 16k +0.6 %,
+// bf16 W4S 16384^2 x 2048 +1.1 %, 16k +0.2 %; never slower.
+template <int DT, bool MASK, bool SCALE, int NB = 8, bool NTS = true>
 __device__ __forceinline__ void store_block16(char* buf, const f32x4 (&v)[NB], float alpha, char* C,
                                               long long ldc_b, int row0, int col0, int M, int N,
                                               int lane) {
@@ -157,13 +162,16 @@ __device__ __forceinline__ void store_block16(char* buf, const f32x4 (&v)[NB], f
     char* p = C + (long long)row * ldc_b + (long long)col * 2;
     if constexpr (MASK) {
       if (row < M) {
-        if (col + 8 <= N)
-          *(u32x4*)p = x;
-        else if (col + 4 <= N)
+        if (col + 8 <= N) {
+          if constexpr (NTS) __builtin_nontemporal_store(x, (u32x4*)p);
+          else *(u32x4*)p = x;
+        } else if (col + 4 <= N) {
           *(u32x2*)p = u32x2{x.x, x.y};
+        }
       }
     } else {
-      *(u32x4*)p = x;
+      if constexpr (NTS) __builtin_nontemporal_store(x, (u32x4*)p);
+      else *(u32x4*)p = x;
     }
   }
 }

@@ -73,7 +73,8 @@ bool experiments_built() {
 }
 
 static bool is_fp8_kernel(int k) {
-  return k == kFp8W4 || k == kFp8W4S || k == kFp8T128 || k == kFp8T256x128 || k == kFp8 || k == kFp8W4Diag || k == kFp8W4Diag2 || k == kFp8W4Diag3 ||
+  return k == kFp8W4 || k == kFp8W4S || k == kFp8T128 || k == kFp8T256x128 || k == kFp8 || k == kFp8W4TS ||
+         k == kFp8W4STS || k == kFp8W4Diag || k == kFp8W4Diag2 || k == kFp8W4Diag3 ||
          k == kFp8W4Tall || k == kFp8W4Wide || k == kFp8W4Scaled || k == kFp8W4Trace;
 }
 
@@ -84,6 +85,7 @@ static bool is_experiment(int k) {
     case kFp8W4Diag2: case kFp8W4Diag3: case kF32NoDma: case kMfmaW4Tall: case kMfmaW4Wide: case kMfmaW4Il32:
     case kMfmaW4Pers: case kMfmaW4PersTrace: case kMfmaW4STrace: case kMfmaW4SRot: case kMfmaW4SRotTrace:
     case kFp8W4Tall: case kFp8W4Wide: case kFp8W4Scaled: case kFp8W4Trace: case kMfmaW4Trace:
+    case kFp8W4TS: case kFp8W4STS: case kMfmaW4STS:
       return true;
     default:
       return false;
@@ -110,7 +112,7 @@ int resolve_kernel(const Problem& p, int kernel) {
         !gemm_fp8_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C))
       return -1;
     const bool s_fits = gemm_fp8_w4s_fits(a) && device_cus() % 8 == 0;
-    if (kernel == kFp8W4S) return s_fits ? kFp8W4S : -1;
+    if (kernel == kFp8W4S || kernel == kFp8W4STS) return s_fits ? kernel : -1;
     if (kernel == kFp8T128 || kernel == kFp8T256x128) return supports(p, kernel) ? kernel : -1;
     if (kernel != kAuto) return kernel;
     // the streaming kernel on a device of its own with >= 2 tiles per CU (as W4S)
@@ -158,7 +160,7 @@ int resolve_kernel(const Problem& p, int kernel) {
     case kMfmaW4Tall: case kMfmaW4Wide: case kMfmaW4Il32: case kMfmaW4Trace:
     case kMfmaW4PersTrace:
       return (p.dtype == kBF16 && w4) ? kernel : -1;
-    case kMfmaW4STrace: case kMfmaW4SRot: case kMfmaW4SRotTrace:
+    case kMfmaW4STrace: case kMfmaW4SRot: case kMfmaW4SRotTrace: case kMfmaW4STS:
       return (p.dtype == kBF16 && w4 && w4s_fits(p)) ? kernel : -1;
     case kMfmaW4Pers: return w4 ? kernel : -1;  // bf16 and fp16
 #endif
@@ -397,7 +399,7 @@ static hipError_t tiled_launch(const Problem& p, int k, GemmArgs a, void* part, 
     }
   }
   a.splitk = S;
-  if (sub >= 7 && sub <= 10) {  // W4S: unsplit, one workgroup per usable CU (a multiple of 8)
+  if (sub >= 7 && sub <= 11) {  // W4S: unsplit, one workgroup per usable CU (a multiple of 8)
     if (S > 1) {
       sub = 0;
     } else {
@@ -651,6 +653,13 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kFp8W4Wide: return gemm_fp8_launch(a, 13, stream);
     case kFp8W4Scaled: return gemm_fp8_launch(a, 14, stream);
     case kFp8W4Trace: return gemm_fp8_launch(a, 15, stream);
+    case kFp8W4TS: return gemm_fp8_launch(a, 16, stream);
+    case kFp8W4STS: {
+      GemmArgs s = a;
+      s.pers_grid = ((p.cus > 0 ? p.cus : device_cus()) / 8) * 8;
+      return gemm_fp8_launch(s, 17, stream);
+    }
+    case kMfmaW4STS: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 11);
     case kMfma256: return gemm256_launch(p.dtype, a, 0, stream);
     case kMfma256b: return gemm256_launch(p.dtype, a, 1, stream);
     case kMfma256c: return gemm256_launch(p.dtype, a, 2, stream);
@@ -772,6 +781,9 @@ const char* kernel_name(int kernel) {
     case kMfmaW4STrace: return "pdmb_w4s_trace";
     case kMfmaW4SRot: return "pdmb_w4s_rot";
     case kMfmaW4SRotTrace: return "pdmb_w4s_rot_trace";
+    case kFp8W4TS: return "pdmb_fp8_w4_nt_tstore";
+    case kFp8W4STS: return "pdmb_fp8_w4s_tstore";
+    case kMfmaW4STS: return "pdmb_w4s_tstore";
     case kFp8W4Trace: return "pdmb_fp8_w4_nt_trace";
     default: return "auto";
   }

@@ -443,7 +443,8 @@ __device__ __forceinline__ void ktile_w4(const Ctx4& c, const char* smem, int t,
 // SUB: XCD sub-block shape (map_tile); 1 (8x4) and 2 (2x16) are A/B experiments.
 // SCALED: see mfma_f8_acc (1 = kFp8W4Scaled, A/B only).
 // TRACE: write the tile timeline (common.h tile_trace_write; kFp8W4Trace).
-template <int DIAG_NOWAIT, int SUB = 0, int SCALED = 0, int TRACE = 0>
+// NTS: non-temporal C stores (common.h store_block16; false: A/B kFp8W4TS).
+template <int DIAG_NOWAIT, int SUB = 0, int SCALED = 0, int TRACE = 0, bool NTS = true>
 __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE4];
   TileTrace tr;
@@ -562,10 +563,10 @@ __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4(GemmArgs a) {
       splitk_row<8, 8, NT4>(a, sl, slice, i, acc, v);
     }
     if (interior)
-      store_block16<kBF16, false, true>(ebuf + (i & 1) * kEpiBuf, v, alpha, Cb, (long long)a.ldc * 2,
+      store_block16<kBF16, false, true, 8, NTS>(ebuf + (i & 1) * kEpiBuf, v, alpha, Cb, (long long)a.ldc * 2,
                                         m0 + wr * 128 + i * 16, n0 + wc * 128, a.M, a.N, lane);
     else
-      store_block16<kBF16, true, true>(ebuf + (i & 1) * kEpiBuf, v, alpha, Cb, (long long)a.ldc * 2,
+      store_block16<kBF16, true, true, 8, NTS>(ebuf + (i & 1) * kEpiBuf, v, alpha, Cb, (long long)a.ldc * 2,
                                        m0 + wr * 128 + i * 16, n0 + wc * 128, a.M, a.N, lane);
   }
   if constexpr (TRACE) {
@@ -650,6 +651,7 @@ __device__ __forceinline__ void ktile_w4s(const Ctx4& c, const char* smem, u32x4
   }
 }
 
+template <bool NTS = true>  // NTS: non-temporal C stores (false: A/B kFp8W4STS)
 __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4s(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE4 + 4 * kEpiBuf];
   const int T = a.tiles_m * a.tiles_n * a.batch;
@@ -777,7 +779,7 @@ __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4s(GemmArgs a) {
     const int eln = (int)__builtin_amdgcn_mbcnt_hi(all, __builtin_amdgcn_mbcnt_lo(all, 0u));
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-      store_block16<kBF16, false, true>(ebuf, acc[i], a.alpha, Cb, (long long)a.ldc * 2,
+      store_block16<kBF16, false, true, 8, NTS>(ebuf, acc[i], a.alpha, Cb, (long long)a.ldc * 2,
                                         tm * BM + wr * 128 + i * 16, tn * BN + wc * 128, a.M, a.N, eln);
     __builtin_amdgcn_sched_barrier(0);
     if (!more) break;
@@ -838,7 +840,7 @@ hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream) {
   if (variant == 2) {  // kFp8W4S: streaming persistent (host: gemm_fp8_w4s_fits, pers_grid % 8 == 0)
     if (!gemm_fp8_w4s_fits(a) || a.pers_grid <= 0 || a.pers_grid % 8) return hipErrorInvalidValue;
     const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
-    hipLaunchKernelGGL(k8::gemm_fp8_w4s, pg, dim3(k8::NT4), 0, stream, a);
+    hipLaunchKernelGGL(k8::gemm_fp8_w4s<true>, pg, dim3(k8::NT4), 0, stream, a);
     return hipGetLastError();
   }
 #ifdef PDMB_EXPERIMENTS
@@ -856,6 +858,13 @@ hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream) {
     hipLaunchKernelGGL((k8::gemm_fp8_w4<0, 0, 1>), grid, dim3(k8::NT4), 0, stream, a);
   else if (variant == 15)
     hipLaunchKernelGGL((k8::gemm_fp8_w4<0, 0, 0, 1>), grid, dim3(k8::NT4), 0, stream, a);
+  else if (variant == 16)
+    hipLaunchKernelGGL((k8::gemm_fp8_w4<0, 0, 0, 0, false>), grid, dim3(k8::NT4), 0, stream, a);
+  else if (variant == 17) {
+    if (!gemm_fp8_w4s_fits(a) || a.pers_grid <= 0 || a.pers_grid % 8) return hipErrorInvalidValue;
+    const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
+    hipLaunchKernelGGL(k8::gemm_fp8_w4s<false>, pg, dim3(k8::NT4), 0, stream, a);
+  }
   else
     hipLaunchKernelGGL(k8::gemm_fp8_nt, grid, dim3(k8::NTHREADS), 0, stream, a);
 #else

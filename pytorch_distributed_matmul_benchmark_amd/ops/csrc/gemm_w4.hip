@@ -543,7 +543,7 @@ __device__ __forceinline__ void ktile_s(const Ctx& c, const char* smem, u32x4 ra
 
 // TRACE (kMfmaW4STrace): each workgroup stamps its start and end (after the
 // final drain) into the tile-trace row blockIdx.x, for the per-XCD tail.
-template <int DT, int TRACE = 0>
+template <int DT, int TRACE = 0, bool NTS = true>  // NTS: non-temporal C stores (false: A/B)
 __global__ void __launch_bounds__(NT, 1) gemm_w4s(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 4 * kEpiBuf];
   TileTrace tr;
@@ -729,8 +729,9 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4s(GemmArgs a) {
       f32x4 v[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = acc[i][j];
-      store_block16<DT, false, false>(ebuf, v, 1.0f, Cb, (long long)a.ldc * 2,
-                                      tm * BM + wr * 128 + i * 16, tn * BN + wc * 128, a.M, a.N, eln);
+      store_block16<DT, false, false, 8, NTS>(ebuf, v, 1.0f, Cb, (long long)a.ldc * 2,
+                                              tm * BM + wr * 128 + i * 16, tn * BN + wc * 128, a.M,
+                                              a.N, eln);
     }
     __builtin_amdgcn_sched_barrier(0);
     if (!more) break;
@@ -815,6 +816,13 @@ hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
   }
 #endif
 #ifdef PDMB_EXPERIMENTS
+  if (sub == 11) {  // W4S with plain (temporal) C stores
+    if (S > 1 || a.pers_grid <= 0 || a.pers_grid % 8 || (a.K / kw4::BK) % 2 || a.K / kw4::BK < 6)
+      return hipErrorInvalidValue;
+    const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
+    hipLaunchKernelGGL((kw4::gemm_w4s<kBF16, 0, false>), pg, block, 0, stream, a);
+    return hipGetLastError();
+  }
   if (sub == 9) {  // W4S with the per-round rotating XCD block map (supertile 6)
     if (S > 1 || a.pers_grid <= 0 || a.pers_grid % 8 || (a.K / kw4::BK) % 2 || a.K / kw4::BK < 6)
       return hipErrorInvalidValue;
