@@ -253,3 +253,26 @@ def test_fp8_tile_family_refusals_and_race_screen():
     assert _relerr(ref, (A8.double() * sa) @ (B8.double() * sb)) < 8e-3
     for _ in range(20):
         assert torch.equal(gemm.matmul(A8, B8, alpha=sa * sb, kernel="fp8_t128"), ref)
+
+
+def test_fp8_planner_choices():
+    """Auto on the reference's default sizes and their matrix_parallel shards
+    (profiles/r2_fp8_tile_family_ab.jsonl): the fp8 tile family for grids
+    that under-fill the 256 CUs with 256^2 tiles, W4 at one tile per CU,
+    W4S from two."""
+    if torch.cuda.get_device_properties(0).multi_processor_count != 256:
+        pytest.skip("planner constants are for the 256-CU MI355X")
+
+    def pick(M, N, K):
+        A = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).to(FP8)
+        B = _colmajor(torch.empty(K, N, device="cuda", dtype=torch.bfloat16).to(FP8))
+        return gemm.kernel_for(A, B)
+
+    assert pick(2048, 2048, 2048) == "pdmb_fp8_t128_nt"
+    assert pick(4096, 512, 4096) == "pdmb_fp8_t128_nt"
+    assert pick(4096, 1024, 4096) == "pdmb_fp8_t128_nt"
+    assert pick(8192, 1024, 8192) == "pdmb_fp8_t256x128_nt"
+    assert pick(4096, 4096, 4096) == "pdmb_fp8_w4_nt"
+    assert pick(16384, 16384, 16384) == "pdmb_fp8_w4s"
+    with gemm.shared_device():
+        assert pick(16384, 16384, 16384) == "pdmb_fp8_w4_nt"
