@@ -176,6 +176,36 @@ __device__ __forceinline__ void store_block16(char* buf, const f32x4 (&v)[NB], f
   }
 }
 
+// fp32 C (exact-fp32 kernels): the same whole-row epilogue for f32x4 C^T
+// blocks. Buffer rows are NB * 64 + 16 bytes (528 for NB = 8: the b128
+// writes of 16 rows at one column land 4 banks apart, conflict-free); each
+// read instruction moves 64 / (NB * 4) whole rows; stores are non-temporal.
+// MASK: rows >= M skipped, 16-B chunks at or past N dropped (N % 4 == 0).
+template <int NB>
+constexpr int epi_buf_f32() { return 16 * (NB * 64 + 16); }
+
+template <bool MASK, int NB = 8>
+__device__ __forceinline__ void store_block16_f32(char* buf, const f32x4 (&v)[NB], char* C, long long ldc_b,
+                                                  int row0, int col0, int M, int N, int lane) {
+  constexpr int P = NB * 64 + 16;
+  constexpr int CPR = NB * 4;    // 16-B chunks per row
+  constexpr int RPI = 64 / CPR;  // rows per read instruction
+  const int l16 = lane & 15, g = lane >> 4;
+  typedef __attribute__((address_space(3))) char lds_char;
+  lds_char* lb = (lds_char*)(lds_void*)buf;
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+    *(__attribute__((address_space(3))) f32x4*)(lb + l16 * P + (j * 16 + 4 * g) * 4) = v[j];
+  const int rl = lane / CPR, ch = lane % CPR;
+#pragma unroll
+  for (int r = 0; r < 16 / RPI; ++r) {
+    const u32x4 x = *(lds_u32x4_t*)(lb + (RPI * r + rl) * P + ch * 16);
+    const int row = row0 + RPI * r + rl, col = col0 + 4 * ch;
+    char* p = C + (long long)row * ldc_b + (long long)col * 4;
+    if (!MASK || (row < M && col + 4 <= N)) __builtin_nontemporal_store(x, (u32x4*)p);
+  }
+}
+
 // ---- Tile timeline trace (diagnostic kernel ids; a.dbg != nullptr) --------
 // Per tile 8 u64 at dbg[row * 8] (row = the tile's virtual block): [0] start, [1] first K-tile's
 // fragments in registers, [2] K-loop done, [3] C stored and drained

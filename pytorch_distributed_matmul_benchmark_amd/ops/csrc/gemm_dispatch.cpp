@@ -85,7 +85,7 @@ static bool is_experiment(int k) {
     case kFp8W4Diag2: case kFp8W4Diag3: case kF32NoDma: case kMfmaW4Tall: case kMfmaW4Wide: case kMfmaW4Il32:
     case kMfmaW4Pers: case kMfmaW4PersTrace: case kMfmaW4STrace: case kMfmaW4SRot: case kMfmaW4SRotTrace:
     case kFp8W4Tall: case kFp8W4Wide: case kFp8W4Scaled: case kFp8W4Trace: case kMfmaW4Trace:
-    case kFp8W4TS: case kFp8W4STS: case kMfmaW4STS:
+    case kFp8W4TS: case kFp8W4STS: case kMfmaW4STS: case kF32_256sDirect:
       return true;
     default:
       return false;
@@ -94,6 +94,7 @@ static bool is_experiment(int k) {
 
 static int device_cus();
 static int fp8_split(const Problem& p);
+static int f32_split(const Problem& p);
 static bool w4s_fits(const Problem& p);
 static bool w4s_auto(const Problem& p);
 static bool supports(const Problem& p, int kernel);
@@ -140,9 +141,13 @@ int resolve_kernel(const Problem& p, int kernel) {
         const Plan pl = plan(p, kAuto);
         return pl.kernel == kMfmaW4 && pl.splitk == 1 && w4s_auto(p) ? kMfmaW4S : pl.kernel;
       }
-      // fp32: the 4-wave kernel (150.4 vs 150.1 TF for f32_256s at 16k,
-      // profiles/r2_f32_w4_ab_v2.jsonl; hipBLASLt 154.4).
-      return fast ? kMfma256d : f32fast ? kF32W4 : kGeneric;
+      // fp32: the 8-wave f32_256s where the grid fills the chip — ahead of
+      // f32_w4 by 1.0-2.2 % on three boxes, behind by 0.2-0.4 % on one
+      // (profiles/r2_f32_lds_epilogue_ab_box*.jsonl, r2_f32_splitk_ab.jsonl) —
+      // and f32_w4 with split-K where it does not (f32_split).
+      if (fast) return kMfma256d;
+      if (!f32fast) return kGeneric;
+      return f32_split(p) > 1 ? kF32W4 : kF32_256s;
     case kGeneric: return kGeneric;
     case kMfma256d: return fast ? kMfma256d : -1;
     case kMfmaW4: return w4 ? kMfmaW4 : -1;
@@ -153,7 +158,7 @@ int resolve_kernel(const Problem& p, int kernel) {
     case kF32_256s: return f32fast ? kF32_256s : -1;
     case kF32W4: return f32fast ? kF32W4 : -1;  // same constraints as f32_256
 #ifdef PDMB_EXPERIMENTS
-    case kF32_256: case kF32NoDma: return f32fast ? kernel : -1;
+    case kF32_256: case kF32NoDma: case kF32_256sDirect: return f32fast ? kernel : -1;
     case kMfma256: case kMfma256b: case kMfma256c: return fast ? kernel : -1;
     case kMfma256X1: case kMfma256X2: case kMfma256X4: case kMfma256Stamp:
       return (fast && p.dtype == kBF16) ? kernel : -1;
@@ -320,6 +325,7 @@ int choose_splitk(const Problem& p, int kernel) {
   const int k = resolve_kernel(p, kernel);
   if (k == kMfmaW4S || k == kFp8W4S) return 1;
   if (k == kFp8W4) return fp8_split(p);
+  if (k == kF32W4) return f32_split(p);
   if (!is_tiled(k)) return 0;
   return plan(p, k).splitk;
 }
@@ -341,6 +347,22 @@ static int fp8_split(const Problem& p) {
     if (T * s <= cus && nk / s >= 16 && T <= kMaxSplitTiles) S = s;
   return S;
 }
+// fp32 W4 split-K (gemm_f32_w4.hip): the same rule for exact fp32, whose
+// 256x256x32 K-tile takes ~7 us, so slices of >= 8 K-tiles dwarf the meet.
+// matrix_parallel's fp32 shards at the reference's sizes (4096 x {2048, 1024,
+// 512} x 4096: 128 / 64 / 32 tiles) otherwise leave 1/2 .. 7/8 of the CUs idle
+// (75 / 37.5 TF vs hipBLASLt 140 / 130, profiles/r2_f32_lds_epilogue_ab_box*.jsonl).
+static int f32_split(const Problem& p) {
+  if (p.splitk > 0) return p.splitk;
+  const long long T = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256) * (p.batch < 1 ? 1 : p.batch);
+  const int nk = p.K / 32;
+  const long long cus = p.cus > 0 ? p.cus : device_cus();
+  int S = 1;
+  for (int s : {2, 4, 8})
+    if (T * s <= cus && nk / s >= 8 && T <= kMaxSplitTiles) S = s;
+  return S;
+}
+
 static size_t fp8_split_bytes(const Problem& p, int S) {
   if (S <= 1) return 0;
   const long long T = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256) * (p.batch < 1 ? 1 : p.batch);
@@ -544,6 +566,7 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel) {
   const int k = resolve_kernel(p, kernel);
   if (is_tiled(k)) return splitk_bytes(p, k, plan(p, k).splitk);
   if (k == kFp8W4) return fp8_split_bytes(p, fp8_split(p));
+  if (k == kF32W4) return fp8_split_bytes(p, f32_split(p));  // same 256x256 fp32 slots
   if (k == kMfmaW4Tall || k == kMfmaW4Wide || k == kMfmaW4Il32 || k == kMfmaW4Trace ||
       k == kMfmaW4Pers || k == kMfmaW4PersTrace)
     return splitk_bytes(p, kMfmaW4, plan(p, kMfmaW4).splitk);
@@ -643,7 +666,22 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kFp8T256x128: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream);
     case kMfmaW4S: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 7);
     case kF32_256s: return gemm_f32_256_launch(a, 1, stream);
-    case kF32W4: return gemm_f32_w4_launch(a, stream);
+    case kF32W4: {
+      GemmArgs s = a;
+      s.splitk = 1;
+      const int S = f32_split(p);
+      if (S > 1) {
+        unsigned* flags = stream_counters(stream);
+        if (flags && p.workspace && p.workspace_bytes >= fp8_split_bytes(p, S)) {
+          s.splitk = S;
+          s.part = (float*)p.workspace;
+          s.flags = flags;
+        } else if (p.splitk > 1) {
+          return hipErrorInvalidValue;  // explicitly requested: no silent change
+        }
+      }
+      return gemm_f32_w4_launch(s, stream);
+    }
 #ifdef PDMB_EXPERIMENTS
     case kFp8: return gemm_fp8_launch(a, 0, stream);
     case kFp8W4Diag: return gemm_fp8_launch(a, 9, stream);
@@ -675,6 +713,7 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kMfmaW4SRotTrace: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 10);
     case kF32_256: return gemm_f32_256_launch(a, 0, stream);
     case kF32NoDma: return gemm_f32_256_launch(a, 9, stream);
+    case kF32_256sDirect: return gemm_f32_256_launch(a, 10, stream);
     case kMfma256X1: case kMfma256X2: case kMfma256X4:
       return gemm256_launch(p.dtype, a, 10 + (k - kMfma256X1 + 1), stream);
 #endif
@@ -784,6 +823,7 @@ const char* kernel_name(int kernel) {
     case kFp8W4TS: return "pdmb_fp8_w4_nt_tstore";
     case kFp8W4STS: return "pdmb_fp8_w4s_tstore";
     case kMfmaW4STS: return "pdmb_w4s_tstore";
+    case kF32_256sDirect: return "pdmb_f32_256s_direct";
     case kFp8W4Trace: return "pdmb_fp8_w4_nt_trace";
     default: return "auto";
   }

@@ -114,7 +114,9 @@ __device__ __forceinline__ void tile_barrier() {
 
 // NODMA: timing-only diagnostic (the K-loop issues no loads, results are
 // wrong): the ceiling of the compute + barrier structure alone.
-template <bool STAGGER, bool NODMA = false>
+// LDSEPI: C through LDS as whole rows with non-temporal stores (common.h
+// store_block16_f32; the shipping form); false: direct 16-B stores (A/B).
+template <bool STAGGER, bool NODMA = false, bool LDSEPI = true>
 __global__ void __launch_bounds__(NT, 2) gemm_f32_256(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
@@ -166,6 +168,21 @@ __global__ void __launch_bounds__(NT, 2) gemm_f32_256(GemmArgs a) {
     }
   }
 
+  if constexpr (LDSEPI) {  // the loop ended at a barrier: every wave is done with the stages
+    char* Cb = (char*)a.C + (long long)bz * a.sC * 4;
+    char* ebuf = smem + wu * epi_buf_f32<4>();
+    const bool interior = m0 + BM <= a.M && n0 + BN <= a.N;
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+      if (interior)
+        store_block16_f32<false, 4>(ebuf, acc[mi], Cb, (long long)a.ldc * 4, m0 + wr * 128 + mi * 16,
+                                    n0 + wc * 64, a.M, a.N, lane);
+      else
+        store_block16_f32<true, 4>(ebuf, acc[mi], Cb, (long long)a.ldc * 4, m0 + wr * 128 + mi * 16,
+                                   n0 + wc * 64, a.M, a.N, lane);
+    }
+    return;
+  }
   float* Cb = (float*)a.C + (long long)bz * a.sC;
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi) {
@@ -209,6 +226,8 @@ hipError_t gemm_f32_256_launch(GemmArgs a, int variant, hipStream_t stream) {
 #ifdef PDMB_EXPERIMENTS
   if (variant == 9)
     hipLaunchKernelGGL((kf32::gemm_f32_256<false, true>), grid, block, 0, stream, a);
+  else if (variant == 10)  // kF32_256sDirect: the shipping kernel with direct C stores
+    hipLaunchKernelGGL((kf32::gemm_f32_256<true, false, false>), grid, block, 0, stream, a);
   else
     hipLaunchKernelGGL(kf32::gemm_f32_256<false>, grid, block, 0, stream, a);
   return hipGetLastError();

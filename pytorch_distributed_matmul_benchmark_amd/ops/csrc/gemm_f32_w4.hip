@@ -27,10 +27,12 @@
 // read latency is exposed (round 2's first version waited at the top of each
 // tile and ran 1 % behind f32_256s).
 // Operands swapped (B element as the MFMA's A) so each lane owns 4
-// consecutive output columns -> 16-B stores. Edges: the DMA descriptors'
+// consecutive output columns; C leaves through LDS as whole rows. Edges: the DMA descriptors'
 // extents read zeros past M / N / K, the stores are masked, so any M and
 // N % 4 == 0 runs here (the host checks K % 32, alignment).
+#include "api.h"
 #include "common.h"
+#include "splitk.h"
 
 namespace pdmb {
 namespace kf32w4 {
@@ -136,6 +138,16 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4(GemmArgs a) {
 
   int bz, tm, tn;
   map_tile(a, blockIdx.x, bz, tm, tn);
+  // Split-K (under-filled grids: matrix_parallel's fp32 column shards): the
+  // grid's batch is batch x S with the slice innermost, as in gemm_w4.hip;
+  // slice s runs K-tiles [s * kt_per, +kt_per) and the S slices of a tile
+  // meet in the epilogue (splitk.h).
+  int slice = 0;
+  if (a.splitk > 1) {
+    slice = bz % a.splitk;
+    bz /= a.splitk;
+  }
+  const int kt0 = slice * a.kt_per;
   const int m0 = tm * BM, n0 = tn * BN;
   const int lane = threadIdx.x & 63;
   const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -147,11 +159,12 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4(GemmArgs a) {
   c.lds0 = (uint32_t)(size_t)((lds_void*)smem);
   c.lda4 = a.lda * 4;
   c.ldb4 = a.ldb * 4;
-  c.nk = a.K / BK;
-  c.Ab = (const char*)a.A + ((long long)bz * a.sA + (long long)m0 * a.lda) * 4;
-  c.Bb = (const char*)a.B + ((long long)bz * a.sB + n0) * 4;
-  c.a_bytes = ((long long)(a.M - m0 - 1) * a.lda + a.K) * 4;
-  c.b_bytes = ((long long)(a.K - 1) * a.ldb + (a.N - n0)) * 4;
+  c.nk = a.splitk > 1 ? min(a.kt_per, a.K / BK - kt0) : a.K / BK;
+  const long long k0 = (long long)kt0 * BK;
+  c.Ab = (const char*)a.A + ((long long)bz * a.sA + (long long)m0 * a.lda + k0) * 4;
+  c.Bb = (const char*)a.B + ((long long)bz * a.sB + k0 * a.ldb + n0) * 4;
+  c.a_bytes = ((long long)(a.M - m0 - 1) * a.lda + (a.K - k0)) * 4;
+  c.b_bytes = ((long long)(a.K - k0 - 1) * a.ldb + (a.N - n0)) * 4;
   {
     const int r = wu * 8 + (lane >> 3);  // row of A piece 0
     c.voffA = (uint32_t)(r * c.lda4 + (((lane & 7) ^ ((r >> 1) & 7)) * 16));
@@ -218,28 +231,55 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4(GemmArgs a) {
   // hipcc's hazard recognizer).
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
 
-  float* Cb = (float*)a.C + (long long)bz * a.sC;
+  // Split-K: only the last slice of a tile to arrive writes C, summing the
+  // slices' fp32 slots in slice order (bitwise reproducible).
+  SplitSlots sl;
+  const bool split = a.splitk > 1;
+  if (split && !splitk_meet<8, 8, NT>(a, smem, ((long long)bz * a.tiles_m + tm) * a.tiles_n + tn, slice,
+                                      acc, sl))
+    return;
+  // Epilogue through LDS as whole 512-B rows, non-temporal (common.h
+  // store_block16_f32), once every wave is done with the stages.
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  char* Cb = (char*)a.C + (long long)bz * a.sC * 4;
+  char* ebuf = smem + 1024 + wu * epi_buf_f32<8>();  // past splitk_meet's ticket word
+  const bool interior = m0 + BM <= a.M && n0 + BN <= a.N;
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi) {
-    const int row = m0 + wr * 128 + mi * 16 + l16;
-    if (row < a.M) {
-      float* crow = Cb + (long long)row * a.ldc;
+    f32x4 v[8];
+    if (!split) {
 #pragma unroll
-      for (int ni = 0; ni < 8; ++ni) {
-        const int col = n0 + wc * 128 + ni * 16 + 4 * g;
-        if (col < a.N) *(f32x4*)(crow + col) = acc[mi][ni];
-      }
+      for (int j = 0; j < 8; ++j) v[j] = acc[mi][j];
+    } else {
+      splitk_row<8, 8, NT>(a, sl, slice, mi, acc, v);
     }
+    if (interior)
+      store_block16_f32<false>(ebuf, v, Cb, (long long)a.ldc * 4, m0 + wr * 128 + mi * 16,
+                               n0 + wc * 128, a.M, a.N, lane);
+    else
+      store_block16_f32<true>(ebuf, v, Cb, (long long)a.ldc * 4, m0 + wr * 128 + mi * 16,
+                              n0 + wc * 128, a.M, a.N, lane);
   }
 }
 
 }  // namespace kf32w4
 
+// a.splitk > 1: split-K with a.part / a.flags (gemm_dispatch.cpp f32_split).
 hipError_t gemm_f32_w4_launch(GemmArgs a, hipStream_t stream) {
   a.tiles_m = (a.M + kf32w4::BM - 1) / kf32w4::BM;
   a.tiles_n = (a.N + kf32w4::BN - 1) / kf32w4::BN;
   a.supertile = choose_supertile(a.tiles_m, a.tiles_n);
-  const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch;
+  const int S = a.splitk > 1 ? a.splitk : 1;
+  if (S > 1) {
+    const int nk = a.K / kf32w4::BK;
+    a.kt_per = (nk + S - 1) / S;
+    if ((S - 1) * a.kt_per >= nk || !a.part || !a.flags ||
+        (long long)a.tiles_m * a.tiles_n * a.batch > kMaxSplitTiles)
+      return hipErrorInvalidValue;  // every slice must own >= 1 K-tile
+  } else {
+    a.splitk = 1;
+  }
+  const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch * S;
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
   hipLaunchKernelGGL(kf32w4::gemm_f32_w4, dim3((unsigned)nblocks), dim3(kf32w4::NT), 0, stream, a);

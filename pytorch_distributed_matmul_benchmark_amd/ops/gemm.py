@@ -37,7 +37,8 @@ EXPERIMENT_KERNELS = {"mfma256": 1, "mfma256b": 3, "mfma256c": 4, "mfma256c_stam
                       "x_w4_il32": 30, "x_fp8_w4_scaled": 31, "diag_w4_trace": 32,
                       "diag_fp8_w4_trace": 33, "x_w4_pers": 34, "diag_w4_pers_trace": 35,
                       "diag_w4s_trace": 38, "x_w4s_rot": 39, "diag_w4s_rot_trace": 40,
-                      "x_fp8_w4_tstore": 43, "x_fp8_w4s_tstore": 44, "x_w4s_tstore": 45}
+                      "x_fp8_w4_tstore": 43, "x_fp8_w4s_tstore": 44, "x_w4s_tstore": 45,
+                      "x_f32_256s_direct": 46}
 KERNEL_NAMES = {0: "auto", 2: "pdmb_generic_nn", 7: "pdmb_f32_256s_nn", 9: "pdmb_mfma256d_nn",
                 16: "pdmb_fp8_w4_nt", 21: "pdmb_w4_nn", 26: "pdmb_t128_nn",
                 27: "pdmb_t128x2_nn", 28: "pdmb_t256x128_nn", 29: "pdmb_f32_w4_nn", 36: "pdmb_w4s",
@@ -205,7 +206,7 @@ def padded_kernel_for(A: torch.Tensor, B: torch.Tensor) -> Optional[str]:
     out = torch.empty(_out_shape(A, B), dtype=out_dtype(A.dtype), device=A.device)
     A, B = _prep_pair(A, B)
     k = int(C.resolve_padded(A, B, out))
-    return KERNEL_NAMES[k] if k >= 0 else None
+    return _name(C, k) if k >= 0 else None
 
 
 def bmm(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
@@ -227,7 +228,12 @@ def kernel_for(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = N
     if out is None:
         out = torch.empty(_out_shape(A, B), dtype=out_dtype(A.dtype), device=A.device)
     A, B = _prep_pair(A, B)
-    return KERNEL_NAMES[int(C.resolve(A, B, out, _kid(kernel), _cus()))]
+    return _name(C, int(C.resolve(A, B, out, _kid(kernel), _cus())))
+
+
+def _name(C, k: int) -> str:
+    """Kernel name of id ``k`` (the library's own table for ids not mirrored here)."""
+    return KERNEL_NAMES.get(k) or str(C.kernel_name(k))
 
 
 def splitk_for(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,

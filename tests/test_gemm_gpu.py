@@ -160,8 +160,8 @@ def test_fp32_exact_mfma_path():
     torch.manual_seed(3)
     A = torch.randn(512, 512, device="cuda", dtype=torch.float32)
     B = torch.randn(512, 512, device="cuda", dtype=torch.float32)
-    assert gemm.kernel_for(A, B) == "pdmb_f32_w4_nn"
-    for k in ("auto", "generic", "f32_256s"):
+    assert gemm.kernel_for(A, B) == "pdmb_f32_w4_nn"  # 4 tiles: split-K on f32_w4
+    for k in ("auto", "generic", "f32_256s", "f32_w4"):
         C = gemm.matmul(A, B, kernel=k)
         assert _relerr(C, _ref(A, B)) < TOL[torch.float32]
 
@@ -202,7 +202,7 @@ def test_race_screen_repeated_runs(kernel):
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 32), (512, 768, 96), (1000, 1052, 320),
                                    (300, 200, 64), (2304, 2048, 1024)])
-@pytest.mark.parametrize("kernel", ["f32_256", "f32_256s", "f32_w4"])
+@pytest.mark.parametrize("kernel", ["f32_256", "f32_256s", "f32_w4", "x_f32_256s_direct"])
 def test_f32_256_exact_and_random(M, N, K, kernel):
     _need(kernel)
     g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
@@ -217,6 +217,30 @@ def test_f32_256_exact_and_random(M, N, K, kernel):
     assert _relerr(C, _ref(A, B)) < TOL[torch.float32]
 
 
+@pytest.mark.parametrize("M,N,K,splitk,expect", [(4096, 1024, 4096, 0, 4), (4096, 2048, 4096, 0, 2),
+                                                 (2048, 2048, 2048, 0, 4), (1000, 1052, 4096, 0, 8),
+                                                 (512, 512, 1024, 2, 2), (4096, 4096, 4096, 0, 1)])
+def test_f32_w4_splitk_exact(M, N, K, splitk, expect):
+    """Exact-fp32 W4 split-K for under-filled grids (matrix_parallel's fp32
+    shards): slices meet in-launch (splitk.h), edge tiles masked; exact on small
+    integers, and bitwise stable across launches (slot sums in slice order)."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + splitk)
+    A = torch.randint(-3, 4, (M, K), device="cuda", generator=g).float()
+    B = torch.randint(-3, 4, (K, N), device="cuda", generator=g).float()
+    assert gemm.kernel_for(A, B) == ("pdmb_f32_w4_nn" if expect > 1 else "pdmb_f32_256s_nn")
+    assert gemm.splitk_for(A, B, splitk=splitk) == (expect if expect > 1 else 0)
+    ref = _ref(A, B)
+    for _ in range(2):  # counters re-zeroed by every launch
+        C = torch.full((M, N), float("nan"), device="cuda")
+        gemm.matmul(A, B, out=C, splitk=splitk)
+        assert torch.equal(C.double(), ref)
+    A = torch.randn(M, K, device="cuda", generator=g)
+    B = torch.randn(K, N, device="cuda", generator=g)
+    C = gemm.matmul(A, B, splitk=splitk)
+    assert _relerr(C, _ref(A, B)) < TOL[torch.float32]
+    assert torch.equal(gemm.matmul(A, B, splitk=splitk), C)
+
+
 def test_f32_256_identity_batched_and_shards():
     n = 512
     A = torch.eye(n, device="cuda")
@@ -225,7 +249,7 @@ def test_f32_256_identity_batched_and_shards():
     torch.manual_seed(7)
     A3 = torch.randn(3, 384, 256, device="cuda")
     B3 = torch.randn(3, 256, 640, device="cuda")
-    assert gemm.kernel_for(A3, B3) == "pdmb_f32_w4_nn"
+    assert gemm.kernel_for(A3, B3) == "pdmb_f32_256s_nn"  # 18 tiles of 8 K-tiles: no split
     assert _relerr(gemm.bmm(A3, B3), torch.bmm(A3.double(), B3.double())) < TOL[torch.float32]
     Bf = torch.randn(1024, 1024, device="cuda")
     Af = torch.randn(1024, 1024, device="cuda")
@@ -256,7 +280,7 @@ def test_odd_sizes_padded_to_fast_path(dtype, M, N, K):
     A = torch.randn(M, K, device="cuda", dtype=dt)
     B = torch.randn(K, N, device="cuda", dtype=dt)
     assert gemm.kernel_for(A, B) == "pdmb_generic_nn"  # unpadded, only generic could run it
-    assert gemm.padded_kernel_for(A, B) in ("pdmb_mfma256d_nn", "pdmb_f32_w4_nn")
+    assert gemm.padded_kernel_for(A, B) in ("pdmb_mfma256d_nn", "pdmb_f32_w4_nn", "pdmb_f32_256s_nn")
     C = gemm.matmul(A, B)
     assert C.shape == (M, N)
     assert _relerr(C, _ref(A, B)) < TOL[dt]
