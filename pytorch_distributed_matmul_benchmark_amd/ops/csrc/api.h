@@ -58,6 +58,7 @@ enum ExperimentKernel : int {
   kFp8W4STS = 44,     // kFp8W4S with plain C stores
   kMfmaW4STS = 45,    // kMfmaW4S (bf16) with plain C stores
   kF32_256sDirect = 46,  // kF32_256s with direct (not LDS-staged, temporal) C stores
+  kFp8W4Unfused = 47,    // kFp8W4 with the epilogue after (not inside) the last K-tile
 };
 
 // True iff this library was built with the experiment kernels.

@@ -74,7 +74,7 @@ bool experiments_built() {
 
 static bool is_fp8_kernel(int k) {
   return k == kFp8W4 || k == kFp8W4S || k == kFp8T128 || k == kFp8T256x128 || k == kFp8 || k == kFp8W4TS ||
-         k == kFp8W4STS || k == kFp8W4Diag || k == kFp8W4Diag2 || k == kFp8W4Diag3 ||
+         k == kFp8W4STS || k == kFp8W4Unfused || k == kFp8W4Diag || k == kFp8W4Diag2 || k == kFp8W4Diag3 ||
          k == kFp8W4Tall || k == kFp8W4Wide || k == kFp8W4Scaled || k == kFp8W4Trace;
 }
 
@@ -85,7 +85,7 @@ static bool is_experiment(int k) {
     case kFp8W4Diag2: case kFp8W4Diag3: case kF32NoDma: case kMfmaW4Tall: case kMfmaW4Wide: case kMfmaW4Il32:
     case kMfmaW4Pers: case kMfmaW4PersTrace: case kMfmaW4STrace: case kMfmaW4SRot: case kMfmaW4SRotTrace:
     case kFp8W4Tall: case kFp8W4Wide: case kFp8W4Scaled: case kFp8W4Trace: case kMfmaW4Trace:
-    case kFp8W4TS: case kFp8W4STS: case kMfmaW4STS: case kF32_256sDirect:
+    case kFp8W4TS: case kFp8W4STS: case kMfmaW4STS: case kF32_256sDirect: case kFp8W4Unfused:
       return true;
     default:
       return false;
@@ -692,6 +692,7 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kFp8W4Scaled: return gemm_fp8_launch(a, 14, stream);
     case kFp8W4Trace: return gemm_fp8_launch(a, 15, stream);
     case kFp8W4TS: return gemm_fp8_launch(a, 16, stream);
+    case kFp8W4Unfused: return gemm_fp8_launch(a, 18, stream);
     case kFp8W4STS: {
       GemmArgs s = a;
       s.pers_grid = ((p.cus > 0 ? p.cus : device_cus()) / 8) * 8;
@@ -824,6 +825,7 @@ const char* kernel_name(int kernel) {
     case kFp8W4STS: return "pdmb_fp8_w4s_tstore";
     case kMfmaW4STS: return "pdmb_w4s_tstore";
     case kF32_256sDirect: return "pdmb_f32_256s_direct";
+    case kFp8W4Unfused: return "pdmb_fp8_w4_nt_unfused";
     case kFp8W4Trace: return "pdmb_fp8_w4_nt_trace";
     default: return "auto";
   }

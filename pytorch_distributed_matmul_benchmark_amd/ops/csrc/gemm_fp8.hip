@@ -440,13 +440,56 @@ __device__ __forceinline__ void ktile_w4(const Ctx4& c, const char* smem, int t,
   }
 }
 
+// The last K-tile of an unsplit tile with the epilogue folded in: block row
+// mi - 1 of C leaves (store_block16 through this wave's own LDS buffer, past
+// the two stages) while block row mi's MFMAs run, so the C stores of a tile
+// overlap its final MFMAs instead of following them (one tile per CU, e.g.
+// 4096^3: the whole kernel is one tile). No fragment reads or DMAs: the
+// fragments of the last K-tile are in registers, and no barrier is needed
+// (the stages are neither read nor refilled). Block mi's eight MFMAs separate
+// block mi - 1's last accumulator write from its AGPR reads.
+template <int SCALED, bool NTS>
+__device__ __forceinline__ void ktile_w4_last(f32x4 (&acc)[8][8], const i32x8 (&A)[8], const i32x8& A7c,
+                                              const i32x8 (&Bc)[8], int sc, char* ebuf, char* Cb,
+                                              long long ldc_b, int row0, int col0, int M, int N,
+                                              bool interior, float alpha, int lane) {
+  // The lane id is re-formed (v_mbcnt of an opaque mask) at every store so
+  // hipcc cannot hoist the eight stores' per-lane addresses above the MFMAs,
+  // where they would be live at once and spill (as W4S's epilogue).
+  (void)lane;
+  auto store = [&](int i) {
+    unsigned all = ~0u;
+    asm volatile("" : "+s"(all));
+    const int eln = (int)__builtin_amdgcn_mbcnt_hi(all, __builtin_amdgcn_mbcnt_lo(all, 0u));
+    if (interior)
+      store_block16<kBF16, false, true, 8, NTS>(ebuf, acc[i], alpha, Cb, ldc_b, row0 + i * 16, col0, M, N,
+                                                eln);
+    else
+      store_block16<kBF16, true, true, 8, NTS>(ebuf, acc[i], alpha, Cb, ldc_b, row0 + i * 16, col0, M, N,
+                                               eln);
+  };
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+#pragma unroll
+    for (int ni = 0; ni < 8; ++ni) mfma_f8_acc<SCALED>(acc[mi][ni], Bc[ni], mi == 7 ? A7c : A[mi], sc);
+    __builtin_amdgcn_sched_barrier(0);
+    if (mi >= 1) store(mi - 1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  store(7);
+}
+
 // SUB: XCD sub-block shape (map_tile); 1 (8x4) and 2 (2x16) are A/B experiments.
 // SCALED: see mfma_f8_acc (1 = kFp8W4Scaled, A/B only).
 // TRACE: write the tile timeline (common.h tile_trace_write; kFp8W4Trace).
 // NTS: non-temporal C stores (common.h store_block16; false: A/B kFp8W4TS).
-template <int DIAG_NOWAIT, int SUB = 0, int SCALED = 0, int TRACE = 0, bool NTS = true>
+// FUSED: unsplit tiles store C during their last K-tile (ktile_w4_last;
+// false: A/B kFp8W4Unfused).
+template <int DIAG_NOWAIT, int SUB = 0, int SCALED = 0, int TRACE = 0, bool NTS = true, bool FUSED = true>
 __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4(GemmArgs a) {
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE4];
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE4 + (FUSED ? 4 * kEpiBuf : 0)];
   TileTrace tr;
   if constexpr (TRACE) tr.t[0] = tile_clock();
 
@@ -527,12 +570,31 @@ __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4(GemmArgs a) {
   if constexpr (TRACE) tr.t[1] = tile_clock();
 #pragma unroll
   for (int h = 8; h < 16; ++h) issue_piece(c, 0, t2, h);
+  const bool split = a.splitk > 1;
+  constexpr bool kFuse = FUSED && TRACE == 0 && DIAG_NOWAIT == 0;
+  const bool fuse = kFuse && !split && (nk & 1) == 0;
+  const int nloop = fuse ? nk - 1 : nk;  // fused: the last K-tile is ktile_w4_last
   int t = 0;
-  for (; t + 1 < nk; t += 2) {  // branch-free body: B0/B1 and A7a/A7b swap roles every K-tile
+  for (; t + 1 < nloop; t += 2) {  // branch-free body: B0/B1 and A7a/A7b swap roles every K-tile
     ktile_w4<0, DIAG_NOWAIT, SCALED>(c, smem, t, acc, A, A7a, A7b, B0, B1, sc);
     ktile_w4<STAGE4, DIAG_NOWAIT, SCALED>(c, smem, t + 1, acc, A, A7b, A7a, B1, B0, sc);
   }
-  if (t < nk) ktile_w4<0, DIAG_NOWAIT, SCALED>(c, smem, t, acc, A, A7a, A7b, B0, B1, sc);  // odd count
+  if (t < nloop) ktile_w4<0, DIAG_NOWAIT, SCALED>(c, smem, t, acc, A, A7a, A7b, B0, B1, sc);  // odd count
+  if constexpr (kFuse) {
+    if (fuse) {
+      // nk even (host: fuse only then): the last K-tile nk-1 is odd and
+      // computes from (A7b, B1). Handling both parities here kept both sets
+      // live through the stores and made hipcc spill (AGPR copies it places
+      // next to the asm MFMAs, which it does not know to wait for).
+      char* Cb = (char*)a.C + (long long)bz * a.sC * 2;
+      char* ebuf = smem + 2 * STAGE4 + wu * kEpiBuf;
+      const bool interior = m0 + BM <= a.M && n0 + BN <= a.N;
+      ktile_w4_last<SCALED, NTS>(acc, A, A7b, B1, sc, ebuf, Cb, (long long)a.ldc * 2, m0 + wr * 128,
+                                 n0 + wc * 128, a.M, a.N, interior, a.alpha, lane);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail DMAs landed before the LDS is released
+      return;
+    }
+  }
   // Drain the tail DMAs and give the last MFMAs time to write their AGPRs
   // (asm MFMAs are invisible to hipcc's hazard recognizer).
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
@@ -541,7 +603,6 @@ __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4(GemmArgs a) {
   // Split-K: only the last slice of a tile to arrive writes C, summing the
   // slices' fp32 slots (unscaled) block row by block row (splitk.h).
   SplitSlots sl;
-  const bool split = a.splitk > 1;
   if (split && !splitk_meet<8, 8, NT4>(a, smem, ((long long)bz * a.tiles_m + tm) * a.tiles_n + tn,
                                        slice, acc, sl))
     return;
@@ -860,6 +921,8 @@ hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream) {
     hipLaunchKernelGGL((k8::gemm_fp8_w4<0, 0, 0, 1>), grid, dim3(k8::NT4), 0, stream, a);
   else if (variant == 16)
     hipLaunchKernelGGL((k8::gemm_fp8_w4<0, 0, 0, 0, false>), grid, dim3(k8::NT4), 0, stream, a);
+  else if (variant == 18)  // kFp8W4Unfused: the epilogue after the last K-tile
+    hipLaunchKernelGGL((k8::gemm_fp8_w4<0, 0, 0, 0, true, false>), grid, dim3(k8::NT4), 0, stream, a);
   else if (variant == 17) {
     if (!gemm_fp8_w4s_fits(a) || a.pers_grid <= 0 || a.pers_grid % 8) return hipErrorInvalidValue;
     const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
