@@ -11,4 +11,5 @@ step all_tests timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeou
 step smoke timeout -k 10 120 python __graft_entry__.py smoke &&
 step bench timeout -k 10 300 python bench.py &&
 step rocprof timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/rocprof -o bench -- python3 bench.py --steps 20 --warmup 5 &&
-step selflaunch timeout -k 10 300 python bench.py --gpus 2 --dist-backend gloo --size 4096 --steps 3 --warmup 1 --extra-steps 2 --extra-warmup 1
+step selflaunch timeout -k 10 300 python bench.py --gpus 2 --dist-backend gloo --size 4096 --steps 3 --warmup 1 --extra-steps 2 --extra-warmup 1 &&
+step selflaunch4 timeout -k 10 300 python bench.py --gpus 4 --dist-backend gloo --size 4096 --steps 3 --warmup 1 --extra-steps 2 --extra-warmup 1
