@@ -601,6 +601,7 @@ static hipError_t gemm_padded(const Problem& p, hipStream_t stream, int* used) {
   if (used) *used = k;
   if (k == kGeneric || k < 0) return hipErrorInvalidValue;  // cannot happen: q is aligned
   GemmArgs a = to_args(q);
+  a.splitk = 0;  // only the tiled kernels below split here (their slots follow the copies)
   char* part = Cp + d.c_bytes;
   const size_t part_bytes = p.workspace_bytes - (d.a_bytes + d.b_bytes + d.c_bytes);
   e = k == kF32W4     ? gemm_f32_w4_launch(a, stream)
