@@ -59,6 +59,8 @@ enum ExperimentKernel : int {
   kMfmaW4STS = 45,    // kMfmaW4S (bf16) with plain C stores
   kF32_256sDirect = 46,  // kF32_256s with direct (not LDS-staged, temporal) C stores
   kFp8W4Unfused = 47,    // kFp8W4 with the epilogue after (not inside) the last K-tile
+  kT128Unfused = 48,     // kT128 (bf16 / fp16) with the epilogue after the last K-tile
+  kFp8T128Unfused = 49,  // kFp8T128 with the epilogue after the last K-tile
 };
 
 // True iff this library was built with the experiment kernels.

@@ -74,7 +74,7 @@ bool experiments_built() {
 
 static bool is_fp8_kernel(int k) {
   return k == kFp8W4 || k == kFp8W4S || k == kFp8T128 || k == kFp8T256x128 || k == kFp8 || k == kFp8W4TS ||
-         k == kFp8W4STS || k == kFp8W4Unfused || k == kFp8W4Diag || k == kFp8W4Diag2 || k == kFp8W4Diag3 ||
+         k == kFp8W4STS || k == kFp8W4Unfused || k == kFp8T128Unfused || k == kFp8W4Diag || k == kFp8W4Diag2 || k == kFp8W4Diag3 ||
          k == kFp8W4Tall || k == kFp8W4Wide || k == kFp8W4Scaled || k == kFp8W4Trace;
 }
 
@@ -86,6 +86,7 @@ static bool is_experiment(int k) {
     case kMfmaW4Pers: case kMfmaW4PersTrace: case kMfmaW4STrace: case kMfmaW4SRot: case kMfmaW4SRotTrace:
     case kFp8W4Tall: case kFp8W4Wide: case kFp8W4Scaled: case kFp8W4Trace: case kMfmaW4Trace:
     case kFp8W4TS: case kFp8W4STS: case kMfmaW4STS: case kF32_256sDirect: case kFp8W4Unfused:
+    case kT128Unfused: case kFp8T128Unfused:
       return true;
     default:
       return false;
@@ -115,6 +116,7 @@ int resolve_kernel(const Problem& p, int kernel) {
     const bool s_fits = gemm_fp8_w4s_fits(a) && device_cus() % 8 == 0;
     if (kernel == kFp8W4S || kernel == kFp8W4STS) return s_fits ? kernel : -1;
     if (kernel == kFp8T128 || kernel == kFp8T256x128) return supports(p, kernel) ? kernel : -1;
+    if (kernel == kFp8T128Unfused) return supports(p, kFp8T128) ? kernel : -1;
     if (kernel != kAuto) return kernel;
     // the streaming kernel on a device of its own with >= 2 tiles per CU (as W4S)
     const long long T = (long long)(p.M / 256) * (p.N / 256) * (p.batch < 1 ? 1 : p.batch);
@@ -159,6 +161,7 @@ int resolve_kernel(const Problem& p, int kernel) {
     case kF32W4: return f32fast ? kF32W4 : -1;  // same constraints as f32_256
 #ifdef PDMB_EXPERIMENTS
     case kF32_256: case kF32NoDma: case kF32_256sDirect: return f32fast ? kernel : -1;
+    case kT128Unfused: return t128 ? kernel : -1;
     case kMfma256: case kMfma256b: case kMfma256c: return fast ? kernel : -1;
     case kMfma256X1: case kMfma256X2: case kMfma256X4: case kMfma256Stamp:
       return (fast && p.dtype == kBF16) ? kernel : -1;
@@ -694,6 +697,8 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kFp8W4Trace: return gemm_fp8_launch(a, 15, stream);
     case kFp8W4TS: return gemm_fp8_launch(a, 16, stream);
     case kFp8W4Unfused: return gemm_fp8_launch(a, 18, stream);
+    case kT128Unfused:
+    case kFp8T128Unfused: return gemm_tile_launch(k, p.dtype, a, stream);  // unsplit (A/B)
     case kFp8W4STS: {
       GemmArgs s = a;
       s.pers_grid = ((p.cus > 0 ? p.cus : device_cus()) / 8) * 8;
@@ -827,6 +832,8 @@ const char* kernel_name(int kernel) {
     case kMfmaW4STS: return "pdmb_w4s_tstore";
     case kF32_256sDirect: return "pdmb_f32_256s_direct";
     case kFp8W4Unfused: return "pdmb_fp8_w4_nt_unfused";
+    case kT128Unfused: return "pdmb_t128_nn_unfused";
+    case kFp8T128Unfused: return "pdmb_fp8_t128_nt_unfused";
     case kFp8W4Trace: return "pdmb_fp8_w4_nt_trace";
     default: return "auto";
   }

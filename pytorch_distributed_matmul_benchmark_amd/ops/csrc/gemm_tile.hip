@@ -272,9 +272,56 @@ __device__ __forceinline__ void ktile(const Ctx<C>& c, const char* smem, int t, 
   }
 }
 
+// The last K-tile of an unsplit tile with the epilogue folded in (as
+// gemm_fp8.hip ktile_w4_last): block row mi - 1 leaves through this wave's
+// own LDS buffer (past the stages, which tail DMAs may still be writing)
+// while block row mi's MFMAs run. MFMAs in block-row order (per accumulator
+// the same ks sequence as ktile: bitwise equal); no fragment reads, DMAs or
+// barrier. Block mi's MFMAs separate block mi - 1's last accumulator write
+// from its AGPR reads.
 template <int DT, class C>
+__device__ __forceinline__ void ktile_last(f32x4 (&acc)[C::MB][C::NB], const Frag (&Ac)[C::MB],
+                                           const Frag (&Bc)[C::NB], char* ebuf, char* Cb, long long ldc_b,
+                                           int row0, int col0, int M, int N, float alpha) {
+  auto store = [&](int i) {
+    unsigned all = ~0u;  // lane id formed here: the stores' addresses are not hoisted
+    asm volatile("" : "+s"(all));
+    const int eln = (int)__builtin_amdgcn_mbcnt_hi(all, __builtin_amdgcn_mbcnt_lo(all, 0u));
+    if constexpr (DT == kFP8)
+      store_block16<kBF16, false, true, C::NB>(ebuf, acc[i], alpha, Cb, ldc_b, row0 + i * 16, col0, M, N, eln);
+    else
+      store_block16<DT, false, false, C::NB>(ebuf, acc[i], 1.0f, Cb, ldc_b, row0 + i * 16, col0, M, N, eln);
+  };
+#pragma unroll
+  for (int mi = 0; mi < C::MB; ++mi) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ni = 0; ni < C::NB; ++ni) {
+        if constexpr (DT == kFP8) {
+          if (ks == 0) mfma_acc_f8(acc[mi][ni], Bc[ni].k, Ac[mi].k);
+        } else {
+          mfma_acc<DT>(acc[mi][ni], Bc[ni].k[ks], Ac[mi].k[ks]);
+        }
+      }
+    __builtin_amdgcn_sched_barrier(0);
+    if (mi >= 1) store(mi - 1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  store(C::MB - 1);
+}
+
+// FUSED: unsplit tiles with an even K-tile count store C during their last
+// K-tile (ktile_last; false: the A/B kernels kT128Unfused / kFp8T128Unfused).
+template <int DT, class C, bool FUSED = true>
 __global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
-  __shared__ __attribute__((aligned(1024))) char smem[C::NS * C::STAGE];
+  // T128x2 (2 workgroups / CU) keeps the separate epilogue: in its 128-register
+  // budget the fused last K-tile made hipcc shuffle fragment registers next
+  // to the inline-asm MFMAs (wrong results on the GPU).
+  constexpr bool kFused = FUSED && C::OCC == 1;
+  __shared__ __attribute__((aligned(1024))) char smem[C::NS * C::STAGE + (kFused ? 4 * epi_buf<C::NB>() : 0)];
   constexpr int MB = C::MB, NB = C::NB, NS = C::NS;
 
   int bz, tm, tn;
@@ -385,22 +432,35 @@ __global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
   }
   // Steady state: K-tile t computes from set (t & 1), reads t+1 into the
   // other set from stage (t+1) % NS, refills stage t % NS with tile t + NS.
+  // Fused (unsplit, nk even): the loop stops before K-tile nk-1, whose
+  // fragments it leaves in (A1, B1), and ktile_last runs it with the stores.
+  const bool split = a.splitk > 1;
+  const bool fuse = kFused && !split && (nk & 1) == 0;
+  const int nloop = fuse ? nk - 1 : nk;
   int t = 0;
-  for (; t + 1 < nk; t += 2) {
+  for (; t + 1 < nloop; t += 2) {
     ktile<DT, C>(c, smem, t, (uint32_t)((t % NS) * C::STAGE), (uint32_t)(((t + 1) % NS) * C::STAGE),
                  acc, A0, B0, A1, B1);
     ktile<DT, C>(c, smem, t + 1, (uint32_t)(((t + 1) % NS) * C::STAGE),
                  (uint32_t)(((t + 2) % NS) * C::STAGE), acc, A1, B1, A0, B0);
   }
-  if (t < nk)  // odd count: the last tile's "next" reads are clamped re-reads
-    ktile<DT, C>(c, smem, t, (uint32_t)((t % NS) * C::STAGE), (uint32_t)((t % NS) * C::STAGE), acc,
-                 A0, B0, A1, B1);
+  if (t < nloop)  // odd count: the next tile's reads (fused) or clamped re-reads (the last tile)
+    ktile<DT, C>(c, smem, t, (uint32_t)((t % NS) * C::STAGE),
+                 (uint32_t)(((fuse ? t + 1 : t) % NS) * C::STAGE), acc, A0, B0, A1, B1);
+  if constexpr (kFused) {
+    if (fuse) {
+      ktile_last<DT, C>(acc, A1, B1, smem + C::NS * C::STAGE + wu * epi_buf<NB>(),
+                        (char*)a.C + (long long)bz * a.sC * 2, (long long)a.ldc * 2,
+                        m0 + wr * (C::BM / 2), n0 + wc * (C::BN / 2), a.M, a.N, a.alpha);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail DMAs landed before the LDS is released
+      return;
+    }
+  }
   // Drain the tail DMAs and give the last MFMAs time to write their AGPRs
   // (asm MFMAs are invisible to hipcc's hazard recognizer).
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
 
   SplitSlots sl;
-  const bool split = a.splitk > 1;
   if (split && !splitk_meet<MB, NB, NT>(a, smem, ((long long)bz * a.tiles_m + tm) * a.tiles_n + tn,
                                         slice, acc, sl))
     return;
@@ -432,7 +492,7 @@ __global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
   }
 }
 
-template <class C>
+template <class C, bool FUSED = true>
 hipError_t launch(int dt, GemmArgs a, hipStream_t stream) {
   a.tiles_m = a.M / C::BM;
   a.tiles_n = a.N / C::BN;
@@ -452,12 +512,12 @@ hipError_t launch(int dt, GemmArgs a, hipStream_t stream) {
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
   const dim3 grid((unsigned)nblocks), block(NT);
   if (dt == kBF16) {
-    hipLaunchKernelGGL((gemm_tile_nn<kBF16, C>), grid, block, 0, stream, a);
+    hipLaunchKernelGGL((gemm_tile_nn<kBF16, C, FUSED>), grid, block, 0, stream, a);
   } else if (dt == kF16) {
-    hipLaunchKernelGGL((gemm_tile_nn<kF16, C>), grid, block, 0, stream, a);
+    hipLaunchKernelGGL((gemm_tile_nn<kF16, C, FUSED>), grid, block, 0, stream, a);
   } else {
     if constexpr (C::OCC == 1)  // fp8: T128, T256x128
-      hipLaunchKernelGGL((gemm_tile_nn<kFP8, C>), grid, block, 0, stream, a);
+      hipLaunchKernelGGL((gemm_tile_nn<kFP8, C, FUSED>), grid, block, 0, stream, a);
     else
       return hipErrorInvalidValue;
   }
@@ -497,8 +557,13 @@ bool gemm_tile_supported(int dt, int bm, const GemmArgs& a, size_t align_a, size
 
 // kernel: kT128 | kT128x2 | kT256x128 (bf16 / fp16), kFp8T128 | kFp8T256x128 (fp8)
 hipError_t gemm_tile_launch(int kernel, int dt, GemmArgs a, hipStream_t stream) {
-  if ((dt == kFP8) != (kernel == kFp8T128 || kernel == kFp8T256x128)) return hipErrorInvalidValue;
+  if ((dt == kFP8) != (kernel == kFp8T128 || kernel == kFp8T256x128 || kernel == kFp8T128Unfused))
+    return hipErrorInvalidValue;
   switch (kernel) {
+#ifdef PDMB_EXPERIMENTS
+    case kT128Unfused: return ktile::launch<ktile::CfgT128, false>(dt, a, stream);
+    case kFp8T128Unfused: return ktile::launch<ktile::CfgT128, false>(dt, a, stream);
+#endif
     case kFp8T128: return ktile::launch<ktile::CfgT128>(dt, a, stream);
     case kFp8T256x128: return ktile::launch<ktile::CfgT256x128>(dt, a, stream);
     case kT128: return ktile::launch<ktile::CfgT128>(dt, a, stream);

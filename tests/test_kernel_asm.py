@@ -131,26 +131,32 @@ def test_streaming_kernels_structure(tmp_path, src, pat, dts, zero_per_kt):
         assert len(re.findall(r"global_store_dwordx4", b)) == 32
 
 
+EPI4 = 4 * 16 * (4 * 32 + 8)  # the fused last K-tile's per-wave epilogue buffers (epi_buf<4>)
+
+
 @pytest.mark.parametrize("cfg,lds,waitn,mfma_per_kt,pieces", [
-    ("Li128ELi128ELi4ELi1E", 4 * 32768, 16, 32, 8),    # T128: 4-stage ring
-    ("Li256ELi128ELi3ELi1E", 3 * 49152, 12, 64, 12),   # T256x128: 3-stage ring
+    ("Li128ELi128ELi4ELi1E", 4 * 32768 + EPI4, 16, 32, 8),    # T128: 4-stage ring
+    ("Li256ELi128ELi3ELi1E", 3 * 49152 + EPI4, 12, 64, 12),   # T256x128: 3-stage ring
 ])
 def test_tile_family_pipelined(tmp_path, cfg, lds, waitn, mfma_per_kt, pieces):
     """gemm_tile.hip (1 workgroup / CU members): no spills, AGPR accumulators,
-    one vmcnt(P*(NS-2))-counted barrier per K-tile, one vmcnt(0) drain before the
-    split-K epilogue, prologue + 3 unrolled K-tiles of DMA pieces, sc1 slots."""
+    one vmcnt(P*(NS-2))-counted barrier per K-tile, vmcnt(0) only at the exits
+    (before the split-K / unfused epilogue and after the fused last K-tile), prologue
+    + 3 unrolled K-tiles of DMA pieces, sc1 slots."""
     ks = _kernels("gemm_tile.hip", tmp_path)
     for dt, mfma in (("ILi2E", "v_mfma_f32_16x16x32_bf16"), ("ILi1E", "v_mfma_f32_16x16x32_f16")):
-        name = [k for k in ks if "gemm_tile_nn" + dt in k and cfg in k]
+        name = [k for k in ks if "gemm_tile_nn" + dt in k and cfg in k and "Lb1E" in k]
         assert name, sorted(ks)
         k = ks[name[0]]
         b = k["body"]
         assert k["spill"] == 0 and k["lds"] == lds and k["vgpr"] <= 256
         assert re.search(r"v_mfma_f32_16x16x32_\w+ a\[", b)
         loop = b[:b.find("global_atomic")]
-        assert len(re.findall(r"s_waitcnt vmcnt\(0\)", loop)) == 1
+        assert len(re.findall(r"s_waitcnt vmcnt\(0\)", loop)) == 1  # the unfused / split-K drain
+        assert len(re.findall(r"s_waitcnt vmcnt\(0\)", b[b.rfind("v_mfma"):])) >= 1  # the fused exit's drain
         assert len(re.findall(rf"s_waitcnt vmcnt\({waitn}\) lgkmcnt\(0\)", b)) == 3
-        assert len(re.findall(mfma, b)) == 3 * mfma_per_kt  # 2 unrolled K-tiles + the odd tail
+        # 2 unrolled K-tiles + the odd tail + the fused last K-tile
+        assert len(re.findall(mfma, b)) == 4 * mfma_per_kt
         stages = lds // (lds // {16: 4, 12: 3}[waitn])
         assert len(re.findall(r"buffer_load_dwordx4 .* lds", b)) == (stages + 3) * pieces
         assert len(re.findall(r"buffer_store_dwordx4 .* sc1", b)) == mfma_per_kt // 2  # slots
@@ -164,5 +170,6 @@ def test_t128x2_two_workgroups_per_cu(tmp_path):
     name = [k for k in ks if "gemm_tile_nnILi2E" in k and "Li128ELi128ELi2ELi2E" in k]
     assert name, sorted(ks)
     k = ks[name[0]]
-    assert k["spill"] == 0 and k["lds"] == 2 * 32768 and k["vgpr"] <= 128
+    assert k["spill"] == 0 and k["lds"] == 2 * 32768
+    assert k["vgpr"] <= 128
     assert len(re.findall(r"s_waitcnt vmcnt\(0\) lgkmcnt\(0\)", k["body"])) == 4
