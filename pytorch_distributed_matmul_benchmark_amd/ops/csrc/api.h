@@ -61,6 +61,7 @@ enum ExperimentKernel : int {
   kFp8W4Unfused = 47,    // kFp8W4 with the epilogue after (not inside) the last K-tile
   kT128Unfused = 48,     // kT128 (bf16 / fp16) with the epilogue after the last K-tile
   kFp8T128Unfused = 49,  // kFp8T128 with the epilogue after the last K-tile
+  kMfmaW4Unfused = 50,   // kMfmaW4 (bf16) with the epilogue after the last K-tile
 };
 
 // True iff this library was built with the experiment kernels.

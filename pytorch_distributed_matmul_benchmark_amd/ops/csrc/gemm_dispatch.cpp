@@ -86,7 +86,7 @@ static bool is_experiment(int k) {
     case kMfmaW4Pers: case kMfmaW4PersTrace: case kMfmaW4STrace: case kMfmaW4SRot: case kMfmaW4SRotTrace:
     case kFp8W4Tall: case kFp8W4Wide: case kFp8W4Scaled: case kFp8W4Trace: case kMfmaW4Trace:
     case kFp8W4TS: case kFp8W4STS: case kMfmaW4STS: case kF32_256sDirect: case kFp8W4Unfused:
-    case kT128Unfused: case kFp8T128Unfused:
+    case kT128Unfused: case kFp8T128Unfused: case kMfmaW4Unfused:
       return true;
     default:
       return false;
@@ -162,6 +162,7 @@ int resolve_kernel(const Problem& p, int kernel) {
 #ifdef PDMB_EXPERIMENTS
     case kF32_256: case kF32NoDma: case kF32_256sDirect: return f32fast ? kernel : -1;
     case kT128Unfused: return t128 ? kernel : -1;
+    case kMfmaW4Unfused: return (p.dtype == kBF16 && w4) ? kernel : -1;
     case kMfma256: case kMfma256b: case kMfma256c: return fast ? kernel : -1;
     case kMfma256X1: case kMfma256X2: case kMfma256X4: case kMfma256Stamp:
       return (fast && p.dtype == kBF16) ? kernel : -1;
@@ -699,6 +700,7 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kFp8W4Unfused: return gemm_fp8_launch(a, 18, stream);
     case kT128Unfused:
     case kFp8T128Unfused: return gemm_tile_launch(k, p.dtype, a, stream);  // unsplit (A/B)
+    case kMfmaW4Unfused: return gemm_w4_launch(p.dtype, a, stream, 12);   // unsplit (A/B)
     case kFp8W4STS: {
       GemmArgs s = a;
       s.pers_grid = ((p.cus > 0 ? p.cus : device_cus()) / 8) * 8;
@@ -834,6 +836,7 @@ const char* kernel_name(int kernel) {
     case kFp8W4Unfused: return "pdmb_fp8_w4_nt_unfused";
     case kT128Unfused: return "pdmb_t128_nn_unfused";
     case kFp8T128Unfused: return "pdmb_fp8_t128_nt_unfused";
+    case kMfmaW4Unfused: return "pdmb_w4_nn_unfused";
     case kFp8W4Trace: return "pdmb_fp8_w4_nt_trace";
     default: return "auto";
   }

@@ -216,6 +216,37 @@ __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, f32
   }
 }
 
+// The last K-tile of an unsplit tile with the epilogue folded in (as
+// gemm_fp8.hip ktile_w4_last): block row mi - 1 leaves through this wave's
+// LDS buffer past the two stages while block row mi's 16 MFMAs run (same
+// per-accumulator MFMA order as ktile: bitwise equal). No fragment reads,
+// DMAs or barrier.
+template <int DT>
+__device__ __forceinline__ void ktile_last(f32x4 (&acc)[8][8], const Frag (&A)[8], const Frag& A7c,
+                                           const Frag (&Bc)[8], char* ebuf, char* Cb, long long ldc_b,
+                                           int row0, int col0, int M, int N) {
+  auto store = [&](int i) {
+    unsigned all = ~0u;  // lane id formed here: the stores' addresses are not hoisted
+    asm volatile("" : "+s"(all));
+    const int eln = (int)__builtin_amdgcn_mbcnt_hi(all, __builtin_amdgcn_mbcnt_lo(all, 0u));
+    store_block16<DT, false, false>(ebuf, acc[i], 1.0f, Cb, ldc_b, row0 + i * 16, col0, M, N, eln);
+  };
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+#pragma unroll
+    for (int gap = 0; gap < 16; ++gap) {
+      const int ks = gap >> 3, ni = gap & 7;
+      mfma_acc<DT>(acc[mi][ni], Bc[ni].k[ks], mi == 7 ? A7c.k[ks] : A[mi].k[ks]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (mi >= 1) store(mi - 1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  store(7);
+}
+
 // SUB: XCD sub-block shape (map_tile): 0 = 4 x 8 (default), 1 = 8 x 4
 // (kMfmaW4Tall), 2 = 2 x 16 (kMfmaW4Wide); 1 and 2 are A/B experiments.
 // IL: B half interleave in columns (64 default; 32 = kMfmaW4Il32, A/B only).
@@ -224,7 +255,10 @@ __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, f32
 // kernel; no split-K): thread 0 takes the next ticket of its XCD's queue
 // `qpre` as the tile starts and returns it; it is first read after the
 // K-loop's vmcnt(0), so the atomic's latency hides behind the tile.
-template <int DT, int SUB, int IL, int TRACE, bool PERS>
+// FUSED (needs 4 kEpiBuf of LDS past the stages): an unsplit tile with an
+// even K-tile count stores C during its last K-tile (ktile_last); its
+// fragments are then in (A7b, B1) — one register set, as in gemm_fp8.hip.
+template <int DT, int SUB, int IL, int TRACE, bool PERS, bool FUSED = false>
 __device__ __forceinline__ unsigned w4_tile(const GemmArgs& a, char* smem, int vb, unsigned* qpre) {
   TileTrace tr;
   if constexpr (TRACE) tr.t[0] = tile_clock();
@@ -342,12 +376,24 @@ __device__ __forceinline__ unsigned w4_tile(const GemmArgs& a, char* smem, int v
 #pragma unroll
     for (int h = 8; h < 16; ++h) issue_piece<IL>(c, rb2, 0, t2, h);
   }
+  const bool split = !PERS && a.splitk > 1;
+  constexpr bool kFuse = FUSED && !PERS && TRACE == 0;
+  const bool fuse = kFuse && !split && (nk & 1) == 0;
+  const int nloop = fuse ? nk - 1 : nk;
   int t = 0;
-  for (; t + 1 < nk; t += 2) {  // branch-free body: B0/B1 and A7a/A7b swap roles every K-tile
+  for (; t + 1 < nloop; t += 2) {  // branch-free body: B0/B1 and A7a/A7b swap roles every K-tile
     ktile<DT, IL, 0>(c, smem, t, acc, A, A7a, A7b, B0, B1);
     ktile<DT, IL, STAGE>(c, smem, t + 1, acc, A, A7b, A7a, B1, B0);
   }
-  if (t < nk) ktile<DT, IL, 0>(c, smem, t, acc, A, A7a, A7b, B0, B1);  // odd count
+  if (t < nloop) ktile<DT, IL, 0>(c, smem, t, acc, A, A7a, A7b, B0, B1);  // odd count
+  if constexpr (kFuse) {
+    if (fuse) {
+      ktile_last<DT>(acc, A, A7b, B1, smem + 2 * STAGE + wu * kEpiBuf, (char*)a.C + (long long)bz * a.sC * 2,
+                     (long long)a.ldc * 2, m0 + wr * 128, n0 + wc * 128, a.M, a.N);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail DMAs landed before the LDS is released
+      return pre;
+    }
+  }
   // Drain the tail DMAs and give the last MFMAs time to write their AGPRs
   // (asm MFMAs are invisible to hipcc's hazard recognizer).
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
@@ -357,7 +403,6 @@ __device__ __forceinline__ unsigned w4_tile(const GemmArgs& a, char* smem, int v
   // other slices' fp32 slots block row by block row while storing, so no
   // more than 2 x 8 fragments are live in VGPRs (splitk.h).
   SplitSlots sl;
-  const bool split = !PERS && a.splitk > 1;
   if (split && !splitk_meet<8, 8, NT>(a, smem, ((long long)bz * a.tiles_m + tm) * a.tiles_n + tn,
                                       slice, acc, sl))
     return pre;
@@ -389,10 +434,12 @@ __device__ __forceinline__ unsigned w4_tile(const GemmArgs& a, char* smem, int v
   return pre;
 }
 
-template <int DT, int SUB = 0, int IL = 64, int TRACE = 0>
+// FUSED: see w4_tile (false: the A/B kernel kMfmaW4Unfused).
+template <int DT, int SUB = 0, int IL = 64, int TRACE = 0, bool FUSED = true>
 __global__ void __launch_bounds__(NT, 1) gemm_w4_nn(GemmArgs a) {
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
-  (void)w4_tile<DT, SUB, IL, TRACE, false>(a, smem, blockIdx.x, nullptr);
+  constexpr bool kFused = FUSED && TRACE == 0;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + (kFused ? 4 * kEpiBuf : 0)];
+  (void)w4_tile<DT, SUB, IL, TRACE, false, kFused>(a, smem, blockIdx.x, nullptr);
 }
 
 // Persistent W4: one workgroup per CU, tiles from per-XCD queues. The tile
@@ -806,6 +853,10 @@ hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
   }
   if (dt == kBF16 && sub == 4) {
     hipLaunchKernelGGL((kw4::gemm_w4_nn<kBF16, 0, 64, 1>), grid, block, 0, stream, a);
+    return hipGetLastError();
+  }
+  if (dt == kBF16 && sub == 12) {  // kMfmaW4Unfused: the epilogue after the last K-tile
+    hipLaunchKernelGGL((kw4::gemm_w4_nn<kBF16, 0, 64, 0, false>), grid, block, 0, stream, a);
     return hipGetLastError();
   }
   if (dt == kBF16 && sub == 6) {  // persistent + tile timeline

@@ -76,7 +76,8 @@ def test_bf16_two_quadrant_schedule(tmp_path):
 
 
 def test_w4_kernel_agpr_accumulators_and_counted_waits(tmp_path):
-    """gemm_w4.hip: 256 AGPR accumulators, no spills, 128 KiB LDS (1 workgroup/CU),
+    """gemm_w4.hip: 256 AGPR accumulators, no spills, 128 KiB LDS + the fused last
+    K-tile's epilogue buffers (1 workgroup/CU),
     counted vmcnt(16) waits at the two barriers of each K-tile and one vmcnt(0) drain."""
     ks = _kernels("gemm_w4.hip", tmp_path)
     for dt, mfma in (("ILi2E", "v_mfma_f32_16x16x32_bf16"), ("ILi1E", "v_mfma_f32_16x16x32_f16")):
@@ -84,15 +85,15 @@ def test_w4_kernel_agpr_accumulators_and_counted_waits(tmp_path):
         assert name, sorted(ks)
         k = ks[name[0]]
         b = k["body"]
-        assert k["spill"] == 0 and k["lds"] == 2 * 65536
+        assert k["spill"] == 0 and k["lds"] == 2 * 65536 + 4 * 4224  # + fused epilogue buffers
         assert re.search(r"v_mfma_f32_16x16x32_\w+ a\[", b)  # accumulators live in AGPRs
         assert k["vgpr"] <= 256
         loop = b[:b.find("global_atomic")]  # K-loop + drain; the split-K epilogue follows
         assert "global_atomic" in b  # the fused split-K meeting point is compiled in
         assert len(re.findall(r"s_waitcnt vmcnt\(0\)", loop)) == 1
         assert len(re.findall(r"s_waitcnt vmcnt\(16\) lgkmcnt\(0\)", b)) >= 4
-        # loop body: 2 K-tiles x 8 blocks x 16 MFMAs, plus one odd tail K-tile
-        assert len(re.findall(mfma, b)) == 3 * 128
+        # loop body: 2 K-tiles x 8 blocks x 16 MFMAs, one odd tail K-tile, the fused last K-tile
+        assert len(re.findall(mfma, b)) == 4 * 128
         assert len(re.findall(r"buffer_load_dwordx4 .* lds", b)) >= 3 * 16
 
 
