@@ -55,7 +55,7 @@ struct Opts {
   int gpus = 1;
   std::vector<int> sizes{4096, 8192, 16384};
   int iters = 50, warmup = 10;
-  int dtype = 2;  // pdmb::DType: 0 f32, 1 f16, 2 bf16
+  int dtype = 2;  // pdmb::DType: 0 f32, 1 f16, 2 bf16, 3 fp8 e4m3 (column-major B, bf16 C)
   Mode mode = kIndependent;
   int batch = 4, chunks = 4, kernel = 0;
   bool overlap = false, check = false;
@@ -69,14 +69,32 @@ const char* mode_name(Mode m) {
          : m == kMatrixParallel ? "matrix_parallel"
                                 : "ring_parallel";
 }
-const char* dtype_name(int d) { return d == 0 ? "float32" : d == 1 ? "float16" : "bfloat16"; }
-size_t esize(int d) { return d == 0 ? 4 : 2; }
-ncclDataType_t nccl_type(int d) { return d == 0 ? ncclFloat32 : d == 1 ? ncclFloat16 : ncclBfloat16; }
+const char* dtype_name(int d) {
+  return d == 0 ? "float32" : d == 1 ? "float16" : d == 2 ? "bfloat16" : "float8_e4m3fn";
+}
+// Operand and output element types: fp8 (3) multiplies e4m3 operands into a
+// bf16 C (the library's kFP8 contract; B column-major, i.e. stored as Bt).
+int out_dtype(int d) { return d == 3 ? 2 : d; }
+size_t esize(int d) { return d == 0 ? 4 : d == 3 ? 1 : 2; }
+size_t oesize(int d) { return esize(out_dtype(d)); }
+ncclDataType_t nccl_type(int d) {
+  return d == 0 ? ncclFloat32 : d == 1 ? ncclFloat16 : d == 2 ? ncclBfloat16 : ncclUint8;
+}
+ncclDataType_t nccl_out_type(int d) { return nccl_type(out_dtype(d)); }
 int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 // ---- device helpers -------------------------------------------------------
+// OCP e4m3fn (gfx950's fp8): bias 7, no infinities, S.1111.111 = NaN.
+__host__ __device__ __forceinline__ float e4m3_to_float(unsigned char b) {
+  const int e = (b >> 3) & 15, m = b & 7;
+  const float mag = e == 0 ? (float)m * 0.001953125f /* 2^-9 */
+                           : (1.0f + (float)m * 0.125f) * (float)(1 << e) * 0.0078125f /* 2^-7 */;
+  return (b & 0x80) ? -mag : mag;
+}
+
 __device__ __forceinline__ float to_float(const void* p, long long i, int dt) {
   if (dt == 0) return ((const float*)p)[i];
+  if (dt == 3) return e4m3_to_float(((const unsigned char*)p)[i]);
   const unsigned short v = ((const unsigned short*)p)[i];
   if (dt == 2) return __uint_as_float(((unsigned int)v) << 16);
   return (float)__builtin_bit_cast(_Float16, v);
@@ -92,6 +110,11 @@ __global__ void fill_uniform(void* p, long long n, int dt, unsigned long long se
     x *= 0xBF58476D1CE4E5B9ull;
     x ^= x >> 29;
     const float u = (float)(x >> 40) * (1.0f / 8388608.0f) - 1.0f;  // 24 random bits
+    if (dt == 3) {  // random e4m3 bits: sign, exponent 1..8 (|v| in [2^-6, 3.75]), mantissa
+      const unsigned e = 1u + (unsigned)((x >> 40) & 7u), m = (unsigned)(x >> 44) & 7u;
+      ((unsigned char*)p)[i] = (unsigned char)(((x >> 63) << 7) | (e << 3) | m);
+      continue;
+    }
     if (dt == 0) {
       ((float*)p)[i] = u;
     } else if (dt == 2) {
@@ -111,8 +134,10 @@ __global__ void ref_rows(const void* A, const void* B, const int* rows, int R, i
   const int r = (int)(idx / N), j = (int)(idx % N);
   double s = 0.0;
   const long long arow = (long long)rows[r] * lda;
-  for (int k = 0; k < K; ++k)
-    s += (double)to_float(A, arow + k, dt) * (double)to_float(B, (long long)k * ldb + j, dt);
+  for (int k = 0; k < K; ++k) {
+    const long long bi = dt == 3 ? (long long)j * ldb + k : (long long)k * ldb + j;  // fp8: Bt [N,K]
+    s += (double)to_float(A, arow + k, dt) * (double)to_float(B, bi, dt);
+  }
   out[idx] = s;
 }
 
@@ -271,7 +296,7 @@ void check_rows(int dt, const void* A, const void* B, const void* C, int M, int 
   hipLaunchKernelGGL(ref_rows, dim3(ceil_div(tot, 256)), dim3(256), 0, s, A, B, drows.as<int>(), R,
                      K, N, lda, ldb, dt, dref.as<double>());
   hipLaunchKernelGGL(take_rows, dim3(ceil_div(tot, 256)), dim3(256), 0, s, C, drows.as<int>(), R, N,
-                     ldc, dt, dgot.as<double>());
+                     ldc, out_dtype(dt), dgot.as<double>());
   HIP_OK(hipGetLastError());
   ref.resize(tot);
   got.resize(tot);
@@ -301,7 +326,7 @@ std::vector<std::pair<int, int>> row_chunks(int m, int chunks) {
 void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Result& res) {
   HIP_OK(hipSetDevice(rank));
   const int ws = o.gpus, dt = o.dtype;
-  const size_t es = esize(dt);
+  const size_t es = esize(dt), oes = oesize(dt);  // operand / output element bytes
   hipStream_t st, cs;
   int lo = 0, hi = 0;
   HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -320,7 +345,7 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
   const bool dist = comm != nullptr;
 
   if (o.mode == kIndependent) {
-    Buf A((size_t)n * n * es), B((size_t)n * n * es), C((size_t)n * n * es);
+    Buf A((size_t)n * n * es), B((size_t)n * n * es), C((size_t)n * n * oes);
     fill(A.p, (long long)n * n, dt, 2 * rank + 1, st);
     fill(B.p, (long long)n * n, dt, 2 * rank + 2, st);
     const pdmb::Problem p = problem(dt, A.p, B.p, C.p, n, n, n, n, n, n);
@@ -342,7 +367,7 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     res.local_batch = lb;
     res.global_batch = gb;
     const size_t mat = (size_t)n * n;
-    Buf A(lb * mat * es), B(lb * mat * es), C(lb * mat * es);
+    Buf A(lb * mat * es), B(lb * mat * es), C(lb * mat * oes);
     fill(A.p, (long long)(lb * mat), dt, 2 * rank + 1, st);
     fill(B.p, (long long)(lb * mat), dt, 2 * rank + 2, st);
     const pdmb::Problem p = problem(dt, A.p, B.p, C.p, n, n, n, n, n, n, lb, mat, mat, mat);
@@ -362,19 +387,19 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     auto serial_iter = [&](hipEvent_t em) {
       gemm(p, o.kernel, st);
       if (em) HIP_OK(hipEventRecord(em, st));
-      if (dist) NCCL_OK(ncclAllReduce(C.p, C.p, lb * mat, nccl_type(dt), ncclSum, comm, st));
+      if (dist) NCCL_OK(ncclAllReduce(C.p, C.p, lb * mat, nccl_out_type(dt), ncclSum, comm, st));
     };
     auto overlap_iter = [&]() {
       for (size_t u = 0; u < units.size(); ++u) {
         const Unit& un = units[u];
         char* a = (char*)A.p + (un.b * mat + (size_t)un.r0 * n) * es;
         char* b = (char*)B.p + un.b * mat * es;
-        char* c = (char*)C.p + (un.b * mat + (size_t)un.r0 * n) * es;
+        char* c = (char*)C.p + (un.b * mat + (size_t)un.r0 * n) * oes;
         if (used[u]) HIP_OK(hipStreamWaitEvent(st, done[u], 0));
         gemm(problem(dt, a, b, c, un.r1 - un.r0, n, n, n, n, n), o.kernel, st);
         HIP_OK(hipEventRecord(ready[u], st));
         HIP_OK(hipStreamWaitEvent(cs, ready[u], 0));
-        NCCL_OK(ncclAllReduce(c, c, (size_t)(un.r1 - un.r0) * n, nccl_type(dt), ncclSum, comm, cs));
+        NCCL_OK(ncclAllReduce(c, c, (size_t)(un.r1 - un.r0) * n, nccl_out_type(dt), ncclSum, comm, cs));
         HIP_OK(hipEventRecord(done[u], cs));
         used[u] = true;
       }
@@ -427,6 +452,7 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     if (o.check)  // C[0] = sum over ranks of A_r[0] @ B_r[0]: partial refs are summed on the host
       check_rows(dt, A.p, B.p, C.p, n, n, n, n, n, n, st, res.ref, res.got);
   } else if (o.mode == kRingParallel) {
+    if (dt == 3) throw std::runtime_error("ring_parallel: fp8 is not supported by the native executor");
     // All-gather-GEMM over BOTH ring directions (models/ring_parallel.py): A
     // row-sharded in blocks of rp rows, B column-sharded. Each block is cut
     // into a top (ht rows, 256-aligned) and a bottom half; tops travel r -> r+1,
@@ -528,14 +554,18 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     const int c0 = std::min(rank * shard, n), width = std::max(0, std::min(n, c0 + shard) - c0);
     res.shard = shard;
     Buf A((size_t)n * n * es), Bg((size_t)n * n * es), Bl((size_t)n * shard * es);
-    Buf Cl((size_t)n * shard * es), G((size_t)ws * n * shard * es);
+    Buf Cl((size_t)n * shard * oes), G((size_t)ws * n * shard * oes);
     fill(A.p, (long long)n * n, dt, 1000, st);
     fill(Bg.p, (long long)n * n, dt, 1001, st);
     HIP_OK(hipMemsetAsync(Bl.p, 0, Bl.bytes, st));
-    if (width)
+    // fp8: B is column-major (Bt [N,K]), so a column shard is a row range of Bt
+    const int ldb = dt == 3 ? n : shard;
+    if (width && dt == 3)
+      HIP_OK(hipMemcpyAsync(Bl.p, (char*)Bg.p + (size_t)c0 * n, (size_t)width * n, hipMemcpyDeviceToDevice, st));
+    else if (width)
       HIP_OK(hipMemcpy2DAsync(Bl.p, shard * es, (char*)Bg.p + c0 * es, n * es, width * es, n,
                               hipMemcpyDeviceToDevice, st));
-    const pdmb::Problem p = problem(dt, A.p, Bl.p, Cl.p, n, shard, n, n, shard, shard);
+    const pdmb::Problem p = problem(dt, A.p, Bl.p, Cl.p, n, shard, n, n, ldb, shard);
     res.kernel = pdmb::kernel_name(pdmb::resolve_kernel(p, o.kernel));
     const int ch = o.overlap ? effective_chunks(n, shard, o.chunks, dt) : 1;
     res.chunks = ch;
@@ -545,7 +575,7 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     size_t off = 0;
     for (auto rc : rcs) {
       gb.push_back((char*)G.p + off);
-      off += (size_t)ws * (rc.second - rc.first) * shard * es;
+      off += (size_t)ws * (rc.second - rc.first) * shard * oes;
     }
     std::vector<hipEvent_t> ready, done;
     for (size_t j = 0; j < rcs.size(); ++j) {
@@ -560,16 +590,16 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     // transfer has its own xGMI link; no forwarding hops).
     auto allgather = [&](const void* send, char* recv, size_t count, hipStream_t s) {
       if (!o.direct) {
-        NCCL_OK(ncclAllGather(send, recv, count, nccl_type(dt), comm, s));
+        NCCL_OK(ncclAllGather(send, recv, count, nccl_out_type(dt), comm, s));
         return;
       }
-      const size_t bytes = count * es;
+      const size_t bytes = count * oes;
       HIP_OK(hipMemcpyAsync(recv + (size_t)rank * bytes, send, bytes, hipMemcpyDeviceToDevice, s));
       NCCL_OK(ncclGroupStart());
       for (int d = 1; d < ws; ++d) {
         const int to = (rank + d) % ws, from = (rank - d + ws) % ws;
-        NCCL_OK(ncclSend(send, count, nccl_type(dt), to, comm, s));
-        NCCL_OK(ncclRecv(recv + (size_t)from * bytes, count, nccl_type(dt), from, comm, s));
+        NCCL_OK(ncclSend(send, count, nccl_out_type(dt), to, comm, s));
+        NCCL_OK(ncclRecv(recv + (size_t)from * bytes, count, nccl_out_type(dt), from, comm, s));
       }
       NCCL_OK(ncclGroupEnd());
     };
@@ -583,9 +613,9 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
       for (size_t j = 0; j < rcs.size(); ++j) {
         const int r0 = rcs[j].first, r1 = rcs[j].second;
         char* a = (char*)A.p + (size_t)r0 * n * es;
-        char* c = (char*)Cl.p + (size_t)r0 * shard * es;
+        char* c = (char*)Cl.p + (size_t)r0 * shard * oes;
         if (used[j]) HIP_OK(hipStreamWaitEvent(st, done[j], 0));
-        gemm(problem(dt, a, Bl.p, c, r1 - r0, shard, n, n, shard, shard), o.kernel, st);
+        gemm(problem(dt, a, Bl.p, c, r1 - r0, shard, n, n, ldb, shard), o.kernel, st);
         HIP_OK(hipEventRecord(ready[j], st));
         HIP_OK(hipStreamWaitEvent(cs, ready[j], 0));
         allgather(c, gb[j], (size_t)(r1 - r0) * shard, cs);
@@ -629,7 +659,7 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
       // gathered rows of EVERY shard as seen on this rank go to `got`
       // ([ws][rows][shard] order); the host matches got(0)[r] with ref(r).
       std::vector<double> own;
-      check_rows(dt, A.p, Bl.p, Cl.p, n, shard, n, n, shard, shard, st, res.ref, own);
+      check_rows(dt, A.p, Bl.p, Cl.p, n, shard, n, n, ldb, shard, st, res.ref, own);
       const std::vector<int> rows = sample_rows(n, 32);
       std::vector<unsigned short> h16;
       std::vector<float> h32;
@@ -639,8 +669,8 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
           size_t j = 0;
           while (j + 1 < rcs.size() && row >= rcs[j].second) ++j;
           const int r0 = rcs[j].first, rows_j = rcs[j].second - r0;
-          const char* base = o.overlap ? gb[j] + ((size_t)r * rows_j + (row - r0)) * shard * es
-                                       : (char*)G.p + ((size_t)r * n + row) * shard * es;
+          const char* base = o.overlap ? gb[j] + ((size_t)r * rows_j + (row - r0)) * shard * oes
+                                       : (char*)G.p + ((size_t)r * n + row) * shard * oes;
           if (dt == 0) {
             h32.resize(shard);
             HIP_OK(hipMemcpy(h32.data(), base, shard * 4, hipMemcpyDeviceToHost));
@@ -650,7 +680,7 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
             HIP_OK(hipMemcpy(h16.data(), base, shard * 2, hipMemcpyDeviceToHost));
             for (unsigned short v : h16) {
               float f;
-              if (dt == 2) {
+              if (out_dtype(dt) == 2) {
                 unsigned int u = (unsigned int)v << 16;
                 std::memcpy(&f, &u, 4);
               } else {
@@ -679,7 +709,7 @@ double norm_relerr(const std::vector<double>& got, const std::vector<double>& re
 void usage() {
   std::printf(
       "pdmb_bench [--gpus N] [--sizes N ...] [--iterations I] [--warmup W]\n"
-      "           [--dtype bfloat16|float16|float32] [--mode independent|batch_parallel|matrix_parallel|ring_parallel]\n"
+      "           [--dtype bfloat16|float16|float32|float8_e4m3fn] [--mode independent|batch_parallel|matrix_parallel|ring_parallel]\n"
       "           [--batch B] [--overlap] [--chunks C] [--allgather rccl|direct] [--kernel ID]\n"
       "           [--check] [--json FILE]\n");
 }
@@ -704,7 +734,7 @@ Opts parse(int argc, char** argv) {
     else if (a == "--json") o.json = next();
     else if (a == "--dtype") {
       const std::string d = next();
-      o.dtype = d == "float32" ? 0 : d == "float16" ? 1 : d == "bfloat16" ? 2 : -1;
+      o.dtype = d == "float32" ? 0 : d == "float16" ? 1 : d == "bfloat16" ? 2 : d == "float8_e4m3fn" ? 3 : -1;
       if (o.dtype < 0) throw std::runtime_error("bad --dtype " + d);
     } else if (a == "--mode") {
       const std::string m = next();
@@ -827,7 +857,7 @@ int main(int argc, char** argv) {
       } else {
         for (auto& r : res) relerr = std::max(relerr, norm_relerr(r.got, r.ref));
       }
-      const double tol = o.dtype == 0 ? 1e-5 : o.dtype == 1 ? 2e-3 : 1e-2;
+      const double tol = o.dtype == 0 ? 1e-5 : o.dtype == 1 ? 2e-3 : 1e-2;  // fp8: bf16 C
       const bool ok = relerr < tol;
       failures += !ok;
       std::printf("  - Check: max rel. error %.2e (%s)\n", relerr, ok ? "PASS" : "FAIL");
