@@ -452,7 +452,6 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     if (o.check)  // C[0] = sum over ranks of A_r[0] @ B_r[0]: partial refs are summed on the host
       check_rows(dt, A.p, B.p, C.p, n, n, n, n, n, n, st, res.ref, res.got);
   } else if (o.mode == kRingParallel) {
-    if (dt == 3) throw std::runtime_error("ring_parallel: fp8 is not supported by the native executor");
     // All-gather-GEMM over BOTH ring directions (models/ring_parallel.py): A
     // row-sharded in blocks of rp rows, B column-sharded. Each block is cut
     // into a top (ht rows, 256-aligned) and a bottom half; tops travel r -> r+1,
@@ -468,12 +467,15 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     res.shard = shard;
     const size_t blk = (size_t)rp * n, blt = (size_t)ht * n, blb = (size_t)hb * n;
     Buf Ag((size_t)n * n * es), Bg((size_t)n * n * es), Bl((size_t)n * shard * es);
-    Buf Cl((size_t)n * shard * es), Al(blk * es), Rt0(blt * es), Rt1(blt * es), Rb0(blb * es),
+    Buf Cl((size_t)n * shard * oes), Al(blk * es), Rt0(blt * es), Rt1(blt * es), Rb0(blb * es),
         Rb1(blb * es);
     fill(Ag.p, (long long)n * n, dt, 1000, st);
     fill(Bg.p, (long long)n * n, dt, 1001, st);
     HIP_OK(hipMemsetAsync(Bl.p, 0, Bl.bytes, st));
-    if (width)
+    const int ldb = dt == 3 ? n : shard;  // fp8: B column-major, its column shard a row range of Bt
+    if (width && dt == 3)
+      HIP_OK(hipMemcpyAsync(Bl.p, (char*)Bg.p + (size_t)c0 * n, (size_t)width * n, hipMemcpyDeviceToDevice, st));
+    else if (width)
       HIP_OK(hipMemcpy2DAsync(Bl.p, shard * es, (char*)Bg.p + c0 * es, n * es, width * es, n,
                               hipMemcpyDeviceToDevice, st));
     HIP_OK(hipMemsetAsync(Al.p, 0, Al.bytes, st));
@@ -481,7 +483,7 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
       HIP_OK(hipMemcpyAsync(Al.p, (char*)Ag.p + (size_t)rank * rp * n * es,
                             (size_t)rows_of(rank) * n * es, hipMemcpyDeviceToDevice, st));
     res.kernel = pdmb::kernel_name(
-        pdmb::resolve_kernel(problem(dt, Al.p, Bl.p, Cl.p, ht, shard, n, n, shard, shard), o.kernel));
+        pdmb::resolve_kernel(problem(dt, Al.p, Bl.p, Cl.p, ht, shard, n, n, ldb, shard), o.kernel));
     char* Rt[2] = {(char*)Rt0.p, (char*)Rt1.p};
     char* Rb[2] = {(char*)Rb0.p, (char*)Rb1.p};
     std::vector<hipEvent_t> gdone, rdone;
@@ -492,8 +494,8 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     auto part_gemm = [&](const char* a, int j, int r0, int r1) {
       r1 = std::min(r1, rows_of(j));
       if (r1 > r0)
-        gemm(problem(dt, a, Bl.p, (char*)Cl.p + ((size_t)j * rp + r0) * shard * es, r1 - r0, shard,
-                     n, n, shard, shard),
+        gemm(problem(dt, a, Bl.p, (char*)Cl.p + ((size_t)j * rp + r0) * shard * oes, r1 - r0, shard,
+                     n, n, ldb, shard),
              o.kernel, st);
     };
     auto block_gemm = [&](const char* a, int j) { part_gemm(a, j, 0, rp); };
@@ -548,7 +550,7 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     res.flops_local = 2.0 * n * (double)shard * n;
     res.flops_total = flop;
     // Cl is C[:, S_r] exactly (blocks are contiguous, unpadded): sampled rows vs A @ B_local.
-    if (o.check) check_rows(dt, Ag.p, Bl.p, Cl.p, n, shard, n, n, shard, shard, st, res.ref, res.got);
+    if (o.check) check_rows(dt, Ag.p, Bl.p, Cl.p, n, shard, n, n, ldb, shard, st, res.ref, res.got);
   } else {  // matrix_parallel: replicated A, padded column shard of one global B
     const int shard = ceil_div(ceil_div(n, ws), 8) * 8;
     const int c0 = std::min(rank * shard, n), width = std::max(0, std::min(n, c0 + shard) - c0);
