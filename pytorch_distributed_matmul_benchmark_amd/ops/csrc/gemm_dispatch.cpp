@@ -255,9 +255,10 @@ static int device_cus() {
 // sequence; there, and on CU-masked streams, the dispatch-balanced W4 runs.
 // Measured (profiles/r2_w4s_ab.jsonl): +3.1 % at 16384^2 x 2048, +2.8 % at
 // K = 4096, +2.2 % on the 16384 x 2048 x 16384 ws=8 shard, +0.1 % at 16k.
-static bool w4s_fits(const Problem& p) {
+static bool w4s_fits(const Problem& p) {  // interior tiles only (its epilogue is unmasked)
   const int nk = p.K / 64;
-  return (p.dtype == kBF16 || p.dtype == kF16) && nk % 2 == 0 && nk >= 6 && device_cus() % 8 == 0;
+  return (p.dtype == kBF16 || p.dtype == kF16) && p.M % 256 == 0 && p.N % 256 == 0 && nk % 2 == 0 &&
+         nk >= 6 && device_cus() % 8 == 0;
 }
 static bool w4s_auto(const Problem& p) {
   return p.cus == 0 && w4s_fits(p) && tiles_of(p, kMfmaW4) >= 2LL * device_cus();
@@ -517,9 +518,13 @@ static bool wants_padding(const Problem& p, int kernel) {
 }
 
 // The zero-padded problem `gemm_padded` runs (operands in the workspace).
+// direct_c: only K is padded (N already on its granule) and the caller's C is
+// aligned, so the kernel writes C in place — no padded C, no unpad copy
+// (for 8192^2 x 1000 bf16 that copy moved 256 MB).
 struct Padded {
   Problem q;
   size_t a_bytes, b_bytes, c_bytes, a_el, b_el, c_el;
+  bool direct_c;
 };
 
 static Padded padded_problem(const Problem& p, char* w) {
@@ -530,9 +535,11 @@ static Padded padded_problem(const Problem& p, char* w) {
   d.a_el = (size_t)p.M * Kp;
   d.b_el = (size_t)Kp * Np;
   d.c_el = (size_t)p.M * Np;
+  d.direct_c = Np == p.N && (uintptr_t)p.C % 16 == 0 && p.ldc % 8 == 0 && p.ldc >= p.N &&
+               (batch == 1 || p.sC % 8 == 0);
   d.a_bytes = round_up(d.a_el * es * batch, 256);
   d.b_bytes = round_up(d.b_el * es * batch, 256);
-  d.c_bytes = round_up(d.c_el * es * batch, 256);
+  d.c_bytes = d.direct_c ? 0 : round_up(d.c_el * es * batch, 256);
   Problem& q = d.q;
   q = p;
   q.A = w;
@@ -549,6 +556,11 @@ static Padded padded_problem(const Problem& p, char* w) {
   q.sA = (long long)d.a_el;
   q.sB = (long long)d.b_el;
   q.sC = (long long)d.c_el;
+  if (d.direct_c) {
+    q.C = p.C;
+    q.ldc = p.ldc;
+    q.sC = p.sC;
+  }
   q.batch = batch;
   q.workspace = nullptr;
   q.workspace_bytes = 0;
@@ -584,7 +596,7 @@ static hipError_t gemm_padded(const Problem& p, hipStream_t stream, int* used) {
   const Problem& q = d.q;
   char* Ap = (char*)q.A;
   char* Bp = (char*)q.B;
-  char* Cp = (char*)q.C;
+  char* Cp = (char*)p.workspace + d.a_bytes + d.b_bytes;  // padded C (unless direct_c)
   const int batch = q.batch;
   const int Kp = q.K, Np = q.N;
   const bool f32 = p.dtype == kF32;
@@ -613,6 +625,7 @@ static hipError_t gemm_padded(const Problem& p, hipStream_t stream, int* used) {
       : is_tiled(k) ? tiled_launch(q, k, a, part, part_bytes, stream)
                      : gemm256_launch(q.dtype, a, 4, stream);
   if (e != hipSuccess) return e;
+  if (d.direct_c) return hipSuccess;  // the kernel wrote the caller's C
   for (int b = 0; b < batch; ++b) {
     char* C = (char*)p.C + (size_t)b * p.sC * es;
     const char* Cs = Cp + b * d.c_el * es;

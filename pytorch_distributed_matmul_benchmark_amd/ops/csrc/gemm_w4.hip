@@ -377,8 +377,9 @@ __device__ __forceinline__ unsigned w4_tile(const GemmArgs& a, char* smem, int v
     for (int h = 8; h < 16; ++h) issue_piece<IL>(c, rb2, 0, t2, h);
   }
   const bool split = !PERS && a.splitk > 1;
+  const bool interior = m0 + BM <= a.M && n0 + BN <= a.N;
   constexpr bool kFuse = FUSED && !PERS && TRACE == 0;
-  const bool fuse = kFuse && !split && (nk & 1) == 0;
+  const bool fuse = kFuse && !split && interior && (nk & 1) == 0;
   const int nloop = fuse ? nk - 1 : nk;
   int t = 0;
   for (; t + 1 < nloop; t += 2) {  // branch-free body: B0/B1 and A7a/A7b swap roles every K-tile
@@ -409,7 +410,7 @@ __device__ __forceinline__ unsigned w4_tile(const GemmArgs& a, char* smem, int v
 
   // Epilogue: acc[i][j] holds C^T of a 16x16 tile (lane: row l16, columns
   // 4g..4g+3), stored through LDS as whole rows (common.h store_block16;
-  // interior tiles only: no masks). Every wave's DMAs have landed and every
+  // edge tiles masked at M / N). Every wave's DMAs have landed and every
   // fragment read is done before any wave writes its staging buffers.
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   char* Cb = (char*)a.C + (long long)bz * a.sC * 2;
@@ -423,8 +424,12 @@ __device__ __forceinline__ unsigned w4_tile(const GemmArgs& a, char* smem, int v
     } else if constexpr (!PERS) {
       splitk_row<8, 8, NT>(a, sl, slice, i, acc, v);
     }
-    store_block16<DT, false, false>(ebuf + (i & 1) * kEpiBuf, v, 1.0f, Cb, (long long)a.ldc * 2,
-                             m0 + wr * 128 + i * 16, n0 + wc * 128, a.M, a.N, lane);
+    if (interior)
+      store_block16<DT, false, false>(ebuf + (i & 1) * kEpiBuf, v, 1.0f, Cb, (long long)a.ldc * 2,
+                                      m0 + wr * 128 + i * 16, n0 + wc * 128, a.M, a.N, lane);
+    else
+      store_block16<DT, true, false>(ebuf + (i & 1) * kEpiBuf, v, 1.0f, Cb, (long long)a.ldc * 2,
+                                     m0 + wr * 128 + i * 16, n0 + wc * 128, a.M, a.N, lane);
   }
   if constexpr (TRACE) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -803,10 +808,14 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4s(GemmArgs a) {
 
 }  // namespace kw4
 
+// Edge tiles (M or N not a multiple of 256): rows of A past M read zeros
+// through the descriptor's extent; B columns past N read the next row's
+// elements (or zeros past the end) and only feed C columns the masked
+// epilogue drops. N % 8: 16-B B rows for the LDS-DMA.
 bool gemm_w4_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c) {
   if (dt != kBF16 && dt != kF16) return false;
   if (a.M <= 0 || a.N <= 0 || a.K <= 0) return false;
-  if (a.M % 256 || a.N % 256 || a.K % 64) return false;
+  if (a.N % 8 || a.K % 64) return false;
   if (a.lda % 8 || a.ldb % 8 || a.ldc % 4) return false;
   if (a.lda < a.K || a.ldb < a.N || a.ldc < a.N) return false;
   if (a.batch > 1 && (a.sA % 8 || a.sB % 8 || a.sC % 4)) return false;
@@ -819,8 +828,8 @@ bool gemm_w4_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b
 }
 
 hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
-  a.tiles_m = a.M / kw4::BM;
-  a.tiles_n = a.N / kw4::BN;
+  a.tiles_m = (a.M + kw4::BM - 1) / kw4::BM;  // edge tiles: masked epilogue
+  a.tiles_n = (a.N + kw4::BN - 1) / kw4::BN;
   const int S = a.splitk > 1 ? a.splitk : 1;
   if (S > 1) {
     const int nk = a.K / kw4::BK;

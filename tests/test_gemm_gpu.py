@@ -280,7 +280,7 @@ def test_odd_sizes_padded_to_fast_path(dtype, M, N, K):
     A = torch.randn(M, K, device="cuda", dtype=dt)
     B = torch.randn(K, N, device="cuda", dtype=dt)
     assert gemm.kernel_for(A, B) == "pdmb_generic_nn"  # unpadded, only generic could run it
-    assert gemm.padded_kernel_for(A, B) in ("pdmb_mfma256d_nn", "pdmb_f32_w4_nn", "pdmb_f32_256s_nn")
+    assert gemm.padded_kernel_for(A, B) in ("pdmb_mfma256d_nn", "pdmb_f32_w4_nn", "pdmb_f32_256s_nn") + TILED
     C = gemm.matmul(A, B)
     assert C.shape == (M, N)
     assert _relerr(C, _ref(A, B)) < TOL[dt]
@@ -294,15 +294,31 @@ def test_padded_path_misaligned_views_and_batches():
     big = torch.randn(1100, 2051, device="cuda", dtype=torch.bfloat16)
     A = big[:, 1:2049]            # lda = 2051 (misaligned), K = 2048
     B = torch.randn(2048, 1500, device="cuda", dtype=torch.bfloat16)
-    assert gemm.padded_kernel_for(A, B) == "pdmb_mfma256d_nn"
+    assert gemm.padded_kernel_for(A, B) == "pdmb_w4_nn"  # M = 1100: W4's masked edge tiles
     assert _relerr(gemm.matmul(A, B), _ref(A, B)) < TOL[torch.bfloat16]
     A3 = torch.randn(3, 700, 1000, device="cuda", dtype=torch.float16)
     B3 = torch.randn(3, 1000, 1300, device="cuda", dtype=torch.float16)
-    assert gemm.padded_kernel_for(A3, B3) == "pdmb_mfma256d_nn"
+    assert gemm.padded_kernel_for(A3, B3) == "pdmb_w4_nn"
     assert _relerr(gemm.bmm(A3, B3), torch.bmm(A3.double(), B3.double())) < TOL[torch.float16]
     out = torch.empty(1100, 1500, device="cuda", dtype=torch.bfloat16)
     ms = gemm.bench_matmul(A, B, out, iters=3, warmup=1)  # native loop takes the padded path too
     assert ms > 0 and _relerr(out, _ref(A, B)) < TOL[torch.bfloat16]
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
+def test_padded_k_only_writes_c_in_place(dtype):
+    """Only K off its granule: A / B are padded copies but the kernel writes the
+    caller's C directly (no padded C, no unpad copy) — and nothing past N or M."""
+    dt = DT[dtype]
+    torch.manual_seed(13)
+    A = torch.randn(1500, 1000, device="cuda", dtype=dt)
+    B = torch.randn(1000, 1024, device="cuda", dtype=dt)
+    assert gemm.kernel_for(A, B) == "pdmb_generic_nn" and gemm.padded_kernel_for(A, B) is not None
+    big = torch.full((1504, 1048), float("nan"), device="cuda", dtype=dt)
+    out = big[:1500, :1024]
+    gemm.matmul(A, B, out=out)
+    assert _relerr(out, _ref(A, B)) < TOL[dt]
+    assert torch.isnan(big[:, 1024:]).all() and torch.isnan(big[1500:]).all()
 
 
 # ---- W4: 4 waves x 128x128 per wave (gemm_w4.hip), the auto kernel for whole 256-tiles ----
@@ -337,11 +353,33 @@ def test_w4_random_matches_sched3(dtype):
     assert torch.equal(C, gemm.matmul(A, B, kernel="mfma256d"))
 
 
-def test_w4_rejects_edge_tiles_and_auto_falls_back():
-    A = torch.randn(300, 256, device="cuda", dtype=torch.bfloat16)
-    B = torch.randn(256, 512, device="cuda", dtype=torch.bfloat16)
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+@pytest.mark.parametrize("b,M,N,K,splitk", [(1, 300, 512, 256, 0), (1, 1000, 1000, 512, 0),
+                                           (1, 257, 264, 128, 0), (2, 700, 1304, 1024, 0),
+                                           (1, 16000, 16000, 128, 0), (1, 3000, 520, 4096, 2)])
+def test_w4_edge_tiles_masked(dtype, b, M, N, K, splitk):
+    """M / N not multiples of 256 (N % 8 == 0): rows past M load zeros through
+    the descriptor extent, B columns past N only feed dropped outputs, and the
+    epilogue masks its stores — exact on small integers, unsplit and split, and
+    nothing is written past N inside a wider row (ldc > N) or past M."""
+    dt = DT[dtype]
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K + b)
+    A = torch.randint(-3, 4, (b, M, K), device="cuda", generator=g).to(dt)
+    B = torch.randint(-3, 4, (b, K, N), device="cuda", generator=g).to(dt)
+    big = torch.full((b, M + 16, N + 24), float("nan"), device="cuda", dtype=dt)
+    out = big[:, :M, :N]
+    if b == 1:
+        A, B, out = A[0], B[0], out[0]
+    assert gemm.kernel_for(A, B, out, kernel="w4") == "pdmb_w4_nn"
+    gemm.matmul(A, B, out=out, kernel="w4", splitk=splitk)
+    assert torch.equal(out, (A.double() @ B.double()).to(dt))
+    assert torch.isnan(big[..., :M, N:]).all() and torch.isnan(big[..., M:, :]).all()
+
+
+def test_w4_rejects_unaligned_n():
+    A = torch.randn(256, 256, device="cuda", dtype=torch.bfloat16)
+    B = torch.randn(256, 300, device="cuda", dtype=torch.bfloat16)  # N % 8 != 0
     assert gemm.kernel_for(A, B, kernel="w4") == "unsupported"
-    assert gemm.kernel_for(A, B) == "pdmb_mfma256d_nn"
     with pytest.raises(RuntimeError):
         gemm.matmul(A, B, kernel="w4")
 
