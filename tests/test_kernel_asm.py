@@ -90,7 +90,9 @@ def test_w4_kernel_agpr_accumulators_and_counted_waits(tmp_path):
         assert k["vgpr"] <= 256
         loop = b[:b.find("global_atomic")]  # K-loop + drain; the split-K epilogue follows
         assert "global_atomic" in b  # the fused split-K meeting point is compiled in
-        assert len(re.findall(r"s_waitcnt vmcnt\(0\)", loop)) == 1
+        # two drains, both outside the K-loop: before the separate epilogue, and at the
+        # fused last K-tile's exit (the MFMA-to-store path has none)
+        assert len(re.findall(r"s_waitcnt vmcnt\(0\)", loop)) == 2
         assert len(re.findall(r"s_waitcnt vmcnt\(16\) lgkmcnt\(0\)", b)) >= 4
         # loop body: 2 K-tiles x 8 blocks x 16 MFMAs, one odd tail K-tile, the fused last K-tile
         assert len(re.findall(mfma, b)) == 4 * 128
