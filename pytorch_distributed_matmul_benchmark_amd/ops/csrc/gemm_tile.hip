@@ -47,9 +47,9 @@
 // same item schedule runs with the MFMA at every other gap: 16 MFMAs and 24
 // loads per K-tile per wave, as many cycles as the bf16 kernel's 32 + 24.
 //
-// Fast-path constraints (host-checked): M % BM == 0, N % BN == 0 (interior
-// tiles only), K % 64 == 0 (fp8: K % 128), lda / ldb % 8 == 0 (fp8: % 16),
-// ldc % 4 == 0, 16-B aligned A / B, 8-B aligned C.
+// Fast-path constraints (host-checked): N % 8 == 0 (fp8: % 4; M and N edge
+// tiles masked at the store), K % 64 == 0 (fp8: K % 128), lda / ldb % 8 == 0
+// (fp8: % 16), ldc % 4 == 0, 16-B aligned A / B, 8-B aligned C.
 #include "api.h"
 #include "common.h"
 #include "splitk.h"
@@ -435,7 +435,8 @@ __global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
   // Fused (unsplit, nk even): the loop stops before K-tile nk-1, whose
   // fragments it leaves in (A1, B1), and ktile_last runs it with the stores.
   const bool split = a.splitk > 1;
-  const bool fuse = kFused && !split && (nk & 1) == 0;
+  const bool interior = m0 + C::BM <= a.M && n0 + C::BN <= a.N;  // else: masked edge tile
+  const bool fuse = kFused && !split && interior && (nk & 1) == 0;
   const int nloop = fuse ? nk - 1 : nk;
   int t = 0;
   for (; t + 1 < nloop; t += 2) {
@@ -481,21 +482,26 @@ __global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
     } else {
       splitk_row<MB, NB, NT>(a, sl, slice, i, acc, v);
     }
-    if constexpr (DT == kFP8)  // alpha (the per-tensor scales), bf16 out
-      store_block16<kBF16, false, true, NB>(ebuf + (i & 1) * epi_buf<NB>(), v, a.alpha, Cb,
-                                            (long long)a.ldc * 2, m0 + wr * (C::BM / 2) + i * 16,
-                                            n0 + wc * (C::BN / 2), a.M, a.N, lane);
-    else
-      store_block16<DT, false, false, NB>(ebuf + (i & 1) * epi_buf<NB>(), v, 1.0f, Cb,
-                                          (long long)a.ldc * 2, m0 + wr * (C::BM / 2) + i * 16,
-                                          n0 + wc * (C::BN / 2), a.M, a.N, lane);
+    char* eb = ebuf + (i & 1) * epi_buf<NB>();
+    const int row0 = m0 + wr * (C::BM / 2) + i * 16, col0 = n0 + wc * (C::BN / 2);
+    if constexpr (DT == kFP8) {  // alpha (the per-tensor scales), bf16 out
+      if (interior)
+        store_block16<kBF16, false, true, NB>(eb, v, a.alpha, Cb, (long long)a.ldc * 2, row0, col0, a.M, a.N, lane);
+      else
+        store_block16<kBF16, true, true, NB>(eb, v, a.alpha, Cb, (long long)a.ldc * 2, row0, col0, a.M, a.N, lane);
+    } else {
+      if (interior)
+        store_block16<DT, false, false, NB>(eb, v, 1.0f, Cb, (long long)a.ldc * 2, row0, col0, a.M, a.N, lane);
+      else
+        store_block16<DT, true, false, NB>(eb, v, 1.0f, Cb, (long long)a.ldc * 2, row0, col0, a.M, a.N, lane);
+    }
   }
 }
 
 template <class C, bool FUSED = true>
 hipError_t launch(int dt, GemmArgs a, hipStream_t stream) {
-  a.tiles_m = a.M / C::BM;
-  a.tiles_n = a.N / C::BN;
+  a.tiles_m = (a.M + C::BM - 1) / C::BM;  // edge tiles: masked epilogue
+  a.tiles_n = (a.N + C::BN - 1) / C::BN;
   const int S = a.splitk > 1 ? a.splitk : 1;
   if (S > 1) {
     const int nk = a.K / (dt == kFP8 ? 128 : BK);
@@ -529,9 +535,12 @@ hipError_t launch(int dt, GemmArgs a, hipStream_t stream) {
 // bm x 128 tiles (bm = 128 or 256).
 bool gemm_tile_supported(int dt, int bm, const GemmArgs& a, size_t align_a, size_t align_b,
                          size_t align_c) {
+  // Edge tiles (M % bm, N % 128): rows of A (and fp8's Bt) past M / N load
+  // zeros through the descriptor extents; bf16 / fp16 B columns past N feed
+  // only C columns the masked epilogue drops.
   if (dt == kFP8) {  // A [M,K] row-major, Bt [N,K] row-major, bf16 C
     if (a.M <= 0 || a.N <= 0 || a.K <= 0) return false;
-    if (a.M % bm || a.N % 128 || a.K % 128) return false;
+    if (a.N % 4 || a.K % 128) return false;
     if (a.lda % 16 || a.ldb % 16 || a.ldc % 4) return false;
     if (a.lda < a.K || a.ldb < a.K || a.ldc < a.N) return false;
     if (a.batch > 1 && (a.sA % 16 || a.sB % 16 || a.sC % 4)) return false;
@@ -543,7 +552,7 @@ bool gemm_tile_supported(int dt, int bm, const GemmArgs& a, size_t align_a, size
   }
   if (dt != kBF16 && dt != kF16) return false;
   if (a.M <= 0 || a.N <= 0 || a.K <= 0) return false;
-  if (a.M % bm || a.N % 128 || a.K % 64) return false;
+  if (a.N % 8 || a.K % 64) return false;
   if (a.lda % 8 || a.ldb % 8 || a.ldc % 4) return false;
   if (a.lda < a.K || a.ldb < a.N || a.ldc < a.N) return false;
   if (a.batch > 1 && (a.sA % 8 || a.sB % 8 || a.sC % 4)) return false;

@@ -243,10 +243,9 @@ def test_fp8_tile_family_matches_w4_bitwise(kernel):
 
 def test_fp8_tile_family_refusals_and_race_screen():
     g = torch.Generator(device="cuda").manual_seed(4)
-    A = torch.randn(1000, 512, device="cuda", generator=g).to(FP8)  # M % 128 != 0
-    B = _colmajor(torch.randn(512, 512, device="cuda", generator=g).to(FP8))
+    A = torch.randn(1000, 512, device="cuda", generator=g).to(FP8)
+    B = _colmajor(torch.randn(512, 522, device="cuda", generator=g).to(FP8))  # N % 4 != 0
     assert gemm.kernel_for(A, B, kernel="fp8_t128") == "unsupported"
-    assert gemm.kernel_for(A, B) == "pdmb_fp8_w4_nt"  # auto: edge tiles on W4
     A8, sa = gemm.fp8_quantize(torch.randn(4096, 4096, device="cuda", generator=g))
     B8, sb = gemm.fp8_quantize(torch.randn(4096, 512, device="cuda", generator=g), colmajor=True)
     ref = gemm.matmul(A8, B8, alpha=sa * sb, kernel="fp8_t128")
@@ -276,3 +275,19 @@ def test_fp8_planner_choices():
     assert pick(16384, 16384, 16384) == "pdmb_fp8_w4s"
     with gemm.shared_device():
         assert pick(16384, 16384, 16384) == "pdmb_fp8_w4_nt"
+
+
+@pytest.mark.parametrize("kernel", ["fp8_t128", "fp8_t256x128"])
+@pytest.mark.parametrize("M,N,K,splitk", [(300, 516, 256, 1), (1000, 1000, 512, 1), (700, 264, 2048, 2)])
+def test_fp8_tile_family_edge_tiles(kernel, M, N, K, splitk):
+    """fp8 tile family edge tiles: A and Bt rows past M / N load zeros through the
+    descriptor extents; the bf16 stores are masked (N % 4)."""
+    g = torch.Generator(device="cuda").manual_seed(M + 7 * N + K)
+    Af, Bf = _ints((M, K), g, -2, 3), _ints((K, N), g, -2, 3)
+    A8, B8 = Af.to(FP8), _colmajor(Bf.to(FP8))
+    big = torch.full((M + 16, N + 24), float("nan"), device="cuda", dtype=torch.bfloat16)
+    out = big[:M, :N]
+    assert gemm.kernel_for(A8, B8, out, kernel=kernel) == f"pdmb_{kernel}_nt"
+    gemm.matmul(A8, B8, out=out, kernel=kernel, splitk=splitk, alpha=0.5)
+    assert torch.equal(out, (0.5 * (Af.double() @ Bf.double())).to(torch.bfloat16))
+    assert torch.isnan(big[:, N:]).all() and torch.isnan(big[M:]).all()

@@ -294,11 +294,11 @@ def test_padded_path_misaligned_views_and_batches():
     big = torch.randn(1100, 2051, device="cuda", dtype=torch.bfloat16)
     A = big[:, 1:2049]            # lda = 2051 (misaligned), K = 2048
     B = torch.randn(2048, 1500, device="cuda", dtype=torch.bfloat16)
-    assert gemm.padded_kernel_for(A, B) == "pdmb_w4_nn"  # M = 1100: W4's masked edge tiles
+    assert gemm.padded_kernel_for(A, B) in TILED  # M = 1100: masked edge tiles
     assert _relerr(gemm.matmul(A, B), _ref(A, B)) < TOL[torch.bfloat16]
     A3 = torch.randn(3, 700, 1000, device="cuda", dtype=torch.float16)
     B3 = torch.randn(3, 1000, 1300, device="cuda", dtype=torch.float16)
-    assert gemm.padded_kernel_for(A3, B3) == "pdmb_w4_nn"
+    assert gemm.padded_kernel_for(A3, B3) in TILED
     assert _relerr(gemm.bmm(A3, B3), torch.bmm(A3.double(), B3.double())) < TOL[torch.float16]
     out = torch.empty(1100, 1500, device="cuda", dtype=torch.bfloat16)
     ms = gemm.bench_matmul(A, B, out, iters=3, warmup=1)  # native loop takes the padded path too
@@ -374,6 +374,24 @@ def test_w4_edge_tiles_masked(dtype, b, M, N, K, splitk):
     gemm.matmul(A, B, out=out, kernel="w4", splitk=splitk)
     assert torch.equal(out, (A.double() @ B.double()).to(dt))
     assert torch.isnan(big[..., :M, N:]).all() and torch.isnan(big[..., M:, :]).all()
+
+
+@pytest.mark.parametrize("kernel", ["t128", "t256x128", "t128x2"])
+@pytest.mark.parametrize("M,N,K,splitk", [(300, 520, 256, 1), (1000, 1000, 512, 1), (3000, 7000, 512, 1),
+                                         (700, 264, 2048, 2)])
+def test_tile_family_edge_tiles_masked(kernel, M, N, K, splitk):
+    """The tile family's edge tiles (M % BM, N % 128): exact small integers, and
+    nothing written past N in a wider row or past M."""
+    dt = torch.bfloat16
+    g = torch.Generator(device="cuda").manual_seed(M + 5 * N + K)
+    A = torch.randint(-3, 4, (M, K), device="cuda", generator=g).to(dt)
+    B = torch.randint(-3, 4, (K, N), device="cuda", generator=g).to(dt)
+    big = torch.full((M + 16, N + 24), float("nan"), device="cuda", dtype=dt)
+    out = big[:M, :N]
+    assert gemm.kernel_for(A, B, out, kernel=kernel) == f"pdmb_{kernel}_nn"
+    gemm.matmul(A, B, out=out, kernel=kernel, splitk=splitk)
+    assert torch.equal(out, (A.double() @ B.double()).to(dt))
+    assert torch.isnan(big[:, N:]).all() and torch.isnan(big[M:]).all()
 
 
 def test_w4_rejects_unaligned_n():
