@@ -106,7 +106,7 @@ def test_bench_self_launches_n_ranks():
     assert d["n_gpus"] == 4 and d["config"]["parallelism"] == "independent4"
     assert d["single_gpu_tflops"] > 0
     assert d["scaling_efficiency"] == pytest.approx(d["value"] / (4 * d["single_gpu_tflops"]),
-                                                    rel=1e-3)
+                                                    rel=1e-3, abs=2e-4)  # fields rounded to 4 places
     for key, m in d["modes"].items():
         assert m["scaling_efficiency"] is not None, key
 
