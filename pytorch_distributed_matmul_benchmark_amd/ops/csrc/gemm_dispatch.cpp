@@ -195,9 +195,10 @@ int resolve_kernel(const Problem& p, int kernel) {
 //           writes and the last reads back an fp32 tile slab,
 //           T * (S-1) * 2 * BM * BN * 4 B / kSlabBw + kMeetUs.
 // kt per K-tile at full occupancy (us, random bf16, profiles/r2_*sweep*.jsonl):
-// W4 1.42, T256x128 0.87 (16k: 1187 vs 1438 TF for W4 on one box), T128 0.46,
-// T128x2 0.86 per pair of co-resident workgroups. The fit
-// reproduces the measured times of the shard shapes within ~10 %.
+// W4 1.42, T256x128 0.80 (0.80-0.85 on the 2-13-wave grids it competes on,
+// profiles/r2_planner_fit.jsonl; 0.87 at 16k, where the chip is power-bound and
+// W4 wins anyway), T128 0.46, T128x2 0.86 per pair of co-resident workgroups.
+// The fit reproduces the measured times of the shard shapes within ~10 %.
 //
 // fp8 (one K-tile = 128 e4m3: the same bytes per row and MFMA cycles as a
 // bf16 K-tile of 64) is planned over its own models: fp8 W4 (edge tiles too;
@@ -209,7 +210,7 @@ struct KernelModel {
 };
 static constexpr KernelModel kModels[] = {
     {kMfmaW4, 256, 256, 1, 1.42, false},
-    {kT256x128, 256, 128, 1, 0.87, false},
+    {kT256x128, 256, 128, 1, 0.80, false},
     {kT128, 128, 128, 1, 0.46, false},
     {kT128x2, 128, 128, 2, 0.86, false},
     {kFp8W4, 256, 256, 1, 1.30, true},

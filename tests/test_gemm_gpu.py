@@ -477,6 +477,9 @@ def test_auto_plan_for_shard_shapes():
         k, S = plan(*shape)  # more workgroups than 256x256 tiles: a smaller tile or a split W4
         assert k in TILED[1:] or (k == "pdmb_w4_nn" and S > 1), (shape, k, S)
     assert plan(16384, 1024, 256)[1] == 1  # too little K to split
+    # edge tiles: 3 waves of 256x128 beat 2 of 256x256 at 66 % busy (profiles/r2_planner_fit.jsonl)
+    assert plan(3000, 7000, 5056) == ("pdmb_t256x128_nn", 1)
+    assert plan(6000, 6000, 6144)[0] == "pdmb_w4_nn"
 
 
 @pytest.mark.parametrize("kernel,M,N,K,splitk", [
