@@ -4,6 +4,8 @@
 #include <hip/hip_runtime_api.h>
 #include <stddef.h>
 
+#include <utility>
+
 namespace pdmb {
 
 // Shipping kernels (the public `kernel=` surface of ops/gemm.py).
@@ -108,6 +110,11 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel);
 // K slices the W4 / T128 kernel that `kernel` resolves to would use for this
 // problem (1 = no split; 0 = neither runs it, or p.splitk is not possible).
 int choose_splitk(const Problem& p, int kernel);
+
+// Wave-quantisation tail (gemm_dispatch.cpp): {M1, S} when auto runs rows
+// [0, M1) as one launch and rows [M1, M) split S ways as a second; {0, 1} if
+// the problem runs as one launch.
+std::pair<int, int> tail_split(const Problem& p, int kernel);
 
 // Which kernel `kernel` (kAuto allowed) resolves to for this problem;
 // -1 if the requested kernel cannot run it.

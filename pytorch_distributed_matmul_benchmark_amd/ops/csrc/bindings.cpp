@@ -6,6 +6,7 @@
 #include <torch/extension.h>
 
 #include <string>
+#include <tuple>
 
 #include "api.h"
 
@@ -160,6 +161,15 @@ int64_t splitk_for(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C
   return pdmb::choose_splitk(p, (int)kernel);
 }
 
+// {M1, S}: auto runs rows [0, M1) unsplit and [M1, M) split S ways; {0, 1}: one launch.
+std::tuple<int64_t, int64_t> tail_split_for(const at::Tensor& A, const at::Tensor& B,
+                                            const at::Tensor& C, int64_t kernel, int64_t cus) {
+  pdmb::Problem p = make_problem(A, B, C);
+  p.cus = (int)cus;
+  const auto t = pdmb::tail_split(p, (int)kernel);
+  return {t.first, t.second};
+}
+
 // Total milliseconds for `iters` timed launches (after `warmup`).
 double bench(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t iters,
              int64_t warmup, bool graph, int64_t kernel, int64_t splitk) {
@@ -250,6 +260,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("splitk_for", &splitk_for, "W4 K slices for this problem (0: not W4)", py::arg("A"),
         py::arg("B"), py::arg("out"), py::arg("kernel") = 0, py::arg("splitk") = 0,
         py::arg("cus") = 0);
+  m.def("tail_split_for", &tail_split_for, "auto's wave-quantisation tail {M1, S} ({0, 1}: none)",
+        py::arg("A"), py::arg("B"), py::arg("out"), py::arg("kernel") = 0, py::arg("cus") = 0);
   m.def("bench", &bench, "native hipEvent timing loop; returns total ms", py::arg("A"),
         py::arg("B"), py::arg("out"), py::arg("iters"), py::arg("warmup"),
         py::arg("graph") = false, py::arg("kernel") = 0, py::arg("splitk") = 0);

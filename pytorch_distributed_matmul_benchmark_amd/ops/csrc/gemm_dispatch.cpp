@@ -103,6 +103,7 @@ static bool supports(const Problem& p, int kernel);
 struct Plan {
   int kernel;  // kMfmaW4 | kT128 | -1
   int splitk;
+  double cost = 0.0;  // plan_cost (us) of the choice
 };
 static Plan plan(const Problem& p, int kernel);
 
@@ -312,7 +313,7 @@ static Plan plan(const Problem& p, int kernel) {
       const double c = plan_cost(p, m.kernel, S);
       if (c < bc * 0.97) {  // a different choice only for a clear win
         bc = c;
-        best = Plan{m.kernel, S};
+        best = Plan{m.kernel, S, c};
       }
     }
   }
@@ -334,6 +335,66 @@ int choose_splitk(const Problem& p, int kernel) {
   if (k == kF32W4) return f32_split(p);
   if (!is_tiled(k)) return 0;
   return plan(p, k).splitk;
+}
+
+// ---- wave-quantisation tail (bf16/fp16 W4) ----------------------------------
+// A grid of 256x256 tiles whose last wave is mostly empty (6000^2 x 6144: 576
+// tiles = 2.25 waves of 256 CUs) runs as two launches on the stream: the first
+// M1 rows (a multiple of 256, tile rows that fill whole waves) unsplit, then
+// the remaining tile rows as one split-K wave (splitk.h) that fills the chip
+// instead of a quarter of it. Priced with plan_cost against the best
+// single-launch plan; taken only for a >= 3 % win. Measured (ms, auto before
+// -> tail, hipBLASLt; profiles/r2_tail_split_probe.jsonl): 6000^2 x 6144
+// 0.375 -> 0.342 (0.362), 6144^3 0.365 -> 0.339 (0.373), 3000 x 7000 x 5056
+// 0.203 -> 0.187 (0.193), 10000^2 x 10048 1.518 -> 1.457 (1.684); 5000^2 x 5056
+// has no split that helps and stays one launch. The tail rows keep their
+// fixed slice order, so results stay bitwise reproducible run to run.
+struct TailPlan {
+  int m1 = 0;  // rows of the first (unsplit) launch; 0 = one launch
+  int S = 1;   // K slices of the tail launch
+};
+
+static TailPlan tail_plan(const Problem& p, int kernel) {
+  TailPlan best;
+  if (kernel != kAuto || p.splitk != 0 || p.cus > 0) return best;
+  if ((p.dtype != kBF16 && p.dtype != kF16) || p.M <= 256 || p.K <= 0) return best;
+  if (resolve_kernel(p, kAuto) < 0 || !supports(p, kMfmaW4)) return best;
+  const Plan whole = plan(p, kAuto);  // the best single launch (W4 or a smaller tile)
+  if (whole.kernel < 0 || whole.splitk != 1) return best;
+  const long long slots = device_cus();
+  const int tm = (p.M + 255) / 256, tn = (p.N + 255) / 256, batch = p.batch < 1 ? 1 : p.batch;
+  double bc = whole.cost * 0.97;
+  for (int r = 1; r < tm; ++r) {  // r tail tile rows
+    Problem a = p, b = p;
+    a.M = (tm - r) * 256;
+    b.M = p.M - a.M;
+    const double c1 = plan_cost(a, kMfmaW4, 1);
+    for (int S : {2, 4}) {
+      if ((long long)r * tn * batch * S > slots || !split_ok(b, kMfmaW4, S)) continue;
+      const double c = c1 + plan_cost(b, kMfmaW4, S);
+      if (c < bc) {
+        bc = c;
+        best.m1 = a.M;
+        best.S = S;
+      }
+    }
+  }
+  return best;
+}
+
+static Problem tail_part(const Problem& p, const TailPlan& t) {  // rows [m1, M), split S ways
+  const size_t es = 2;
+  Problem b = p;
+  b.M = p.M - t.m1;
+  b.A = (const char*)p.A + (size_t)t.m1 * p.lda * es;
+  b.C = (char*)p.C + (size_t)t.m1 * p.ldc * es;
+  b.splitk = t.S;
+  return b;
+}
+
+std::pair<int, int> tail_split(const Problem& p, int kernel) {
+  const TailPlan t = tail_plan(p, kernel);
+  return {t.m1, t.S};
 }
 
 // fp8 W4 split-K (gemm_fp8.hip): grids of 256x256 tiles that fill at most
@@ -581,6 +642,8 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel) {
     return copies + (is_tiled(k) ? splitk_bytes(d.q, k, plan(d.q, k).splitk) : 0);
   }
   const int k = resolve_kernel(p, kernel);
+  const TailPlan t = tail_plan(p, kernel);
+  if (t.m1 > 0) return splitk_bytes(tail_part(p, t), kMfmaW4, t.S);  // the first launch is unsplit
   if (is_tiled(k)) return splitk_bytes(p, k, plan(p, k).splitk);
   if (k == kFp8W4) return fp8_split_bytes(p, fp8_split(p));
   if (k == kF32W4) return fp8_split_bytes(p, f32_split(p));  // same 256x256 fp32 slots
@@ -637,12 +700,31 @@ static hipError_t gemm_padded(const Problem& p, hipStream_t stream, int* used) {
   return hipSuccess;
 }
 
+// The two launches of a tail plan; false: run the problem as one launch (the
+// stream has no split-K counters yet inside a graph capture, or the workspace
+// was sized for another plan).
+static bool gemm_tail(const Problem& p, const TailPlan& t, hipStream_t stream, hipError_t* e) {
+  const Problem b = tail_part(p, t);
+  if (!p.workspace || p.workspace_bytes < splitk_bytes(b, kMfmaW4, t.S) || !stream_counters(stream))
+    return false;
+  Problem a = p;
+  a.M = t.m1;
+  *e = tiled_launch(a, kMfmaW4, to_args(a), nullptr, 0, stream, w4s_auto(a) ? 7 : 0);
+  if (*e == hipSuccess) *e = tiled_launch(b, kMfmaW4, to_args(b), p.workspace, p.workspace_bytes, stream);
+  return true;
+}
+
 hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
   if (wants_padding(p, kernel)) return gemm_padded(p, stream, used);
   const int k = resolve_kernel(p, kernel);
   if (used) *used = k;
   if (k < 0) return hipErrorInvalidValue;
   if (p.M == 0 || p.N == 0 || p.batch == 0) return hipSuccess;
+  if (p.K > 0) {
+    const TailPlan t = tail_plan(p, kernel);
+    hipError_t e = hipSuccess;
+    if (t.m1 > 0 && gemm_tail(p, t, stream, &e)) return e;
+  }
   GemmArgs a = to_args(p);
   if (p.K == 0) {
     // C = 0 (empty reduction).

@@ -250,6 +250,21 @@ def splitk_for(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = N
     return int(C.splitk_for(A, B, out, _kid(kernel), int(splitk), _cus()))
 
 
+def tail_split_for(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
+                   kernel="auto") -> tuple:
+    """(M1, S): auto runs rows [0, M1) as one W4 launch and the remaining tile rows
+    as a second, S-way split-K launch that fills the chip (gemm_dispatch.cpp
+    tail_plan); (0, 1) when the problem runs as one launch."""
+    if A.device.type != "cuda":
+        return (0, 1)
+    C = _native.load()
+    if out is None:
+        out = torch.empty(_out_shape(A, B), dtype=out_dtype(A.dtype), device=A.device)
+    A, B = _prep_pair(A, B)
+    m1, s = C.tail_split_for(A, B, out, _kid(kernel), _cus())
+    return (int(m1), int(s))
+
+
 def bench_matmul(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, iters: int,
                  warmup: int, graph: bool = False, kernel="auto", splitk: int = 0) -> float:
     """Native timing loop (hipEvents around ``iters`` launches). Returns TOTAL ms."""

@@ -394,6 +394,39 @@ def test_tile_family_edge_tiles_masked(kernel, M, N, K, splitk):
     assert torch.isnan(big[:, N:]).all() and torch.isnan(big[M:]).all()
 
 
+@pytest.mark.parametrize("M,N,K", [(6000, 6000, 6144), (10000, 10000, 10048), (6144, 6144, 6144)])
+def test_auto_wave_tail_split(M, N, K):
+    """Auto's wave-quantisation tail: rows [0, M1) as one W4 launch, the last
+    tile rows split-K in a second. Exact small integers, nothing written past
+    N in a wider row or past M, the same bits under graph replay."""
+    dt = torch.bfloat16
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    A = torch.randint(-3, 4, (M, K), device="cuda", generator=g).to(dt)
+    B = torch.randint(-3, 4, (K, N), device="cuda", generator=g).to(dt)
+    big = torch.full((M + 16, N + 24), float("nan"), device="cuda", dtype=dt)
+    out = big[:M, :N]
+    m1, S = gemm.tail_split_for(A, B, out)
+    assert 0 < m1 < M and m1 % 256 == 0 and S in (2, 4), (m1, S)
+    gemm.matmul(A, B, out=out)
+    ref = (A.double() @ B.double()).to(dt)
+    assert torch.equal(out, ref)
+    assert torch.isnan(big[:, N:]).all() and torch.isnan(big[M:]).all()
+    C2 = torch.empty(M, N, device="cuda", dtype=dt)
+    assert gemm.bench_matmul(A, B, C2, 3, 1, graph=True) > 0
+    assert torch.equal(C2, ref)
+
+
+def test_no_tail_split_where_it_does_not_pay():
+    def tail(M, N, K, **kw):
+        A = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
+        B = torch.empty(K, N, device="cuda", dtype=torch.bfloat16)
+        return gemm.tail_split_for(A, B, **kw)
+    assert tail(5000, 5000, 5056) == (0, 1)      # no split of the last rows fills the chip
+    assert tail(16384, 16384, 16384) == (0, 1)   # whole waves
+    assert tail(8192, 1024, 8192) == (0, 1)      # under-filled: the planner's split / small tiles
+    assert tail(6000, 6000, 6144, kernel="w4") == (0, 1)  # explicit kernels run as asked
+
+
 def test_w4_rejects_unaligned_n():
     A = torch.randn(256, 256, device="cuda", dtype=torch.bfloat16)
     B = torch.randn(256, 300, device="cuda", dtype=torch.bfloat16)  # N % 8 != 0
