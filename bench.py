@@ -245,14 +245,6 @@ def _free(ctx) -> None:
         torch.cuda.empty_cache()
 
 
-def _free_port() -> int:
-    import socket
-
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def _self_launch(a) -> int:
     """``--gpus N > 1`` outside torchrun: start N ranks as a child
     ``torch.distributed.run`` (the reference's launcher pattern,
@@ -268,10 +260,12 @@ def _self_launch(a) -> int:
                   f"per rank (use --dist-backend gloo to rehearse more ranks than GPUs)",
                   file=sys.stderr, flush=True)
             return 2
+    # no --master-port: --standalone binds port 0 itself (a port picked here
+    # could be taken by another process before the child listens on it)
+    where = ([f"--master-addr=127.0.0.1", f"--master-port={a.master_port}"] if a.master_port
+             else ["--standalone", "--local-addr=127.0.0.1"])
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-           f"--nproc-per-node={a.gpus}", "--master-addr=127.0.0.1",
-           f"--master-port={a.master_port or _free_port()}", os.path.abspath(__file__),
-           *sys.argv[1:]]
+           f"--nproc-per-node={a.gpus}", *where, os.path.abspath(__file__), *sys.argv[1:]]
     env = dict(os.environ, PDMB_BENCH_CHILD="1")
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
     env.setdefault("OMP_NUM_THREADS", "1")

@@ -639,6 +639,8 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel) {
     const Padded d = padded_problem(p, nullptr);
     const size_t copies = d.a_bytes + d.b_bytes + d.c_bytes;
     const int k = resolve_kernel(d.q, kAuto);
+    const TailPlan t = tail_plan(d.q, kAuto);
+    if (t.m1 > 0) return copies + splitk_bytes(tail_part(d.q, t), kMfmaW4, t.S);
     return copies + (is_tiled(k) ? splitk_bytes(d.q, k, plan(d.q, k).splitk) : 0);
   }
   const int k = resolve_kernel(p, kernel);
@@ -651,6 +653,20 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel) {
       k == kMfmaW4Pers || k == kMfmaW4PersTrace)
     return splitk_bytes(p, kMfmaW4, plan(p, kMfmaW4).splitk);
   return 0;
+}
+
+// The two launches of a tail plan; false: run the problem as one launch (the
+// stream has no split-K counters yet inside a graph capture, or the workspace
+// was sized for another plan).
+static bool gemm_tail(const Problem& p, const TailPlan& t, hipStream_t stream, hipError_t* e) {
+  const Problem b = tail_part(p, t);
+  if (!p.workspace || p.workspace_bytes < splitk_bytes(b, kMfmaW4, t.S) || !stream_counters(stream))
+    return false;
+  Problem a = p;
+  a.M = t.m1;
+  *e = tiled_launch(a, kMfmaW4, to_args(a), nullptr, 0, stream, w4s_auto(a) ? 7 : 0);
+  if (*e == hipSuccess) *e = tiled_launch(b, kMfmaW4, to_args(b), p.workspace, p.workspace_bytes, stream);
+  return true;
 }
 
 static hipError_t gemm_padded(const Problem& p, hipStream_t stream, int* used) {
@@ -684,7 +700,12 @@ static hipError_t gemm_padded(const Problem& p, hipStream_t stream, int* used) {
   a.splitk = 0;  // only the tiled kernels below split here (their slots follow the copies)
   char* part = Cp + d.c_bytes;
   const size_t part_bytes = p.workspace_bytes - (d.a_bytes + d.b_bytes + d.c_bytes);
-  e = k == kF32W4     ? gemm_f32_w4_launch(a, stream)
+  const TailPlan t = tail_plan(q, kAuto);
+  Problem qt = q;  // the tail plan's split slots follow the copies too
+  qt.workspace = part;
+  qt.workspace_bytes = part_bytes;
+  if (!(t.m1 > 0 && gemm_tail(qt, t, stream, &e)))
+    e = k == kF32W4     ? gemm_f32_w4_launch(a, stream)
       : k == kF32_256s ? gemm_f32_256_launch(a, 1, stream)
       : is_tiled(k) ? tiled_launch(q, k, a, part, part_bytes, stream)
                      : gemm256_launch(q.dtype, a, 4, stream);
@@ -698,20 +719,6 @@ static hipError_t gemm_padded(const Problem& p, hipStream_t stream, int* used) {
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
-}
-
-// The two launches of a tail plan; false: run the problem as one launch (the
-// stream has no split-K counters yet inside a graph capture, or the workspace
-// was sized for another plan).
-static bool gemm_tail(const Problem& p, const TailPlan& t, hipStream_t stream, hipError_t* e) {
-  const Problem b = tail_part(p, t);
-  if (!p.workspace || p.workspace_bytes < splitk_bytes(b, kMfmaW4, t.S) || !stream_counters(stream))
-    return false;
-  Problem a = p;
-  a.M = t.m1;
-  *e = tiled_launch(a, kMfmaW4, to_args(a), nullptr, 0, stream, w4s_auto(a) ? 7 : 0);
-  if (*e == hipSuccess) *e = tiled_launch(b, kMfmaW4, to_args(b), p.workspace, p.workspace_bytes, stream);
-  return true;
 }
 
 hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {

@@ -416,6 +416,23 @@ def test_auto_wave_tail_split(M, N, K):
     assert torch.equal(C2, ref)
 
 
+@pytest.mark.parametrize("M,N,K", [(6000, 6000, 6100), (6000, 5996, 6144)])
+def test_padded_wave_tail_split(M, N, K):
+    """The padded fast path (K or N off the granule) runs the padded problem with
+    the same tail plan (6000 x 6000 x 6144 after padding): exact, nothing written
+    outside C."""
+    dt = torch.bfloat16
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
+    A = torch.randint(-3, 4, (M, K), device="cuda", generator=g).to(dt)
+    B = torch.randint(-3, 4, (K, N), device="cuda", generator=g).to(dt)
+    big = torch.full((M + 16, N + 24), float("nan"), device="cuda", dtype=dt)
+    out = big[:M, :N]
+    assert gemm.padded_kernel_for(A, B) in TILED
+    gemm.matmul(A, B, out=out)
+    assert torch.equal(out, (A.double() @ B.double()).to(dt))
+    assert torch.isnan(big[:, N:]).all() and torch.isnan(big[M:]).all()
+
+
 def test_no_tail_split_where_it_does_not_pay():
     def tail(M, N, K, **kw):
         A = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
