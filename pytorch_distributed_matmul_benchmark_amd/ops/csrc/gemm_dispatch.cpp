@@ -524,22 +524,38 @@ static long long round_up(long long x, long long m) { return (x + m - 1) / m * m
 
 // dst[r][c] = (r < rows && c < cols) ? src[r][c] : 0 for r < drows, c < dcols.
 // dst rows are 16-B aligned (ldd % VEC == 0); each thread writes one 16-B
-// vector and reads its VEC source elements with plain (possibly unaligned)
-// scalar loads, which coalesce across the wave. One pass, no memset.
+// vector. Its VEC source elements come as one 16-B or two 8-B loads when the
+// source base and row pitch allow (src_align, uniform over the grid: K = 6100
+// bf16 rows are 8-B aligned), else as scalar loads, which coalesce across the
+// wave. One pass, no memset.
 template <typename T>
 __global__ void pad_copy(const T* __restrict__ src, long long lds, int rows, int cols,
-                         T* __restrict__ dst, long long ldd, int drows, int dcols) {
+                         T* __restrict__ dst, long long ldd, int drows, int dcols, int src_align) {
   constexpr int VEC = 16 / sizeof(T);
+  union Vec {
+    uint4 u;
+    uint2 h[2];
+    T e[VEC];
+  };
   const int vpr = dcols / VEC;  // vectors per dst row (dcols % VEC == 0)
   const long long total = (long long)drows * vpr;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const int r = (int)(i / vpr), c0 = (int)(i % vpr) * VEC;
-    T v[VEC];
+    const T* s = src + r * lds + c0;
+    Vec v;
+    if (src_align >= 8 && r < rows && c0 + VEC <= cols) {
+      if (src_align >= 16) {
+        v.u = *(const uint4*)s;
+      } else {
+        v.h[0] = ((const uint2*)s)[0];
+        v.h[1] = ((const uint2*)s)[1];
+      }
+    } else {
 #pragma unroll
-    for (int e = 0; e < VEC; ++e)
-      v[e] = (r < rows && c0 + e < cols) ? src[r * lds + c0 + e] : (T)0;
-    *(uint4*)(dst + r * ldd + c0) = *(const uint4*)v;
+      for (int e = 0; e < VEC; ++e) v.e[e] = (r < rows && c0 + e < cols) ? s[e] : (T)0;
+    }
+    *(uint4*)(dst + r * ldd + c0) = v.u;
   }
 }
 
@@ -558,8 +574,10 @@ __global__ void unpad_copy(const T* __restrict__ src, long long lds, int rows, i
 template <typename T>
 static hipError_t pad_copy_launch(const void* src, long long lds, int rows, int cols, void* dst,
                                   long long ldd, int drows, int dcols, hipStream_t s) {
+  const uintptr_t pitch = (uintptr_t)lds * sizeof(T), base = (uintptr_t)src;
+  const int align = (base | pitch) % 16 == 0 ? 16 : (base | pitch) % 8 == 0 ? 8 : 1;
   hipLaunchKernelGGL(pad_copy<T>, dim3(4096), dim3(256), 0, s, (const T*)src, lds, rows, cols,
-                     (T*)dst, ldd, drows, dcols);
+                     (T*)dst, ldd, drows, dcols, align);
   return hipGetLastError();
 }
 
