@@ -18,17 +18,28 @@ After the headline measurement (which is what ``value`` reports) the same
 process also times the reference's other two scaling modes — batch_parallel
 (matmul_scaling_benchmark.py:106-165) and matrix_parallel (:167-238), each
 serialized as in the reference and with the collective overlapped on the
-comm stream — for ``--extra-steps`` steps each, and reports them under
+comm stream (parallel/overlap.py OverlapPipeline: whole GEMMs, a ring of
+outputs, pieces started by the GEMM's own completion signals; the plan is
+in the line) — for ``--extra-steps`` steps each, and reports them under
 ``"modes"`` in the same JSON line, so one launch at N GPUs yields the
-BASELINE configs 3-5 (``--extra-steps 0`` skips them).
+BASELINE configs 3-5 (``--extra-steps 0`` skips them). Each secondary mode
+warms up for at least ``--extra-warmup-ms`` of GPU time and is compared
+with a same-shape reference run on rank 0 alone just before its family
+(batch: the bmm of the local batch; matrix: the whole N x N GEMM), so its
+``scaling_efficiency`` isolates communication from clock drift.
+
+Verifiability: the line carries the process-group backend, the world size
+the group saw, the RCCL version, the collective self-test result (run
+before any timing), per-rank TFLOPS min / max, the serialized modes'
+compute / comm split, and per-mode mean GFX clock and power (amdsmi).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
 ``--gpus N > 1`` without torchrun self-launches N ranks (a child
-``torch.distributed.run``, started before anything touches the GPU) and exits
-with its code; under torchrun, ``WORLD_SIZE != --gpus`` is an error. At N > 1
+``torch.distributed.run``, started before anything touches the GPU; the GPU
+count comes from sysfs / amdsmi, never HIP) and exits with its code; under torchrun, ``WORLD_SIZE != --gpus`` is an error. At N > 1
 the job also times the headline GEMM on rank 0 alone (others at a barrier)
 and reports ``scaling_efficiency = value / (N x single_gpu_tflops)`` — the
 1 -> N curve's efficiency from one launch. Every mode's setup is agreed
@@ -42,6 +53,7 @@ import argparse
 import contextlib
 import gc
 import json
+import math
 import os
 import sys
 import time
@@ -52,13 +64,16 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from pytorch_distributed_matmul_benchmark_amd.ops import gemm  # noqa: E402
-from pytorch_distributed_matmul_benchmark_amd.parallel.overlap import (  # noqa: E402
-    BidirRing, GatherOverlap, ReduceOverlap, all_gather_now, compute_ctx, compute_stream, gemm_chunks)
 from pytorch_distributed_matmul_benchmark_amd.parallel.comm import CommStream  # noqa: E402
 from pytorch_distributed_matmul_benchmark_amd.parallel.dist import (  # noqa: E402
-    DistContext, all_ok, barrier, cleanup_distributed, reduce_scalar, setup_distributed)
+    DistContext, all_ok, barrier, cleanup_distributed, gather_scalars, reduce_scalar,
+    setup_distributed, verify_collectives)
+from pytorch_distributed_matmul_benchmark_amd.parallel.overlap import (  # noqa: E402
+    BidirRing, OverlapPipeline, all_gather_now, compute_ctx, compute_stream, plan_for_units)
 from pytorch_distributed_matmul_benchmark_amd.parallel.partition import (  # noqa: E402
     column_shard, global_batch, local_batch)
+from pytorch_distributed_matmul_benchmark_amd.utils.telemetry import (  # noqa: E402
+    ClockSampler, visible_gpus)
 
 # Reference numbers (README.md:43-46): whole-system TFLOPS at 16k bf16.
 BASELINE_TFLOPS = {"independent": {1: 140.0, 2: 294.0},
@@ -70,9 +85,12 @@ DTYPES = {"bfloat16": torch.bfloat16, "float16": torch.float16, "float32": torch
 
 
 class Workload:
-    """Operands + one timed ``step()`` of a scaling mode on this rank."""
+    """Operands + one timed ``step()`` of a scaling mode on this rank.
 
-    def __init__(self, a, ctx, mode: str, overlap: bool):
+    ``batch`` (independent only): GEMMs per step (a bmm), the rank-0-alone
+    reference of batch_parallel's local batch."""
+
+    def __init__(self, a, ctx, mode: str, overlap: bool, batch: int = 1):
         self.ctx, self.mode, self.overlap = ctx, mode, overlap
         self.cuda = ctx.device.type == "cuda"
         self.dt = DTYPES[a.dtype]
@@ -82,22 +100,31 @@ class Workload:
         self._g = torch.Generator(device=dev)
         flop_gemm = 2.0 * n * n * n
         overlap = overlap and ws > 1
+        self.finish = lambda: None       # issues what a pipelined step left pending + joins
+        self.split = None                # serialized modes: [(ev0, ev_compute, ev_comm)] per timed step
+        self.recording = False
+        self.plan = None
+        self.pipe = None
+        self.step = None                 # set below, or by _pipeline
         comp = torch.cuda.current_stream(dev) if self.cuda else None
         self._mask = None
-        if overlap and self.cuda and a.comm_cus > 0:
-            # GEMM chunks on a CU-masked stream, RCCL gets the free CUs at once
+        if overlap and self.cuda and a.comm_cus > 0 and mode in ("batch_parallel", "matrix_parallel",
+                                                                 "ring_parallel"):
+            # GEMMs on a CU-masked stream, RCCL gets the free CUs at once
             comp, self._mask = compute_stream(dev, a.comm_cus)
         self.comp = comp
 
         if mode == "independent":
-            A, B = self._rnd(n, n, seed=2 * ctx.rank), self._rnd(n, n, seed=2 * ctx.rank + 1, b=True)
-            C = torch.empty(n, n, device=dev, dtype=odt)
+            shape = (batch, n, n) if batch > 1 else (n, n)
+            A = self._rnd(*shape, seed=2 * ctx.rank)
+            B = self._rnd(*shape, seed=2 * ctx.rank + 1, b=True)
+            C = torch.empty(*shape, device=dev, dtype=odt)
             self.kernel = self._label(A, B, C)
 
             def step():
                 self._mm(A, B, C)
-            self.flops = flop_gemm * ws
-            self.global_batch, self.parallelism = ws, f"independent{ws}"
+            self.flops = flop_gemm * ws * batch
+            self.global_batch, self.parallelism = ws * batch, f"independent{ws}"
         elif mode == "batch_parallel":
             lb, gb = local_batch(ws), global_batch(ws)
             A = self._rnd(lb, n, n, seed=2 * ctx.rank)
@@ -105,19 +132,24 @@ class Workload:
             C = torch.empty(lb, n, n, device=dev, dtype=odt)
             self.kernel = self._label(A, B, C)
             if overlap:
-                ov = ReduceOverlap(lb, gemm_chunks(n, n, a.chunks, dt, dev), dev)
-                _, s0, e0 = ov.units[0]  # what a chunk runs beside the reductions
-                self.kernel = self._label(A[0, s0:e0], B[0], C[0, s0:e0], shared=True)
+                # ring over the batch's own outputs; one element: a second C (reference C1/C2)
+                units = ([(A[b], B[b], C[b]) for b in range(lb)] if lb >= 2 else
+                         [(A[0], B[0], C[0]), (A[0], B[0], torch.empty_like(C[0]))])
+                cs = CommStream(dev)
+
+                def coll(r, p, s, e, after, done):
+                    cs.all_reduce(units[r][2][s:e], after=after, done=done)
+                self._pipeline(a, units, coll, lb, "all_reduce", n * n * C.element_size(), cs)
+            else:
+                self._serial_split()
 
                 def step():
-                    with compute_ctx(self.comp, self._mask):
-                        ov.step(self._mm, A, B, C, self.comp)
-                    self._join()
-            else:
-                def step():
+                    self._seg(0)
                     self._mm(A, B, C)
+                    self._seg(1)
                     if ws > 1:
                         dist.all_reduce(C)
+                    self._seg(2)
             self.flops = flop_gemm * gb
             self.global_batch, self.parallelism = gb, f"dp{ws}"
         elif mode == "matrix_parallel":
@@ -131,24 +163,31 @@ class Workload:
             Cl = torch.empty(n, sh.padded, device=dev, dtype=odt)
             self.kernel = self._label(A, Bl, Cl)
             if overlap:
-                ov = GatherOverlap(n, sh.padded, ws, dev, odt,
-                                   gemm_chunks(n, sh.padded, a.chunks, dt, dev),
-                                   pieces=a.comm_chunks, requested=a.chunks, impl=a.allgather)
-                s0, e0 = ov.chunks[0]  # what a chunk runs beside the gathers
-                self.kernel = self._label(A[s0:e0], Bl, Cl[s0:e0], shared=True)
+                units = [(A, Bl, Cl), (A, Bl, torch.empty_like(Cl))]
+                cs = CommStream(dev)
+                self._gathered = {}
 
-                def step():
-                    with compute_ctx(self.comp, self._mask):
-                        ov.step(self._mm, A, Bl, Cl, self.comp)
-                    self._join()
+                def coll(r, p, s, e, after, done):
+                    key = (r, p)
+                    if key not in self._gathered:
+                        self._gathered[key] = torch.empty(ws * (e - s), sh.padded, device=dev,
+                                                          dtype=odt)
+                    g = cs.all_gather_direct if a.allgather == "direct" else cs.all_gather_into
+                    g(self._gathered[key], units[r][2][s:e], after=after, done=done)
+                self._pipeline(a, units, coll, 1, "all_gather", n * sh.padded * Cl.element_size(),
+                               cs)
             else:
                 gathered = torch.empty(ws * n, sh.padded, device=dev, dtype=odt)
                 cs = CommStream(dev) if a.allgather == "direct" else None
+                self._serial_split()
 
                 def step():
+                    self._seg(0)
                     self._mm(A, Bl, Cl)
+                    self._seg(1)
                     if ws > 1:
                         all_gather_now(gathered, Cl, a.allgather, cs)
+                    self._seg(2)
             self.flops = flop_gemm
             self.global_batch, self.parallelism = 1, f"tp{ws}"
         elif mode == "ring_parallel":
@@ -171,14 +210,94 @@ class Workload:
             ring = BidirRing(Al, rp, ctx.rank, ws, dev)
 
             def step():
-                with gemm.shared_device():  # the hops' transfers run beside these GEMMs
+                # the hops' transfers run beside these GEMMs: shared device, and
+                # on the (possibly CU-masked) compute stream the ring's events
+                # are recorded on, joined back to the timing stream after
+                with compute_ctx(self.comp, self._mask):
                     ring.step(self._mm, Bl, Cl, self.comp)
+                self._join()
             self.flops = flop_gemm
             self.global_batch, self.parallelism = 1, f"ring{ws}"
         else:
             raise ValueError(mode)
-        self.step = step
+        if self.step is None:
+            self.step = step
 
+    # -- overlap ---------------------------------------------------------------
+    def _pipeline(self, a, units, coll, per_step, kind, payload, cs):
+        """The overlapped step: plan (parallel/overlap.py plan_overlap), then an
+        OverlapPipeline, or the serialized step when the plan says overlap loses."""
+        A, B, C = units[0]
+        self.plan = plan_for_units(units, self.ctx.world_size, kind, payload,
+                                   native=self.backend == "native", requested=a.chunks,
+                                   steps=max(a.extra_steps, 1), owner=self._mask)
+        if not self.plan.overlap:  # the planner refuses a losing overlap: serialize
+            self.step = self._serial_fallback(units, per_step, kind, a.allgather)
+            return
+        self.pipe = OverlapPipeline(self._mm, units, coll, self.ctx.device, self.plan,
+                                    per_step=per_step, compute=self.comp, owner=self._mask, comm=cs)
+        self.kernel = ("pdmb_w4_nn (completion signals)" if self.pipe.signalled
+                       else self._label(A, B, C, shared=True))
+
+        def finish():
+            self.pipe.finish()
+            self._join()
+        self.step = self.pipe.step
+        self.finish = finish
+
+    def _serial_fallback(self, units, per_step, kind, impl):
+        """The serialized step over the same units (collective on the current stream)."""
+        ws, dev = self.ctx.world_size, self.ctx.device
+        gathered = {}
+        cs = CommStream(dev) if impl == "direct" else None
+
+        def step():
+            for r in range(per_step):
+                Ar, Br, Cr = units[r]
+                self._mm(Ar, Br, Cr)
+                if ws <= 1:
+                    continue
+                if kind == "all_reduce":
+                    dist.all_reduce(Cr)
+                else:
+                    if r not in gathered:
+                        gathered[r] = torch.empty(ws * Cr.shape[0], Cr.shape[1], device=dev,
+                                                  dtype=Cr.dtype)
+                    all_gather_now(gathered[r], Cr, impl, cs)
+        return step
+
+    # -- serialized compute / comm split ------------------------------------------
+    def _serial_split(self):
+        self.split = []
+
+    def _seg(self, i):
+        if self.split is None or not self.recording:
+            return
+        if i == 0:
+            self.split.append([])
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+        else:
+            e = time.perf_counter()
+        self.split[-1].append(e)
+
+    def split_ms(self):
+        """(compute_ms, comm_ms) per step of the last timed region, or (None, None)."""
+        if not self.split:
+            return None, None
+        comp = comm = 0.0
+        for e0, e1, e2 in self.split:
+            if self.cuda:
+                comp += e0.elapsed_time(e1)
+                comm += e1.elapsed_time(e2)
+            else:
+                comp += (e1 - e0) * 1e3
+                comm += (e2 - e1) * 1e3
+        k = len(self.split)
+        return comp / k, comm / k
+
+    # -- operands / kernels ----------------------------------------------------
     def _rnd(self, *shape, seed, b=False):
         """N(0,1) operand; fp8: rounded to e4m3 (scale 1), a B operand column-major."""
         self._g.manual_seed(seed)
@@ -192,6 +311,11 @@ class Workload:
     def _mm(self, A, B, out):
         if self.dt == gemm.FP8 and self.cuda and self.backend == "torch":
             one = torch.ones((), device=A.device)
+            if A.dim() == 3:
+                for i in range(A.shape[0]):
+                    torch._scaled_mm(A[i], B[i], scale_a=one, scale_b=one, out_dtype=torch.bfloat16,
+                                     out=out[i])
+                return out
             return torch._scaled_mm(A, B, scale_a=one, scale_b=one, out_dtype=torch.bfloat16,
                                     out=out)
         if (self.backend == "torch" or not self.cuda) and self.dt != gemm.FP8:
@@ -217,25 +341,58 @@ class Workload:
         if self.cuda:
             torch.cuda.synchronize(self.ctx.device)
 
-    def timed(self, warmup: int, steps: int) -> float:
-        """W untimed steps, then K steps bracketed by sync+barrier; max-over-ranks seconds."""
+    def warm(self, warmup: int, warmup_ms: float = 0.0) -> float:
+        """``warmup`` untimed steps, then more until at least ``warmup_ms`` of wall
+        time has run (GPU only; the count is agreed across ranks, MAX, so ranks
+        stepping collectives stay in lock-step). Returns the warm-up ms."""
+        t0 = time.perf_counter()
         for _ in range(warmup):
             self.step()
+        self.finish()
         self._sync()
-        barrier(self.ctx)
-        self._sync()
-        t0 = time.perf_counter()
-        for _ in range(steps):
+        if warmup_ms > 0 and self.cuda:
+            done = (time.perf_counter() - t0) * 1e3
+            t1 = time.perf_counter()
             self.step()
+            self.finish()
+            self._sync()
+            one = max((time.perf_counter() - t1) * 1e3, 1e-3)
+            done += one
+            extra = 0 if done >= warmup_ms else min(10_000, math.ceil((warmup_ms - done) / one))
+            extra = int(reduce_scalar(self.ctx, float(extra), "max"))
+            for _ in range(extra):
+                self.step()
+            self.finish()
+            self._sync()
+        return (time.perf_counter() - t0) * 1e3
+
+    def timed(self, steps: int):
+        """K steps bracketed by sync + barrier on both sides. Returns
+        (max-over-ranks seconds, this rank's seconds, telemetry dict)."""
         self._sync()
         barrier(self.ctx)
         self._sync()
-        elapsed = time.perf_counter() - t0
+        self.recording = True
+        with ClockSampler(self.ctx.device) as smp:
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                self.step()
+            self.finish()
+            self._sync()
+            barrier(self.ctx)
+            self._sync()
+            elapsed = time.perf_counter() - t0
+        self.recording = False
+        mine = elapsed
         if self.ctx.is_distributed:
             t = torch.tensor([elapsed], dtype=torch.float64, device=self.ctx.device)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
-        return elapsed
+        return elapsed, mine, smp.result()
+
+    def close(self):
+        if self.pipe is not None:
+            self.pipe.close()
 
 
 def _free(ctx) -> None:
@@ -248,13 +405,14 @@ def _free(ctx) -> None:
 def _self_launch(a) -> int:
     """``--gpus N > 1`` outside torchrun: start N ranks as a child
     ``torch.distributed.run`` (the reference's launcher pattern,
-    run_scaling_benchmark.sh:23-31) and exit with its code. Nothing here has
-    touched the GPU (``import torch`` does not initialise HIP), so the child
-    ranks own their devices from scratch; the parent only waits."""
+    run_scaling_benchmark.sh:23-31) and exit with its code. Nothing here
+    touches HIP (``import torch`` does not initialise it; the GPU count comes
+    from sysfs / amdsmi, utils/telemetry.py), so the child ranks own their
+    devices from scratch; the parent only waits."""
     import subprocess
 
     if a.device == "cuda" and a.dist_backend in ("auto", "nccl"):
-        ndev = torch.cuda.device_count()  # does not initialise HIP on this image
+        ndev = visible_gpus()
         if ndev < a.gpus:
             print(f"bench.py: --gpus {a.gpus} but only {ndev} GPU(s) visible; RCCL needs one GPU "
                   f"per rank (use --dist-backend gloo to rehearse more ranks than GPUs)",
@@ -299,46 +457,65 @@ def _die(ctx, key: str, exc: BaseException) -> None:
     os._exit(1)
 
 
-def _measure(a, ctx, mode: str, overlap: bool, warmup: int, steps: int, key: str):
+def _measure(a, ctx, mode: str, overlap: bool, warmup: int, steps: int, key: str,
+             warmup_ms: float = 0.0, batch: int = 1):
     """Build (agreed across ranks) and time one workload. Returns
-    ``(tflops, seconds, workload_info)`` or ``(None, None, error_string)``."""
+    ``(tflops, seconds, info)`` or ``(None, None, error_string)``."""
     w, err = None, None
     try:
         _fault(ctx, key, "setup")
-        w = Workload(a, ctx, mode, overlap)
+        w = Workload(a, ctx, mode, overlap, batch=batch)
     except Exception as e:  # OOM, unsupported shape, ...: every rank skips together
         err = f"{type(e).__name__}: {e}"
         print(f"[rank {ctx.rank}] {key} setup failed: {err}", file=sys.stderr, flush=True)
     if not all_ok(ctx, err is None):
+        if w is not None:
+            w.close()
         del w
         _free(ctx)
         return None, None, err or "failed on another rank"
     try:
         _fault(ctx, key, "timed")
-        el = w.timed(warmup, steps)
+        wms = w.warm(warmup, warmup_ms)
+        el, mine, tel = w.timed(steps)
     except Exception as e:
         _die(ctx, key, e)
     v = w.flops * steps / el / 1e12 if el > 0 else 0.0
-    info = dict(global_batch=w.global_batch, parallelism=w.parallelism, kernel=w.kernel)
+    # per-rank rate: this rank's share of the FLOPs over its own wall time
+    share = w.flops / ctx.world_size if mode in ("independent", "batch_parallel") else w.flops
+    rates = gather_scalars(ctx, share * steps / mine / 1e12 if mine > 0 else 0.0)
+    clocks = gather_scalars(ctx, tel["sclk_mhz"] or 0.0)
+    comp, comm = w.split_ms()
+    info = dict(global_batch=w.global_batch, parallelism=w.parallelism, kernel=w.kernel,
+                warmup_ms=round(wms, 1),
+                per_rank_tflops={"min": round(min(rates), 4), "max": round(max(rates), 4)},
+                sclk_mhz=tel["sclk_mhz"], power_w=tel["power_w"],
+                sclk_mhz_min_over_ranks=(round(min(clocks), 1) if min(clocks) > 0 else None))
+    if comp is not None:
+        info["compute_ms"], info["comm_ms"] = round(comp, 4), round(comm, 4)
+    if w.plan is not None:
+        info["plan"] = w.plan.as_dict()
+        info["plan"]["signalled"] = bool(w.pipe is not None and w.pipe.signalled)
+    w.close()
     del w
     _free(ctx)
     return v, el, info
 
 
-def _single_gpu_tflops(a, ctx):
-    """The '1 GPU' denominator of the scaling efficiency: the headline GEMM
-    timed on rank 0 alone (same K/W, same device) while every other rank
-    waits at a barrier — measured in the same job, so the 1 -> N curve needs
-    no second launch. The reference's own "Scaling efficiency" is rank
+def _rank0_alone(a, ctx, warmup: int, steps: int, warmup_ms: float, batch: int = 1):
+    """TFLOPS of ``batch`` N x N GEMMs per step on rank 0 ALONE (the others wait
+    at a barrier), measured inside this job: the '1 GPU' denominator of a
+    scaling efficiency. The reference's own "Scaling efficiency" is rank
     imbalance, not scaling (matmul_scaling_benchmark.py:315)."""
     val = 0.0
     barrier(ctx)
     if ctx.rank == 0:
         try:
             one = DistContext(rank=0, world_size=1, local_rank=ctx.local_rank, device=ctx.device)
-            w = Workload(a, one, "independent", False)
-            el = w.timed(a.warmup, a.steps)
-            val = w.flops * a.steps / el / 1e12 if el > 0 else 0.0
+            w = Workload(a, one, "independent", False, batch=batch)
+            w.warm(warmup, warmup_ms)
+            el, _, _ = w.timed(steps)
+            val = w.flops * steps / el / 1e12 if el > 0 else 0.0
             del w
         except Exception as e:  # a failed reference is "no efficiency", never a hang
             print(f"[rank 0] single-GPU reference failed: {e!r}", file=sys.stderr, flush=True)
@@ -347,6 +524,16 @@ def _single_gpu_tflops(a, ctx):
     barrier(ctx)
     v = reduce_scalar(ctx, val, "sum")
     return v if v > 0 else None
+
+
+def _rccl_version(ctx):
+    if not (ctx.is_distributed and ctx.backend == "nccl"):
+        return None
+    try:
+        v = torch.cuda.nccl.version()
+        return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception:
+        return None
 
 
 def main() -> int:
@@ -359,12 +546,11 @@ def main() -> int:
     ap.add_argument("--mode", default="independent",
                     choices=["independent", "batch_parallel", "matrix_parallel", "ring_parallel"])
     ap.add_argument("--overlap", action="store_true",
-                    help="batch/matrix_parallel: hide the collective behind the GEMM chunks")
-    ap.add_argument("--chunks", type=int, default=4,
-                    help="overlap: GEMM row chunks (capped so each chunk fills the chip)")
-    ap.add_argument("--comm-chunks", type=int, default=0,
-                    help="matrix_parallel --overlap: all-gather pieces per GEMM chunk "
-                         "(0: enough pieces for --chunks in total)")
+                    help="batch/matrix_parallel: hide the collective behind the GEMMs")
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="overlap: collective pieces per GEMM, each started by the GEMM's own "
+                         "completion signals (0: the planner's choice; 1: whole collectives, "
+                         "pipelined across GEMMs)")
     ap.add_argument("--comm-cus", type=int, default=0,
                     help="overlap: CUs kept free of GEMM workgroups for RCCL (CU-masked "
                          "compute stream; 0 = no mask)")
@@ -380,8 +566,11 @@ def main() -> int:
                     help="timed steps for each secondary mode reported under \"modes\" "
                          "(batch_parallel / matrix_parallel, serialized and overlapped); 0: skip")
     ap.add_argument("--extra-warmup", type=int, default=3)
+    ap.add_argument("--extra-warmup-ms", type=float, default=300.0,
+                    help="secondary modes (and their rank-0 references) warm up for at least "
+                         "this much wall time (GPU only)")
     ap.add_argument("--no-scaling-ref", action="store_true",
-                    help="N > 1: skip the in-job 1-GPU reference (scaling_efficiency = null)")
+                    help="skip the in-job rank-0-alone references (scaling_efficiency = null at N > 1)")
     a = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ:
@@ -398,6 +587,13 @@ def main() -> int:
     ws = ctx.world_size
     dt = DTYPES[a.dtype]
     headline16k = dt == torch.bfloat16 and a.size == 16384 and cuda
+    # The collective self-test gates the job (matmul_scaling_benchmark.py:388-394).
+    verified = verify_collectives(ctx, verbose=False) if ctx.is_distributed else None
+    if verified is False:
+        if ctx.is_main:
+            print("bench.py: collective self-test failed", file=sys.stderr, flush=True)
+        cleanup_distributed()
+        return 1
 
     def vs_base(mode, value):
         base = BASELINE_TFLOPS.get(mode, {}).get(ws) if headline16k else None
@@ -414,34 +610,38 @@ def main() -> int:
 
     single = value if ws == 1 and a.mode == "independent" else None
     if ws > 1 and not a.no_scaling_ref:
-        single = _single_gpu_tflops(a, ctx)
+        single = _rank0_alone(a, ctx, a.warmup, a.steps, 0.0)
 
-    def eff(v):
-        return round(v / (ws * single), 4) if single and v is not None else None
+    def eff(v, ref):
+        return round(v / (ws * ref), 4) if ref and v is not None else None
 
-    # Secondary modes (BASELINE configs 4-5): same operands' shapes and dtype, own timing.
-    # At ws = 1 there is no collective to overlap: those entries are null, not a
-    # second copy of the serialized number.
+    # Secondary modes (BASELINE configs 4-5), each family after its own
+    # rank-0-alone reference of the same per-rank shape. At ws = 1 there is no
+    # collective to overlap: those entries are null.
     modes = {}
     if a.extra_steps > 0:
-        for mode, ov in (("batch_parallel", False), ("batch_parallel", True),
-                         ("matrix_parallel", False), ("matrix_parallel", True)):
-            if mode == a.mode and ov == a.overlap:
-                continue
-            key = mode + ("+overlap" if ov else "")
-            if ov and ws == 1:
-                modes[key] = None
-                continue
-            v, el, info = _measure(a, ctx, mode, ov, a.extra_warmup, a.extra_steps, key)
-            if v is None:
-                modes[key] = {"error": info}
-                continue
-            modes[key] = {"value": round(v, 4), "ms_per_step": round(el / a.extra_steps * 1e3, 4),
-                          "steps": a.extra_steps, "warmup": a.extra_warmup,
-                          "global_batch": info["global_batch"], "parallelism": info["parallelism"],
-                          "scaling": "strong" if mode == "matrix_parallel" else "weak",
-                          "vs_baseline": vs_base(mode, v), "scaling_efficiency": eff(v),
-                          "kernel": info["kernel"]}
+        wms = a.extra_warmup_ms
+        for family, ref_batch in (("batch_parallel", local_batch(ws)), ("matrix_parallel", 1)):
+            ref = None
+            if not a.no_scaling_ref or ws == 1:
+                ref = _rank0_alone(a, ctx, a.extra_warmup, a.extra_steps, wms, batch=ref_batch)
+            for ov in (False, True):
+                if family == a.mode and ov == a.overlap:
+                    continue
+                key = family + ("+overlap" if ov else "")
+                if ov and ws == 1:
+                    modes[key] = None
+                    continue
+                v, el, info = _measure(a, ctx, family, ov, a.extra_warmup, a.extra_steps, key,
+                                       warmup_ms=wms)
+                if v is None:
+                    modes[key] = {"error": info}
+                    continue
+                modes[key] = {"value": round(v, 4), "ms_per_step": round(el / a.extra_steps * 1e3, 4),
+                              "steps": a.extra_steps, "warmup": a.extra_warmup,
+                              "scaling": "strong" if family == "matrix_parallel" else "weak",
+                              "vs_baseline": vs_base(family, v), "scaling_efficiency": eff(v, ref),
+                              "ref_tflops_rank0_alone": round(ref, 4) if ref else None, **info}
 
     if ctx.is_main:
         out = {
@@ -450,7 +650,7 @@ def main() -> int:
             "ms_per_step": round(ms_step, 4), "higher_is_better": True,
             "scaling": "strong" if a.mode in ("matrix_parallel", "ring_parallel") else "weak",
             "vs_baseline": vs_base(a.mode, value),
-            "scaling_efficiency": eff(value),
+            "scaling_efficiency": eff(value, single),
             "single_gpu_tflops": round(single, 4) if single else None,
             "dtype": {"bfloat16": "bf16", "float16": "fp16", "float32": "fp32",
                       "float8_e4m3fn": "fp8_e4m3"}[a.dtype],
@@ -460,11 +660,20 @@ def main() -> int:
                        "global_batch": head["global_batch"], "seq_len": a.size,
                        "parallelism": head["parallelism"], "mode": a.mode,
                        "overlap": bool(a.overlap), "backend": a.backend, "kernel": head["kernel"]},
+            "dist_backend": ctx.backend,
+            "world_size_seen": dist.get_world_size() if ctx.is_distributed else 1,
+            "rccl_version": _rccl_version(ctx),
+            "collectives_verified": verified,
+            "per_rank_tflops": head["per_rank_tflops"],
+            "sclk_mhz": head["sclk_mhz"], "power_w": head["power_w"],
+            "sclk_mhz_min_over_ranks": head["sclk_mhz_min_over_ranks"],
             "per_gpu_tflops": (round(value / ws, 2)
                                if a.mode not in ("matrix_parallel", "ring_parallel") else None),
             "vs_reference_1gpu_linear": round(value / (140.0 * ws), 3),
             "modes": modes,
         }
+        if "plan" in head:
+            out["config"]["overlap_plan"] = head["plan"]
         print(json.dumps(out), flush=True)
     cleanup_distributed()
     return 0

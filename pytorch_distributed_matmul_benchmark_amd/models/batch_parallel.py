@@ -12,21 +12,27 @@ Differences:
     the FLOPs actually executed.
   * Q10: segment boundaries are hipEvents recorded on the stream; the host
     never synchronises inside the timed loop.
-  * ``overlap=True``: the local batch is cut into units (batch element ×
-    row chunk). Unit u's GEMM runs on the compute stream; its all-reduce
-    runs on a high-priority comm stream as soon as u's ready-event fires,
-    while unit u+1 computes. The next iteration's GEMM into a unit waits for
-    that unit's done-event (no write-while-reducing race, Q7). Time per
-    iteration is then wall time; compute-only time is measured in a separate
-    loop and both are reported (Q9).
+  * ``overlap=True`` (parallel/overlap.py OverlapPipeline): each batch
+    element is one whole GEMM (a unit); its all-reduce runs on a
+    high-priority comm stream while the next element — or the next
+    iteration's first — computes, and the next GEMM into a buffer waits
+    only for that buffer's last all-reduce (no write-while-reducing race,
+    Q7). With one element per rank (ws >= 4) the ring has a second C, the
+    reference's C1/C2 (backup/matmul_overlap_benchmark.py:98-101). Where the
+    planner says so, the all-reduce of an element starts piece by piece as
+    the GEMM's own tiles complete (W4 completion signals). A plan that loses
+    to serializing runs serialized. Time per iteration is wall time; the
+    compute-only time is measured in a separate loop, under the same
+    shared-device context the pipeline's GEMMs run in, and both are reported
+    (Q9).
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
 
-from ..parallel.comm import current_stream
-from ..parallel.overlap import ReduceOverlap, compute_ctx, compute_stream, gemm_chunks
+from ..parallel.comm import CommStream, current_stream
+from ..parallel.overlap import OverlapPipeline, compute_ctx, compute_stream, plan_for_units
 from ..parallel.dist import DistContext
 from ..parallel.partition import global_batch, local_batch
 from ..utils.metrics import gemm_flops, tflops_from
@@ -52,7 +58,17 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
             dist.all_reduce(C)
 
     extra = {"global_batch": gb, "local_batch": lb, "overlap": bool(w.overlap and distributed)}
-    if not (w.overlap and distributed):
+    plan = None
+    units = ([(A[b], B[b], C[b]) for b in range(lb)] if lb >= 2 else
+             [(A[0], B[0], C[0]), (A[0], B[0], torch.empty_like(C[0]))])
+    compute, owner = (compute_stream(dev, w.comm_cus) if (w.overlap and distributed)
+                      else (current_stream(dev), None))
+    if w.overlap and distributed:
+        plan = plan_for_units(units, ws, "all_reduce", n * n * C.element_size(),
+                              native=w.backend == "native", requested=w.chunks,
+                              steps=max(w.iters, 1), owner=owner)
+        extra["plan"] = plan.as_dict()
+    if plan is None or not plan.overlap:
         def serial_step():
             mm(A, B, C)
             reduce_all()
@@ -77,43 +93,68 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
                          tflops=tflops_from(flops, avg / 1e3), compute_ms=comp, comm_ms=comm,
                          compute_only_tflops=tflops_from(flops, comp / 1e3), kernel=label,
                          extra=extra)
+        checked = [C[b] for b in range(lb)]
     else:
-        ov = ReduceOverlap(lb, gemm_chunks(n, n, w.chunks, w.dtype, dev), dev)
-        extra["units"] = len(ov.units)
-        _, s0, e0 = ov.units[0]  # what a chunk runs beside the reductions
-        label = kernel_label(w, A[0, s0:e0], B[0], C[0, s0:e0], shared=True)
-        compute, owner = compute_stream(dev, w.comm_cus)
+        cs = CommStream(dev)
+
+        def coll(r, p, s, e, after, done):
+            cs.all_reduce(units[r][2][s:e], after=after, done=done)
+
+        pipe = OverlapPipeline(mm, units, coll, dev, plan, per_step=lb, compute=compute,
+                               owner=owner, comm=cs)
+        extra["units_per_step"] = lb
+        extra["ring"] = len(units)
+        extra["pieces"] = len(pipe.pieces)
+        extra["signalled"] = pipe.signalled
         extra["comm_cus"] = w.comm_cus
+        label = ("pdmb_w4_nn (completion signals)" if pipe.signalled
+                 else kernel_label(w, A[0], B[0], C[0], shared=True))
 
         def step():
-            with compute_ctx(compute, owner):
-                ov.step(mm, A, B, C, compute)
+            pipe.step()
+
+        def finish():
+            pipe.finish()
             if compute is not None:  # the timing stream joins the (masked) compute stream
                 current_stream(dev).wait_stream(compute)
 
-        warmup(step, w, ctx)
-        # compute-only reference time (reference: 10 GEMM-only iterations), taken
-        # BEFORE the timed loop so the loop's last reduced C stays checkable.
+        warmup(lambda: (step(), finish()), w, ctx)
+        # compute-only reference time (reference: 10 GEMM-only iterations) of the
+        # same GEMMs in the same context (shared device / CU budget), taken BEFORE
+        # the timed loop so the loop's last reduced C stays checkable.
         synchronize(dev)
         k = max(1, min(w.iters, 10))
-        comp = time_loop_ms(lambda: mm(A, B, C), k, 0, dev) / k
+
+        scratch = torch.empty_like(C[0])  # the ring's outputs keep their reduced values
+
+        def gemms_only():
+            with compute_ctx(compute, owner):
+                for b in range(lb):
+                    mm(A[b], B[b], scratch)
+            if compute is not None:
+                current_stream(dev).wait_stream(compute)
+        comp = time_loop_ms(gemms_only, k, 0, dev) / k
         align_ranks(ctx)
         sw = Stopwatch(dev)
         sw.start(current_stream(dev))
         for _ in range(w.iters):
             step()
+        finish()
         sw.stop(current_stream(dev))
         avg = sw.elapsed_ms() / max(w.iters, 1)
+        pipe.close()
         res = ModeResult(mode="batch_parallel", n=n, world_size=ws, avg_ms=avg,
                          flops_local=flops, flops_total=flops * ws,
                          tflops=tflops_from(flops, avg / 1e3), compute_ms=comp,
                          comm_ms=max(avg - comp, 0.0),
                          compute_only_tflops=tflops_from(flops, comp / 1e3), kernel=label,
                          extra=extra)
+        checked = [u[2] for u in units]
     if w.check:
         # Every timed iteration recomputes C and all-reduces it, so after the
         # loop C[b] must equal Σ_ranks A_r[b] @ B_r[b] (checks GEMM + RCCL +
         # the overlap event ordering end to end).
         synchronize(dev)
-        res.relerr = max(allreduced_relerr(ctx, A[b], B[b], C[b]) for b in range(lb))
+        res.relerr = max(allreduced_relerr(ctx, A[min(i, lb - 1)], B[min(i, lb - 1)], Cb)
+                         for i, Cb in enumerate(checked))
     return res

@@ -35,8 +35,7 @@ class Workload:
     kernel: str = "auto"        # native kernel selection (auto | mfma256 | generic)
     batch: int = 4              # batch_parallel requested global batch (rounded up to a multiple of ws)
     overlap: bool = False       # comm/compute overlap on a second stream
-    chunks: int = 4             # overlap granularity (row chunks per GEMM)
-    comm_chunks: int = 0        # matrix_parallel overlap: all-gather pieces per GEMM chunk (0: auto)
+    chunks: int = 0             # overlap: collective pieces per GEMM (signalled; 0 = planner, 1 = whole)
     comm_cus: int = 0           # overlap: CUs kept free of GEMM workgroups for RCCL (CU-masked stream)
     allgather: str = "rccl"     # matrix_parallel all-gather: rccl | direct (P2P to every peer at once)
     graph: bool = False         # independent: replay the timed loop as one hipGraph

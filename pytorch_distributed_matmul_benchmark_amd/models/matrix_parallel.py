@@ -16,20 +16,22 @@ Differences:
     ``[ws*N, shard]`` filled by ``all_gather_into_tensor`` (block r =
     C[:, r*shard:(r+1)*shard]); no per-iteration allocation and no list
     copy-out.
-  * ``overlap=True``: C_local is computed in row chunks (``gemm_chunks``:
-    as many as still fill the chip, split-K included); chunk j is
-    all-gathered in ``comm_chunks`` pieces on the high-priority comm stream
-    while chunk j+1 is computed (event-ordered, parallel/overlap.py), the
-    GEMM optionally on a CU-masked stream (``comm_cus``). Gather layout: per
-    piece ``[ws*rows_p, shard]``.
+  * ``overlap=True`` (parallel/overlap.py OverlapPipeline): C_local is ONE
+    GEMM launch per iteration into a ring of two buffers (the reference's
+    C1/C2, backup/matmul_overlap_benchmark.py:98-101); iteration i's
+    all-gather runs on the high-priority comm stream while iteration i+1
+    computes, and — where the planner says so — starts piece by piece as the
+    GEMM's own tiles complete (W4 completion signals), the GEMM optionally on
+    a CU-masked stream (``comm_cus``). Gather layout: per (ring slot, piece)
+    ``[ws*rows_p, shard]``. A plan that loses to serializing runs serialized.
 """
 from __future__ import annotations
 
 import torch
 
 from ..parallel.comm import CommStream, current_stream
-from ..parallel.overlap import (GatherOverlap, all_gather_now, compute_ctx, compute_stream,
-                                gemm_chunks)
+from ..parallel.overlap import (OverlapPipeline, all_gather_now, compute_ctx, compute_stream,
+                                plan_for_units)
 from ..parallel.dist import DistContext
 from ..parallel.partition import column_shard
 from ..utils.metrics import gemm_flops, tflops_from
@@ -78,8 +80,16 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     flops_local = gemm_flops(n, sh.padded, n)
     flops_total = gemm_flops(n, n, n)
     extra = {"shard_cols": sh.padded, "overlap": bool(w.overlap), "allgather": w.allgather}
+    units = [(A, B_local, C_local), (A, B_local, torch.empty_like(C_local))]
+    plan = None
+    compute, owner = compute_stream(dev, w.comm_cus) if w.overlap else (current_stream(dev), None)
+    if w.overlap:
+        plan = plan_for_units(units, ws, "all_gather", n * sh.padded * C_local.element_size(),
+                              native=w.backend == "native", requested=w.chunks,
+                              steps=max(w.iters, 1), owner=owner)
+        extra["plan"] = plan.as_dict()
 
-    if not w.overlap:
+    if plan is None or not plan.overlap:
         # dim-0 concatenation [ws*N, shard] (the layout both gloo and RCCL accept);
         # block r = gathered.view(ws, N, shard)[r] = C[:, r*shard:(r+1)*shard].
         gathered = torch.empty((ws * n, sh.padded), device=dev, dtype=out_dtype(w))
@@ -109,35 +119,51 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         avg = comp + cm
         full = (lambda: assemble(gathered, n, ws))
     else:
-        ov = GatherOverlap(n, sh.padded, ws, dev, out_dtype(w),
-                           gemm_chunks(n, sh.padded, w.chunks, w.dtype, dev),
-                           pieces=w.comm_chunks, requested=w.chunks, impl=w.allgather)
-        extra["chunks"] = len(ov.chunks)
-        s0, e0 = ov.chunks[0]  # what a chunk runs beside the gathers
-        label = kernel_label(w, A[s0:e0], B_local, C_local[s0:e0], shared=True)
-        extra["comm_pieces"] = ov.n_pieces
-        extra["comm_cus"] = w.comm_cus
-        compute, owner = compute_stream(dev, w.comm_cus)
+        cs = CommStream(dev)
+        bufs = {}
 
-        def step():
-            with compute_ctx(compute, owner):
-                ov.step(mm, A, B_local, C_local, compute)
+        def coll(r, p, s, e, after, done):
+            if (r, p) not in bufs:
+                bufs[(r, p)] = torch.empty((ws * (e - s), sh.padded), device=dev,
+                                           dtype=out_dtype(w))
+            g = cs.all_gather_direct if w.allgather == "direct" else cs.all_gather_into
+            g(bufs[(r, p)], units[r][2][s:e], after=after, done=done)
+
+        pipe = OverlapPipeline(mm, units, coll, dev, plan, per_step=1, compute=compute,
+                               owner=owner, comm=cs)
+        extra["pieces"] = len(pipe.pieces)
+        extra["signalled"] = pipe.signalled
+        extra["comm_cus"] = w.comm_cus
+        label = ("pdmb_w4_nn (completion signals)" if pipe.signalled
+                 else kernel_label(w, A, B_local, C_local, shared=True))
+
+        def finish():
+            pipe.finish()
             if compute is not None:  # the timing stream joins the (masked) compute stream
                 current_stream(dev).wait_stream(compute)
 
-        warmup(step, w, ctx)
+        warmup(lambda: (pipe.step(), finish()), w, ctx)
         align_ranks(ctx)
         sw = Stopwatch(dev)
         sw.start(current_stream(dev))
         for _ in range(w.iters):
-            step()
+            pipe.step()
+        finish()
         sw.stop(current_stream(dev))
         avg = sw.elapsed_ms() / max(w.iters, 1)
+        last = (pipe.k - 1) % len(units)  # the ring slot the last iteration gathered
         synchronize(dev)
         k = max(1, min(w.iters, 10))
-        comp = time_loop_ms(lambda: mm(A, B_local, C_local), k, 1, dev) / k
+
+        def gemm_only():  # same context as the pipeline's GEMMs; into the other slot
+            with compute_ctx(compute, owner):
+                mm(*units[1 - last])
+            if compute is not None:
+                current_stream(dev).wait_stream(compute)
+        comp = time_loop_ms(gemm_only, k, 1, dev) / k
         cm = max(avg - comp, 0.0)
-        full = (lambda: assemble(ov.gathered(), n, ws))
+        pipe.close()
+        full = (lambda: assemble([bufs[(last, p)] for p in range(len(pipe.pieces))], n, ws))
 
     res = ModeResult(mode="matrix_parallel", n=n, world_size=ws, avg_ms=avg,
                      flops_local=flops_local, flops_total=flops_total,

@@ -92,7 +92,37 @@ struct Problem {
   // (padded-path copies, split-K partials), stream-ordered with the launch.
   void* workspace = nullptr;
   size_t workspace_bytes = 0;
+  // Completion signals (signal_create; nullptr = off): the launch runs the
+  // W4 kernel with per-slot tile counters (common.h GemmArgs::sig) — one
+  // slot per sig_rows 256-row tile rows of each batch element — and writes
+  // sig_epoch into a slot's host flag once all its tiles are stored. Only W4
+  // runs signalled (auto: W4 where it would have chosen W4 / W4S; otherwise
+  // hipErrorNotSupported); no tail split, no padded path.
+  struct Signal* sig = nullptr;
+  int sig_rows = 0;
+  unsigned sig_epoch = 0;
 };
+
+// Completion-signal set of `slots` slots on `device`: device counters
+// (hipMalloc, zeroed once, never reset: launch e of the set completes a slot
+// at e x its tile count) and host-mapped fine-grained flags the GPU writes
+// and a host thread polls.
+struct Signal {
+  unsigned* dev = nullptr;       // tile counters
+  unsigned* host = nullptr;      // flags, host address
+  unsigned* host_dev = nullptr;  // flags, device address of the same memory
+  int slots = 0;
+  int device = 0;
+};
+hipError_t signal_create(int device, int slots, Signal** out);
+void signal_destroy(Signal* s);
+// Host wait until flag[slot] reaches `epoch` (wrap-safe); false on timeout.
+bool signal_wait(const Signal* s, int slot, unsigned epoch, double timeout_s);
+unsigned signal_flag(const Signal* s, int slot);
+// Tile rows of one completion unit for this problem on W4: the rows of one
+// 256-workgroup round of its XCD-aware order (map_tile), so pieces finish in
+// order and each piece is a whole number of rounds. 0: cannot be signalled.
+int signal_granule(const Problem& p, int kernel);
 
 // Split-K arrival counters are a library resource: one zeroed block per
 // (device, stream), created on first use and left zeroed by every launch

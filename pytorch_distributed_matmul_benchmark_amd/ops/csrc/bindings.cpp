@@ -125,20 +125,60 @@ at::Tensor workspace_for(pdmb::Problem& p, int kernel, const at::Tensor& like) {
   return ws;
 }
 
+pdmb::Signal* as_signal(int64_t h) { return reinterpret_cast<pdmb::Signal*>((uintptr_t)h); }
+
+// sig (a signal_create handle, 0 = none), sig_rows, sig_epoch: the launch
+// signals per-slot completion (api.h Problem::sig).
 at::Tensor matmul(const at::Tensor& A, const at::Tensor& B, c10::optional<at::Tensor> out,
-                  int64_t kernel, double alpha, int64_t splitk, int64_t cus) {
+                  int64_t kernel, double alpha, int64_t splitk, int64_t cus, int64_t sig,
+                  int64_t sig_rows, int64_t sig_epoch) {
   at::Tensor C = out.has_value() ? *out : alloc_out(A, B);
   pdmb::Problem p = make_problem(A, B, C, alpha);
   p.splitk = (int)splitk;
   p.cus = (int)cus;
+  if (sig) {
+    p.sig = as_signal(sig);
+    TORCH_CHECK(p.sig->device == A.device().index(), "pdmb: signal set lives on another device");
+    p.sig_rows = (int)sig_rows;
+    p.sig_epoch = (unsigned)sig_epoch;
+  }
   c10::hip::HIPGuard guard(A.device().index());
   hipStream_t s = c10::hip::getCurrentHIPStream(A.device().index()).stream();
   at::Tensor ws = workspace_for(p, (int)kernel, A);
   int used = -1;
   hipError_t e = pdmb::gemm(p, (int)kernel, s, &used);
-  TORCH_CHECK(used >= 0, "pdmb: kernel ", kernel, " cannot run this problem");
+  TORCH_CHECK(used >= 0, "pdmb: kernel ", kernel, " cannot run this problem",
+              sig ? " signalled (W4 only)" : "");
   check_hip(e, "gemm launch");
   return C;
+}
+
+int64_t signal_create(int64_t device, int64_t slots) {
+  pdmb::Signal* s = nullptr;
+  check_hip(pdmb::signal_create((int)device, (int)slots, &s), "signal_create");
+  return (int64_t)(uintptr_t)s;
+}
+
+void signal_destroy(int64_t h) { pdmb::signal_destroy(as_signal(h)); }
+
+// Host wait (GIL released) until slot's flag reaches epoch; false on timeout.
+bool signal_wait(int64_t h, int64_t slot, int64_t epoch, double timeout_s) {
+  TORCH_CHECK(h != 0, "pdmb: null signal set");
+  py::gil_scoped_release nogil;
+  return pdmb::signal_wait(as_signal(h), (int)slot, (unsigned)epoch, timeout_s);
+}
+
+int64_t signal_flag(int64_t h, int64_t slot) {
+  TORCH_CHECK(h != 0 && slot >= 0 && slot < as_signal(h)->slots, "pdmb: bad signal slot");
+  return (int64_t)pdmb::signal_flag(as_signal(h), (int)slot);
+}
+
+// Tile rows per completion unit (0: the problem cannot run signalled).
+int64_t signal_granule(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t kernel,
+                       int64_t cus) {
+  pdmb::Problem p = make_problem(A, B, C);
+  p.cus = (int)cus;
+  return pdmb::signal_granule(p, (int)kernel);
 }
 
 int64_t resolve(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t kernel,
@@ -252,7 +292,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) native GEMM kernels and timing loop";
   m.def("matmul", &matmul, "C = A @ B on gfx950 MFMA (fp8: C = alpha * A @ B, bf16 out)",
         py::arg("A"), py::arg("B"), py::arg("out") = py::none(), py::arg("kernel") = 0,
-        py::arg("alpha") = 1.0, py::arg("splitk") = 0, py::arg("cus") = 0);
+        py::arg("alpha") = 1.0, py::arg("splitk") = 0, py::arg("cus") = 0, py::arg("sig") = 0,
+        py::arg("sig_rows") = 0, py::arg("sig_epoch") = 0);
+  m.def("signal_create", &signal_create, py::arg("device"), py::arg("slots"));
+  m.def("signal_destroy", &signal_destroy, py::arg("handle"));
+  m.def("signal_wait", &signal_wait, py::arg("handle"), py::arg("slot"), py::arg("epoch"),
+        py::arg("timeout_s"));
+  m.def("signal_flag", &signal_flag, py::arg("handle"), py::arg("slot"));
+  m.def("signal_granule", &signal_granule, py::arg("A"), py::arg("B"), py::arg("out"),
+        py::arg("kernel") = 0, py::arg("cus") = 0);
   m.def("resolve", &resolve, "kernel id that would run (or -1)", py::arg("A"), py::arg("B"),
         py::arg("out"), py::arg("kernel") = 0, py::arg("cus") = 0);
   m.def("resolve_padded", &resolve_padded, "kernel the padded fast path runs (or -1)",

@@ -100,7 +100,32 @@ struct GemmArgs {
   // zero at launch) and the grid (one workgroup per usable CU).
   unsigned* queue;
   int pers_grid;
+  // Completion signals (W4 only; sig == nullptr = off; parallel/overlap.py
+  // signalled pieces). Output tile rows are grouped into slots of sig_rows
+  // tile rows, sig_slots per batch element. A tile's C leaves write-through
+  // (sc1), every storing wave drains, then one lane adds 1 to the slot's
+  // device counter (relaxed, agent); the tile whose add completes the slot
+  // for this launch (counter == sig_epoch x tiles in the slot; counters are
+  // never reset, so launch e of one signal set completes at e x tiles) stores
+  // sig_epoch into the slot's host-mapped flag (system scope), which a host
+  // thread polls before issuing that piece's collective.
+  unsigned* sig;
+  unsigned* sig_host;
+  int sig_rows, sig_slots;
+  unsigned sig_epoch;
 };
+
+// Slot of output tile (bz, tm) and the counter value that completes it in
+// this launch (GemmArgs::sig).
+__device__ __forceinline__ void signal_tile(const GemmArgs& a, int bz, int tm) {
+  const int pr = tm / a.sig_rows;
+  const int slot = bz * a.sig_slots + pr;
+  const int rows = min(a.sig_rows, a.tiles_m - pr * a.sig_rows);
+  const unsigned target = a.sig_epoch * (unsigned)(rows * a.tiles_n);
+  const unsigned old = __hip_atomic_fetch_add(a.sig + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (old + 1u == target)
+    __hip_atomic_store(a.sig_host + slot, a.sig_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // ---- C epilogue through LDS (W4 bf16/fp16, W4 fp8) --------------------------
 // After the K-loop a wave holds 128 columns of 16-row blocks as C^T MFMA
@@ -132,7 +157,11 @@ constexpr int kEpiBuf = epi_buf<8>();  // one 16-row block of W4, 4224 B
 // the same way ("NTD"). Measured vs plain stores (profiles/
 // r2_ntstore_ab.jsonl): fp8 W4 4096^3 2538 -> 2760 TF, fp8 W4S 16k +0.6 %,
 // bf16 W4S 16384^2 x 2048 +1.1 %, 16k +0.2 %; never slower.
-template <int DT, bool MASK, bool SCALE, int NB = 8, bool NTS = true>
+// WT: write-through (sc1) buffer stores instead — a tile whose C another
+// kernel reads while this launch still runs (GemmArgs::sig): with every
+// storing wave drained, the bytes are in memory when the slot is signalled
+// (cdna_hip_programming.md Guideline 16 R1; no release fence).
+template <int DT, bool MASK, bool SCALE, int NB = 8, bool NTS = true, bool WT = false>
 __device__ __forceinline__ void store_block16(char* buf, const f32x4 (&v)[NB], float alpha, char* C,
                                               long long ldc_b, int row0, int col0, int M, int N,
                                               int lane) {
@@ -155,6 +184,23 @@ __device__ __forceinline__ void store_block16(char* buf, const f32x4 (&v)[NB], f
     *(lds_u32x2*)(lb + l16 * P + (j * 16 + 4 * g) * 2) = w;
   }
   const int rl = lane / CPR, ch = lane % CPR;
+  if constexpr (WT) {
+    // one descriptor per 16-row block (uniform base; offsets < 16 rows x ldc_b)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        C + (long long)row0 * ldc_b + (long long)col0 * 2, 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int r = 0; r < 16 / RPI; ++r) {
+      const u32x4 x = *(lds_u32x4_t*)(lb + (RPI * r + rl) * P + ch * 16);
+      const int row = row0 + RPI * r + rl, col = col0 + 8 * ch;
+      const int off = (RPI * r + rl) * (int)ldc_b + ch * 16;
+      if (!MASK || (row < M && col + 8 <= N)) {
+        __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 16 /* sc1 */);
+      } else if (row < M && col + 4 <= N) {
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{x.x, x.y}, rs, off, 0, 16);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int r = 0; r < 16 / RPI; ++r) {
     const u32x4 x = *(lds_u32x4_t*)(lb + (RPI * r + rl) * P + ch * 16);

@@ -6,7 +6,9 @@
 // allocator in the timed region, each launch writes a caller-owned output,
 // and the launches can be captured once into a hipGraph.
 #include <stdint.h>
+#include <string.h>
 
+#include <chrono>
 #include <mutex>
 #include <unordered_map>
 
@@ -51,6 +53,14 @@ static GemmArgs to_args(const Problem& p) {
   a.batch = p.batch < 1 ? 1 : p.batch;
   a.dbg = g_debug_buffer;
   a.alpha = p.alpha;
+  if (p.sig) {
+    a.sig = p.sig->dev;
+    a.sig_host = p.sig->host_dev;
+    a.sig_rows = p.sig_rows;
+    const int tm = (p.M + 255) / 256;
+    a.sig_slots = p.sig_rows > 0 ? (tm + p.sig_rows - 1) / p.sig_rows : 0;
+    a.sig_epoch = p.sig_epoch;
+  }
   return a;
 }
 
@@ -99,6 +109,7 @@ static int f32_split(const Problem& p);
 static bool w4s_fits(const Problem& p);
 static bool w4s_auto(const Problem& p);
 static bool supports(const Problem& p, int kernel);
+static int signal_kernel(const Problem& p, int kernel);
 
 struct Plan {
   int kernel;  // kMfmaW4 | kT128 | -1
@@ -356,7 +367,7 @@ struct TailPlan {
 
 static TailPlan tail_plan(const Problem& p, int kernel) {
   TailPlan best;
-  if (kernel != kAuto || p.splitk != 0 || p.cus > 0) return best;
+  if (kernel != kAuto || p.splitk != 0 || p.cus > 0 || p.sig) return best;
   if ((p.dtype != kBF16 && p.dtype != kF16) || p.M <= 256 || p.K <= 0) return best;
   if (resolve_kernel(p, kAuto) < 0 || !supports(p, kMfmaW4)) return best;
   const Plan whole = plan(p, kAuto);  // the best single launch (W4 or a smaller tile)
@@ -590,7 +601,7 @@ static hipError_t unpad_copy_launch(const void* src, long long lds, int rows, in
 }
 
 static bool wants_padding(const Problem& p, int kernel) {
-  if (p.dtype == kFP8) return false;
+  if (p.dtype == kFP8 || p.sig) return false;
   if (kernel != kAuto || p.M <= 0 || p.N <= 0 || p.K <= 0) return false;
   const double flops = 2.0 * p.M * (double)p.N * p.K * (p.batch < 1 ? 1 : p.batch);
   if (flops < kPadMinFlops) return false;
@@ -653,6 +664,10 @@ int resolve_padded(const Problem& p) {
 }
 
 size_t gemm_workspace_bytes(const Problem& p, int kernel) {
+  if (p.sig) {
+    const int k = signal_kernel(p, kernel);
+    return k < 0 ? 0 : splitk_bytes(p, kMfmaW4, plan(p, kMfmaW4).splitk);
+  }
   if (wants_padding(p, kernel)) {
     const Padded d = padded_problem(p, nullptr);
     const size_t copies = d.a_bytes + d.b_bytes + d.c_bytes;
@@ -739,7 +754,43 @@ static hipError_t gemm_padded(const Problem& p, hipStream_t stream, int* used) {
   return hipSuccess;
 }
 
+// The kernel a signalled launch runs: W4 where `kernel` resolves to W4 or
+// W4S (the persistent W4S leaves no CU to the consumers of the signals and
+// drains its stores a tile late), otherwise -1.
+static int signal_kernel(const Problem& p, int kernel) {
+  Problem q = p;
+  q.sig = nullptr;
+  const int k = resolve_kernel(q, kernel);
+  return (k == kMfmaW4 || k == kMfmaW4S) ? kMfmaW4 : -1;
+}
+
+int signal_granule(const Problem& p, int kernel) {
+  if (signal_kernel(p, kernel) < 0 || p.K <= 0) return 0;
+  const int tm = (p.M + 255) / 256, tn = (p.N + 255) / 256;
+  switch (choose_supertile(tm, tn)) {  // rows of one 256-tile round of map_tile's order
+    case 1: return 16;
+    case 2: return 8;
+    case 3: return 32;
+    case 4: return 4;
+    case 5: return 64;
+    default: return 16 * ((256 + 16 * tn - 1) / (16 * tn));  // grouped: whole 16-row groups of a round
+  }
+}
+
+static hipError_t gemm_signalled(const Problem& p, int kernel, hipStream_t stream, int* used) {
+  const int k = signal_kernel(p, kernel);
+  if (used) *used = k;
+  if (k < 0 || p.dtype == kFP8) return hipErrorNotSupported;
+  if (p.sig_rows <= 0 || p.sig_epoch == 0 || !p.sig->dev || !p.sig->host_dev) return hipErrorInvalidValue;
+  const int tm = (p.M + 255) / 256;
+  const int slots = (tm + p.sig_rows - 1) / p.sig_rows * (p.batch < 1 ? 1 : p.batch);
+  if (slots > p.sig->slots) return hipErrorInvalidValue;
+  if (p.M == 0 || p.N == 0 || p.batch == 0 || p.K == 0) return hipErrorInvalidValue;
+  return tiled_launch(p, kMfmaW4, to_args(p), p.workspace, p.workspace_bytes, stream);
+}
+
 hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
+  if (p.sig) return gemm_signalled(p, kernel, stream, used);
   if (wants_padding(p, kernel)) return gemm_padded(p, stream, used);
   const int k = resolve_kernel(p, kernel);
   if (used) *used = k;
@@ -900,6 +951,60 @@ hipError_t bench_gemm(const Problem& p, int kernel, int iters, int warmup, bool 
   if (exec) hipGraphExecDestroy(exec);
   if (graph) hipGraphDestroy(graph);
   return e;
+}
+
+// ---- completion signals ------------------------------------------------------
+hipError_t signal_create(int device, int slots, Signal** out) {
+  *out = nullptr;
+  if (slots <= 0) return hipErrorInvalidValue;
+  int prev = 0;
+  hipError_t e = hipGetDevice(&prev);
+  if (e != hipSuccess) return e;
+  if ((e = hipSetDevice(device)) != hipSuccess) return e;
+  Signal* s = new Signal();
+  s->slots = slots;
+  s->device = device;
+  const size_t bytes = ((size_t)slots * sizeof(unsigned) + 255) / 256 * 256;
+  e = hipMalloc(&s->dev, bytes);
+  if (e == hipSuccess) e = hipMemset(s->dev, 0, bytes);
+  // fine-grained, host-mapped: the GPU's system-scope flag stores land in host memory
+  if (e == hipSuccess) e = hipHostMalloc(&s->host, bytes, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) {
+    memset(s->host, 0, bytes);
+    e = hipHostGetDevicePointer((void**)&s->host_dev, s->host, 0);
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess) {
+    signal_destroy(s);
+    return e;
+  }
+  *out = s;
+  return hipSuccess;
+}
+
+void signal_destroy(Signal* s) {
+  if (!s) return;
+  if (s->dev) (void)hipFree(s->dev);
+  if (s->host) (void)hipHostFree(s->host);
+  delete s;
+}
+
+unsigned signal_flag(const Signal* s, int slot) {
+  return __atomic_load_n((volatile unsigned*)s->host + slot, __ATOMIC_ACQUIRE);
+}
+
+bool signal_wait(const Signal* s, int slot, unsigned epoch, double timeout_s) {
+  if (!s || slot < 0 || slot >= s->slots) return false;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spin = 0;; ++spin) {
+    if ((int)(signal_flag(s, slot) - epoch) >= 0) return true;
+    if ((spin & 1023) == 1023) {
+      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (el > timeout_s) return false;
+    }
+    __builtin_ia32_pause();
+  }
 }
 
 // ---- comm proxy ------------------------------------------------------------

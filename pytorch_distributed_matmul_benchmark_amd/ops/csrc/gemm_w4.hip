@@ -221,7 +221,7 @@ __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, f32
 // LDS buffer past the two stages while block row mi's 16 MFMAs run (same
 // per-accumulator MFMA order as ktile: bitwise equal). No fragment reads,
 // DMAs or barrier.
-template <int DT>
+template <int DT, bool WT = false>
 __device__ __forceinline__ void ktile_last(f32x4 (&acc)[8][8], const Frag (&A)[8], const Frag& A7c,
                                            const Frag (&Bc)[8], char* ebuf, char* Cb, long long ldc_b,
                                            int row0, int col0, int M, int N) {
@@ -229,7 +229,7 @@ __device__ __forceinline__ void ktile_last(f32x4 (&acc)[8][8], const Frag (&A)[8
     unsigned all = ~0u;  // lane id formed here: the stores' addresses are not hoisted
     asm volatile("" : "+s"(all));
     const int eln = (int)__builtin_amdgcn_mbcnt_hi(all, __builtin_amdgcn_mbcnt_lo(all, 0u));
-    store_block16<DT, false, false>(ebuf, acc[i], 1.0f, Cb, ldc_b, row0 + i * 16, col0, M, N, eln);
+    store_block16<DT, false, false, 8, true, WT>(ebuf, acc[i], 1.0f, Cb, ldc_b, row0 + i * 16, col0, M, N, eln);
   };
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi) {
@@ -258,7 +258,9 @@ __device__ __forceinline__ void ktile_last(f32x4 (&acc)[8][8], const Frag (&A)[8
 // FUSED (needs 4 kEpiBuf of LDS past the stages): an unsplit tile with an
 // even K-tile count stores C during its last K-tile (ktile_last); its
 // fragments are then in (A7b, B1) — one register set, as in gemm_fp8.hip.
-template <int DT, int SUB, int IL, int TRACE, bool PERS, bool FUSED = false>
+// WT: C stores write-through (GemmArgs::sig). Returns the next ticket (PERS)
+// or whether this workgroup wrote C (1; 0: a split-K slice that did not).
+template <int DT, int SUB, int IL, int TRACE, bool PERS, bool FUSED = false, bool WT = false>
 __device__ __forceinline__ unsigned w4_tile(const GemmArgs& a, char* smem, int vb, unsigned* qpre) {
   TileTrace tr;
   if constexpr (TRACE) tr.t[0] = tile_clock();
@@ -389,10 +391,11 @@ __device__ __forceinline__ unsigned w4_tile(const GemmArgs& a, char* smem, int v
   if (t < nloop) ktile<DT, IL, 0>(c, smem, t, acc, A, A7a, A7b, B0, B1);  // odd count
   if constexpr (kFuse) {
     if (fuse) {
-      ktile_last<DT>(acc, A, A7b, B1, smem + 2 * STAGE + wu * kEpiBuf, (char*)a.C + (long long)bz * a.sC * 2,
-                     (long long)a.ldc * 2, m0 + wr * 128, n0 + wc * 128, a.M, a.N);
+      ktile_last<DT, WT>(acc, A, A7b, B1, smem + 2 * STAGE + wu * kEpiBuf,
+                         (char*)a.C + (long long)bz * a.sC * 2, (long long)a.ldc * 2, m0 + wr * 128,
+                         n0 + wc * 128, a.M, a.N);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail DMAs landed before the LDS is released
-      return pre;
+      return PERS ? pre : 1u;
     }
   }
   // Drain the tail DMAs and give the last MFMAs time to write their AGPRs
@@ -406,7 +409,7 @@ __device__ __forceinline__ unsigned w4_tile(const GemmArgs& a, char* smem, int v
   SplitSlots sl;
   if (split && !splitk_meet<8, 8, NT>(a, smem, ((long long)bz * a.tiles_m + tm) * a.tiles_n + tn,
                                       slice, acc, sl))
-    return pre;
+    return PERS ? pre : 0u;
 
   // Epilogue: acc[i][j] holds C^T of a 16x16 tile (lane: row l16, columns
   // 4g..4g+3), stored through LDS as whole rows (common.h store_block16;
@@ -425,26 +428,44 @@ __device__ __forceinline__ unsigned w4_tile(const GemmArgs& a, char* smem, int v
       splitk_row<8, 8, NT>(a, sl, slice, i, acc, v);
     }
     if (interior)
-      store_block16<DT, false, false>(ebuf + (i & 1) * kEpiBuf, v, 1.0f, Cb, (long long)a.ldc * 2,
-                                      m0 + wr * 128 + i * 16, n0 + wc * 128, a.M, a.N, lane);
+      store_block16<DT, false, false, 8, true, WT>(ebuf + (i & 1) * kEpiBuf, v, 1.0f, Cb,
+                                                   (long long)a.ldc * 2, m0 + wr * 128 + i * 16,
+                                                   n0 + wc * 128, a.M, a.N, lane);
     else
-      store_block16<DT, true, false>(ebuf + (i & 1) * kEpiBuf, v, 1.0f, Cb, (long long)a.ldc * 2,
-                                     m0 + wr * 128 + i * 16, n0 + wc * 128, a.M, a.N, lane);
+      store_block16<DT, true, false, 8, true, WT>(ebuf + (i & 1) * kEpiBuf, v, 1.0f, Cb,
+                                                  (long long)a.ldc * 2, m0 + wr * 128 + i * 16,
+                                                  n0 + wc * 128, a.M, a.N, lane);
   }
   if constexpr (TRACE) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     tr.t[3] = tile_clock();
     tile_trace_write(a, tr, vb, tm, tn);
   }
-  return pre;
+  return PERS ? pre : 1u;
 }
 
 // FUSED: see w4_tile (false: the A/B kernel kMfmaW4Unfused).
-template <int DT, int SUB = 0, int IL = 64, int TRACE = 0, bool FUSED = true>
+// SIG: completion signals (GemmArgs::sig, common.h signal_tile): the tile's C
+// goes out write-through, every wave drains it, the workgroup meets at a
+// barrier and one lane signals the tile's slot (Guideline 16 R1: sc1
+// payload, drained by every storing wave, one atomic add behind a barrier).
+template <int DT, int SUB = 0, int IL = 64, int TRACE = 0, bool FUSED = true, bool SIG = false>
 __global__ void __launch_bounds__(NT, 1) gemm_w4_nn(GemmArgs a) {
   constexpr bool kFused = FUSED && TRACE == 0;
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + (kFused ? 4 * kEpiBuf : 0)];
-  (void)w4_tile<DT, SUB, IL, TRACE, false, kFused>(a, smem, blockIdx.x, nullptr);
+  const unsigned wrote = w4_tile<DT, SUB, IL, TRACE, false, kFused, SIG>(a, smem, blockIdx.x, nullptr);
+  if constexpr (SIG) {
+    if (wrote) {  // uniform: a split-K slice that handed its sums on wrote nothing
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        int bz, tm, tn;
+        map_tile(a, blockIdx.x, bz, tm, tn, SUB);
+        if (a.splitk > 1) bz /= a.splitk;
+        signal_tile(a, bz, tm);
+      }
+    }
+  }
 }
 
 // Persistent W4: one workgroup per CU, tiles from per-XCD queues. The tile
@@ -929,6 +950,16 @@ hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
   }
 #endif
   if (sub != 0) return hipErrorInvalidValue;
+  if (a.sig) {  // completion signals (overlap schedules)
+    if (!a.sig_host || a.sig_rows <= 0 || a.sig_slots * a.sig_rows < a.tiles_m ||
+        (long long)a.ldc * 2 * 16 >= (1LL << 31))
+      return hipErrorInvalidValue;
+    if (dt == kBF16)
+      hipLaunchKernelGGL((kw4::gemm_w4_nn<kBF16, 0, 64, 0, true, true>), grid, block, 0, stream, a);
+    else
+      hipLaunchKernelGGL((kw4::gemm_w4_nn<kF16, 0, 64, 0, true, true>), grid, block, 0, stream, a);
+    return hipGetLastError();
+  }
   if (dt == kBF16)
     hipLaunchKernelGGL(kw4::gemm_w4_nn<kBF16>, grid, block, 0, stream, a);
   else

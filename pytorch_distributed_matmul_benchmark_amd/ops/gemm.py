@@ -1,12 +1,21 @@
 """GEMM entry points: ``matmul`` / ``bmm`` / ``bench_matmul``.
 
-GPU tensors run on the hand-written gfx950 MFMA kernels of ``ops/csrc``:
-``gemm_mfma256.hip`` (bf16/fp16) and ``gemm_f32_256.hip`` (exact fp32) for
-every shape whose K / N / alignment fit their LDS-DMA granule — larger
-problems that do not are zero-padded onto them by the C++ dispatch — and
-``gemm_generic.hip`` for the rest. CPU tensors use ``torch.matmul`` — the
-reference's own compute call (matmul_benchmark.py:46) — which is the
-BASELINE config #1 CPU path ("4k fp32 matmul, single process on CPU").
+GPU tensors run on the hand-written gfx950 MFMA kernels of ``ops/csrc``,
+chosen per problem by the C++ planner (gemm_dispatch.cpp): bf16/fp16 on
+``gemm_w4.hip`` (W4, and its persistent streaming form W4S on a device the
+GEMM has to itself), the ``gemm_tile.hip`` family (T128 / T256x128 /
+T128x2, split-K) for grids that under-fill the 256 CUs, SCHED 3 of
+``gemm_mfma256.hip`` for edge tiles the others do not take; exact fp32 on
+``gemm_f32_256.hip`` / ``gemm_f32_w4.hip``; fp8 e4m3 on ``gemm_fp8.hip`` and
+the fp8 tile family; ``gemm_generic.hip`` for anything else. Large problems
+whose K / N / alignment miss the LDS-DMA granule are zero-padded onto the
+fast kernels. CPU tensors use ``torch.matmul`` — the reference's own
+compute call (matmul_benchmark.py:46) — which is the BASELINE config #1 CPU
+path ("4k fp32 matmul, single process on CPU").
+
+``matmul(..., signal=(SignalSet, rows, epoch))`` runs W4 with per-piece
+completion signals: the overlap schedules (parallel/overlap.py) start each
+row piece's collective while the rest of the same launch still computes.
 
 Every call writes into a caller-provided (or freshly allocated) ``out``
 and is enqueued on the current HIP stream, so it composes with
@@ -158,12 +167,69 @@ def fp8_quantize(x: torch.Tensor, colmajor: bool = False):
     return (x8.transpose(-1, -2) if colmajor else x8), scale
 
 
+class SignalSet:
+    """Completion signals of one GEMM output (api.h ``Signal``): ``slots``
+    device tile counters plus host-mapped flags. Launch ``e`` (``next_epoch``)
+    of a signalled GEMM writes ``e`` into slot s's flag once every tile of
+    row piece s is stored (write-through, drained); ``wait`` blocks this host
+    thread (GIL released) until then."""
+
+    def __init__(self, device: torch.device, slots: int):
+        self._C = _native.load()
+        self.device = device
+        self.slots = int(slots)
+        self.handle = int(self._C.signal_create(device.index, self.slots))
+        self.epoch = 0
+
+    def next_epoch(self) -> int:
+        self.epoch += 1
+        return self.epoch
+
+    def flag(self, slot: int) -> int:
+        return int(self._C.signal_flag(self.handle, slot))
+
+    def wait(self, slot: int, epoch: int, timeout_s: float = 120.0) -> None:
+        if not self._C.signal_wait(self.handle, int(slot), int(epoch), float(timeout_s)):
+            raise TimeoutError(f"GEMM completion signal: slot {slot} did not reach epoch {epoch} "
+                               f"within {timeout_s:.0f} s (flag {self.flag(slot)})")
+
+    def close(self) -> None:
+        if self.handle:
+            torch.cuda.synchronize(self.device)
+            self._C.signal_destroy(self.handle)
+            self.handle = 0
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def signal_granule(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
+                   kernel="auto") -> int:
+    """256-row tile rows of one completion unit of a signalled ``matmul`` (one
+    256-workgroup round of W4's tile order); 0 if the problem cannot run
+    signalled (not W4, fp8, CPU)."""
+    if A.device.type != "cuda" or A.dtype not in (torch.bfloat16, torch.float16):
+        return 0
+    C = _native.load()
+    if out is None:
+        out = torch.empty(_out_shape(A, B), dtype=out_dtype(A.dtype), device=A.device)
+    A, B = _prep_pair(A, B)
+    return int(C.signal_granule(A, B, out, _kid(kernel), _cus()))
+
+
 def matmul(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
-           kernel="auto", alpha: float = 1.0, splitk: int = 0) -> torch.Tensor:
+           kernel="auto", alpha: float = 1.0, splitk: int = 0, signal=None) -> torch.Tensor:
     """``out = A @ B`` for 2-D/3-D row-major operands (3-D = batched).
 
     ``splitk`` (W4 / T128 only): K slices per output tile, 0 = auto (split only
     grids that under-fill the 256 CUs, ``splitk_for``), 1 = never.
+
+    ``signal=(SignalSet, rows, epoch)``: run W4 with completion signals, one
+    slot per ``rows`` 256-row tile rows (per batch element); raises if the
+    problem does not run on W4 (``signal_granule`` == 0).
 
     float8_e4m3fn operands: ``out = alpha * (A @ B)`` in bfloat16 on the
     block-scaled fp8 MFMA (B is used column-major; a row-major B is copied).
@@ -193,7 +259,12 @@ def matmul(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
     if out is None:
         out = torch.empty(_out_shape(A, B), dtype=out_dtype(A.dtype), device=A.device)
     # auto: odd K/N/alignment padded onto the fast path (C++; not for fp8)
-    C.matmul(A, B, out, _kid(kernel), float(alpha), int(splitk), _cus())
+    if signal is not None:
+        sig, rows, epoch = signal
+        C.matmul(A, B, out, _kid(kernel), float(alpha), int(splitk), _cus(), sig.handle, int(rows),
+                 int(epoch))
+    else:
+        C.matmul(A, B, out, _kid(kernel), float(alpha), int(splitk), _cus())
     return out
 
 

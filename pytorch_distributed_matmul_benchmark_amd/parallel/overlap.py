@@ -1,56 +1,209 @@
-"""Overlap schedules shared by ``bench.py`` and ``models/``: chunked GEMM on a
-(possibly CU-masked) compute stream, collective pieces on the comm stream.
+"""Overlap schedules shared by ``bench.py`` and ``models/``: whole GEMMs on the
+compute stream, their collectives on the comm stream, pipelined across units
+through a ring of output buffers — and, within a unit, started piece by piece
+as the SAME GEMM launch's tiles finish.
 
 Reference: backup/matmul_overlap_benchmark.py:93-180 (two streams, double
-buffer, the collective issued with no dependency on its producer — SURVEY Q7)
-and matmul_scaling_benchmark.py:167-238 (matrix_parallel, serialized). Here:
+buffer: the all-reduce of buffer i runs while buffer i±1 computes; the
+collective is issued with no dependency on its producer — SURVEY Q7) and
+matmul_scaling_benchmark.py:106-238 (batch_parallel / matrix_parallel,
+serialized). Here (``OverlapPipeline``):
 
-* ``gemm_chunks`` — how many row chunks the GEMM is cut into. A chunk is
-  worth having only if its GEMM still fills the chip: with W4 split-K
-  (gemm_w4.hip) a chunk of >= 64 256x256 tiles does (S = 4 slices), so the
-  8k ws=8 shard (128 tiles) now overlaps in 2 chunks instead of running
-  serialized (round 1 required >= 256 tiles per chunk).
-* ``GatherOverlap`` — matrix_parallel: GEMM chunk j, then its rows are
-  all-gathered in ``pieces`` calls (independent of the GEMM chunking; RCCL's
-  all_gather_into_tensor or the direct P2P all-gather, ``impl``),
-  each on the comm stream after an event recorded behind chunk j; the step
-  ends with the compute stream waiting for every piece (the timed region
-  includes the last collective).
-* ``ReduceOverlap`` — batch_parallel: (batch element, row chunk) units, each
-  all-reduced behind its GEMM.
-* ``compute_stream(device, comm_cus)`` — a HIP stream whose kernels may not
-  use ``comm_cus`` CUs (hipExtStreamCreateWithCUMask, spread evenly over the
-  8 XCDs), so RCCL's workgroups start on those CUs at once instead of waiting
-  for a 1-workgroup-per-CU GEMM wave to retire.
+* **No chunked GEMM.** Round 2 cut the GEMM into row-chunk launches so a
+  chunk's collective could start early; at the ws = 8 shard the 4-chunk GEMM
+  ran 977 TF against 1560 unchunked and the overlap lost to serializing
+  (profiles/r2_cu_mask_overlap_v2.jsonl). Every unit is now ONE launch of
+  the best kernel for the whole problem.
+* **Ring of outputs (cross-unit pipelining).** Unit k writes ring buffer
+  k % R; its collective runs on the comm stream while unit k+1 computes, and
+  unit k+R waits only for unit k's collective (write-after-read), never for
+  the most recent one: only the last unit of a timed region is exposed.
+  batch_parallel with >= 2 local batch elements rings over its own C[b];
+  with one element, and for matrix_parallel, R = 2 (the reference's C1/C2).
+* **Signalled pieces (within a unit).** With ``pieces`` > 1 the unit's GEMM
+  is the W4 kernel with completion signals (ops/csrc gemm_w4.hip SIG,
+  common.h signal_tile): each tile's C leaves write-through, and the tile
+  that completes a row piece writes the launch's epoch into that piece's
+  host-mapped flag. The host thread — which has already enqueued the next
+  unit's GEMM — waits for piece p's flag and issues piece p's collective at
+  once, so communication starts while the same launch still computes, with
+  no chunk launches, no CU set aside for a polling kernel and no GPU-side
+  wait a shared hardware queue could deadlock.
+* ``plan_overlap`` prices serial vs overlapped (P pieces) from a GEMM model
+  and an xGMI bus-bandwidth model of the collective and refuses plans that
+  lose (``OverlapPlan.overlap`` False: the mode runs serialized).
+* ``compute_stream(device, comm_cus)`` — optionally a HIP stream whose
+  kernels may not use ``comm_cus`` CUs (hipExtStreamCreateWithCUMask, spread
+  evenly over the 8 XCDs), so RCCL's workgroups start on those CUs at once.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence, Tuple
+import os
+from dataclasses import asdict, dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 
 from .comm import CommStream, new_event, stream_ctx
-from .partition import ceil_div, effective_chunks, row_chunks
-
-# 256x256 output tiles a GEMM chunk needs to fill the chip (ops/gemm.py
-# min_chunk_tiles): 64 for the split-K W4 kernel (bf16/fp16), a full wave of
-# 256 for the others.
-_SPLITK_MIN_TILES = 64
+from .partition import ceil_div
 
 
-def min_chunk_tiles(dtype: torch.dtype, device: torch.device) -> int:
-    if device.type != "cuda":
-        return 1
-    return _SPLITK_MIN_TILES if dtype in (torch.bfloat16, torch.float16) else 256
+# ---- the planner -------------------------------------------------------------
+# GEMM rate (TFLOPS) of a full grid per dtype on one MI355X, measured
+# (README.md headline table: W4 / W4S 16k bf16 1526, fp16 ~ bf16, exact
+# fp32 152, fp8 3300); an under-filled grid runs at the fraction of the
+# 256 CUs its 256x256 tiles fill (split-K recovers part: floor 0.6).
+GEMM_TFLOPS = {torch.bfloat16: 1500.0, torch.float16: 1500.0, torch.float32: 150.0,
+               torch.float8_e4m3fn: 3200.0}
+# RCCL bus bandwidth (GB/s) by world size on a fully connected 8 x MI355X
+# xGMI node (7 links per GPU, ~153 GB/s each; one link between any pair),
+# the busBW convention of rccl-tests: t = bytes x factor / busbw with factor
+# (ws-1)/ws for all-gather (bytes = gathered total) and 2(ws-1)/ws for
+# all-reduce. Defaults are conservative estimates, NOT measured here (no
+# multi-GPU node in this build's reach); override with
+# PDMB_BUSBW_GBPS="2:80,4:200,8:320" once measured.
+DEFAULT_BUSBW_GBPS = {2: 70.0, 4: 180.0, 8: 300.0}
+COLLECTIVE_LAT_US = 30.0   # per collective call: host issue + RCCL launch + handshake
+PIECE_HOST_US = 15.0       # per signalled piece: host flag latency + issue
+RCCL_CU_SHARE = 0.125      # GEMM slowdown while a collective runs beside it (~32 of 256 CUs)
 
 
-def gemm_chunks(m: int, n: int, requested: int, dtype: torch.dtype,
-                device: torch.device) -> List[Tuple[int, int]]:
-    """Row chunks [start, stop) of an [m, n] GEMM output for an overlap schedule."""
-    if device.type != "cuda":
-        return row_chunks(m, requested)
-    return row_chunks(m, effective_chunks(m, n, requested,
-                                          min_tiles=min_chunk_tiles(dtype, device)))
+def busbw_gbps(ws: int) -> float:
+    env = os.environ.get("PDMB_BUSBW_GBPS", "")
+    table = dict(DEFAULT_BUSBW_GBPS)
+    for item in filter(None, (x.strip() for x in env.split(","))):
+        k, v = item.split(":")
+        table[int(k)] = float(v)
+    if ws in table:
+        return table[ws]
+    ks = sorted(table)
+    lo = max([k for k in ks if k <= ws], default=ks[0])
+    return table[lo]
+
+
+def gemm_us(m: int, n: int, k: int, dtype: torch.dtype, batch: int = 1) -> float:
+    """Model time of one [m, k] @ [k, n] GEMM (x batch) on one MI355X."""
+    tiles = ceil_div(max(m, 1), 256) * ceil_div(max(n, 1), 256) * max(batch, 1)
+    waves = ceil_div(tiles, 256)
+    fill = max(tiles / (waves * 256.0), 0.6)
+    return 2.0 * m * n * k * max(batch, 1) / (GEMM_TFLOPS.get(dtype, 1500.0) * 1e6 * fill)
+
+
+def collective_us(kind: str, payload_bytes: float, ws: int) -> float:
+    """Model time of ONE collective on ``payload_bytes`` per rank (all_reduce:
+    the reduced tensor; all_gather: this rank's contribution)."""
+    if ws <= 1:
+        return 0.0
+    bw = busbw_gbps(ws) * 1e3  # bytes per us
+    if kind == "all_reduce":
+        moved = 2.0 * (ws - 1) / ws * payload_bytes
+    elif kind == "all_gather":
+        moved = (ws - 1) * payload_bytes  # (ws-1)/ws of the gathered total
+    else:
+        raise ValueError(kind)
+    return moved / bw + COLLECTIVE_LAT_US
+
+
+@dataclass
+class OverlapPlan:
+    overlap: bool          # False: serialize (the overlap loses or cannot help)
+    pieces: int            # collective pieces per unit (1: behind the whole GEMM)
+    rows: int              # 256-row tile rows per piece (signal slot; 0 if pieces == 1)
+    gemm_us: float
+    comm_us: float
+    serial_us: float       # predicted per unit, serialized
+    overlap_us: float      # predicted per unit, overlapped with the chosen pieces
+    candidates: Dict[int, float] = field(default_factory=dict)
+    reason: str = ""
+
+    def as_dict(self) -> dict:
+        d = asdict(self)
+        d["candidates"] = {str(k): round(v, 1) for k, v in self.candidates.items()}
+        for k in ("gemm_us", "comm_us", "serial_us", "overlap_us"):
+            d[k] = round(d[k], 1)
+        return d
+
+
+def plan_overlap(m: int, n: int, k: int, dtype: torch.dtype, ws: int, kind: str,
+                 payload_bytes: float, granule: int = 0, steps: int = 10,
+                 requested: int = 0, gemm_time_us: Optional[float] = None,
+                 comm_time_us: Optional[float] = None,
+                 piece_us: float = COLLECTIVE_LAT_US + PIECE_HOST_US) -> OverlapPlan:
+    """Choose how a unit (one [m, k] @ [k, n] GEMM whose output's collective
+    follows) overlaps: serialize, pipeline whole collectives across units
+    (pieces = 1), or start P row pieces as the GEMM's tiles finish (P > 1,
+    needs ``granule`` > 0: tile rows of one completion unit; P <= the number
+    of such units). Per unit, over a timed region of ``steps`` units:
+
+        serial      = G + C
+        overlap(P)  = max(G', C') + min(G', C') / P / steps
+        G'          = G + RCCL_CU_SHARE * min(G, C')
+        C'          = C + (P - 1) * piece_us   (per extra collective call)
+
+    (the steady state is the slower of the two streams; what is exposed once
+    per timed region is the faster stream's first / last piece).
+
+    ``requested`` > 0 is an explicit request: P = ``requested`` (clamped to
+    what the granule allows), overlapped even where the model predicts a
+    loss; 0 lets the planner choose, and it refuses an overlap that does not
+    beat serial by 3 %. ``gemm_time_us`` / ``comm_time_us`` replace the
+    models (measured values, e.g. the 1-GPU proxy sweep)."""
+    G = gemm_time_us if gemm_time_us is not None else gemm_us(m, n, k, dtype)
+    C = comm_time_us if comm_time_us is not None else collective_us(kind, payload_bytes, ws)
+    serial = G + C
+    tm = ceil_div(max(m, 1), 256)
+    units = tm // granule if granule > 0 else 1
+    choices = [p for p in (1, 2, 4, 8) if p == 1 or (granule > 0 and p <= units)]
+    if requested > 0:
+        allowed = [p for p in choices if p <= requested]
+        choices = [max(allowed)] if allowed else [1]
+
+    def cost(P: int) -> float:
+        Cp = C + (P - 1) * piece_us
+        Gp = G + RCCL_CU_SHARE * min(G, Cp)
+        return max(Gp, Cp) + min(Gp, Cp) / P / max(steps, 1)
+
+    cands = {P: cost(P) for P in choices}
+    best = min(cands, key=lambda P: (cands[P], P))
+    ov = cands[best]
+    if C <= 0.0:
+        return OverlapPlan(False, 1, 0, G, C, serial, serial, cands, "no collective (ws = 1)")
+    if ov >= serial * 0.97 and requested <= 0:
+        return OverlapPlan(False, 1, 0, G, C, serial, ov, cands,
+                           f"overlap predicted {ov:.0f} us vs serial {serial:.0f} us: serialize")
+    rows = 0
+    if best > 1:
+        rows = ceil_div(units, best) * granule
+    why = "requested" if requested > 0 else "planned"
+    return OverlapPlan(True, best, rows, G, C, serial, ov, cands,
+                       f"{why}: {best} piece(s), {ov:.0f} us vs serial {serial:.0f} us")
+
+
+def plan_for_units(units: Sequence[Tuple], ws: int, kind: str, payload_bytes: float,
+                   native: bool = True, requested: int = 0, steps: int = 10,
+                   owner=None) -> OverlapPlan:
+    """``plan_overlap`` for a ring of (A, B, out) units: the shapes of unit 0,
+    and the signal granule of its GEMM as the pipeline would issue it (beside
+    collectives: ``gemm.shared_device``, a masked stream's CU budget)."""
+    import contextlib
+
+    from ..ops import gemm
+
+    A, B, C = units[0]
+    granule = 0
+    if C.device.type == "cuda" and native and A.dtype in (torch.bfloat16, torch.float16):
+        with gemm.shared_device(), (owner.budget() if owner is not None else contextlib.nullcontext()):
+            granule = gemm.signal_granule(A, B, C)
+    return plan_overlap(C.shape[-2], C.shape[-1], A.shape[-1], A.dtype, ws, kind, payload_bytes,
+                        granule=granule, steps=steps, requested=requested)
+
+
+def piece_rows(m: int, rows: int) -> List[Tuple[int, int]]:
+    """Row ranges [start, stop) of the pieces: ``rows`` 256-row tile rows each."""
+    if rows <= 0:
+        return [(0, m)]
+    step = rows * 256
+    return [(s, min(m, s + step)) for s in range(0, m, step)]
 
 
 def _xcd_spread(ncu: int, k: int, nxcd: int = 8) -> List[int]:
@@ -129,65 +282,98 @@ def compute_stream(device: torch.device, comm_cus: int = 0):
     return ms.stream, ms
 
 
-class GatherOverlap:
-    """matrix_parallel overlap: C_local rows in GEMM chunks, each all-gathered in pieces."""
+class OverlapPipeline:
+    """The overlap schedule (module docstring): a ring of ``units`` — (A, B,
+    out) triples; unit k computes ``units[k % R]`` — whose outputs go through
+    ``collective(r, p, start, stop, after, done)`` piece by piece on the comm
+    stream. ``step()`` issues ``per_step`` units; ``finish()`` issues what is
+    still pending and joins the compute stream behind every collective (call
+    it before reading the outputs or stopping a timer).
 
-    def __init__(self, n_rows: int, shard: int, ws: int, device: torch.device,
-                 out_dtype: torch.dtype, chunks: Sequence[Tuple[int, int]], pieces: int = 0,
-                 requested: int = 4, comm: Optional[CommStream] = None, impl: str = "rccl"):
-        if impl not in ("rccl", "direct"):
-            raise ValueError(f"all-gather impl {impl!r}: rccl | direct")
-        self.impl = impl
-        self.chunks = list(chunks)
-        per = pieces if pieces > 0 else max(1, ceil_div(max(requested, 1), len(self.chunks)))
-        self.pieces = []
-        for s, e in self.chunks:
-            self.pieces.append([(s + ps, s + pe) for ps, pe in row_chunks(e - s, per, align=8)])
-        self.bufs = [[torch.empty((ws * (pe - ps), shard), device=device, dtype=out_dtype)
-                      for ps, pe in pcs] for pcs in self.pieces]
-        self.ready = [new_event(device) for _ in self.chunks]
-        self.done = [[new_event(device) for _ in pcs] for pcs in self.pieces]
+    ``collective`` must enqueue the collective of rows [start, stop) of ring
+    slot r's output on the comm stream after event ``after`` (None: the rows
+    are known complete) and record ``done`` behind it (CommStream's
+    all_reduce / all_gather_into accept exactly these)."""
+
+    def __init__(self, mm: Callable, units: Sequence[Tuple], collective: Callable,
+                 device: torch.device, plan: OverlapPlan, per_step: int = 1,
+                 compute=None, owner=None, comm: Optional[CommStream] = None,
+                 timeout_s: float = 120.0):
+        from ..ops import gemm
+
+        self.mm, self.units, self.collective = mm, list(units), collective
+        self.R = len(self.units)
+        if self.R < 2:
+            raise ValueError("OverlapPipeline needs a ring of >= 2 output buffers")
+        self.device, self.plan, self.per_step = device, plan, max(1, int(per_step))
+        self.compute, self.owner = compute, owner
         self.cs = comm or CommStream(device)
-        self.device = device
+        self.timeout_s = timeout_s
+        m = self.units[0][2].shape[-2]
+        self.signalled = device.type == "cuda" and plan.pieces > 1 and plan.rows > 0
+        self.pieces = piece_rows(m, plan.rows if self.signalled else 0)
+        self.sigs = ([gemm.SignalSet(device, len(self.pieces)) for _ in range(self.R)]
+                     if self.signalled else None)
+        self.ready = [new_event(device) for _ in range(self.R)]
+        self.done = [new_event(device) for _ in range(self.R)]
+        self.used = [False] * self.R
+        self.k = 0
+        self.pending: Optional[Tuple[int, int]] = None  # (ring slot, epoch) awaiting its pieces
 
-    @property
-    def n_pieces(self) -> int:
-        return sum(len(p) for p in self.pieces)
+    def _gemm(self, r: int) -> Optional[int]:
+        from ..ops import gemm
 
-    def step(self, mm, A, B_local, C_local, compute) -> None:
-        for j, (s, e) in enumerate(self.chunks):
-            mm(A[s:e], B_local, C_local[s:e])
-            self.ready[j].record(compute)
-            gather = self.cs.all_gather_direct if self.impl == "direct" else self.cs.all_gather_into
-            for p, (ps, pe) in enumerate(self.pieces[j]):
-                gather(self.bufs[j][p], C_local[ps:pe], after=self.ready[j] if p == 0 else None,
-                       done=self.done[j][p])
-        if compute is not None:
-            for dj in self.done:
-                compute.wait_event(dj[-1])  # comm stream is in order: last piece => all
+        A, B, out = self.units[r]
+        with compute_ctx(self.compute, self.owner):
+            cur = self.compute if self.compute is not None else None
+            if self.used[r] and cur is not None:
+                cur.wait_event(self.done[r])  # WAR: the buffer's last collective is done
+            if self.signalled:
+                epoch = self.sigs[r].next_epoch()
+                gemm.matmul(A, B, out=out, signal=(self.sigs[r], self.plan.rows, epoch))
+            else:
+                epoch = None
+                self.mm(A, B, out)
+            self.ready[r].record(cur)
+        return epoch
 
-    def gathered(self) -> List[torch.Tensor]:
-        """Gather buffers in row order (models.matrix_parallel.assemble)."""
-        return [b for bj in self.bufs for b in bj]
+    def _issue(self, r: int, epoch: Optional[int]) -> None:
+        last = len(self.pieces) - 1
+        for p, (s, e) in enumerate(self.pieces):
+            if epoch is not None:
+                self.sigs[r].wait(p, epoch, self.timeout_s)  # rows [s, e) are stored
+                after = None
+            else:
+                after = self.ready[r]
+            self.collective(r, p, s, e, after, self.done[r] if p == last else None)
+        self.used[r] = True
 
+    def step(self) -> None:
+        for _ in range(self.per_step):
+            r = self.k % self.R
+            self.k += 1
+            epoch = self._gemm(r)
+            if self.signalled:
+                # the next GEMM is queued before this host thread blocks on the
+                # previous unit's pieces, so the compute stream never runs dry
+                if self.pending is not None:
+                    self._issue(*self.pending)
+                self.pending = (r, epoch)
+            else:
+                self._issue(r, None)
 
-class ReduceOverlap:
-    """batch_parallel overlap: per (batch element, row chunk) GEMM, then all-reduce."""
+    def finish(self) -> None:
+        if self.pending is not None:
+            self._issue(*self.pending)
+            self.pending = None
+        if self.compute is not None:
+            for r in range(self.R):
+                if self.used[r]:
+                    self.compute.wait_event(self.done[r])
 
-    def __init__(self, local_batch: int, chunks: Sequence[Tuple[int, int]],
-                 device: torch.device, comm: Optional[CommStream] = None):
-        self.units = [(b, s, e) for b in range(local_batch) for (s, e) in chunks]
-        self.ready = [new_event(device) for _ in self.units]
-        self.done = [new_event(device) for _ in self.units]
-        self.cs = comm or CommStream(device)
-
-    def step(self, mm, A, B, C, compute) -> None:
-        for u, (b, s, e) in enumerate(self.units):
-            mm(A[b, s:e], B[b], C[b, s:e])
-            self.ready[u].record(compute)
-            self.cs.all_reduce(C[b, s:e], after=self.ready[u], done=self.done[u])
-        if compute is not None and self.done:
-            compute.wait_event(self.done[-1])
+    def close(self) -> None:
+        for s in self.sigs or []:
+            s.close()
 
 
 class BidirRing:

@@ -86,9 +86,10 @@ def build_parser(kind: str) -> argparse.ArgumentParser:
                    help="batch_parallel global batch (rounded up to a multiple of the world size)")
     g.add_argument("--overlap", action="store_true",
                    help="batch/matrix_parallel: overlap the collective with the GEMM on a second stream")
-    g.add_argument("--chunks", type=int, default=4, help="overlap granularity (row chunks per GEMM)")
-    g.add_argument("--comm-chunks", type=int, default=0,
-                   help="matrix_parallel --overlap: all-gather pieces per GEMM chunk (0: auto)")
+    g.add_argument("--chunks", type=int, default=0,
+                   help="--overlap: collective pieces per GEMM, each started by the GEMM's own "
+                        "tile-completion signals (0: the overlap planner's choice; 1: whole "
+                        "collectives pipelined across GEMMs)")
     g.add_argument("--allgather", default="rccl", choices=["rccl", "direct"],
                    help="matrix_parallel all-gather: RCCL's all_gather_into_tensor, or direct: one "
                         "batched P2P group sending this rank's shard to every peer at once (each "
@@ -131,7 +132,7 @@ def _mode_of(kind: str, args) -> str:
 def _workload(args, n: int, dtype: torch.dtype) -> Workload:
     return Workload(n=n, dtype=dtype, iters=args.iterations, warmup=args.warmup, seed=args.seed,
                     backend=args.backend, kernel=args.kernel, batch=args.batch,
-                    overlap=args.overlap, chunks=args.chunks, comm_chunks=args.comm_chunks,
+                    overlap=args.overlap, chunks=args.chunks,
                     comm_cus=args.comm_cus, allgather=args.allgather, graph=args.graph,
                     check=args.check,
                     min_warmup_ms=args.min_warmup_ms)
@@ -384,8 +385,8 @@ def run_benchmarks(kind: str, ctx: DistContext, rep: Reporter, args) -> List[Dic
 def main(kind: str, argv=None) -> int:
     parser = build_parser(kind)
     args = parser.parse_args(argv)
-    if args.iterations < 1 or args.warmup < 0 or args.chunks < 1 or args.batch < 1:
-        parser.error("--iterations and --chunks must be >= 1, --batch >= 1, --warmup >= 0")
+    if args.iterations < 1 or args.warmup < 0 or args.chunks < 0 or args.batch < 1:
+        parser.error("--iterations must be >= 1, --batch >= 1, --warmup and --chunks >= 0")
     ctx = setup_distributed(args.device, timeout_s=args.timeout,
                             backend=None if args.dist_backend == "auto" else args.dist_backend)
     rep = Reporter(is_main=ctx.is_main, json_path=args.json)

@@ -1,0 +1,62 @@
+#!/bin/bash
+# One GPU session on the box: named stages, each under its own time limit, chained so
+# that the first failure (or fault / time limit) ends the session. Output per stage in
+# gpurun_out/<tag>/<stage>.log (JSON results next to it); docs/REPRODUCE.md lists the
+# sessions whose results are committed under profiles/.
+#
+#   scripts/gpu_session.sh TAG STAGE [STAGE ...] [-- NAME SECONDS COMMAND...]
+#
+# Stages: tests (whole GPU suite), tests_signal (signals + overlap), smoke, bench
+# (driver form), bench_quick, overlap_proxy, rocprof_bench, selflaunch2, selflaunch4,
+# gpus2_refused (bench.py --gpus 2 on a 1-GPU box must exit 2 at once), ab_bf16,
+# ab_fp32, ab_fp8. After "--": one ad-hoc step NAME with a SECONDS limit.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${1:?tag}; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+step() {  # step NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  tail -6 "$OUT/$name.log"
+  echo "== $name rc=$rc"
+  return $rc
+}
+PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+run_stage() {
+  case "$1" in
+    tests) step tests 1500 $PYT tests -m gpu ;;
+    tests_signal) step tests_signal 600 $PYT tests/test_signal_gpu.py tests/test_overlap_gpu.py -m gpu ;;
+    smoke) step smoke 180 python __graft_entry__.py smoke ;;
+    bench) step bench 400 python bench.py && grep '^{' "$OUT/bench.log" > "$OUT/bench.json" ;;
+    bench_quick) step bench_quick 400 python bench.py --steps 10 --warmup 3 --extra-steps 5 &&
+                 grep '^{' "$OUT/bench_quick.log" > "$OUT/bench_quick.json" ;;
+    overlap_proxy) step overlap_proxy 900 python scripts/overlap_proxy.py &&
+                   grep '^{' "$OUT/overlap_proxy.log" > "$OUT/overlap_proxy.jsonl" ;;
+    rocprof_bench) step rocprof_bench 400 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof" -o bench -- \
+                     python3 bench.py --steps 20 --warmup 5 ;;
+    selflaunch2) step selflaunch2 400 python bench.py --gpus 2 --dist-backend gloo --size 4096 --steps 3 \
+                   --warmup 1 --extra-steps 2 --extra-warmup 1 ;;
+    selflaunch4) step selflaunch4 400 python bench.py --gpus 4 --dist-backend gloo --size 4096 --steps 3 \
+                   --warmup 1 --extra-steps 2 --extra-warmup 1 ;;
+    gpus2_refused) echo "== gpus2_refused"; timeout -k 10 120 python bench.py --gpus 2 > "$OUT/gpus2_refused.log" 2>&1
+                   local rc=$?; cat "$OUT/gpus2_refused.log"; echo "== gpus2_refused rc=$rc (want 2)"; [ $rc -eq 2 ] ;;
+    ab_bf16) step ab_bf16 600 python scripts/ab_kernels.py --dtype bfloat16 ;;
+    ab_fp32) step ab_fp32 600 python scripts/ab_kernels.py --dtype float32 ;;
+    ab_fp8) step ab_fp8 600 python scripts/ab_kernels.py --dtype float8_e4m3fn ;;
+    *) echo "unknown stage $1"; return 2 ;;
+  esac
+}
+while [ $# -gt 0 ]; do
+  if [ "$1" = "--" ]; then
+    shift
+    step "$@" || exit $?
+    break
+  fi
+  run_stage "$1" || exit $?
+  shift
+done
+echo "== session $TAG done"

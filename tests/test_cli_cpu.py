@@ -193,7 +193,7 @@ def test_fp8_cli_cpu_and_gloo(tmp_path):
         assert out.count("PASS") == 1 and "FAIL" not in out and "ERROR" not in out
 
 
-@pytest.mark.parametrize("ws,extra", [(2, []), (3, ["--overlap", "--chunks", "2", "--comm-chunks", "2"]),
+@pytest.mark.parametrize("ws,extra", [(2, []), (3, ["--overlap", "--chunks", "2"]),
                                       (4, ["--overlap", "--chunks", "3"])])
 def test_matrix_parallel_direct_allgather(ws, extra):
     """--allgather direct: the shard goes to every peer in one batched P2P group

@@ -68,14 +68,16 @@ def test_two_ranks_share_gpu_bench_ring():
 
 
 @pytest.mark.parametrize("mode,extra", [
-    ("matrix_parallel", ["--overlap", "--chunks", "4", "--comm-chunks", "3", "--comm-cus", "16"]),
+    ("matrix_parallel", ["--overlap", "--chunks", "4", "--comm-cus", "16"]),
     ("batch_parallel", ["--overlap", "--chunks", "2", "--comm-cus", "32"]),
-    ("matrix_parallel", ["--overlap", "--chunks", "1", "--comm-chunks", "4"]),
+    ("matrix_parallel", ["--overlap", "--chunks", "1"]),
+    ("batch_parallel", ["--overlap", "--chunks", "4", "--batch", "2"]),
     ("matrix_parallel", ["--allgather", "direct"]),
-    ("matrix_parallel", ["--allgather", "direct", "--overlap", "--chunks", "2", "--comm-chunks", "2"])])
+    ("matrix_parallel", ["--allgather", "direct", "--overlap", "--chunks", "2"])])
 def test_two_ranks_cu_masked_overlap_checked(mode, extra):
-    """GEMM chunks on a CU-masked stream, collectives in pieces decoupled from the
-    GEMM chunking: the float64 Σ-over-ranks / gathered-C checks still pass."""
+    """The overlap pipeline (ring of outputs; signalled pieces where --chunks > 1
+    and the GEMM is W4), optionally on a CU-masked stream: the float64
+    Σ-over-ranks / gathered-C checks still pass."""
     out = _run(2, "matmul_scaling_benchmark.py", "--sizes", "2048", "--iterations", "3",
                "--warmup", "1", "--mode", mode, "--check", *extra)
     assert "PASS" in out and "FAIL" not in out and "ERROR" not in out
