@@ -24,6 +24,7 @@ enum Kernel : int {
   kFp8W4S = 37,   // gemm_fp8.hip: the fp8 W4 kernel as one K-tile stream per CU (interior tiles)
   kFp8T128 = 41,      // gemm_tile.hip fp8: 128x128 tile, 4 waves x 64x64, split-K (M, N % 128)
   kFp8T256x128 = 42,  // gemm_tile.hip fp8: 256x128 tile, 4 waves x 128x64, split-K (M % 256, N % 128)
+  kF32T128 = 51,      // gemm_f32_tile.hip: exact fp32, 128x128 tile, 4 waves x 64x64, split-K (any M, N % 4)
 };
 
 // Experiment / diagnostic ids (A/B and timing-only builds). Compiled and
@@ -149,6 +150,17 @@ std::pair<int, int> tail_split(const Problem& p, int kernel);
 // Which kernel `kernel` (kAuto allowed) resolves to for this problem;
 // -1 if the requested kernel cannot run it.
 int resolve_kernel(const Problem& p, int kernel);
+
+// The planner's whole decision for a problem (shape-only use is fine: the
+// operand pointers are only checked for alignment): the kernel, its split-K,
+// the cost model's time (us; 0 for kernels it does not price) and the
+// wave-quantisation tail plan {tail_m1, tail_S} ({0, 1}: one launch).
+struct PlanInfo {
+  int kernel, splitk;
+  double cost_us;
+  int tail_m1, tail_S;
+};
+PlanInfo plan_info(const Problem& p, int kernel);
 
 // Enqueue C = A @ B on `stream`. Returns hipSuccess or an error; *used (if
 // non-null) receives the kernel that ran. With kAuto, a large problem whose K /

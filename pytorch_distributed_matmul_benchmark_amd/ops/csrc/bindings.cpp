@@ -210,6 +210,30 @@ std::tuple<int64_t, int64_t> tail_split_for(const at::Tensor& A, const at::Tenso
   return {t.first, t.second};
 }
 
+// The planner's decision for a SHAPE (no tensors: contiguous operands at an
+// aligned stand-in address, so it runs without a GPU): (kernel id, split-K,
+// model cost us, tail M1, tail S). dtype: 0 f32, 1 f16, 2 bf16, 3 fp8.
+std::tuple<int64_t, int64_t, double, int64_t, int64_t> plan_shape(int64_t dtype, int64_t M, int64_t N,
+                                                                  int64_t K, int64_t batch,
+                                                                  int64_t kernel, int64_t cus) {
+  pdmb::Problem p{};
+  p.dtype = (int)dtype;
+  p.A = p.B = p.C = (void*)(uintptr_t)4096;
+  p.M = (int)M;
+  p.N = (int)N;
+  p.K = (int)K;
+  p.lda = (int)K;
+  p.ldb = dtype == 3 ? (int)K : (int)N;  // fp8 B is column-major (Bt [N, K])
+  p.ldc = (int)N;
+  p.batch = (int)batch;
+  p.sA = M * K;
+  p.sB = K * N;
+  p.sC = M * N;
+  p.cus = (int)cus;
+  const pdmb::PlanInfo r = pdmb::plan_info(p, (int)kernel);
+  return {r.kernel, r.splitk, r.cost_us, r.tail_m1, r.tail_S};
+}
+
 // Total milliseconds for `iters` timed launches (after `warmup`).
 double bench(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t iters,
              int64_t warmup, bool graph, int64_t kernel, int64_t splitk) {
@@ -314,6 +338,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("B"), py::arg("out"), py::arg("iters"), py::arg("warmup"),
         py::arg("graph") = false, py::arg("kernel") = 0, py::arg("splitk") = 0);
   m.def("kernel_name", &kernel_name);
+  m.def("plan_shape", &plan_shape, py::arg("dtype"), py::arg("M"), py::arg("N"), py::arg("K"),
+        py::arg("batch") = 1, py::arg("kernel") = 0, py::arg("cus") = 0);
   m.def("comm_proxy", &comm_proxy, py::arg("dst"), py::arg("src"), py::arg("blocks"));
   m.def("set_debug_buffer", &set_debug_buffer, py::arg("buf") = py::none());
   m.def("create_cu_masked_stream", &create_cu_masked_stream, py::arg("device"),

@@ -23,6 +23,8 @@ hipError_t gemm_generic_launch(int dt, GemmArgs a, bool vec, hipStream_t stream)
 bool gemm_f32_256_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 hipError_t gemm_f32_256_launch(GemmArgs a, int variant, hipStream_t stream);
 hipError_t gemm_f32_w4_launch(GemmArgs a, hipStream_t stream);
+bool gemm_f32_tile_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
+hipError_t gemm_f32_tile_launch(GemmArgs a, hipStream_t stream);
 bool gemm_fp8_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream);
 bool gemm_fp8_w4s_fits(const GemmArgs& a);
@@ -105,7 +107,6 @@ static bool is_experiment(int k) {
 
 static int device_cus();
 static int fp8_split(const Problem& p);
-static int f32_split(const Problem& p);
 static bool w4s_fits(const Problem& p);
 static bool w4s_auto(const Problem& p);
 static bool supports(const Problem& p, int kernel);
@@ -155,13 +156,16 @@ int resolve_kernel(const Problem& p, int kernel) {
         const Plan pl = plan(p, kAuto);
         return pl.kernel == kMfmaW4 && pl.splitk == 1 && w4s_auto(p) ? kMfmaW4S : pl.kernel;
       }
-      // fp32: the 8-wave f32_256s where the grid fills the chip — ahead of
-      // f32_w4 by 1.0-2.2 % on three boxes, behind by 0.2-0.4 % on one
-      // (profiles/r2_f32_lds_epilogue_ab_box*.jsonl, r2_f32_splitk_ab.jsonl) —
-      // and f32_w4 with split-K where it does not (f32_split).
+      // fp32: the planner over the exact-fp32 family — f32_256s (8 waves,
+      // 256x256: ahead of f32_w4 by 1.0-2.2 % on full grids, profiles/
+      // r2_f32_lds_epilogue_ab_box*.jsonl), f32_w4 (256x256, split-K) and
+      // f32_t128 (128x128, split-K) for grids that under-fill the chip.
       if (fast) return kMfma256d;
       if (!f32fast) return kGeneric;
-      return f32_split(p) > 1 ? kF32W4 : kF32_256s;
+      {
+        const Plan pl = plan(p, kAuto);
+        return pl.kernel >= 0 ? pl.kernel : kF32_256s;
+      }
     case kGeneric: return kGeneric;
     case kMfma256d: return fast ? kMfma256d : -1;
     case kMfmaW4: return w4 ? kMfmaW4 : -1;
@@ -171,6 +175,7 @@ int resolve_kernel(const Problem& p, int kernel) {
     case kT256x128: return t256 ? kT256x128 : -1;
     case kF32_256s: return f32fast ? kF32_256s : -1;
     case kF32W4: return f32fast ? kF32W4 : -1;  // same constraints as f32_256
+    case kF32T128: return p.dtype == kF32 && supports(p, kF32T128) ? kF32T128 : -1;
 #ifdef PDMB_EXPERIMENTS
     case kF32_256: case kF32NoDma: case kF32_256sDirect: return f32fast ? kernel : -1;
     case kT128Unfused: return t128 ? kernel : -1;
@@ -215,20 +220,33 @@ int resolve_kernel(const Problem& p, int kernel) {
 // fp8 (one K-tile = 128 e4m3: the same bytes per row and MFMA cycles as a
 // bf16 K-tile of 64) is planned over its own models: fp8 W4 (edge tiles too;
 // its split stays fp8_split's measured rule) and the fp8 tile family.
+//
+// Exact fp32 (K-tile = 32; fp32 MFMA is not power-bound — f32_256s runs 95 %
+// MFMA busy at 2.38 GHz, profiles/r1_fp32_ablation.md — so no idle-CU boost):
+// f32_256s 7.0 us per 256x256 K-tile (152 TF at 16k), f32_w4 7.1, f32_t128
+// 1.81 per 128x128 K-tile (fit to 4096 x {1024, 2048} x 4096: 237 / 471 us,
+// profiles/r3_f32_t128_ab.jsonl). f32_t128 is listed before f32_w4: it
+// measured ahead of the split W4 on every under-filled shard shape (4096 x
+// 2048 x 4096 145.8 vs 141.6 TF), so the 3 % hysteresis favours it.
 struct KernelModel {
   int kernel, bm, bn, occ;
   double kt;
-  bool fp8;
+  int cls;   // 0: bf16 / fp16, 1: fp8, 2: fp32
+  int maxS;  // largest split-K (1: the kernel does not split)
 };
 static constexpr KernelModel kModels[] = {
-    {kMfmaW4, 256, 256, 1, 1.42, false},
-    {kT256x128, 256, 128, 1, 0.80, false},
-    {kT128, 128, 128, 1, 0.46, false},
-    {kT128x2, 128, 128, 2, 0.86, false},
-    {kFp8W4, 256, 256, 1, 1.30, true},
-    {kFp8T256x128, 256, 128, 1, 0.80, true},
-    {kFp8T128, 128, 128, 1, 0.42, true},
+    {kMfmaW4, 256, 256, 1, 1.42, 0, 8},
+    {kT256x128, 256, 128, 1, 0.80, 0, 8},
+    {kT128, 128, 128, 1, 0.46, 0, 8},
+    {kT128x2, 128, 128, 2, 0.86, 0, 8},
+    {kFp8W4, 256, 256, 1, 1.30, 1, 4},
+    {kFp8T256x128, 256, 128, 1, 0.80, 1, 8},
+    {kFp8T128, 128, 128, 1, 0.42, 1, 8},
+    {kF32_256s, 256, 256, 1, 7.0, 2, 1},
+    {kF32T128, 128, 128, 1, 1.81, 2, 8},
+    {kF32W4, 256, 256, 1, 7.1, 2, 8},
 };
+static int dt_class(const Problem& p) { return p.dtype == kFP8 ? 1 : p.dtype == kF32 ? 2 : 0; }
 static constexpr double kFixedUs = 4.0;   // launch + prologue + epilogue
 static constexpr double kMeetUs = 4.0;    // combine latency (poll, serial slab read)
 static constexpr double kSlabBw = 4.0e6;  // bytes per us of slab traffic, chip-wide
@@ -245,7 +263,7 @@ static long long tiles_of(const Problem& p, int kernel) {  // ceil: fp8 W4 runs 
   return (long long)((p.M + m.bm - 1) / m.bm) * ((p.N + m.bn - 1) / m.bn) * (p.batch < 1 ? 1 : p.batch);
 }
 
-static int ktiles(const Problem& p) { return p.K / (p.dtype == kFP8 ? 128 : 64); }
+static int ktiles(const Problem& p) { return p.K / (p.dtype == kFP8 ? 128 : p.dtype == kF32 ? 32 : 64); }
 
 static int device_cus() {
   static int n[64] = {0};
@@ -286,7 +304,8 @@ static double plan_cost(const Problem& p, int kernel, int S) {
   const long long units = T * S;
   const long long waves = (units + slots - 1) / slots;
   const double busy = (double)units / (double)(waves * slots);
-  double t = (double)waves * (per * m.kt * (0.62 + 0.38 * busy) + kFixedUs);
+  const double boost = m.cls == 2 ? 1.0 : 0.62 + 0.38 * busy;  // power headroom (not fp32)
+  double t = (double)waves * (per * m.kt * boost + kFixedUs);
   if (S > 1) t += (double)T * (S - 1) * 2.0 * m.bm * m.bn * 4.0 / kSlabBw + kMeetUs;
   return t;
 }
@@ -294,15 +313,21 @@ static double plan_cost(const Problem& p, int kernel, int S) {
 static bool split_ok(const Problem& p, int kernel, int S) {
   if (kernel == kFp8W4) return S == fp8_split(p);  // its measured rule (fp8_split)
   if (S == 1) return true;
+  if (S > model_of(kernel).maxS) return false;
   const int nk = ktiles(p);
   const int per = (nk + S - 1) / S;
-  return per >= kMinKt && (S - 1) * per < nk && tiles_of(p, kernel) <= kMaxSplitTiles;
+  const int min_kt = p.dtype == kF32 ? 8 : kMinKt;  // fp32 K-tiles are 32 deep
+  return per >= min_kt && (S - 1) * per < nk && tiles_of(p, kernel) <= kMaxSplitTiles;
 }
 
 static bool supports(const Problem& p, int kernel) {
   const GemmArgs a = to_args(p);
   if (kernel == kMfmaW4) return gemm_w4_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   if (kernel == kFp8W4) return gemm_fp8_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
+  if (kernel == kF32_256s || kernel == kF32W4)
+    return p.dtype == kF32 && gemm_f32_256_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
+  if (kernel == kF32T128)
+    return p.dtype == kF32 && gemm_f32_tile_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   return gemm_tile_supported(p.dtype, model_of(kernel).bm, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
 }
 
@@ -315,7 +340,7 @@ static Plan plan(const Problem& p, int kernel) {
   static const int kS[] = {1, 2, 4, 8};
   for (const KernelModel& m : kModels) {
     if (kernel != kAuto && kernel != m.kernel) continue;
-    if (m.fp8 != (p.dtype == kFP8) || !supports(p, m.kernel)) continue;
+    if (m.cls != dt_class(p) || !supports(p, m.kernel)) continue;
     any = true;
     for (int S : kS) {
       if (S > 4 && p.splitk != S) continue;
@@ -330,20 +355,20 @@ static Plan plan(const Problem& p, int kernel) {
   }
   if (best.kernel < 0 && any)  // the requested split is impossible for this K
     for (const KernelModel& m : kModels)
-      if ((kernel == kAuto || kernel == m.kernel) && m.fp8 == (p.dtype == kFP8) && supports(p, m.kernel))
+      if ((kernel == kAuto || kernel == m.kernel) && m.cls == dt_class(p) && supports(p, m.kernel))
         return Plan{m.kernel, 0};
   return best;
 }
 
 static bool is_tiled(int k) {
-  return k == kMfmaW4 || k == kT128 || k == kT128x2 || k == kT256x128 || k == kFp8T128 || k == kFp8T256x128;
+  return k == kMfmaW4 || k == kT128 || k == kT128x2 || k == kT256x128 || k == kFp8T128 || k == kFp8T256x128 ||
+         k == kF32W4 || k == kF32T128;
 }
 
 int choose_splitk(const Problem& p, int kernel) {
   const int k = resolve_kernel(p, kernel);
   if (k == kMfmaW4S || k == kFp8W4S) return 1;
   if (k == kFp8W4) return fp8_split(p);
-  if (k == kF32W4) return f32_split(p);
   if (!is_tiled(k)) return 0;
   return plan(p, k).splitk;
 }
@@ -403,6 +428,20 @@ static Problem tail_part(const Problem& p, const TailPlan& t) {  // rows [m1, M)
   return b;
 }
 
+PlanInfo plan_info(const Problem& p, int kernel) {
+  PlanInfo r{};
+  r.kernel = resolve_kernel(p, kernel);
+  r.splitk = r.kernel >= 0 ? choose_splitk(p, kernel) : 0;
+  if (is_tiled(r.kernel) || r.kernel == kF32_256s || r.kernel == kFp8W4) {
+    const int S = r.splitk > 0 ? r.splitk : 1;
+    r.cost_us = plan_cost(p, r.kernel, S);
+  }
+  const TailPlan t = tail_plan(p, kernel);
+  r.tail_m1 = t.m1;
+  r.tail_S = t.S;
+  return r;
+}
+
 std::pair<int, int> tail_split(const Problem& p, int kernel) {
   const TailPlan t = tail_plan(p, kernel);
   return {t.m1, t.S};
@@ -425,22 +464,6 @@ static int fp8_split(const Problem& p) {
     if (T * s <= cus && nk / s >= 16 && T <= kMaxSplitTiles) S = s;
   return S;
 }
-// fp32 W4 split-K (gemm_f32_w4.hip): the same rule for exact fp32, whose
-// 256x256x32 K-tile takes ~7 us, so slices of >= 8 K-tiles dwarf the meet.
-// matrix_parallel's fp32 shards at the reference's sizes (4096 x {2048, 1024,
-// 512} x 4096: 128 / 64 / 32 tiles) otherwise leave 1/2 .. 7/8 of the CUs idle
-// (75 / 37.5 TF vs hipBLASLt 140 / 130, profiles/r2_f32_lds_epilogue_ab_box*.jsonl).
-static int f32_split(const Problem& p) {
-  if (p.splitk > 0) return p.splitk;
-  const long long T = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256) * (p.batch < 1 ? 1 : p.batch);
-  const int nk = p.K / 32;
-  const long long cus = p.cus > 0 ? p.cus : device_cus();
-  int S = 1;
-  for (int s : {2, 4, 8})
-    if (T * s <= cus && nk / s >= 8 && T <= kMaxSplitTiles) S = s;
-  return S;
-}
-
 static size_t fp8_split_bytes(const Problem& p, int S) {
   if (S <= 1) return 0;
   const long long T = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256) * (p.batch < 1 ? 1 : p.batch);
@@ -515,6 +538,8 @@ static hipError_t tiled_launch(const Problem& p, int k, GemmArgs a, void* part, 
       a.pers_grid = p.cus > 0 ? p.cus : device_cus();
     }
   }
+  if (k == kF32W4) return gemm_f32_w4_launch(a, stream);
+  if (k == kF32T128) return gemm_f32_tile_launch(a, stream);
   return k == kMfmaW4 ? gemm_w4_launch(p.dtype, a, stream, sub) : gemm_tile_launch(k, p.dtype, a, stream);
 }
 
@@ -681,7 +706,6 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel) {
   if (t.m1 > 0) return splitk_bytes(tail_part(p, t), kMfmaW4, t.S);  // the first launch is unsplit
   if (is_tiled(k)) return splitk_bytes(p, k, plan(p, k).splitk);
   if (k == kFp8W4) return fp8_split_bytes(p, fp8_split(p));
-  if (k == kF32W4) return fp8_split_bytes(p, f32_split(p));  // same 256x256 fp32 slots
   if (k == kMfmaW4Tall || k == kMfmaW4Wide || k == kMfmaW4Il32 || k == kMfmaW4Trace ||
       k == kMfmaW4Pers || k == kMfmaW4PersTrace)
     return splitk_bytes(p, kMfmaW4, plan(p, kMfmaW4).splitk);
@@ -738,8 +762,7 @@ static hipError_t gemm_padded(const Problem& p, hipStream_t stream, int* used) {
   qt.workspace = part;
   qt.workspace_bytes = part_bytes;
   if (!(t.m1 > 0 && gemm_tail(qt, t, stream, &e)))
-    e = k == kF32W4     ? gemm_f32_w4_launch(a, stream)
-      : k == kF32_256s ? gemm_f32_256_launch(a, 1, stream)
+    e = k == kF32_256s ? gemm_f32_256_launch(a, 1, stream)
       : is_tiled(k) ? tiled_launch(q, k, a, part, part_bytes, stream)
                      : gemm256_launch(q.dtype, a, 4, stream);
   if (e != hipSuccess) return e;
@@ -843,22 +866,8 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kFp8T256x128: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream);
     case kMfmaW4S: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 7);
     case kF32_256s: return gemm_f32_256_launch(a, 1, stream);
-    case kF32W4: {
-      GemmArgs s = a;
-      s.splitk = 1;
-      const int S = f32_split(p);
-      if (S > 1) {
-        unsigned* flags = stream_counters(stream);
-        if (flags && p.workspace && p.workspace_bytes >= fp8_split_bytes(p, S)) {
-          s.splitk = S;
-          s.part = (float*)p.workspace;
-          s.flags = flags;
-        } else if (p.splitk > 1) {
-          return hipErrorInvalidValue;  // explicitly requested: no silent change
-        }
-      }
-      return gemm_f32_w4_launch(s, stream);
-    }
+    case kF32W4:
+    case kF32T128: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream);
 #ifdef PDMB_EXPERIMENTS
     case kFp8: return gemm_fp8_launch(a, 0, stream);
     case kFp8W4Diag: return gemm_fp8_launch(a, 9, stream);
@@ -1037,6 +1046,7 @@ const char* kernel_name(int kernel) {
     case kT128x2: return "pdmb_t128x2_nn";
     case kT256x128: return "pdmb_t256x128_nn";
     case kF32W4: return "pdmb_f32_w4_nn";
+    case kF32T128: return "pdmb_f32_t128_nn";
     case kMfma256: return "pdmb_mfma256_nn";
     case kMfma256b: return "pdmb_mfma256b_nn";
     case kMfma256c: return "pdmb_mfma256c_nn";

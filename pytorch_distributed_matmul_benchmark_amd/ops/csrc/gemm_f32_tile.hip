@@ -1,0 +1,339 @@
+// gemm_f32_tile.hip — exact-fp32 C = A @ B (row-major NN) on v_mfma_f32_16x16x4_f32
+// with a 128x128 output tile: the fp32 member of the tile family (gemm_tile.hip)
+// for grids that under-fill the 256 CUs with 256x256 tiles.
+//
+// Why: matrix_parallel's fp32 column shards at the reference's default sizes
+// (matmul_scaling_benchmark.py:179-188 at :351-352; --dtype float32 is a
+// reference choice, matmul_benchmark.py:163-174) are 4096 x {2048, 1024, 512} x
+// 4096 = 128 / 64 / 32 256x256 tiles, and 2048^3 has 64. gemm_f32_w4.hip fills
+// them only by splitting K over 256 KiB fp32 slabs per slice (95-120 TF vs
+// hipBLASLt 127-140). A 128x128 tile gives 4x the workgroups, a
+// 64 KiB slab per slice, and needs no split at all on the 64-tile shapes.
+//
+// Structure (W4 / tile-family idioms):
+//  * 4 waves as 2 x 2, one per SIMD, each owning 64x64 outputs: 4 x 4 MFMA
+//    16x16 blocks, 64 fp32 accumulators in AGPRs (asm MFMAs on "+a" operands);
+//    operands swapped (the B element is the MFMA's A) so a lane owns 4
+//    consecutive output columns and C leaves through LDS as whole rows.
+//  * K-tile = 32 (128 B of A per row). LDS images per stage (32 KiB):
+//      A [128 rows][128 B], 16-B chunk c of row r at c ^ ((r >> 1) & 7)
+//        (gemm_f32_w4.hip's image; one ds_read_b128 = 4 consecutive k);
+//      B [32 k][512 B], 16-B chunk c of k-row k at c ^ 4 * ((k >> 2) & 3),
+//        UNPADDED so one 64-lane LDS-DMA fills two k-rows: a wave's four B
+//        pieces all have (k >> 2) & 3 == wave id, so its swizzle is one
+//        per-lane source offset. A B fragment read (16 columns x k = 16 kb +
+//        4 g + e over the lane groups g) then hits chunk groups 4 (q ^ g): all
+//        64 banks once, conflict-free.
+//  * 4-stage ring filled by LDS-DMA (buffer_load ... lds), 8 x 1 KiB pieces
+//    per wave per K-tile; one barrier per K-tile (s_waitcnt vmcnt(16): tile
+//    t+1 landed, t+2 / t+3 may fly; lgkmcnt(0): this wave's reads of t's
+//    stage done). Tile t+1's fragments are read during t's 128 MFMAs into a
+//    second register set; every load sits in an MFMA gap (Sched).
+//  * Split-K over K-tile ranges with the in-launch combine of splitk.h.
+// Edges: A rows past M and B past its extent read zeros through the DMA
+// descriptors; B columns past N feed only C columns the masked epilogue drops
+// (N % 4 == 0; the host checks K % 32, lda / ldb % 4, 16-B alignment).
+#include "api.h"
+#include "common.h"
+#include "splitk.h"
+
+namespace pdmb {
+namespace kf32t {
+
+constexpr int BM = 128, BN = 128, BK = 32, NT = 256, NS = 4;
+constexpr int MB = 4, NB = 4;                 // 16x16 blocks per wave
+constexpr int A_BYTES = BM * BK * 4;          // 16 KiB
+constexpr int B_BYTES = BK * BN * 4;          // 16 KiB
+constexpr int STAGE = A_BYTES + B_BYTES;      // 32 KiB
+constexpr int P = 8;                          // DMA pieces per wave per K-tile (4 A + 4 B)
+constexpr int G = 2 * 4 * MB * NB;            // MFMAs per K-tile per wave (kb, e, mi, ni) = 128
+constexpr int LDS_BYTES = NS * STAGE;         // 128 KiB
+typedef __attribute__((address_space(3))) f32x4 lds_f32x4;
+typedef __attribute__((address_space(3))) float lds_f32;
+
+__device__ __forceinline__ void mfma(f32x4& acc, float b, float a) {
+  asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+}
+
+// LDS-DMA with a scalar offset; M0 is clobbered (declared), not saved.
+__device__ __forceinline__ void dma16_m0(u32x4 rsrc, uint32_t voff, uint32_t soff, uint32_t lds) {
+  asm volatile(
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %0, %1, %2 offen lds"
+      :
+      : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds)
+      : "memory", "m0");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_lgkm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+// Item schedule of one K-tile (gemm_tile.hip Sched, fp32 classes): 8 A
+// fragment reads (b128: 2 kb x 4 mi), 32 B element reads (b32: 2 kb x 4 ni x
+// 4 e) and 8 DMA pieces spread Bresenham-style over the 128 MFMA gaps, at
+// most one per gap. Encoding: 0 none; 1 + piece; 100 + B read q; 200 + A read q.
+struct Sched {
+  int item[G];
+  constexpr Sched() : item() {
+    const int T[3] = {32, 8, P};
+    int n[3] = {0, 0, 0};
+    for (int g = 0; g < G; ++g) {
+      int best = -1, bd = 0;
+      for (int k = 0; k < 3; ++k) {
+        const int d = T[k] * (g + 1) - n[k] * G;
+        if (n[k] < T[k] && d > bd) {
+          bd = d;
+          best = k;
+        }
+      }
+      if (best == 0) item[g] = 100 + n[0]++;
+      else if (best == 1) item[g] = 200 + n[1]++;
+      else if (best == 2) item[g] = 1 + n[2]++;
+      else item[g] = 0;
+    }
+  }
+};
+
+struct Frag {  // one K-tile's fragments: A rows (4 k each) and B elements
+  f32x4 a[2][MB];      // [kb][mi]
+  float b[2][NB][4];   // [kb][ni][e]
+};
+
+struct Ctx {
+  u32x4 ra;             // A descriptor at this slice's first K
+  const char* Bb;       // B at this slice's first K row, column n0
+  long long b_bytes;
+  int lda4, ldb4, nk, wu;
+  uint32_t voffA, voffB;
+  uint32_t lds0;
+  // Per-lane fragment bases in stage 0 (the rest of each offset is an
+  // immediate): A block mi of half kb at abase[kb] + mi * 2048 (the row
+  // swizzle (r >> 1) & 7 does not depend on mi); B element (kb, ni, e) at
+  // bbase[ni] + kb * 8192 + e * 512 (k = 16 kb + 4 g + e; g is in the base).
+  uint32_t abase[2];
+  uint32_t bbase[NB];
+};
+
+__device__ __forceinline__ u32x4 b_rsrc(const Ctx& c, int tile) {
+  const long long off = (long long)tile * BK * c.ldb4;
+  return make_rsrc(c.Bb + off, c.b_bytes - off);
+}
+
+// DMA piece h (0..7) of K-tile `tile` into the stage at byte offset `so`.
+// h < 4: A rows 32 h + 8 wu + [0, 8) (8 x 128 B). h >= 4: B k-rows k0, k0 + 1
+// with k0 = 16 ((h-4) >> 1) + 4 wu + 2 ((h-4) & 1) (2 x 512 B).
+__device__ __forceinline__ void issue_piece(const Ctx& c, u32x4 rb, uint32_t so, int tile, int h) {
+  if (h < 4) {
+    dma16_m0(c.ra, c.voffA, (uint32_t)tile * (BK * 4) + (uint32_t)(h * 32 * c.lda4),
+             c.lds0 + so + (h * 32 + c.wu * 8) * 128);
+  } else {
+    const int j = h - 4;
+    const int k0 = 16 * (j >> 1) + 4 * c.wu + 2 * (j & 1);
+    dma16_m0(rb, c.voffB, (uint32_t)(k0 * c.ldb4), c.lds0 + so + A_BYTES + k0 * 512);
+  }
+}
+
+// One K-tile: 128 MFMAs on `cur` (tile t), reading tile t+1's fragments into
+// `nxt` from stage `sn`, DMA of tile t + NS into stage `sc`.
+__device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, uint32_t sc, uint32_t sn,
+                                      f32x4 (&acc)[MB][NB], const Frag& cur, Frag& nxt) {
+  constexpr Sched S{};
+  const int td = t + NS < c.nk ? t + NS : c.nk - 1;  // clamped tail DMAs (harmless re-reads)
+  const u32x4 rb = b_rsrc(c, td);
+  wait_lgkm_barrier<P * (NS - 2)>();
+  __builtin_amdgcn_sched_barrier(0);
+  uint32_t ab[2], bb[NB];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) ab[kb] = c.abase[kb] + sn;
+#pragma unroll
+  for (int ni = 0; ni < NB; ++ni) bb[ni] = c.bbase[ni] + sn;
+#pragma unroll
+  for (int gap = 0; gap < G; ++gap) {
+    const int kb = gap >> 6, e = (gap >> 4) & 3, mi = (gap >> 2) & 3, ni = gap & 3;
+    mfma(acc[mi][ni], cur.b[kb][ni][e], cur.a[kb][mi][e]);
+    const int it = S.item[gap];
+    if (it >= 200) {
+      const int q = it - 200, qk = q >> 2, qm = q & 3;
+      nxt.a[qk][qm] = *(const lds_f32x4*)(smem + ab[qk] + qm * 2048);
+    } else if (it >= 100) {
+      const int q = it - 100, qk = q >> 4, qn = (q >> 2) & 3, qe = q & 3;
+      nxt.b[qk][qn][qe] = *(const lds_f32*)(smem + bb[qn] + qk * 8192 + qe * 512);
+    } else if (it >= 1) {
+      issue_piece(c, rb, sc, td, it - 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+__global__ void __launch_bounds__(NT, 1) gemm_f32_t128(GemmArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+
+  int bz, tm, tn;
+  map_tile(a, blockIdx.x, bz, tm, tn);
+  int slice = 0;  // split-K: grid batch = batch x S, slice innermost (as W4)
+  if (a.splitk > 1) {
+    slice = bz % a.splitk;
+    bz /= a.splitk;
+  }
+  const int kt0 = slice * a.kt_per;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int lane = threadIdx.x & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wu >> 1, wc = wu & 1;
+  const int l16 = lane & 15, g = lane >> 4;
+
+  Ctx c;
+  c.wu = wu;
+  c.lds0 = (uint32_t)(size_t)((lds_void*)smem);
+  c.lda4 = a.lda * 4;
+  c.ldb4 = a.ldb * 4;
+  {
+    const int nk_all = a.K / BK;
+    c.nk = a.splitk > 1 ? min(a.kt_per, nk_all - kt0) : nk_all;
+  }
+  const long long k0 = (long long)kt0 * BK;
+  c.ra = make_rsrc((const char*)a.A + ((long long)bz * a.sA + (long long)m0 * a.lda + k0) * 4,
+                   ((long long)(a.M - m0 - 1) * a.lda + (a.K - k0)) * 4);
+  c.Bb = (const char*)a.B + ((long long)bz * a.sB + k0 * a.ldb + n0) * 4;
+  c.b_bytes = ((long long)(a.K - k0 - 1) * a.ldb + (a.N - n0)) * 4;
+  {
+    const int r = wu * 8 + (lane >> 3);  // row of A piece 0 (the swizzle is 32-row periodic)
+    c.voffA = (uint32_t)(r * c.lda4 + (((lane & 7) ^ ((r >> 1) & 7)) * 16));
+    // B: lanes 0-31 row k0, 32-63 row k0 + 1; LDS chunk (lane & 31) holds
+    // global chunk (lane & 31) ^ 4 wu ((k0 >> 2) & 3 == wu for every piece)
+    c.voffB = (uint32_t)((lane >> 5) * c.ldb4 + (((lane & 31) ^ (4 * wu)) * 16));
+    const int rr = wr * 64 + l16;  // + 16 mi: same swizzle
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      uint32_t ao = (uint32_t)(rr * 128 + (((kb * 4 + g) ^ ((rr >> 1) & 7)) * 16));
+      asm volatile("" : "+v"(ao));  // opaque: one base VGPR each
+      c.abase[kb] = ao;
+    }
+#pragma unroll
+    for (int ni = 0; ni < NB; ++ni) {  // k = 16 kb + 4 g + e: (k >> 2) & 3 == g
+      const int col = wc * 64 + ni * 16 + l16;
+      const int ch = (col >> 2) ^ (4 * g);
+      uint32_t bo = (uint32_t)(A_BYTES + 4 * g * 512 + ch * 16 + (col & 3) * 4);
+      asm volatile("" : "+v"(bo));
+      c.bbase[ni] = bo;
+    }
+  }
+
+  f32x4 acc[MB][NB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Prologue: tiles 0 .. NS-1 into stages 0 .. NS-1 (clamped), wait for tile
+  // 0 everywhere, read its fragments.
+  const int nk = c.nk;
+#pragma unroll
+  for (int st = 0; st < NS; ++st) {
+    const int tl = st < nk ? st : nk - 1;
+    const u32x4 rb = b_rsrc(c, tl);
+#pragma unroll
+    for (int h = 0; h < P; ++h) issue_piece(c, rb, st * STAGE, tl, h);
+  }
+  wait_barrier<P * (NS - 1)>();
+  Frag F0, F1;
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi) F0.a[kb][mi] = *(const lds_f32x4*)(smem + c.abase[kb] + mi * 2048);
+#pragma unroll
+    for (int ni = 0; ni < NB; ++ni)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        F0.b[kb][ni][e] = *(const lds_f32*)(smem + c.bbase[ni] + kb * 8192 + e * 512);
+  }
+  // K-tile t computes from set t & 1, reads t+1 into the other set from
+  // stage (t+1) % NS, refills stage t % NS with tile t + NS.
+  int t = 0;
+  for (; t + 1 < nk; t += 2) {
+    ktile(c, smem, t, (uint32_t)((t % NS) * STAGE), (uint32_t)(((t + 1) % NS) * STAGE), acc, F0, F1);
+    ktile(c, smem, t + 1, (uint32_t)(((t + 1) % NS) * STAGE), (uint32_t)(((t + 2) % NS) * STAGE), acc,
+          F1, F0);
+  }
+  if (t < nk)  // odd count: the last tile (its "next" reads are clamped re-reads)
+    ktile(c, smem, t, (uint32_t)((t % NS) * STAGE), (uint32_t)((t % NS) * STAGE), acc, F0, F1);
+  // Drain the tail DMAs and give the last MFMAs time to write their AGPRs
+  // (asm MFMAs are invisible to hipcc's hazard recognizer).
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+
+  SplitSlots sl;
+  const bool split = a.splitk > 1;
+  if (split && !splitk_meet<MB, NB, NT>(a, smem, ((long long)bz * a.tiles_m + tm) * a.tiles_n + tn,
+                                        slice, acc, sl))
+    return;
+
+  // Epilogue through LDS as whole 256-B rows (common.h store_block16_f32),
+  // once every wave is done with the stages.
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  char* Cb = (char*)a.C + (long long)bz * a.sC * 4;
+  char* ebuf = smem + 1024 + wu * epi_buf_f32<NB>();  // past splitk_meet's ticket word
+  const bool interior = m0 + BM <= a.M && n0 + BN <= a.N;
+#pragma unroll
+  for (int mi = 0; mi < MB; ++mi) {
+    f32x4 v[NB];
+    if (!split) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) v[j] = acc[mi][j];
+    } else {
+      splitk_row<MB, NB, NT>(a, sl, slice, mi, acc, v);
+    }
+    const int row0 = m0 + wr * 64 + mi * 16, col0 = n0 + wc * 64;
+    if (interior)
+      store_block16_f32<false, NB>(ebuf, v, Cb, (long long)a.ldc * 4, row0, col0, a.M, a.N, lane);
+    else
+      store_block16_f32<true, NB>(ebuf, v, Cb, (long long)a.ldc * 4, row0, col0, a.M, a.N, lane);
+  }
+}
+
+}  // namespace kf32t
+
+// Same operand constraints as gemm_f32_256 / gemm_f32_w4 (K % 32, N % 4,
+// lda / ldb % 4, 16-B aligned A / B, 16-B aligned C rows).
+bool gemm_f32_tile_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c) {
+  if (a.M <= 0 || a.N <= 0 || a.K <= 0) return false;
+  if (a.K % 32 || a.N % 4) return false;
+  if (a.lda % 4 || a.ldb % 4 || a.ldc % 4) return false;
+  if (a.lda < a.K || a.ldb < a.N || a.ldc < a.N) return false;
+  if (a.batch > 1 && (a.sA % 4 || a.sB % 4 || a.sC % 4)) return false;
+  if (align_a % 16 || align_b % 16 || align_c % 16) return false;
+  // 32-bit offsets: A rows up to 127 * lda (+ K bytes), B rows up to 31 * ldb.
+  if ((long long)128 * a.lda * 4 + (long long)a.K * 4 >= (1LL << 31)) return false;
+  if ((long long)32 * a.ldb * 4 + 512 >= (1LL << 31)) return false;
+  return true;
+}
+
+// a.splitk > 1: split-K with a.part / a.flags (gemm_dispatch.cpp f32 planner).
+hipError_t gemm_f32_tile_launch(GemmArgs a, hipStream_t stream) {
+  a.tiles_m = (a.M + kf32t::BM - 1) / kf32t::BM;
+  a.tiles_n = (a.N + kf32t::BN - 1) / kf32t::BN;
+  a.supertile = choose_supertile(a.tiles_m, a.tiles_n);
+  const int S = a.splitk > 1 ? a.splitk : 1;
+  if (S > 1) {
+    const int nk = a.K / kf32t::BK;
+    a.kt_per = (nk + S - 1) / S;
+    if ((S - 1) * a.kt_per >= nk || !a.part || !a.flags ||
+        (long long)a.tiles_m * a.tiles_n * a.batch > kMaxSplitTiles)
+      return hipErrorInvalidValue;  // every slice must own >= 1 K-tile
+  } else {
+    a.splitk = 1;
+  }
+  const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch * S;
+  if (nblocks <= 0) return hipSuccess;
+  if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(kf32t::gemm_f32_t128, dim3((unsigned)nblocks), dim3(kf32t::NT), 0, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace pdmb

@@ -4,8 +4,13 @@
 // batch_parallel | matrix_parallel, reference matmul_scaling_benchmark.py:
 // 69-238, plus ring_parallel, models/ring_parallel.py) driven entirely from C++: one host thread per GPU in one process,
 // RCCL communicators from ncclCommInitAll over xGMI, the gfx950 MFMA GEMM
-// library of ops/csrc (pdmb::gemm), hipEvents for timing and an
-// event-ordered comm stream for the --overlap variants. No PyTorch, no Python:
+// library of ops/csrc (pdmb::gemm), hipEvents for timing and, for --overlap,
+// the schedule of parallel/overlap.py OverlapPipeline: whole GEMMs into a
+// ring of outputs, each output's collective on a high-priority comm stream
+// while the next GEMM runs, and with --chunks P > 1 the collective started
+// piece by piece as the SAME launch's tiles finish (W4 completion signals,
+// api.h pdmb::Signal; the rank's host thread waits for each piece's flag and
+// issues its RCCL call at once). No PyTorch, no Python:
 // useful to separate framework overhead from kernel/fabric behaviour and as a
 // reference implementation of the scaling modes for MI355X nodes.
 //
@@ -25,6 +30,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <stdexcept>
@@ -57,7 +63,7 @@ struct Opts {
   int iters = 50, warmup = 10;
   int dtype = 2;  // pdmb::DType: 0 f32, 1 f16, 2 bf16, 3 fp8 e4m3 (column-major B, bf16 C)
   Mode mode = kIndependent;
-  int batch = 4, chunks = 4, kernel = 0;
+  int batch = 4, chunks = 1, kernel = 0;  // chunks: collective pieces per GEMM (signalled)
   bool overlap = false, check = false;
   bool direct = false;  // --allgather direct: P2P to every peer in one group (own link each)
   std::string json;
@@ -231,29 +237,33 @@ pdmb::Problem problem(int dt, const void* A, const void* B, void* C, int M, int 
   return p;
 }
 
-// Launch scratch (padded copies / split-K partials), one growing buffer per
-// stream. Growing waits for the stream first; it happens in warm-up only.
-void* scratch(hipStream_t s, size_t bytes) {
-  static std::map<hipStream_t, Buf>* m = new std::map<hipStream_t, Buf>();
-  Buf& b = (*m)[s];
-  if (b.bytes < bytes) {
-    HIP_OK(hipStreamSynchronize(s));
-    b = Buf(bytes);
+// Launch scratch (padded copies / split-K partials): one growing buffer per
+// stream, owned by the rank that owns the streams (run_rank), so no two rank
+// threads share the map and a buffer dies with its rank's streams. Growing
+// waits for the stream first; it happens in warm-up only.
+struct Scratch {
+  std::map<hipStream_t, Buf> m;
+  void* get(hipStream_t s, size_t bytes) {
+    Buf& b = m[s];
+    if (b.bytes < bytes) {
+      HIP_OK(hipStreamSynchronize(s));
+      b = Buf(bytes);
+    }
+    return b.p;
   }
-  return b.p;
-}
+};
 
 // --overlap and ring_parallel run collectives beside the GEMMs: the planner
 // then keeps to dispatch-balanced kernels (Problem::cus = -1: no persistent
 // W4S, whose static tile assignment assumes every CU is its own).
 static bool g_shared_device = false;
 
-void gemm(const pdmb::Problem& p0, int kernel, hipStream_t s) {
+void gemm(const pdmb::Problem& p0, int kernel, hipStream_t s, Scratch& ws) {
   pdmb::Problem p = p0;
   if (g_shared_device && p.cus == 0) p.cus = -1;
   const size_t need = pdmb::gemm_workspace_bytes(p, kernel);
   if (need) {
-    p.workspace = scratch(s, need);
+    p.workspace = ws.get(s, need);
     p.workspace_bytes = need;
   }
   int used = -1;
@@ -305,27 +315,116 @@ void check_rows(int dt, const void* A, const void* B, const void* C, int M, int 
   HIP_OK(hipStreamSynchronize(s));
 }
 
-// Row chunks of an overlapped GEMM: as many as still fill the chip. With the
-// 128x128 T128 tiles and split-K (bf16 / fp16) a chunk of 64 256x256-tile
-// equivalents does; the fp32 kernel needs a full wave of 256 (as
-// parallel/overlap.py gemm_chunks).
-int effective_chunks(int m, int n, int chunks, int dt) {
-  const long long tiles = (long long)ceil_div(m, 256) * ceil_div(n, 256);
-  const long long min_tiles = dt == 0 ? 256 : 64;  // dt 0 = float32
-  return std::max(1, (int)std::min<long long>(chunks, tiles / min_tiles));
-}
+// ---- the overlap pipeline (parallel/overlap.py OverlapPipeline) -------------
+// A ring of R output buffers; unit k computes ring slot k % R on the compute
+// stream `st` (one whole GEMM launch), and its rows go through `coll(r, r0,
+// r1, piece)` on the comm stream `cs`. The next GEMM into a slot waits only
+// for that slot's last collective. pieces > 1: the GEMM runs with completion
+// signals and this host thread — after queueing the next unit's GEMM — waits
+// for each piece's flag and issues that piece's collective at once.
+struct Pipeline {
+  struct Slot {
+    pdmb::Problem p;
+    pdmb::Signal* sig = nullptr;
+    unsigned epoch = 0;
+    hipEvent_t ready = nullptr, done = nullptr;
+    bool used = false;
+  };
+  std::vector<Slot> slots;
+  std::vector<std::pair<int, int>> pieces;  // row ranges [r0, r1)
+  int sig_rows = 0, kernel = 0;
+  long long k = 0;
+  int pending = -1;
+  hipStream_t st = nullptr, cs = nullptr;
+  Scratch* ws = nullptr;
+  std::function<void(int, int, int, int)> coll;
 
-std::vector<std::pair<int, int>> row_chunks(int m, int chunks) {
-  const int step = ceil_div(ceil_div(m, chunks), 256) * 256;
-  std::vector<std::pair<int, int>> out;
-  for (int s = 0; s < m; s += step) out.push_back({s, std::min(m, s + step)});
-  return out;
-}
+  void init(const std::vector<pdmb::Problem>& ring, int requested, int kern, hipStream_t s,
+            hipStream_t c, Scratch& w, int device) {
+    st = s;
+    cs = c;
+    ws = &w;
+    kernel = kern;
+    const int M = ring[0].M;
+    pdmb::Problem q = ring[0];
+    q.cus = -1;  // as issued beside collectives
+    const int granule = requested > 1 ? pdmb::signal_granule(q, kern) : 0;
+    const int tm = ceil_div(M, 256);
+    if (granule > 0) {
+      const int units = tm / granule;
+      int P = 1;
+      for (int c : {2, 4, 8})
+        if (c <= requested && c <= units) P = c;
+      if (P > 1) sig_rows = ceil_div(units, P) * granule;
+    }
+    const int step = sig_rows > 0 ? sig_rows * 256 : M;
+    for (int r0 = 0; r0 < M; r0 += step) pieces.push_back({r0, std::min(M, r0 + step)});
+    for (const auto& p : ring) {
+      Slot sl;
+      sl.p = p;
+      HIP_OK(hipEventCreateWithFlags(&sl.ready, hipEventDisableTiming));
+      HIP_OK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+      if (sig_rows > 0) HIP_OK(pdmb::signal_create(device, (int)pieces.size(), &sl.sig));
+      slots.push_back(sl);
+    }
+  }
+  bool signalled() const { return sig_rows > 0; }
+  void issue(int r) {
+    Slot& sl = slots[r];
+    for (size_t j = 0; j < pieces.size(); ++j) {
+      if (signalled()) {
+        if (!pdmb::signal_wait(sl.sig, (int)j, sl.epoch, 120.0))
+          throw std::runtime_error("GEMM completion signal timed out");
+      } else if (j == 0) {
+        HIP_OK(hipStreamWaitEvent(cs, sl.ready, 0));
+      }
+      coll(r, pieces[j].first, pieces[j].second, (int)j);
+    }
+    HIP_OK(hipEventRecord(sl.done, cs));
+    sl.used = true;
+  }
+  void step(int units) {
+    for (int u = 0; u < units; ++u) {
+      const int r = (int)(k++ % (long long)slots.size());
+      Slot& sl = slots[r];
+      if (sl.used) HIP_OK(hipStreamWaitEvent(st, sl.done, 0));  // WAR: the slot's collective is done
+      pdmb::Problem p = sl.p;
+      if (signalled()) {
+        p.sig = sl.sig;
+        p.sig_rows = sig_rows;
+        p.sig_epoch = ++sl.epoch;
+      }
+      gemm(p, kernel, st, *ws);
+      HIP_OK(hipEventRecord(sl.ready, st));
+      if (signalled()) {
+        if (pending >= 0) issue(pending);  // the next GEMM is queued before this thread blocks
+        pending = r;
+      } else {
+        issue(r);
+      }
+    }
+  }
+  void finish() {
+    if (pending >= 0) issue(pending);
+    pending = -1;
+    for (auto& sl : slots)
+      if (sl.used) HIP_OK(hipStreamWaitEvent(st, sl.done, 0));
+  }
+  int last_slot() const { return (int)((k + (long long)slots.size() - 1) % (long long)slots.size()); }
+  ~Pipeline() {
+    for (auto& sl : slots) {
+      if (sl.ready) (void)hipEventDestroy(sl.ready);
+      if (sl.done) (void)hipEventDestroy(sl.done);
+      pdmb::signal_destroy(sl.sig);
+    }
+  }
+};
 
 // ---- one rank ---------------------------------------------------------------
 void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Result& res) {
   HIP_OK(hipSetDevice(rank));
   const int ws = o.gpus, dt = o.dtype;
+  Scratch scr;  // this rank's launch scratch, freed with its streams
   const size_t es = esize(dt), oes = oesize(dt);  // operand / output element bytes
   hipStream_t st, cs;
   int lo = 0, hi = 0;
@@ -350,12 +449,12 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     fill(B.p, (long long)n * n, dt, 2 * rank + 2, st);
     const pdmb::Problem p = problem(dt, A.p, B.p, C.p, n, n, n, n, n, n);
     res.kernel = pdmb::kernel_name(pdmb::resolve_kernel(p, o.kernel));
-    for (int i = 0; i < o.warmup; ++i) gemm(p, o.kernel, st);
+    for (int i = 0; i < o.warmup; ++i) gemm(p, o.kernel, st, scr);
     HIP_OK(hipStreamSynchronize(st));
     bar.wait();
     hipEvent_t e0 = event(), e1 = event();
     HIP_OK(hipEventRecord(e0, st));
-    for (int i = 0; i < o.iters; ++i) gemm(p, o.kernel, st);
+    for (int i = 0; i < o.iters; ++i) gemm(p, o.kernel, st, scr);
     HIP_OK(hipEventRecord(e1, st));
     HIP_OK(hipEventSynchronize(e1));
     res.avg_ms = res.comp_ms = elapsed(e0, e1) / std::max(o.iters, 1);
@@ -372,47 +471,46 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     fill(B.p, (long long)(lb * mat), dt, 2 * rank + 2, st);
     const pdmb::Problem p = problem(dt, A.p, B.p, C.p, n, n, n, n, n, n, lb, mat, mat, mat);
     res.kernel = pdmb::kernel_name(pdmb::resolve_kernel(p, o.kernel));
-    struct Unit { int b, r0, r1; };
-    std::vector<Unit> units;
-    const int ch = o.overlap ? effective_chunks(n, n, o.chunks, dt) : 1;
-    for (int b = 0; b < lb; ++b)
-      for (auto rc : row_chunks(n, ch)) units.push_back({b, rc.first, rc.second});
-    res.chunks = ch;
-    std::vector<hipEvent_t> ready, done;
-    for (size_t u = 0; u < units.size(); ++u) {
-      ready.push_back(event());
-      done.push_back(event());
+    const bool ov = o.overlap && dist;
+    // overlap ring: the batch's own outputs (lb >= 2) or C plus a second buffer (C1/C2)
+    Buf C2(ov && lb == 1 ? mat * oes : 0);
+    Pipeline pipe;
+    if (ov) {
+      std::vector<pdmb::Problem> ring;
+      for (int b = 0; b < lb; ++b)
+        ring.push_back(problem(dt, (char*)A.p + b * mat * es, (char*)B.p + b * mat * es,
+                               (char*)C.p + b * mat * oes, n, n, n, n, n, n));
+      if (lb == 1) ring.push_back(problem(dt, A.p, B.p, C2.p, n, n, n, n, n, n));
+      pipe.coll = [&](int r, int r0, int r1, int) {
+        char* c = (char*)pipe.slots[r].p.C + (size_t)r0 * n * oes;
+        NCCL_OK(ncclAllReduce(c, c, (size_t)(r1 - r0) * n, nccl_out_type(dt), ncclSum, comm, cs));
+      };
+      pipe.init(ring, o.chunks, o.kernel, st, cs, scr, rank);
+      res.chunks = (int)pipe.pieces.size();
     }
-    std::vector<bool> used(units.size(), false);
     auto serial_iter = [&](hipEvent_t em) {
-      gemm(p, o.kernel, st);
+      gemm(p, o.kernel, st, scr);
       if (em) HIP_OK(hipEventRecord(em, st));
       if (dist) NCCL_OK(ncclAllReduce(C.p, C.p, lb * mat, nccl_out_type(dt), ncclSum, comm, st));
     };
-    auto overlap_iter = [&]() {
-      for (size_t u = 0; u < units.size(); ++u) {
-        const Unit& un = units[u];
-        char* a = (char*)A.p + (un.b * mat + (size_t)un.r0 * n) * es;
-        char* b = (char*)B.p + un.b * mat * es;
-        char* c = (char*)C.p + (un.b * mat + (size_t)un.r0 * n) * oes;
-        if (used[u]) HIP_OK(hipStreamWaitEvent(st, done[u], 0));
-        gemm(problem(dt, a, b, c, un.r1 - un.r0, n, n, n, n, n), o.kernel, st);
-        HIP_OK(hipEventRecord(ready[u], st));
-        HIP_OK(hipStreamWaitEvent(cs, ready[u], 0));
-        NCCL_OK(ncclAllReduce(c, c, (size_t)(un.r1 - un.r0) * n, nccl_out_type(dt), ncclSum, comm, cs));
-        HIP_OK(hipEventRecord(done[u], cs));
-        used[u] = true;
+    for (int i = 0; i < o.warmup; ++i) {
+      if (ov) {
+        pipe.step(lb);
+        pipe.finish();
+      } else {
+        serial_iter(nullptr);
       }
-      for (size_t u = 0; u < units.size(); ++u) HIP_OK(hipStreamWaitEvent(st, done[u], 0));
-    };
-    const bool ov = o.overlap && dist;
-    for (int i = 0; i < o.warmup; ++i) ov ? overlap_iter() : serial_iter(nullptr);
+    }
     HIP_OK(hipStreamSynchronize(st));
-    // compute-only reference time
+    // compute-only reference time (into a scratch output: the ring keeps its reduced values)
     {
+      Buf Cs(mat * oes);
       hipEvent_t c0 = event(), c1 = event();
       HIP_OK(hipEventRecord(c0, st));
-      for (int i = 0; i < std::min(o.iters, 10); ++i) gemm(p, o.kernel, st);
+      for (int i = 0; i < std::min(o.iters, 10); ++i)
+        for (int b = 0; b < lb; ++b)
+          gemm(problem(dt, (char*)A.p + b * mat * es, (char*)B.p + b * mat * es, Cs.p, n, n, n, n, n, n),
+               o.kernel, st, scr);
       HIP_OK(hipEventRecord(c1, st));
       HIP_OK(hipEventSynchronize(c1));
       res.comp_ms = elapsed(c0, c1) / std::max(1, std::min(o.iters, 10));
@@ -421,7 +519,8 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     if (ov) {
       hipEvent_t e0 = event(), e1 = event();
       HIP_OK(hipEventRecord(e0, st));
-      for (int i = 0; i < o.iters; ++i) overlap_iter();
+      for (int i = 0; i < o.iters; ++i) pipe.step(lb);
+      pipe.finish();
       HIP_OK(hipEventRecord(e1, st));
       HIP_OK(hipEventSynchronize(e1));
       res.avg_ms = elapsed(e0, e1) / std::max(o.iters, 1);
@@ -450,7 +549,8 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     res.flops_local = flop * lb;
     res.flops_total = flop * gb;
     if (o.check)  // C[0] = sum over ranks of A_r[0] @ B_r[0]: partial refs are summed on the host
-      check_rows(dt, A.p, B.p, C.p, n, n, n, n, n, n, st, res.ref, res.got);
+      check_rows(dt, A.p, B.p, ov && lb == 1 ? pipe.slots[pipe.last_slot()].p.C : C.p, n, n, n, n, n,
+                 n, st, res.ref, res.got);
   } else if (o.mode == kRingParallel) {
     // All-gather-GEMM over BOTH ring directions (models/ring_parallel.py): A
     // row-sharded in blocks of rp rows, B column-sharded. Each block is cut
@@ -496,7 +596,7 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
       if (r1 > r0)
         gemm(problem(dt, a, Bl.p, (char*)Cl.p + ((size_t)j * rp + r0) * shard * oes, r1 - r0, shard,
                      n, n, ldb, shard),
-             o.kernel, st);
+             o.kernel, st, scr);
     };
     auto block_gemm = [&](const char* a, int j) { part_gemm(a, j, 0, rp); };
     auto iter = [&]() {
@@ -569,22 +669,6 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
                               hipMemcpyDeviceToDevice, st));
     const pdmb::Problem p = problem(dt, A.p, Bl.p, Cl.p, n, shard, n, n, ldb, shard);
     res.kernel = pdmb::kernel_name(pdmb::resolve_kernel(p, o.kernel));
-    const int ch = o.overlap ? effective_chunks(n, shard, o.chunks, dt) : 1;
-    res.chunks = ch;
-    const auto rcs = row_chunks(n, ch);
-    // per-chunk gather buffers [ws * rows, shard] carved out of G
-    std::vector<char*> gb;
-    size_t off = 0;
-    for (auto rc : rcs) {
-      gb.push_back((char*)G.p + off);
-      off += (size_t)ws * (rc.second - rc.first) * shard * oes;
-    }
-    std::vector<hipEvent_t> ready, done;
-    for (size_t j = 0; j < rcs.size(); ++j) {
-      ready.push_back(event());
-      done.push_back(event());
-    }
-    std::vector<bool> used(rcs.size(), false);
     // All-gather `count` elements per rank from `send` into `recv` (rank-major):
     // RCCL's ring/channel algorithm, or --allgather direct: this rank's block
     // sent straight to every peer and every peer's block received straight
@@ -605,33 +689,48 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
       }
       NCCL_OK(ncclGroupEnd());
     };
+    // overlap: a ring of two C_local / gather buffer pairs (gather per piece: [ws * rows, shard])
+    Buf Cl2(o.overlap ? Cl.bytes : 0), G2(o.overlap ? G.bytes : 0);
+    Pipeline pipe;
+    std::vector<std::vector<char*>> gbuf;  // [slot][piece]
+    if (o.overlap) {
+      pipe.init({p, problem(dt, A.p, Bl.p, Cl2.p, n, shard, n, n, ldb, shard)}, o.chunks, o.kernel, st,
+                cs, scr, rank);
+      for (int r = 0; r < 2; ++r) {
+        std::vector<char*> v;
+        size_t off = 0;
+        for (auto pc : pipe.pieces) {
+          v.push_back((char*)(r ? G2.p : G.p) + off);
+          off += (size_t)ws * (pc.second - pc.first) * shard * oes;
+        }
+        gbuf.push_back(v);
+      }
+      pipe.coll = [&](int r, int r0, int r1, int j) {
+        allgather((char*)pipe.slots[r].p.C + (size_t)r0 * shard * oes, gbuf[r][j],
+                  (size_t)(r1 - r0) * shard, cs);
+      };
+      res.chunks = (int)pipe.pieces.size();
+    }
     auto iter = [&](hipEvent_t em) {
       if (!o.overlap) {
-        gemm(p, o.kernel, st);
+        gemm(p, o.kernel, st, scr);
         if (em) HIP_OK(hipEventRecord(em, st));
         allgather(Cl.p, (char*)G.p, (size_t)n * shard, st);
         return;
       }
-      for (size_t j = 0; j < rcs.size(); ++j) {
-        const int r0 = rcs[j].first, r1 = rcs[j].second;
-        char* a = (char*)A.p + (size_t)r0 * n * es;
-        char* c = (char*)Cl.p + (size_t)r0 * shard * oes;
-        if (used[j]) HIP_OK(hipStreamWaitEvent(st, done[j], 0));
-        gemm(problem(dt, a, Bl.p, c, r1 - r0, shard, n, n, ldb, shard), o.kernel, st);
-        HIP_OK(hipEventRecord(ready[j], st));
-        HIP_OK(hipStreamWaitEvent(cs, ready[j], 0));
-        allgather(c, gb[j], (size_t)(r1 - r0) * shard, cs);
-        HIP_OK(hipEventRecord(done[j], cs));
-        used[j] = true;
-      }
-      for (size_t j = 0; j < rcs.size(); ++j) HIP_OK(hipStreamWaitEvent(st, done[j], 0));
+      pipe.step(1);
     };
-    for (int i = 0; i < o.warmup; ++i) iter(nullptr);
+    for (int i = 0; i < o.warmup; ++i) {
+      iter(nullptr);
+      if (o.overlap) pipe.finish();
+    }
     HIP_OK(hipStreamSynchronize(st));
     {
+      // compute-only time; overlap: into the slot the timed loop's last unit will NOT gather
+      const pdmb::Problem pc = o.overlap ? pipe.slots[(pipe.k + o.iters) % 2].p : p;
       hipEvent_t q0 = event(), q1 = event();
       HIP_OK(hipEventRecord(q0, st));
-      for (int i = 0; i < std::min(o.iters, 10); ++i) gemm(p, o.kernel, st);
+      for (int i = 0; i < std::min(o.iters, 10); ++i) gemm(pc, o.kernel, st, scr);
       HIP_OK(hipEventRecord(q1, st));
       HIP_OK(hipEventSynchronize(q1));
       res.comp_ms = elapsed(q0, q1) / std::max(1, std::min(o.iters, 10));
@@ -643,6 +742,7 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     HIP_OK(hipEventRecord(marks[0], st));
     for (int i = 0; i < o.iters; ++i) {
       iter(o.overlap ? nullptr : mids[i]);
+      if (o.overlap && i + 1 == o.iters) pipe.finish();  // the last gathers are in the time
       HIP_OK(hipEventRecord(marks[i + 1], st));
     }
     HIP_OK(hipEventSynchronize(marks[o.iters]));
@@ -666,13 +766,16 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
       std::vector<unsigned short> h16;
       std::vector<float> h32;
       res.got.clear();
+      const int last = o.overlap ? pipe.last_slot() : 0;
       for (int r = 0; r < ws; ++r)
         for (int row : rows) {
-          size_t j = 0;
-          while (j + 1 < rcs.size() && row >= rcs[j].second) ++j;
-          const int r0 = rcs[j].first, rows_j = rcs[j].second - r0;
-          const char* base = o.overlap ? gb[j] + ((size_t)r * rows_j + (row - r0)) * shard * oes
-                                       : (char*)G.p + ((size_t)r * n + row) * shard * oes;
+          const char* base = (char*)G.p + ((size_t)r * n + row) * shard * oes;
+          if (o.overlap) {
+            size_t j = 0;
+            while (j + 1 < pipe.pieces.size() && row >= pipe.pieces[j].second) ++j;
+            const int r0 = pipe.pieces[j].first, rows_j = pipe.pieces[j].second - r0;
+            base = gbuf[last][j] + ((size_t)r * rows_j + (row - r0)) * shard * oes;
+          }
           if (dt == 0) {
             h32.resize(shard);
             HIP_OK(hipMemcpy(h32.data(), base, shard * 4, hipMemcpyDeviceToHost));
@@ -870,10 +973,10 @@ int main(int argc, char** argv) {
                    "\"dtype\": \"%s\", \"world_size\": %d, \"iterations\": %d, \"warmup\": %d, "
                    "\"avg_ms\": %.6f, \"max_ms\": %.6f, \"compute_ms\": %.6f, \"comm_ms\": %.6f, "
                    "\"tflops_rank0\": %.3f, \"node_tflops\": %.3f, \"actual_tflops\": %.3f, "
-                   "\"kernel\": \"%s\", \"relerr\": %s}\n",
+                   "\"kernel\": \"%s\", \"pieces\": %d, \"relerr\": %s}\n",
                    mode_name(o.mode), o.overlap ? "true" : "false", n, dtype_name(o.dtype), o.gpus,
                    o.iters, o.warmup, avg, mx, comp, cm, per_gpu, node, actual, r0.kernel.c_str(),
-                   relerr < 0 ? "null" : std::to_string(relerr).c_str());
+                   r0.chunks, relerr < 0 ? "null" : std::to_string(relerr).c_str());
       std::fflush(js);
     }
   }

@@ -45,7 +45,13 @@ run_stage() {
     gpus2_refused) echo "== gpus2_refused"; timeout -k 10 120 python bench.py --gpus 2 > "$OUT/gpus2_refused.log" 2>&1
                    local rc=$?; cat "$OUT/gpus2_refused.log"; echo "== gpus2_refused rc=$rc (want 2)"; [ $rc -eq 2 ] ;;
     ab_bf16) step ab_bf16 600 python scripts/ab_kernels.py --dtype bfloat16 ;;
-    ab_fp32) step ab_fp32 600 python scripts/ab_kernels.py --dtype float32 ;;
+    ab_fp32) step ab_fp32 900 python scripts/ab_kernels.py --dtype float32 --kernels auto,f32_w4,f32_t128,torch \
+               --rounds 3 --shapes 4096,2048,4096 4096,1024,4096 4096,512,4096 2048,2048,2048 6144,6144,6144 \
+               8192,8192,8192 16384,16384,16384 &&
+             grep '^{' "$OUT/ab_fp32.log" > "$OUT/ab_fp32.jsonl" ;;
+    tests_gemm) step tests_gemm 900 $PYT tests/test_gemm_gpu.py tests/test_modes_gpu.py -m gpu ;;
+    tests_overlap) step tests_overlap 900 $PYT tests/test_signal_gpu.py tests/test_overlap_gpu.py \
+                     tests/test_native_bench_gpu.py tests/test_multirank_gpu.py -m gpu ;;
     ab_fp8) step ab_fp8 600 python scripts/ab_kernels.py --dtype float8_e4m3fn ;;
     *) echo "unknown stage $1"; return 2 ;;
   esac

