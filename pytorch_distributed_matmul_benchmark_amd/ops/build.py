@@ -144,7 +144,7 @@ def probe_path() -> Path:
 
 def build_probe(verbose: bool = False, force: bool = False) -> Path:
     """The stand-alone MFMA-shape probe (runtime/mfma_probe.hip): 16x16x32 vs
-    32x32x16 bf16 FLOP rate on random operands (scripts/gpu_r2c.sh)."""
+    32x32x16 bf16 FLOP rate on random operands (profiles/r2_mfma_shape_probe.jsonl)."""
     out = probe_path()
     if force or _needs_build(out, [PROBE_SRC]):
         _run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", PROBE_SRC, "-o", out], verbose)

@@ -373,7 +373,7 @@ int choose_splitk(const Problem& p, int kernel) {
   return plan(p, k).splitk;
 }
 
-// ---- wave-quantisation tail (bf16/fp16 W4) ----------------------------------
+// ---- wave-quantisation tail (bf16/fp16 W4, fp8 W4) -----------------------------
 // A grid of 256x256 tiles whose last wave is mostly empty (6000^2 x 6144: 576
 // tiles = 2.25 waves of 256 CUs) runs as two launches on the stream: the first
 // M1 rows (a multiple of 256, tile rows that fill whole waves) unsplit, then
@@ -385,18 +385,26 @@ int choose_splitk(const Problem& p, int kernel) {
 // 0.203 -> 0.187 (0.193), 10000^2 x 10048 1.518 -> 1.457 (1.684); 5000^2 x 5056
 // has no split that helps and stays one launch. The tail rows keep their
 // fixed slice order, so results stay bitwise reproducible run to run.
+// fp8: the same plan on fp8 W4 (the first launch fp8 W4S where it has >= 2
+// tiles per CU; the tail split by fp8_split's measured rule). Probe (us, one
+// launch -> tail, hipBLASLt; profiles/r2_fp8_tail_probe.jsonl): 6144^3 196.9
+// -> 175.2 (187.6), 6000^2 x 6144 183.9 -> 177.4 (191.0), 7168^3 278.2 ->
+// 269.1 (314.9).
 struct TailPlan {
   int m1 = 0;  // rows of the first (unsplit) launch; 0 = one launch
   int S = 1;   // K slices of the tail launch
 };
 
+static int tail_kernel(const Problem& p) { return p.dtype == kFP8 ? kFp8W4 : kMfmaW4; }
+
 static TailPlan tail_plan(const Problem& p, int kernel) {
   TailPlan best;
   if (kernel != kAuto || p.splitk != 0 || p.cus > 0 || p.sig) return best;
-  if ((p.dtype != kBF16 && p.dtype != kF16) || p.M <= 256 || p.K <= 0) return best;
-  if (resolve_kernel(p, kAuto) < 0 || !supports(p, kMfmaW4)) return best;
+  if ((p.dtype != kBF16 && p.dtype != kF16 && p.dtype != kFP8) || p.M <= 256 || p.K <= 0) return best;
+  const int kw = tail_kernel(p);
+  if (resolve_kernel(p, kAuto) < 0 || !supports(p, kw)) return best;
   const Plan whole = plan(p, kAuto);  // the best single launch (W4 or a smaller tile)
-  if (whole.kernel < 0 || whole.splitk != 1) return best;
+  if (whole.kernel != kw || whole.splitk != 1) return best;
   const long long slots = device_cus();
   const int tm = (p.M + 255) / 256, tn = (p.N + 255) / 256, batch = p.batch < 1 ? 1 : p.batch;
   double bc = whole.cost * 0.97;
@@ -404,10 +412,10 @@ static TailPlan tail_plan(const Problem& p, int kernel) {
     Problem a = p, b = p;
     a.M = (tm - r) * 256;
     b.M = p.M - a.M;
-    const double c1 = plan_cost(a, kMfmaW4, 1);
+    const double c1 = plan_cost(a, kw, 1);
     for (int S : {2, 4}) {
-      if ((long long)r * tn * batch * S > slots || !split_ok(b, kMfmaW4, S)) continue;
-      const double c = c1 + plan_cost(b, kMfmaW4, S);
+      if ((long long)r * tn * batch * S > slots || !split_ok(b, kw, S)) continue;
+      const double c = c1 + plan_cost(b, kw, S);
       if (c < bc) {
         bc = c;
         best.m1 = a.M;
@@ -419,11 +427,11 @@ static TailPlan tail_plan(const Problem& p, int kernel) {
 }
 
 static Problem tail_part(const Problem& p, const TailPlan& t) {  // rows [m1, M), split S ways
-  const size_t es = 2;
+  const size_t esa = p.dtype == kFP8 ? 1 : 2, esc = 2;  // fp8: e4m3 A, bf16 C
   Problem b = p;
   b.M = p.M - t.m1;
-  b.A = (const char*)p.A + (size_t)t.m1 * p.lda * es;
-  b.C = (char*)p.C + (size_t)t.m1 * p.ldc * es;
+  b.A = (const char*)p.A + (size_t)t.m1 * p.lda * esa;
+  b.C = (char*)p.C + (size_t)t.m1 * p.ldc * esc;
   b.splitk = t.S;
   return b;
 }
@@ -698,12 +706,12 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel) {
     const size_t copies = d.a_bytes + d.b_bytes + d.c_bytes;
     const int k = resolve_kernel(d.q, kAuto);
     const TailPlan t = tail_plan(d.q, kAuto);
-    if (t.m1 > 0) return copies + splitk_bytes(tail_part(d.q, t), kMfmaW4, t.S);
+    if (t.m1 > 0) return copies + splitk_bytes(tail_part(d.q, t), tail_kernel(d.q), t.S);
     return copies + (is_tiled(k) ? splitk_bytes(d.q, k, plan(d.q, k).splitk) : 0);
   }
   const int k = resolve_kernel(p, kernel);
   const TailPlan t = tail_plan(p, kernel);
-  if (t.m1 > 0) return splitk_bytes(tail_part(p, t), kMfmaW4, t.S);  // the first launch is unsplit
+  if (t.m1 > 0) return splitk_bytes(tail_part(p, t), tail_kernel(p), t.S);  // the first launch is unsplit
   if (is_tiled(k)) return splitk_bytes(p, k, plan(p, k).splitk);
   if (k == kFp8W4) return fp8_split_bytes(p, fp8_split(p));
   if (k == kMfmaW4Tall || k == kMfmaW4Wide || k == kMfmaW4Il32 || k == kMfmaW4Trace ||
@@ -717,10 +725,18 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel) {
 // was sized for another plan).
 static bool gemm_tail(const Problem& p, const TailPlan& t, hipStream_t stream, hipError_t* e) {
   const Problem b = tail_part(p, t);
-  if (!p.workspace || p.workspace_bytes < splitk_bytes(b, kMfmaW4, t.S) || !stream_counters(stream))
+  if (!p.workspace || p.workspace_bytes < splitk_bytes(b, tail_kernel(p), t.S) || !stream_counters(stream))
     return false;
   Problem a = p;
   a.M = t.m1;
+  if (p.dtype == kFP8) {  // both launches through the fp8 cases of gemm()
+    a.splitk = 1;
+    a.workspace = nullptr;
+    a.workspace_bytes = 0;
+    *e = gemm(a, resolve_kernel(a, kAuto) == kFp8W4S ? kFp8W4S : kFp8W4, stream, nullptr);
+    if (*e == hipSuccess) *e = gemm(b, kFp8W4, stream, nullptr);
+    return true;
+  }
   *e = tiled_launch(a, kMfmaW4, to_args(a), nullptr, 0, stream, w4s_auto(a) ? 7 : 0);
   if (*e == hipSuccess) *e = tiled_launch(b, kMfmaW4, to_args(b), p.workspace, p.workspace_bytes, stream);
   return true;

@@ -71,13 +71,3 @@ def row_chunks(m: int, chunks: int, align: int = 256) -> list:
         out.append((s, e))
         s = e
     return out or [(0, 0)]
-
-
-def effective_chunks(m: int, n: int, chunks: int, tile: int = 256, min_tiles: int = 256) -> int:
-    """Largest chunk count ≤ ``chunks`` that still gives every row chunk of an
-    [m, n] GEMM output at least ``min_tiles`` 256×256 tiles — one full wave of
-    workgroups on the 256-CU MI355X. Chunking below that would leave CUs idle
-    in every chunk's GEMM and cost more than the overlap gains (e.g. the ws=8
-    matrix_parallel shard [16384, 2048] has 512 tiles: at most 2 chunks)."""
-    tiles = ceil_div(max(m, 1), tile) * ceil_div(max(n, 1), tile)
-    return max(1, min(int(chunks), tiles // max(min_tiles, 1)))

@@ -14,8 +14,11 @@ Arms (interleaved rounds, best of each), per (k, proxy size):
                 mask), planned for the CUs it may use (ops.gemm.cu_budget)
   proxy         the comm proxy alone on the high-priority comm stream
   both_k        GEMM chunk j (masked by k), then proxy piece j on the comm
-                stream behind an event recorded after it — the overlap
-                schedule's shape (parallel/overlap.py GatherOverlap)
+                stream behind an event recorded after it — round 2's chunked
+                overlap schedule (profiles/r2_cu_mask_overlap_v*.jsonl: the
+                chunked GEMM lost more than the overlap hid; round 3 replaced
+                it with parallel/overlap.py OverlapPipeline, measured by
+                scripts/overlap_proxy.py)
 speedup_k = (gemm_0 + proxy) / both_k: the gain over running the same work
 serialized without a mask (1 = nothing hidden, 2 = perfect overlap of equals).
 

@@ -6,10 +6,14 @@
 #
 #   scripts/gpu_session.sh TAG STAGE [STAGE ...] [-- NAME SECONDS COMMAND...]
 #
-# Stages: tests (whole GPU suite), tests_signal (signals + overlap), smoke, bench
-# (driver form), bench_quick, overlap_proxy, rocprof_bench, selflaunch2, selflaunch4,
-# gpus2_refused (bench.py --gpus 2 on a 1-GPU box must exit 2 at once), ab_bf16,
-# ab_fp32, ab_fp8. After "--": one ad-hoc step NAME with a SECONDS limit.
+# Stages: validate (= tests smoke bench rocprof_bench selflaunch2 selflaunch4, the
+# closing pass), tests (whole GPU suite), tests_gemm / tests_fp8 / tests_signal /
+# tests_overlap (subsets), smoke, bench (driver form), bench_quick, bench_fp8,
+# native16k (pdmb_bench bf16 / fp8 at 16k), overlap_proxy, rocprof_bench, selflaunch2,
+# selflaunch4, gpus2_refused (bench.py --gpus 2 on a 1-GPU box must exit 2 at once),
+# ab_bf16 / ab_fp32 / ab_fp8 (auto vs hipBLASLt A/B tables), final_table (auto vs
+# hipBLASLt, every dtype at 4k / 8k / 16k), pmc (PMC passes: scripts/gpu_pmc.sh with
+# N / KS / DT from the environment). After "--": one ad-hoc step NAME with a SECONDS limit.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -28,7 +32,20 @@ step() {  # step NAME SECONDS CMD...
 PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
 run_stage() {
   case "$1" in
+    validate) for st in tests smoke bench rocprof_bench selflaunch2 selflaunch4; do run_stage $st || return $?; done ;;
     tests) step tests 1500 $PYT tests -m gpu ;;
+    bench_fp8) step bench_fp8 400 python bench.py --dtype float8_e4m3fn --steps 20 --warmup 5 --extra-steps 5 \
+                 --extra-warmup 2 && grep '^{' "$OUT/bench_fp8.log" > "$OUT/bench_fp8.json" ;;
+    native16k) step native16k 400 pytorch_distributed_matmul_benchmark_amd/runtime/pdmb_bench --gpus 1 \
+                 --sizes 16384 --check &&
+               step native16k_fp8 400 pytorch_distributed_matmul_benchmark_amd/runtime/pdmb_bench --gpus 1 \
+                 --sizes 16384 --dtype float8_e4m3fn --check ;;
+    final_table) for dt in bfloat16 float16 float32 float8_e4m3fn; do
+                   step final_$dt 500 python scripts/ab_kernels.py --dtype $dt --kernels auto,torch \
+                     --sizes 4096 8192 16384 --rounds 5 --iters 10 || return $?
+                   grep '^{' "$OUT/final_$dt.log" > "$OUT/final_$dt.jsonl"
+                 done ;;
+    pmc) (export OUT="$OUT/pmc"; mkdir -p "$OUT"; step pmc 1200 bash scripts/gpu_pmc.sh) ;;
     tests_signal) step tests_signal 600 $PYT tests/test_signal_gpu.py tests/test_overlap_gpu.py -m gpu ;;
     smoke) step smoke 180 python __graft_entry__.py smoke ;;
     bench) step bench 400 python bench.py && grep '^{' "$OUT/bench.log" > "$OUT/bench.json" ;;
@@ -52,7 +69,11 @@ run_stage() {
     tests_gemm) step tests_gemm 900 $PYT tests/test_gemm_gpu.py tests/test_modes_gpu.py -m gpu ;;
     tests_overlap) step tests_overlap 900 $PYT tests/test_signal_gpu.py tests/test_overlap_gpu.py \
                      tests/test_native_bench_gpu.py tests/test_multirank_gpu.py -m gpu ;;
-    ab_fp8) step ab_fp8 600 python scripts/ab_kernels.py --dtype float8_e4m3fn ;;
+    ab_fp8) step ab_fp8 900 python scripts/ab_kernels.py --dtype float8_e4m3fn --kernels auto,fp8_w4,torch \
+              --rounds 3 --shapes 6144,6144,6144 6000,6000,6144 7168,7168,7168 4096,4096,4096 \
+              8192,2048,8192 10240,10240,10240 16384,16384,16384 &&
+            grep '^{' "$OUT/ab_fp8.log" > "$OUT/ab_fp8.jsonl" ;;
+    tests_fp8) step tests_fp8 600 $PYT tests/test_fp8_gpu.py -m gpu ;;
     *) echo "unknown stage $1"; return 2 ;;
   esac
 }

@@ -291,3 +291,28 @@ def test_fp8_tile_family_edge_tiles(kernel, M, N, K, splitk):
     gemm.matmul(A8, B8, out=out, kernel=kernel, splitk=splitk, alpha=0.5)
     assert torch.equal(out, (0.5 * (Af.double() @ Bf.double())).to(torch.bfloat16))
     assert torch.isnan(big[:, N:]).all() and torch.isnan(big[M:]).all()
+
+
+@pytest.mark.parametrize("M,N,K", [(6144, 6144, 6144), (6000, 6000, 6144), (7168, 7168, 1024)])
+def test_fp8_wave_tail_split(M, N, K):
+    """fp8 wave-quantisation tail (gemm_dispatch.cpp tail_plan on fp8 W4): the
+    whole-wave rows as one fp8 W4 / W4S launch, the last tile rows split-K in a
+    second; exact on small integers (alpha folded in), nothing written outside
+    C, the same bits every launch and under graph replay."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    Af, Bf = _ints((M, K), g, -2, 3), _ints((K, N), g, -2, 3)
+    A8, B8 = Af.to(FP8), _colmajor(Bf.to(FP8))
+    big = torch.full((M + 16, N + 24), float("nan"), device="cuda", dtype=torch.bfloat16)
+    out = big[:M, :N]
+    m1, S = gemm.tail_split_for(A8, B8, out)
+    if K == 6144:
+        assert 0 < m1 < M and m1 % 256 == 0 and S in (2, 4), (m1, S)
+    gemm.matmul(A8, B8, out=out, alpha=0.5)
+    ref = (0.5 * (Af.double() @ Bf.double())).to(torch.bfloat16)
+    assert torch.equal(out, ref)
+    assert torch.isnan(big[:, N:]).all() and torch.isnan(big[M:]).all()
+    for _ in range(3):
+        assert torch.equal(gemm.matmul(A8, B8, alpha=0.5), ref)
+    C2 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    assert gemm.bench_matmul(A8, B8, C2, 3, 1, graph=True) > 0
+    assert torch.equal(C2, (Af.double() @ Bf.double()).to(torch.bfloat16))

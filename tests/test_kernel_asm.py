@@ -81,7 +81,7 @@ def test_w4_kernel_agpr_accumulators_and_counted_waits(tmp_path):
     counted vmcnt(16) waits at the two barriers of each K-tile and one vmcnt(0) drain."""
     ks = _kernels("gemm_w4.hip", tmp_path)
     for dt, mfma in (("ILi2E", "v_mfma_f32_16x16x32_bf16"), ("ILi1E", "v_mfma_f32_16x16x32_f16")):
-        name = [k for k in ks if "gemm_w4_nn" in k and dt in k]
+        name = [k for k in ks if "gemm_w4_nn" in k and dt in k and "Lb1ELb0EE" in k]  # not signalled
         assert name, sorted(ks)
         k = ks[name[0]]
         b = k["body"]
@@ -97,6 +97,32 @@ def test_w4_kernel_agpr_accumulators_and_counted_waits(tmp_path):
         # loop body: 2 K-tiles x 8 blocks x 16 MFMAs, one odd tail K-tile, the fused last K-tile
         assert len(re.findall(mfma, b)) == 4 * 128
         assert len(re.findall(r"buffer_load_dwordx4 .* lds", b)) >= 3 * 16
+
+
+def test_w4_signalled_variant_publishes_write_through(tmp_path):
+    """gemm_w4.hip SIG (completion signals, parallel/overlap.py): every C store is a
+    write-through (sc1) buffer store — none of the plain / non-temporal global
+    stores of the shipping epilogue — the K-loop is the plain kernel's, and each
+    workgroup's signal is one returning agent atomic add behind an explicit
+    vmcnt(0) drain and a barrier, then a system-scope flag store."""
+    ks = _kernels("gemm_w4.hip", tmp_path)
+    for dt in ("ILi2E", "ILi1E"):
+        sig = [k for k in ks if "gemm_w4_nn" in k and dt in k and "Lb1ELb1EE" in k]
+        plain = [k for k in ks if "gemm_w4_nn" in k and dt in k and "Lb1ELb0EE" in k]
+        assert sig and plain, sorted(ks)
+        b, p = ks[sig[0]]["body"], ks[plain[0]]["body"]
+        assert ks[sig[0]]["spill"] == 0 and ks[sig[0]]["vgpr"] <= 256
+        assert not re.findall(r"global_store_dwordx4", b)  # C leaves only as sc1 buffer stores
+        assert len(re.findall(r"buffer_store_dwordx4 .* sc1", b)) >= 2 * 64
+        assert len(re.findall(r"s_waitcnt vmcnt\(16\) lgkmcnt\(0\)", b)) == \
+            len(re.findall(r"s_waitcnt vmcnt\(16\) lgkmcnt\(0\)", p))
+        # the signal's own drain (asm, invisible to the compiler) on top of the plain kernel's
+        drain = r";;#ASMSTART\s+s_waitcnt vmcnt\(0\)\s+;;#ASMEND"
+        assert len(re.findall(drain, b)) == len(re.findall(drain, p)) + 1
+        i_flag = b.find("sc0 sc1")  # the system-scope host-flag store
+        i_add = b.rfind("global_atomic_add", 0, i_flag)  # the slot counter add it follows
+        assert 0 <= i_add < i_flag and " sc0" in b[i_add:b.find("\n", i_add)]  # returning add
+        assert b[i_add:i_flag].count("s_waitcnt vmcnt(0)") >= 1  # the flag waits for the add
 
 
 def test_default_build_has_no_experiment_kernels(tmp_path):

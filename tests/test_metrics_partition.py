@@ -89,10 +89,3 @@ def test_row_chunks(m, chunks):
     assert len(rc) <= max(chunks, 1)
     assert all(s % 256 == 0 for s, _ in rc)
 
-
-def test_effective_chunks_keeps_full_waves():
-    assert P.effective_chunks(16384, 16384, 4) == 4          # 4096 tiles
-    assert P.effective_chunks(16384, 2048, 4) == 2           # ws=8 matrix_parallel shard: 512 tiles
-    assert P.effective_chunks(4096, 4096, 4) == 1            # 256 tiles: one wave only
-    assert P.effective_chunks(4096, 512, 8) == 1             # fewer tiles than CUs
-    assert P.effective_chunks(16384, 16384, 64) == 16
