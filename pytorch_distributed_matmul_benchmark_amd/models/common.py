@@ -101,7 +101,7 @@ def kernel_label(w: Workload, A, B, out, shared: bool = False) -> str:
         return "torch._scaled_mm(hipBLASLt)" if w.dtype == _gemm.FP8 else "torch.matmul(hipBLASLt)"
     with (_gemm.shared_device() if shared else contextlib.nullcontext()):
         if w.kernel == "auto":
-            padded = _gemm.padded_kernel_for(A, B)
+            padded = _gemm.padded_kernel_for(A, B, out)
             if padded:
                 return f"{padded} (zero-padded K/N)"
         return _gemm.kernel_for(A, B, out, kernel=w.kernel)

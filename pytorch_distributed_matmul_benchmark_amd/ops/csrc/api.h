@@ -102,6 +102,9 @@ struct Problem {
   struct Signal* sig = nullptr;
   int sig_rows = 0;
   unsigned sig_epoch = 0;
+  // Rows of B holding data (0: all K). The padded path sets it to the caller's
+  // K when it pads only A's K (B read in place, rows past K zero by extent).
+  int kb = 0;
 };
 
 // Completion-signal set of `slots` slots on `device`: device counters
@@ -129,6 +132,13 @@ int signal_granule(const Problem& p, int kernel);
 // (device, stream), created on first use and left zeroed by every launch
 // (launches on one stream never overlap). kMaxSplitTiles bounds the tiles of
 // one split-K launch.
+// Graphs: a split-K launch captured on stream s bakes s's counter block into
+// the graph (a stream still capturing with no block yet runs unsplit instead:
+// hipMalloc is not capturable). Two replays of graphs captured on the same
+// stream, or a replay beside eager split-K launches on that stream, must
+// therefore not run concurrently — they would share arrival counters. The
+// library's own timing loop (bench_gemm) captures on a private stream and
+// replays one graph at a time.
 constexpr int kMaxSplitTiles = 4096;
 
 // Kernel an `auto` call runs through zero-padded workspace copies (the

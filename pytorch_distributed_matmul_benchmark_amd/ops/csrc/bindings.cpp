@@ -37,22 +37,27 @@ void check_hip(hipError_t e, const char* what) {
 // C: [M,N] | [b,M,N]; innermost stride must be 1 (leading dims free).
 // float8_e4m3fn: B must be column-major (stride(-2) == 1, e.g. Bt.t() of a
 // row-major [N,K] Bt) and C is bfloat16.
-pdmb::Problem make_problem(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C,
+// Cp == nullptr: a probe-only Problem (kernel_for / splitk_for / ... without
+// an `out`): C is taken as a contiguous [batch,] M x N at a 256-B aligned
+// stand-in address the planner only checks for alignment — nothing is
+// allocated just to ask which kernel would run.
+pdmb::Problem make_problem(const at::Tensor& A, const at::Tensor& B, const at::Tensor* Cp,
                            double alpha = 1.0) {
-  TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "pdmb: tensors must be on the GPU");
-  TORCH_CHECK(A.device() == B.device() && A.device() == C.device(), "pdmb: device mismatch");
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && (!Cp || Cp->is_cuda()), "pdmb: tensors must be on the GPU");
+  TORCH_CHECK(A.device() == B.device() && (!Cp || A.device() == Cp->device()), "pdmb: device mismatch");
   const bool fp8 = A.scalar_type() == at::kFloat8_e4m3fn;
   TORCH_CHECK(A.scalar_type() == B.scalar_type() &&
-                  C.scalar_type() == (fp8 ? at::kBFloat16 : A.scalar_type()),
+                  (!Cp || Cp->scalar_type() == (fp8 ? at::kBFloat16 : A.scalar_type())),
               "pdmb: dtype mismatch (fp8 operands take a bfloat16 output)");
   TORCH_CHECK(A.dim() == 2 || A.dim() == 3, "pdmb: A must be 2-D or 3-D");
   TORCH_CHECK(B.dim() == 2 || B.dim() == 3, "pdmb: B must be 2-D or 3-D");
-  TORCH_CHECK(C.dim() == std::max(A.dim(), B.dim()), "pdmb: bad output rank");
-  const bool batched = C.dim() == 3;
-  const int64_t batch = batched ? C.size(0) : 1;
+  const int64_t cdim = Cp ? Cp->dim() : std::max(A.dim(), B.dim());
+  TORCH_CHECK(cdim == std::max(A.dim(), B.dim()), "pdmb: bad output rank");
+  const bool batched = cdim == 3;
+  const int64_t batch = batched ? (Cp ? Cp->size(0) : (A.dim() == 3 ? A.size(0) : B.size(0))) : 1;
   const int64_t M = A.size(-2), K = A.size(-1), N = B.size(-1);
   TORCH_CHECK(B.size(-2) == K, "pdmb: inner dimensions differ: ", A.sizes(), " @ ", B.sizes());
-  TORCH_CHECK(C.size(-2) == M && C.size(-1) == N, "pdmb: output shape mismatch");
+  TORCH_CHECK(!Cp || (Cp->size(-2) == M && Cp->size(-1) == N), "pdmb: output shape mismatch");
   if (batched) {
     TORCH_CHECK(A.dim() == 2 || A.size(0) == batch, "pdmb: batch mismatch");
     TORCH_CHECK(B.dim() == 2 || B.size(0) == batch, "pdmb: batch mismatch");
@@ -63,7 +68,7 @@ pdmb::Problem make_problem(const at::Tensor& A, const at::Tensor& B, const at::T
   auto colmajor_ok = [](const at::Tensor& t) {
     return t.size(-2) <= 1 || t.stride(-2) == 1;
   };
-  TORCH_CHECK(inner_ok(A) && (fp8 ? colmajor_ok(B) : inner_ok(B)) && inner_ok(C),
+  TORCH_CHECK(inner_ok(A) && (fp8 ? colmajor_ok(B) : inner_ok(B)) && (!Cp || inner_ok(*Cp)),
               fp8 ? "pdmb: fp8 needs row-major A / C and column-major B"
                   : "pdmb: innermost dim must be contiguous");
   // Leading dimension = the real row stride. A row stride below the row
@@ -77,13 +82,13 @@ pdmb::Problem make_problem(const at::Tensor& A, const at::Tensor& B, const at::T
                 " < row length ", cols, " (overlapping or expanded view)");
     return t.stride(-2);
   };
-  TORCH_CHECK(!batched || C.size(0) <= 1 || C.stride(0) >= C.size(-2) * ld(C, "out"),
+  TORCH_CHECK(!Cp || !batched || Cp->size(0) <= 1 || Cp->stride(0) >= Cp->size(-2) * ld(*Cp, "out"),
               "pdmb: out batch stride overlaps (expanded or aliased output)");
   pdmb::Problem p{};
   p.dtype = dtype_code(A.scalar_type());
   p.A = A.data_ptr();
   p.B = B.data_ptr();
-  p.C = C.data_ptr();
+  p.C = Cp ? Cp->data_ptr() : (void*)(uintptr_t)256;
   p.M = (int)M;
   p.N = (int)N;
   p.K = (int)K;
@@ -96,10 +101,10 @@ pdmb::Problem make_problem(const at::Tensor& A, const at::Tensor& B, const at::T
     p.ldb = (int)ld(B, "B");
   }
   p.alpha = (float)alpha;
-  p.ldc = (int)ld(C, "out");
+  p.ldc = Cp ? (int)ld(*Cp, "out") : (int)std::max<int64_t>(N, 1);
   p.sA = (batched && A.dim() == 3) ? A.stride(0) : 0;
   p.sB = (batched && B.dim() == 3) ? B.stride(0) : 0;
-  p.sC = batched ? C.stride(0) : 0;
+  p.sC = batched ? (Cp ? Cp->stride(0) : M * N) : 0;
   p.batch = (int)batch;
   return p;
 }
@@ -125,6 +130,8 @@ at::Tensor workspace_for(pdmb::Problem& p, int kernel, const at::Tensor& like) {
   return ws;
 }
 
+const at::Tensor* opt(const c10::optional<at::Tensor>& C) { return C.has_value() ? &*C : nullptr; }
+
 pdmb::Signal* as_signal(int64_t h) { return reinterpret_cast<pdmb::Signal*>((uintptr_t)h); }
 
 // sig (a signal_create handle, 0 = none), sig_rows, sig_epoch: the launch
@@ -133,7 +140,7 @@ at::Tensor matmul(const at::Tensor& A, const at::Tensor& B, c10::optional<at::Te
                   int64_t kernel, double alpha, int64_t splitk, int64_t cus, int64_t sig,
                   int64_t sig_rows, int64_t sig_epoch) {
   at::Tensor C = out.has_value() ? *out : alloc_out(A, B);
-  pdmb::Problem p = make_problem(A, B, C, alpha);
+  pdmb::Problem p = make_problem(A, B, &C, alpha);
   p.splitk = (int)splitk;
   p.cus = (int)cus;
   if (sig) {
@@ -174,28 +181,31 @@ int64_t signal_flag(int64_t h, int64_t slot) {
 }
 
 // Tile rows per completion unit (0: the problem cannot run signalled).
-int64_t signal_granule(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t kernel,
+int64_t signal_granule(const at::Tensor& A, const at::Tensor& B, c10::optional<at::Tensor> C, int64_t kernel,
                        int64_t cus) {
-  pdmb::Problem p = make_problem(A, B, C);
+  pdmb::Problem p = make_problem(A, B, opt(C));
   p.cus = (int)cus;
   return pdmb::signal_granule(p, (int)kernel);
 }
 
-int64_t resolve(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t kernel,
+int64_t resolve(const at::Tensor& A, const at::Tensor& B, c10::optional<at::Tensor> C, int64_t kernel,
                 int64_t cus) {
-  pdmb::Problem p = make_problem(A, B, C);
+  pdmb::Problem p = make_problem(A, B, opt(C));
   p.cus = (int)cus;
   return pdmb::resolve_kernel(p, (int)kernel);
 }
 
-int64_t resolve_padded(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C) {
-  return pdmb::resolve_padded(make_problem(A, B, C));
+int64_t resolve_padded(const at::Tensor& A, const at::Tensor& B, c10::optional<at::Tensor> C,
+                       int64_t cus) {
+  pdmb::Problem p = make_problem(A, B, opt(C));
+  p.cus = (int)cus;
+  return pdmb::resolve_padded(p);
 }
 
 // K slices the W4 / T128 kernel would use (1 = no split; 0 if neither runs it).
-int64_t splitk_for(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t kernel,
+int64_t splitk_for(const at::Tensor& A, const at::Tensor& B, c10::optional<at::Tensor> C, int64_t kernel,
                    int64_t splitk, int64_t cus) {
-  pdmb::Problem p = make_problem(A, B, C);
+  pdmb::Problem p = make_problem(A, B, opt(C));
   p.splitk = (int)splitk;
   p.cus = (int)cus;
   return pdmb::choose_splitk(p, (int)kernel);
@@ -203,8 +213,8 @@ int64_t splitk_for(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C
 
 // {M1, S}: auto runs rows [0, M1) unsplit and [M1, M) split S ways; {0, 1}: one launch.
 std::tuple<int64_t, int64_t> tail_split_for(const at::Tensor& A, const at::Tensor& B,
-                                            const at::Tensor& C, int64_t kernel, int64_t cus) {
-  pdmb::Problem p = make_problem(A, B, C);
+                                            c10::optional<at::Tensor> C, int64_t kernel, int64_t cus) {
+  pdmb::Problem p = make_problem(A, B, opt(C));
   p.cus = (int)cus;
   const auto t = pdmb::tail_split(p, (int)kernel);
   return {t.first, t.second};
@@ -237,7 +247,7 @@ std::tuple<int64_t, int64_t, double, int64_t, int64_t> plan_shape(int64_t dtype,
 // Total milliseconds for `iters` timed launches (after `warmup`).
 double bench(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t iters,
              int64_t warmup, bool graph, int64_t kernel, int64_t splitk) {
-  pdmb::Problem p = make_problem(A, B, C);
+  pdmb::Problem p = make_problem(A, B, &C);
   p.splitk = (int)splitk;
   TORCH_CHECK(pdmb::resolve_kernel(p, (int)kernel) >= 0, "pdmb: kernel cannot run this problem");
   c10::hip::HIPGuard guard(A.device().index());
@@ -323,17 +333,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("signal_wait", &signal_wait, py::arg("handle"), py::arg("slot"), py::arg("epoch"),
         py::arg("timeout_s"));
   m.def("signal_flag", &signal_flag, py::arg("handle"), py::arg("slot"));
-  m.def("signal_granule", &signal_granule, py::arg("A"), py::arg("B"), py::arg("out"),
+  m.def("signal_granule", &signal_granule, py::arg("A"), py::arg("B"), py::arg("out") = py::none(),
         py::arg("kernel") = 0, py::arg("cus") = 0);
   m.def("resolve", &resolve, "kernel id that would run (or -1)", py::arg("A"), py::arg("B"),
-        py::arg("out"), py::arg("kernel") = 0, py::arg("cus") = 0);
+        py::arg("out") = py::none(), py::arg("kernel") = 0, py::arg("cus") = 0);
   m.def("resolve_padded", &resolve_padded, "kernel the padded fast path runs (or -1)",
-        py::arg("A"), py::arg("B"), py::arg("out"));
+        py::arg("A"), py::arg("B"), py::arg("out") = py::none(), py::arg("cus") = 0);
   m.def("splitk_for", &splitk_for, "W4 K slices for this problem (0: not W4)", py::arg("A"),
-        py::arg("B"), py::arg("out"), py::arg("kernel") = 0, py::arg("splitk") = 0,
+        py::arg("B"), py::arg("out") = py::none(), py::arg("kernel") = 0, py::arg("splitk") = 0,
         py::arg("cus") = 0);
   m.def("tail_split_for", &tail_split_for, "auto's wave-quantisation tail {M1, S} ({0, 1}: none)",
-        py::arg("A"), py::arg("B"), py::arg("out"), py::arg("kernel") = 0, py::arg("cus") = 0);
+        py::arg("A"), py::arg("B"), py::arg("out") = py::none(), py::arg("kernel") = 0,
+        py::arg("cus") = 0);
   m.def("bench", &bench, "native hipEvent timing loop; returns total ms", py::arg("A"),
         py::arg("B"), py::arg("out"), py::arg("iters"), py::arg("warmup"),
         py::arg("graph") = false, py::arg("kernel") = 0, py::arg("splitk") = 0);

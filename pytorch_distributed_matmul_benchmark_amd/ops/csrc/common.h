@@ -83,6 +83,8 @@ struct GemmArgs {
   const void* B;
   void* C;
   int M, N, K;
+  int kb;  // rows of B holding data (<= K): rows [kb, K) read as zeros through the B
+           // descriptors' extent (the padded path's K tail: only A is copied)
   int lda, ldb, ldc;
   long long sA, sB, sC;
   int batch;

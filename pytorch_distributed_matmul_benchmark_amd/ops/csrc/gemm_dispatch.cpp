@@ -53,6 +53,7 @@ static GemmArgs to_args(const Problem& p) {
   a.sB = p.sB;
   a.sC = p.sC;
   a.batch = p.batch < 1 ? 1 : p.batch;
+  a.kb = p.kb > 0 && p.kb < p.K ? p.kb : p.K;
   a.dbg = g_debug_buffer;
   a.alpha = p.alpha;
   if (p.sig) {
@@ -645,10 +646,17 @@ static bool wants_padding(const Problem& p, int kernel) {
 // direct_c: only K is padded (N already on its granule) and the caller's C is
 // aligned, so the kernel writes C in place — no padded C, no unpad copy
 // (for 8192^2 x 1000 bf16 that copy moved 256 MB).
+// direct_b: N is on its granule and B's base, row pitch and batch stride meet
+// the fast kernels' 16-B alignment, so B is read in place: its rows past K
+// read as zeros through the DMA descriptors' extent (Problem::kb = K), and
+// only A is copied with zero columns K .. Kp (6000^2 x 6100 bf16: 293 MB of
+// copy traffic down to 147 MB). A's own columns past K cannot be left to the
+// next row's data: a non-finite value there would turn a 0-weighted product
+// into NaN.
 struct Padded {
   Problem q;
   size_t a_bytes, b_bytes, c_bytes, a_el, b_el, c_el;
-  bool direct_c;
+  bool direct_c, direct_b;
 };
 
 static Padded padded_problem(const Problem& p, char* w) {
@@ -661,8 +669,11 @@ static Padded padded_problem(const Problem& p, char* w) {
   d.c_el = (size_t)p.M * Np;
   d.direct_c = Np == p.N && (uintptr_t)p.C % 16 == 0 && p.ldc % 8 == 0 && p.ldc >= p.N &&
                (batch == 1 || p.sC % 8 == 0);
+  const int vec = (int)(16 / es);  // elements per 16 B
+  d.direct_b = Np == p.N && (uintptr_t)p.B % 16 == 0 && p.ldb % vec == 0 && p.ldb >= p.N &&
+               (batch == 1 || p.sB % vec == 0 || p.sB == 0);
   d.a_bytes = round_up(d.a_el * es * batch, 256);
-  d.b_bytes = round_up(d.b_el * es * batch, 256);
+  d.b_bytes = d.direct_b ? 0 : round_up(d.b_el * es * batch, 256);
   d.c_bytes = d.direct_c ? 0 : round_up(d.c_el * es * batch, 256);
   Problem& q = d.q;
   q = p;
@@ -684,6 +695,12 @@ static Padded padded_problem(const Problem& p, char* w) {
     q.C = p.C;
     q.ldc = p.ldc;
     q.sC = p.sC;
+  }
+  if (d.direct_b) {
+    q.B = p.B;
+    q.ldb = p.ldb;
+    q.sB = p.sB;
+    q.kb = p.K;
   }
   q.batch = batch;
   q.workspace = nullptr;
@@ -762,6 +779,7 @@ static hipError_t gemm_padded(const Problem& p, hipStream_t stream, int* used) {
     e = f32 ? pad_copy_launch<float>(A, p.lda, p.M, p.K, Ad, Kp, p.M, Kp, stream)
             : pad_copy_launch<unsigned short>(A, p.lda, p.M, p.K, Ad, Kp, p.M, Kp, stream);
     if (e != hipSuccess) return e;
+    if (d.direct_b) continue;  // read in place (rows past K: zeros by extent)
     e = f32 ? pad_copy_launch<float>(B, p.ldb, p.K, p.N, Bd, Np, Kp, Np, stream)
             : pad_copy_launch<unsigned short>(B, p.ldb, p.K, p.N, Bd, Np, Kp, Np, stream);
     if (e != hipSuccess) return e;

@@ -137,7 +137,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_f32_256(GemmArgs a) {
   c.Ab = (const char*)a.A + ((long long)bz * a.sA + (long long)m0 * a.lda) * 4;
   c.Bb = (const char*)a.B + ((long long)bz * a.sB + n0) * 4;
   c.a_bytes = ((long long)(a.M - m0 - 1) * a.lda + a.K) * 4;
-  c.b_bytes = ((long long)(a.K - 1) * a.ldb + (a.N - n0)) * 4;
+  c.b_bytes = ((long long)(a.kb - 1) * a.ldb + (a.N - n0)) * 4;
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
     const int r = (h * 8 + wu) * 8 + (lane >> 3);

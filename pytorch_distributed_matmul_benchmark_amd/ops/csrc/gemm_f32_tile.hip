@@ -202,7 +202,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_t128(GemmArgs a) {
   c.ra = make_rsrc((const char*)a.A + ((long long)bz * a.sA + (long long)m0 * a.lda + k0) * 4,
                    ((long long)(a.M - m0 - 1) * a.lda + (a.K - k0)) * 4);
   c.Bb = (const char*)a.B + ((long long)bz * a.sB + k0 * a.ldb + n0) * 4;
-  c.b_bytes = ((long long)(a.K - k0 - 1) * a.ldb + (a.N - n0)) * 4;
+  c.b_bytes = ((long long)(a.kb - k0 - 1) * a.ldb + (a.N - n0)) * 4;
   {
     const int r = wu * 8 + (lane >> 3);  // row of A piece 0 (the swizzle is 32-row periodic)
     c.voffA = (uint32_t)(r * c.lda4 + (((lane & 7) ^ ((r >> 1) & 7)) * 16));

@@ -164,7 +164,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4(GemmArgs a) {
   c.Ab = (const char*)a.A + ((long long)bz * a.sA + (long long)m0 * a.lda + k0) * 4;
   c.Bb = (const char*)a.B + ((long long)bz * a.sB + k0 * a.ldb + n0) * 4;
   c.a_bytes = ((long long)(a.M - m0 - 1) * a.lda + (a.K - k0)) * 4;
-  c.b_bytes = ((long long)(a.K - k0 - 1) * a.ldb + (a.N - n0)) * 4;
+  c.b_bytes = ((long long)(a.kb - k0 - 1) * a.ldb + (a.N - n0)) * 4;
   {
     const int r = wu * 8 + (lane >> 3);  // row of A piece 0
     c.voffA = (uint32_t)(r * c.lda4 + (((lane & 7) ^ ((r >> 1) & 7)) * 16));

@@ -384,7 +384,7 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm256_nn(GemmArgs a) {
   // its N / K, not at its leading dimension), so no DMA can touch memory
   // outside the tensor: rows >= M and the tail of B's last row read zeros.
   c.a_bytes = ((long long)(a.M - m0 - 1) * a.lda + a.K) * 2;
-  c.b_bytes = ((long long)(a.K - 1) * a.ldb + (a.N - n0)) * 2;
+  c.b_bytes = ((long long)(a.kb - 1) * a.ldb + (a.N - n0)) * 2;
 
   {
     const int lr8 = lane >> 3, lc8 = lane & 7;

@@ -374,7 +374,7 @@ __global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
   } else {
     c.rb = c.ra;
     c.Bb = (const char*)a.B + ((long long)bz * a.sB + (long long)k0 * a.ldb + n0) * 2;
-    c.b_bytes = ((long long)(a.K - k0 - 1) * a.ldb + (a.N - n0)) * 2;
+    c.b_bytes = ((long long)(a.kb - k0 - 1) * a.ldb + (a.N - n0)) * 2;
     const int r = wu * 8 + (lane >> 3), lc8 = lane & 7;  // row of A piece 0
     c.voffA = (uint32_t)(r * c.lda2 + ((lc8 ^ ((r >> 1) & 7)) * 16));
     const int lr16 = lane >> 4, lc16 = lane & 15;

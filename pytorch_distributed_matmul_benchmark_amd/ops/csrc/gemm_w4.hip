@@ -309,7 +309,7 @@ __device__ __forceinline__ unsigned w4_tile(const GemmArgs& a, char* smem, int v
   const char* Ab = (const char*)a.A + ((long long)bz * a.sA + (long long)m0 * a.lda + k0) * 2;
   c.ra = make_rsrc(Ab, ((long long)(a.M - m0 - 1) * a.lda + (a.K - k0)) * 2);
   c.Bb = (const char*)a.B + ((long long)bz * a.sB + (long long)k0 * a.ldb + n0) * 2;
-  c.b_bytes = ((long long)(a.K - k0 - 1) * a.ldb + (a.N - n0)) * 2;
+  c.b_bytes = ((long long)(a.kb - k0 - 1) * a.ldb + (a.N - n0)) * 2;
   {
     const int r = wu * 8 + (lane >> 3), lc8 = lane & 7;  // row of A piece 0
     c.voffA = (uint32_t)(r * c.lda2 + ((lc8 ^ ((r >> 1) & 7)) * 16));
@@ -553,7 +553,7 @@ __device__ __forceinline__ Src tile_src(const GemmArgs& a, int bz, int tm, int t
   s.ra = make_rsrc((const char*)a.A + ((long long)bz * a.sA + (long long)m0 * a.lda) * 2,
                    ((long long)(a.M - m0 - 1) * a.lda + a.K) * 2);
   s.Bb = (const char*)a.B + ((long long)bz * a.sB + n0) * 2;
-  s.b_bytes = ((long long)(a.K - 1) * a.ldb + (a.N - n0)) * 2;
+  s.b_bytes = ((long long)(a.kb - 1) * a.ldb + (a.N - n0)) * 2;
   return s;
 }
 

@@ -215,8 +215,6 @@ def signal_granule(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor]
     if A.device.type != "cuda" or A.dtype not in (torch.bfloat16, torch.float16):
         return 0
     C = _native.load()
-    if out is None:
-        out = torch.empty(_out_shape(A, B), dtype=out_dtype(A.dtype), device=A.device)
     A, B = _prep_pair(A, B)
     return int(C.signal_granule(A, B, out, _kid(kernel), _cus()))
 
@@ -272,14 +270,15 @@ def matmul(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
 PAD_MIN_FLOPS = 2.0 ** 31  # gemm_dispatch.cpp kPadMinFlops
 
 
-def padded_kernel_for(A: torch.Tensor, B: torch.Tensor) -> Optional[str]:
-    """Fast kernel an ``auto`` call runs through zero-padded copies, or None."""
+def padded_kernel_for(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None
+                      ) -> Optional[str]:
+    """Fast kernel an ``auto`` call runs through zero-padded copies, or None
+    (under the caller's CU budget / shared-device context, like ``matmul``)."""
     if A.device.type != "cuda" or A.dtype not in SUPPORTED_DTYPES:
         return None
     C = _native.load()
-    out = torch.empty(_out_shape(A, B), dtype=out_dtype(A.dtype), device=A.device)
     A, B = _prep_pair(A, B)
-    k = int(C.resolve_padded(A, B, out))
+    k = int(C.resolve_padded(A, B, out, _cus()))
     return _name(C, k) if k >= 0 else None
 
 
@@ -299,8 +298,6 @@ def kernel_for(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = N
     if A.device.type != "cuda":
         return "torch.matmul(cpu)"
     C = _native.load()
-    if out is None:
-        out = torch.empty(_out_shape(A, B), dtype=out_dtype(A.dtype), device=A.device)
     A, B = _prep_pair(A, B)
     return _name(C, int(C.resolve(A, B, out, _kid(kernel), _cus())))
 
@@ -316,8 +313,6 @@ def splitk_for(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = N
     if A.device.type != "cuda":
         return 0
     C = _native.load()
-    if out is None:
-        out = torch.empty(_out_shape(A, B), dtype=out_dtype(A.dtype), device=A.device)
     A, B = _prep_pair(A, B)
     return int(C.splitk_for(A, B, out, _kid(kernel), int(splitk), _cus()))
 
@@ -330,8 +325,6 @@ def tail_split_for(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor]
     if A.device.type != "cuda":
         return (0, 1)
     C = _native.load()
-    if out is None:
-        out = torch.empty(_out_shape(A, B), dtype=out_dtype(A.dtype), device=A.device)
     A, B = _prep_pair(A, B)
     m1, s = C.tail_split_for(A, B, out, _kid(kernel), _cus())
     return (int(m1), int(s))

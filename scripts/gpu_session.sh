@@ -61,7 +61,9 @@ run_stage() {
                    --warmup 1 --extra-steps 2 --extra-warmup 1 ;;
     gpus2_refused) echo "== gpus2_refused"; timeout -k 10 120 python bench.py --gpus 2 > "$OUT/gpus2_refused.log" 2>&1
                    local rc=$?; cat "$OUT/gpus2_refused.log"; echo "== gpus2_refused rc=$rc (want 2)"; [ $rc -eq 2 ] ;;
-    ab_bf16) step ab_bf16 600 python scripts/ab_kernels.py --dtype bfloat16 ;;
+    ab_bf16) step ab_bf16 900 python scripts/ab_kernels.py --dtype bfloat16 --kernels auto,torch --rounds 5 \
+               --shapes 6000,6000,6100 8192,8192,1000 12345,12345,12345 6000,6000,6144 2048,2048,2049 \
+               16384,16384,16384 && grep '^{' "$OUT/ab_bf16.log" > "$OUT/ab_bf16.jsonl" ;;
     ab_fp32) step ab_fp32 900 python scripts/ab_kernels.py --dtype float32 --kernels auto,f32_w4,f32_t128,torch \
                --rounds 3 --shapes 4096,2048,4096 4096,1024,4096 4096,512,4096 2048,2048,2048 6144,6144,6144 \
                8192,8192,8192 16384,16384,16384 &&

@@ -814,3 +814,29 @@ def test_streaming_kernels_in_graphs():
     graph8.replay()
     torch.cuda.synchronize()
     assert torch.equal(out8, R)
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
+@pytest.mark.parametrize("M,N,K,batch,bcast", [(1500, 1024, 1000, 1, False), (700, 512, 1000, 3, False),
+                                               (700, 512, 1000, 3, True), (6000, 6000, 6100, 1, False),
+                                               (2048, 2048, 2049, 1, False),  # K % 64 == 1
+                                               (1000, 1024, 1055, 1, False),  # K % 64 == 31
+                                               (1000, 1024, 1087, 1, False)])  # K % 64 == 63
+def test_padded_k_reads_b_in_place(dtype, M, N, K, batch, bcast):
+    """K off the granule with an aligned B: only A is copied (zero columns K ..
+    Kp); B is read in place and its rows past K come in as zeros through the
+    DMA descriptors' extent — even when the memory after B's last row holds inf
+    (B a view of a bigger buffer). Exact on small integers."""
+    dt = DT[dtype]
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + batch)
+    lead = (batch,) if batch > 1 else ()
+    A = torch.randint(-3, 4, lead + (M, K), device="cuda", generator=g).to(dt)
+    blead = () if bcast else lead
+    big = torch.full(blead + (K + 37, N), float("inf"), device="cuda", dtype=dt)
+    big[..., :K, :] = torch.randint(-3, 4, blead + (K, N), device="cuda", generator=g).to(dt)
+    B = big[..., :K, :]
+    assert gemm.kernel_for(A, B) == "pdmb_generic_nn" and gemm.padded_kernel_for(A, B) is not None
+    C = gemm.matmul(A, B)
+    R = torch.matmul(A.double(), B.double())
+    assert torch.isfinite(C).all()
+    assert torch.equal(C, R.to(dt))
