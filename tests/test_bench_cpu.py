@@ -153,3 +153,63 @@ def test_bench_fault_exits_fast(spec):
     assert r.returncode != 0
     assert time.time() - t0 < 90
     assert "injected fault" in r.stderr
+
+
+_NO_HIP = """
+import runpy, sys, torch
+sys.path.insert(0, {root!r})
+def boom(*a, **k):
+    raise RuntimeError("the self-launch parent touched HIP")
+torch._C._cuda_getDeviceCount = boom
+torch.cuda.device_count = boom
+torch.cuda.is_available = boom
+{extra}
+sys.argv = ["bench.py"] + {args!r}
+runpy.run_path({path!r}, run_name="__main__")
+"""
+
+
+def _parent_without_hip(args, extra=""):
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    code = _NO_HIP.format(extra=extra, args=list(args), path=os.path.join(ROOT, "bench.py"), root=ROOT)
+    return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                          cwd="/tmp", env=env)
+
+
+def test_self_launch_parent_never_counts_gpus_through_hip():
+    """The --gpus N parent counts GPUs from sysfs / amdsmi only (utils/telemetry.py):
+    with HIP's device count patched to raise it still self-launches 4 ranks, and
+    on a box with too few GPUs it refuses with rc 2 at once."""
+    r = _parent_without_hip(["--device", "cpu", "--gpus", "4", "--size", "128", "--steps", "1",
+                             "--warmup", "0", "--extra-steps", "0"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert _line(r)["n_gpus"] == 4
+    r = _parent_without_hip(["--gpus", "2", "--size", "128"],
+                            extra="import pytorch_distributed_matmul_benchmark_amd.utils.telemetry as t;"
+                                  " t.visible_gpus = lambda: 1")
+    assert r.returncode == 2 and "only 1 GPU" in r.stderr, r.stderr[-2000:]
+
+
+def test_bench_json_verifiability_fields():
+    """ws = 1 (no process group) and ws = 2 (gloo) lines carry every field the
+    driver needs to check a multi-GPU run: backend, world size the group saw,
+    RCCL version, collective self-test, per-rank TFLOPS, per-mode split / plan /
+    warm-up and the rank-0-alone references."""
+    keys = ("dist_backend", "world_size_seen", "rccl_version", "collectives_verified",
+            "per_rank_tflops", "sclk_mhz", "power_w")
+    d1 = _line(_plain("--size", "128", "--steps", "1", "--warmup", "0", "--extra-steps", "1",
+                      "--extra-warmup", "0"))
+    assert all(k in d1 for k in keys)
+    assert d1["world_size_seen"] == 1 and d1["dist_backend"] is None
+    d2 = _bench(2, "--size", "128", "--steps", "1", "--warmup", "0", "--extra-steps", "1",
+                "--extra-warmup", "0", "--chunks", "1")
+    assert d2["dist_backend"] == "gloo" and d2["world_size_seen"] == 2
+    assert d2["collectives_verified"] is True
+    assert d2["per_rank_tflops"]["min"] <= d2["per_rank_tflops"]["max"]
+    for key in ("batch_parallel", "matrix_parallel"):
+        m = d2["modes"][key]
+        assert m["compute_ms"] >= 0 and m["comm_ms"] >= 0 and "warmup_ms" in m
+        assert m["ref_tflops_rank0_alone"] > 0 and m["scaling_efficiency"] is not None
+    assert d2["modes"]["batch_parallel+overlap"]["plan"]["overlap"] is True  # --chunks 1: requested
