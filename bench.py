@@ -378,6 +378,7 @@ class Workload:
             for _ in range(steps):
                 self.step()
             self.finish()
+            issued = time.perf_counter() - t0  # host time to enqueue every step
             self._sync()
             barrier(self.ctx)
             self._sync()
@@ -388,7 +389,9 @@ class Workload:
             t = torch.tensor([elapsed], dtype=torch.float64, device=self.ctx.device)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
-        return elapsed, mine, smp.result()
+        tel = smp.result()
+        tel["host_issue_ms"] = issued * 1e3
+        return elapsed, mine, tel
 
     def close(self):
         if self.pipe is not None:
@@ -490,7 +493,10 @@ def _measure(a, ctx, mode: str, overlap: bool, warmup: int, steps: int, key: str
                 warmup_ms=round(wms, 1),
                 per_rank_tflops={"min": round(min(rates), 4), "max": round(max(rates), 4)},
                 sclk_mhz=tel["sclk_mhz"], power_w=tel["power_w"],
-                sclk_mhz_min_over_ranks=(round(min(clocks), 1) if min(clocks) > 0 else None))
+                sclk_mhz_min_over_ranks=(round(min(clocks), 1) if min(clocks) > 0 else None),
+                # host enqueue time per step (rank max) against ms_per_step: a host-bound
+                # schedule shows host_issue close to the step time with the GPU waiting
+                host_issue_ms_per_step=round(max(gather_scalars(ctx, tel["host_issue_ms"])) / steps, 4))
     if comp is not None:
         info["compute_ms"], info["comm_ms"] = round(comp, 4), round(comm, 4)
     if w.plan is not None:
