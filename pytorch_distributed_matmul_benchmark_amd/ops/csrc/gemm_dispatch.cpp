@@ -713,7 +713,33 @@ int resolve_padded(const Problem& p) {
   return resolve_kernel(padded_problem(p, nullptr).q, kAuto);
 }
 
+// ---- batched streaming GEMMs: one launch per element -------------------------
+// A batched problem that auto runs on W4S / fp8 W4S, with every element alone
+// >= 2 tiles per CU, runs as one launch per element on the stream, each
+// element planned alone (its wave tail included), all on one workspace
+// (stream-ordered). Measured in one process (profiles/r3_batch_seq_ab.jsonl):
+// bmm of 4 16k bf16 as one launch 1444 TF, as four launches 1515 TF.
+static bool batch_split(const Problem& p, int kernel) {
+  if (kernel != kAuto || p.batch <= 1 || p.sig || p.splitk != 0) return false;
+  Problem q = p;
+  q.batch = 1;
+  const int k = resolve_kernel(q, kAuto);
+  return k == kMfmaW4S || k == kFp8W4S;
+}
+
+static Problem batch_elem(const Problem& p, int b) {
+  const size_t esa = p.dtype == kFP8 ? 1 : p.dtype == kF32 ? 4 : 2;  // fp8: e4m3 A / B
+  const size_t esc = p.dtype == kF32 ? 4 : 2;                         // fp8: bf16 C
+  Problem q = p;
+  q.batch = 1;
+  q.A = (const char*)p.A + (size_t)b * p.sA * esa;
+  q.B = (const char*)p.B + (size_t)b * p.sB * esa;
+  q.C = (char*)p.C + (size_t)b * p.sC * esc;
+  return q;
+}
+
 size_t gemm_workspace_bytes(const Problem& p, int kernel) {
+  if (!wants_padding(p, kernel) && batch_split(p, kernel)) return gemm_workspace_bytes(batch_elem(p, 0), kAuto);
   if (p.sig) {
     const int k = signal_kernel(p, kernel);
     return k < 0 ? 0 : splitk_bytes(p, kMfmaW4, plan(p, kMfmaW4).splitk);
@@ -853,6 +879,13 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
   if (used) *used = k;
   if (k < 0) return hipErrorInvalidValue;
   if (p.M == 0 || p.N == 0 || p.batch == 0) return hipSuccess;
+  if (p.K > 0 && batch_split(p, kernel)) {
+    for (int b = 0; b < p.batch; ++b) {
+      const hipError_t e = gemm(batch_elem(p, b), kAuto, stream, nullptr);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
   if (p.K > 0) {
     const TailPlan t = tail_plan(p, kernel);
     hipError_t e = hipSuccess;

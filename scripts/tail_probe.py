@@ -69,7 +69,10 @@ def main():
         flops = 2.0 * M * N * K * max(a.batch, 1)
 
         def vendor():
-            if fp8:
+            if fp8 and a.batch:  # _scaled_mm takes matrices only
+                for b in range(a.batch):
+                    torch._scaled_mm(A[b], B[b], one, one, out_dtype=torch.bfloat16, out=C[b])
+            elif fp8:
                 torch._scaled_mm(A, B, one, one, out_dtype=torch.bfloat16, out=C)
             else:
                 torch.matmul(A, B, out=C)

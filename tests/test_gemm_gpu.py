@@ -840,3 +840,32 @@ def test_padded_k_reads_b_in_place(dtype, M, N, K, batch, bcast):
     R = torch.matmul(A.double(), B.double())
     assert torch.isfinite(C).all()
     assert torch.equal(C, R.to(dt))
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float8_e4m3fn"])
+@pytest.mark.parametrize("bcast", [False, True])
+def test_batched_streaming_gemm_runs_per_element(dtype, bcast):
+    """A batch whose elements each fill >= 2 waves of W4S runs as one launch per
+    element (gemm_dispatch.cpp batch_split): exact on small integers, bitwise
+    equal to each element computed alone, B broadcast (stride 0) included; the
+    native timing loop takes the same path."""
+    g = torch.Generator(device="cuda").manual_seed(11)
+    M, N, K, b = 8192, 4096, 1024, 3
+    A = torch.randint(-1, 2, (b, M, K), device="cuda", generator=g).float()  # |C| << 256: exact in bf16
+    B = torch.randint(-1, 2, ((1,) if bcast else (b,)) + (K, N), device="cuda", generator=g).float()
+    if dtype == "float8_e4m3fn":
+        A8 = A.to(torch.float8_e4m3fn)
+        B8 = B.transpose(-1, -2).contiguous().to(torch.float8_e4m3fn).transpose(-1, -2)
+    else:
+        A8, B8 = A.to(torch.bfloat16), B.to(torch.bfloat16)
+    if bcast:
+        B8 = B8.expand(b, K, N)
+    assert gemm.kernel_for(A8, B8) in ("pdmb_w4s", "pdmb_fp8_w4s")
+    C = gemm.matmul(A8, B8)
+    R = torch.matmul(A.double(), B.double())
+    assert torch.equal(C.double(), R.expand_as(C.double()) if bcast else R)
+    for i in range(b):
+        assert torch.equal(gemm.matmul(A8[i], B8[i]), C[i])
+    out = torch.empty_like(C)
+    gemm.bench_matmul(A8, B8, out, iters=2, warmup=1)
+    assert torch.equal(out, C)
