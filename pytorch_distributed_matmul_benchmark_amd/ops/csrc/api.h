@@ -25,6 +25,7 @@ enum Kernel : int {
   kFp8T128 = 41,      // gemm_tile.hip fp8: 128x128 tile, 4 waves x 64x64, split-K (M, N % 128)
   kFp8T256x128 = 42,  // gemm_tile.hip fp8: 256x128 tile, 4 waves x 128x64, split-K (M % 256, N % 128)
   kF32T128 = 51,      // gemm_f32_tile.hip: exact fp32, 128x128 tile, 4 waves x 64x64, split-K (any M, N % 4)
+  kF32T128x2 = 53,    // kF32T128 on 2 LDS stages, two workgroups per CU (grids of >= 2 tiles per CU)
 };
 
 // Experiment / diagnostic ids (A/B and timing-only builds). Compiled and
@@ -65,6 +66,8 @@ enum ExperimentKernel : int {
   kT128Unfused = 48,     // kT128 (bf16 / fp16) with the epilogue after the last K-tile
   kFp8T128Unfused = 49,  // kFp8T128 with the epilogue after the last K-tile
   kMfmaW4Unfused = 50,   // kMfmaW4 (bf16) with the epilogue after the last K-tile
+  kF32T128B32 = 52,      // kF32T128 with one b32 LDS read per B operand (round 3's first version)
+  kF32W4B32 = 54,        // kF32W4 with one b32 LDS read per B operand (round 2's version)
 };
 
 // True iff this library was built with the experiment kernels.

@@ -232,9 +232,13 @@ __device__ __forceinline__ void store_block16(char* buf, const f32x4 (&v)[NB], f
 template <int NB>
 constexpr int epi_buf_f32() { return 16 * (NB * 64 + 16); }
 
-template <bool MASK, int NB = 8>
+// PERM: v[j] holds columns 64 (j >> 2) + 16 g + 4 (j & 3) .. + 3 of the lane's
+// row (the b128-B-read mapping of gemm_f32_tile.hip / gemm_f32_w4.hip)
+// instead of 16 j + 4 g .. + 3.
+template <bool MASK, int NB = 8, bool PERM = false>
 __device__ __forceinline__ void store_block16_f32(char* buf, const f32x4 (&v)[NB], char* C, long long ldc_b,
                                                   int row0, int col0, int M, int N, int lane) {
+  static_assert(!PERM || NB % 4 == 0, "PERM: groups of 4 column blocks");
   constexpr int P = NB * 64 + 16;
   constexpr int CPR = NB * 4;    // 16-B chunks per row
   constexpr int RPI = 64 / CPR;  // rows per read instruction
@@ -243,7 +247,8 @@ __device__ __forceinline__ void store_block16_f32(char* buf, const f32x4 (&v)[NB
   lds_char* lb = (lds_char*)(lds_void*)buf;
 #pragma unroll
   for (int j = 0; j < NB; ++j)
-    *(__attribute__((address_space(3))) f32x4*)(lb + l16 * P + (j * 16 + 4 * g) * 4) = v[j];
+    *(__attribute__((address_space(3))) f32x4*)(lb + l16 * P + (PERM ? 64 * (j >> 2) + 16 * g + 4 * (j & 3) : j * 16 + 4 * g) * 4) =
+        v[j];
   const int rl = lane / CPR, ch = lane % CPR;
 #pragma unroll
   for (int r = 0; r < 16 / RPI; ++r) {

@@ -22,9 +22,9 @@ hipError_t gemm256_launch(int dt, GemmArgs a, int sched, hipStream_t stream);
 hipError_t gemm_generic_launch(int dt, GemmArgs a, bool vec, hipStream_t stream);
 bool gemm_f32_256_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 hipError_t gemm_f32_256_launch(GemmArgs a, int variant, hipStream_t stream);
-hipError_t gemm_f32_w4_launch(GemmArgs a, hipStream_t stream);
+hipError_t gemm_f32_w4_launch(GemmArgs a, hipStream_t stream, int variant);
 bool gemm_f32_tile_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
-hipError_t gemm_f32_tile_launch(GemmArgs a, hipStream_t stream);
+hipError_t gemm_f32_tile_launch(GemmArgs a, hipStream_t stream, int variant);
 bool gemm_fp8_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream);
 bool gemm_fp8_w4s_fits(const GemmArgs& a);
@@ -99,7 +99,8 @@ static bool is_experiment(int k) {
     case kMfmaW4Pers: case kMfmaW4PersTrace: case kMfmaW4STrace: case kMfmaW4SRot: case kMfmaW4SRotTrace:
     case kFp8W4Tall: case kFp8W4Wide: case kFp8W4Scaled: case kFp8W4Trace: case kMfmaW4Trace:
     case kFp8W4TS: case kFp8W4STS: case kMfmaW4STS: case kF32_256sDirect: case kFp8W4Unfused:
-    case kT128Unfused: case kFp8T128Unfused: case kMfmaW4Unfused:
+    case kT128Unfused: case kFp8T128Unfused: case kMfmaW4Unfused: case kF32T128B32:
+    case kF32W4B32:
       return true;
     default:
       return false;
@@ -177,9 +178,12 @@ int resolve_kernel(const Problem& p, int kernel) {
     case kF32_256s: return f32fast ? kF32_256s : -1;
     case kF32W4: return f32fast ? kF32W4 : -1;  // same constraints as f32_256
     case kF32T128: return p.dtype == kF32 && supports(p, kF32T128) ? kF32T128 : -1;
+    case kF32T128x2: return p.dtype == kF32 && supports(p, kF32T128) ? kF32T128x2 : -1;
 #ifdef PDMB_EXPERIMENTS
     case kF32_256: case kF32NoDma: case kF32_256sDirect: return f32fast ? kernel : -1;
     case kT128Unfused: return t128 ? kernel : -1;
+    case kF32T128B32: return p.dtype == kF32 && supports(p, kF32T128) ? kernel : -1;
+    case kF32W4B32: return f32fast ? kernel : -1;
     case kMfmaW4Unfused: return (p.dtype == kBF16 && w4) ? kernel : -1;
     case kMfma256: case kMfma256b: case kMfma256c: return fast ? kernel : -1;
     case kMfma256X1: case kMfma256X2: case kMfma256X4: case kMfma256Stamp:
@@ -226,9 +230,12 @@ int resolve_kernel(const Problem& p, int kernel) {
 // MFMA busy at 2.38 GHz, profiles/r1_fp32_ablation.md — so no idle-CU boost):
 // f32_256s 7.0 us per 256x256 K-tile (152 TF at 16k), f32_w4 7.1, f32_t128
 // 1.81 per 128x128 K-tile (fit to 4096 x {1024, 2048} x 4096: 237 / 471 us,
-// profiles/r3_f32_t128_ab.jsonl). f32_t128 is listed before f32_w4: it
-// measured ahead of the split W4 on every under-filled shard shape (4096 x
-// 2048 x 4096 145.8 vs 141.6 TF), so the 3 % hysteresis favours it.
+// profiles/r3_f32_t128_ab.jsonl), f32_t128x2 3.53 per pair of co-resident
+// 128x128 workgroups (4096 x 2048 x 4096 458 us, 8192^3 7241 us:
+// profiles/r3_f32_t128x2_ab.jsonl), priced only where it has two workgroups
+// on every CU. The tiles are listed before f32_w4: they measured ahead of the
+// split W4 on every under-filled shard shape (4096 x 2048 x 4096 145.8 vs
+// 141.6 TF), so the 3 % hysteresis favours them.
 struct KernelModel {
   int kernel, bm, bn, occ;
   double kt;
@@ -245,6 +252,7 @@ static constexpr KernelModel kModels[] = {
     {kFp8T128, 128, 128, 1, 0.42, 1, 8},
     {kF32_256s, 256, 256, 1, 7.0, 2, 1},
     {kF32T128, 128, 128, 1, 1.81, 2, 8},
+    {kF32T128x2, 128, 128, 2, 3.53, 2, 8},
     {kF32W4, 256, 256, 1, 7.1, 2, 8},
 };
 static int dt_class(const Problem& p) { return p.dtype == kFP8 ? 1 : p.dtype == kF32 ? 2 : 0; }
@@ -327,7 +335,7 @@ static bool supports(const Problem& p, int kernel) {
   if (kernel == kFp8W4) return gemm_fp8_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   if (kernel == kF32_256s || kernel == kF32W4)
     return p.dtype == kF32 && gemm_f32_256_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
-  if (kernel == kF32T128)
+  if (kernel == kF32T128 || kernel == kF32T128x2)
     return p.dtype == kF32 && gemm_f32_tile_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   return gemm_tile_supported(p.dtype, model_of(kernel).bm, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
 }
@@ -347,6 +355,11 @@ static Plan plan(const Problem& p, int kernel) {
       if (S > 4 && p.splitk != S) continue;
       if (p.splitk > 0 && S != p.splitk) continue;
       if (!split_ok(p, m.kernel, S)) continue;
+      // a two-per-CU fp32 tile only on grids that put two on every CU: alone on
+      // a CU its 2-stage ring runs slower than the 4-stage one-per-CU tile
+      if (m.cls == 2 && m.occ > 1 &&
+          tiles_of(p, m.kernel) * S < (long long)(p.cus > 0 ? p.cus : device_cus()) * m.occ)
+        continue;
       const double c = plan_cost(p, m.kernel, S);
       if (c < bc * 0.97) {  // a different choice only for a clear win
         bc = c;
@@ -363,7 +376,7 @@ static Plan plan(const Problem& p, int kernel) {
 
 static bool is_tiled(int k) {
   return k == kMfmaW4 || k == kT128 || k == kT128x2 || k == kT256x128 || k == kFp8T128 || k == kFp8T256x128 ||
-         k == kF32W4 || k == kF32T128;
+         k == kF32W4 || k == kF32T128 || k == kF32T128x2;
 }
 
 int choose_splitk(const Problem& p, int kernel) {
@@ -547,8 +560,8 @@ static hipError_t tiled_launch(const Problem& p, int k, GemmArgs a, void* part, 
       a.pers_grid = p.cus > 0 ? p.cus : device_cus();
     }
   }
-  if (k == kF32W4) return gemm_f32_w4_launch(a, stream);
-  if (k == kF32T128) return gemm_f32_tile_launch(a, stream);
+  if (k == kF32W4) return gemm_f32_w4_launch(a, stream, sub);  // sub: the variant (experiments)
+  if (k == kF32T128 || k == kF32T128x2) return gemm_f32_tile_launch(a, stream, sub);  // sub: the variant
   return k == kMfmaW4 ? gemm_w4_launch(p.dtype, a, stream, sub) : gemm_tile_launch(k, p.dtype, a, stream);
 }
 
@@ -760,6 +773,8 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel) {
   if (k == kMfmaW4Tall || k == kMfmaW4Wide || k == kMfmaW4Il32 || k == kMfmaW4Trace ||
       k == kMfmaW4Pers || k == kMfmaW4PersTrace)
     return splitk_bytes(p, kMfmaW4, plan(p, kMfmaW4).splitk);
+  if (k == kF32T128B32) return splitk_bytes(p, kF32T128, plan(p, kF32T128).splitk);
+  if (k == kF32W4B32) return splitk_bytes(p, kF32W4, plan(p, kF32W4).splitk);
   return 0;
 }
 
@@ -935,6 +950,7 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kF32_256s: return gemm_f32_256_launch(a, 1, stream);
     case kF32W4:
     case kF32T128: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream);
+    case kF32T128x2: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream, 2);
 #ifdef PDMB_EXPERIMENTS
     case kFp8: return gemm_fp8_launch(a, 0, stream);
     case kFp8W4Diag: return gemm_fp8_launch(a, 9, stream);
@@ -971,6 +987,8 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kF32_256: return gemm_f32_256_launch(a, 0, stream);
     case kF32NoDma: return gemm_f32_256_launch(a, 9, stream);
     case kF32_256sDirect: return gemm_f32_256_launch(a, 10, stream);
+    case kF32T128B32: return tiled_launch(p, kF32T128, a, p.workspace, p.workspace_bytes, stream, 1);
+    case kF32W4B32: return tiled_launch(p, kF32W4, a, p.workspace, p.workspace_bytes, stream, 1);
     case kMfma256X1: case kMfma256X2: case kMfma256X4:
       return gemm256_launch(p.dtype, a, 10 + (k - kMfma256X1 + 1), stream);
 #endif
@@ -1140,6 +1158,9 @@ const char* kernel_name(int kernel) {
     case kT128Unfused: return "pdmb_t128_nn_unfused";
     case kFp8T128Unfused: return "pdmb_fp8_t128_nt_unfused";
     case kMfmaW4Unfused: return "pdmb_w4_nn_unfused";
+    case kF32T128B32: return "pdmb_f32_t128_b32";
+    case kF32T128x2: return "pdmb_f32_t128x2_nn";
+    case kF32W4B32: return "pdmb_f32_w4_b32";
     case kFp8W4Trace: return "pdmb_fp8_w4_nt_trace";
     default: return "auto";
   }

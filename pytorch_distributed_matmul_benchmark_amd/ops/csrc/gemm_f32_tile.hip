@@ -40,14 +40,13 @@
 namespace pdmb {
 namespace kf32t {
 
-constexpr int BM = 128, BN = 128, BK = 32, NT = 256, NS = 4;
+constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
 constexpr int MB = 4, NB = 4;                 // 16x16 blocks per wave
 constexpr int A_BYTES = BM * BK * 4;          // 16 KiB
 constexpr int B_BYTES = BK * BN * 4;          // 16 KiB
 constexpr int STAGE = A_BYTES + B_BYTES;      // 32 KiB
 constexpr int P = 8;                          // DMA pieces per wave per K-tile (4 A + 4 B)
 constexpr int G = 2 * 4 * MB * NB;            // MFMAs per K-tile per wave (kb, e, mi, ni) = 128
-constexpr int LDS_BYTES = NS * STAGE;         // 128 KiB
 typedef __attribute__((address_space(3))) f32x4 lds_f32x4;
 typedef __attribute__((address_space(3))) float lds_f32;
 
@@ -76,13 +75,15 @@ __device__ __forceinline__ void wait_barrier() {
 }
 
 // Item schedule of one K-tile (gemm_tile.hip Sched, fp32 classes): 8 A
-// fragment reads (b128: 2 kb x 4 mi), 32 B element reads (b32: 2 kb x 4 ni x
-// 4 e) and 8 DMA pieces spread Bresenham-style over the 128 MFMA gaps, at
-// most one per gap. Encoding: 0 none; 1 + piece; 100 + B read q; 200 + A read q.
+// fragment reads (b128: 2 kb x 4 mi), the B reads (BV: 8 b128, 2 kb x 4 e;
+// else 32 b32, 2 kb x 4 ni x 4 e) and 8 DMA pieces spread Bresenham-style
+// over the 128 MFMA gaps, at most one per gap. Encoding: 0 none; 1 + piece;
+// 100 + B read q; 200 + A read q.
+template <bool BV>
 struct Sched {
   int item[G];
   constexpr Sched() : item() {
-    const int T[3] = {32, 8, P};
+    const int T[3] = {BV ? 8 : 32, 8, P};
     int n[3] = {0, 0, 0};
     for (int g = 0; g < G; ++g) {
       int best = -1, bd = 0;
@@ -101,9 +102,20 @@ struct Sched {
   }
 };
 
-struct Frag {  // one K-tile's fragments: A rows (4 k each) and B elements
+// One K-tile's fragments: A rows (4 k each) and B. BV (b128 B reads): b4[kb][e]
+// holds B[k][c0 + 4 l16 + ni] for ni = 0..3 — MFMA ni of the lane's column
+// group uses output column 16 g + 4 r + ni of the wave's 64 (a column
+// permutation undone by the epilogue), so one read feeds four MFMAs. Else
+// b[kb][ni][e] = B[k][16 ni + l16] (one b32 read per MFMA operand).
+template <bool BV>
+struct Frag {
   f32x4 a[2][MB];      // [kb][mi]
   float b[2][NB][4];   // [kb][ni][e]
+};
+template <>
+struct Frag<true> {
+  f32x4 a[2][MB];      // [kb][mi]
+  f32x4 b4[2][4];      // [kb][e], lanes ni
 };
 
 struct Ctx {
@@ -116,7 +128,8 @@ struct Ctx {
   // Per-lane fragment bases in stage 0 (the rest of each offset is an
   // immediate): A block mi of half kb at abase[kb] + mi * 2048 (the row
   // swizzle (r >> 1) & 7 does not depend on mi); B element (kb, ni, e) at
-  // bbase[ni] + kb * 8192 + e * 512 (k = 16 kb + 4 g + e; g is in the base).
+  // bbase[ni] + kb * 8192 + e * 512 (k = 16 kb + 4 g + e; g is in the base);
+  // BV: B chunk (kb, e) at bbase[0] + kb * 8192 + e * 512.
   uint32_t abase[2];
   uint32_t bbase[NB];
 };
@@ -142,9 +155,10 @@ __device__ __forceinline__ void issue_piece(const Ctx& c, u32x4 rb, uint32_t so,
 
 // One K-tile: 128 MFMAs on `cur` (tile t), reading tile t+1's fragments into
 // `nxt` from stage `sn`, DMA of tile t + NS into stage `sc`.
+template <int NS, bool BV>
 __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, uint32_t sc, uint32_t sn,
-                                      f32x4 (&acc)[MB][NB], const Frag& cur, Frag& nxt) {
-  constexpr Sched S{};
+                                      f32x4 (&acc)[MB][NB], const Frag<BV>& cur, Frag<BV>& nxt) {
+  constexpr Sched<BV> S{};
   const int td = t + NS < c.nk ? t + NS : c.nk - 1;  // clamped tail DMAs (harmless re-reads)
   const u32x4 rb = b_rsrc(c, td);
   wait_lgkm_barrier<P * (NS - 2)>();
@@ -157,14 +171,22 @@ __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, uin
 #pragma unroll
   for (int gap = 0; gap < G; ++gap) {
     const int kb = gap >> 6, e = (gap >> 4) & 3, mi = (gap >> 2) & 3, ni = gap & 3;
-    mfma(acc[mi][ni], cur.b[kb][ni][e], cur.a[kb][mi][e]);
+    if constexpr (BV)
+      mfma(acc[mi][ni], cur.b4[kb][e][ni], cur.a[kb][mi][e]);
+    else
+      mfma(acc[mi][ni], cur.b[kb][ni][e], cur.a[kb][mi][e]);
     const int it = S.item[gap];
     if (it >= 200) {
       const int q = it - 200, qk = q >> 2, qm = q & 3;
       nxt.a[qk][qm] = *(const lds_f32x4*)(smem + ab[qk] + qm * 2048);
     } else if (it >= 100) {
-      const int q = it - 100, qk = q >> 4, qn = (q >> 2) & 3, qe = q & 3;
-      nxt.b[qk][qn][qe] = *(const lds_f32*)(smem + bb[qn] + qk * 8192 + qe * 512);
+      if constexpr (BV) {
+        const int q = it - 100, qk = q >> 2, qe = q & 3;
+        nxt.b4[qk][qe] = *(const lds_f32x4*)(smem + bb[0] + qk * 8192 + qe * 512);
+      } else {
+        const int q = it - 100, qk = q >> 4, qn = (q >> 2) & 3, qe = q & 3;
+        nxt.b[qk][qn][qe] = *(const lds_f32*)(smem + bb[qn] + qk * 8192 + qe * 512);
+      }
     } else if (it >= 1) {
       issue_piece(c, rb, sc, td, it - 1);
     }
@@ -172,7 +194,11 @@ __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, uin
   }
 }
 
-__global__ void __launch_bounds__(NT, 1) gemm_f32_t128(GemmArgs a) {
+// NS: LDS stages (4: 128 KiB, one workgroup per CU; 2: 64 KiB, two per CU).
+// BV: b128 B reads (column-permuted MFMAs) instead of b32 ones.
+template <int NS, bool BV>
+__global__ void __launch_bounds__(NT, NS == 2 ? 2 : 1) gemm_f32_t128(GemmArgs a) {
+  constexpr int LDS_BYTES = NS * STAGE;
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
   int bz, tm, tn;
@@ -218,11 +244,13 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_t128(GemmArgs a) {
     }
 #pragma unroll
     for (int ni = 0; ni < NB; ++ni) {  // k = 16 kb + 4 g + e: (k >> 2) & 3 == g
-      const int col = wc * 64 + ni * 16 + l16;
+      // BV: chunk wc * 16 + l16 (columns wc * 64 + 4 l16 .. + 3), bbase[0] only
+      const int col = BV ? wc * 64 + 4 * l16 : wc * 64 + ni * 16 + l16;
       const int ch = (col >> 2) ^ (4 * g);
       uint32_t bo = (uint32_t)(A_BYTES + 4 * g * 512 + ch * 16 + (col & 3) * 4);
       asm volatile("" : "+v"(bo));
       c.bbase[ni] = bo;
+      if (BV) break;
     }
   }
 
@@ -243,27 +271,32 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_t128(GemmArgs a) {
     for (int h = 0; h < P; ++h) issue_piece(c, rb, st * STAGE, tl, h);
   }
   wait_barrier<P * (NS - 1)>();
-  Frag F0, F1;
+  Frag<BV> F0, F1;
 #pragma unroll
   for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
     for (int mi = 0; mi < MB; ++mi) F0.a[kb][mi] = *(const lds_f32x4*)(smem + c.abase[kb] + mi * 2048);
+    if constexpr (BV) {
 #pragma unroll
-    for (int ni = 0; ni < NB; ++ni)
+      for (int e = 0; e < 4; ++e) F0.b4[kb][e] = *(const lds_f32x4*)(smem + c.bbase[0] + kb * 8192 + e * 512);
+    } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        F0.b[kb][ni][e] = *(const lds_f32*)(smem + c.bbase[ni] + kb * 8192 + e * 512);
+      for (int ni = 0; ni < NB; ++ni)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          F0.b[kb][ni][e] = *(const lds_f32*)(smem + c.bbase[ni] + kb * 8192 + e * 512);
+    }
   }
   // K-tile t computes from set t & 1, reads t+1 into the other set from
   // stage (t+1) % NS, refills stage t % NS with tile t + NS.
   int t = 0;
   for (; t + 1 < nk; t += 2) {
-    ktile(c, smem, t, (uint32_t)((t % NS) * STAGE), (uint32_t)(((t + 1) % NS) * STAGE), acc, F0, F1);
-    ktile(c, smem, t + 1, (uint32_t)(((t + 1) % NS) * STAGE), (uint32_t)(((t + 2) % NS) * STAGE), acc,
-          F1, F0);
+    ktile<NS>(c, smem, t, (uint32_t)((t % NS) * STAGE), (uint32_t)(((t + 1) % NS) * STAGE), acc, F0, F1);
+    ktile<NS>(c, smem, t + 1, (uint32_t)(((t + 1) % NS) * STAGE), (uint32_t)(((t + 2) % NS) * STAGE), acc,
+              F1, F0);
   }
   if (t < nk)  // odd count: the last tile (its "next" reads are clamped re-reads)
-    ktile(c, smem, t, (uint32_t)((t % NS) * STAGE), (uint32_t)((t % NS) * STAGE), acc, F0, F1);
+    ktile<NS>(c, smem, t, (uint32_t)((t % NS) * STAGE), (uint32_t)((t % NS) * STAGE), acc, F0, F1);
   // Drain the tail DMAs and give the last MFMAs time to write their AGPRs
   // (asm MFMAs are invisible to hipcc's hazard recognizer).
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
@@ -289,11 +322,18 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_t128(GemmArgs a) {
     } else {
       splitk_row<MB, NB, NT>(a, sl, slice, mi, acc, v);
     }
+    if constexpr (BV) {  // v[ni][r] is column 16 g + 4 r + ni: w[r] = columns 16 g + 4 r .. + 3
+      f32x4 w[NB];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[r] = f32x4{v[0][r], v[1][r], v[2][r], v[3][r]};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = w[r];
+    }
     const int row0 = m0 + wr * 64 + mi * 16, col0 = n0 + wc * 64;
     if (interior)
-      store_block16_f32<false, NB>(ebuf, v, Cb, (long long)a.ldc * 4, row0, col0, a.M, a.N, lane);
+      store_block16_f32<false, NB, BV>(ebuf, v, Cb, (long long)a.ldc * 4, row0, col0, a.M, a.N, lane);
     else
-      store_block16_f32<true, NB>(ebuf, v, Cb, (long long)a.ldc * 4, row0, col0, a.M, a.N, lane);
+      store_block16_f32<true, NB, BV>(ebuf, v, Cb, (long long)a.ldc * 4, row0, col0, a.M, a.N, lane);
   }
 }
 
@@ -315,7 +355,9 @@ bool gemm_f32_tile_supported(const GemmArgs& a, size_t align_a, size_t align_b, 
 }
 
 // a.splitk > 1: split-K with a.part / a.flags (gemm_dispatch.cpp f32 planner).
-hipError_t gemm_f32_tile_launch(GemmArgs a, hipStream_t stream) {
+// variant 0: kF32T128 (4 stages, b128 B reads); 2: kF32T128x2 (2 stages, two
+// workgroups per CU); experiment builds: 1 = b32 B reads (round 3's first version).
+hipError_t gemm_f32_tile_launch(GemmArgs a, hipStream_t stream, int variant) {
   a.tiles_m = (a.M + kf32t::BM - 1) / kf32t::BM;
   a.tiles_n = (a.N + kf32t::BN - 1) / kf32t::BN;
   a.supertile = choose_supertile(a.tiles_m, a.tiles_n);
@@ -332,7 +374,18 @@ hipError_t gemm_f32_tile_launch(GemmArgs a, hipStream_t stream) {
   const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch * S;
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(kf32t::gemm_f32_t128, dim3((unsigned)nblocks), dim3(kf32t::NT), 0, stream, a);
+#ifdef PDMB_EXPERIMENTS
+  if (variant == 1) {
+    hipLaunchKernelGGL((kf32t::gemm_f32_t128<4, false>), dim3((unsigned)nblocks), dim3(kf32t::NT), 0, stream, a);
+    return hipGetLastError();
+  }
+#endif
+  if (variant == 2) {  // kF32T128x2
+    hipLaunchKernelGGL((kf32t::gemm_f32_t128<2, true>), dim3((unsigned)nblocks), dim3(kf32t::NT), 0, stream, a);
+    return hipGetLastError();
+  }
+  if (variant != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((kf32t::gemm_f32_t128<4, true>), dim3((unsigned)nblocks), dim3(kf32t::NT), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -68,9 +68,20 @@ struct Ctx {
   uint32_t lds0;
 };
 
-struct Half {  // fragments of one 16-k block: A rows (4 k each) and B elements
+// Fragments of one 16-k block: A rows (4 k each) and B. BV (b128 B reads):
+// b4[e][h] = B[k][wc * 128 + 64 h + 4 l16 + j] for j = 0..3 — MFMA ni = 4 h + j
+// of the lane's column group uses output column 64 h + 16 g + 4 r + j (a
+// column permutation the epilogue undoes), so one read feeds four MFMAs.
+// Else b[ni][e] = B[k][16 ni + l16], one b32 read per MFMA operand.
+template <bool BV>
+struct Half {
   f32x4 a[8];
   float b[8][4];
+};
+template <>
+struct Half<true> {
+  f32x4 a[8];
+  f32x4 b4[4][2];
 };
 
 // DMA piece h (0..15) of K-tile `tile` into stage `stg`: h < 8: A rows
@@ -101,12 +112,19 @@ __device__ __forceinline__ float read_b(const char* smem, int stg, int kb, int n
   const int col = wc * 128 + ni * 16 + l16;
   return *(const float*)(smem + stg * STAGE + A_BYTES + k * B_PITCH + col * 4);
 }
+__device__ __forceinline__ f32x4 read_b4(const char* smem, int stg, int kb, int h, int e, int wc,
+                                         int l16, int g) {
+  const int k = kb * 16 + 4 * g + e;
+  const int col = wc * 128 + h * 64 + 4 * l16;
+  return *(const f32x4*)(smem + stg * STAGE + A_BYTES + k * B_PITCH + col * 4);
+}
 
 // One 16-k half: 256 MFMAs from `cur`; in their gaps read the other half's
 // fragments into `nxt` (kb_next >= 0) and issue DMA pieces [p0, p0 + np) of
 // the next tile (one per 4 MFMAs from the start).
+template <bool BV>
 __device__ __forceinline__ void half_step(const Ctx& c, const char* smem, f32x4 (&acc)[8][8],
-                                          const Half& cur, Half& nxt, int stg_rd, int kb_next,
+                                          const Half<BV>& cur, Half<BV>& nxt, int stg_rd, int kb_next,
                                           int wr, int wc, int l16, int g, u32x4 ra, u32x4 rb,
                                           int stg_dma, int p0, int np) {
 #pragma unroll
@@ -116,14 +134,20 @@ __device__ __forceinline__ void half_step(const Ctx& c, const char* smem, f32x4 
 #pragma unroll
       for (int ni = 0; ni < 8; ++ni) {
         const int gap = (e * 8 + mi) * 8 + ni;  // 0..255
-        mfma(acc[mi][ni], cur.b[ni][e], cur.a[mi][e]);
+        if constexpr (BV)
+          mfma(acc[mi][ni], cur.b4[e][ni >> 2][ni & 3], cur.a[mi][e]);
+        else
+          mfma(acc[mi][ni], cur.b[ni][e], cur.a[mi][e]);
         if (gap % 4 == 3 && gap / 4 < np) {
           issue_piece(c, ra, rb, stg_dma, p0 + gap / 4);
-        } else if (kb_next >= 0 && gap % 4 == 1 && gap / 4 < 40) {
-          // 40 reads: 8 A rows (b128) then 32 B elements (b32), one per 4 MFMAs
+        } else if (kb_next >= 0 && gap % 4 == 1 && gap / 4 < (BV ? 16 : 40)) {
+          // 8 A rows (b128) then the B reads (BV: 8 b128; else 32 b32), one per 4 MFMAs
           const int q = gap / 4;
           if (q < 8) {
             nxt.a[q] = read_a(smem, stg_rd, kb_next, q, wr, l16, g);
+          } else if constexpr (BV) {
+            const int e2 = (q - 8) >> 1, h2 = (q - 8) & 1;
+            nxt.b4[e2][h2] = read_b4(smem, stg_rd, kb_next, h2, e2, wc, l16, g);
           } else {
             const int e2 = (q - 8) >> 3, ni2 = (q - 8) & 7;
             nxt.b[ni2][e2] = read_b(smem, stg_rd, kb_next, ni2, e2, wc, l16, g);
@@ -133,6 +157,8 @@ __device__ __forceinline__ void half_step(const Ctx& c, const char* smem, f32x4 
       }
 }
 
+// BV: b128 B reads (column-permuted MFMAs) instead of b32 ones.
+template <bool BV>
 __global__ void __launch_bounds__(NT, 1) gemm_f32_w4(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
@@ -201,14 +227,19 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4(GemmArgs a) {
   } else {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   }
-  Half h0, h1;
+  Half<BV> h0, h1;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {  // in the order the MFMAs consume them
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi)
       if (e == 0) h0.a[mi] = read_a(smem, 0, 0, mi, wr, l16, g);
+    if constexpr (BV) {
 #pragma unroll
-    for (int ni = 0; ni < 8; ++ni) h0.b[ni][e] = read_b(smem, 0, 0, ni, e, wc, l16, g);
+      for (int h = 0; h < 2; ++h) h0.b4[e][h] = read_b4(smem, 0, 0, h, e, wc, l16, g);
+    } else {
+#pragma unroll
+      for (int ni = 0; ni < 8; ++ni) h0.b[ni][e] = read_b(smem, 0, 0, ni, e, wc, l16, g);
+    }
   }
   // K-tile t (stage s = t & 1; tile t+1 in s ^ 1 was issued a tile ago):
   //   half 0: MFMAs from h0 | read half 1 of t from s into h1
@@ -253,19 +284,30 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4(GemmArgs a) {
     } else {
       splitk_row<8, 8, NT>(a, sl, slice, mi, acc, v);
     }
+    if constexpr (BV) {  // v[4 h + j][r] is column 64 h + 16 g + 4 r + j: regroup by r
+      f32x4 w[8];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          w[4 * h + r] = f32x4{v[4 * h][r], v[4 * h + 1][r], v[4 * h + 2][r], v[4 * h + 3][r]};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = w[j];
+    }
     if (interior)
-      store_block16_f32<false>(ebuf, v, Cb, (long long)a.ldc * 4, m0 + wr * 128 + mi * 16,
-                               n0 + wc * 128, a.M, a.N, lane);
+      store_block16_f32<false, 8, BV>(ebuf, v, Cb, (long long)a.ldc * 4, m0 + wr * 128 + mi * 16,
+                                      n0 + wc * 128, a.M, a.N, lane);
     else
-      store_block16_f32<true>(ebuf, v, Cb, (long long)a.ldc * 4, m0 + wr * 128 + mi * 16,
-                              n0 + wc * 128, a.M, a.N, lane);
+      store_block16_f32<true, 8, BV>(ebuf, v, Cb, (long long)a.ldc * 4, m0 + wr * 128 + mi * 16,
+                                     n0 + wc * 128, a.M, a.N, lane);
   }
 }
 
 }  // namespace kf32w4
 
 // a.splitk > 1: split-K with a.part / a.flags (gemm_dispatch.cpp f32_split).
-hipError_t gemm_f32_w4_launch(GemmArgs a, hipStream_t stream) {
+// variant 0: the shipping kernel (b128 B reads); 1 (experiment builds): b32 B reads.
+hipError_t gemm_f32_w4_launch(GemmArgs a, hipStream_t stream, int variant) {
   a.tiles_m = (a.M + kf32w4::BM - 1) / kf32w4::BM;
   a.tiles_n = (a.N + kf32w4::BN - 1) / kf32w4::BN;
   a.supertile = choose_supertile(a.tiles_m, a.tiles_n);
@@ -282,7 +324,14 @@ hipError_t gemm_f32_w4_launch(GemmArgs a, hipStream_t stream) {
   const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch * S;
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(kf32w4::gemm_f32_w4, dim3((unsigned)nblocks), dim3(kf32w4::NT), 0, stream, a);
+#ifdef PDMB_EXPERIMENTS
+  if (variant == 1) {
+    hipLaunchKernelGGL(kf32w4::gemm_f32_w4<false>, dim3((unsigned)nblocks), dim3(kf32w4::NT), 0, stream, a);
+    return hipGetLastError();
+  }
+#endif
+  if (variant != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(kf32w4::gemm_f32_w4<true>, dim3((unsigned)nblocks), dim3(kf32w4::NT), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -34,7 +34,7 @@ from . import _native
 # The shipping kernels: the public ``kernel=`` surface (api.h ``Kernel``).
 KERNELS = {"auto": 0, "generic": 2, "f32_256s": 7, "mfma256d": 9, "fp8_w4": 16, "w4": 21,
            "t128": 26, "t128x2": 27, "t256x128": 28, "f32_w4": 29, "w4s": 36, "fp8_w4s": 37,
-           "fp8_t128": 41, "fp8_t256x128": 42, "f32_t128": 51}
+           "fp8_t128": 41, "fp8_t256x128": 42, "f32_t128": 51, "f32_t128x2": 53}
 # A/B and timing-only diagnostic kernels (api.h ``ExperimentKernel``): accepted
 # only by a library built with ``PDMB_EXPERIMENTS=1``; ``diag_*`` ones skip waits
 # or data movement on purpose and compute WRONG results.
@@ -49,12 +49,12 @@ EXPERIMENT_KERNELS = {"mfma256": 1, "mfma256b": 3, "mfma256c": 4, "mfma256c_stam
                       "x_fp8_w4_tstore": 43, "x_fp8_w4s_tstore": 44, "x_w4s_tstore": 45,
                       "x_f32_256s_direct": 46, "x_fp8_w4_unfused": 47,
                       "x_t128_unfused": 48, "x_fp8_t128_unfused": 49,
-                      "x_w4_unfused": 50}
+                      "x_w4_unfused": 50, "x_f32_t128_b32": 52, "x_f32_w4_b32": 54}
 KERNEL_NAMES = {0: "auto", 2: "pdmb_generic_nn", 7: "pdmb_f32_256s_nn", 9: "pdmb_mfma256d_nn",
                 16: "pdmb_fp8_w4_nt", 21: "pdmb_w4_nn", 26: "pdmb_t128_nn",
                 27: "pdmb_t128x2_nn", 28: "pdmb_t256x128_nn", 29: "pdmb_f32_w4_nn", 36: "pdmb_w4s",
                 37: "pdmb_fp8_w4s", 41: "pdmb_fp8_t128_nt", 42: "pdmb_fp8_t256x128_nt",
-                51: "pdmb_f32_t128_nn",
+                51: "pdmb_f32_t128_nn", 53: "pdmb_f32_t128x2_nn",
                 1: "pdmb_mfma256_nn",
                 3: "pdmb_mfma256b_nn", 4: "pdmb_mfma256c_nn", 5: "pdmb_mfma256c_stamp",
                 6: "pdmb_f32_256_nn", 15: "pdmb_fp8_256_nt", -1: "unsupported"}

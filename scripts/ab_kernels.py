@@ -89,8 +89,11 @@ def main():
         for _ in range(2):  # warm clocks
             for k in ks:
                 bench(k, 5)
-        for _ in range(a.rounds):
-            for k in ks:
+        for r in range(a.rounds):
+            # rotate the arm order every round: no arm always runs first (right
+            # after the previous round's last arm), which biased the medians by
+            # a few % on short kernels (profiles/r3_ldc_probe_*.jsonl)
+            for k in ks[r % len(ks):] + ks[:r % len(ks)]:
                 res[k].append(flops / bench(k, a.iters) / 1e9)
         for k in ks:
             med = statistics.median(res[k])

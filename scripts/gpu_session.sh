@@ -12,7 +12,8 @@
 # native16k (pdmb_bench bf16 / fp8 at 16k), overlap_proxy, rocprof_bench, selflaunch2,
 # selflaunch4, gpus2_refused (bench.py --gpus 2 on a 1-GPU box must exit 2 at once),
 # ab_bf16 / ab_fp32 / ab_fp8 (auto vs hipBLASLt A/B tables), final_table (auto vs
-# hipBLASLt, every dtype at 4k / 8k / 16k), pmc (PMC passes: scripts/gpu_pmc.sh with
+# hipBLASLt, every dtype at 4k / 8k / 16k), ldc_probe (output row pitch vs GEMM time,
+# scripts/ldc_probe.py), pmc (PMC passes: scripts/gpu_pmc.sh with
 # N / KS / DT from the environment). After "--": one ad-hoc step NAME with a SECONDS limit.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -76,6 +77,11 @@ run_stage() {
               8192,2048,8192 10240,10240,10240 16384,16384,16384 &&
             grep '^{' "$OUT/ab_fp8.log" > "$OUT/ab_fp8.jsonl" ;;
     tests_fp8) step tests_fp8 600 $PYT tests/test_fp8_gpu.py -m gpu ;;
+    ldc_probe) step ldc_fp8 600 python scripts/ldc_probe.py --dtype float8_e4m3fn &&
+               grep '^{' "$OUT/ldc_fp8.log" > "$OUT/ldc_fp8.jsonl" &&
+               step ldc_bf16 600 python scripts/ldc_probe.py --dtype bfloat16 \
+                 --shapes 8192,2048,8192 4096,4096,4096 2048,8192,8192 16384,2048,16384 &&
+               grep '^{' "$OUT/ldc_bf16.log" > "$OUT/ldc_bf16.jsonl" ;;
     *) echo "unknown stage $1"; return 2 ;;
   esac
 }

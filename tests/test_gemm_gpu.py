@@ -33,7 +33,7 @@ FAST = ["mfma256d", "mfma256", "mfma256b", "mfma256c"]
 
 
 TILED = ("pdmb_w4_nn", "pdmb_t256x128_nn", "pdmb_t128_nn", "pdmb_t128x2_nn", "pdmb_w4s")
-F32 = ("pdmb_f32_256s_nn", "pdmb_f32_w4_nn", "pdmb_f32_t128_nn")
+F32 = ("pdmb_f32_256s_nn", "pdmb_f32_w4_nn", "pdmb_f32_t128_nn", "pdmb_f32_t128x2_nn")
 
 
 def _need(kernel):
@@ -203,7 +203,8 @@ def test_race_screen_repeated_runs(kernel):
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 32), (512, 768, 96), (1000, 1052, 320),
                                    (300, 200, 64), (2304, 2048, 1024)])
-@pytest.mark.parametrize("kernel", ["f32_256", "f32_256s", "f32_w4", "x_f32_256s_direct", "f32_t128"])
+@pytest.mark.parametrize("kernel", ["f32_256", "f32_256s", "f32_w4", "x_f32_256s_direct", "f32_t128",
+                                    "f32_t128x2", "x_f32_w4_b32", "x_f32_t128_b32"])
 def test_f32_256_exact_and_random(M, N, K, kernel):
     _need(kernel)
     g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
@@ -252,35 +253,44 @@ def test_f32_splitk_exact(kernel, M, N, K, splitk, split):
     assert torch.equal(gemm.matmul(A, B, kernel=kernel, splitk=splitk), C)
 
 
+F32_T128_ARMS = ["f32_t128", "f32_t128x2", "x_f32_t128_b32"]
+
+
 @pytest.mark.parametrize("M,N,K,b", [(128, 128, 32, 1), (256, 384, 96, 1), (1000, 1052, 320, 1),
                                      (300, 200, 64, 1), (384, 640, 256, 3), (4096, 512, 4096, 1),
                                      (1, 4, 32, 1), (129, 132, 1024, 2)])
-def test_f32_t128_exact_identity_and_batched(M, N, K, b):
-    """The 128x128 exact-fp32 tile (gemm_f32_tile.hip): small integers exact
-    (every fp32 partial sum exact), A = I with an asymmetric B, batched, edge
-    tiles in M and N, one-K-tile problems."""
+@pytest.mark.parametrize("kernel", F32_T128_ARMS)
+def test_f32_t128_exact_identity_and_batched(M, N, K, b, kernel):
+    """The 128x128 exact-fp32 tile (gemm_f32_tile.hip; shipping: b128 B reads
+    with column-permuted MFMAs; experiment arms: b32 B reads, 2 stages x 2
+    workgroups per CU): small integers exact (every fp32 partial sum exact),
+    A = I with an asymmetric B (catches a column permutation the epilogue
+    fails to undo), batched, edge tiles in M and N, one-K-tile problems."""
+    _need(kernel)
     g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K + b)
     A = torch.randint(-3, 4, (b, M, K), device="cuda", generator=g).float()
     B = torch.randint(-3, 4, (b, K, N), device="cuda", generator=g).float()
     if b == 1:
         A, B = A[0], B[0]
-    C = gemm.matmul(A, B, kernel="f32_t128")
+    C = gemm.matmul(A, B, kernel=kernel)
     assert torch.equal(C.double(), torch.matmul(A.double(), B.double()))
     n = 512
     I = torch.eye(n, device="cuda")
     Bs = (torch.arange(n * 640, device="cuda").view(n, 640) % 97).float()
-    assert torch.equal(gemm.matmul(I, Bs, kernel="f32_t128"), Bs)
+    assert torch.equal(gemm.matmul(I, Bs, kernel=kernel), Bs)
 
 
-def test_f32_t128_race_screen():
+@pytest.mark.parametrize("kernel", F32_T128_ARMS)
+def test_f32_t128_race_screen(kernel):
+    _need(kernel)
     torch.manual_seed(21)
     A = torch.randn(4096, 2048, device="cuda")
     B = torch.randn(2048, 1024, device="cuda")
     for S in (1, 2):
-        ref = gemm.matmul(A, B, kernel="f32_t128", splitk=S)
+        ref = gemm.matmul(A, B, kernel=kernel, splitk=S)
         assert _relerr(ref, _ref(A, B)) < TOL[torch.float32]
         for _ in range(10):
-            assert torch.equal(gemm.matmul(A, B, kernel="f32_t128", splitk=S), ref)
+            assert torch.equal(gemm.matmul(A, B, kernel=kernel, splitk=S), ref)
 
 
 def test_f32_256_identity_batched_and_shards():

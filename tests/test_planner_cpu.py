@@ -32,11 +32,11 @@ def test_f32_shards_fill_the_chip(C, n, ws):
     wave, and the under-filled 4096 shards go to the small tile or a split W4."""
     shard = n // ws
     k, S, cost, _ = plan(C, F32, n, shard, n)
-    bm = 128 if k == "pdmb_f32_t128_nn" else 256
+    bm = 128 if k in ("pdmb_f32_t128_nn", "pdmb_f32_t128x2_nn") else 256
     units = -(-n // bm) * -(-shard // bm) * max(S, 1)
     assert units >= 192, (n, ws, k, S)
     if n == 4096:
-        assert k == "pdmb_f32_t128_nn" or (k == "pdmb_f32_w4_nn" and S > 1)
+        assert k in ("pdmb_f32_t128_nn", "pdmb_f32_t128x2_nn") or (k == "pdmb_f32_w4_nn" and S > 1)
 
 
 def test_f32_full_grids_keep_the_256_kernel(C):
@@ -50,12 +50,24 @@ def test_f32_planner_prefers_cheaper_plan(C):
     for shape in ((4096, 512, 4096), (4096, 1024, 4096), (4096, 2048, 4096), (2048, 2048, 2048),
                   (1000, 1052, 4096), (8192, 1024, 8192), (6144, 6144, 6144)):
         auto = plan(C, F32, *shape)
-        for forced in (29, 51):
+        for forced in (29, 51, 53):
             f = plan(C, F32, *shape, kernel=forced)
             assert auto[2] <= f[2] / 0.97 + 1e-6, (shape, auto, f)
-    # the measured winner on the under-filled shards (profiles/r3_f32_t128_ab.jsonl)
-    for shape in ((4096, 2048, 4096), (4096, 1024, 4096), (2048, 2048, 2048)):
+    # the measured winners on the under-filled shards (profiles/r3_f32_t128x2_ab.jsonl):
+    # two 128x128 workgroups per CU where the grid has two per CU, else one
+    assert plan(C, F32, 4096, 2048, 4096)[0] == "pdmb_f32_t128x2_nn"
+    for shape in ((4096, 1024, 4096), (2048, 2048, 2048)):
         assert plan(C, F32, *shape)[0] == "pdmb_f32_t128_nn"
+
+
+def test_f32_two_per_cu_tile_needs_two_per_cu(C):
+    """f32_t128x2 (2-stage ring, two workgroups per CU) is never planned on a
+    grid that leaves CUs with one workgroup (its ring is too shallow alone)."""
+    for shape in ((4096, 1024, 4096), (2048, 2048, 2048), (4096, 512, 4096), (1000, 1052, 4096),
+                  (4096, 2048, 4096), (8192, 4096, 8192), (6144, 6144, 6144)):
+        k, S, _, _ = plan(C, F32, *shape)
+        if k == "pdmb_f32_t128x2_nn":
+            assert -(-shape[0] // 128) * -(-shape[1] // 128) * max(S, 1) >= 512, (shape, S)
 
 
 def test_bf16_plans(C):
