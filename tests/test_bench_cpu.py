@@ -80,6 +80,27 @@ def test_bench_reports_secondary_modes():
     assert d0["modes"] == {}
 
 
+def test_bench_eight_ranks_driver_form():
+    """The driver's N = 8 launch (torchrun --nproc-per-node 8 ... bench.py --gpus 8)
+    rehearsed on gloo: every secondary mode, serialized and overlapped, runs at
+    ws = 8 with its agreed plan; batch_parallel's global batch is rounded up to
+    one element per rank, matrix_parallel shards 8 ways."""
+    d = _bench(8, "--size", "128", "--steps", "2", "--warmup", "1", "--extra-steps", "1",
+               "--extra-warmup", "0")
+    assert d["n_gpus"] == 8 and d["world_size_seen"] == 8 and d["collectives_verified"] is True
+    assert d["config"]["parallelism"] == "independent8" and d["scaling_efficiency"] is not None
+    assert set(d["modes"]) == {"batch_parallel", "batch_parallel+overlap", "matrix_parallel",
+                               "matrix_parallel+overlap"}
+    for key, m in d["modes"].items():
+        assert "error" not in m, (key, m)
+        gb = 8 if key.startswith("batch") else 1
+        assert m["global_batch"] == gb and m["parallelism"] == ("dp8" if gb == 8 else "tp8")
+        assert m["value"] == pytest.approx(2.0 * 128 ** 3 * gb / (m["ms_per_step"] / 1e3) / 1e12,
+                                           rel=0.02, abs=1e-4)
+        if key.endswith("+overlap"):
+            assert "plan" in m, key
+
+
 def _plain(*args, env_extra=None, timeout=300):
     """bench.py run WITHOUT torchrun (the driver's 1-GPU form; --gpus N self-launches)."""
     env = dict(os.environ, OMP_NUM_THREADS="1", **(env_extra or {}))
