@@ -126,8 +126,12 @@ def test_bench_self_launches_n_ranks():
     d = _line(r)
     assert d["n_gpus"] == 4 and d["config"]["parallelism"] == "independent4"
     assert d["single_gpu_tflops"] > 0
-    assert d["scaling_efficiency"] == pytest.approx(d["value"] / (4 * d["single_gpu_tflops"]),
-                                                    rel=1e-3, abs=2e-4)  # fields rounded to 4 places
+    # value / single / efficiency are each rounded to 4 places, and on the CPU at this size
+    # the TFLOPS fields are ~1e-3, so bound the efficiency by the rounding interval instead
+    # of a relative tolerance.
+    v, s, h = d["value"], d["single_gpu_tflops"], 5e-5
+    lo, hi = (v - h) / (4 * (s + h)), (v + h) / (4 * max(s - h, 1e-12))
+    assert lo - h <= d["scaling_efficiency"] <= hi + h, (d["scaling_efficiency"], lo, hi)
     for key, m in d["modes"].items():
         assert m["scaling_efficiency"] is not None, key
 
