@@ -69,7 +69,7 @@ from pytorch_distributed_matmul_benchmark_amd.parallel.dist import (  # noqa: E4
     DistContext, all_ok, barrier, cleanup_distributed, gather_scalars, reduce_scalar,
     setup_distributed, verify_collectives)
 from pytorch_distributed_matmul_benchmark_amd.parallel.overlap import (  # noqa: E402
-    BidirRing, OverlapPipeline, all_gather_now, compute_ctx, compute_stream, plan_for_units)
+    BidirRing, OverlapPipeline, all_gather_now, all_reduce_now, compute_ctx, compute_stream, plan_for_units)
 from pytorch_distributed_matmul_benchmark_amd.parallel.partition import (  # noqa: E402
     column_shard, global_batch, local_batch)
 from pytorch_distributed_matmul_benchmark_amd.utils.telemetry import (  # noqa: E402
@@ -136,19 +136,21 @@ class Workload:
                 units = ([(A[b], B[b], C[b]) for b in range(lb)] if lb >= 2 else
                          [(A[0], B[0], C[0]), (A[0], B[0], torch.empty_like(C[0]))])
                 cs = CommStream(dev)
+                ar = cs.all_reduce_direct if a.allreduce == "direct" else cs.all_reduce
 
                 def coll(r, p, s, e, after, done):
-                    cs.all_reduce(units[r][2][s:e], after=after, done=done)
+                    ar(units[r][2][s:e], after=after, done=done)
                 self._pipeline(a, units, coll, lb, "all_reduce", n * n * C.element_size(), cs)
             else:
                 self._serial_split()
+                cs = CommStream(dev) if a.allreduce == "direct" else None
 
                 def step():
                     self._seg(0)
                     self._mm(A, B, C)
                     self._seg(1)
                     if ws > 1:
-                        dist.all_reduce(C)
+                        all_reduce_now(C, a.allreduce, cs)
                     self._seg(2)
             self.flops = flop_gemm * gb
             self.global_batch, self.parallelism = gb, f"dp{ws}"
@@ -232,7 +234,8 @@ class Workload:
                                    native=self.backend == "native", requested=a.chunks,
                                    steps=max(a.extra_steps, 1), owner=self._mask)
         if not self.plan.overlap:  # the planner refuses a losing overlap: serialize
-            self.step = self._serial_fallback(units, per_step, kind, a.allgather)
+            self.step = self._serial_fallback(units, per_step, kind,
+                                              a.allreduce if kind == "all_reduce" else a.allgather)
             return
         self.pipe = OverlapPipeline(self._mm, units, coll, self.ctx.device, self.plan,
                                     per_step=per_step, compute=self.comp, owner=self._mask, comm=cs)
@@ -258,7 +261,7 @@ class Workload:
                 if ws <= 1:
                     continue
                 if kind == "all_reduce":
-                    dist.all_reduce(Cr)
+                    all_reduce_now(Cr, impl, cs)
                 else:
                     if r not in gathered:
                         gathered[r] = torch.empty(ws * Cr.shape[0], Cr.shape[1], device=dev,
@@ -560,6 +563,9 @@ def main() -> int:
     ap.add_argument("--comm-cus", type=int, default=0,
                     help="overlap: CUs kept free of GEMM workgroups for RCCL (CU-masked "
                          "compute stream; 0 = no mask)")
+    ap.add_argument("--allreduce", default="rccl", choices=["rccl", "direct"],
+                    help="batch_parallel all-reduce: RCCL, or a two-shot exchange over P2P links "
+                         "(reduce-scatter group, native fp32 sum, all-gather group)")
     ap.add_argument("--allgather", default="rccl", choices=["rccl", "direct"],
                     help="matrix_parallel all-gather: RCCL, or direct P2P to every peer at once")
     ap.add_argument("--backend", default="native", choices=["native", "torch"])

@@ -29,10 +29,9 @@ Differences:
 from __future__ import annotations
 
 import torch
-import torch.distributed as dist
-
 from ..parallel.comm import CommStream, current_stream
-from ..parallel.overlap import OverlapPipeline, compute_ctx, compute_stream, plan_for_units
+from ..parallel.overlap import (OverlapPipeline, all_reduce_now, compute_ctx, compute_stream,
+                                plan_for_units)
 from ..parallel.dist import DistContext
 from ..parallel.partition import global_batch, local_batch
 from ..utils.metrics import gemm_flops, tflops_from
@@ -53,11 +52,14 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     distributed = ctx.is_distributed
     flops = gemm_flops(n, n, n, lb)
 
+    direct = CommStream(dev) if w.allreduce == "direct" else None
+
     def reduce_all():
         if distributed:
-            dist.all_reduce(C)
+            all_reduce_now(C, w.allreduce, direct)
 
-    extra = {"global_batch": gb, "local_batch": lb, "overlap": bool(w.overlap and distributed)}
+    extra = {"global_batch": gb, "local_batch": lb, "overlap": bool(w.overlap and distributed),
+             "allreduce": w.allreduce}
     plan = None
     units = ([(A[b], B[b], C[b]) for b in range(lb)] if lb >= 2 else
              [(A[0], B[0], C[0]), (A[0], B[0], torch.empty_like(C[0]))])
@@ -95,10 +97,11 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
                          extra=extra)
         checked = [C[b] for b in range(lb)]
     else:
-        cs = CommStream(dev)
+        cs = direct or CommStream(dev)
+        ar = cs.all_reduce_direct if w.allreduce == "direct" else cs.all_reduce
 
         def coll(r, p, s, e, after, done):
-            cs.all_reduce(units[r][2][s:e], after=after, done=done)
+            ar(units[r][2][s:e], after=after, done=done)
 
         pipe = OverlapPipeline(mm, units, coll, dev, plan, per_step=lb, compute=compute,
                                owner=owner, comm=cs)

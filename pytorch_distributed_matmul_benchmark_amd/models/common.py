@@ -38,6 +38,7 @@ class Workload:
     chunks: int = 0             # overlap: collective pieces per GEMM (signalled; 0 = planner, 1 = whole)
     comm_cus: int = 0           # overlap: CUs kept free of GEMM workgroups for RCCL (CU-masked stream)
     allgather: str = "rccl"     # matrix_parallel all-gather: rccl | direct (P2P to every peer at once)
+    allreduce: str = "rccl"     # all-reduce: rccl | direct (two-shot over P2P links, native sum)
     graph: bool = False         # independent: replay the timed loop as one hipGraph
     check: bool = False         # verify the result against a float64 reference
     min_warmup_ms: float = 0.0  # extend the warm-up until this much GPU time has run (DVFS)

@@ -11,9 +11,8 @@ and efficiency is compute / total (100 % = comm free).
 from __future__ import annotations
 
 import torch
-import torch.distributed as dist
-
-from ..parallel.comm import current_stream
+from ..parallel.comm import CommStream, current_stream
+from ..parallel.overlap import all_reduce_now
 from ..parallel.dist import DistContext
 from ..utils.metrics import gemm_flops, tflops_from
 from ..utils.timing import SegmentTimer
@@ -29,10 +28,12 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     mm = gemm_fn(w, dev)
     label = kernel_label(w, A, B, C)
     distributed = ctx.is_distributed
+    direct = CommStream(dev) if w.allreduce == "direct" else None
+
     def step():
         mm(A, B, C)
         if distributed:
-            dist.all_reduce(C)
+            all_reduce_now(C, w.allreduce, direct)
 
     warmup(step, w, ctx)
     align_ranks(ctx)
@@ -43,7 +44,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         mm(A, B, C)
         seg.mark("compute", st)
         if distributed:
-            dist.all_reduce(C)
+            all_reduce_now(C, w.allreduce, direct)
         seg.mark("comm", st)
     tot = seg.totals_ms()
     it = max(w.iters, 1)
@@ -52,7 +53,8 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     res = ModeResult(mode="data_parallel", n=n, world_size=ws, avg_ms=comp + comm,
                      flops_local=flops, flops_total=flops * ws,
                      tflops=tflops_from(flops, comp / 1e3), compute_ms=comp, comm_ms=comm,
-                     compute_only_tflops=tflops_from(flops, comp / 1e3), kernel=label)
+                     compute_only_tflops=tflops_from(flops, comp / 1e3), kernel=label,
+                     extra={"allreduce": w.allreduce})
     if w.check:
         res.relerr = allreduced_relerr(ctx, A, B, C)
     return res

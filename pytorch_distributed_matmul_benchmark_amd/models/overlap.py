@@ -29,11 +29,11 @@ compute-only TFLOPS.
 from __future__ import annotations
 
 import torch
-import torch.distributed as dist
 
 from ..ops import gemm
 from ..parallel.comm import CommStream, current_stream, new_event
 from ..parallel.dist import DistContext
+from ..parallel.overlap import all_reduce_now
 from ..utils.metrics import gemm_flops, tflops_from
 from ..utils.timing import Stopwatch, synchronize, time_loop_ms
 from .common import (ModeResult, Workload, align_ranks, allreduced_relerr, gemm_fn, kernel_label,
@@ -59,14 +59,17 @@ def run(w: Workload, ctx: DistContext, mode: str = "overlap", depth: int = None)
 
     used = [True] + [False] * (depth - 1)
     if depth == 1 or not distributed:
+        direct = CommStream(dev) if w.allreduce == "direct" else None
+
         def run_iters(k):
             for _ in range(k):
                 mm(As[0], Bs[0], Cs[0])
                 if distributed:
-                    dist.all_reduce(Cs[0])
+                    all_reduce_now(Cs[0], w.allreduce, direct)
         finish = (lambda: None)
     else:
         cs = CommStream(dev)
+        ar = cs.all_reduce_direct if w.allreduce == "direct" else cs.all_reduce
         ready = [new_event(dev) for _ in range(depth)]
         done = [new_event(dev) for _ in range(depth)]
         used[0] = False
@@ -81,7 +84,7 @@ def run(w: Workload, ctx: DistContext, mode: str = "overlap", depth: int = None)
                 with gemm.shared_device():  # earlier buffers' all-reduces run beside it
                     mm(As[i], Bs[i], Cs[i])
                 ready[i].record(compute)
-                cs.all_reduce(Cs[i], after=ready[i], done=done[i])
+                ar(Cs[i], after=ready[i], done=done[i])
                 used[i] = True
 
         def finish():

@@ -28,7 +28,7 @@ ARCH = os.environ.get("PDMB_OFFLOAD_ARCH", "gfx950")
 EXT_NAME = "_C"
 
 HIP_SOURCES = ["gemm_mfma256.hip", "gemm_f32_256.hip", "gemm_fp8.hip", "gemm_generic.hip", "gemm_w4.hip",
-               "gemm_tile.hip", "gemm_f32_w4.hip", "gemm_f32_tile.hip", "gemm_dispatch.cpp"]
+               "gemm_tile.hip", "gemm_f32_w4.hip", "gemm_f32_tile.hip", "reduce.hip", "gemm_dispatch.cpp"]
 HOST_SOURCES = ["bindings.cpp"]
 
 

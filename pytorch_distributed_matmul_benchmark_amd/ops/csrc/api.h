@@ -195,6 +195,13 @@ const char* kernel_name(int kernel);
 // workgroups, the footprint of an RCCL collective's channels.
 hipError_t comm_proxy(void* dst, const void* src, size_t bytes, int blocks, hipStream_t stream);
 
+// dst[i] = sum over s < nsrc of srcs[s][i] (fp32 accumulate, sources in index
+// order, RNE to the element type; dtype 0 f32, 1 f16, 2 bf16). dst may alias a
+// source; 16-B vectors when every pointer is 16-B aligned. The local step of the direct two-shot
+// all-reduce (reduce.hip).
+constexpr int kMaxReduceSrcs = 16;
+hipError_t reduce_sum(void* dst, const void* const* srcs, int nsrc, int64_t n, int dtype, hipStream_t stream);
+
 // Diagnostic builds write per-wave stamps here (device memory; nullptr = off).
 void set_debug_buffer(void* p);
 

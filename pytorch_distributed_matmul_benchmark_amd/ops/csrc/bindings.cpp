@@ -309,6 +309,26 @@ void comm_proxy(const at::Tensor& dst, const at::Tensor& src, int64_t blocks) {
             "comm_proxy");
 }
 
+// out = sum of srcs (fp32 accumulate, in list order) on the current stream: the
+// local step of the direct two-shot all-reduce. out may be one of srcs.
+void reduce_sum(const at::Tensor& out, const std::vector<at::Tensor>& srcs) {
+  TORCH_CHECK(!srcs.empty() && (int)srcs.size() <= pdmb::kMaxReduceSrcs, "pdmb: reduce_sum takes 1..",
+              pdmb::kMaxReduceSrcs, " sources");
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous(), "pdmb: reduce_sum out must be a contiguous GPU tensor");
+  const int dt = dtype_code(out.scalar_type());
+  TORCH_CHECK(dt <= 2, "pdmb: reduce_sum takes float32 / float16 / bfloat16");
+  std::vector<const void*> ptrs;
+  for (const auto& t : srcs) {
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.device() == out.device() &&
+                    t.scalar_type() == out.scalar_type() && t.numel() == out.numel(),
+                "pdmb: reduce_sum sources must be contiguous, on out's device, of its dtype and length");
+    ptrs.push_back(t.data_ptr());
+  }
+  c10::hip::HIPGuard guard(out.device().index());
+  hipStream_t s = c10::hip::getCurrentHIPStream(out.device().index()).stream();
+  check_hip(pdmb::reduce_sum(out.data_ptr(), ptrs.data(), (int)ptrs.size(), out.numel(), dt, s), "reduce_sum");
+}
+
 // Diagnostic: set (or clear, with None) the device buffer the stamp kernel writes.
 void set_debug_buffer(c10::optional<at::Tensor> buf) {
   if (buf.has_value()) {
@@ -352,6 +372,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("plan_shape", &plan_shape, py::arg("dtype"), py::arg("M"), py::arg("N"), py::arg("K"),
         py::arg("batch") = 1, py::arg("kernel") = 0, py::arg("cus") = 0);
   m.def("comm_proxy", &comm_proxy, py::arg("dst"), py::arg("src"), py::arg("blocks"));
+  m.def("reduce_sum", &reduce_sum, "out = sum(srcs) (fp32 accumulate, list order)", py::arg("out"),
+        py::arg("srcs"));
   m.def("set_debug_buffer", &set_debug_buffer, py::arg("buf") = py::none());
   m.def("create_cu_masked_stream", &create_cu_masked_stream, py::arg("device"),
         py::arg("excluded"));

@@ -115,24 +115,31 @@ class CommStream:
         every hop drives two xGMI links (one per direction) instead of one.
         Transfer i carries tag i (gloo matches on it; RCCL matches in issue
         order, which is the same list order on every rank), so two transfers
-        between the same pair (ws = 2) never cross."""
+        between the same pair (ws = 2) never cross; a (tensor, rank, tag)
+        triple sets the tag explicitly (lists that skip empty transfers)."""
         with stream_ctx(self.stream):
             if after is not None:
                 self.wait_event(after)
             # gloo P2P takes host memory only: GPU tensors of a gloo rehearsal
             # (ranks sharing one GPU) hop through host copies on this stream.
-            staged = bool(sends) and sends[0][0].is_cuda and dist.get_backend(self.group) == "gloo"
+            first = (list(sends) + list(recvs))[:1]
+            staged = bool(first) and first[0][0].is_cuda and dist.get_backend(self.group) == "gloo"
             ops, landing = [], []
             for i in range(max(len(sends), len(recvs))):
                 if i < len(sends):
-                    t, dst = sends[i]
+                    t, dst, *tag = sends[i]
                     ops.append(dist.P2POp(dist.isend, t.cpu() if staged else t, dst,
-                                          group=self.group, tag=i))
+                                          group=self.group, tag=tag[0] if tag else i))
                 if i < len(recvs):
-                    t, src = recvs[i]
+                    t, src, *tag = recvs[i]
                     r_t = torch.empty(t.shape, dtype=t.dtype) if staged else t
                     landing.append((t, r_t))
-                    ops.append(dist.P2POp(dist.irecv, r_t, src, group=self.group, tag=i))
+                    ops.append(dist.P2POp(dist.irecv, r_t, src, group=self.group,
+                                          tag=tag[0] if tag else i))
+            if not ops:
+                if done is not None:
+                    done.record(self.stream)
+                return []
             works = dist.batch_isend_irecv(ops)
             for wk in works:
                 wk.wait()
@@ -166,9 +173,91 @@ class CommStream:
                                     for d in range(1, group_ws)],
                                    after=None, done=done)
 
+    def _scratch(self, t: torch.Tensor, numel: int) -> torch.Tensor:
+        """Landing space for the ws-1 chunks of the reduce-scatter phase, one
+        per (device, dtype), grown on demand. Only the comm stream touches it,
+        so stream order makes reuse across collectives safe."""
+        buf = getattr(self, "_ar_scratch", None)
+        if buf is None or buf.dtype != t.dtype or buf.numel() < numel:
+            with stream_ctx(self.stream):
+                buf = torch.empty(max(numel, 1), dtype=t.dtype, device=t.device)
+            self._ar_scratch = buf
+        return buf
+
+    def all_reduce_direct(self, t: torch.Tensor, after=None, done=None):
+        """SUM all-reduce of contiguous ``t`` as a two-shot exchange over
+        point-to-point links (``--allreduce direct``):
+
+          1. reduce-scatter: ``t`` is cut into ws chunks (64-element multiples);
+             chunk p goes straight to rank p and every peer's copy of this
+             rank's chunk lands in a scratch slot, as ONE batched P2P group;
+          2. the native ``reduce_sum`` kernel (ops/csrc/reduce.hip) adds the ws
+             copies in rank order with fp32 accumulation into this rank's chunk;
+          3. all-gather: the reduced chunk goes to every peer, theirs land in
+             place, again one batched group.
+
+        On a fully connected 8 x MI355X node every transfer of a phase has its
+        own xGMI link, each byte crosses a link twice (RCCL's ring all-reduce:
+        2(ws-1)/ws of the buffer through every ring hop), and the sum is exact
+        to fp32 then rounded once (a ring rounds after every hop). Ranks sum in
+        the same order, so every rank gets identical bits."""
+        assert t.is_contiguous(), "all_reduce_direct needs a contiguous tensor"
+        group_ws = dist.get_world_size(self.group)
+        me = dist.get_rank(self.group)
+        flat = t.view(-1)
+        n = flat.numel()
+        if group_ws == 1 or n == 0:
+            with stream_ctx(self.stream):
+                if after is not None:
+                    self.wait_event(after)
+                if done is not None:
+                    done.record(self.stream)
+            return None
+        chunk = -(-n // group_ws)
+        chunk = -(-chunk // 64) * 64  # 16-B aligned chunk starts for every dtype
+        bounds = [(min(r * chunk, n), min((r + 1) * chunk, n)) for r in range(group_ws)]
+        part = [flat[s:e] for s, e in bounds]
+        mine = part[me]
+        m = mine.numel()
+        g = lambda r: dist.get_global_rank(self.group, r) if self.group is not None else r  # noqa: E731
+        peers = [(me + d) % group_ws for d in range(1, group_ws)]
+        srcs = [(me - d) % group_ws for d in range(1, group_ws)]
+        scratch = self._scratch(t, (group_ws - 1) * chunk)
+        slot = {src: scratch[i * chunk:i * chunk + m] for i, src in enumerate(srcs)}
+        # 1. reduce-scatter (chunks past the end are empty on every rank alike;
+        # the tag is the ring distance d, the same at both ends of a transfer)
+        sends = [(part[p], g(p), d) for d, p in enumerate(peers, 1) if part[p].numel()]
+        recvs = [(slot[s], g(s), d) for d, s in enumerate(srcs, 1) if m]
+        self.exchange_multi(sends, recvs, after=after)
+        # 2. local sum in rank order
+        with stream_ctx(self.stream):
+            if m:
+                ordered = [mine if r == me else slot[r] for r in range(group_ws)]
+                reduce_sum_(mine, ordered)
+        # 3. all-gather of the reduced chunks
+        sends = [(mine, g(p), d) for d, p in enumerate(peers, 1)] if m else []
+        recvs = [(part[s], g(s), d) for d, s in enumerate(srcs, 1) if part[s].numel()]
+        return self.exchange_multi(sends, recvs, done=done)
+
     def synchronize(self) -> None:
         if self.stream is not None:
             self.stream.synchronize()
+
+
+def reduce_sum_(out: torch.Tensor, srcs) -> None:
+    """out = sum(srcs) with fp32 accumulation in list order, rounded once (out
+    may be one of srcs). GPU tensors run the native ``reduce_sum`` kernel —
+    no eager fallback on a GPU; CPU tensors (gloo rehearsals) the same sum in
+    torch."""
+    if out.is_cuda:
+        from ..ops import _native
+
+        _native.load(build_if_missing=False).reduce_sum(out, list(srcs))
+        return
+    acc = torch.zeros(out.shape, dtype=torch.float32)
+    for s in srcs:
+        acc += s.float()
+    out.copy_(acc)
 
 
 def all_reduce_(t: torch.Tensor, group=None) -> None:

@@ -432,3 +432,21 @@ def all_gather_now(out: torch.Tensor, inp: torch.Tensor, impl: str = "rccl",
     comm.all_gather_direct(out, inp, after=ready, done=done)
     if cur is not None:
         cur.wait_event(done)
+
+
+def all_reduce_now(t: torch.Tensor, impl: str = "rccl", comm: Optional[CommStream] = None) -> None:
+    """Serialized SUM all-reduce on the current stream: RCCL's ``all_reduce``,
+    or the direct two-shot exchange (``CommStream.all_reduce_direct``) on
+    ``comm`` with the current stream joined behind it."""
+    import torch.distributed as dist
+
+    if impl == "rccl":
+        dist.all_reduce(t)
+        return
+    dev = t.device
+    cur = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
+    ready, done = new_event(dev), new_event(dev)
+    ready.record(cur)
+    comm.all_reduce_direct(t, after=ready, done=done)
+    if cur is not None:
+        cur.wait_event(done)

@@ -94,6 +94,10 @@ def build_parser(kind: str) -> argparse.ArgumentParser:
                    help="matrix_parallel all-gather: RCCL's all_gather_into_tensor, or direct: one "
                         "batched P2P group sending this rank's shard to every peer at once (each "
                         "over its own xGMI link on a fully connected node)")
+    g.add_argument("--allreduce", default="rccl", choices=["rccl", "direct"],
+                   help="batch_parallel / data_parallel / overlap all-reduce: RCCL's all_reduce, or "
+                        "direct: a two-shot exchange over point-to-point links (reduce-scatter as one "
+                        "batched P2P group, native fp32-accumulating sum, all-gather as another)")
     g.add_argument("--comm-cus", type=int, default=0,
                    help="--overlap: CUs kept free of GEMM workgroups for RCCL (CU-masked "
                         "compute stream, spread over the 8 XCDs; 0 = no mask)")
@@ -133,7 +137,7 @@ def _workload(args, n: int, dtype: torch.dtype) -> Workload:
     return Workload(n=n, dtype=dtype, iters=args.iterations, warmup=args.warmup, seed=args.seed,
                     backend=args.backend, kernel=args.kernel, batch=args.batch,
                     overlap=args.overlap, chunks=args.chunks,
-                    comm_cus=args.comm_cus, allgather=args.allgather, graph=args.graph,
+                    comm_cus=args.comm_cus, allgather=args.allgather, allreduce=args.allreduce, graph=args.graph,
                     check=args.check,
                     min_warmup_ms=args.min_warmup_ms)
 

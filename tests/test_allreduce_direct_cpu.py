@@ -1,0 +1,125 @@
+"""Direct two-shot all-reduce (parallel/comm.py ``CommStream.all_reduce_direct``)
+on gloo, ws = 2 / 3 / 4: every rank must end with the same bits, equal to the
+fp32 sum of the ranks' inputs in rank order rounded once to the dtype; sizes
+cover empty trailing chunks (numel < ws * 64), odd lengths and 2-D row slices.
+The CLI paths (batch_parallel / data_parallel / overlap with ``--allreduce
+direct --check``) run end to end under torchrun."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+SIZES = [1, 7, 63, 130, 1000, 4099]
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _inputs(rank, n, dtype):
+    g = torch.Generator().manual_seed(1000 * rank + n)
+    return torch.randn(n, generator=g).to(dtype)
+
+
+def _worker(rank, ws, port, dtype_name, q):
+    from pytorch_distributed_matmul_benchmark_amd.parallel.comm import CommStream
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    dtype = getattr(torch, dtype_name)
+    cs = CommStream(torch.device("cpu"))
+    out = {}
+    for n in SIZES:
+        t = _inputs(rank, n, dtype)
+        cs.all_reduce_direct(t)
+        out[n] = t.clone()
+    # a row slice of a 2-D tensor (the overlap pipeline reduces row pieces)
+    big = torch.stack([_inputs(rank, 96, dtype) for _ in range(10)])
+    cs.all_reduce_direct(big[3:7])
+    out["rows"] = big.clone()
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ws", [2, 3, 4])
+@pytest.mark.parametrize("dtype_name", ["float32", "bfloat16"])
+def test_all_reduce_direct_matches_rank_order_fp32_sum(ws, dtype_name):
+    dtype = getattr(torch, dtype_name)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, dtype_name, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(ws))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for n in SIZES:
+        acc = torch.zeros(n)
+        for r in range(ws):
+            acc += _inputs(r, n, dtype).float()
+        want = acc.to(dtype)
+        for r in range(ws):
+            assert torch.equal(res[r][n], want), (ws, n, r)
+    # rows 3..6 reduced, the others untouched
+    for r in range(ws):
+        mine = torch.stack([_inputs(r, 96, dtype) for _ in range(10)])
+        acc = torch.zeros(4, 96)
+        for q_ in range(ws):
+            acc += torch.stack([_inputs(q_, 96, dtype) for _ in range(10)])[3:7].float()
+        assert torch.equal(res[r]["rows"][3:7], acc.to(dtype))
+        assert torch.equal(res[r]["rows"][:3], mine[:3]) and torch.equal(res[r]["rows"][7:], mine[7:])
+
+
+def _torchrun(ws, script, *args):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ws}",
+           "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, script), *args]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd="/tmp")
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return r.stdout
+
+
+@pytest.mark.parametrize("ws,extra", [(2, []), (3, ["--overlap", "--chunks", "2"]),
+                                      (4, ["--overlap", "--chunks", "1"])])
+def test_batch_parallel_direct_allreduce_cli(ws, extra):
+    out = _torchrun(ws, "matmul_scaling_benchmark.py", "--device", "cpu", "--sizes", "200",
+                    "--iterations", "2", "--warmup", "1", "--dtype", "float32", "--mode",
+                    "batch_parallel", "--allreduce", "direct", "--check", *extra)
+    assert "PASS" in out and "FAIL" not in out and "ERROR" not in out
+
+
+def test_backup_modes_direct_allreduce_cli():
+    out = _torchrun(2, "backup/matmul_distributed_benchmark.py", "--device", "cpu", "--sizes", "160",
+                    "--iterations", "2", "--warmup", "1", "--dtype", "float32", "--allreduce",
+                    "direct", "--check")
+    assert "PASS" in out and "FAIL" not in out
+    for mode in ("no_overlap", "overlap", "pipeline"):
+        out = _torchrun(2, "backup/matmul_overlap_benchmark.py", "--device", "cpu", "--sizes", "160",
+                        "--iterations", "3", "--warmup", "1", "--dtype", "float32", "--mode", mode,
+                        "--allreduce", "direct", "--check")
+        assert "PASS" in out and "FAIL" not in out, mode
+
+
+def test_bench_direct_allreduce_ws2():
+    import json
+
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--gpus", "2",
+                        "--size", "128", "--steps", "2", "--warmup", "1", "--extra-steps", "2",
+                        "--extra-warmup", "1", "--allreduce", "direct"],
+                       capture_output=True, text=True, timeout=300, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    for key in ("batch_parallel", "batch_parallel+overlap"):
+        assert d["modes"][key] and d["modes"][key]["value"] > 0, key

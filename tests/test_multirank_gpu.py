@@ -73,7 +73,9 @@ def test_two_ranks_share_gpu_bench_ring():
     ("matrix_parallel", ["--overlap", "--chunks", "1"]),
     ("batch_parallel", ["--overlap", "--chunks", "4", "--batch", "2"]),
     ("matrix_parallel", ["--allgather", "direct"]),
-    ("matrix_parallel", ["--allgather", "direct", "--overlap", "--chunks", "2"])])
+    ("matrix_parallel", ["--allgather", "direct", "--overlap", "--chunks", "2"]),
+    ("batch_parallel", ["--allreduce", "direct"]),
+    ("batch_parallel", ["--allreduce", "direct", "--overlap", "--chunks", "2"])])
 def test_two_ranks_cu_masked_overlap_checked(mode, extra):
     """The overlap pipeline (ring of outputs; signalled pieces where --chunks > 1
     and the GEMM is W4), optionally on a CU-masked stream: the float64
