@@ -65,7 +65,8 @@ struct Opts {
   Mode mode = kIndependent;
   int batch = 4, chunks = 1, kernel = 0;  // chunks: collective pieces per GEMM (signalled)
   bool overlap = false, check = false;
-  bool direct = false;  // --allgather direct: P2P to every peer in one group (own link each)
+  bool direct = false;     // --allgather direct: P2P to every peer in one group (own link each)
+  bool direct_ar = false;  // --allreduce direct: two-shot P2P exchange + native reduce_sum
   std::string json;
 };
 
@@ -474,6 +475,48 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     const bool ov = o.overlap && dist;
     // overlap ring: the batch's own outputs (lb >= 2) or C plus a second buffer (C1/C2)
     Buf C2(ov && lb == 1 ? mat * oes : 0);
+    // SUM all-reduce of `count` output elements in place: RCCL, or --allreduce
+    // direct (parallel/comm.py all_reduce_direct): chunk p goes straight to
+    // rank p and the peers' copies of this rank's chunk land in scratch (one
+    // group), reduce_sum adds the ws copies in rank order in fp32 into the
+    // chunk, then the reduced chunk goes to every peer (a second group). Every
+    // transfer of a group has its own xGMI link on a fully connected node.
+    auto ar_chunk = [&](size_t count) { return ((count + ws - 1) / ws + 63) / 64 * 64; };  // 16-B aligned chunks
+    const size_t ar_chunk_max = ar_chunk(lb * mat);
+    Buf ARs(o.direct_ar && ws > 1 ? (size_t)(ws - 1) * ar_chunk_max * oes : 0);
+    auto allreduce = [&](void* buf, size_t count, hipStream_t s) {
+      if (!o.direct_ar) {
+        NCCL_OK(ncclAllReduce(buf, buf, count, nccl_out_type(dt), ncclSum, comm, s));
+        return;
+      }
+      if (ws == 1 || count == 0) return;
+      const size_t chunk = ar_chunk(count);
+      auto lo_of = [&](int r) { return std::min(count, (size_t)r * chunk); };
+      auto len_of = [&](int r) { return std::min(count, (size_t)(r + 1) * chunk) - lo_of(r); };
+      char* base = (char*)buf;
+      const size_t m = len_of(rank);
+      auto slot = [&](int d) { return (char*)ARs.p + (size_t)(d - 1) * chunk * oes; };  // from rank - d
+      NCCL_OK(ncclGroupStart());
+      for (int d = 1; d < ws; ++d) {
+        const int to = (rank + d) % ws, from = (rank - d + ws) % ws;
+        if (len_of(to)) NCCL_OK(ncclSend(base + lo_of(to) * oes, len_of(to), nccl_out_type(dt), to, comm, s));
+        if (m) NCCL_OK(ncclRecv(slot(d), m, nccl_out_type(dt), from, comm, s));
+      }
+      NCCL_OK(ncclGroupEnd());
+      if (m) {
+        std::vector<const void*> srcs(ws);
+        for (int r = 0; r < ws; ++r)
+          srcs[r] = r == rank ? (const void*)(base + lo_of(rank) * oes) : (const void*)slot((rank - r + ws) % ws);
+        HIP_OK(pdmb::reduce_sum(base + lo_of(rank) * oes, srcs.data(), ws, (int64_t)m, out_dtype(dt), s));
+      }
+      NCCL_OK(ncclGroupStart());
+      for (int d = 1; d < ws; ++d) {
+        const int to = (rank + d) % ws, from = (rank - d + ws) % ws;
+        if (m) NCCL_OK(ncclSend(base + lo_of(rank) * oes, m, nccl_out_type(dt), to, comm, s));
+        if (len_of(from)) NCCL_OK(ncclRecv(base + lo_of(from) * oes, len_of(from), nccl_out_type(dt), from, comm, s));
+      }
+      NCCL_OK(ncclGroupEnd());
+    };
     Pipeline pipe;
     if (ov) {
       std::vector<pdmb::Problem> ring;
@@ -483,7 +526,7 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
       if (lb == 1) ring.push_back(problem(dt, A.p, B.p, C2.p, n, n, n, n, n, n));
       pipe.coll = [&](int r, int r0, int r1, int) {
         char* c = (char*)pipe.slots[r].p.C + (size_t)r0 * n * oes;
-        NCCL_OK(ncclAllReduce(c, c, (size_t)(r1 - r0) * n, nccl_out_type(dt), ncclSum, comm, cs));
+        allreduce(c, (size_t)(r1 - r0) * n, cs);
       };
       pipe.init(ring, o.chunks, o.kernel, st, cs, scr, rank);
       res.chunks = (int)pipe.pieces.size();
@@ -491,7 +534,7 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     auto serial_iter = [&](hipEvent_t em) {
       gemm(p, o.kernel, st, scr);
       if (em) HIP_OK(hipEventRecord(em, st));
-      if (dist) NCCL_OK(ncclAllReduce(C.p, C.p, lb * mat, nccl_out_type(dt), ncclSum, comm, st));
+      if (dist) allreduce(C.p, lb * mat, st);
     };
     for (int i = 0; i < o.warmup; ++i) {
       if (ov) {
@@ -815,7 +858,8 @@ void usage() {
   std::printf(
       "pdmb_bench [--gpus N] [--sizes N ...] [--iterations I] [--warmup W]\n"
       "           [--dtype bfloat16|float16|float32|float8_e4m3fn] [--mode independent|batch_parallel|matrix_parallel|ring_parallel]\n"
-      "           [--batch B] [--overlap] [--chunks C] [--allgather rccl|direct] [--kernel ID]\n"
+      "           [--batch B] [--overlap] [--chunks C] [--allgather rccl|direct] [--allreduce rccl|direct]\n"
+      "           [--kernel ID]\n"
       "           [--check] [--json FILE]\n");
 }
 
@@ -835,6 +879,7 @@ Opts parse(int argc, char** argv) {
     else if (a == "--kernel") o.kernel = std::stoi(next());
     else if (a == "--overlap") o.overlap = true;
     else if (a == "--allgather") o.direct = next() == "direct";
+    else if (a == "--allreduce") o.direct_ar = next() == "direct";
     else if (a == "--check") o.check = true;
     else if (a == "--json") o.json = next();
     else if (a == "--dtype") {

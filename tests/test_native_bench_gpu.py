@@ -25,6 +25,8 @@ def exe():
                                         ("matrix_parallel", ["--overlap"]),
                                         ("matrix_parallel", ["--allgather", "direct"]),
                                         ("matrix_parallel", ["--overlap", "--allgather", "direct"]),
+                                        ("batch_parallel", ["--allreduce", "direct"]),
+                                        ("batch_parallel", ["--overlap", "--allreduce", "direct"]),
                                         ("ring_parallel", [])])
 @pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
 def test_native_executor_modes(exe, mode, extra, dtype, tmp_path):
