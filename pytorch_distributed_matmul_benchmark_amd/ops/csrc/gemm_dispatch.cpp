@@ -355,9 +355,10 @@ static Plan plan(const Problem& p, int kernel) {
       if (S > 4 && p.splitk != S) continue;
       if (p.splitk > 0 && S != p.splitk) continue;
       if (!split_ok(p, m.kernel, S)) continue;
-      // a two-per-CU fp32 tile only on grids that put two on every CU: alone on
-      // a CU its 2-stage ring runs slower than the 4-stage one-per-CU tile
-      if (m.cls == 2 && m.occ > 1 &&
+      // auto takes a two-per-CU fp32 tile only on grids that put two on every CU:
+      // alone on a CU its 2-stage ring runs slower than the 4-stage one-per-CU
+      // tile (an explicit request runs it on any grid)
+      if (kernel == kAuto && m.cls == 2 && m.occ > 1 &&
           tiles_of(p, m.kernel) * S < (long long)(p.cus > 0 ? p.cus : device_cus()) * m.occ)
         continue;
       const double c = plan_cost(p, m.kernel, S);

@@ -81,3 +81,11 @@ def test_bf16_plans(C):
 def test_fp8_plans(C):
     assert plan(C, FP8, 16384, 16384, 16384)[0] == "pdmb_fp8_w4s"
     assert plan(C, FP8, 4096, 512, 4096)[0].startswith("pdmb_fp8_")
+
+
+def test_explicit_two_per_cu_fp32_tile_runs_any_grid(C):
+    """An explicit f32_t128x2 request gets a runnable plan (split >= 1) even on a
+    grid auto would not give it (one 128x128 tile, K = 32: a GPU test shape)."""
+    for shape in ((256, 256, 32), (128, 128, 64), (4096, 512, 4096)):
+        k, S, _, _ = plan(C, F32, *shape, kernel=53)
+        assert k == "pdmb_f32_t128x2_nn" and S >= 1, (shape, k, S)
