@@ -68,6 +68,7 @@ enum ExperimentKernel : int {
   kMfmaW4Unfused = 50,   // kMfmaW4 (bf16) with the epilogue after the last K-tile
   kF32T128B32 = 52,      // kF32T128 with one b32 LDS read per B operand (round 3's first version)
   kF32W4B32 = 54,        // kF32W4 with one b32 LDS read per B operand (round 2's version)
+  kF32_256p = 55,        // kF32_256s with software-pipelined fragments and a mid-tile barrier
 };
 
 // True iff this library was built with the experiment kernels.

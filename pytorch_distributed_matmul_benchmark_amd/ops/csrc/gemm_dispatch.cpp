@@ -100,7 +100,7 @@ static bool is_experiment(int k) {
     case kFp8W4Tall: case kFp8W4Wide: case kFp8W4Scaled: case kFp8W4Trace: case kMfmaW4Trace:
     case kFp8W4TS: case kFp8W4STS: case kMfmaW4STS: case kF32_256sDirect: case kFp8W4Unfused:
     case kT128Unfused: case kFp8T128Unfused: case kMfmaW4Unfused: case kF32T128B32:
-    case kF32W4B32:
+    case kF32W4B32: case kF32_256p:
       return true;
     default:
       return false;
@@ -158,10 +158,10 @@ int resolve_kernel(const Problem& p, int kernel) {
         const Plan pl = plan(p, kAuto);
         return pl.kernel == kMfmaW4 && pl.splitk == 1 && w4s_auto(p) ? kMfmaW4S : pl.kernel;
       }
-      // fp32: the planner over the exact-fp32 family — f32_256s (8 waves,
-      // 256x256: ahead of f32_w4 by 1.0-2.2 % on full grids, profiles/
-      // r2_f32_lds_epilogue_ab_box*.jsonl), f32_w4 (256x256, split-K) and
-      // f32_t128 (128x128, split-K) for grids that under-fill the chip.
+      // fp32: the planner over the exact-fp32 family — f32_t128x2 (two
+      // 128x128 workgroups per CU) on grids with >= 2 tiles per CU, f32_256s
+      // (8 waves, 256x256), f32_w4 (256x256, split-K) and f32_t128 (128x128,
+      // split-K) for grids that under-fill the chip.
       if (fast) return kMfma256d;
       if (!f32fast) return kGeneric;
       {
@@ -180,7 +180,7 @@ int resolve_kernel(const Problem& p, int kernel) {
     case kF32T128: return p.dtype == kF32 && supports(p, kF32T128) ? kF32T128 : -1;
     case kF32T128x2: return p.dtype == kF32 && supports(p, kF32T128) ? kF32T128x2 : -1;
 #ifdef PDMB_EXPERIMENTS
-    case kF32_256: case kF32NoDma: case kF32_256sDirect: return f32fast ? kernel : -1;
+    case kF32_256: case kF32NoDma: case kF32_256sDirect: case kF32_256p: return f32fast ? kernel : -1;
     case kT128Unfused: return t128 ? kernel : -1;
     case kF32T128B32: return p.dtype == kF32 && supports(p, kF32T128) ? kernel : -1;
     case kF32W4B32: return f32fast ? kernel : -1;
@@ -228,14 +228,18 @@ int resolve_kernel(const Problem& p, int kernel) {
 //
 // Exact fp32 (K-tile = 32; fp32 MFMA is not power-bound — f32_256s runs 95 %
 // MFMA busy at 2.38 GHz, profiles/r1_fp32_ablation.md — so no idle-CU boost):
-// f32_256s 7.0 us per 256x256 K-tile (152 TF at 16k), f32_w4 7.1, f32_t128
+// f32_256s 7.1 us per 256x256 K-tile (150-152 TF at 16k), f32_w4 7.1, f32_t128
 // 1.81 per 128x128 K-tile (fit to 4096 x {1024, 2048} x 4096: 237 / 471 us,
 // profiles/r3_f32_t128_ab.jsonl), f32_t128x2 3.53 per pair of co-resident
 // 128x128 workgroups (4096 x 2048 x 4096 458 us, 8192^3 7241 us:
 // profiles/r3_f32_t128x2_ab.jsonl), priced only where it has two workgroups
-// on every CU. The tiles are listed before f32_w4: they measured ahead of the
-// split W4 on every under-filled shard shape (4096 x 2048 x 4096 145.8 vs
-// 141.6 TF), so the 3 % hysteresis favours them.
+// on every CU. f32_t128x2 is listed first — the incumbent the 3 % hysteresis
+// keeps: on full grids it measured ahead of f32_256s in the same process
+// (4096^3 149.7 vs 148.4, 8192^3 151.9 vs 149.5, 16384^3 152.0 vs 150.0 TF;
+// profiles/r3i_f32_256p_ab.jsonl; f32_256s 7.05-7.16 us per 256x256 K-tile
+// across boxes). The other tiles are listed before f32_w4: they measured
+// ahead of the split W4 on every under-filled shard shape (4096 x 2048 x 4096
+// 145.8 vs 141.6 TF).
 struct KernelModel {
   int kernel, bm, bn, occ;
   double kt;
@@ -250,9 +254,9 @@ static constexpr KernelModel kModels[] = {
     {kFp8W4, 256, 256, 1, 1.30, 1, 4},
     {kFp8T256x128, 256, 128, 1, 0.80, 1, 8},
     {kFp8T128, 128, 128, 1, 0.42, 1, 8},
-    {kF32_256s, 256, 256, 1, 7.0, 2, 1},
-    {kF32T128, 128, 128, 1, 1.81, 2, 8},
     {kF32T128x2, 128, 128, 2, 3.53, 2, 8},
+    {kF32_256s, 256, 256, 1, 7.1, 2, 1},
+    {kF32T128, 128, 128, 1, 1.81, 2, 8},
     {kF32W4, 256, 256, 1, 7.1, 2, 8},
 };
 static int dt_class(const Problem& p) { return p.dtype == kFP8 ? 1 : p.dtype == kF32 ? 2 : 0; }
@@ -355,11 +359,14 @@ static Plan plan(const Problem& p, int kernel) {
       if (S > 4 && p.splitk != S) continue;
       if (p.splitk > 0 && S != p.splitk) continue;
       if (!split_ok(p, m.kernel, S)) continue;
-      // auto takes a two-per-CU fp32 tile only on grids that put two on every CU:
-      // alone on a CU its 2-stage ring runs slower than the 4-stage one-per-CU
-      // tile (an explicit request runs it on any grid)
+      // auto takes a two-per-CU fp32 tile only on grids whose tiles (not split
+      // slices) put two on every CU: alone on a CU its 2-stage ring runs slower
+      // than the 4-stage one-per-CU tile, and split into pairs it lost to the
+      // 4-stage tile on 4096 x 1024 x 4096 and 2048^3 (142.3 / 138.3 vs 146.5 /
+      // 143.8 TF, profiles/r3_f32_t128x2_ab.jsonl). An explicit request runs it
+      // on any grid.
       if (kernel == kAuto && m.cls == 2 && m.occ > 1 &&
-          tiles_of(p, m.kernel) * S < (long long)(p.cus > 0 ? p.cus : device_cus()) * m.occ)
+          tiles_of(p, m.kernel) < (long long)(p.cus > 0 ? p.cus : device_cus()) * m.occ)
         continue;
       const double c = plan_cost(p, m.kernel, S);
       if (c < bc * 0.97) {  // a different choice only for a clear win
@@ -988,6 +995,7 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kF32_256: return gemm_f32_256_launch(a, 0, stream);
     case kF32NoDma: return gemm_f32_256_launch(a, 9, stream);
     case kF32_256sDirect: return gemm_f32_256_launch(a, 10, stream);
+    case kF32_256p: return gemm_f32_256_launch(a, 11, stream);
     case kF32T128B32: return tiled_launch(p, kF32T128, a, p.workspace, p.workspace_bytes, stream, 1);
     case kF32W4B32: return tiled_launch(p, kF32W4, a, p.workspace, p.workspace_bytes, stream, 1);
     case kMfma256X1: case kMfma256X2: case kMfma256X4:
@@ -1155,6 +1163,7 @@ const char* kernel_name(int kernel) {
     case kFp8W4STS: return "pdmb_fp8_w4s_tstore";
     case kMfmaW4STS: return "pdmb_w4s_tstore";
     case kF32_256sDirect: return "pdmb_f32_256s_direct";
+    case kF32_256p: return "pdmb_f32_256p_nn";
     case kFp8W4Unfused: return "pdmb_fp8_w4_nt_unfused";
     case kT128Unfused: return "pdmb_t128_nn_unfused";
     case kFp8T128Unfused: return "pdmb_fp8_t128_nt_unfused";

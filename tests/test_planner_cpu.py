@@ -39,9 +39,11 @@ def test_f32_shards_fill_the_chip(C, n, ws):
         assert k in ("pdmb_f32_t128_nn", "pdmb_f32_t128x2_nn") or (k == "pdmb_f32_w4_nn" and S > 1)
 
 
-def test_f32_full_grids_keep_the_256_kernel(C):
+def test_f32_full_grids_take_two_128_tiles_per_cu(C):
+    """Full fp32 grids run f32_t128x2 (measured ahead of f32_256s at 4k / 8k /
+    16k in the same process, profiles/r3i_f32_256p_ab.jsonl)."""
     for n in (4096, 8192, 16384):
-        assert plan(C, F32, n, n, n)[0] == "pdmb_f32_256s_nn"
+        assert plan(C, F32, n, n, n)[0] == "pdmb_f32_t128x2_nn"
 
 
 def test_f32_planner_prefers_cheaper_plan(C):
