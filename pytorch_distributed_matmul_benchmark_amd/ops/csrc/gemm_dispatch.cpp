@@ -510,7 +510,12 @@ static size_t splitk_bytes(const Problem& p, int kernel, int S) {
 // never freed (~32 KiB each): split-K (2 per tile, kMaxSplitTiles tiles),
 // then the persistent kernels' work queues (kQueueWords). Returns nullptr if the
 // stream is being captured and has none yet (hipMalloc is not capturable):
-// the caller then runs unsplit.
+// the caller then runs unsplit. The "zero again after every launch" invariant
+// holds per stream: a graph captured on a stream bakes that stream's counters
+// into its split-K nodes, so graphs captured on one stream must not be
+// replayed concurrently with each other or with eager split-K launches on
+// that stream (bench_gemm captures one launch sequence and replays it
+// serially on the capture stream).
 static constexpr int kQueueWords = 16;  // 8 XCD ticket counters + exit counter (+ pad)
 
 static unsigned* stream_counters(hipStream_t s) {
