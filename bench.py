@@ -65,11 +65,12 @@ import torch.distributed as dist  # noqa: E402
 
 from pytorch_distributed_matmul_benchmark_amd.ops import gemm  # noqa: E402
 from pytorch_distributed_matmul_benchmark_amd.parallel.comm import CommStream  # noqa: E402
+from pytorch_distributed_matmul_benchmark_amd.parallel.ipc import ipc_empty  # noqa: E402
 from pytorch_distributed_matmul_benchmark_amd.parallel.dist import (  # noqa: E402
     DistContext, all_ok, barrier, cleanup_distributed, gather_scalars, reduce_scalar,
     setup_distributed, verify_collectives)
 from pytorch_distributed_matmul_benchmark_amd.parallel.overlap import (  # noqa: E402
-    BidirRing, OverlapPipeline, all_gather_now, all_reduce_now, compute_ctx, compute_stream, plan_for_units)
+    BidirRing, OverlapPipeline, all_gather_now, all_reduce_now, compute_ctx, gather_fn, make_gatherer, compute_stream, plan_for_units)
 from pytorch_distributed_matmul_benchmark_amd.parallel.partition import (  # noqa: E402
     column_shard, global_batch, local_batch)
 from pytorch_distributed_matmul_benchmark_amd.utils.telemetry import (  # noqa: E402
@@ -106,6 +107,7 @@ class Workload:
         self.plan = None
         self.pipe = None
         self.step = None                 # set below, or by _pipeline
+        self._closers = []               # collective teardown (IpcGather.close), run by close()
         comp = torch.cuda.current_stream(dev) if self.cuda else None
         self._mask = None
         if overlap and self.cuda and a.comm_cus > 0 and mode in ("batch_parallel", "matrix_parallel",
@@ -162,11 +164,18 @@ class Workload:
                   else torch.zeros(n, sh.padded, device=dev, dtype=dt))
             Bl[:, :sh.width].copy_(Bg[:, sh.start:sh.stop])
             del Bg
-            Cl = torch.empty(n, sh.padded, device=dev, dtype=odt)
+            # --allgather ipc: peers pull their blocks out of Cl over xGMI peer
+            # memory, so the outputs live in IPC-exportable allocations
+            alloc = ((lambda: ipc_empty((n, sh.padded), odt, dev)) if a.allgather == "ipc"
+                     else (lambda: torch.empty(n, sh.padded, device=dev, dtype=odt)))
+            Cl = alloc()
             self.kernel = self._label(A, Bl, Cl)
             if overlap:
-                units = [(A, Bl, Cl), (A, Bl, torch.empty_like(Cl))]
+                units = [(A, Bl, Cl), (A, Bl, alloc())]
                 cs = CommStream(dev)
+                gath = make_gatherer(a.allgather, dev, [u[2] for u in units], comm=cs)
+                self._closers.append(getattr(gath, "close", None))
+                g = gather_fn(a.allgather, gath)
                 self._gathered = {}
 
                 def coll(r, p, s, e, after, done):
@@ -174,13 +183,14 @@ class Workload:
                     if key not in self._gathered:
                         self._gathered[key] = torch.empty(ws * (e - s), sh.padded, device=dev,
                                                           dtype=odt)
-                    g = cs.all_gather_direct if a.allgather == "direct" else cs.all_gather_into
                     g(self._gathered[key], units[r][2][s:e], after=after, done=done)
                 self._pipeline(a, units, coll, 1, "all_gather", n * sh.padded * Cl.element_size(),
-                               cs)
+                               cs, gath)
             else:
                 gathered = torch.empty(ws * n, sh.padded, device=dev, dtype=odt)
-                cs = CommStream(dev) if a.allgather == "direct" else None
+                cs = (make_gatherer(a.allgather, dev, [Cl]) if a.allgather != "rccl" and ws > 1
+                      else None)
+                self._closers.append(getattr(cs, "close", None))
                 self._serial_split()
 
                 def step():
@@ -226,7 +236,7 @@ class Workload:
             self.step = step
 
     # -- overlap ---------------------------------------------------------------
-    def _pipeline(self, a, units, coll, per_step, kind, payload, cs):
+    def _pipeline(self, a, units, coll, per_step, kind, payload, cs, gath=None):
         """The overlapped step: plan (parallel/overlap.py plan_overlap), then an
         OverlapPipeline, or the serialized step when the plan says overlap loses."""
         A, B, C = units[0]
@@ -235,7 +245,8 @@ class Workload:
                                    steps=max(a.extra_steps, 1), owner=self._mask)
         if not self.plan.overlap:  # the planner refuses a losing overlap: serialize
             self.step = self._serial_fallback(units, per_step, kind,
-                                              a.allreduce if kind == "all_reduce" else a.allgather)
+                                              a.allreduce if kind == "all_reduce" else a.allgather,
+                                              gath)
             return
         self.pipe = OverlapPipeline(self._mm, units, coll, self.ctx.device, self.plan,
                                     per_step=per_step, compute=self.comp, owner=self._mask, comm=cs)
@@ -248,11 +259,11 @@ class Workload:
         self.step = self.pipe.step
         self.finish = finish
 
-    def _serial_fallback(self, units, per_step, kind, impl):
+    def _serial_fallback(self, units, per_step, kind, impl, gath=None):
         """The serialized step over the same units (collective on the current stream)."""
         ws, dev = self.ctx.world_size, self.ctx.device
         gathered = {}
-        cs = CommStream(dev) if impl == "direct" else None
+        cs = gath if gath is not None else (CommStream(dev) if impl != "rccl" else None)
 
         def step():
             for r in range(per_step):
@@ -399,6 +410,10 @@ class Workload:
     def close(self):
         if self.pipe is not None:
             self.pipe.close()
+        for fn in self._closers:  # IpcGather: unmap peers' buffers (collective barrier)
+            if fn is not None:
+                fn()
+        self._closers = []
 
 
 def _free(ctx) -> None:
@@ -566,7 +581,7 @@ def main() -> int:
     ap.add_argument("--allreduce", default="rccl", choices=["rccl", "direct"],
                     help="batch_parallel all-reduce: RCCL, or a two-shot exchange over P2P links "
                          "(reduce-scatter group, native fp32 sum, all-gather group)")
-    ap.add_argument("--allgather", default="rccl", choices=["rccl", "direct"],
+    ap.add_argument("--allgather", default="rccl", choices=["rccl", "direct", "ipc"],
                     help="matrix_parallel all-gather: RCCL, or direct P2P to every peer at once")
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],

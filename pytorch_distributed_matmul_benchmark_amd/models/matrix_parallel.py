@@ -16,6 +16,10 @@ Differences:
     ``[ws*N, shard]`` filled by ``all_gather_into_tensor`` (block r =
     C[:, r*shard:(r+1)*shard]); no per-iteration allocation and no list
     copy-out.
+  * ``--allgather``: RCCL's ``all_gather_into_tensor`` (default), the direct
+    P2P group (``direct``), or ``ipc``: every rank pulls the peers' blocks
+    out of their C_local over xGMI peer memory with DMA-engine copies
+    (parallel/ipc.py; C_local lives in IPC-exportable allocations).
   * ``overlap=True`` (parallel/overlap.py OverlapPipeline): C_local is ONE
     GEMM launch per iteration into a ring of two buffers (the reference's
     C1/C2, backup/matmul_overlap_benchmark.py:98-101); iteration i's
@@ -30,8 +34,9 @@ from __future__ import annotations
 import torch
 
 from ..parallel.comm import CommStream, current_stream
+from ..parallel.ipc import ipc_empty
 from ..parallel.overlap import (OverlapPipeline, all_gather_now, compute_ctx, compute_stream,
-                                plan_for_units)
+                                gather_fn, make_gatherer, plan_for_units)
 from ..parallel.dist import DistContext
 from ..parallel.partition import column_shard
 from ..utils.metrics import gemm_flops, tflops_from
@@ -74,13 +79,17 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         return r
     dev, n = ctx.device, w.n
     A, B_local, sh = make_operands(w, ctx)
-    C_local = torch.empty((n, sh.padded), device=dev, dtype=out_dtype(w))
+    # --allgather ipc: peers pull their blocks straight out of C_local, so the
+    # outputs live in IPC-exportable allocations (parallel/ipc.py)
+    alloc = ((lambda: ipc_empty((n, sh.padded), out_dtype(w), dev)) if w.allgather == "ipc"
+             else (lambda: torch.empty((n, sh.padded), device=dev, dtype=out_dtype(w))))
+    C_local = alloc()
     mm = gemm_fn(w, dev)
     label = kernel_label(w, A, B_local, C_local)
     flops_local = gemm_flops(n, sh.padded, n)
     flops_total = gemm_flops(n, n, n)
     extra = {"shard_cols": sh.padded, "overlap": bool(w.overlap), "allgather": w.allgather}
-    units = [(A, B_local, C_local), (A, B_local, torch.empty_like(C_local))]
+    units = [(A, B_local, C_local), (A, B_local, alloc())]
     plan = None
     compute, owner = compute_stream(dev, w.comm_cus) if w.overlap else (current_stream(dev), None)
     if w.overlap:
@@ -94,7 +103,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         # block r = gathered.view(ws, N, shard)[r] = C[:, r*shard:(r+1)*shard].
         gathered = torch.empty((ws * n, sh.padded), device=dev, dtype=out_dtype(w))
 
-        cs = CommStream(dev) if w.allgather == "direct" else None
+        cs = make_gatherer(w.allgather, dev, [C_local]) if w.allgather != "rccl" else None
 
         def comm():
             all_gather_now(gathered, C_local, w.allgather, cs)
@@ -120,13 +129,14 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         full = (lambda: assemble(gathered, n, ws))
     else:
         cs = CommStream(dev)
+        gath = make_gatherer(w.allgather, dev, [u[2] for u in units], comm=cs)
+        g = gather_fn(w.allgather, gath)
         bufs = {}
 
         def coll(r, p, s, e, after, done):
             if (r, p) not in bufs:
                 bufs[(r, p)] = torch.empty((ws * (e - s), sh.padded), device=dev,
                                            dtype=out_dtype(w))
-            g = cs.all_gather_direct if w.allgather == "direct" else cs.all_gather_into
             g(bufs[(r, p)], units[r][2][s:e], after=after, done=done)
 
         pipe = OverlapPipeline(mm, units, coll, dev, plan, per_step=1, compute=compute,
@@ -176,4 +186,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         C = full()
         Bg = randn((n, n), w, dev, seed=10_001 + w.seed, operand="B")
         res.relerr = sampled_relerr(A, Bg, C)
+    gatherer = cs if (plan is None or not plan.overlap) else gath
+    if hasattr(gatherer, "close"):  # IpcGather: unmap the peers' buffers before anyone frees
+        gatherer.close()
     return res

@@ -5,6 +5,7 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
+#include <cstring>
 #include <string>
 #include <tuple>
 
@@ -329,6 +330,78 @@ void reduce_sum(const at::Tensor& out, const std::vector<at::Tensor>& srcs) {
   check_hip(pdmb::reduce_sum(out.data_ptr(), ptrs.data(), (int)ptrs.size(), out.numel(), dt, s), "reduce_sum");
 }
 
+// ---- xGMI peer memory (parallel/ipc.py IpcGather) --------------------------
+// A tensor in its own hipMalloc allocation (so its IPC handle maps exactly
+// it, offset 0), freed by hipFree when the last torch reference goes.
+at::Tensor ipc_empty(std::vector<int64_t> shape, at::ScalarType dtype, int64_t device) {
+  c10::hip::HIPGuard guard((c10::DeviceIndex)device);
+  int64_t n = 1;
+  for (int64_t d : shape) {
+    TORCH_CHECK(d >= 0, "pdmb: ipc_empty: negative dimension");
+    n *= d;
+  }
+  const size_t bytes = std::max<size_t>((size_t)n * c10::elementSize(dtype), 256);
+  void* p = nullptr;
+  check_hip(hipMalloc(&p, bytes), "hipMalloc (ipc_empty)");
+  const int dev = (int)device;
+  return at::from_blob(
+      p, shape,
+      [dev](void* q) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(dev);
+        (void)hipFree(q);
+        (void)hipSetDevice(cur);
+      },
+      at::TensorOptions().dtype(dtype).device(at::Device(at::kCUDA, (c10::DeviceIndex)device)));
+}
+
+// The IPC handle of an ipc_empty tensor (its data pointer must be the base
+// of its allocation).
+py::bytes ipc_handle(const at::Tensor& t) {
+  TORCH_CHECK(t.is_cuda(), "pdmb: ipc_handle needs a GPU tensor");
+  c10::hip::HIPGuard guard(t.device().index());
+  void* base = nullptr;
+  size_t size = 0;
+  check_hip(hipMemGetAddressRange(&base, &size, t.data_ptr()), "hipMemGetAddressRange");
+  TORCH_CHECK(base == t.data_ptr(), "pdmb: ipc_handle: the tensor must start its own allocation "
+              "(allocate it with ipc_empty)");
+  hipIpcMemHandle_t h;
+  check_hip(hipIpcGetMemHandle(&h, base), "hipIpcGetMemHandle");
+  return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+// Map a peer's allocation into this process (device `device`); returns the
+// local address. Close with ipc_close before the exporter frees it.
+int64_t ipc_open(py::bytes handle, int64_t device) {
+  const std::string s = handle;
+  TORCH_CHECK(s.size() == sizeof(hipIpcMemHandle_t), "pdmb: ipc_open: bad handle size");
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, s.data(), sizeof(h));
+  c10::hip::HIPGuard guard((c10::DeviceIndex)device);
+  void* p = nullptr;
+  check_hip(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+  return (int64_t)(uintptr_t)p;
+}
+
+void ipc_close(int64_t ptr, int64_t device) {
+  c10::hip::HIPGuard guard((c10::DeviceIndex)device);
+  check_hip(hipIpcCloseMemHandle((void*)(uintptr_t)ptr), "hipIpcCloseMemHandle");
+}
+
+// dst (contiguous, this device) <- `dst.nbytes()` bytes at a peer address
+// (an ipc_open mapping + offset), on the current stream: a DMA-engine copy
+// over the xGMI link to that peer, no CUs.
+void copy_from_peer(const at::Tensor& dst, int64_t src_addr) {
+  TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "pdmb: copy_from_peer: dst must be a contiguous GPU tensor");
+  TORCH_CHECK(src_addr != 0, "pdmb: copy_from_peer: null source");
+  c10::hip::HIPGuard guard(dst.device().index());
+  hipStream_t s = c10::hip::getCurrentHIPStream(dst.device().index()).stream();
+  check_hip(hipMemcpyAsync(dst.data_ptr(), (const void*)(uintptr_t)src_addr, dst.nbytes(),
+                           hipMemcpyDeviceToDevice, s),
+            "hipMemcpyAsync (copy_from_peer)");
+}
+
 // Diagnostic: set (or clear, with None) the device buffer the stamp kernel writes.
 void set_debug_buffer(c10::optional<at::Tensor> buf) {
   if (buf.has_value()) {
@@ -374,6 +447,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("comm_proxy", &comm_proxy, py::arg("dst"), py::arg("src"), py::arg("blocks"));
   m.def("reduce_sum", &reduce_sum, "out = sum(srcs) (fp32 accumulate, list order)", py::arg("out"),
         py::arg("srcs"));
+  m.def("ipc_empty", &ipc_empty, "tensor in its own hipMalloc allocation (IPC-exportable)",
+        py::arg("shape"), py::arg("dtype"), py::arg("device"));
+  m.def("ipc_handle", &ipc_handle, py::arg("t"));
+  m.def("ipc_open", &ipc_open, py::arg("handle"), py::arg("device"));
+  m.def("ipc_close", &ipc_close, py::arg("ptr"), py::arg("device"));
+  m.def("copy_from_peer", &copy_from_peer, py::arg("dst"), py::arg("src_addr"));
   m.def("set_debug_buffer", &set_debug_buffer, py::arg("buf") = py::none());
   m.def("create_cu_masked_stream", &create_cu_masked_stream, py::arg("device"),
         py::arg("excluded"));

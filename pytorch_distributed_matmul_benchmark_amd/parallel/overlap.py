@@ -415,11 +415,40 @@ class BidirRing:
                 top, bot = self.Rt[(s + 1) % 2], self.Rb[(s + 1) % 2]
 
 
-def all_gather_now(out: torch.Tensor, inp: torch.Tensor, impl: str = "rccl",
-                   comm: Optional[CommStream] = None) -> None:
+def gather_fn(impl: str, comm) -> Callable:
+    """The ``(out, inp, after, done)`` all-gather of ``--allgather impl`` on
+    ``comm``: RCCL's ``all_gather_into_tensor`` / the direct P2P group on a
+    CommStream, or the peer-memory pull of an IpcGather (parallel/ipc.py; a
+    CommStream there means CPU tensors: the direct group stands in)."""
+    from .ipc import IpcGather
+
+    if isinstance(comm, IpcGather):
+        return comm.all_gather
+    if impl in ("direct", "ipc"):
+        return comm.all_gather_direct
+    return comm.all_gather_into
+
+
+def make_gatherer(impl: str, device: torch.device, sources=(), comm: Optional[CommStream] = None):
+    """The comm object for ``--allgather impl``: an IpcGather over ``comm``
+    with ``sources`` (ipc_empty buffers the inputs live in) registered when
+    ``impl == "ipc"`` on a GPU, else the CommStream itself."""
+    from .ipc import IpcGather
+
+    cs = comm or CommStream(device)
+    if impl == "ipc" and device.type == "cuda":
+        ig = IpcGather(cs)
+        for src in sources:
+            ig.register(src)
+        return ig
+    return cs
+
+
+def all_gather_now(out: torch.Tensor, inp: torch.Tensor, impl: str = "rccl", comm=None) -> None:
     """Serialized all-gather on the current stream: RCCL's
-    ``all_gather_into_tensor``, or the direct P2P all-gather (every block over
-    its own link) on ``comm`` with the current stream joined behind it."""
+    ``all_gather_into_tensor``, or (``comm``: a CommStream / IpcGather from
+    ``make_gatherer``) the direct P2P group or the peer-memory pull, with the
+    current stream joined behind it."""
     import torch.distributed as dist
 
     if impl == "rccl":
@@ -429,7 +458,7 @@ def all_gather_now(out: torch.Tensor, inp: torch.Tensor, impl: str = "rccl",
     cur = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
     ready, done = new_event(dev), new_event(dev)
     ready.record(cur)
-    comm.all_gather_direct(out, inp, after=ready, done=done)
+    gather_fn(impl, comm)(out, inp, after=ready, done=done)
     if cur is not None:
         cur.wait_event(done)
 

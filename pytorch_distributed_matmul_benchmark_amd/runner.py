@@ -90,10 +90,12 @@ def build_parser(kind: str) -> argparse.ArgumentParser:
                    help="--overlap: collective pieces per GEMM, each started by the GEMM's own "
                         "tile-completion signals (0: the overlap planner's choice; 1: whole "
                         "collectives pipelined across GEMMs)")
-    g.add_argument("--allgather", default="rccl", choices=["rccl", "direct"],
-                   help="matrix_parallel all-gather: RCCL's all_gather_into_tensor, or direct: one "
+    g.add_argument("--allgather", default="rccl", choices=["rccl", "direct", "ipc"],
+                   help="matrix_parallel all-gather: RCCL's all_gather_into_tensor; direct: one "
                         "batched P2P group sending this rank's shard to every peer at once (each "
-                        "over its own xGMI link on a fully connected node)")
+                        "over its own xGMI link on a fully connected node); ipc: every rank pulls "
+                        "the peers' shards out of their memory (hipIpc mappings) with DMA-engine "
+                        "copies, one stream per peer, no CUs (CPU tensors: as direct)")
     g.add_argument("--allreduce", default="rccl", choices=["rccl", "direct"],
                    help="batch_parallel / data_parallel / overlap all-reduce: RCCL's all_reduce, or "
                         "direct: a two-shot exchange over point-to-point links (reduce-scatter as one "

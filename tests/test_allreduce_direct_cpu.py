@@ -31,7 +31,7 @@ def _inputs(rank, n, dtype):
     return torch.randn(n, generator=g).to(dtype)
 
 
-def _worker(rank, ws, port, dtype_name, q):
+def _worker(rank, ws, port, dtype_name, outdir):
     from pytorch_distributed_matmul_benchmark_amd.parallel.comm import CommStream
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -47,25 +47,25 @@ def _worker(rank, ws, port, dtype_name, q):
     big = torch.stack([_inputs(rank, 96, dtype) for _ in range(10)])
     cs.all_reduce_direct(big[3:7])
     out["rows"] = big.clone()
-    q.put((rank, out))
+    torch.save(out, os.path.join(outdir, f"r{rank}.pt"))  # files, not an mp.Queue (no socket)
     dist.barrier()
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("ws", [2, 3, 4])
 @pytest.mark.parametrize("dtype_name", ["float32", "bfloat16"])
-def test_all_reduce_direct_matches_rank_order_fp32_sum(ws, dtype_name):
+def test_all_reduce_direct_matches_rank_order_fp32_sum(ws, dtype_name, tmp_path):
     dtype = getattr(torch, dtype_name)
     ctx = mp.get_context("spawn")
-    q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, ws, port, dtype_name, q)) for r in range(ws)]
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, dtype_name, str(tmp_path)))
+             for r in range(ws)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in range(ws))
     for p in procs:
-        p.join(timeout=60)
+        p.join(timeout=180)
         assert p.exitcode == 0
+    res = {r: torch.load(tmp_path / f"r{r}.pt", weights_only=True) for r in range(ws)}
     for n in SIZES:
         acc = torch.zeros(n)
         for r in range(ws):
@@ -122,4 +122,26 @@ def test_bench_direct_allreduce_ws2():
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     for key in ("batch_parallel", "batch_parallel+overlap"):
+        assert d["modes"][key] and d["modes"][key]["value"] > 0, key
+
+
+@pytest.mark.parametrize("extra", [[], ["--overlap", "--chunks", "2"]])
+def test_matrix_parallel_ipc_allgather_cpu_falls_back_to_direct(extra):
+    """--allgather ipc on CPU tensors (no peer memory) runs the direct P2P group."""
+    out = _torchrun(2, "matmul_scaling_benchmark.py", "--device", "cpu", "--sizes", "300",
+                    "--iterations", "2", "--warmup", "1", "--dtype", "float32", "--mode",
+                    "matrix_parallel", "--allgather", "ipc", "--check", *extra)
+    assert "PASS" in out and "FAIL" not in out and "ERROR" not in out
+
+
+def test_bench_ipc_allgather_ws2_cpu():
+    import json
+
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--gpus", "2",
+                        "--size", "128", "--steps", "2", "--warmup", "1", "--extra-steps", "2",
+                        "--extra-warmup", "1", "--allgather", "ipc"],
+                       capture_output=True, text=True, timeout=300, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    for key in ("matrix_parallel", "matrix_parallel+overlap"):
         assert d["modes"][key] and d["modes"][key]["value"] > 0, key

@@ -74,6 +74,9 @@ def test_two_ranks_share_gpu_bench_ring():
     ("batch_parallel", ["--overlap", "--chunks", "4", "--batch", "2"]),
     ("matrix_parallel", ["--allgather", "direct"]),
     ("matrix_parallel", ["--allgather", "direct", "--overlap", "--chunks", "2"]),
+    ("matrix_parallel", ["--allgather", "ipc"]),
+    ("matrix_parallel", ["--allgather", "ipc", "--overlap", "--chunks", "1"]),
+    ("matrix_parallel", ["--allgather", "ipc", "--overlap", "--chunks", "2"]),
     ("batch_parallel", ["--allreduce", "direct"]),
     ("batch_parallel", ["--allreduce", "direct", "--overlap", "--chunks", "2"])])
 def test_two_ranks_cu_masked_overlap_checked(mode, extra):
@@ -100,3 +103,14 @@ def test_two_ranks_self_launch_through_bench():
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["single_gpu_tflops"] > 0
     assert d["scaling_efficiency"] is not None
     assert d["modes"]["matrix_parallel+overlap"]["value"] > 0
+
+
+def test_two_ranks_share_gpu_bench_ipc_allgather():
+    """bench.py with --allgather ipc at ws = 2 (both ranks on one GPU, gloo): the
+    peer-memory pull runs in matrix_parallel serialized and overlapped and the
+    IpcGather teardown (unmap + barrier) leaves the job exiting cleanly."""
+    out = _run(2, "bench.py", "--gpus", "2", "--size", "2048", "--steps", "3", "--warmup", "1",
+               "--extra-steps", "2", "--extra-warmup", "1", "--allgather", "ipc")
+    d = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    for key in ("matrix_parallel", "matrix_parallel+overlap"):
+        assert d["modes"][key] and d["modes"][key]["value"] > 0, key
