@@ -66,6 +66,7 @@ struct Opts {
   int batch = 4, chunks = 1, kernel = 0;  // chunks: collective pieces per GEMM (signalled)
   bool overlap = false, check = false;
   bool direct = false;     // --allgather direct: P2P to every peer in one group (own link each)
+  bool peer = false;       // --allgather ipc: pull every peer's block from its memory (DMA copies)
   bool direct_ar = false;  // --allreduce direct: two-shot P2P exchange + native reduce_sum
   std::string json;
 };
@@ -422,7 +423,16 @@ struct Pipeline {
 };
 
 // ---- one rank ---------------------------------------------------------------
-void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Result& res) {
+// Buffers a rank publishes to its peers (--allgather ipc): every rank thread of
+// this process maps every GPU's memory directly (peer access), the
+// single-process form of parallel/ipc.py's hipIpc mappings.
+struct PeerTable {
+  explicit PeerTable(int ws) : src(ws) {}
+  std::vector<std::vector<char*>> src;  // [rank] -> its gather sources (ring slots)
+};
+
+void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Result& res,
+              PeerTable& peers) {
   HIP_OK(hipSetDevice(rank));
   const int ws = o.gpus, dt = o.dtype;
   Scratch scr;  // this rank's launch scratch, freed with its streams
@@ -717,7 +727,67 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     // sent straight to every peer and every peer's block received straight
     // into its slot, all in one group (on a fully connected node each
     // transfer has its own xGMI link; no forwarding hops).
+    // overlap: a ring of two C_local / gather buffer pairs (gather per piece: [ws * rows, shard])
+    Buf Cl2(o.overlap ? Cl.bytes : 0), G2(o.overlap ? G.bytes : 0);
+    peers.src[rank] = {(char*)Cl.p, (char*)Cl2.p};
+    bar.wait();  // every rank's buffers published before anyone pulls
+    // --allgather ipc: pull each peer's block (same offset in ITS buffer) on a
+    // copy stream per peer (DMA engines, one xGMI link each, no CUs), then a
+    // one-element all-reduce as a stream-ordered barrier: once it completes
+    // every peer has finished reading this rank's block (parallel/ipc.py).
+    struct StreamSet {
+      std::vector<hipStream_t> v;
+      ~StreamSet() {
+        for (hipStream_t q : v) (void)hipStreamDestroy(q);
+      }
+    } cpset;
+    std::vector<hipStream_t>& cps = cpset.v;
+    std::vector<hipEvent_t> cpe;
+    Buf flag(o.peer ? 256 : 0);
+    hipEvent_t fork = nullptr;
+    if (o.peer && ws > 1) {
+      for (int d = 0; d < ws; ++d) {
+        if (d == rank) continue;
+        int can = 0;
+        HIP_OK(hipDeviceCanAccessPeer(&can, rank, d));
+        if (!can) throw std::runtime_error("--allgather ipc: no peer access between GPUs");
+        const hipError_t e = hipDeviceEnablePeerAccess(d, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_OK(e);
+        (void)hipGetLastError();
+      }
+      for (int d = 1; d < ws; ++d) {
+        hipStream_t q;
+        HIP_OK(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+        cps.push_back(q);
+        cpe.push_back(event());
+      }
+      fork = event();
+      HIP_OK(hipMemsetAsync(flag.p, 0, flag.bytes, st));
+    }
+    auto pull_gather = [&](const char* send, char* recv, size_t count, hipStream_t s) {
+      const size_t bytes = count * oes;
+      char* base = o.overlap ? (send >= (char*)Cl2.p && send < (char*)Cl2.p + Cl2.bytes ? (char*)Cl2.p
+                                                                                        : (char*)Cl.p)
+                             : (char*)Cl.p;
+      const int slot = base == (char*)Cl.p ? 0 : 1;
+      const size_t off = (size_t)(send - base);
+      HIP_OK(hipMemcpyAsync(recv + (size_t)rank * bytes, send, bytes, hipMemcpyDeviceToDevice, s));
+      HIP_OK(hipEventRecord(fork, s));
+      for (int d = 1; d < ws; ++d) {
+        const int from = (rank + d) % ws;
+        HIP_OK(hipStreamWaitEvent(cps[d - 1], fork, 0));
+        HIP_OK(hipMemcpyAsync(recv + (size_t)from * bytes, peers.src[from][slot] + off, bytes,
+                              hipMemcpyDeviceToDevice, cps[d - 1]));
+        HIP_OK(hipEventRecord(cpe[d - 1], cps[d - 1]));
+        HIP_OK(hipStreamWaitEvent(s, cpe[d - 1], 0));
+      }
+      NCCL_OK(ncclAllReduce(flag.p, flag.p, 1, ncclFloat, ncclSum, comm, s));
+    };
     auto allgather = [&](const void* send, char* recv, size_t count, hipStream_t s) {
+      if (o.peer && ws > 1) {
+        pull_gather((const char*)send, recv, count, s);
+        return;
+      }
       if (!o.direct) {
         NCCL_OK(ncclAllGather(send, recv, count, nccl_out_type(dt), comm, s));
         return;
@@ -732,8 +802,6 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
       }
       NCCL_OK(ncclGroupEnd());
     };
-    // overlap: a ring of two C_local / gather buffer pairs (gather per piece: [ws * rows, shard])
-    Buf Cl2(o.overlap ? Cl.bytes : 0), G2(o.overlap ? G.bytes : 0);
     Pipeline pipe;
     std::vector<std::vector<char*>> gbuf;  // [slot][piece]
     if (o.overlap) {
@@ -840,6 +908,8 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
         }
     }
   }
+  HIP_OK(hipDeviceSynchronize());
+  bar.wait();  // no rank frees a buffer a peer may still read (--allgather ipc)
   for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(st);
   (void)hipStreamDestroy(cs);
@@ -858,7 +928,7 @@ void usage() {
   std::printf(
       "pdmb_bench [--gpus N] [--sizes N ...] [--iterations I] [--warmup W]\n"
       "           [--dtype bfloat16|float16|float32|float8_e4m3fn] [--mode independent|batch_parallel|matrix_parallel|ring_parallel]\n"
-      "           [--batch B] [--overlap] [--chunks C] [--allgather rccl|direct] [--allreduce rccl|direct]\n"
+      "           [--batch B] [--overlap] [--chunks C] [--allgather rccl|direct|ipc] [--allreduce rccl|direct]\n"
       "           [--kernel ID]\n"
       "           [--check] [--json FILE]\n");
 }
@@ -878,7 +948,11 @@ Opts parse(int argc, char** argv) {
     else if (a == "--chunks") o.chunks = std::stoi(next());
     else if (a == "--kernel") o.kernel = std::stoi(next());
     else if (a == "--overlap") o.overlap = true;
-    else if (a == "--allgather") o.direct = next() == "direct";
+    else if (a == "--allgather") {
+      const std::string g = next();
+      o.direct = g == "direct";
+      o.peer = g == "ipc";
+    }
     else if (a == "--allreduce") o.direct_ar = next() == "direct";
     else if (a == "--check") o.check = true;
     else if (a == "--json") o.json = next();
@@ -946,11 +1020,12 @@ int main(int argc, char** argv) {
     std::printf("\nBenchmarking %dx%d matrix multiplication:\n", n, n);
     std::vector<Result> res(o.gpus);
     Barrier bar(o.gpus);
+    PeerTable peers(o.gpus);
     std::vector<std::thread> th;
     for (int r = 0; r < o.gpus; ++r)
       th.emplace_back([&, r] {
         try {
-          run_rank(r, o, n, comms[r], bar, res[r]);
+          run_rank(r, o, n, comms[r], bar, res[r], peers);
         } catch (const std::exception& e) {
           res[r].error = e.what();
           bar.abort();

@@ -25,6 +25,8 @@ def exe():
                                         ("matrix_parallel", ["--overlap"]),
                                         ("matrix_parallel", ["--allgather", "direct"]),
                                         ("matrix_parallel", ["--overlap", "--allgather", "direct"]),
+                                        ("matrix_parallel", ["--allgather", "ipc"]),
+                                        ("matrix_parallel", ["--overlap", "--allgather", "ipc"]),
                                         ("batch_parallel", ["--allreduce", "direct"]),
                                         ("batch_parallel", ["--overlap", "--allreduce", "direct"]),
                                         ("ring_parallel", [])])
