@@ -52,7 +52,7 @@ def _worker(rank, ws, port, dtype_name, outdir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws", [2, 3, 4])
+@pytest.mark.parametrize("ws", [2, 3, 4, 8])
 @pytest.mark.parametrize("dtype_name", ["float32", "bfloat16"])
 def test_all_reduce_direct_matches_rank_order_fp32_sum(ws, dtype_name, tmp_path):
     dtype = getattr(torch, dtype_name)
