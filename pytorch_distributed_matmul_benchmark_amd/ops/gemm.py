@@ -6,7 +6,9 @@ chosen per problem by the C++ planner (gemm_dispatch.cpp): bf16/fp16 on
 GEMM has to itself), the ``gemm_tile.hip`` family (T128 / T256x128 /
 T128x2, split-K) for grids that under-fill the 256 CUs, SCHED 3 of
 ``gemm_mfma256.hip`` for edge tiles the others do not take; exact fp32 on
-``gemm_f32_256.hip`` / ``gemm_f32_w4.hip``; fp8 e4m3 on ``gemm_fp8.hip`` and
+``gemm_f32_tile.hip`` (f32_t128x2 on grids of >= 2 tiles per CU, f32_t128
+split-K below that), ``gemm_f32_256.hip`` and ``gemm_f32_w4.hip`` (split-K)
+as the planner prices them; fp8 e4m3 on ``gemm_fp8.hip`` and
 the fp8 tile family; ``gemm_generic.hip`` for anything else. Large problems
 whose K / N / alignment miss the LDS-DMA granule are zero-padded onto the
 fast kernels. CPU tensors use ``torch.matmul`` — the reference's own
