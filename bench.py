@@ -70,7 +70,8 @@ from pytorch_distributed_matmul_benchmark_amd.parallel.dist import (  # noqa: E4
     DistContext, all_ok, barrier, cleanup_distributed, gather_scalars, reduce_scalar,
     setup_distributed, verify_collectives)
 from pytorch_distributed_matmul_benchmark_amd.parallel.overlap import (  # noqa: E402
-    BidirRing, OverlapPipeline, all_gather_now, all_reduce_now, compute_ctx, gather_fn, make_gatherer, compute_stream, plan_for_units)
+    BidirRing, OverlapPipeline, all_gather_now, all_reduce_now, compute_ctx, gather_fn, make_gatherer,
+    reduce_fn, compute_stream, plan_for_units)
 from pytorch_distributed_matmul_benchmark_amd.parallel.partition import (  # noqa: E402
     column_shard, global_batch, local_batch)
 from pytorch_distributed_matmul_benchmark_amd.utils.telemetry import (  # noqa: E402
@@ -131,21 +132,29 @@ class Workload:
             lb, gb = local_batch(ws), global_batch(ws)
             A = self._rnd(lb, n, n, seed=2 * ctx.rank)
             B = self._rnd(lb, n, n, seed=2 * ctx.rank + 1, b=True)
-            C = torch.empty(lb, n, n, device=dev, dtype=odt)
+            # --allreduce ipc: peers pull chunks straight out of C (IPC-exportable allocations)
+            alloc = ((lambda *shape: ipc_empty(shape, odt, dev)) if a.allreduce == "ipc"
+                     else (lambda *shape: torch.empty(*shape, device=dev, dtype=odt)))
+            C = alloc(lb, n, n)
             self.kernel = self._label(A, B, C)
             if overlap:
                 # ring over the batch's own outputs; one element: a second C (reference C1/C2)
                 units = ([(A[b], B[b], C[b]) for b in range(lb)] if lb >= 2 else
-                         [(A[0], B[0], C[0]), (A[0], B[0], torch.empty_like(C[0]))])
+                         [(A[0], B[0], C[0]), (A[0], B[0], alloc(n, n))])
                 cs = CommStream(dev)
-                ar = cs.all_reduce_direct if a.allreduce == "direct" else cs.all_reduce
+                srcs = [C] + ([units[1][2]] if lb == 1 else [])
+                peer = make_gatherer(a.allreduce, dev, srcs, comm=cs)
+                self._closers.append(getattr(peer, "close", None))
+                ar = reduce_fn(a.allreduce, peer)
 
                 def coll(r, p, s, e, after, done):
                     ar(units[r][2][s:e], after=after, done=done)
-                self._pipeline(a, units, coll, lb, "all_reduce", n * n * C.element_size(), cs)
+                self._pipeline(a, units, coll, lb, "all_reduce", n * n * C.element_size(), cs, peer)
             else:
                 self._serial_split()
-                cs = CommStream(dev) if a.allreduce == "direct" else None
+                cs = (make_gatherer(a.allreduce, dev, [C]) if a.allreduce != "rccl" and ws > 1
+                      else None)
+                self._closers.append(getattr(cs, "close", None))
 
                 def step():
                     self._seg(0)
@@ -578,7 +587,7 @@ def main() -> int:
     ap.add_argument("--comm-cus", type=int, default=0,
                     help="overlap: CUs kept free of GEMM workgroups for RCCL (CU-masked "
                          "compute stream; 0 = no mask)")
-    ap.add_argument("--allreduce", default="rccl", choices=["rccl", "direct"],
+    ap.add_argument("--allreduce", default="rccl", choices=["rccl", "direct", "ipc"],
                     help="batch_parallel all-reduce: RCCL, or a two-shot exchange over P2P links "
                          "(reduce-scatter group, native fp32 sum, all-gather group)")
     ap.add_argument("--allgather", default="rccl", choices=["rccl", "direct", "ipc"],

@@ -30,8 +30,9 @@ from __future__ import annotations
 
 import torch
 from ..parallel.comm import CommStream, current_stream
+from ..parallel.ipc import ipc_empty
 from ..parallel.overlap import (OverlapPipeline, all_reduce_now, compute_ctx, compute_stream,
-                                plan_for_units)
+                                make_gatherer, plan_for_units, reduce_fn)
 from ..parallel.dist import DistContext
 from ..parallel.partition import global_batch, local_batch
 from ..utils.metrics import gemm_flops, tflops_from
@@ -46,15 +47,16 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     lb = local_batch(ws, w.batch)
     A = randn((lb, n, n), w, dev, seed=2 * (w.seed + ctx.rank))
     B = randn((lb, n, n), w, dev, seed=2 * (w.seed + ctx.rank) + 1, operand="B")
-    C = torch.empty((lb, n, n), device=dev, dtype=out_dtype(w))
+    # --allreduce ipc: peers pull chunks straight out of C (IPC-exportable allocations)
+    alloc = ((lambda *shape: ipc_empty(shape, out_dtype(w), dev)) if w.allreduce == "ipc"
+             else (lambda *shape: torch.empty(shape, device=dev, dtype=out_dtype(w))))
+    C = alloc(lb, n, n)
     mm = gemm_fn(w, dev)
     label = kernel_label(w, A, B, C)
     distributed = ctx.is_distributed
     flops = gemm_flops(n, n, n, lb)
 
-    direct = CommStream(dev) if w.allreduce == "direct" else None
-
-    def reduce_all():
+    def reduce_all():  # `direct` (the collective's comm object) is bound below
         if distributed:
             all_reduce_now(C, w.allreduce, direct)
 
@@ -62,7 +64,12 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
              "allreduce": w.allreduce}
     plan = None
     units = ([(A[b], B[b], C[b]) for b in range(lb)] if lb >= 2 else
-             [(A[0], B[0], C[0]), (A[0], B[0], torch.empty_like(C[0]))])
+             [(A[0], B[0], C[0]), (A[0], B[0], alloc(n, n))])
+    cs = CommStream(dev)
+    # the collective's comm object: the CommStream, or (--allreduce ipc on GPUs)
+    # an IpcGather with every output buffer registered
+    direct = (make_gatherer(w.allreduce, dev, [C] + ([units[1][2]] if lb == 1 else []), comm=cs)
+              if w.allreduce != "rccl" and distributed else None)
     compute, owner = (compute_stream(dev, w.comm_cus) if (w.overlap and distributed)
                       else (current_stream(dev), None))
     if w.overlap and distributed:
@@ -97,8 +104,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
                          extra=extra)
         checked = [C[b] for b in range(lb)]
     else:
-        cs = direct or CommStream(dev)
-        ar = cs.all_reduce_direct if w.allreduce == "direct" else cs.all_reduce
+        ar = reduce_fn(w.allreduce, direct if direct is not None else cs)
 
         def coll(r, p, s, e, after, done):
             ar(units[r][2][s:e], after=after, done=done)
@@ -160,4 +166,6 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         synchronize(dev)
         res.relerr = max(allreduced_relerr(ctx, A[min(i, lb - 1)], B[min(i, lb - 1)], Cb)
                          for i, Cb in enumerate(checked))
+    if hasattr(direct, "close"):  # IpcGather: unmap the peers' buffers before anyone frees
+        direct.close()
     return res

@@ -1,4 +1,6 @@
-"""All-gather over xGMI peer memory (``--allgather ipc``): every rank PULLS each
+"""Collectives over xGMI peer memory (``--allgather ipc``, ``--allreduce ipc``).
+
+All-gather: every rank PULLS each
 peer's shard straight out of that peer's memory with DMA-engine copies, one
 copy stream per peer, so on a fully connected 8 x MI355X node the seven
 transfers run over seven xGMI links at once and use no CUs — the GEMM the
@@ -28,6 +30,11 @@ Mechanics (ops/csrc/bindings.cpp ``ipc_*`` / ``copy_from_peer``):
     record ``done``.
   * ``close()``: unmap the peers' buffers, then a barrier, so no rank frees
     an exported buffer another rank still maps.
+
+``all_reduce(t)`` is the direct two-shot all-reduce on the same mappings:
+pull this rank's chunk from every peer, ``reduce_sum`` in rank order, pull
+every peer's reduced chunk, with three stream-ordered barriers (method
+docstring).
 
 gloo rehearsals (ranks sharing one GPU) exchange handles the same way; the
 barrier becomes a host barrier after the comm stream drains. CPU tensors have
@@ -117,6 +124,89 @@ class IpcGather:
             for ev in joins:
                 cs.wait_event(ev)
             self._barrier()
+            if done is not None:
+                done.record(cs)
+
+    def all_reduce(self, t: torch.Tensor, after=None, done=None) -> None:
+        """SUM all-reduce of ``t`` (a contiguous view into a registered buffer,
+        the same offsets on every rank) over peer memory — the direct
+        two-shot exchange of ``CommStream.all_reduce_direct`` with pulls
+        instead of P2P sends, so DMA engines move the bytes and no CUs do:
+
+          B0 barrier (every rank's ``t`` final) -> pull chunk ``me`` of every
+          peer's ``t`` into scratch (one copy stream per peer) -> native
+          ``reduce_sum`` in rank order into this rank's chunk -> B1 barrier
+          (every chunk reduced) -> pull every peer's reduced chunk into place
+          -> B2 barrier (no peer still reads this rank's chunk when its next
+          producer overwrites ``t``).
+
+        Chunks are 64-element multiples (16-B aligned); every rank sums in the
+        same order, so all ranks hold identical bits."""
+        from .comm import reduce_sum_
+
+        assert t.is_contiguous()
+        if self.ws == 1 or t.numel() == 0:
+            with stream_ctx(self.cs.stream):
+                if after is not None:
+                    self.cs.stream.wait_event(after)
+                if done is not None:
+                    done.record(self.cs.stream)
+            return
+        mod = _mod()
+        cs = self.cs.stream
+        flat = t.view(-1)
+        n = flat.numel()
+        per = -(-n // self.ws)            # ceil(n / ws)
+        chunk = -(-per // 64) * 64         # 64-element multiple: 16-B aligned chunk starts
+        bounds = [(min(r * chunk, n), min((r + 1) * chunk, n)) for r in range(self.ws)]
+        part = [flat[s:e] for s, e in bounds]
+        mine = part[self.me]
+        m = mine.numel()
+        es = t.element_size()
+        scratch = self.cs._scratch(t, (self.ws - 1) * chunk)
+        slot = {}
+        with stream_ctx(cs):
+            if after is not None:
+                cs.wait_event(after)
+            self._barrier()  # B0
+            fork = torch.cuda.Event()
+            fork.record(cs)
+        joins = []
+        peers = [(self.me + d) % self.ws for d in range(1, self.ws)]
+        for i, p in enumerate(peers):
+            slot[p] = scratch[i * chunk:i * chunk + m]
+            if not m:
+                continue
+            st = self.copy_streams[i]
+            with torch.cuda.stream(st):
+                st.wait_event(fork)
+                mod.copy_from_peer(slot[p], self._peer_addr(t, p) + bounds[self.me][0] * es)
+                ev = torch.cuda.Event()
+                ev.record(st)
+                joins.append(ev)
+        with stream_ctx(cs):
+            for ev in joins:
+                cs.wait_event(ev)
+            if m:
+                reduce_sum_(mine, [mine if r == self.me else slot[r] for r in range(self.ws)])
+            self._barrier()  # B1
+            fork = torch.cuda.Event()
+            fork.record(cs)
+        joins = []
+        for i, p in enumerate(peers):
+            if not part[p].numel():
+                continue
+            st = self.copy_streams[i]
+            with torch.cuda.stream(st):
+                st.wait_event(fork)
+                mod.copy_from_peer(part[p], self._peer_addr(t, p) + bounds[p][0] * es)
+                ev = torch.cuda.Event()
+                ev.record(st)
+                joins.append(ev)
+        with stream_ctx(cs):
+            for ev in joins:
+                cs.wait_event(ev)
+            self._barrier()  # B2
             if done is not None:
                 done.record(cs)
 

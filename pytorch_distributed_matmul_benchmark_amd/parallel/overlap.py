@@ -430,9 +430,10 @@ def gather_fn(impl: str, comm) -> Callable:
 
 
 def make_gatherer(impl: str, device: torch.device, sources=(), comm: Optional[CommStream] = None):
-    """The comm object for ``--allgather impl``: an IpcGather over ``comm``
-    with ``sources`` (ipc_empty buffers the inputs live in) registered when
-    ``impl == "ipc"`` on a GPU, else the CommStream itself."""
+    """The comm object for ``--allgather impl`` / ``--allreduce impl``: an
+    IpcGather over ``comm`` with ``sources`` (ipc_empty buffers the inputs
+    live in) registered when ``impl == "ipc"`` on a GPU, else the CommStream
+    itself."""
     from .ipc import IpcGather
 
     cs = comm or CommStream(device)
@@ -463,10 +464,24 @@ def all_gather_now(out: torch.Tensor, inp: torch.Tensor, impl: str = "rccl", com
         cur.wait_event(done)
 
 
-def all_reduce_now(t: torch.Tensor, impl: str = "rccl", comm: Optional[CommStream] = None) -> None:
+def reduce_fn(impl: str, comm) -> Callable:
+    """The ``(t, after, done)`` SUM all-reduce of ``--allreduce impl`` on
+    ``comm``: RCCL's on a CommStream, the direct P2P two-shot exchange, or the
+    peer-memory form of an IpcGather (a CommStream there — CPU tensors, or a
+    mode without registered outputs — runs the direct exchange)."""
+    from .ipc import IpcGather
+
+    if isinstance(comm, IpcGather):
+        return comm.all_reduce
+    if impl in ("direct", "ipc"):
+        return comm.all_reduce_direct
+    return comm.all_reduce
+
+
+def all_reduce_now(t: torch.Tensor, impl: str = "rccl", comm=None) -> None:
     """Serialized SUM all-reduce on the current stream: RCCL's ``all_reduce``,
-    or the direct two-shot exchange (``CommStream.all_reduce_direct``) on
-    ``comm`` with the current stream joined behind it."""
+    or (``comm``: a CommStream / IpcGather) the direct two-shot exchange or
+    its peer-memory form, with the current stream joined behind it."""
     import torch.distributed as dist
 
     if impl == "rccl":
@@ -476,6 +491,6 @@ def all_reduce_now(t: torch.Tensor, impl: str = "rccl", comm: Optional[CommStrea
     cur = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
     ready, done = new_event(dev), new_event(dev)
     ready.record(cur)
-    comm.all_reduce_direct(t, after=ready, done=done)
+    reduce_fn(impl, comm)(t, after=ready, done=done)
     if cur is not None:
         cur.wait_event(done)

@@ -96,10 +96,12 @@ def build_parser(kind: str) -> argparse.ArgumentParser:
                         "over its own xGMI link on a fully connected node); ipc: every rank pulls "
                         "the peers' shards out of their memory (hipIpc mappings) with DMA-engine "
                         "copies, one stream per peer, no CUs (CPU tensors: as direct)")
-    g.add_argument("--allreduce", default="rccl", choices=["rccl", "direct"],
-                   help="batch_parallel / data_parallel / overlap all-reduce: RCCL's all_reduce, or "
+    g.add_argument("--allreduce", default="rccl", choices=["rccl", "direct", "ipc"],
+                   help="batch_parallel / data_parallel / overlap all-reduce: RCCL's all_reduce; "
                         "direct: a two-shot exchange over point-to-point links (reduce-scatter as one "
-                        "batched P2P group, native fp32-accumulating sum, all-gather as another)")
+                        "batched P2P group, native fp32-accumulating sum, all-gather as another); "
+                        "ipc (batch_parallel on GPUs): the same two shots as pulls out of the peers' "
+                        "memory (hipIpc mappings, DMA-engine copies, no CUs); elsewhere as direct")
     g.add_argument("--comm-cus", type=int, default=0,
                    help="--overlap: CUs kept free of GEMM workgroups for RCCL (CU-masked "
                         "compute stream, spread over the 8 XCDs; 0 = no mask)")

@@ -139,9 +139,18 @@ def test_bench_ipc_allgather_ws2_cpu():
 
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--gpus", "2",
                         "--size", "128", "--steps", "2", "--warmup", "1", "--extra-steps", "2",
-                        "--extra-warmup", "1", "--allgather", "ipc"],
+                        "--extra-warmup", "1", "--allgather", "ipc", "--allreduce", "ipc"],
                        capture_output=True, text=True, timeout=300, cwd="/tmp")
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     for key in ("matrix_parallel", "matrix_parallel+overlap"):
         assert d["modes"][key] and d["modes"][key]["value"] > 0, key
+
+
+@pytest.mark.parametrize("extra", [[], ["--overlap", "--chunks", "2"]])
+def test_batch_parallel_ipc_allreduce_cpu_falls_back_to_direct(extra):
+    """--allreduce ipc on CPU tensors (no peer memory) runs the direct exchange."""
+    out = _torchrun(2, "matmul_scaling_benchmark.py", "--device", "cpu", "--sizes", "200",
+                    "--iterations", "2", "--warmup", "1", "--dtype", "float32", "--mode",
+                    "batch_parallel", "--allreduce", "ipc", "--check", *extra)
+    assert "PASS" in out and "FAIL" not in out and "ERROR" not in out

@@ -77,6 +77,9 @@ def test_two_ranks_share_gpu_bench_ring():
     ("matrix_parallel", ["--allgather", "ipc"]),
     ("matrix_parallel", ["--allgather", "ipc", "--overlap", "--chunks", "1"]),
     ("matrix_parallel", ["--allgather", "ipc", "--overlap", "--chunks", "2"]),
+    ("batch_parallel", ["--allreduce", "ipc"]),
+    ("batch_parallel", ["--allreduce", "ipc", "--overlap", "--chunks", "1"]),
+    ("batch_parallel", ["--allreduce", "ipc", "--overlap", "--chunks", "2", "--batch", "2"]),
     ("batch_parallel", ["--allreduce", "direct"]),
     ("batch_parallel", ["--allreduce", "direct", "--overlap", "--chunks", "2"])])
 def test_two_ranks_cu_masked_overlap_checked(mode, extra):
@@ -110,7 +113,7 @@ def test_two_ranks_share_gpu_bench_ipc_allgather():
     peer-memory pull runs in matrix_parallel serialized and overlapped and the
     IpcGather teardown (unmap + barrier) leaves the job exiting cleanly."""
     out = _run(2, "bench.py", "--gpus", "2", "--size", "2048", "--steps", "3", "--warmup", "1",
-               "--extra-steps", "2", "--extra-warmup", "1", "--allgather", "ipc")
+               "--extra-steps", "2", "--extra-warmup", "1", "--allgather", "ipc", "--allreduce", "ipc")
     d = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
-    for key in ("matrix_parallel", "matrix_parallel+overlap"):
+    for key in ("matrix_parallel", "matrix_parallel+overlap", "batch_parallel", "batch_parallel+overlap"):
         assert d["modes"][key] and d["modes"][key]["value"] > 0, key
