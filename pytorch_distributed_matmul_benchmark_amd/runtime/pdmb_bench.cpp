@@ -68,6 +68,7 @@ struct Opts {
   bool direct = false;     // --allgather direct: P2P to every peer in one group (own link each)
   bool peer = false;       // --allgather ipc: pull every peer's block from its memory (DMA copies)
   bool direct_ar = false;  // --allreduce direct: two-shot P2P exchange + native reduce_sum
+  bool peer_ar = false;    // --allreduce ipc: the two shots as pulls from the peers' memory
   std::string json;
 };
 
@@ -493,8 +494,83 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     // transfer of a group has its own xGMI link on a fully connected node.
     auto ar_chunk = [&](size_t count) { return ((count + ws - 1) / ws + 63) / 64 * 64; };  // 16-B aligned chunks
     const size_t ar_chunk_max = ar_chunk(lb * mat);
-    Buf ARs(o.direct_ar && ws > 1 ? (size_t)(ws - 1) * ar_chunk_max * oes : 0);
+    Buf ARs((o.direct_ar || o.peer_ar) && ws > 1 ? (size_t)(ws - 1) * ar_chunk_max * oes : 0);
+    // --allreduce ipc (parallel/ipc.py IpcGather.all_reduce): the same two shots
+    // as pulls out of the peers' C / C2 (direct peer access between this
+    // process's GPUs), one copy stream per peer, three one-element all-reduces
+    // as stream-ordered barriers (outputs final; chunks reduced; nobody still
+    // reading this rank's chunk).
+    struct StreamSet {
+      std::vector<hipStream_t> v;
+      ~StreamSet() {
+        for (hipStream_t q : v) (void)hipStreamDestroy(q);
+      }
+    } arset;
+    std::vector<hipEvent_t> are;
+    Buf arflag(o.peer_ar ? 256 : 0);
+    hipEvent_t arfork = nullptr;
+    peers.src[rank] = {(char*)C.p, (char*)C2.p};
+    if (o.peer_ar && ws > 1) {
+      for (int d = 0; d < ws; ++d) {
+        if (d == rank) continue;
+        int can = 0;
+        HIP_OK(hipDeviceCanAccessPeer(&can, rank, d));
+        if (!can) throw std::runtime_error("--allreduce ipc: no peer access between GPUs");
+        const hipError_t e = hipDeviceEnablePeerAccess(d, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_OK(e);
+        (void)hipGetLastError();
+      }
+      for (int d = 1; d < ws; ++d) {
+        hipStream_t q;
+        HIP_OK(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+        arset.v.push_back(q);
+        are.push_back(event());
+      }
+      arfork = event();
+      HIP_OK(hipMemsetAsync(arflag.p, 0, arflag.bytes, st));
+    }
+    bar.wait();  // every rank's buffers published before anyone pulls
+    auto peer_allreduce = [&](void* buf, size_t count, hipStream_t s) {
+      const size_t chunk = ar_chunk(count);
+      auto lo_of = [&](int r) { return std::min(count, (size_t)r * chunk); };
+      auto len_of = [&](int r) { return std::min(count, (size_t)(r + 1) * chunk) - lo_of(r); };
+      char* b = (char*)buf;
+      const int sid = (b >= (char*)C.p && b < (char*)C.p + C.bytes) ? 0 : 1;
+      const size_t off = (size_t)(b - (sid ? (char*)C2.p : (char*)C.p));
+      const size_t m = len_of(rank);
+      auto slot = [&](int d) { return (char*)ARs.p + (size_t)(d - 1) * chunk * oes; };  // from rank + d
+      auto barrier = [&]() { NCCL_OK(ncclAllReduce(arflag.p, arflag.p, 1, ncclFloat, ncclSum, comm, s)); };
+      auto pulls = [&](bool reduced) {
+        HIP_OK(hipEventRecord(arfork, s));
+        for (int d = 1; d < ws; ++d) {
+          const int from = (rank + d) % ws;
+          const size_t lo = reduced ? lo_of(from) : lo_of(rank), len = reduced ? len_of(from) : m;
+          if (!len) continue;
+          hipStream_t q = arset.v[d - 1];
+          HIP_OK(hipStreamWaitEvent(q, arfork, 0));
+          HIP_OK(hipMemcpyAsync(reduced ? b + lo * oes : slot(d), peers.src[from][sid] + off + lo * oes,
+                                len * oes, hipMemcpyDeviceToDevice, q));
+          HIP_OK(hipEventRecord(are[d - 1], q));
+          HIP_OK(hipStreamWaitEvent(s, are[d - 1], 0));
+        }
+      };
+      barrier();  // B0: every rank's output final
+      pulls(false);
+      if (m) {
+        std::vector<const void*> srcs(ws);
+        for (int r = 0; r < ws; ++r)
+          srcs[r] = r == rank ? (const void*)(b + lo_of(rank) * oes) : (const void*)slot((r - rank + ws) % ws);
+        HIP_OK(pdmb::reduce_sum(b + lo_of(rank) * oes, srcs.data(), ws, (int64_t)m, out_dtype(dt), s));
+      }
+      barrier();  // B1: every chunk reduced
+      pulls(true);
+      barrier();  // B2: no peer still reads this rank's chunk
+    };
     auto allreduce = [&](void* buf, size_t count, hipStream_t s) {
+      if (o.peer_ar) {
+        if (ws > 1 && count) peer_allreduce(buf, count, s);
+        return;
+      }
       if (!o.direct_ar) {
         NCCL_OK(ncclAllReduce(buf, buf, count, nccl_out_type(dt), ncclSum, comm, s));
         return;
@@ -928,7 +1004,7 @@ void usage() {
   std::printf(
       "pdmb_bench [--gpus N] [--sizes N ...] [--iterations I] [--warmup W]\n"
       "           [--dtype bfloat16|float16|float32|float8_e4m3fn] [--mode independent|batch_parallel|matrix_parallel|ring_parallel]\n"
-      "           [--batch B] [--overlap] [--chunks C] [--allgather rccl|direct|ipc] [--allreduce rccl|direct]\n"
+      "           [--batch B] [--overlap] [--chunks C] [--allgather rccl|direct|ipc] [--allreduce rccl|direct|ipc]\n"
       "           [--kernel ID]\n"
       "           [--check] [--json FILE]\n");
 }
@@ -953,7 +1029,11 @@ Opts parse(int argc, char** argv) {
       o.direct = g == "direct";
       o.peer = g == "ipc";
     }
-    else if (a == "--allreduce") o.direct_ar = next() == "direct";
+    else if (a == "--allreduce") {
+      const std::string r = next();
+      o.direct_ar = r == "direct";
+      o.peer_ar = r == "ipc";
+    }
     else if (a == "--check") o.check = true;
     else if (a == "--json") o.json = next();
     else if (a == "--dtype") {

@@ -27,6 +27,8 @@ def exe():
                                         ("matrix_parallel", ["--overlap", "--allgather", "direct"]),
                                         ("matrix_parallel", ["--allgather", "ipc"]),
                                         ("matrix_parallel", ["--overlap", "--allgather", "ipc"]),
+                                        ("batch_parallel", ["--allreduce", "ipc"]),
+                                        ("batch_parallel", ["--overlap", "--allreduce", "ipc"]),
                                         ("batch_parallel", ["--allreduce", "direct"]),
                                         ("batch_parallel", ["--overlap", "--allreduce", "direct"]),
                                         ("ring_parallel", [])])
