@@ -8,11 +8,11 @@
 #
 # Stages: validate (= tests smoke bench rocprof_bench selflaunch2 selflaunch4, the
 # closing pass), tests (whole GPU suite), tests_gemm / tests_fp8 / tests_signal /
-# tests_overlap (subsets), smoke, bench (driver form), bench_quick, bench_fp8,
+# tests_overlap / tests_comm (subsets), smoke, bench (driver form), bench_quick, bench_fp8,
 # native16k (pdmb_bench bf16 / fp8 at 16k), overlap_proxy, rocprof_bench, selflaunch2,
 # selflaunch4, gpus2_refused (bench.py --gpus 2 on a 1-GPU box must exit 2 at once),
 # ab_bf16 / ab_fp32 / ab_fp8 (auto vs hipBLASLt A/B tables), final_table (auto vs
-# hipBLASLt, every dtype at 4k / 8k / 16k), ldc_probe (output row pitch vs GEMM time,
+# hipBLASLt, every dtype at 4k / 8k / 16k), reduce_bench (reduce_sum bandwidth), ldc_probe (output row pitch vs GEMM time,
 # scripts/ldc_probe.py), pmc (PMC passes: scripts/gpu_pmc.sh with
 # N / KS / DT from the environment). After "--": one ad-hoc step NAME with a SECONDS limit.
 set -o pipefail
@@ -77,6 +77,10 @@ run_stage() {
               8192,2048,8192 10240,10240,10240 16384,16384,16384 &&
             grep '^{' "$OUT/ab_fp8.log" > "$OUT/ab_fp8.jsonl" ;;
     tests_fp8) step tests_fp8 600 $PYT tests/test_fp8_gpu.py -m gpu ;;
+    tests_comm) step tests_comm 1000 $PYT tests/test_ipc_gpu.py tests/test_reduce_gpu.py \
+                  tests/test_multirank_gpu.py tests/test_native_bench_gpu.py -m gpu ;;
+    reduce_bench) step reduce_bench 300 python scripts/reduce_bench.py &&
+                  grep '^{' "$OUT/reduce_bench.log" > "$OUT/reduce_bench.jsonl" ;;
     ldc_probe) step ldc_fp8 600 python scripts/ldc_probe.py --dtype float8_e4m3fn &&
                grep '^{' "$OUT/ldc_fp8.log" > "$OUT/ldc_fp8.jsonl" &&
                step ldc_bf16 600 python scripts/ldc_probe.py --dtype bfloat16 \
