@@ -311,6 +311,15 @@ def _completed(args, kind: str, mode: str, ctx: DistContext) -> set:
     return got
 
 
+def dist_backend_name() -> str:
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return "none"
+    be = dist.get_backend()
+    return "RCCL" if be == "nccl" else be
+
+
 def run_benchmarks(kind: str, ctx: DistContext, rep: Reporter, args) -> List[Dict]:
     k = KINDS[kind]
     mode = _mode_of(kind, args)
@@ -331,6 +340,12 @@ def run_benchmarks(kind: str, ctx: DistContext, rep: Reporter, args) -> List[Dic
         rep.line("  - GEMM: native gfx950 MFMA kernels")
     else:
         rep.line("  - GEMM: torch.matmul (hipBLASLt), A/B comparison")
+    if kind != "basic" and ctx.world_size > 1:
+        coll = {"batch_parallel": f"all-reduce: {args.allreduce}",
+                "matrix_parallel": f"all-gather: {args.allgather}",
+                "model_parallel": f"all-gather: {args.allgather}",
+                "ring_parallel": "ring P2P"}.get(mode, f"all-reduce: {args.allreduce}")
+        rep.line(f"  - Collective: {coll} (backend {dist_backend_name()})")
     rep.line(f"  - Iterations per test: {args.iterations}")
     rep.line(f"  - Warmup iterations: {args.warmup}")
     rep.line(f"{'=' * k['width']}\n")
