@@ -697,6 +697,7 @@ def main() -> int:
                        "parallelism": head["parallelism"], "mode": a.mode,
                        "overlap": bool(a.overlap), "backend": a.backend, "kernel": head["kernel"]},
             "dist_backend": ctx.backend,
+            "collectives": {"all_reduce": a.allreduce, "all_gather": a.allgather},
             "world_size_seen": dist.get_world_size() if ctx.is_distributed else 1,
             "rccl_version": _rccl_version(ctx),
             "collectives_verified": verified,
