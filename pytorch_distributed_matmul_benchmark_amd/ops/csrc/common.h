@@ -98,6 +98,10 @@ struct GemmArgs {
   int splitk, kt_per;
   float* part;
   unsigned* flags;
+  // S == 2: the reducer loads the other slice's block rows one row ahead of
+  // their use (splitk.h splitk_load_other); 0 = the row-by-row splitk_row
+  // path (A/B switch: PDMB_SPLITK_PREFETCH=0).
+  int meet_prefetch;
   // Persistent kernels: per-XCD tile queues (8 tickets + 1 exit counter,
   // zero at launch) and the grid (one workgroup per usable CU).
   unsigned* queue;

@@ -12,6 +12,8 @@
 #include <mutex>
 #include <unordered_map>
 
+#include <cstdlib>
+
 #include "api.h"
 #include "common.h"
 
@@ -56,6 +58,10 @@ static GemmArgs to_args(const Problem& p) {
   a.kb = p.kb > 0 && p.kb < p.K ? p.kb : p.K;
   a.dbg = g_debug_buffer;
   a.alpha = p.alpha;
+  {  // read per launch, so an in-process A/B can flip it (scripts/ab_kernels.py)
+    const char* e = std::getenv("PDMB_SPLITK_PREFETCH");
+    a.meet_prefetch = (e && e[0] == '0') ? 0 : 1;
+  }
   if (p.sig) {
     a.sig = p.sig->dev;
     a.sig_host = p.sig->host_dev;

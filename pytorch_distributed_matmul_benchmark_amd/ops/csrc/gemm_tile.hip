@@ -473,12 +473,21 @@ __global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   char* Cb = (char*)a.C + (long long)bz * a.sC * 2;
   char* ebuf = smem + 1024 + wu * 2 * epi_buf<NB>();  // past splitk_meet's ticket word
+  // S == 2: the other slice's rows prefetched a row ahead (splitk.h splitk_load_other)
+  const bool pf2 = split && a.splitk == 2 && a.meet_prefetch;
+  f32x4 qa[NB], qb[NB];
+  if (pf2) splitk_load_other<MB, NB, NT>(sl, slice, 0, qa);
 #pragma unroll
   for (int i = 0; i < MB; ++i) {
     f32x4 v[NB];
     if (!split) {
 #pragma unroll
       for (int j = 0; j < NB; ++j) v[j] = acc[i][j];
+    } else if (pf2) {
+      if (i + 1 < MB) splitk_load_other<MB, NB, NT>(sl, slice, i + 1, (i & 1) ? qa : qb);
+      const f32x4(&q)[NB] = (i & 1) ? qb : qa;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) v[j] = acc[i][j] + q[j];
     } else {
       splitk_row<MB, NB, NT>(a, sl, slice, i, acc, v);
     }

@@ -115,4 +115,22 @@ __device__ __forceinline__ void splitk_row(const GemmArgs& a, const SplitSlots& 
   }
 }
 
+// S == 2 (GemmArgs::meet_prefetch): the reducer's loads of the other slice's
+// block row i, issued a row ahead of their use. The slot bytes sit behind an
+// L2 miss (written through by a workgroup on another XCD, ~1-2 us away), and
+// splitk_row's loads could not leave before the previous row's C stores
+// (the compiler cannot reorder buffer loads across global stores), so every
+// block row paid that latency in turn. Two slices: acc + other is the slice-
+// order sum (fp32 addition commutes), bitwise equal to splitk_row.
+template <int MB, int NB, int NT>
+__device__ __forceinline__ void splitk_load_other(const SplitSlots& sl, int slice, int i, f32x4 (&q)[NB]) {
+  constexpr int NBLK = MB * NB;
+  const int s = 1 - slice;
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+    q[j] = __builtin_bit_cast(
+        f32x4, __builtin_amdgcn_raw_buffer_load_b128(sl.rs, ((s * NBLK + i * NB + j) * NT + sl.t) * 16, 0,
+                                                     16 /* sc1 */));
+}
+
 }  // namespace pdmb
