@@ -184,7 +184,7 @@ def test_tile_family_pipelined(tmp_path, cfg, lds, waitn, mfma_per_kt, pieces):
         assert re.search(r"v_mfma_f32_16x16x32_\w+ a\[", b)
         head = b[:b.find("global_atomic")]
         assert 1 <= len(re.findall(r"s_waitcnt vmcnt\(0\)", head)) <= 2  # unfused / split-K (+ fused exit)
-        kloop = re.search(r"Inner Loop Header.*?s_cbranch_scc1", b, re.S).group(0)
+        kloop = re.search(r"Inner Loop Header.*?s_cbranch_(?:scc1|vccnz) \.LBB", b, re.S).group(0)
         assert "vmcnt(0)" not in kloop and "v_mfma" in kloop  # the K-loop never drains
         assert len(re.findall(r"s_waitcnt vmcnt\(0\)", b[b.rfind("v_mfma"):])) >= 1  # the fused exit's drain
         assert len(re.findall(rf"s_waitcnt vmcnt\({waitn}\) lgkmcnt\(0\)", b)) == 3
