@@ -29,9 +29,26 @@ def pytest_collection_modifyitems(config, items):
 
 
 def free_port() -> int:
-    """An unused TCP port on 127.0.0.1 for a torchrun rendezvous (tests may run under xdist)."""
+    """An unused TCP port on 127.0.0.1 for a torchrun rendezvous (tests may run under xdist).
+
+    Picked below the kernel's ephemeral range (32768+): gloo opens many outgoing
+    connections there, and one of them can take an ephemeral port between this
+    probe and torchrun's bind (EADDRINUSE). Each xdist worker draws from its own
+    slice of 20000-32000."""
+    import random
     import socket
 
+    wid = os.environ.get("PYTEST_XDIST_WORKER", "gw0")
+    slot = int(wid[2:]) if wid[2:].isdigit() else 0
+    lo = 20000 + (slot % 8) * 1500
+    for _ in range(200):
+        port = random.randrange(lo, lo + 1500)
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+            try:
+                s.bind(("127.0.0.1", port))
+            except OSError:
+                continue
+            return port
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
