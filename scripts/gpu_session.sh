@@ -69,6 +69,10 @@ run_stage() {
                --rounds 3 --shapes 4096,2048,4096 4096,1024,4096 4096,512,4096 2048,2048,2048 6144,6144,6144 \
                8192,8192,8192 16384,16384,16384 &&
              grep '^{' "$OUT/ab_fp32.log" > "$OUT/ab_fp32.jsonl" ;;
+    ab_fp32_shards) step ab_fp32_shards 900 python scripts/ab_kernels.py --dtype float32 --rounds 5 \
+                      --kernels auto,f32_t128:1,f32_t128:2,f32_t128:4,f32_t128x2:1,f32_t128x2:2,f32_t128x2:4,torch \
+                      --shapes 4096,512,4096 4096,1024,4096 2048,2048,2048 4096,2048,4096 8192,1024,8192 &&
+                    grep '^{' "$OUT/ab_fp32_shards.log" > "$OUT/ab_fp32_shards.jsonl" ;;
     tests_gemm) step tests_gemm 900 $PYT tests/test_gemm_gpu.py tests/test_modes_gpu.py -m gpu ;;
     tests_overlap) step tests_overlap 900 $PYT tests/test_signal_gpu.py tests/test_overlap_gpu.py \
                      tests/test_native_bench_gpu.py tests/test_multirank_gpu.py -m gpu ;;
