@@ -55,7 +55,9 @@ import gc
 import json
 import math
 import os
+import signal
 import sys
+import threading
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -472,6 +474,50 @@ def _fault(ctx, key: str, phase: str) -> None:
         raise RuntimeError(f"injected fault (rank {ctx.rank}, {key}, {phase})")
 
 
+class _Pending:
+    """Rank 0's JSON line from the moment the headline is measured. The
+    secondary modes run after it and fill ``modes`` in place; if one of them
+    takes the job down — a timed-region failure on rank 0 (``_die``) or
+    torchrun's SIGTERM after another rank died or the driver's time limit — the
+    line is still printed, with the modes that finished and ``modes_incomplete``
+    saying why the rest did not, so a node run never loses its headline value.
+    Printed at most once."""
+    line = None
+    lock = threading.Lock()
+
+    @classmethod
+    def emit(cls, why: str | None = None) -> bool:
+        with cls.lock:
+            out, cls.line = cls.line, None
+        if out is None:
+            return False
+        if why:
+            out["modes_incomplete"] = why
+        sys.stdout.write(json.dumps(out) + "\n")
+        sys.stdout.flush()
+        return True
+
+
+def _arm_pending_on_signals() -> None:
+    """SIGTERM / SIGINT print the pending line, then exit 128 + signo. The work
+    happens on a watcher thread woken through ``signal.set_wakeup_fd`` (written
+    by the C-level handler at once): the main thread may be blocked inside a
+    collective, where a Python-level handler would never get to run."""
+    r, w = os.pipe()
+    os.set_blocking(w, False)
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, lambda signo, frame: None)
+    signal.set_wakeup_fd(w)
+
+    def watch():
+        while True:
+            b = os.read(r, 1)
+            if b and b[0] in (signal.SIGTERM, signal.SIGINT):
+                _Pending.emit(f"terminated by signal {b[0]} during the secondary modes")
+                os._exit(128 + b[0])
+    threading.Thread(target=watch, daemon=True, name="pending-line").start()
+
+
 def _die(ctx, key: str, exc: BaseException) -> None:
     """A failure inside a timed region cannot be agreed on (the other ranks are
     already blocked in a collective this rank will never join): report it and
@@ -483,6 +529,8 @@ def _die(ctx, key: str, exc: BaseException) -> None:
           flush=True)
     traceback.print_exc(file=sys.stderr)
     sys.stderr.flush()
+    if ctx.is_main:
+        _Pending.emit(f"{key} failed in the timed region on rank 0: {exc!r}")
     sys.stdout.flush()
     os._exit(1)
 
@@ -651,34 +699,7 @@ def main() -> int:
     def eff(v, ref):
         return round(v / (ws * ref), 4) if ref and v is not None else None
 
-    # Secondary modes (BASELINE configs 4-5), each family after its own
-    # rank-0-alone reference of the same per-rank shape. At ws = 1 there is no
-    # collective to overlap: those entries are null.
     modes = {}
-    if a.extra_steps > 0:
-        wms = a.extra_warmup_ms
-        for family, ref_batch in (("batch_parallel", local_batch(ws)), ("matrix_parallel", 1)):
-            ref = None
-            if not a.no_scaling_ref or ws == 1:
-                ref = _rank0_alone(a, ctx, a.extra_warmup, a.extra_steps, wms, batch=ref_batch)
-            for ov in (False, True):
-                if family == a.mode and ov == a.overlap:
-                    continue
-                key = family + ("+overlap" if ov else "")
-                if ov and ws == 1:
-                    modes[key] = None
-                    continue
-                v, el, info = _measure(a, ctx, family, ov, a.extra_warmup, a.extra_steps, key,
-                                       warmup_ms=wms)
-                if v is None:
-                    modes[key] = {"error": info}
-                    continue
-                modes[key] = {"value": round(v, 4), "ms_per_step": round(el / a.extra_steps * 1e3, 4),
-                              "steps": a.extra_steps, "warmup": a.extra_warmup,
-                              "scaling": "strong" if family == "matrix_parallel" else "weak",
-                              "vs_baseline": vs_base(family, v), "scaling_efficiency": eff(v, ref),
-                              "ref_tflops_rank0_alone": round(ref, 4) if ref else None, **info}
-
     if ctx.is_main:
         out = {
             "metric": METRIC, "value": round(value, 4), "unit": "TFLOPS",
@@ -711,7 +732,37 @@ def main() -> int:
         }
         if "plan" in head:
             out["config"]["overlap_plan"] = head["plan"]
-        print(json.dumps(out), flush=True)
+        _Pending.line = out
+        _arm_pending_on_signals()
+
+    # Secondary modes (BASELINE configs 4-5), each family after its own
+    # rank-0-alone reference of the same per-rank shape. At ws = 1 there is no
+    # collective to overlap: those entries are null.
+    if a.extra_steps > 0:
+        wms = a.extra_warmup_ms
+        for family, ref_batch in (("batch_parallel", local_batch(ws)), ("matrix_parallel", 1)):
+            ref = None
+            if not a.no_scaling_ref or ws == 1:
+                ref = _rank0_alone(a, ctx, a.extra_warmup, a.extra_steps, wms, batch=ref_batch)
+            for ov in (False, True):
+                if family == a.mode and ov == a.overlap:
+                    continue
+                key = family + ("+overlap" if ov else "")
+                if ov and ws == 1:
+                    modes[key] = None
+                    continue
+                v, el, info = _measure(a, ctx, family, ov, a.extra_warmup, a.extra_steps, key,
+                                       warmup_ms=wms)
+                if v is None:
+                    modes[key] = {"error": info}
+                    continue
+                modes[key] = {"value": round(v, 4), "ms_per_step": round(el / a.extra_steps * 1e3, 4),
+                              "steps": a.extra_steps, "warmup": a.extra_warmup,
+                              "scaling": "strong" if family == "matrix_parallel" else "weak",
+                              "vs_baseline": vs_base(family, v), "scaling_efficiency": eff(v, ref),
+                              "ref_tflops_rank0_alone": round(ref, 4) if ref else None, **info}
+
+    _Pending.emit()
     cleanup_distributed()
     return 0
 

@@ -178,6 +178,30 @@ def test_bench_fault_exits_fast(spec):
     assert r.returncode != 0
     assert time.time() - t0 < 90
     assert "injected fault" in r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    if spec.endswith("setup"):  # the headline itself failed: no line
+        assert lines == []
+    else:  # a secondary mode died after the headline: rank 0 still prints it
+        assert len(lines) == 1, r.stdout
+        d = json.loads(lines[0])
+        assert d["value"] > 0 and "modes_incomplete" in d
+        assert "batch_parallel" not in d["modes"]
+
+
+@pytest.mark.parametrize("spec", ["0:matrix_parallel:timed", "1:matrix_parallel+overlap:timed"])
+def test_bench_headline_survives_a_secondary_mode_death(spec):
+    """A timed-region death in a secondary mode, on rank 0 itself (``_die``) or on
+    another rank (torchrun's SIGTERM reaches rank 0 while it is blocked in a
+    collective): rank 0's one line still carries the headline and the modes that
+    finished, plus ``modes_incomplete``; the job still exits non-zero."""
+    r = _plain("--gpus", "2", "--size", "128", "--steps", "2", "--warmup", "1",
+               "--extra-steps", "2", "--extra-warmup", "1",
+               env_extra={"PDMB_BENCH_FAULT": spec, "PDMB_PG_TIMEOUT": "600"}, timeout=240)
+    assert r.returncode != 0
+    d = _line(r)
+    assert d["value"] > 0 and d["n_gpus"] == 2
+    assert d["modes"]["batch_parallel"]["value"] > 0  # finished before the fault
+    assert "matrix_parallel" in d["modes_incomplete"] or "signal" in d["modes_incomplete"]
 
 
 _NO_HIP = """
