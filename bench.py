@@ -653,6 +653,9 @@ def main() -> int:
     ap.add_argument("--extra-warmup-ms", type=float, default=300.0,
                     help="secondary modes (and their rank-0 references) warm up for at least "
                          "this much wall time (GPU only)")
+    ap.add_argument("--extra-deadline-s", type=float, default=240.0,
+                    help="rank 0 prints its line (modes_incomplete) and ends the job if the "
+                         "secondary modes run longer than this (0: no limit)")
     ap.add_argument("--no-scaling-ref", action="store_true",
                     help="skip the in-job rank-0-alone references (scaling_efficiency = null at N > 1)")
     a = ap.parse_args()
@@ -738,6 +741,14 @@ def main() -> int:
     # Secondary modes (BASELINE configs 4-5), each family after its own
     # rank-0-alone reference of the same per-rank shape. At ws = 1 there is no
     # collective to overlap: those entries are null.
+    if a.extra_steps > 0 and ctx.is_main and a.extra_deadline_s > 0:
+        # a secondary mode stuck in a collective (a peer lost, a hang) must not
+        # outlive the process-group timeout with the headline unprinted
+        def deadline():
+            time.sleep(a.extra_deadline_s)
+            if _Pending.emit(f"secondary modes still running after {a.extra_deadline_s:g} s"):
+                os._exit(3)
+        threading.Thread(target=deadline, daemon=True, name="extra-deadline").start()
     if a.extra_steps > 0:
         wms = a.extra_warmup_ms
         for family, ref_batch in (("batch_parallel", local_batch(ws)), ("matrix_parallel", 1)):

@@ -262,3 +262,19 @@ def test_bench_json_verifiability_fields():
         assert m["compute_ms"] >= 0 and m["comm_ms"] >= 0 and "warmup_ms" in m
         assert m["ref_tflops_rank0_alone"] > 0 and m["scaling_efficiency"] is not None
     assert d2["modes"]["batch_parallel+overlap"]["plan"]["overlap"] is True  # --chunks 1: requested
+
+
+def test_bench_secondary_deadline_prints_the_headline():
+    """Secondary modes that outlive --extra-deadline-s (a stuck collective): rank 0
+    prints its line with modes_incomplete and the job ends, well before the
+    process-group timeout."""
+    import time
+
+    t0 = time.time()
+    r = _plain("--gpus", "2", "--size", "256", "--steps", "2", "--warmup", "1",
+               "--extra-steps", "20000", "--extra-warmup", "1", "--extra-deadline-s", "3",
+               env_extra={"PDMB_PG_TIMEOUT": "600"}, timeout=240)
+    assert time.time() - t0 < 120
+    d = _line(r)
+    assert d["value"] > 0 and "after 3 s" in d["modes_incomplete"]
+    assert r.returncode != 0
