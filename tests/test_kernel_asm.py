@@ -10,6 +10,7 @@ import shutil
 import subprocess
 
 import pytest
+from asm_cache import gfx950_asm
 
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                     "pytorch_distributed_matmul_benchmark_amd", "ops", "csrc")
@@ -17,13 +18,10 @@ HIPCC = "/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else shut
 pytestmark = pytest.mark.skipif(HIPCC is None, reason="hipcc not available")
 
 
-def _kernels(src, tmp_path, experiments=False):
-    """Compile ``src`` (default build, or with the A/B experiment kernels)."""
-    defs = ["-DPDMB_EXPERIMENTS=1"] if experiments else []
-    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{CSRC}", *defs, "-c",
-                    os.path.join(CSRC, src), "-o", str(tmp_path / "k.o"), "-save-temps"],
-                   cwd=tmp_path, check=True, capture_output=True, timeout=600)
-    s = next(tmp_path.glob("*gfx950*.s")).read_text()
+def _kernels(src, tmp_path=None, experiments=False):
+    """Kernels of ``src`` (default build, or with the A/B experiment kernels);
+    one compile per source and flavour per test process (asm_cache.py)."""
+    s = gfx950_asm(src, experiments)
     out = {}
     for m in re.finditer(r"^([A-Za-z_][\w.$]*):\s*;\s*@", s, re.M):
         name = m.group(1)

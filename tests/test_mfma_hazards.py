@@ -19,14 +19,12 @@ linear instruction stream, across block boundaries. One pattern is exempt: a
 writing either in between (the compiler parking an accumulator in a VGPR and
 putting it back): the MFMA reads the same value either way.
 """
-import functools
 import os
 import re
 import shutil
-import subprocess
-import tempfile
 
 import pytest
+from asm_cache import gfx950_asm
 
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                     "pytorch_distributed_matmul_benchmark_amd", "ops", "csrc")
@@ -103,18 +101,6 @@ def hazards(body):
     return bad
 
 
-@functools.lru_cache(maxsize=None)
-def _asm(src):
-    d = tempfile.mkdtemp(prefix="pdmb_hz_")
-    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{CSRC}", "-c",
-                    os.path.join(CSRC, src), "-o", os.path.join(d, "k.o"), "-save-temps"],
-                   cwd=d, check=True, capture_output=True, timeout=900)
-    s = next(f for f in os.listdir(d) if "gfx950" in f and f.endswith(".s"))
-    text = open(os.path.join(d, s)).read()
-    shutil.rmtree(d, ignore_errors=True)
-    return text
-
-
 def _kernels(text):
     for m in re.finditer(r"^([A-Za-z_][\w.$]*):\s*;\s*@", text, re.M):
         yield m.group(1), text[m.end():text.find(".Lfunc_end", m.end())]
@@ -140,5 +126,5 @@ def test_parked_accumulator_is_exempt():
 
 @pytest.mark.parametrize("src", SOURCES)
 def test_no_valu_write_right_before_an_mfma_read(src):
-    found = {name: h for name, body in _kernels(_asm(src)) if (h := hazards(body))}
+    found = {name: h for name, body in _kernels(gfx950_asm(src)) if (h := hazards(body))}
     assert not found, {k[:90]: v[:3] for k, v in found.items()}
