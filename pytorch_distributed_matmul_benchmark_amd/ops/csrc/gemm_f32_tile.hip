@@ -328,16 +328,25 @@ __global__ void __launch_bounds__(NT, NS == 2 ? 2 : 1) gemm_f32_t128(GemmArgs a)
   char* Cb = (char*)a.C + (long long)bz * a.sC * 4;
   char* ebuf = smem + 1024 + wu * epi_buf_f32<NB>();  // past splitk_meet's ticket word
   const bool interior = m0 + BM <= a.M && n0 + BN <= a.N;
-  // (No row-ahead slot prefetch here, unlike gemm_tile.hip: the extra live
-  // registers made hipcc place AGPR copies next to the asm MFMAs of the odd-
-  // count last K-tile of the two-stage variant — wrong results at K / 32 odd,
-  // scripts/race_screen.py — for +1.5 % on one split shape.)
+  // S == 2: the other slice's rows prefetched a row ahead (splitk.h
+  // splitk_load_other), in the 4-stage kernel only: in the two-stage one the
+  // extra live registers made hipcc place register copies right before the asm
+  // MFMAs of the odd-count last K-tile (wrong results at K / 32 odd, found by
+  // scripts/race_screen.py; tests/test_mfma_hazards.py now screens for it).
+  const bool pf2 = NS == 4 && split && a.splitk == 2 && a.meet_prefetch;
+  f32x4 qa[NB], qb[NB];
+  if (pf2) splitk_load_other<MB, NB, NT>(sl, slice, 0, qa);
 #pragma unroll
   for (int mi = 0; mi < MB; ++mi) {
     f32x4 v[NB];
     if (!split) {
 #pragma unroll
       for (int j = 0; j < NB; ++j) v[j] = acc[mi][j];
+    } else if (pf2) {
+      if (mi + 1 < MB) splitk_load_other<MB, NB, NT>(sl, slice, mi + 1, (mi & 1) ? qa : qb);
+      const f32x4(&q)[NB] = (mi & 1) ? qb : qa;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) v[j] = acc[mi][j] + q[j];
     } else {
       splitk_row<MB, NB, NT>(a, sl, slice, mi, acc, v);
     }

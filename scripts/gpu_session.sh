@@ -73,6 +73,8 @@ run_stage() {
                       --kernels auto,f32_t128:1,f32_t128:2,f32_t128:4,f32_t128x2:1,f32_t128x2:2,f32_t128x2:4,torch \
                       --shapes 4096,512,4096 4096,1024,4096 2048,2048,2048 4096,2048,4096 8192,1024,8192 &&
                     grep '^{' "$OUT/ab_fp32_shards.log" > "$OUT/ab_fp32_shards.jsonl" ;;
+    splitk_prefetch) step splitk_prefetch 600 python scripts/splitk_prefetch_ab.py &&
+                     grep '^{' "$OUT/splitk_prefetch.log" > "$OUT/splitk_prefetch.jsonl" ;;
     tests_gemm) step tests_gemm 900 $PYT tests/test_gemm_gpu.py tests/test_modes_gpu.py -m gpu ;;
     tests_overlap) step tests_overlap 900 $PYT tests/test_signal_gpu.py tests/test_overlap_gpu.py \
                      tests/test_native_bench_gpu.py tests/test_multirank_gpu.py -m gpu ;;

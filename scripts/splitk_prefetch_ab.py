@@ -27,6 +27,8 @@ CASES = [  # (dtype, M, N, K, kernel, S)
     ("bfloat16", 8192, 1024, 8192, "t256x128", 2),
     ("float8_e4m3fn", 4096, 512, 4096, "fp8_t128", 2),
     ("float8_e4m3fn", 8192, 1024, 8192, "fp8_t256x128", 2),
+    ("float32", 4096, 512, 4096, "f32_t128", 2),
+    ("float32", 4096, 1024, 4096, "f32_t128", 2),
 ]
 
 
