@@ -514,32 +514,74 @@ static size_t splitk_bytes(const Problem& p, int kernel, int S) {
 
 // Per-(device, stream) counters, zeroed once on the stream before first use,
 // never freed (~32 KiB each): split-K (2 per tile, kMaxSplitTiles tiles),
-// then the persistent kernels' work queues (kQueueWords). Returns nullptr if the
-// stream is being captured and has none yet (hipMalloc is not capturable):
-// the caller then runs unsplit. The "zero again after every launch" invariant
-// holds per stream: a graph captured on a stream bakes that stream's counters
-// into its split-K nodes, so graphs captured on one stream must not be
-// replayed concurrently with each other or with eager split-K launches on
-// that stream (bench_gemm captures one launch sequence and replays it
-// serially on the capture stream).
+// then the persistent kernels' work queues (kQueueWords). Every launch leaves
+// them zero again, so launches on one stream can share them.
+//
+// A stream being captured gets a counter set of its own per capture (taken
+// from a per-device pool of kCapturePool zeroed sets, allocated by the first
+// uncaptured call on that device — hipMalloc is not capturable): each graph
+// bakes its own counters into its split-K / queue nodes, so two graphs
+// captured on one stream may replay concurrently on different streams, and
+// beside eager launches on the capture stream. (One graph replayed on two
+// streams at once still shares its set; once the pool is used up, captures
+// fall back to the capture stream's own set, the serial-replay contract.)
+// Returns nullptr when no set is available (no pool and no stream set yet):
+// the caller then runs unsplit, or refuses an explicitly requested split.
 static constexpr int kQueueWords = 16;  // 8 XCD ticket counters + exit counter (+ pad)
+static constexpr int kCapturePool = 64;
+static constexpr size_t kCounterBytes = sizeof(unsigned) * (2 * kMaxSplitTiles + kQueueWords);
+
+struct CounterPool {
+  unsigned* base = nullptr;
+  int used = 0;
+};
 
 static unsigned* stream_counters(hipStream_t s) {
   static std::mutex mu;
   static std::unordered_map<unsigned long long, unsigned*>* map =
       new std::unordered_map<unsigned long long, unsigned*>();  // leaked on purpose
+  static std::unordered_map<unsigned long long, unsigned*>* captures =
+      new std::unordered_map<unsigned long long, unsigned*>();  // (device, capture id) -> set
+  static CounterPool pools[64];
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  const unsigned long long key = ((unsigned long long)(uintptr_t)s << 8) ^ (unsigned)dev;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  unsigned long long cid = 0;
+  if (hipStreamGetCaptureInfo(s, &st, &cid) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> lk(mu);
+  CounterPool& pool = pools[dev];
+  if (st != hipStreamCaptureStatusNone) {
+    if (st != hipStreamCaptureStatusActive) return nullptr;
+    const unsigned long long key = (cid << 8) ^ (unsigned)dev;
+    auto it = captures->find(key);
+    if (it != captures->end()) return it->second;
+    unsigned* c = nullptr;
+    if (pool.base && pool.used < kCapturePool) {
+      c = pool.base + (size_t)pool.used++ * (kCounterBytes / sizeof(unsigned));
+    } else {  // pool used up: the stream's own set (graphs on it then replay serially)
+      auto own = map->find(((unsigned long long)(uintptr_t)s << 8) ^ (unsigned)dev);
+      if (own == map->end()) return nullptr;
+      c = own->second;
+    }
+    (*captures)[key] = c;
+    return c;
+  }
+  if (!pool.base) {  // zeroed on this stream: ordered before any capture that could use it
+    unsigned* b = nullptr;
+    if (hipMalloc(&b, kCounterBytes * kCapturePool) == hipSuccess) {
+      if (hipMemsetAsync(b, 0, kCounterBytes * kCapturePool, s) == hipSuccess &&
+          hipStreamSynchronize(s) == hipSuccess)
+        pool.base = b;
+      else
+        (void)hipFree(b);
+    }
+  }
+  const unsigned long long key = ((unsigned long long)(uintptr_t)s << 8) ^ (unsigned)dev;
   auto it = map->find(key);
   if (it != map->end()) return it->second;
-  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
   unsigned* c = nullptr;
-  const size_t bytes = sizeof(unsigned) * (2 * kMaxSplitTiles + kQueueWords);
-  if (hipMalloc(&c, bytes) != hipSuccess) return nullptr;
-  if (hipMemsetAsync(c, 0, bytes, s) != hipSuccess) {
+  if (hipMalloc(&c, kCounterBytes) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(c, 0, kCounterBytes, s) != hipSuccess) {
     (void)hipFree(c);
     return nullptr;
   }

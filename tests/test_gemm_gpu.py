@@ -757,6 +757,42 @@ def test_splitk_concurrent_streams_and_graph():
             assert torch.equal(out, R)
 
 
+def test_splitk_graphs_from_one_stream_replay_concurrently():
+    """Each capture takes its own split-K counter set (gemm_dispatch.cpp
+    stream_counters): two graphs captured on ONE stream replay at the same time
+    on two other streams, beside eager split-K launches on the capture stream,
+    and every output stays exact."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    A = torch.randint(-3, 4, (2048, 4096), device="cuda", generator=g).to(torch.bfloat16)
+    B = torch.randint(-3, 4, (4096, 1024), device="cuda", generator=g).to(torch.bfloat16)
+    R = (A.double() @ B.double()).to(torch.bfloat16)
+    for kernel in ("w4", "t128"):
+        s = torch.cuda.Stream()
+        outs = [torch.empty_like(R) for _ in range(3)]
+        with torch.cuda.stream(s):
+            gemm.matmul(A, B, out=outs[2], kernel=kernel, splitk=4)
+        s.synchronize()
+        graphs = []
+        for o in outs[:2]:
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr, stream=s):
+                gemm.matmul(A, B, out=o, kernel=kernel, splitk=4)
+            graphs.append(gr)
+        r1, r2 = torch.cuda.Stream(), torch.cuda.Stream()
+        for _ in range(5):
+            for o in outs:
+                o.fill_(float("nan"))
+            torch.cuda.synchronize()
+            with torch.cuda.stream(r1):
+                graphs[0].replay()
+            with torch.cuda.stream(r2):
+                graphs[1].replay()
+            with torch.cuda.stream(s):
+                gemm.matmul(A, B, out=outs[2], kernel=kernel, splitk=4)
+            torch.cuda.synchronize()
+            assert all(torch.equal(o, R) for o in outs), kernel
+
+
 def test_splitk_native_bench_loop_graph():
     A = torch.randn(2048, 2048, device="cuda", dtype=torch.bfloat16)
     B = torch.randn(2048, 2048, device="cuda", dtype=torch.bfloat16)
