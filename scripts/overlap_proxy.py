@@ -40,7 +40,7 @@ import torch  # noqa: E402
 from pytorch_distributed_matmul_benchmark_amd.ops import gemm  # noqa: E402
 from pytorch_distributed_matmul_benchmark_amd.parallel.comm import new_stream  # noqa: E402
 from pytorch_distributed_matmul_benchmark_amd.parallel.overlap import (  # noqa: E402
-    OverlapPipeline, plan_overlap)
+    OverlapPipeline, compute_ctx, compute_stream, plan_overlap)
 
 
 def main():
@@ -52,6 +52,9 @@ def main():
     ap.add_argument("--pieces", type=int, nargs="+", default=[1, 2, 4])
     ap.add_argument("--units", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--comm-cus", type=int, nargs="+", default=[0],
+                    help="also run every pipe_P with the GEMMs on a stream whose CU mask leaves "
+                         "k CUs to the proxy (arms pipe_P_cuK, gemm_cuK; 0 = no mask)")
     ap.add_argument("--piece-us", type=float, default=10.0,
                     help="planner: cost of one more piece (host flag wait + proxy launch)")
     a = ap.parse_args()
@@ -130,16 +133,38 @@ def main():
                 pipes[P] = OverlapPipeline(lambda x, y, o: gemm.matmul(x, y, out=o), units, coll,
                                            dev, plan, per_step=1, compute=cur, comm=None)
 
-            def run_pipe(P):
+            def run_pipe(pipe, stream=None):
                 def f(k):
+                    if stream is not None:
+                        stream.wait_stream(cur)
                     for _ in range(k):
-                        pipes[P].step()
-                    pipes[P].finish()
+                        pipe.step()
+                    pipe.finish()
+                    if stream is not None:
+                        cur.wait_stream(stream)
                 return f
 
             arms = {"gemm": run_gemm, "proxy": run_proxy, "serial": run_serial}
             for P in pipes:
-                arms[f"pipe_{P}"] = run_pipe(P)
+                arms[f"pipe_{P}"] = run_pipe(pipes[P])
+            owners = []
+            for cus in (c for c in a.comm_cus if c > 0):
+                stream, owner = compute_stream(dev, cus)
+                owners.append(owner)
+
+                def run_gemm_masked(k, stream=stream, owner=owner):
+                    stream.wait_stream(cur)
+                    with compute_ctx(stream, owner):
+                        for i in range(k):
+                            gemm.matmul(A, B, out=Cs[i % 2])
+                    cur.wait_stream(stream)
+                arms[f"gemm_cu{cus}"] = run_gemm_masked
+                for P in [q for q in pipes if isinstance(q, int)]:
+                    pm = OverlapPipeline(lambda x, y, o: gemm.matmul(x, y, out=o), units, coll, dev,
+                                         pipes[P].plan, per_step=1, compute=stream, owner=owner,
+                                         comm=None)
+                    pipes[(P, cus)] = pm
+                    arms[f"pipe_{P}_cu{cus}"] = run_pipe(pm, stream)
             for f in arms.values():  # warm-up: clocks, allocator, counters, signals
                 f(2)
             best = {}
@@ -152,7 +177,8 @@ def main():
             plan = plan_overlap(n, ncols, n, torch.bfloat16, 8, "all_gather", 0.0, granule=granule,
                                 steps=a.units, gemm_time_us=G * 1e3, comm_time_us=Cp * 1e3,
                                 piece_us=a.piece_us)
-            arm_best = min((k for k in best if k.startswith("pipe_")), key=lambda k: best[k])
+            arm_best = min((k for k in best if k.startswith("pipe_") and "_cu" not in k),
+                           key=lambda k: best[k])
             chosen = f"pipe_{plan.pieces}" if plan.overlap else "serial"
             rec = {"shape": shape, "m": n, "n": ncols, "k": n, "proxy_mib": mib,
                    "proxy_blocks": a.proxy_blocks, "units": a.units, "granule": granule,
@@ -168,6 +194,8 @@ def main():
             print(json.dumps(rec), flush=True)
             for p in pipes.values():
                 p.close()
+            for o in owners:
+                o.close()
             del src, dst
         del A, B, Cs
         torch.cuda.empty_cache()
