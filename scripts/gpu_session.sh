@@ -75,6 +75,12 @@ run_stage() {
                     grep '^{' "$OUT/ab_fp32_shards.log" > "$OUT/ab_fp32_shards.jsonl" ;;
     splitk_prefetch) step splitk_prefetch 600 python scripts/splitk_prefetch_ab.py &&
                      grep '^{' "$OUT/splitk_prefetch.log" > "$OUT/splitk_prefetch.jsonl" ;;
+    cli) step cli_basic 400 ./run_benchmark.sh 1 bfloat16 --check &&
+         step cli_batch 400 ./run_scaling_benchmark.sh 1 batch_parallel bfloat16 --overlap --check &&
+         step cli_matrix 400 ./run_scaling_benchmark.sh 1 matrix_parallel bfloat16 --overlap --check &&
+         step cli_pipeline 400 backup/run_overlap_benchmark.sh 1 pipeline bfloat16 &&
+         step cli_dp 400 backup/run_distributed_benchmark.sh 1 data_parallel bfloat16 --check &&
+         step cli_fp8 400 ./run_benchmark.sh 1 float8_e4m3fn --check ;;
     tests_gemm) step tests_gemm 900 $PYT tests/test_gemm_gpu.py tests/test_modes_gpu.py -m gpu ;;
     tests_overlap) step tests_overlap 900 $PYT tests/test_signal_gpu.py tests/test_overlap_gpu.py \
                      tests/test_native_bench_gpu.py tests/test_multirank_gpu.py -m gpu ;;
