@@ -793,6 +793,32 @@ def test_splitk_graphs_from_one_stream_replay_concurrently():
             assert all(torch.equal(o, R) for o in outs), kernel
 
 
+def test_splitk_capture_pool_exhaustion_falls_back():
+    """More captures than the per-device pool holds (64 sets): the later ones
+    share the capture stream's own set and still replay exactly when run one
+    after another (the serial-replay contract)."""
+    g = torch.Generator(device="cuda").manual_seed(6)
+    A = torch.randint(-3, 4, (1024, 2048), device="cuda", generator=g).to(torch.bfloat16)
+    B = torch.randint(-3, 4, (2048, 512), device="cuda", generator=g).to(torch.bfloat16)
+    R = (A.double() @ B.double()).to(torch.bfloat16)
+    s = torch.cuda.Stream()
+    out = torch.empty_like(R)
+    with torch.cuda.stream(s):
+        gemm.matmul(A, B, out=out, kernel="t128", splitk=2)
+    s.synchronize()
+    graphs = []
+    for _ in range(72):
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=s):
+            gemm.matmul(A, B, out=out, kernel="t128", splitk=2)
+        graphs.append(gr)
+    for gr in graphs[::7] + graphs[-3:]:
+        out.fill_(float("nan"))
+        gr.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, R)
+
+
 def test_splitk_native_bench_loop_graph():
     A = torch.randn(2048, 2048, device="cuda", dtype=torch.bfloat16)
     B = torch.randn(2048, 2048, device="cuda", dtype=torch.bfloat16)
