@@ -151,6 +151,18 @@ def build_probe(verbose: bool = False, force: bool = False) -> Path:
     return out
 
 
+MASK_PROBE_SRC = RUNTIME / "cu_mask_probe.hip"
+
+
+def build_mask_probe(verbose: bool = False, force: bool = False) -> Path:
+    """The stand-alone CU-mask placement probe (runtime/cu_mask_probe.hip): which
+    XCD / CU each workgroup of a CU-masked stream runs on."""
+    out = RUNTIME / "cu_mask_probe"
+    if force or _needs_build(out, [MASK_PROBE_SRC]):
+        _run([hipcc(), f"--offload-arch={ARCH}", "-O2", "-std=c++17", MASK_PROBE_SRC, "-o", out], verbose)
+    return out
+
+
 def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -> Path:
     """Compile every HIP/C++ source for gfx950 and link ``_C``. Returns the .so path."""
     headers = sorted(CSRC.glob("*.h"))
@@ -222,6 +234,7 @@ def main(argv=None):
     if not a.no_bench:
         print(build_bench(verbose=a.verbose))
         print(build_probe(verbose=a.verbose))
+        print(build_mask_probe(verbose=a.verbose))
 
 
 if __name__ == "__main__":

@@ -1,0 +1,88 @@
+// cu_mask_probe — where a CU-masked stream's workgroups actually run.
+//
+// parallel/overlap.py MaskedStream leaves k CUs out of the GEMM stream's mask
+// and assumes mask bit i lands on XCD i % 8 (so the first k bits spread the
+// free CUs evenly over the 8 XCDs). This probe checks that assumption on the
+// hardware: it creates a stream with the same mask (hipExtStreamCreateWithCUMask),
+// launches many one-wave workgroups that each record their XCC_ID and HW_ID
+// (CU / SH / SE) with vector stores, and prints, per XCD, how many distinct CUs
+// ran workgroups. Even spread: 32 - k/8 CUs on every XCD.
+//
+//   cu_mask_probe [--exclude k] [--mode first|block]
+//     first: mask bits 0 .. k-1 off (MaskedStream's choice)
+//     block: bits j*(n/k) off for j < k (one every n/k bits)
+#include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <set>
+#include <vector>
+
+#define HIP_OK(x)                                                                    \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) {                                                          \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(1);                                                                       \
+    }                                                                                \
+  } while (0)
+
+__global__ void __launch_bounds__(64) where(unsigned* out, int spin) {
+  unsigned hw, xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  // keep the CU busy a little so later workgroups spread over the free CUs
+  long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < spin) {
+  }
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = hw;
+    out[2 * blockIdx.x + 1] = xcc;
+  }
+}
+
+int main(int argc, char** argv) {
+  int k = 8;
+  const char* mode = "first";
+  for (int i = 1; i + 1 < argc; i += 2) {
+    if (!strcmp(argv[i], "--exclude")) k = atoi(argv[i + 1]);
+    if (!strcmp(argv[i], "--mode")) mode = argv[i + 1];
+  }
+  hipDeviceProp_t prop;
+  HIP_OK(hipGetDeviceProperties(&prop, 0));
+  const int n = prop.multiProcessorCount;
+  std::vector<unsigned> mask((n + 31) / 32, 0);
+  for (int i = 0; i < n; ++i) mask[i / 32] |= 1u << (i % 32);
+  for (int j = 0; j < k && k > 0; ++j) {
+    const int bit = !strcmp(mode, "block") ? j * (n / k) : j;
+    mask[bit / 32] &= ~(1u << (bit % 32));
+  }
+  hipStream_t s;
+  HIP_OK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+  const int blocks = n * 16;
+  unsigned* d = nullptr;
+  HIP_OK(hipMalloc(&d, sizeof(unsigned) * 2 * blocks));
+  HIP_OK(hipMemsetAsync(d, 0xff, sizeof(unsigned) * 2 * blocks, s));
+  hipLaunchKernelGGL(where, dim3(blocks), dim3(64), 0, s, d, 2000);
+  HIP_OK(hipStreamSynchronize(s));
+  std::vector<unsigned> h(2 * blocks);
+  HIP_OK(hipMemcpy(h.data(), d, sizeof(unsigned) * 2 * blocks, hipMemcpyDeviceToHost));
+  std::set<unsigned> cus[16];
+  int per_xcc[16] = {0};
+  for (int b = 0; b < blocks; ++b) {
+    const unsigned hw = h[2 * b], xcc = h[2 * b + 1] & 0xF;
+    // CU id within the XCC: CU_ID [11:8], SH_ID [12], SE_ID [15:13]
+    cus[xcc].insert(((hw >> 13) & 0x7) << 5 | ((hw >> 12) & 0x1) << 4 | ((hw >> 8) & 0xF));
+    ++per_xcc[xcc];
+  }
+  printf("{\"cus\": %d, \"excluded\": %d, \"mode\": \"%s\", \"per_xcd\": [", n, k, mode);
+  for (int x = 0; x < 8; ++x)
+    printf("%s{\"xcd\": %d, \"distinct_cus\": %zu, \"workgroups\": %d}", x ? ", " : "", x, cus[x].size(),
+           per_xcc[x]);
+  printf("]}\n");
+  HIP_OK(hipFree(d));
+  HIP_OK(hipStreamDestroy(s));
+  return 0;
+}

@@ -34,3 +34,25 @@ def test_compute_stream_without_mask_is_current():
     dev = torch.device("cuda", 0)
     s, owner = compute_stream(dev, 0)
     assert owner is None and s == torch.cuda.current_stream(dev)
+
+
+@pytest.mark.parametrize("k", [8, 32])
+@pytest.mark.parametrize("kernel", ["auto", "w4", "w4s"])
+def test_budgeted_gemm_on_masked_stream_is_exact(k, kernel):
+    """GEMMs planned for the CU budget of a masked stream (ops.gemm.cu_budget:
+    W4 with its budget-sized split / grid, W4S with G = 256 - k workgroups) on the
+    ws = 8 shard's tile grid (64 x 8 tiles of 256^2 on 248 / 224 CUs) are exact."""
+    dev = torch.device("cuda", 0)
+    ms = MaskedStream(dev, k)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(100 + k)
+        A = torch.randint(-3, 4, (16384, 1024), device="cuda", generator=g).to(torch.bfloat16)
+        B = torch.randint(-3, 4, (1024, 2048), device="cuda", generator=g).to(torch.bfloat16)
+        R = (A.double() @ B.double()).to(torch.bfloat16)
+        with torch.cuda.stream(ms.stream), ms.budget():
+            C = gemm.matmul(A, B, kernel=kernel)
+        torch.cuda.current_stream().wait_stream(ms.stream)
+        torch.cuda.synchronize()
+        assert torch.equal(C, R)
+    finally:
+        ms.close()
