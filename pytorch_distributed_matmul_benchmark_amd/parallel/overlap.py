@@ -208,7 +208,11 @@ def piece_rows(m: int, rows: int) -> List[Tuple[int, int]]:
 
 def _xcd_spread(ncu: int, k: int, nxcd: int = 8) -> List[int]:
     """k CU indices spread evenly over the XCDs (HIP CU-mask bit i lands on
-    XCD i % nxcd on multi-XCD parts): the first k indices do exactly that."""
+    XCD i % nxcd on multi-XCD parts): the first k indices do exactly that.
+    Checked on the hardware (runtime/cu_mask_probe.hip,
+    profiles/r3zo_cu_mask_placement_probe.jsonl): with bits 0..k-1 off every
+    XCD runs on 32 - k/8 CUs, and workgroups still go round-robin, 1/8 to each
+    XCD; clearing k bits of one residue class instead starves that one XCD."""
     return list(range(min(max(k, 0), ncu)))
 
 
