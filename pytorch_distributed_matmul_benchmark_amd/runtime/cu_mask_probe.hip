@@ -6,9 +6,11 @@
 // hardware: it creates a stream with the same mask (hipExtStreamCreateWithCUMask),
 // launches many one-wave workgroups that each record their XCC_ID and HW_ID
 // (CU / SH / SE) with vector stores, and prints, per XCD, how many distinct CUs
-// ran workgroups. Even spread: 32 - k/8 CUs on every XCD.
+// ran workgroups (even spread: 32 - k/8 CUs on every XCD), plus how many
+// workgroups did not run on XCD blockIdx % 8 (the kernels' XCD-aware tile maps
+// assume they all do).
 //
-//   cu_mask_probe [--exclude k] [--mode first|block]
+//   cu_mask_probe [--exclude k] [--mode first|block] [--blocks N (default 16 per CU)]
 //     first: mask bits 0 .. k-1 off (MaskedStream's choice)
 //     block: bits j*(n/k) off for j < k (one every n/k bits)
 #include <hip/hip_runtime.h>
@@ -44,11 +46,12 @@ __global__ void __launch_bounds__(64) where(unsigned* out, int spin) {
 }
 
 int main(int argc, char** argv) {
-  int k = 8;
+  int k = 8, nblocks = 0;
   const char* mode = "first";
   for (int i = 1; i + 1 < argc; i += 2) {
     if (!strcmp(argv[i], "--exclude")) k = atoi(argv[i + 1]);
     if (!strcmp(argv[i], "--mode")) mode = argv[i + 1];
+    if (!strcmp(argv[i], "--blocks")) nblocks = atoi(argv[i + 1]);
   }
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, 0));
@@ -61,7 +64,7 @@ int main(int argc, char** argv) {
   }
   hipStream_t s;
   HIP_OK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
-  const int blocks = n * 16;
+  const int blocks = nblocks > 0 ? nblocks : n * 16;  // n - k: one per free CU, like W4S
   unsigned* d = nullptr;
   HIP_OK(hipMalloc(&d, sizeof(unsigned) * 2 * blocks));
   HIP_OK(hipMemsetAsync(d, 0xff, sizeof(unsigned) * 2 * blocks, s));
@@ -71,8 +74,10 @@ int main(int argc, char** argv) {
   HIP_OK(hipMemcpy(h.data(), d, sizeof(unsigned) * 2 * blocks, hipMemcpyDeviceToHost));
   std::set<unsigned> cus[16];
   int per_xcc[16] = {0};
+  int off_residue = 0;  // workgroups NOT on XCD blockIdx % 8 (what map_tile's L2 grouping assumes)
   for (int b = 0; b < blocks; ++b) {
     const unsigned hw = h[2 * b], xcc = h[2 * b + 1] & 0xF;
+    off_residue += (int)(xcc != (unsigned)(b % 8));
     // CU id within the XCC: CU_ID [11:8], SH_ID [12], SE_ID [15:13]
     cus[xcc].insert(((hw >> 13) & 0x7) << 5 | ((hw >> 12) & 0x1) << 4 | ((hw >> 8) & 0xF));
     ++per_xcc[xcc];
@@ -81,7 +86,7 @@ int main(int argc, char** argv) {
   for (int x = 0; x < 8; ++x)
     printf("%s{\"xcd\": %d, \"distinct_cus\": %zu, \"workgroups\": %d}", x ? ", " : "", x, cus[x].size(),
            per_xcc[x]);
-  printf("]}\n");
+  printf("], \"blocks\": %d, \"not_on_xcd_blockidx_mod8\": %d}\n", blocks, off_residue);
   HIP_OK(hipFree(d));
   HIP_OK(hipStreamDestroy(s));
   return 0;
