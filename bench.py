@@ -31,7 +31,8 @@ with a same-shape reference run on rank 0 alone just before its family
 Verifiability: the line carries the process-group backend, the world size
 the group saw, the RCCL version, the collective self-test result (run
 before any timing), per-rank TFLOPS min / max, the serialized modes'
-compute / comm split, and per-mode mean GFX clock and power (amdsmi).
+compute / comm split, and per-mode median GFX clock and power (amdsmi, 5 ms
+poll, with the sample counts).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
@@ -73,7 +74,7 @@ from pytorch_distributed_matmul_benchmark_amd.parallel.dist import (  # noqa: E4
     setup_distributed, verify_collectives)
 from pytorch_distributed_matmul_benchmark_amd.parallel.overlap import (  # noqa: E402
     BidirRing, OverlapPipeline, all_gather_now, all_reduce_now, compute_ctx, gather_fn, make_gatherer,
-    reduce_fn, compute_stream, plan_for_units)
+    measured_plan, reduce_fn, compute_stream)
 from pytorch_distributed_matmul_benchmark_amd.parallel.partition import (  # noqa: E402
     column_shard, global_batch, local_batch)
 from pytorch_distributed_matmul_benchmark_amd.utils.telemetry import (  # noqa: E402
@@ -151,7 +152,8 @@ class Workload:
 
                 def coll(r, p, s, e, after, done):
                     ar(units[r][2][s:e], after=after, done=done)
-                self._pipeline(a, units, coll, lb, "all_reduce", n * n * C.element_size(), cs, peer)
+                self._pipeline(a, units, coll, lb, "all_reduce", n * n * C.element_size(), cs, peer,
+                               probe=lambda s, e: ar(units[0][2][s:e]))
             else:
                 self._serial_split()
                 cs = (make_gatherer(a.allreduce, dev, [C]) if a.allreduce != "rccl" and ws > 1
@@ -195,8 +197,15 @@ class Workload:
                         self._gathered[key] = torch.empty(ws * (e - s), sh.padded, device=dev,
                                                           dtype=odt)
                     g(self._gathered[key], units[r][2][s:e], after=after, done=done)
+                probe_out = {}
+
+                def probe(s, e):  # one piece's all-gather into a scratch gather buffer
+                    if e - s not in probe_out:
+                        probe_out[e - s] = torch.empty(ws * (e - s), sh.padded, device=dev, dtype=odt)
+                    g(probe_out[e - s], units[0][2][s:e])
                 self._pipeline(a, units, coll, 1, "all_gather", n * sh.padded * Cl.element_size(),
-                               cs, gath)
+                               cs, gath, probe=probe)
+                probe_out.clear()
             else:
                 gathered = torch.empty(ws * n, sh.padded, device=dev, dtype=odt)
                 cs = (make_gatherer(a.allgather, dev, [Cl]) if a.allgather != "rccl" and ws > 1
@@ -247,13 +256,16 @@ class Workload:
             self.step = step
 
     # -- overlap ---------------------------------------------------------------
-    def _pipeline(self, a, units, coll, per_step, kind, payload, cs, gath=None):
-        """The overlapped step: plan (parallel/overlap.py plan_overlap), then an
+    def _pipeline(self, a, units, coll, per_step, kind, payload, cs, gath=None, probe=None):
+        """The overlapped step: plan (parallel/overlap.py measured_plan: this
+        job's own GEMM and collective times, MAX over ranks; ``probe(s, e)``
+        issues one collective of rows [s, e) of ring slot 0), then an
         OverlapPipeline, or the serialized step when the plan says overlap loses."""
         A, B, C = units[0]
-        self.plan = plan_for_units(units, self.ctx.world_size, kind, payload,
-                                   native=self.backend == "native", requested=a.chunks,
-                                   steps=max(a.extra_steps, 1), owner=self._mask)
+        self.plan = measured_plan(units, self.ctx, kind, payload, self._mm, probe,
+                                  native=self.backend == "native", requested=a.chunks,
+                                  steps=max(a.extra_steps, 1), compute=self.comp,
+                                  owner=self._mask, comm=cs)
         if not self.plan.overlap:  # the planner refuses a losing overlap: serialize
             self.step = self._serial_fallback(units, per_step, kind,
                                               a.allreduce if kind == "all_reduce" else a.allgather,
@@ -568,6 +580,8 @@ def _measure(a, ctx, mode: str, overlap: bool, warmup: int, steps: int, key: str
                 warmup_ms=round(wms, 1),
                 per_rank_tflops={"min": round(min(rates), 4), "max": round(max(rates), 4)},
                 sclk_mhz=tel["sclk_mhz"], power_w=tel["power_w"],
+                sclk_samples=tel["sclk_samples"], power_samples=tel["power_samples"],
+                power_key=tel["power_key"],
                 sclk_mhz_min_over_ranks=(round(min(clocks), 1) if min(clocks) > 0 else None),
                 # host enqueue time per step (rank max) against ms_per_step: a host-bound
                 # schedule shows host_issue close to the step time with the GPU waiting
@@ -726,7 +740,10 @@ def main() -> int:
             "rccl_version": _rccl_version(ctx),
             "collectives_verified": verified,
             "per_rank_tflops": head["per_rank_tflops"],
+            # medians of a 5 ms amdsmi poll over the timed region, with the sample counts
             "sclk_mhz": head["sclk_mhz"], "power_w": head["power_w"],
+            "sclk_samples": head["sclk_samples"], "power_samples": head["power_samples"],
+            "power_key": head["power_key"],
             "sclk_mhz_min_over_ranks": head["sclk_mhz_min_over_ranks"],
             "per_gpu_tflops": (round(value / ws, 2)
                                if a.mode not in ("matrix_parallel", "ring_parallel") else None),

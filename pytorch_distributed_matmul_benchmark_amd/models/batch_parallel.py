@@ -32,7 +32,7 @@ import torch
 from ..parallel.comm import CommStream, current_stream
 from ..parallel.ipc import ipc_empty
 from ..parallel.overlap import (OverlapPipeline, all_reduce_now, compute_ctx, compute_stream,
-                                make_gatherer, plan_for_units, reduce_fn)
+                                make_gatherer, measured_plan, reduce_fn)
 from ..parallel.dist import DistContext
 from ..parallel.partition import global_batch, local_batch
 from ..utils.metrics import gemm_flops, tflops_from
@@ -72,10 +72,13 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
               if w.allreduce != "rccl" and distributed else None)
     compute, owner = (compute_stream(dev, w.comm_cus) if (w.overlap and distributed)
                       else (current_stream(dev), None))
+    ar = reduce_fn(w.allreduce, direct if direct is not None else cs)
     if w.overlap and distributed:
-        plan = plan_for_units(units, ws, "all_reduce", n * n * C.element_size(),
-                              native=w.backend == "native", requested=w.chunks,
-                              steps=max(w.iters, 1), owner=owner)
+        # priced from this job's own GEMM and all-reduce times (MAX over ranks)
+        plan = measured_plan(units, ctx, "all_reduce", n * n * C.element_size(), mm,
+                             lambda s, e: ar(units[0][2][s:e]), native=w.backend == "native",
+                             requested=w.chunks, steps=max(w.iters, 1), compute=compute,
+                             owner=owner, comm=cs)
         extra["plan"] = plan.as_dict()
     if plan is None or not plan.overlap:
         def serial_step():
@@ -102,10 +105,8 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
                          tflops=tflops_from(flops, avg / 1e3), compute_ms=comp, comm_ms=comm,
                          compute_only_tflops=tflops_from(flops, comp / 1e3), kernel=label,
                          extra=extra)
-        checked = [C[b] for b in range(lb)]
+        checked = [(b, C[b]) for b in range(lb)]
     else:
-        ar = reduce_fn(w.allreduce, direct if direct is not None else cs)
-
         def coll(r, p, s, e, after, done):
             ar(units[r][2][s:e], after=after, done=done)
 
@@ -158,14 +159,17 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
                          comm_ms=max(avg - comp, 0.0),
                          compute_only_tflops=tflops_from(flops, comp / 1e3), kernel=label,
                          extra=extra)
-        checked = [u[2] for u in units]
+        # only the ring slots the pipeline wrote (a slot never used holds no sum)
+        checked = [(i, u[2]) for i, (u, used) in enumerate(zip(units, pipe.used)) if used]
     if w.check:
         # Every timed iteration recomputes C and all-reduces it, so after the
         # loop C[b] must equal Σ_ranks A_r[b] @ B_r[b] (checks GEMM + RCCL +
         # the overlap event ordering end to end).
         synchronize(dev)
-        res.relerr = max(allreduced_relerr(ctx, A[min(i, lb - 1)], B[min(i, lb - 1)], Cb)
-                         for i, Cb in enumerate(checked))
+        res.relerr = max((allreduced_relerr(ctx, A[min(i, lb - 1)], B[min(i, lb - 1)], Cb)
+                          for i, Cb in checked), default=0.0)
+    if hasattr(direct, "npeers"):  # IpcGather: peers mapped for the pulls
+        res.extra["ipc_peers"] = direct.npeers
     if hasattr(direct, "close"):  # IpcGather: unmap the peers' buffers before anyone frees
         direct.close()
     return res

@@ -11,8 +11,9 @@ and efficiency is compute / total (100 % = comm free).
 from __future__ import annotations
 
 import torch
-from ..parallel.comm import CommStream, current_stream
-from ..parallel.overlap import all_reduce_now
+from ..parallel.comm import current_stream
+from ..parallel.ipc import ipc_empty
+from ..parallel.overlap import all_reduce_now, make_gatherer
 from ..parallel.dist import DistContext
 from ..utils.metrics import gemm_flops, tflops_from
 from ..utils.timing import SegmentTimer
@@ -24,11 +25,14 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     dev, n, ws = ctx.device, w.n, ctx.world_size
     A = randn((n, n), w, dev, seed=2 * (w.seed + ctx.rank))
     B = randn((n, n), w, dev, seed=2 * (w.seed + ctx.rank) + 1, operand="B")
-    C = torch.empty((n, n), device=dev, dtype=out_dtype(w))
+    # --allreduce ipc: peers pull chunks straight out of C (IPC-exportable allocation)
+    C = (ipc_empty((n, n), out_dtype(w), dev) if w.allreduce == "ipc"
+         else torch.empty((n, n), device=dev, dtype=out_dtype(w)))
     mm = gemm_fn(w, dev)
     label = kernel_label(w, A, B, C)
     distributed = ctx.is_distributed
-    direct = CommStream(dev) if w.allreduce == "direct" else None
+    # the collective's comm object: a CommStream (direct) or an IpcGather (ipc)
+    direct = make_gatherer(w.allreduce, dev, [C]) if w.allreduce != "rccl" and distributed else None
 
     def step():
         mm(A, B, C)
@@ -57,4 +61,6 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
                      extra={"allreduce": w.allreduce})
     if w.check:
         res.relerr = allreduced_relerr(ctx, A, B, C)
+    if hasattr(direct, "close"):  # IpcGather: unmap the peers' buffers before anyone frees
+        direct.close()
     return res

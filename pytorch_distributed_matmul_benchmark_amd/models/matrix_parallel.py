@@ -36,7 +36,7 @@ import torch
 from ..parallel.comm import CommStream, current_stream
 from ..parallel.ipc import ipc_empty
 from ..parallel.overlap import (OverlapPipeline, all_gather_now, compute_ctx, compute_stream,
-                                gather_fn, make_gatherer, plan_for_units)
+                                gather_fn, make_gatherer, measured_plan)
 from ..parallel.dist import DistContext
 from ..parallel.partition import column_shard
 from ..utils.metrics import gemm_flops, tflops_from
@@ -57,6 +57,14 @@ def make_operands(w: Workload, ctx: DistContext):
         B_local[:, :sh.width].copy_(Bg[:, sh.start:sh.stop])
     del Bg
     return A, B_local, sh
+
+
+def scaled_b(B: torch.Tensor, s: float) -> torch.Tensor:
+    """``B x s`` in B's own layout (fp8: column-major, scaled through fp32; a
+    power-of-two ``s`` is exact in every dtype, short of overflow)."""
+    if B.dtype == torch.float8_e4m3fn:
+        return (B.t().float() * s).to(B.dtype).t()
+    return B * s
 
 
 def assemble(gathered, n: int, ws: int) -> torch.Tensor:
@@ -93,9 +101,21 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     plan = None
     compute, owner = compute_stream(dev, w.comm_cus) if w.overlap else (current_stream(dev), None)
     if w.overlap:
-        plan = plan_for_units(units, ws, "all_gather", n * sh.padded * C_local.element_size(),
-                              native=w.backend == "native", requested=w.chunks,
-                              steps=max(w.iters, 1), owner=owner)
+        cs = CommStream(dev)
+        gath = make_gatherer(w.allgather, dev, [u[2] for u in units], comm=cs)
+        g = gather_fn(w.allgather, gath)
+        probe_out = {}
+
+        def probe(s, e):  # one piece's all-gather, into a scratch gather buffer
+            if e - s not in probe_out:
+                probe_out[e - s] = torch.empty((ws * (e - s), sh.padded), device=dev,
+                                               dtype=out_dtype(w))
+            g(probe_out[e - s], units[0][2][s:e])
+        # priced from this job's own GEMM and all-gather times (MAX over ranks)
+        plan = measured_plan(units, ctx, "all_gather", n * sh.padded * C_local.element_size(), mm,
+                             probe, native=w.backend == "native", requested=w.chunks,
+                             steps=max(w.iters, 1), compute=compute, owner=owner, comm=cs)
+        del probe_out
         extra["plan"] = plan.as_dict()
 
     if plan is None or not plan.overlap:
@@ -103,7 +123,10 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         # block r = gathered.view(ws, N, shard)[r] = C[:, r*shard:(r+1)*shard].
         gathered = torch.empty((ws * n, sh.padded), device=dev, dtype=out_dtype(w))
 
-        cs = make_gatherer(w.allgather, dev, [C_local]) if w.allgather != "rccl" else None
+        if w.overlap:  # the planner serialized: the gatherer built for it is the one
+            cs = gath
+        else:
+            cs = make_gatherer(w.allgather, dev, [C_local]) if w.allgather != "rccl" else None
 
         def comm():
             all_gather_now(gathered, C_local, w.allgather, cs)
@@ -128,9 +151,6 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         avg = comp + cm
         full = (lambda: assemble(gathered, n, ws))
     else:
-        cs = CommStream(dev)
-        gath = make_gatherer(w.allgather, dev, [u[2] for u in units], comm=cs)
-        g = gather_fn(w.allgather, gath)
         bufs = {}
 
         def coll(r, p, s, e, after, done):
@@ -139,8 +159,18 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
                                            dtype=out_dtype(w))
             g(bufs[(r, p)], units[r][2][s:e], after=after, done=done)
 
+        operands = None
+        if w.check:
+            # every unit its own product: B_local x 2^(k mod 3) — exact in every
+            # dtype (a power-of-two scale), and a unit's ring slot last held
+            # another scale's product, so a piece gathered before its GEMM
+            # rewrote the slot (or after the next one did) fails the check
+            scaled = [B_local, scaled_b(B_local, 2), scaled_b(B_local, 4)]
+
+            def operands(k):
+                return A, scaled[k % 3]
         pipe = OverlapPipeline(mm, units, coll, dev, plan, per_step=1, compute=compute,
-                               owner=owner, comm=cs)
+                               owner=owner, comm=cs, operands=operands)
         extra["pieces"] = len(pipe.pieces)
         extra["signalled"] = pipe.signalled
         extra["comm_cus"] = w.comm_cus
@@ -161,19 +191,22 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         finish()
         sw.stop(current_stream(dev))
         avg = sw.elapsed_ms() / max(w.iters, 1)
-        last = (pipe.k - 1) % len(units)  # the ring slot the last iteration gathered
         synchronize(dev)
+        # the gathered C of the last R units, each with its own scale (check)
+        gathered_units = [(pipe.slot_unit[r], [bufs[(r, p)] for p in range(len(pipe.pieces))])
+                          for r in range(len(units)) if pipe.used[r]]
         k = max(1, min(w.iters, 10))
+        spare = torch.empty_like(C_local)
 
-        def gemm_only():  # same context as the pipeline's GEMMs; into the other slot
+        def gemm_only():  # same context as the pipeline's GEMMs; the ring keeps its outputs
             with compute_ctx(compute, owner):
-                mm(*units[1 - last])
+                mm(A, B_local, spare)
             if compute is not None:
                 current_stream(dev).wait_stream(compute)
         comp = time_loop_ms(gemm_only, k, 1, dev) / k
         cm = max(avg - comp, 0.0)
         pipe.close()
-        full = (lambda: assemble([bufs[(last, p)] for p in range(len(pipe.pieces))], n, ws))
+        full = None
 
     res = ModeResult(mode="matrix_parallel", n=n, world_size=ws, avg_ms=avg,
                      flops_local=flops_local, flops_total=flops_total,
@@ -183,10 +216,20 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
                      kernel=label, extra=extra)
     if w.check:
         synchronize(dev)
-        C = full()
         Bg = randn((n, n), w, dev, seed=10_001 + w.seed, operand="B")
-        res.relerr = sampled_relerr(A, Bg, C)
+        if full is not None:
+            res.relerr = sampled_relerr(A, Bg, full())
+        else:
+            # every gathered piece of the last R units against ITS unit's product
+            # (256 sampled rows: a stale piece spans >= 256 rows of the 4096+)
+            Bd = Bg.double()
+            res.relerr = max((sampled_relerr(A, Bd * float(2 ** (k % 3)), assemble(pieces, n, ws),
+                                             rows=256)
+                              for k, pieces in gathered_units), default=float("inf"))
+            extra["checked_units"] = [k for k, _ in gathered_units]
     gatherer = cs if (plan is None or not plan.overlap) else gath
+    if hasattr(gatherer, "npeers"):  # IpcGather: peers mapped for the pulls
+        res.extra["ipc_peers"] = gatherer.npeers
     if hasattr(gatherer, "close"):  # IpcGather: unmap the peers' buffers before anyone frees
         gatherer.close()
     return res

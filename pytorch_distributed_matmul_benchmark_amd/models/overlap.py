@@ -33,7 +33,8 @@ import torch
 from ..ops import gemm
 from ..parallel.comm import CommStream, current_stream, new_event
 from ..parallel.dist import DistContext
-from ..parallel.overlap import all_reduce_now
+from ..parallel.ipc import ipc_empty
+from ..parallel.overlap import all_reduce_now, make_gatherer, reduce_fn
 from ..utils.metrics import gemm_flops, tflops_from
 from ..utils.timing import Stopwatch, synchronize, time_loop_ms
 from .common import (ModeResult, Workload, align_ranks, allreduced_relerr, gemm_fn, kernel_label,
@@ -51,25 +52,28 @@ def run(w: Workload, ctx: DistContext, mode: str = "overlap", depth: int = None)
     depth = DEPTH[mode] if depth is None else max(1, int(depth))
     As = [randn((n, n), w, dev, seed=100 * (w.seed + ctx.rank) + 2 * i) for i in range(depth)]
     Bs = [randn((n, n), w, dev, seed=100 * (w.seed + ctx.rank) + 2 * i + 1, operand="B") for i in range(depth)]
-    Cs = [torch.empty((n, n), device=dev, dtype=out_dtype(w)) for _ in range(depth)]
+    # --allreduce ipc: peers pull chunks straight out of the C ring (IPC-exportable)
+    Cs = [ipc_empty((n, n), out_dtype(w), dev) if w.allreduce == "ipc"
+          else torch.empty((n, n), device=dev, dtype=out_dtype(w)) for _ in range(depth)]
     mm = gemm_fn(w, dev)
     distributed = ctx.is_distributed
     label = kernel_label(w, As[0], Bs[0], Cs[0], shared=depth > 1 and distributed)
     compute = current_stream(dev)
+    # the collective's comm object: the CommStream, or (ipc on GPUs) an IpcGather
+    # with every ring buffer registered
+    cs = CommStream(dev)
+    comm = make_gatherer(w.allreduce, dev, Cs, comm=cs) if distributed and w.allreduce != "rccl" else cs
 
     used = [True] + [False] * (depth - 1)
     if depth == 1 or not distributed:
-        direct = CommStream(dev) if w.allreduce == "direct" else None
-
         def run_iters(k):
             for _ in range(k):
                 mm(As[0], Bs[0], Cs[0])
                 if distributed:
-                    all_reduce_now(Cs[0], w.allreduce, direct)
+                    all_reduce_now(Cs[0], w.allreduce, comm)
         finish = (lambda: None)
     else:
-        cs = CommStream(dev)
-        ar = cs.all_reduce_direct if w.allreduce == "direct" else cs.all_reduce
+        ar = reduce_fn(w.allreduce, comm)
         ready = [new_event(dev) for _ in range(depth)]
         done = [new_event(dev) for _ in range(depth)]
         used[0] = False
@@ -121,4 +125,6 @@ def run(w: Workload, ctx: DistContext, mode: str = "overlap", depth: int = None)
         synchronize(dev)
         res.relerr = max(allreduced_relerr(ctx, As[i], Bs[i], Cs[i])
                          for i in range(depth) if used[i] or i == 0)
+    if hasattr(comm, "close"):  # IpcGather: unmap the peers' buffers before anyone frees
+        comm.close()
     return res

@@ -127,6 +127,10 @@ void signal_destroy(Signal* s);
 // Host wait until flag[slot] reaches `epoch` (wrap-safe); false on timeout.
 bool signal_wait(const Signal* s, int slot, unsigned epoch, double timeout_s);
 unsigned signal_flag(const Signal* s, int slot);
+// Host store of flag[slot] (release); gate(): a one-wave kernel on `stream`
+// that waits until flag[slot] reaches `value` or `timeout_s` pass (reduce.hip).
+void signal_set(Signal* s, int slot, unsigned value);
+hipError_t gate(const Signal* s, int slot, unsigned value, double timeout_s, hipStream_t stream);
 // Tile rows of one completion unit for this problem on W4: the rows of one
 // 256-workgroup round of its XCD-aware order (map_tile), so pieces finish in
 // order and each piece is a whole number of rounds. 0: cannot be signalled.
@@ -199,9 +203,19 @@ hipError_t comm_proxy(void* dst, const void* src, size_t bytes, int blocks, hipS
 // dst[i] = sum over s < nsrc of srcs[s][i] (fp32 accumulate, sources in index
 // order, RNE to the element type; dtype 0 f32, 1 f16, 2 bf16). dst may alias a
 // source; 16-B vectors when every pointer is 16-B aligned. The local step of the direct two-shot
-// all-reduce (reduce.hip).
+// all-reduce (reduce.hip). Sources may be peer-mapped (IPC) addresses.
+// max_blocks > 0 caps the grid (a reduce running beside a GEMM).
 constexpr int kMaxReduceSrcs = 16;
-hipError_t reduce_sum(void* dst, const void* const* srcs, int nsrc, int64_t n, int dtype, hipStream_t stream);
+hipError_t reduce_sum(void* dst, const void* const* srcs, int nsrc, int64_t n, int dtype, hipStream_t stream,
+                      int max_blocks = 0);
+
+// n <= kMaxCopies copies dsts[i] <- srcs[i] (bytes[i] bytes each; zero-length
+// entries skipped) in ONE launch, `blocks_per` 256-thread workgroups per copy
+// (0: 32). The peer-memory all-gather's pull (parallel/ipc.py): every peer's
+// block is read over its own xGMI link at once, from one stream.
+constexpr int kMaxCopies = 16;
+hipError_t multi_copy(void* const* dsts, const void* const* srcs, const size_t* bytes, int n, int blocks_per,
+                      hipStream_t stream);
 
 // Diagnostic builds write per-wave stamps here (device memory; nullptr = off).
 void set_debug_buffer(void* p);

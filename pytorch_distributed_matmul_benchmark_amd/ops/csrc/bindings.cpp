@@ -181,6 +181,21 @@ int64_t signal_flag(int64_t h, int64_t slot) {
   return (int64_t)pdmb::signal_flag(as_signal(h), (int)slot);
 }
 
+void signal_set(int64_t h, int64_t slot, int64_t value) {
+  TORCH_CHECK(h != 0 && slot >= 0 && slot < as_signal(h)->slots, "pdmb: bad signal slot");
+  pdmb::signal_set(as_signal(h), (int)slot, (unsigned)value);
+}
+
+// A one-wave kernel on the current stream that holds it until flag[slot] >=
+// value (signal_set from the host) or timeout_s pass.
+void gate(int64_t h, int64_t slot, int64_t value, double timeout_s) {
+  TORCH_CHECK(h != 0, "pdmb: null signal set");
+  pdmb::Signal* s = as_signal(h);
+  c10::hip::HIPGuard guard((c10::DeviceIndex)s->device);
+  hipStream_t st = c10::hip::getCurrentHIPStream((c10::DeviceIndex)s->device).stream();
+  check_hip(pdmb::gate(s, (int)slot, (unsigned)value, timeout_s, st), "gate");
+}
+
 // Tile rows per completion unit (0: the problem cannot run signalled).
 int64_t signal_granule(const at::Tensor& A, const at::Tensor& B, c10::optional<at::Tensor> C, int64_t kernel,
                        int64_t cus) {
@@ -390,16 +405,61 @@ void ipc_close(int64_t ptr, int64_t device) {
 }
 
 // dst (contiguous, this device) <- `dst.nbytes()` bytes at a peer address
-// (an ipc_open mapping + offset), on the current stream: a DMA-engine copy
-// over the xGMI link to that peer, no CUs.
-void copy_from_peer(const at::Tensor& dst, int64_t src_addr) {
+// (an ipc_open mapping + offset), on the current stream. sdma: the
+// hipMemcpyDeviceToDeviceNoCU kind, a DMA-engine copy that takes no CU (a
+// plain DeviceToDevice copy runs the runtime's blit kernel on CUs); else the
+// plain kind (the runtime picks).
+void copy_from_peer(const at::Tensor& dst, int64_t src_addr, bool sdma) {
   TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "pdmb: copy_from_peer: dst must be a contiguous GPU tensor");
   TORCH_CHECK(src_addr != 0, "pdmb: copy_from_peer: null source");
   c10::hip::HIPGuard guard(dst.device().index());
   hipStream_t s = c10::hip::getCurrentHIPStream(dst.device().index()).stream();
   check_hip(hipMemcpyAsync(dst.data_ptr(), (const void*)(uintptr_t)src_addr, dst.nbytes(),
-                           hipMemcpyDeviceToDevice, s),
+                           sdma ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToDevice, s),
             "hipMemcpyAsync (copy_from_peer)");
+}
+
+// dsts[i] (contiguous, this device) <- dsts[i].nbytes() bytes at srcs[i] (a
+// peer mapping + offset, or a local address), every copy in ONE kernel launch
+// on the current stream (reduce.hip multi_copy: all links read at once).
+void peer_copy(const std::vector<at::Tensor>& dsts, const std::vector<int64_t>& srcs, int64_t blocks_per) {
+  TORCH_CHECK(dsts.size() == srcs.size() && (int)dsts.size() <= pdmb::kMaxCopies,
+              "pdmb: peer_copy takes equal-length lists of at most ", pdmb::kMaxCopies);
+  if (dsts.empty()) return;
+  std::vector<void*> d;
+  std::vector<const void*> s;
+  std::vector<size_t> b;
+  for (size_t i = 0; i < dsts.size(); ++i) {
+    TORCH_CHECK(dsts[i].is_cuda() && dsts[i].is_contiguous() && dsts[i].device() == dsts[0].device(),
+                "pdmb: peer_copy destinations must be contiguous tensors on one GPU");
+    TORCH_CHECK(srcs[i] != 0 || dsts[i].nbytes() == 0, "pdmb: peer_copy: null source");
+    d.push_back(dsts[i].data_ptr());
+    s.push_back((const void*)(uintptr_t)srcs[i]);
+    b.push_back(dsts[i].nbytes());
+  }
+  c10::hip::HIPGuard guard(dsts[0].device().index());
+  hipStream_t st = c10::hip::getCurrentHIPStream(dsts[0].device().index()).stream();
+  check_hip(pdmb::multi_copy(d.data(), s.data(), b.data(), (int)d.size(), (int)blocks_per, st), "multi_copy");
+}
+
+// out = sum over the sources at raw device addresses (peer mappings + offsets,
+// or local; each out.numel() elements of out's dtype), fp32 accumulate in list
+// order, on the current stream; blocks > 0 caps the grid.
+void reduce_sum_addrs(const at::Tensor& out, const std::vector<int64_t>& addrs, int64_t blocks) {
+  TORCH_CHECK(!addrs.empty() && (int)addrs.size() <= pdmb::kMaxReduceSrcs, "pdmb: reduce_sum_addrs takes 1..",
+              pdmb::kMaxReduceSrcs, " sources");
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous(), "pdmb: reduce_sum_addrs out must be a contiguous GPU tensor");
+  const int dt = dtype_code(out.scalar_type());
+  TORCH_CHECK(dt <= 2, "pdmb: reduce_sum_addrs takes float32 / float16 / bfloat16");
+  std::vector<const void*> ptrs;
+  for (int64_t a : addrs) {
+    TORCH_CHECK(a != 0, "pdmb: reduce_sum_addrs: null source");
+    ptrs.push_back((const void*)(uintptr_t)a);
+  }
+  c10::hip::HIPGuard guard(out.device().index());
+  hipStream_t s = c10::hip::getCurrentHIPStream(out.device().index()).stream();
+  check_hip(pdmb::reduce_sum(out.data_ptr(), ptrs.data(), (int)ptrs.size(), out.numel(), dt, s, (int)blocks),
+            "reduce_sum");
 }
 
 // Diagnostic: set (or clear, with None) the device buffer the stamp kernel writes.
@@ -426,6 +486,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("signal_wait", &signal_wait, py::arg("handle"), py::arg("slot"), py::arg("epoch"),
         py::arg("timeout_s"));
   m.def("signal_flag", &signal_flag, py::arg("handle"), py::arg("slot"));
+  m.def("signal_set", &signal_set, py::arg("handle"), py::arg("slot"), py::arg("value"));
+  m.def("gate", &gate, "one-wave kernel holding the current stream until flag[slot] >= value",
+        py::arg("handle"), py::arg("slot"), py::arg("value"), py::arg("timeout_s"));
   m.def("signal_granule", &signal_granule, py::arg("A"), py::arg("B"), py::arg("out") = py::none(),
         py::arg("kernel") = 0, py::arg("cus") = 0);
   m.def("resolve", &resolve, "kernel id that would run (or -1)", py::arg("A"), py::arg("B"),
@@ -452,7 +515,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ipc_handle", &ipc_handle, py::arg("t"));
   m.def("ipc_open", &ipc_open, py::arg("handle"), py::arg("device"));
   m.def("ipc_close", &ipc_close, py::arg("ptr"), py::arg("device"));
-  m.def("copy_from_peer", &copy_from_peer, py::arg("dst"), py::arg("src_addr"));
+  m.def("copy_from_peer", &copy_from_peer, py::arg("dst"), py::arg("src_addr"), py::arg("sdma") = true);
+  m.def("peer_copy", &peer_copy, "dsts[i] <- bytes at srcs[i], one launch", py::arg("dsts"), py::arg("srcs"),
+        py::arg("blocks_per") = 0);
+  m.def("reduce_sum_addrs", &reduce_sum_addrs, "out = sum of the sources at raw addresses", py::arg("out"),
+        py::arg("addrs"), py::arg("blocks") = 0);
+  m.attr("MAX_COPIES") = pdmb::kMaxCopies;
   m.def("set_debug_buffer", &set_debug_buffer, py::arg("buf") = py::none());
   m.def("create_cu_masked_stream", &create_cu_masked_stream, py::arg("device"),
         py::arg("excluded"));

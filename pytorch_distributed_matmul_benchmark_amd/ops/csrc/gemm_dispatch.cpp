@@ -1150,6 +1150,11 @@ unsigned signal_flag(const Signal* s, int slot) {
   return __atomic_load_n((volatile unsigned*)s->host + slot, __ATOMIC_ACQUIRE);
 }
 
+void signal_set(Signal* s, int slot, unsigned value) {
+  if (!s || slot < 0 || slot >= s->slots) return;
+  __atomic_store_n((volatile unsigned*)s->host + slot, value, __ATOMIC_RELEASE);
+}
+
 bool signal_wait(const Signal* s, int slot, unsigned epoch, double timeout_s) {
   if (!s || slot < 0 || slot >= s->slots) return false;
   const auto t0 = std::chrono::steady_clock::now();

@@ -197,6 +197,15 @@ class SignalSet:
             raise TimeoutError(f"GEMM completion signal: slot {slot} did not reach epoch {epoch} "
                                f"within {timeout_s:.0f} s (flag {self.flag(slot)})")
 
+    def set(self, slot: int, value: int) -> None:
+        """Host store of slot's flag (opens a ``gate`` waiting for ``value``)."""
+        self._C.signal_set(self.handle, int(slot), int(value))
+
+    def gate(self, slot: int, value: int, timeout_s: float = 20.0) -> None:
+        """Enqueue on the current stream a one-wave kernel that holds the stream
+        until slot's flag reaches ``value`` (``set``) or ``timeout_s`` pass."""
+        self._C.gate(self.handle, int(slot), int(value), float(timeout_s))
+
     def close(self) -> None:
         if self.handle:
             torch.cuda.synchronize(self.device)

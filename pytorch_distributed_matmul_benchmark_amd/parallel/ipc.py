@@ -1,48 +1,58 @@
 """Collectives over xGMI peer memory (``--allgather ipc``, ``--allreduce ipc``).
 
-All-gather: every rank PULLS each
-peer's shard straight out of that peer's memory with DMA-engine copies, one
-copy stream per peer, so on a fully connected 8 x MI355X node the seven
-transfers run over seven xGMI links at once and use no CUs — the GEMM the
-collective overlaps keeps every CU (an RCCL all-gather runs its channels as
-kernels on the same CUs).
+Every rank maps its peers' output buffers once (``hipIpcOpenMemHandle``) and
+then PULLS what it needs straight out of their memory: on a fully connected
+8 x MI355X node each peer sits behind its own xGMI link, so a pull from all
+seven peers drives all seven links at once with no forwarding hop (RCCL's
+ring all-gather forwards every block ws - 1 times, one link per hop).
 
 SURVEY §7.2 (K5-K7 stretch): "custom xGMI peer-memory all-gather (hipIpc
 handles, 7 links in parallel)"; the reference's all-gather call site is
-matmul_scaling_benchmark.py:204-224 (NCCL ``all_gather``).
+matmul_scaling_benchmark.py:221 (NCCL ``all_gather``).
 
-Mechanics (ops/csrc/bindings.cpp ``ipc_*`` / ``copy_from_peer``):
+Two copy engines (``PDMB_IPC_ENGINE``):
 
-  * ``register(src)``: ``src`` (an ``ipc_empty`` tensor: its own hipMalloc
-    allocation) is exported with ``hipIpcGetMemHandle``; the handles are
-    exchanged once (a host all-gather of objects) and every peer's is mapped
-    with ``hipIpcOpenMemHandle``. Every rank registers corresponding buffers
-    in the same order.
-  * ``all_gather(out, inp, after, done)``: ``inp`` is a view into a
-    registered buffer (the same offset on every rank, e.g. a row block of
-    the local output C). On the comm stream: wait ``after``; copy the local
-    block; fork one copy stream per peer and ``hipMemcpyAsync`` that peer's
-    block (same offset in ITS buffer) into ``out``; join; then a
-    stream-ordered barrier (a one-element RCCL all-reduce): when it
-    completes on a rank, every peer has finished pulling from that rank, so
-    the rank's next GEMM may overwrite its shard (pull keeps ``out`` written
-    only by its owner, so no cross-rank hazard on the gathered buffer);
-    record ``done``.
-  * ``close()``: unmap the peers' buffers, then a barrier, so no rank frees
-    an exported buffer another rank still maps.
+  * ``kernel`` (default): ONE launch on the comm stream does every pull
+    (ops/csrc reduce.hip ``multi_copy``: blockIdx.y = peer, 32 workgroups
+    per peer by default, ``PDMB_IPC_BLOCKS``), and the all-reduce's sum reads
+    its chunk straight out of every peer's buffer (``reduce_sum`` over peer
+    addresses: pull and sum fused, no landing copy). It uses CUs — about as
+    many workgroups as RCCL's channels — but adds no streams: a rank runs its
+    compute stream, the comm stream and RCCL's internal stream, inside the
+    process's 4 hardware queues (``GPU_MAX_HW_QUEUES``).
+  * ``sdma``: ``hipMemcpyDeviceToDeviceNoCU`` copies (the DMA engines, no
+    CU; a plain DeviceToDevice copy runs the runtime's blit kernel) spread
+    over at most two copy streams (``COPY_STREAMS``), so the rank stays at
+    five streams: copies on one stream run one after another, which is the
+    price of the bounded stream count.
 
-``all_reduce(t)`` is the direct two-shot all-reduce on the same mappings:
-pull this rank's chunk from every peer, ``reduce_sum`` in rank order, pull
-every peer's reduced chunk, with three stream-ordered barriers (method
-docstring).
+Ordering (both engines; every barrier is stream-ordered — a one-element
+RCCL all-reduce on the comm stream, whose completion on a rank means every
+peer's comm stream has passed the same point):
 
-gloo rehearsals (ranks sharing one GPU) exchange handles the same way; the
-barrier becomes a host barrier after the comm stream drains. CPU tensors have
-no peer memory: ``--allgather ipc`` falls back to the direct P2P all-gather
-there (parallel/comm.py ``all_gather_direct``).
+  * ``all_gather(out, inp, after, done)``: wait ``after`` -> B0 (every
+    rank's ``inp`` is final before anyone reads it) -> pull every peer's
+    block (same offset in ITS buffer) into ``out``, copy the local one ->
+    B1 (every peer has finished reading this rank's block, so its next
+    producer may overwrite it) -> record ``done``.
+  * ``all_reduce(t, after, done)``: B0 -> this rank's chunk = the sum in rank
+    order of that chunk of every rank's ``t`` -> B1 (every chunk reduced) ->
+    pull every peer's reduced chunk into place -> B2.
+
+``register(src)`` exports ``src`` (an ``ipc_empty`` tensor: its own
+hipMalloc allocation) and maps every peer's counterpart (handles exchanged by
+a host all-gather of objects); every rank registers corresponding buffers in
+the same order. ``close()`` unmaps, then barriers, so no rank frees an
+exported buffer another rank still maps.
+
+gloo rehearsals (ranks sharing one GPU) exchange handles the same way; a
+barrier becomes "drain the comm stream, then a host barrier". CPU tensors
+have no peer memory: ``--allgather ipc`` runs the direct P2P exchange there
+(parallel/comm.py).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -64,10 +74,25 @@ def ipc_empty(shape, dtype: torch.dtype, device: torch.device) -> torch.Tensor:
     return _mod().ipc_empty(list(shape), dtype, device.index if device.index is not None else 0)
 
 
-class IpcGather:
-    """Peer-memory all-gather on a CommStream (module docstring)."""
+ENGINES = ("kernel", "sdma")
+COPY_STREAMS = 2  # sdma engine: copy streams per rank (compute + comm + RCCL + 2 = 5)
 
-    def __init__(self, comm: CommStream, group=None):
+
+def engine() -> str:
+    e = os.environ.get("PDMB_IPC_ENGINE", "kernel")
+    if e not in ENGINES:
+        raise ValueError(f"PDMB_IPC_ENGINE={e!r}: one of {ENGINES}")
+    return e
+
+
+def blocks_per_peer() -> int:
+    return int(os.environ.get("PDMB_IPC_BLOCKS", "0"))  # 0: the kernel's default (32)
+
+
+class IpcGather:
+    """Peer-memory all-gather / all-reduce on a CommStream (module docstring)."""
+
+    def __init__(self, comm: CommStream, group=None, engine_name: Optional[str] = None):
         self.cs = comm
         self.group = group
         self.device = comm.device
@@ -75,10 +100,19 @@ class IpcGather:
         self.me = dist.get_rank(group)
         self.gloo = dist.get_backend(group) == "gloo"
         self.dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self.engine = engine_name or engine()
+        if self.engine not in ENGINES:
+            raise ValueError(f"IpcGather engine {self.engine!r}: one of {ENGINES}")
+        self.blocks = blocks_per_peer()
         # registered buffers: (local base address, bytes) -> {peer rank: mapped address}
         self.bufs: List[Tuple[int, int, Dict[int, int]]] = []
-        self.copy_streams = [torch.cuda.Stream(device=self.device) for _ in range(max(self.ws - 1, 0))]
+        self.copy_streams = ([torch.cuda.Stream(device=self.device)
+                              for _ in range(min(COPY_STREAMS, max(self.ws - 1, 0)))]
+                             if self.engine == "sdma" else [])
         self.flag = torch.zeros(1, device=self.device)
+        # test-only fault injection (tests/test_ipc_gpu.py negative control):
+        # skip the pre-read barrier B0 so a pull can see a peer's previous data
+        self._skip_b0 = os.environ.get("PDMB_TEST_IPC_SKIP_B0") == "1"
 
     def register(self, src: torch.Tensor) -> None:
         """Export ``src`` and map every peer's corresponding buffer (collective)."""
@@ -90,70 +124,92 @@ class IpcGather:
         peers = {r: mod.ipc_open(h, self.dev_index) for r, h in enumerate(handles) if r != self.me}
         self.bufs.append((src.data_ptr(), src.untyped_storage().nbytes(), peers))
 
+    @property
+    def npeers(self) -> int:
+        """Peers whose buffers are mapped (ws - 1 once a buffer is registered)."""
+        return len(self.bufs[0][2]) if self.bufs else 0
+
     def _peer_addr(self, t: torch.Tensor, peer: int) -> int:
+        """Address of ``t``'s counterpart in ``peer``'s buffer (``t`` itself for this rank)."""
         p = t.data_ptr()
+        if peer == self.me:
+            return p
         for base, nbytes, peers in self.bufs:
             if base <= p and p + t.nbytes <= base + nbytes:
                 return peers[peer] + (p - base)
         raise ValueError("IpcGather: the input is not inside a registered buffer")
+
+    def _pull(self, jobs) -> None:
+        """Issue ``jobs`` [(dst tensor, src address)] on the comm stream (kernel
+        engine: one launch) or over the copy streams forked from / joined back
+        to it (sdma engine). Call with the comm stream current."""
+        jobs = [(d, a) for d, a in jobs if d.numel()]
+        if not jobs:
+            return
+        mod = _mod()
+        cs = self.cs.stream
+        if self.engine == "kernel":
+            mod.peer_copy([d for d, _ in jobs], [a for _, a in jobs], self.blocks)
+            return
+        fork = torch.cuda.Event()
+        fork.record(cs)
+        joins = []
+        for i, st in enumerate(self.copy_streams):
+            mine = jobs[i::len(self.copy_streams)]
+            if not mine:
+                continue
+            with torch.cuda.stream(st):
+                st.wait_event(fork)
+                for d, a in mine:
+                    mod.copy_from_peer(d, a, True)
+                ev = torch.cuda.Event()
+                ev.record(st)
+                joins.append(ev)
+        for ev in joins:
+            cs.wait_event(ev)
 
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor, after=None, done=None) -> None:
         """``out`` [ws * rows, ...] (contiguous) <- every rank's ``inp`` [rows, ...]."""
         assert inp.is_contiguous() and out.is_contiguous()
         rows = inp.shape[0]
         blocks = [out[r * rows:(r + 1) * rows] for r in range(self.ws)]
-        mod = _mod()
         cs = self.cs.stream
         with stream_ctx(cs):
             if after is not None:
                 cs.wait_event(after)
-            blocks[self.me].copy_(inp)
-            fork = torch.cuda.Event()
-            fork.record(cs)
-        joins = []
-        for i, d in enumerate(range(1, self.ws)):
-            p = (self.me + d) % self.ws
-            st = self.copy_streams[i]
-            with torch.cuda.stream(st):
-                st.wait_event(fork)
-                mod.copy_from_peer(blocks[p], self._peer_addr(inp, p))
-                ev = torch.cuda.Event()
-                ev.record(st)
-                joins.append(ev)
-        with stream_ctx(cs):
-            for ev in joins:
-                cs.wait_event(ev)
-            self._barrier()
+            if not self._skip_b0:
+                self._barrier()  # B0: every rank's block is final
+            if self.engine == "sdma":
+                blocks[self.me].copy_(inp)
+                jobs = []
+            else:
+                jobs = [(blocks[self.me], inp.data_ptr())]
+            jobs += [(blocks[p], self._peer_addr(inp, p))
+                     for p in ((self.me + d) % self.ws for d in range(1, self.ws))]
+            self._pull(jobs)
+            self._barrier()  # B1: no peer still reads this rank's block
             if done is not None:
                 done.record(cs)
 
     def all_reduce(self, t: torch.Tensor, after=None, done=None) -> None:
         """SUM all-reduce of ``t`` (a contiguous view into a registered buffer,
-        the same offsets on every rank) over peer memory — the direct
-        two-shot exchange of ``CommStream.all_reduce_direct`` with pulls
-        instead of P2P sends, so DMA engines move the bytes and no CUs do:
-
-          B0 barrier (every rank's ``t`` final) -> pull chunk ``me`` of every
-          peer's ``t`` into scratch (one copy stream per peer) -> native
-          ``reduce_sum`` in rank order into this rank's chunk -> B1 barrier
-          (every chunk reduced) -> pull every peer's reduced chunk into place
-          -> B2 barrier (no peer still reads this rank's chunk when its next
-          producer overwrites ``t``).
-
-        Chunks are 64-element multiples (16-B aligned); every rank sums in the
-        same order, so all ranks hold identical bits."""
+        the same offsets on every rank) over peer memory — the two-shot
+        exchange of ``CommStream.all_reduce_direct`` with pulls instead of
+        P2P sends (module docstring). Chunks are 64-element multiples (16-B
+        aligned); every rank sums in rank order, so all ranks hold identical
+        bits."""
         from .comm import reduce_sum_
 
         assert t.is_contiguous()
+        cs = self.cs.stream
         if self.ws == 1 or t.numel() == 0:
-            with stream_ctx(self.cs.stream):
+            with stream_ctx(cs):
                 if after is not None:
-                    self.cs.stream.wait_event(after)
+                    cs.wait_event(after)
                 if done is not None:
-                    done.record(self.cs.stream)
+                    done.record(cs)
             return
         mod = _mod()
-        cs = self.cs.stream
         flat = t.view(-1)
         n = flat.numel()
         per = -(-n // self.ws)            # ceil(n / ws)
@@ -163,50 +219,25 @@ class IpcGather:
         mine = part[self.me]
         m = mine.numel()
         es = t.element_size()
-        scratch = self.cs._scratch(t, (self.ws - 1) * chunk)
-        slot = {}
+        peers = [(self.me + d) % self.ws for d in range(1, self.ws)]
         with stream_ctx(cs):
             if after is not None:
                 cs.wait_event(after)
-            self._barrier()  # B0
-            fork = torch.cuda.Event()
-            fork.record(cs)
-        joins = []
-        peers = [(self.me + d) % self.ws for d in range(1, self.ws)]
-        for i, p in enumerate(peers):
-            slot[p] = scratch[i * chunk:i * chunk + m]
-            if not m:
-                continue
-            st = self.copy_streams[i]
-            with torch.cuda.stream(st):
-                st.wait_event(fork)
-                mod.copy_from_peer(slot[p], self._peer_addr(t, p) + bounds[self.me][0] * es)
-                ev = torch.cuda.Event()
-                ev.record(st)
-                joins.append(ev)
-        with stream_ctx(cs):
-            for ev in joins:
-                cs.wait_event(ev)
+            self._barrier()  # B0: every rank's t is final
             if m:
-                reduce_sum_(mine, [mine if r == self.me else slot[r] for r in range(self.ws)])
-            self._barrier()  # B1
-            fork = torch.cuda.Event()
-            fork.record(cs)
-        joins = []
-        for i, p in enumerate(peers):
-            if not part[p].numel():
-                continue
-            st = self.copy_streams[i]
-            with torch.cuda.stream(st):
-                st.wait_event(fork)
-                mod.copy_from_peer(part[p], self._peer_addr(t, p) + bounds[p][0] * es)
-                ev = torch.cuda.Event()
-                ev.record(st)
-                joins.append(ev)
-        with stream_ctx(cs):
-            for ev in joins:
-                cs.wait_event(ev)
-            self._barrier()  # B2
+                if self.engine == "kernel":
+                    # pull and sum fused: this chunk of every rank's t, read in place
+                    addrs = [self._peer_addr(t, r) + bounds[self.me][0] * es for r in range(self.ws)]
+                    mod.reduce_sum_addrs(mine, addrs, 0)
+                else:
+                    scratch = self.cs._scratch(t, (self.ws - 1) * chunk)
+                    slot = {p: scratch[i * chunk:i * chunk + m] for i, p in enumerate(peers)}
+                    self._pull([(slot[p], self._peer_addr(t, p) + bounds[self.me][0] * es)
+                                for p in peers])
+                    reduce_sum_(mine, [mine if r == self.me else slot[r] for r in range(self.ws)])
+            self._barrier()  # B1: every chunk reduced
+            self._pull([(part[p], self._peer_addr(t, p) + bounds[p][0] * es) for p in peers])
+            self._barrier()  # B2: no peer still reads this rank's chunk
             if done is not None:
                 done.record(cs)
 

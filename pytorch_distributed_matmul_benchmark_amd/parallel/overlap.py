@@ -115,10 +115,15 @@ class OverlapPlan:
     overlap_us: float      # predicted per unit, overlapped with the chosen pieces
     candidates: Dict[int, float] = field(default_factory=dict)
     reason: str = ""
+    # "measured": gemm_us / comm_us / piece_us timed on this job's ranks (MAX
+    # over ranks, measured_plan); "model": the GEMM and busBW tables above
+    source: str = "model"
+    piece_us: Dict[int, float] = field(default_factory=dict)  # measured: one piece's collective, per P
 
     def as_dict(self) -> dict:
         d = asdict(self)
         d["candidates"] = {str(k): round(v, 1) for k, v in self.candidates.items()}
+        d["piece_us"] = {str(k): round(v, 1) for k, v in self.piece_us.items()}
         for k in ("gemm_us", "comm_us", "serial_us", "overlap_us"):
             d[k] = round(d[k], 1)
         return d
@@ -128,7 +133,9 @@ def plan_overlap(m: int, n: int, k: int, dtype: torch.dtype, ws: int, kind: str,
                  payload_bytes: float, granule: int = 0, steps: int = 10,
                  requested: int = 0, gemm_time_us: Optional[float] = None,
                  comm_time_us: Optional[float] = None,
-                 piece_us: float = COLLECTIVE_LAT_US + PIECE_HOST_US) -> OverlapPlan:
+                 piece_us: float = COLLECTIVE_LAT_US + PIECE_HOST_US,
+                 piece_time_us: Optional[Dict[int, float]] = None,
+                 source: str = "model") -> OverlapPlan:
     """Choose how a unit (one [m, k] @ [k, n] GEMM whose output's collective
     follows) overlaps: serialize, pipeline whole collectives across units
     (pieces = 1), or start P row pieces as the GEMM's tiles finish (P > 1,
@@ -147,55 +154,174 @@ def plan_overlap(m: int, n: int, k: int, dtype: torch.dtype, ws: int, kind: str,
     what the granule allows), overlapped even where the model predicts a
     loss; 0 lets the planner choose, and it refuses an overlap that does not
     beat serial by 3 %. ``gemm_time_us`` / ``comm_time_us`` replace the
-    models (measured values, e.g. the 1-GPU proxy sweep)."""
+    models (measured values: ``measured_plan``, or the 1-GPU proxy sweep);
+    ``piece_time_us[P]`` (measured time of ONE piece's collective when a unit
+    is cut into P pieces) replaces C' with P x piece_time_us[P]."""
     G = gemm_time_us if gemm_time_us is not None else gemm_us(m, n, k, dtype)
     C = comm_time_us if comm_time_us is not None else collective_us(kind, payload_bytes, ws)
     serial = G + C
     tm = ceil_div(max(m, 1), 256)
     units = tm // granule if granule > 0 else 1
-    choices = [p for p in (1, 2, 4, 8) if p == 1 or (granule > 0 and p <= units)]
-    if requested > 0:
-        allowed = [p for p in choices if p <= requested]
-        choices = [max(allowed)] if allowed else [1]
+    choices = piece_choices(m, granule, requested)
+    measured = dict(piece_time_us or {})
 
     def cost(P: int) -> float:
-        Cp = C + (P - 1) * piece_us
+        Cp = P * measured[P] if P in measured else C + (P - 1) * piece_us
         Gp = G + RCCL_CU_SHARE * min(G, Cp)
         return max(Gp, Cp) + min(Gp, Cp) / P / max(steps, 1)
 
     cands = {P: cost(P) for P in choices}
     best = min(cands, key=lambda P: (cands[P], P))
     ov = cands[best]
+    kw = dict(candidates=cands, source=source, piece_us=measured)
     if C <= 0.0:
-        return OverlapPlan(False, 1, 0, G, C, serial, serial, cands, "no collective (ws = 1)")
+        return OverlapPlan(False, 1, 0, G, C, serial, serial, reason="no collective (ws = 1)", **kw)
     if ov >= serial * 0.97 and requested <= 0:
-        return OverlapPlan(False, 1, 0, G, C, serial, ov, cands,
-                           f"overlap predicted {ov:.0f} us vs serial {serial:.0f} us: serialize")
+        return OverlapPlan(False, 1, 0, G, C, serial, ov,
+                           reason=f"overlap predicted {ov:.0f} us vs serial {serial:.0f} us: serialize",
+                           **kw)
     rows = 0
     if best > 1:
         rows = ceil_div(units, best) * granule
     why = "requested" if requested > 0 else "planned"
-    return OverlapPlan(True, best, rows, G, C, serial, ov, cands,
-                       f"{why}: {best} piece(s), {ov:.0f} us vs serial {serial:.0f} us")
+    return OverlapPlan(True, best, rows, G, C, serial, ov,
+                       reason=f"{why}: {best} piece(s), {ov:.0f} us vs serial {serial:.0f} us", **kw)
 
 
-def plan_for_units(units: Sequence[Tuple], ws: int, kind: str, payload_bytes: float,
-                   native: bool = True, requested: int = 0, steps: int = 10,
-                   owner=None) -> OverlapPlan:
-    """``plan_overlap`` for a ring of (A, B, out) units: the shapes of unit 0,
-    and the signal granule of its GEMM as the pipeline would issue it (beside
-    collectives: ``gemm.shared_device``, a masked stream's CU budget)."""
+def piece_choices(m: int, granule: int, requested: int = 0) -> List[int]:
+    """The piece counts ``plan_overlap`` considers for an m-row unit."""
+    tm = ceil_div(max(m, 1), 256)
+    units = tm // granule if granule > 0 else 1
+    choices = [p for p in (1, 2, 4, 8) if p == 1 or (granule > 0 and p <= units)]
+    if requested > 0:
+        allowed = [p for p in choices if p <= requested]
+        choices = [max(allowed)] if allowed else [1]
+    return choices
+
+
+def piece_span(m: int, granule: int, P: int) -> int:
+    """Rows of the first (largest) piece when an m-row unit is cut into P pieces."""
+    if P <= 1 or granule <= 0:
+        return m
+    tm = ceil_div(max(m, 1), 256)
+    return min(m, ceil_div(tm // granule, P) * granule * 256)
+
+
+def _granule(units: Sequence[Tuple], native: bool, owner=None) -> int:
+    """The signal granule of unit 0's GEMM as the pipeline would issue it
+    (beside collectives: ``gemm.shared_device``, a masked stream's CU budget)."""
     import contextlib
 
     from ..ops import gemm
 
     A, B, C = units[0]
-    granule = 0
     if C.device.type == "cuda" and native and A.dtype in (torch.bfloat16, torch.float16):
         with gemm.shared_device(), (owner.budget() if owner is not None else contextlib.nullcontext()):
-            granule = gemm.signal_granule(A, B, C)
+            return gemm.signal_granule(A, B, C)
+    return 0
+
+
+def plan_for_units(units: Sequence[Tuple], ws: int, kind: str, payload_bytes: float,
+                   native: bool = True, requested: int = 0, steps: int = 10,
+                   owner=None) -> OverlapPlan:
+    """``plan_overlap`` for a ring of (A, B, out) units from the MODELS: the
+    shapes of unit 0 and the signal granule of its GEMM. ``measured_plan`` is
+    the one the modes use; this is its fallback."""
+    A, B, C = units[0]
     return plan_overlap(C.shape[-2], C.shape[-1], A.shape[-1], A.dtype, ws, kind, payload_bytes,
-                        granule=granule, steps=steps, requested=requested)
+                        granule=_granule(units, native, owner), steps=steps, requested=requested)
+
+
+def measured_plan(units: Sequence[Tuple], ctx, kind: str, payload_bytes: float, mm: Callable,
+                  piece_collective: Callable[[int, int], None], *, native: bool = True,
+                  requested: int = 0, steps: int = 10, compute=None, owner=None,
+                  comm: Optional[CommStream] = None, reps: int = 3) -> OverlapPlan:
+    """``plan_overlap`` from times measured on this job's own ranks — the
+    reference judges its serialized and overlapped modes by measured time
+    (backup/matmul_overlap_benchmark.py:155-164, matmul_scaling_benchmark.py:
+    204-224), so the plan is priced the same way instead of from the busBW
+    guesses above:
+
+      * G: unit 0's GEMM, ``reps`` launches on the compute stream in the
+        context the pipeline issues it in (``compute_ctx``: shared device,
+        a masked stream's CU budget), timed with events;
+      * C(P) for every piece count P the planner may choose: one collective
+        of the first piece's rows, ``piece_collective(start, stop)`` (the
+        mode's own collective — RCCL / direct / ipc — on ring slot 0, issued
+        on the comm stream), ``reps`` times after a barrier, host-timed
+        until the comm stream drains (so a piece's host issue cost counts);
+      * every value is the MAX over ranks, so all ranks hold the same plan.
+
+    Only the GEMM's slowdown while a collective runs beside it
+    (``RCCL_CU_SHARE``) stays modelled. If measuring fails on any rank the
+    model plan (``plan_for_units``) is returned, ``source == "model"``.
+    Collective: every rank must call it."""
+    import time
+
+    from .dist import all_ok, barrier, reduce_scalar
+
+    A, B, C = units[0]
+    m, ws, dev = C.shape[-2], ctx.world_size, C.device
+    granule = _granule(units, native, owner)
+    model = plan_overlap(m, C.shape[-1], A.shape[-1], A.dtype, ws, kind, payload_bytes,
+                         granule=granule, steps=steps, requested=requested)
+    if ws <= 1:
+        return model
+    choices = piece_choices(m, granule, requested)
+    if 1 not in choices:
+        choices = [1] + choices
+    cuda = dev.type == "cuda"
+    cs = comm or CommStream(dev)
+    err = None
+    G, piece = 0.0, {}
+    try:
+        def sync():
+            if cuda:
+                torch.cuda.synchronize(dev)
+
+        # GEMM: events on the compute stream, in the pipeline's issue context
+        sync()
+        with compute_ctx(compute, owner):
+            mm(A, B, C)  # first launch outside the timing (kernel selection, workspace)
+        sync()
+        if cuda:
+            cur = compute if compute is not None else torch.cuda.current_stream(dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with compute_ctx(compute, owner):
+                e0.record(cur)
+                for _ in range(reps):
+                    mm(A, B, C)
+                e1.record(cur)
+            e1.synchronize()
+            G = e0.elapsed_time(e1) * 1e3 / reps
+        else:
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                mm(A, B, C)
+            G = (time.perf_counter() - t0) * 1e6 / reps
+        # collectives: one piece per candidate P, after a barrier
+        for P in choices:
+            span = piece_span(m, granule, P)
+            piece_collective(0, span)  # untimed first call (buffers, communicator paths)
+            cs.synchronize()
+            sync()
+            barrier(ctx)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                piece_collective(0, span)
+            cs.synchronize()
+            sync()
+            piece[P] = (time.perf_counter() - t0) * 1e6 / reps
+    except Exception as e:  # a failed measurement falls back to the model, on every rank alike
+        err = f"{type(e).__name__}: {e}"
+    if not all_ok(ctx, err is None):
+        model.reason += f" (measuring failed: {err or 'on another rank'})"
+        return model
+    G = reduce_scalar(ctx, G, "max")
+    piece = {P: reduce_scalar(ctx, v, "max") for P, v in sorted(piece.items())}
+    return plan_overlap(m, C.shape[-1], A.shape[-1], A.dtype, ws, kind, payload_bytes,
+                        granule=granule, steps=steps, requested=requested, gemm_time_us=G,
+                        comm_time_us=piece[1], piece_time_us=piece, source="measured")
 
 
 def piece_rows(m: int, rows: int) -> List[Tuple[int, int]]:
@@ -297,15 +423,31 @@ class OverlapPipeline:
     ``collective`` must enqueue the collective of rows [start, stop) of ring
     slot r's output on the comm stream after event ``after`` (None: the rows
     are known complete) and record ``done`` behind it (CommStream's
-    all_reduce / all_gather_into accept exactly these)."""
+    all_reduce / all_gather_into accept exactly these).
+
+    ``operands(k)`` (optional) returns the (A, B) of unit number k (counting
+    from 0 over the pipeline's life) instead of its ring slot's own: the
+    ``--check`` runs give every unit a distinct product, so a collective
+    that reads a ring slot before its GEMM has rewritten it (or after the
+    next one has) sees another unit's bits and the check fails.
+    ``slot_unit[r]`` is the unit number that last wrote ring slot r.
+
+    Test-only fault injection (the checks' negative control):
+    ``PDMB_TEST_SKIP_READY_WAIT=<cycles>`` issues every collective without
+    its producer dependency (no ready event, no signal wait) and delays each
+    GEMM by ``<cycles>`` GPU clocks on the compute stream, so the collective
+    reliably reads the slot's previous contents."""
 
     def __init__(self, mm: Callable, units: Sequence[Tuple], collective: Callable,
                  device: torch.device, plan: OverlapPlan, per_step: int = 1,
                  compute=None, owner=None, comm: Optional[CommStream] = None,
-                 timeout_s: float = 120.0):
+                 timeout_s: float = 120.0, operands: Optional[Callable[[int], Tuple]] = None):
         from ..ops import gemm
 
         self.mm, self.units, self.collective = mm, list(units), collective
+        self.operands = operands
+        skip = os.environ.get("PDMB_TEST_SKIP_READY_WAIT", "")
+        self._skip_cycles = int(skip) if skip else None
         self.R = len(self.units)
         if self.R < 2:
             raise ValueError("OverlapPipeline needs a ring of >= 2 output buffers")
@@ -321,17 +463,23 @@ class OverlapPipeline:
         self.ready = [new_event(device) for _ in range(self.R)]
         self.done = [new_event(device) for _ in range(self.R)]
         self.used = [False] * self.R
+        self.slot_unit = [-1] * self.R
         self.k = 0
         self.pending: Optional[Tuple[int, int]] = None  # (ring slot, epoch) awaiting its pieces
 
-    def _gemm(self, r: int) -> Optional[int]:
+    def _gemm(self, r: int, k: int) -> Optional[int]:
         from ..ops import gemm
 
         A, B, out = self.units[r]
+        if self.operands is not None:
+            A, B = self.operands(k)
+        self.slot_unit[r] = k
         with compute_ctx(self.compute, self.owner):
             cur = self.compute if self.compute is not None else None
             if self.used[r] and cur is not None:
                 cur.wait_event(self.done[r])  # WAR: the buffer's last collective is done
+            if self._skip_cycles and cur is not None:
+                torch.cuda._sleep(self._skip_cycles)  # test-only: see the class docstring
             if self.signalled:
                 epoch = self.sigs[r].next_epoch()
                 gemm.matmul(A, B, out=out, signal=(self.sigs[r], self.plan.rows, epoch))
@@ -344,7 +492,9 @@ class OverlapPipeline:
     def _issue(self, r: int, epoch: Optional[int]) -> None:
         last = len(self.pieces) - 1
         for p, (s, e) in enumerate(self.pieces):
-            if epoch is not None:
+            if self._skip_cycles is not None:
+                after = None  # test-only: no producer dependency at all
+            elif epoch is not None:
                 self.sigs[r].wait(p, epoch, self.timeout_s)  # rows [s, e) are stored
                 after = None
             else:
@@ -354,9 +504,9 @@ class OverlapPipeline:
 
     def step(self) -> None:
         for _ in range(self.per_step):
-            r = self.k % self.R
+            r, k = self.k % self.R, self.k
             self.k += 1
-            epoch = self._gemm(r)
+            epoch = self._gemm(r, k)
             if self.signalled:
                 # the next GEMM is queued before this host thread blocks on the
                 # previous unit's pieces, so the compute stream never runs dry

@@ -495,20 +495,14 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     auto ar_chunk = [&](size_t count) { return ((count + ws - 1) / ws + 63) / 64 * 64; };  // 16-B aligned chunks
     const size_t ar_chunk_max = ar_chunk(lb * mat);
     Buf ARs((o.direct_ar || o.peer_ar) && ws > 1 ? (size_t)(ws - 1) * ar_chunk_max * oes : 0);
-    // --allreduce ipc (parallel/ipc.py IpcGather.all_reduce): the same two shots
-    // as pulls out of the peers' C / C2 (direct peer access between this
-    // process's GPUs), one copy stream per peer, three one-element all-reduces
-    // as stream-ordered barriers (outputs final; chunks reduced; nobody still
-    // reading this rank's chunk).
-    struct StreamSet {
-      std::vector<hipStream_t> v;
-      ~StreamSet() {
-        for (hipStream_t q : v) (void)hipStreamDestroy(q);
-      }
-    } arset;
-    std::vector<hipEvent_t> are;
+    // --allreduce ipc (parallel/ipc.py IpcGather.all_reduce, kernel engine):
+    // the same two shots read straight out of the peers' C / C2 (direct peer
+    // access between this process's GPUs) from the comm stream — the chunk's
+    // sum reads every rank's copy in place (reduce_sum over peer addresses),
+    // the reduced chunks come back in one multi_copy launch — with three
+    // one-element all-reduces as stream-ordered barriers (outputs final;
+    // chunks reduced; nobody still reading this rank's chunk). No copy streams.
     Buf arflag(o.peer_ar ? 256 : 0);
-    hipEvent_t arfork = nullptr;
     peers.src[rank] = {(char*)C.p, (char*)C2.p};
     if (o.peer_ar && ws > 1) {
       for (int d = 0; d < ws; ++d) {
@@ -520,13 +514,6 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
         if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_OK(e);
         (void)hipGetLastError();
       }
-      for (int d = 1; d < ws; ++d) {
-        hipStream_t q;
-        HIP_OK(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
-        arset.v.push_back(q);
-        are.push_back(event());
-      }
-      arfork = event();
       HIP_OK(hipMemsetAsync(arflag.p, 0, arflag.bytes, st));
     }
     bar.wait();  // every rank's buffers published before anyone pulls
@@ -538,32 +525,24 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
       const int sid = (b >= (char*)C.p && b < (char*)C.p + C.bytes) ? 0 : 1;
       const size_t off = (size_t)(b - (sid ? (char*)C2.p : (char*)C.p));
       const size_t m = len_of(rank);
-      auto slot = [&](int d) { return (char*)ARs.p + (size_t)(d - 1) * chunk * oes; };  // from rank + d
       auto barrier = [&]() { NCCL_OK(ncclAllReduce(arflag.p, arflag.p, 1, ncclFloat, ncclSum, comm, s)); };
-      auto pulls = [&](bool reduced) {
-        HIP_OK(hipEventRecord(arfork, s));
-        for (int d = 1; d < ws; ++d) {
-          const int from = (rank + d) % ws;
-          const size_t lo = reduced ? lo_of(from) : lo_of(rank), len = reduced ? len_of(from) : m;
-          if (!len) continue;
-          hipStream_t q = arset.v[d - 1];
-          HIP_OK(hipStreamWaitEvent(q, arfork, 0));
-          HIP_OK(hipMemcpyAsync(reduced ? b + lo * oes : slot(d), peers.src[from][sid] + off + lo * oes,
-                                len * oes, hipMemcpyDeviceToDevice, q));
-          HIP_OK(hipEventRecord(are[d - 1], q));
-          HIP_OK(hipStreamWaitEvent(s, are[d - 1], 0));
-        }
-      };
       barrier();  // B0: every rank's output final
-      pulls(false);
       if (m) {
         std::vector<const void*> srcs(ws);
-        for (int r = 0; r < ws; ++r)
-          srcs[r] = r == rank ? (const void*)(b + lo_of(rank) * oes) : (const void*)slot((r - rank + ws) % ws);
+        for (int r = 0; r < ws; ++r) srcs[r] = peers.src[r][sid] + off + lo_of(rank) * oes;
         HIP_OK(pdmb::reduce_sum(b + lo_of(rank) * oes, srcs.data(), ws, (int64_t)m, out_dtype(dt), s));
       }
       barrier();  // B1: every chunk reduced
-      pulls(true);
+      std::vector<void*> dsts;
+      std::vector<const void*> srcs;
+      std::vector<size_t> lens;
+      for (int d = 1; d < ws; ++d) {
+        const int from = (rank + d) % ws;
+        dsts.push_back(b + lo_of(from) * oes);
+        srcs.push_back(peers.src[from][sid] + off + lo_of(from) * oes);
+        lens.push_back(len_of(from) * oes);
+      }
+      HIP_OK(pdmb::multi_copy(dsts.data(), srcs.data(), lens.data(), (int)dsts.size(), 0, s));
       barrier();  // B2: no peer still reads this rank's chunk
     };
     auto allreduce = [&](void* buf, size_t count, hipStream_t s) {
@@ -807,20 +786,13 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     Buf Cl2(o.overlap ? Cl.bytes : 0), G2(o.overlap ? G.bytes : 0);
     peers.src[rank] = {(char*)Cl.p, (char*)Cl2.p};
     bar.wait();  // every rank's buffers published before anyone pulls
-    // --allgather ipc: pull each peer's block (same offset in ITS buffer) on a
-    // copy stream per peer (DMA engines, one xGMI link each, no CUs), then a
-    // one-element all-reduce as a stream-ordered barrier: once it completes
-    // every peer has finished reading this rank's block (parallel/ipc.py).
-    struct StreamSet {
-      std::vector<hipStream_t> v;
-      ~StreamSet() {
-        for (hipStream_t q : v) (void)hipStreamDestroy(q);
-      }
-    } cpset;
-    std::vector<hipStream_t>& cps = cpset.v;
-    std::vector<hipEvent_t> cpe;
+    // --allgather ipc (parallel/ipc.py IpcGather.all_gather, kernel engine):
+    // a one-element all-reduce as a stream-ordered barrier (every peer's block
+    // final), then every peer's block (same offset in ITS buffer) and the
+    // local one in ONE multi_copy launch — every xGMI link read at once from
+    // the comm stream, no copy streams — then a second barrier: once it
+    // completes every peer has finished reading this rank's block.
     Buf flag(o.peer ? 256 : 0);
-    hipEvent_t fork = nullptr;
     if (o.peer && ws > 1) {
       for (int d = 0; d < ws; ++d) {
         if (d == rank) continue;
@@ -831,13 +803,6 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
         if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_OK(e);
         (void)hipGetLastError();
       }
-      for (int d = 1; d < ws; ++d) {
-        hipStream_t q;
-        HIP_OK(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
-        cps.push_back(q);
-        cpe.push_back(event());
-      }
-      fork = event();
       HIP_OK(hipMemsetAsync(flag.p, 0, flag.bytes, st));
     }
     auto pull_gather = [&](const char* send, char* recv, size_t count, hipStream_t s) {
@@ -847,17 +812,18 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
                              : (char*)Cl.p;
       const int slot = base == (char*)Cl.p ? 0 : 1;
       const size_t off = (size_t)(send - base);
-      HIP_OK(hipMemcpyAsync(recv + (size_t)rank * bytes, send, bytes, hipMemcpyDeviceToDevice, s));
-      HIP_OK(hipEventRecord(fork, s));
-      for (int d = 1; d < ws; ++d) {
+      NCCL_OK(ncclAllReduce(flag.p, flag.p, 1, ncclFloat, ncclSum, comm, s));  // B0: blocks final
+      std::vector<void*> dsts;
+      std::vector<const void*> srcs;
+      std::vector<size_t> lens;
+      for (int d = 0; d < ws; ++d) {
         const int from = (rank + d) % ws;
-        HIP_OK(hipStreamWaitEvent(cps[d - 1], fork, 0));
-        HIP_OK(hipMemcpyAsync(recv + (size_t)from * bytes, peers.src[from][slot] + off, bytes,
-                              hipMemcpyDeviceToDevice, cps[d - 1]));
-        HIP_OK(hipEventRecord(cpe[d - 1], cps[d - 1]));
-        HIP_OK(hipStreamWaitEvent(s, cpe[d - 1], 0));
+        dsts.push_back(recv + (size_t)from * bytes);
+        srcs.push_back(d == 0 ? (const void*)send : (const void*)(peers.src[from][slot] + off));
+        lens.push_back(bytes);
       }
-      NCCL_OK(ncclAllReduce(flag.p, flag.p, 1, ncclFloat, ncclSum, comm, s));
+      HIP_OK(pdmb::multi_copy(dsts.data(), srcs.data(), lens.data(), (int)dsts.size(), 0, s));
+      NCCL_OK(ncclAllReduce(flag.p, flag.p, 1, ncclFloat, ncclSum, comm, s));  // B1: reads done
     };
     auto allgather = [&](const void* send, char* recv, size_t count, hipStream_t s) {
       if (o.peer && ws > 1) {

@@ -68,17 +68,23 @@ def visible_gpus() -> int:
 
 
 class ClockSampler:
-    """Mean GFX clock (MHz) and socket power (W) of one GPU while active.
+    """Median GFX clock (MHz) and socket power (W) of one GPU while active,
+    polled every ``period_s`` (5 ms: a 0.1 s timed region still gets ~20
+    samples), with the sample counts — a median of a handful of samples is
+    reported as such, and a region shorter than the sensor's own averaging
+    window (the socket-power reading lags by tens of ms) shows it in
+    ``power_key``.
 
     ``with ClockSampler(device) as s: ...`` then ``s.result()`` ->
-    ``{"sclk_mhz": .., "power_w": .., "samples": n}`` (values None when amdsmi
-    is unavailable or the device cannot be matched)."""
+    ``{"sclk_mhz", "power_w", "sclk_samples", "power_samples", "power_key"}``
+    (values None when amdsmi is unavailable or the device cannot be matched)."""
 
-    def __init__(self, device, period_s: float = 0.02):
+    def __init__(self, device, period_s: float = 0.005):
         self.device = device
         self.period = period_s
         self._clk: List[float] = []
         self._pwr: List[float] = []
+        self._pkey: Optional[str] = None
         self._stop = threading.Event()
         self._t = None
         self._h = None
@@ -113,6 +119,7 @@ class ClockSampler:
                     w = p.get(key)
                     if isinstance(w, (int, float)) and w > 0:
                         self._pwr.append(float(w))
+                        self._pkey = key
                         break
             except Exception:
                 pass
@@ -141,6 +148,13 @@ class ClockSampler:
         return False
 
     def result(self) -> dict:
-        mean = (lambda xs: round(sum(xs) / len(xs), 1) if xs else None)
-        return {"sclk_mhz": mean(self._clk), "power_w": mean(self._pwr), "samples": len(self._clk)}
+        def median(xs):
+            if not xs:
+                return None
+            v = sorted(xs)
+            h = len(v) // 2
+            return round(v[h] if len(v) % 2 else 0.5 * (v[h - 1] + v[h]), 1)
+        return {"sclk_mhz": median(self._clk), "power_w": median(self._pwr),
+                "sclk_samples": len(self._clk), "power_samples": len(self._pwr),
+                "power_key": self._pkey}
 

@@ -60,6 +60,16 @@ run_stage() {
                    --warmup 1 --extra-steps 2 --extra-warmup 1 ;;
     selflaunch4) step selflaunch4 400 python bench.py --gpus 4 --dist-backend gloo --size 4096 --steps 3 \
                    --warmup 1 --extra-steps 2 --extra-warmup 1 ;;
+    selflaunch8) step selflaunch8 500 python bench.py --gpus 8 --dist-backend gloo --size 4096 --steps 3 \
+                   --warmup 1 --extra-steps 2 --extra-warmup 1 &&
+                 grep '^{' "$OUT/selflaunch8.log" > "$OUT/selflaunch8.json" ;;
+    selflaunch8_ipc) step selflaunch8_ipc 500 python bench.py --gpus 8 --dist-backend gloo --size 4096 \
+                       --steps 3 --warmup 1 --extra-steps 2 --extra-warmup 1 --allgather ipc --allreduce ipc &&
+                     grep '^{' "$OUT/selflaunch8_ipc.log" > "$OUT/selflaunch8_ipc.json" ;;
+    selflaunch8_chunks) step selflaunch8_chunks 500 python bench.py --gpus 8 --dist-backend gloo --size 4096 \
+                          --steps 3 --warmup 1 --extra-steps 2 --extra-warmup 1 --allgather ipc --allreduce ipc \
+                          --mode matrix_parallel --overlap --chunks 2 &&
+                        grep '^{' "$OUT/selflaunch8_chunks.log" > "$OUT/selflaunch8_chunks.json" ;;
     gpus2_refused) echo "== gpus2_refused"; timeout -k 10 120 python bench.py --gpus 2 > "$OUT/gpus2_refused.log" 2>&1
                    local rc=$?; cat "$OUT/gpus2_refused.log"; echo "== gpus2_refused rc=$rc (want 2)"; [ $rc -eq 2 ] ;;
     ab_bf16) step ab_bf16 900 python scripts/ab_kernels.py --dtype bfloat16 --kernels auto,torch --rounds 5 \

@@ -23,8 +23,11 @@ Arms (interleaved rounds, best of each; ms per unit over --units units):
              pipelined across units; P > 1: signalled pieces)
 Reported: speedup = serial / arm, the GEMM rate the schedule sustains
 (unit FLOPs / arm time, meaningful where the step is compute-bound), and
-the planner's choice (plan_overlap fed the measured gemm / proxy times)
-with its distance from the best measured arm.
+the planner's choice with its distance from the best measured arm. The
+planner is the production one, ``measured_plan`` (parallel/overlap.py): it
+times the unit's GEMM and one proxy piece per candidate piece count itself,
+exactly as the modes do on their ranks (``plan`` in the record, source
+"measured"); ``plan_model`` is the table-model plan for comparison.
 
     python scripts/overlap_proxy.py [--units 10] [--rounds 3] [--proxy-mib 16 256]
 """
@@ -38,9 +41,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from pytorch_distributed_matmul_benchmark_amd.ops import gemm  # noqa: E402
-from pytorch_distributed_matmul_benchmark_amd.parallel.comm import new_stream  # noqa: E402
+from pytorch_distributed_matmul_benchmark_amd.parallel.comm import CommStream  # noqa: E402
+from pytorch_distributed_matmul_benchmark_amd.parallel.dist import DistContext  # noqa: E402
 from pytorch_distributed_matmul_benchmark_amd.parallel.overlap import (  # noqa: E402
-    OverlapPipeline, compute_ctx, compute_stream, plan_overlap)
+    OverlapPipeline, compute_ctx, compute_stream, measured_plan, plan_overlap)
 
 
 def main():
@@ -61,7 +65,11 @@ def main():
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev)
     n = a.n
-    comm = new_stream(dev, high_priority=True)
+    cstream = CommStream(dev)  # high priority, as the modes' comm stream
+    comm = cstream.stream
+    # the planner's view of the job: 8 ranks (no process group: its MAX over
+    # ranks is this process's own measurement)
+    ctx8 = DistContext(rank=0, world_size=8, local_rank=0, device=dev)
     cur = torch.cuda.current_stream(dev)
 
     def rnd(*shape, seed):
@@ -172,11 +180,16 @@ def main():
                 for name, f in arms.items():
                     best[name] = min(best.get(name, 1e9), timed(f, a.units))
             G, Cp, S = best["gemm"], best["proxy"], best["serial"]
-            # per extra piece: the host's flag wait + one proxy launch (an RCCL call costs more:
-            # plan_overlap's default)
-            plan = plan_overlap(n, ncols, n, torch.bfloat16, 8, "all_gather", 0.0, granule=granule,
-                                steps=a.units, gemm_time_us=G * 1e3, comm_time_us=Cp * 1e3,
-                                piece_us=a.piece_us)
+
+            def probe(s, e):
+                with torch.cuda.stream(comm):
+                    proxy(s, e)
+            plan = measured_plan(units, ctx8, "all_gather", 0.0,
+                                 lambda x, y, o: gemm.matmul(x, y, out=o), probe, steps=a.units,
+                                 compute=cur, comm=cstream, reps=5)
+            model = plan_overlap(n, ncols, n, torch.bfloat16, 8, "all_gather", 0.0, granule=granule,
+                                 steps=a.units, gemm_time_us=G * 1e3, comm_time_us=Cp * 1e3,
+                                 piece_us=a.piece_us)
             arm_best = min((k for k in best if k.startswith("pipe_") and "_cu" not in k),
                            key=lambda k: best[k])
             chosen = f"pipe_{plan.pieces}" if plan.overlap else "serial"
@@ -190,6 +203,7 @@ def main():
                    "tflops_in_schedule": {k: round(flops / v / 1e9, 1) for k, v in best.items()
                                           if k.startswith("pipe_")},
                    "best_arm": arm_best, "planner": chosen, "plan": plan.as_dict(),
+                   "plan_model": model.as_dict(),
                    "planner_vs_best": round(best.get(chosen, S) / best[arm_best], 4)}
             print(json.dumps(rec), flush=True)
             for p in pipes.values():

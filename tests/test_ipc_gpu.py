@@ -1,8 +1,10 @@
-"""xGMI peer-memory primitives (ops/csrc/bindings.cpp ipc_*, parallel/ipc.py) on
-one GPU: an ipc_empty tensor is its own allocation, its handle maps back, and a
-DMA copy out of the mapping is bitwise the source. (Opening a handle in the
-exporting process itself is refused by HIP, so the mapping is opened by a child
-process; the 2-rank pull all-gather runs in tests/test_multirank_gpu.py.)"""
+"""xGMI peer-memory primitives (ops/csrc/bindings.cpp ipc_* / peer_copy /
+reduce_sum_addrs, parallel/ipc.py) on one GPU: an ipc_empty tensor is its own
+allocation, its handle maps back, and a DMA copy out of the mapping is bitwise
+the source; the one-launch multi-peer copy and the by-address sum are bitwise;
+a rank's stream set has no false hardware-queue dependency. (Opening a handle
+in the exporting process itself is refused by HIP, so the mapping is opened by
+a child process; the multi-rank pulls run in tests/test_multirank_gpu.py.)"""
 import os
 import subprocess
 import sys
@@ -47,3 +49,92 @@ def test_ipc_empty_is_its_own_allocation_and_maps_back():
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
     del t
     torch.cuda.synchronize()
+
+
+DEV = torch.device("cuda", 0)
+
+
+def test_peer_copy_one_launch_bitwise():
+    """reduce.hip multi_copy: several copies (odd lengths, an unaligned source,
+    an empty one) in one launch are bitwise the sources, for default and
+    explicit workgroup counts."""
+    m = _native.load(build_if_missing=False)
+    g = torch.Generator(device="cuda").manual_seed(7)
+    lens = [1, 15, 16, 4097, 1 << 20, (3 << 20) + 5, 0]
+    srcs = [torch.randint(0, 256, (n,), dtype=torch.uint8, device=DEV, generator=g) for n in lens]
+    big = torch.randint(0, 256, (1 << 16,), dtype=torch.uint8, device=DEV, generator=g)
+    srcs.append(big[3:])  # a 16-B-unaligned source: the byte path
+    for blocks in (0, 1, 5):
+        dsts = [torch.full((s.numel(),), 0xAB, dtype=torch.uint8, device=DEV) for s in srcs]
+        m.peer_copy(dsts, [s.data_ptr() for s in srcs], blocks)
+        torch.cuda.synchronize()
+        for s, d in zip(srcs, dsts):
+            assert torch.equal(s, d), (blocks, s.numel())
+    with pytest.raises(RuntimeError):
+        m.peer_copy([torch.empty(4, device=DEV)] * (m.MAX_COPIES + 1), [1] * (m.MAX_COPIES + 1), 0)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+def test_reduce_sum_addrs_matches_reduce_sum(dtype):
+    """The fused pull + sum of the peer-memory all-reduce (sources by address)
+    is bitwise the tensor-list reduce_sum, with and without a grid cap."""
+    m = _native.load(build_if_missing=False)
+    g = torch.Generator(device="cuda").manual_seed(11)
+    srcs = [torch.randn(1_000_003, device=DEV, dtype=dtype, generator=g) for _ in range(8)]
+    ref = torch.empty_like(srcs[0])
+    m.reduce_sum(ref, srcs)
+    for blocks in (0, 3):
+        out = torch.empty_like(ref)
+        m.reduce_sum_addrs(out, [s.data_ptr() for s in srcs], blocks)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), blocks
+    want = torch.stack([s.float() for s in srcs]).sum(0)
+    assert torch.allclose(ref.float(), want, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("sdma", [True, False])
+def test_copy_from_peer_kinds_bitwise(sdma):
+    """copy_from_peer: the NoCU (DMA engine) kind and the plain kind copy the same bytes."""
+    m = _native.load(build_if_missing=False)
+    src = torch.randn(3 << 20, device=DEV)
+    dst = torch.zeros_like(src)
+    m.copy_from_peer(dst, src.data_ptr(), sdma)
+    torch.cuda.synchronize()
+    assert torch.equal(src, dst)
+
+
+def test_gate_holds_the_stream_until_released():
+    """ops gemm.SignalSet.gate: the stream stays blocked until the host sets the flag."""
+    import time
+
+    from pytorch_distributed_matmul_benchmark_amd.ops import gemm
+
+    sig = gemm.SignalSet(DEV, 1)
+    st = torch.cuda.Stream(device=DEV)
+    try:
+        with torch.cuda.stream(st):
+            sig.gate(0, 1, timeout_s=20.0)
+        ev = torch.cuda.Event()
+        ev.record(st)
+        time.sleep(0.3)
+        held = not ev.query()
+    finally:
+        sig.set(0, 1)
+    t0 = time.perf_counter()
+    ev.synchronize()
+    assert held and time.perf_counter() - t0 < 10.0
+    sig.close()
+
+
+def test_rank_stream_set_has_no_false_queue_dependency():
+    """A rank's streams under --allgather/--allreduce ipc (kernel engine): the
+    compute stream, the comm stream and ProcessGroupNCCL's internal stream —
+    modelled as a gate stream plus two streams waiting behind it — fit the
+    process's 4 hardware queues: a GEMM on the compute stream completes while
+    the others are blocked (scripts/queue_probe.py, one fresh process; the
+    gate releases itself after a timeout, so this cannot hang)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "queue_probe.py"), "--child", "2",
+                        "kernel"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = __import__("json").loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["gate_was_closed"] and d["free"], d

@@ -14,15 +14,20 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(nproc, script, *args, port=None):
+def _run(nproc, script, *args, port=None, env=None):
     port = port or free_port()
-    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    env = dict(os.environ, PYTHONUNBUFFERED="1", **(env or {}))
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1",
                         f"--master-port={port}", script, "--dist-backend", "gloo", *args],
                        cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     return r.stdout
+
+
+def _records(path):
+    with open(path) as f:
+        return [json.loads(l) for l in f if l.strip()]
 
 
 @pytest.mark.parametrize("mode,extra", [("batch_parallel", []), ("batch_parallel", ["--overlap"]),
@@ -117,3 +122,80 @@ def test_two_ranks_share_gpu_bench_ipc_allgather():
     d = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
     for key in ("matrix_parallel", "matrix_parallel+overlap", "batch_parallel", "batch_parallel+overlap"):
         assert d["modes"][key] and d["modes"][key]["value"] > 0, key
+
+
+# ---- the overlap checks can fail (negative control) ---------------------------
+@pytest.mark.parametrize("gather", ["rccl", "direct", "ipc"])
+@pytest.mark.parametrize("chunks", ["1", "2"])
+def test_two_ranks_overlap_check_catches_a_skipped_wait(gather, chunks, tmp_path):
+    """matrix_parallel --overlap --check gives every unit its own product
+    (B x 2^(k mod 3)) and checks each gathered piece of the last two units
+    against its own unit: it PASSes as built and FAILs when the collectives are
+    issued without their producer dependency (PDMB_TEST_SKIP_READY_WAIT), for
+    the RCCL-shaped (here gloo), direct and ipc all-gathers, whole and
+    signalled pieces (8192: two 256-workgroup rounds per shard GEMM)."""
+    args = ["--sizes", "8192", "--iterations", "3", "--warmup", "1", "--mode", "matrix_parallel",
+            "--overlap", "--chunks", chunks, "--check", "--allgather", gather]
+    good = tmp_path / "good.jsonl"
+    out = _run(2, "matmul_scaling_benchmark.py", *args, "--json", str(good))
+    assert "PASS" in out and "FAIL" not in out and "ERROR" not in out
+    rec = _records(good)[-1]
+    assert rec["plan"]["source"] == "measured"
+    assert rec["signalled"] == (chunks == "2"), rec["plan"]
+    assert len(rec["checked_units"]) == 2
+    out = _run(2, "matmul_scaling_benchmark.py", *args,
+               env={"PDMB_TEST_SKIP_READY_WAIT": "20000000"})
+    assert "FAIL" in out and "ERROR" not in out
+
+
+# ---- the ws = 8 job shapes on real HIP (8 gloo ranks sharing the GPU) ---------
+def _bench8(*extra):
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "8", "--dist-backend", "gloo",
+                        "--size", "4096", "--steps", "3", "--warmup", "1", "--extra-steps", "2",
+                        "--extra-warmup", "1", *extra], cwd=ROOT, capture_output=True,
+                       text=True, timeout=900, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == 8 and d["world_size_seen"] == 8 and d["value"] > 0
+    assert d["collectives_verified"] is True and "modes_incomplete" not in d
+    for key, m in d["modes"].items():
+        assert m and "error" not in m and m["value"] > 0, (key, m)
+    return d
+
+
+@pytest.mark.parametrize("extra", [[], ["--allgather", "ipc", "--allreduce", "ipc"],
+                                   ["--mode", "matrix_parallel", "--overlap", "--chunks", "2",
+                                    "--allgather", "ipc"]])
+def test_eight_ranks_self_launch_bench(extra):
+    """bench.py --gpus 8 through the self-launch path, the BASELINE ws = 8
+    shapes (local batch 1 with a two-slot ring, 512-column shards at 4096):
+    every mode runs, with measured overlap plans."""
+    d = _bench8(*extra)
+    plans = [m["plan"] for m in d["modes"].values() if m.get("plan")]
+    plans += [d["config"]["overlap_plan"]] if "overlap_plan" in d["config"] else []
+    assert plans and all(p["source"] == "measured" for p in plans), plans
+
+
+@pytest.mark.parametrize("mode,size,extra", [
+    ("matrix_parallel", "16384", ["--allgather", "ipc", "--chunks", "2"]),
+    ("matrix_parallel", "4096", []),
+    ("batch_parallel", "8192", ["--chunks", "2"]),
+    ("batch_parallel", "8192", ["--allreduce", "ipc", "--chunks", "2"])])
+def test_eight_ranks_scaling_overlap_checked(mode, size, extra, tmp_path):
+    """matmul_scaling_benchmark.py at 8 ranks, overlapped and checked against
+    float64: at 16384 / 8192 the unit GEMM spans two or more 256-workgroup
+    rounds, so --chunks 2 runs signalled pieces; ipc maps all 7 peers."""
+    js = tmp_path / "r.jsonl"
+    out = _run(8, "matmul_scaling_benchmark.py", "--sizes", size, "--iterations", "2", "--warmup", "1",
+               "--mode", mode, "--overlap", "--check", *extra, "--json", str(js))
+    assert "Collective operations verified successfully across 8 GPUs" in out
+    assert "PASS" in out and "FAIL" not in out and "ERROR" not in out
+    rec = _records(js)[-1]
+    assert rec["plan"]["source"] == "measured"
+    if "--chunks" in extra:
+        assert rec["signalled"] is True and rec["pieces"] == 2, rec["plan"]
+    if "ipc" in extra:
+        assert rec["ipc_peers"] == 7

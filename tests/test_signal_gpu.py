@@ -115,17 +115,18 @@ def test_handoff_consumer_sees_finished_pieces_under_load():
         sig.close()
 
 
-@pytest.mark.parametrize("pieces", [1, 2, 4])
-def test_pipeline_with_proxy_collective(pieces):
-    """OverlapPipeline over a 2-slot ring with a copy kernel as the 'collective':
-    every unit's copy holds that unit's finished GEMM, for whole and signalled pieces."""
+def _proxy_pipeline(pieces, steps=5):
+    """OverlapPipeline over a 2-slot ring with a copy kernel as the 'collective'
+    and a distinct A per unit (the operands hook): returns, per ring slot, the
+    unit that last wrote it, its GEMM output, its copy and that unit's product."""
     m, n, k = 8192, 4096, 2048
-    A, B = _ints(m, k, seed=9), _ints(k, n, seed=10)
-    units = [(A, B, torch.empty(m, n, device=DEV, dtype=torch.bfloat16)) for _ in range(2)]
+    As = [_ints(m, k, seed=100 + i) for i in range(steps)]
+    B = _ints(k, n, seed=10)
+    units = [(As[0], B, torch.empty(m, n, device=DEV, dtype=torch.bfloat16)) for _ in range(2)]
     copies = [torch.zeros(m, n, device=DEV, dtype=torch.bfloat16) for _ in range(2)]
     comm = torch.cuda.Stream(device=DEV, priority=-1)
     with gemm.shared_device():
-        granule = gemm.signal_granule(A, B, units[0][2])
+        granule = gemm.signal_granule(As[0], B, units[0][2])
     plan = plan_overlap(m, n, k, torch.bfloat16, 8, "all_gather", 0.0, granule=granule,
                         requested=pieces, gemm_time_us=1.0, comm_time_us=1.0)
     issued = []
@@ -140,16 +141,45 @@ def test_pipeline_with_proxy_collective(pieces):
         issued.append((r, p, s, e))
 
     pipe = OverlapPipeline(lambda x, y, o: gemm.matmul(x, y, out=o), units, coll, DEV, plan,
-                           per_step=1, compute=torch.cuda.current_stream(DEV))
+                           per_step=1, compute=torch.cuda.current_stream(DEV),
+                           operands=lambda i: (As[i], B))
     try:
         assert pipe.signalled == (pieces > 1 and plan.pieces > 1)
-        for _ in range(5):
+        for _ in range(steps):
             pipe.step()
         pipe.finish()
         torch.cuda.synchronize()
-        R = (A.double() @ B.double()).to(torch.bfloat16)
+        assert len(issued) == steps * len(pipe.pieces)
+        out = []
         for r in range(2):
-            assert torch.equal(units[r][2], R) and torch.equal(copies[r], R)
-        assert len(issued) == 5 * len(pipe.pieces)
+            u = pipe.slot_unit[r]
+            R = (As[u].double() @ B.double()).to(torch.bfloat16)
+            out.append((u, units[r][2], copies[r], R))
+        return out, pipe.signalled
     finally:
         pipe.close()
+
+
+@pytest.mark.parametrize("pieces", [1, 2, 4])
+def test_pipeline_with_proxy_collective(pieces):
+    """Every unit has its own product; after the run each ring slot holds the
+    last unit that wrote it (units 3 and 4 of 5), and the 'collective' copied
+    exactly that unit's finished GEMM — whole and signalled pieces."""
+    slots, _ = _proxy_pipeline(pieces)
+    assert sorted(u for u, *_ in slots) == [3, 4]
+    for u, out, copy, R in slots:
+        assert torch.equal(out, R), u
+        assert torch.equal(copy, R), u
+
+
+@pytest.mark.parametrize("pieces", [1, 2])
+def test_pipeline_negative_control_catches_a_skipped_wait(pieces, monkeypatch):
+    """Negative control for the check above: with the producer dependency
+    removed (PDMB_TEST_SKIP_READY_WAIT: no ready event, no signal wait, each
+    GEMM delayed on the compute stream) the copies read the slots' previous
+    units, and the same comparison fails."""
+    monkeypatch.setenv("PDMB_TEST_SKIP_READY_WAIT", "20000000")
+    slots, _ = _proxy_pipeline(pieces)
+    assert any(not torch.equal(copy, R) for u, out, copy, R in slots)
+    for u, out, copy, R in slots:
+        assert torch.equal(out, R), u  # the GEMMs themselves are still right
