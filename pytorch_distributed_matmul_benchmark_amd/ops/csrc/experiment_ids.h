@@ -1,0 +1,49 @@
+// Experiment / diagnostic kernel ids (A/B arms and timing-only builds behind
+// the profiles/ tables, docs/REPRODUCE.md). Accepted only by a library built
+// with PDMB_EXPERIMENTS=1 (ops/build.py; ops/gemm.py EXPERIMENT_KERNELS); the
+// dispatch for them is experiments.h.
+#pragma once
+
+namespace pdmb {
+
+enum ExperimentKernel : int {
+  kMfma256 = 1,       // SCHED 0 (ping-pong)
+  kMfma256b = 3,      // SCHED 1: DMA issued in the read slot
+  kMfma256c = 4,      // SCHED 2: fragment reads balanced over the read slots
+  kMfma256Stamp = 5,  // SCHED 2 with in-kernel barrier-wait stamps (needs a debug buffer)
+  kF32_256 = 6,       // exact-fp32 256x256 without the staggered DMA
+  kMfma256X1 = 10,    // SCHED 2 + per-cluster setprio
+  kMfma256X2 = 11,    // SCHED 2 + static priority of waves 4..7
+  kMfma256X4 = 13,    // SCHED 2 + XCD sub-block 8x4
+  kFp8 = 15,          // fp8 8-wave 256x256 (block-scaled MFMA 16x16x128)
+  kFp8W4Diag = 17,    // timing only (wrong results): kFp8W4 without the DMA wait
+  kFp8W4Diag2 = 18,   // timing only: no wait at all before the barrier
+  kFp8W4Diag3 = 19,   // timing only: MFMAs + barriers, no loads
+  kF32NoDma = 20,     // timing only: f32 K-loop without loads
+  kMfmaW4Tall = 22,   // kMfmaW4 (bf16) with the 8x4 XCD sub-block
+  kMfmaW4Wide = 23,   // kMfmaW4 (bf16) with the 2x16 XCD sub-block
+  kFp8W4Tall = 24,    // kFp8W4 with the 8x4 XCD sub-block
+  kFp8W4Wide = 25,    // kFp8W4 with the 2x16 XCD sub-block
+  kFp8W4Scaled = 31,  // kFp8W4 on the block-scaled MFMA form (scales 1)
+  kMfmaW4Trace = 32,  // kMfmaW4 (bf16) writing the tile timeline into the debug buffer
+  kFp8W4Trace = 33,   // kFp8W4 writing the tile timeline into the debug buffer
+  kMfmaW4Pers = 34,   // persistent W4 (one workgroup per CU, per-XCD work queues)
+  kMfmaW4PersTrace = 35,  // kMfmaW4Pers writing the tile timeline
+  kMfmaW4STrace = 38,  // W4S writing per-workgroup start / end stamps
+  kMfmaW4SRot = 39,    // W4S with the per-round rotating XCD block map (supertile 6)
+  kMfmaW4SRotTrace = 40,  // kMfmaW4SRot with per-workgroup start / end stamps
+  kMfmaW4Il32 = 30,   // kMfmaW4 (bf16) with the 8-wave kernel's 32-column B-half interleave
+  kFp8W4TS = 43,      // kFp8W4 with plain (temporal) C stores (shipping: non-temporal)
+  kFp8W4STS = 44,     // kFp8W4S with plain C stores
+  kMfmaW4STS = 45,    // kMfmaW4S (bf16) with plain C stores
+  kF32_256sDirect = 46,  // kF32_256s with direct (not LDS-staged, temporal) C stores
+  kFp8W4Unfused = 47,    // kFp8W4 with the epilogue after (not inside) the last K-tile
+  kT128Unfused = 48,     // kT128 (bf16 / fp16) with the epilogue after the last K-tile
+  kFp8T128Unfused = 49,  // kFp8T128 with the epilogue after the last K-tile
+  kMfmaW4Unfused = 50,   // kMfmaW4 (bf16) with the epilogue after the last K-tile
+  kF32T128B32 = 52,      // kF32T128 with one b32 LDS read per B operand (round 3's first version)
+  kF32W4B32 = 54,        // kF32W4 with one b32 LDS read per B operand (round 2's version)
+  kF32_256p = 55,        // kF32_256s with software-pipelined fragments and a mid-tile barrier
+};
+
+}  // namespace pdmb

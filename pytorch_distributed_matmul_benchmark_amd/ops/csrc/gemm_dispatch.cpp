@@ -16,6 +16,9 @@
 
 #include "api.h"
 #include "common.h"
+#ifdef PDMB_EXPERIMENTS
+#include "experiment_ids.h"
+#endif
 
 namespace pdmb {
 
@@ -91,26 +94,31 @@ bool experiments_built() {
 #endif
 }
 
-static bool is_fp8_kernel(int k) {
-  return k == kFp8W4 || k == kFp8W4S || k == kFp8T128 || k == kFp8T256x128 || k == kFp8 || k == kFp8W4TS ||
-         k == kFp8W4STS || k == kFp8W4Unfused || k == kFp8T128Unfused || k == kFp8W4Diag || k == kFp8W4Diag2 || k == kFp8W4Diag3 ||
-         k == kFp8W4Tall || k == kFp8W4Wide || k == kFp8W4Scaled || k == kFp8W4Trace;
+// Experiment / diagnostic kernels (experiments.h): every id, its resolution,
+// workspace, launch and name, compiled only into a PDMB_EXPERIMENTS=1 build;
+// the shipping build sees stubs that refuse every non-shipping id.
+#ifdef PDMB_EXPERIMENTS
+static bool is_experiment(int k);
+static bool experiment_is_fp8(int k);
+static int experiment_resolve_fp8(const Problem& p, int kernel, bool s_fits);
+static int experiment_resolve(const Problem& p, int kernel, bool fast, bool w4, bool t128, bool f32fast);
+static size_t experiment_workspace_bytes(const Problem& p, int k);
+static hipError_t experiment_launch(const Problem& p, int k, const GemmArgs& a, hipStream_t stream);
+static const char* experiment_name(int k);
+#else
+static bool is_experiment(int) { return false; }
+static bool experiment_is_fp8(int) { return false; }
+static int experiment_resolve_fp8(const Problem&, int, bool) { return -1; }
+static int experiment_resolve(const Problem&, int, bool, bool, bool, bool) { return -1; }
+static size_t experiment_workspace_bytes(const Problem&, int) { return 0; }
+static hipError_t experiment_launch(const Problem&, int, const GemmArgs&, hipStream_t) {
+  return hipErrorInvalidValue;
 }
+static const char* experiment_name(int) { return "auto"; }
+#endif
 
-static bool is_experiment(int k) {
-  switch (k) {
-    case kMfma256: case kMfma256b: case kMfma256c: case kMfma256Stamp: case kF32_256:
-    case kMfma256X1: case kMfma256X2: case kMfma256X4: case kFp8: case kFp8W4Diag:
-    case kFp8W4Diag2: case kFp8W4Diag3: case kF32NoDma: case kMfmaW4Tall: case kMfmaW4Wide: case kMfmaW4Il32:
-    case kMfmaW4Pers: case kMfmaW4PersTrace: case kMfmaW4STrace: case kMfmaW4SRot: case kMfmaW4SRotTrace:
-    case kFp8W4Tall: case kFp8W4Wide: case kFp8W4Scaled: case kFp8W4Trace: case kMfmaW4Trace:
-    case kFp8W4TS: case kFp8W4STS: case kMfmaW4STS: case kF32_256sDirect: case kFp8W4Unfused:
-    case kT128Unfused: case kFp8T128Unfused: case kMfmaW4Unfused: case kF32T128B32:
-    case kF32W4B32: case kF32_256p:
-      return true;
-    default:
-      return false;
-  }
+static bool is_fp8_kernel(int k) {
+  return k == kFp8W4 || k == kFp8W4S || k == kFp8T128 || k == kFp8T256x128 || experiment_is_fp8(k);
 }
 
 static int device_cus();
@@ -135,9 +143,9 @@ int resolve_kernel(const Problem& p, int kernel) {
         !gemm_fp8_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C))
       return -1;
     const bool s_fits = gemm_fp8_w4s_fits(a) && device_cus() % 8 == 0;
-    if (kernel == kFp8W4S || kernel == kFp8W4STS) return s_fits ? kernel : -1;
+    if (kernel == kFp8W4S) return s_fits ? kernel : -1;
     if (kernel == kFp8T128 || kernel == kFp8T256x128) return supports(p, kernel) ? kernel : -1;
-    if (kernel == kFp8T128Unfused) return supports(p, kFp8T128) ? kernel : -1;
+    if (is_experiment(kernel)) return experiment_resolve_fp8(p, kernel, s_fits);
     if (kernel != kAuto) return kernel;
     // the streaming kernel on a device of its own with >= 2 tiles per CU (as W4S)
     const long long T = (long long)(p.M / 256) * (p.N / 256) * (p.batch < 1 ? 1 : p.batch);
@@ -185,23 +193,8 @@ int resolve_kernel(const Problem& p, int kernel) {
     case kF32W4: return f32fast ? kF32W4 : -1;  // same constraints as f32_256
     case kF32T128: return p.dtype == kF32 && supports(p, kF32T128) ? kF32T128 : -1;
     case kF32T128x2: return p.dtype == kF32 && supports(p, kF32T128) ? kF32T128x2 : -1;
-#ifdef PDMB_EXPERIMENTS
-    case kF32_256: case kF32NoDma: case kF32_256sDirect: case kF32_256p: return f32fast ? kernel : -1;
-    case kT128Unfused: return t128 ? kernel : -1;
-    case kF32T128B32: return p.dtype == kF32 && supports(p, kF32T128) ? kernel : -1;
-    case kF32W4B32: return f32fast ? kernel : -1;
-    case kMfmaW4Unfused: return (p.dtype == kBF16 && w4) ? kernel : -1;
-    case kMfma256: case kMfma256b: case kMfma256c: return fast ? kernel : -1;
-    case kMfma256X1: case kMfma256X2: case kMfma256X4: case kMfma256Stamp:
-      return (fast && p.dtype == kBF16) ? kernel : -1;
-    case kMfmaW4Tall: case kMfmaW4Wide: case kMfmaW4Il32: case kMfmaW4Trace:
-    case kMfmaW4PersTrace:
-      return (p.dtype == kBF16 && w4) ? kernel : -1;
-    case kMfmaW4STrace: case kMfmaW4SRot: case kMfmaW4SRotTrace: case kMfmaW4STS:
-      return (p.dtype == kBF16 && w4 && w4s_fits(p)) ? kernel : -1;
-    case kMfmaW4Pers: return w4 ? kernel : -1;  // bf16 and fp16
-#endif
-    default: return -1;
+    default:
+      return is_experiment(kernel) ? experiment_resolve(p, kernel, fast, w4, t128, f32fast) : -1;
   }
 }
 
@@ -831,12 +824,7 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel) {
   if (t.m1 > 0) return splitk_bytes(tail_part(p, t), tail_kernel(p), t.S);  // the first launch is unsplit
   if (is_tiled(k)) return splitk_bytes(p, k, plan(p, k).splitk);
   if (k == kFp8W4) return fp8_split_bytes(p, fp8_split(p));
-  if (k == kMfmaW4Tall || k == kMfmaW4Wide || k == kMfmaW4Il32 || k == kMfmaW4Trace ||
-      k == kMfmaW4Pers || k == kMfmaW4PersTrace)
-    return splitk_bytes(p, kMfmaW4, plan(p, kMfmaW4).splitk);
-  if (k == kF32T128B32) return splitk_bytes(p, kF32T128, plan(p, kF32T128).splitk);
-  if (k == kF32W4B32) return splitk_bytes(p, kF32W4, plan(p, kF32W4).splitk);
-  return 0;
+  return is_experiment(k) ? experiment_workspace_bytes(p, k) : 0;
 }
 
 // The two launches of a tail plan; false: run the problem as one launch (the
@@ -1012,49 +1000,9 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kF32W4:
     case kF32T128: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream);
     case kF32T128x2: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream, 2);
-#ifdef PDMB_EXPERIMENTS
-    case kFp8: return gemm_fp8_launch(a, 0, stream);
-    case kFp8W4Diag: return gemm_fp8_launch(a, 9, stream);
-    case kFp8W4Diag2: return gemm_fp8_launch(a, 10, stream);
-    case kFp8W4Diag3: return gemm_fp8_launch(a, 11, stream);
-    case kFp8W4Tall: return gemm_fp8_launch(a, 12, stream);
-    case kFp8W4Wide: return gemm_fp8_launch(a, 13, stream);
-    case kFp8W4Scaled: return gemm_fp8_launch(a, 14, stream);
-    case kFp8W4Trace: return gemm_fp8_launch(a, 15, stream);
-    case kFp8W4TS: return gemm_fp8_launch(a, 16, stream);
-    case kFp8W4Unfused: return gemm_fp8_launch(a, 18, stream);
-    case kT128Unfused:
-    case kFp8T128Unfused: return gemm_tile_launch(k, p.dtype, a, stream);  // unsplit (A/B)
-    case kMfmaW4Unfused: return gemm_w4_launch(p.dtype, a, stream, 12);   // unsplit (A/B)
-    case kFp8W4STS: {
-      GemmArgs s = a;
-      s.pers_grid = ((p.cus > 0 ? p.cus : device_cus()) / 8) * 8;
-      return gemm_fp8_launch(s, 17, stream);
-    }
-    case kMfmaW4STS: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 11);
-    case kMfma256: return gemm256_launch(p.dtype, a, 0, stream);
-    case kMfma256b: return gemm256_launch(p.dtype, a, 1, stream);
-    case kMfma256c: return gemm256_launch(p.dtype, a, 2, stream);
-    case kMfma256Stamp: return gemm256_launch(p.dtype, a, 3, stream);
-    case kMfmaW4Tall: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 1);
-    case kMfmaW4Wide: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 2);
-    case kMfmaW4Il32: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 3);
-    case kMfmaW4Trace: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 4);
-    case kMfmaW4Pers: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 5);
-    case kMfmaW4PersTrace: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 6);
-    case kMfmaW4STrace: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 8);
-    case kMfmaW4SRot: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 9);
-    case kMfmaW4SRotTrace: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 10);
-    case kF32_256: return gemm_f32_256_launch(a, 0, stream);
-    case kF32NoDma: return gemm_f32_256_launch(a, 9, stream);
-    case kF32_256sDirect: return gemm_f32_256_launch(a, 10, stream);
-    case kF32_256p: return gemm_f32_256_launch(a, 11, stream);
-    case kF32T128B32: return tiled_launch(p, kF32T128, a, p.workspace, p.workspace_bytes, stream, 1);
-    case kF32W4B32: return tiled_launch(p, kF32W4, a, p.workspace, p.workspace_bytes, stream, 1);
-    case kMfma256X1: case kMfma256X2: case kMfma256X4:
-      return gemm256_launch(p.dtype, a, 10 + (k - kMfma256X1 + 1), stream);
-#endif
-    default: return gemm_generic_launch(p.dtype, a, generic_vec_ok(p), stream);
+    default:
+      if (is_experiment(k)) return experiment_launch(p, k, a, stream);
+      return gemm_generic_launch(p.dtype, a, generic_vec_ok(p), stream);
   }
 }
 
@@ -1199,39 +1147,13 @@ const char* kernel_name(int kernel) {
     case kT256x128: return "pdmb_t256x128_nn";
     case kF32W4: return "pdmb_f32_w4_nn";
     case kF32T128: return "pdmb_f32_t128_nn";
-    case kMfma256: return "pdmb_mfma256_nn";
-    case kMfma256b: return "pdmb_mfma256b_nn";
-    case kMfma256c: return "pdmb_mfma256c_nn";
-    case kMfma256Stamp: return "pdmb_mfma256c_stamp";
-    case kF32_256: return "pdmb_f32_256_nn";
-    case kFp8: return "pdmb_fp8_256_nt";
-    case kMfmaW4Tall: return "pdmb_w4_nn_tall";
-    case kMfmaW4Wide: return "pdmb_w4_nn_wide";
-    case kMfmaW4Il32: return "pdmb_w4_nn_il32";
-    case kFp8W4Tall: return "pdmb_fp8_w4_nt_tall";
-    case kFp8W4Wide: return "pdmb_fp8_w4_nt_wide";
-    case kFp8W4Scaled: return "pdmb_fp8_w4_nt_scaled";
-    case kMfmaW4Trace: return "pdmb_w4_nn_trace";
-    case kMfmaW4Pers: return "pdmb_w4_pers";
-    case kMfmaW4PersTrace: return "pdmb_w4_pers_trace";
-    case kMfmaW4STrace: return "pdmb_w4s_trace";
-    case kMfmaW4SRot: return "pdmb_w4s_rot";
-    case kMfmaW4SRotTrace: return "pdmb_w4s_rot_trace";
-    case kFp8W4TS: return "pdmb_fp8_w4_nt_tstore";
-    case kFp8W4STS: return "pdmb_fp8_w4s_tstore";
-    case kMfmaW4STS: return "pdmb_w4s_tstore";
-    case kF32_256sDirect: return "pdmb_f32_256s_direct";
-    case kF32_256p: return "pdmb_f32_256p_nn";
-    case kFp8W4Unfused: return "pdmb_fp8_w4_nt_unfused";
-    case kT128Unfused: return "pdmb_t128_nn_unfused";
-    case kFp8T128Unfused: return "pdmb_fp8_t128_nt_unfused";
-    case kMfmaW4Unfused: return "pdmb_w4_nn_unfused";
-    case kF32T128B32: return "pdmb_f32_t128_b32";
     case kF32T128x2: return "pdmb_f32_t128x2_nn";
-    case kF32W4B32: return "pdmb_f32_w4_b32";
-    case kFp8W4Trace: return "pdmb_fp8_w4_nt_trace";
-    default: return "auto";
+    default: return is_experiment(kernel) ? experiment_name(kernel) : "auto";
   }
 }
+
+#ifdef PDMB_EXPERIMENTS
+#include "experiments.h"
+#endif
 
 }  // namespace pdmb

@@ -51,6 +51,9 @@
 // tiles masked at the store), K % 64 == 0 (fp8: K % 128), lda / ldb % 8 == 0
 // (fp8: % 16), ldc % 4 == 0, 16-B aligned A / B, 8-B aligned C.
 #include "api.h"
+#ifdef PDMB_EXPERIMENTS
+#include "experiment_ids.h"
+#endif
 #include "common.h"
 #include "splitk.h"
 
@@ -575,8 +578,11 @@ bool gemm_tile_supported(int dt, int bm, const GemmArgs& a, size_t align_a, size
 
 // kernel: kT128 | kT128x2 | kT256x128 (bf16 / fp16), kFp8T128 | kFp8T256x128 (fp8)
 hipError_t gemm_tile_launch(int kernel, int dt, GemmArgs a, hipStream_t stream) {
-  if ((dt == kFP8) != (kernel == kFp8T128 || kernel == kFp8T256x128 || kernel == kFp8T128Unfused))
-    return hipErrorInvalidValue;
+  bool fp8 = kernel == kFp8T128 || kernel == kFp8T256x128;
+#ifdef PDMB_EXPERIMENTS
+  fp8 = fp8 || kernel == kFp8T128Unfused;
+#endif
+  if ((dt == kFP8) != fp8) return hipErrorInvalidValue;
   switch (kernel) {
 #ifdef PDMB_EXPERIMENTS
     case kT128Unfused: return ktile::launch<ktile::CfgT128, false>(dt, a, stream);

@@ -12,8 +12,10 @@
 # native16k (pdmb_bench bf16 / fp8 at 16k), overlap_proxy, rocprof_bench, selflaunch2,
 # selflaunch4, gpus2_refused (bench.py --gpus 2 on a 1-GPU box must exit 2 at once),
 # ab_bf16 / ab_fp32 / ab_fp8 (auto vs hipBLASLt A/B tables), final_table (auto vs
-# hipBLASLt, every dtype at 4k / 8k / 16k), reduce_bench (reduce_sum bandwidth), ldc_probe (output row pitch vs GEMM time,
-# scripts/ldc_probe.py), pmc (PMC passes: scripts/gpu_pmc.sh with
+# hipBLASLt, every dtype at 4k / 8k / 16k), reduce_bench (reduce_sum bandwidth), queue_probe (hardware-queue
+# false dependencies, scripts/queue_probe.py), selflaunch8 / selflaunch8_ipc / selflaunch8_chunks
+# (bench.py --gpus 8 on one GPU over gloo), mask_probe (CU-mask placement at W4S occupancy,
+# runtime/cu_mask_probe), pmc (PMC passes: scripts/gpu_pmc.sh with
 # N / KS / DT from the environment). After "--": one ad-hoc step NAME with a SECONDS limit.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -83,8 +85,6 @@ run_stage() {
                       --kernels auto,f32_t128:1,f32_t128:2,f32_t128:4,f32_t128x2:1,f32_t128x2:2,f32_t128x2:4,torch \
                       --shapes 4096,512,4096 4096,1024,4096 2048,2048,2048 4096,2048,4096 8192,1024,8192 &&
                     grep '^{' "$OUT/ab_fp32_shards.log" > "$OUT/ab_fp32_shards.jsonl" ;;
-    splitk_prefetch) step splitk_prefetch 600 python scripts/splitk_prefetch_ab.py &&
-                     grep '^{' "$OUT/splitk_prefetch.log" > "$OUT/splitk_prefetch.jsonl" ;;
     cli) step cli_basic 400 ./run_benchmark.sh 1 bfloat16 --check &&
          step cli_batch 400 ./run_scaling_benchmark.sh 1 batch_parallel bfloat16 --overlap --check &&
          step cli_matrix 400 ./run_scaling_benchmark.sh 1 matrix_parallel bfloat16 --overlap --check &&
@@ -102,13 +102,17 @@ run_stage() {
     tests_fp8) step tests_fp8 600 $PYT tests/test_fp8_gpu.py -m gpu ;;
     tests_comm) step tests_comm 1000 $PYT tests/test_ipc_gpu.py tests/test_reduce_gpu.py \
                   tests/test_multirank_gpu.py tests/test_native_bench_gpu.py -m gpu ;;
+    mask_probe) P=pytorch_distributed_matmul_benchmark_amd/runtime/cu_mask_probe
+                for k in 0 8 16 32; do
+                  for occ in "--threads 64 --lds 0" "--threads 256 --lds 147968"; do
+                    step mask_probe_k${k}_${occ// /} 60 $P --exclude $k --blocks $((256 - k)) $occ || return $?
+                    cat "$OUT/mask_probe_k${k}_${occ// /}.log" >> "$OUT/mask_probe.jsonl"
+                  done
+                done ;;
+    queue_probe) step queue_probe 300 python scripts/queue_probe.py &&
+                 grep '^{' "$OUT/queue_probe.log" > "$OUT/queue_probe.jsonl" ;;
     reduce_bench) step reduce_bench 300 python scripts/reduce_bench.py &&
                   grep '^{' "$OUT/reduce_bench.log" > "$OUT/reduce_bench.jsonl" ;;
-    ldc_probe) step ldc_fp8 600 python scripts/ldc_probe.py --dtype float8_e4m3fn &&
-               grep '^{' "$OUT/ldc_fp8.log" > "$OUT/ldc_fp8.jsonl" &&
-               step ldc_bf16 600 python scripts/ldc_probe.py --dtype bfloat16 \
-                 --shapes 8192,2048,8192 4096,4096,4096 2048,8192,8192 16384,2048,16384 &&
-               grep '^{' "$OUT/ldc_bf16.log" > "$OUT/ldc_bf16.jsonl" ;;
     *) echo "unknown stage $1"; return 2 ;;
   esac
 }
