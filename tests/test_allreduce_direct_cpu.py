@@ -154,3 +154,31 @@ def test_batch_parallel_ipc_allreduce_cpu_falls_back_to_direct(extra):
                     "--iterations", "2", "--warmup", "1", "--dtype", "float32", "--mode",
                     "batch_parallel", "--allreduce", "ipc", "--check", *extra)
     assert "PASS" in out and "FAIL" not in out and "ERROR" not in out
+
+
+def test_backup_modes_ipc_allreduce_cli():
+    """--allreduce ipc on the backup data_parallel and overlap family (ADVICE r3:
+    data_parallel and overlap depth 1 built no comm object for ipc and raised;
+    overlap depth > 1 silently ran RCCL): on CPU tensors the direct exchange
+    stands in, every mode PASSes its check."""
+    out = _torchrun(2, "backup/matmul_distributed_benchmark.py", "--device", "cpu", "--sizes", "160",
+                    "--iterations", "2", "--warmup", "1", "--dtype", "float32", "--mode",
+                    "data_parallel", "--allreduce", "ipc", "--check")
+    assert "PASS" in out and "FAIL" not in out and "ERROR" not in out
+    for mode in ("no_overlap", "overlap", "pipeline"):
+        out = _torchrun(2, "backup/matmul_overlap_benchmark.py", "--device", "cpu", "--sizes", "160",
+                        "--iterations", "3", "--warmup", "1", "--dtype", "float32", "--mode", mode,
+                        "--allreduce", "ipc", "--check")
+        assert "PASS" in out and "FAIL" not in out and "ERROR" not in out, mode
+
+
+def test_overlap_ipc_allreduce_uses_the_peer_path():
+    """models/overlap.py with --allreduce ipc picks the peer-memory / direct
+    reduce, never RCCL's (reduce_fn on the comm object make_gatherer built)."""
+    import inspect
+
+    from pytorch_distributed_matmul_benchmark_amd.models import data_parallel, overlap
+
+    src = inspect.getsource(overlap.run)
+    assert "reduce_fn(w.allreduce, comm)" in src and "cs.all_reduce_direct if" not in src
+    assert "make_gatherer(w.allreduce" in inspect.getsource(data_parallel.run)

@@ -35,6 +35,8 @@ def test_bench_two_ranks(mode, extra, scaling, gb):
     d = _bench(2, "--size", "256", "--steps", "3", "--warmup", "1", "--mode", mode, *extra)
     for k in KEYS:
         assert k in d, k
+    if "--overlap" in extra:
+        assert d["config"]["overlap_plan"]["source"] == "measured"
     assert d["n_gpus"] == 2 and d["steps"] == 3 and d["warmup"] == 1
     assert d["scaling"] == scaling and d["config"]["global_batch"] == gb
     assert d["value"] > 0 and d["ms_per_step"] > 0 and d["higher_is_better"] is True
@@ -98,7 +100,11 @@ def test_bench_eight_ranks_driver_form():
         assert m["value"] == pytest.approx(2.0 * 128 ** 3 * gb / (m["ms_per_step"] / 1e3) / 1e12,
                                            rel=0.02, abs=1e-4)
         if key.endswith("+overlap"):
-            assert "plan" in m, key
+            # priced from the job's own measured GEMM / collective times (MAX over ranks)
+            plan = m["plan"]
+            assert plan["source"] == "measured", (key, plan)
+            assert plan["comm_us"] == plan["piece_us"]["1"] > 0 and plan["gemm_us"] > 0
+            assert plan["serial_us"] == pytest.approx(plan["gemm_us"] + plan["comm_us"], abs=0.2)
 
 
 def _plain(*args, env_extra=None, timeout=300):

@@ -117,3 +117,56 @@ def test_overlap_entry_points_use_the_pipeline():
         src = inspect.getsource(mod)
         assert "OverlapPipeline(" in src
         assert "GatherOverlap" not in src and "ReduceOverlap" not in src
+
+
+def test_measured_plan_prices_the_job_from_its_own_times():
+    """measured_plan (what bench.py and the modes call) times the unit's GEMM
+    and one collective per candidate piece count itself: the plan carries
+    those numbers (source "measured"), serial = G + C(1), and the choice
+    follows them — a slow collective is overlapped, a free one serialized."""
+    import time
+
+    from pytorch_distributed_matmul_benchmark_amd.parallel.dist import DistContext
+
+    m = 64
+    A = torch.randn(m, m)
+    units = [(A, A, torch.empty(m, m)) for _ in range(2)]
+    ctx = DistContext(rank=0, world_size=2, local_rank=0, device=torch.device("cpu"))
+
+    def mm(x, y, out):
+        time.sleep(0.004)
+        torch.matmul(x, y, out=out)
+
+    calls = []
+
+    def slow_coll(s, e):
+        calls.append((s, e))
+        time.sleep(0.006)
+
+    p = O.measured_plan(units, ctx, "all_reduce", m * m * 4, mm, slow_coll, steps=10)
+    assert p.source == "measured" and set(p.piece_us) == {1}
+    assert 3500 < p.gemm_us < 40000 and 5000 < p.comm_us < 60000
+    assert p.comm_us == p.piece_us[1] and p.serial_us == pytest.approx(p.gemm_us + p.comm_us)
+    assert p.overlap and calls and all(c == (0, m) for c in calls)
+    free = O.measured_plan(units, ctx, "all_reduce", m * m * 4, mm, lambda s, e: None, steps=10)
+    assert free.source == "measured" and not free.overlap
+
+    def broken(s, e):
+        raise RuntimeError("collective unavailable")
+
+    model = O.measured_plan(units, ctx, "all_reduce", m * m * 4, mm, broken, steps=10)
+    assert model.source == "model" and "measuring failed" in model.reason
+
+
+def test_measured_piece_times_choose_the_piece_count():
+    """With measured per-piece times the planner prices P pieces as P x one
+    piece's collective: cheap pieces win, pieces with a large fixed cost lose."""
+    kw = dict(granule=16, steps=10, gemm_time_us=5000.0, comm_time_us=900.0)
+    cheap = O.plan_overlap(16384, 16384, 16384, torch.bfloat16, 8, "all_reduce", 0.0,
+                           piece_time_us={1: 900.0, 2: 455.0, 4: 230.0}, source="measured", **kw)
+    assert cheap.overlap and cheap.pieces == 4 and cheap.source == "measured"
+    assert cheap.candidates[4] < cheap.candidates[2] < cheap.candidates[1]
+    costly = O.plan_overlap(16384, 16384, 16384, torch.bfloat16, 8, "all_reduce", 0.0,
+                            piece_time_us={1: 900.0, 2: 2000.0, 4: 1900.0}, source="measured", **kw)
+    assert costly.overlap and costly.pieces == 1
+    assert costly.as_dict()["piece_us"] == {"1": 900.0, "2": 2000.0, "4": 1900.0}
