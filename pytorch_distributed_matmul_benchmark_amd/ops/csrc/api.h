@@ -120,10 +120,14 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel);
 // problem (1 = no split; 0 = neither runs it, or p.splitk is not possible).
 int choose_splitk(const Problem& p, int kernel);
 
-// Wave-quantisation tail (gemm_dispatch.cpp): {M1, S} when auto runs rows
-// [0, M1) as one launch and rows [M1, M) split S ways as a second; {0, 1} if
-// the problem runs as one launch.
-std::pair<int, int> tail_split(const Problem& p, int kernel);
+// Wave-quantisation tail (gemm_dispatch.cpp tail_plan): {M1, S, 0} when auto
+// runs rows [0, M1) as one launch and rows [M1, M) split S ways as a second;
+// {0, S, T1} (fp8 tile-range form) when it runs the first T1 tiles of its tile
+// order as one launch and the rest split S ways; {0, 1, 0}: one launch.
+struct TailSplit {
+  int m1, S, tiles_dp;
+};
+TailSplit tail_split(const Problem& p, int kernel);
 
 // Which kernel `kernel` (kAuto allowed) resolves to for this problem;
 // -1 if the requested kernel cannot run it.
@@ -136,7 +140,7 @@ int resolve_kernel(const Problem& p, int kernel);
 struct PlanInfo {
   int kernel, splitk;
   double cost_us;
-  int tail_m1, tail_S;
+  int tail_m1, tail_S, tail_tiles_dp;
 };
 PlanInfo plan_info(const Problem& p, int kernel);
 

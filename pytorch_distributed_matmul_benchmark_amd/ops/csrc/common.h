@@ -106,6 +106,13 @@ struct GemmArgs {
   // zero at launch) and the grid (one workgroup per usable CU).
   unsigned* queue;
   int pers_grid;
+  // Tile-range launches of the wave-quantisation tail (fp8 W4 / W4S,
+  // gemm_dispatch.cpp tail_plan): tile_end > 0 — the launch covers tiles
+  // [0, tile_end) of map_tile's order only (the whole waves); tile_span > 0 —
+  // it covers tiles [tile_base, tile_base + tile_span), each split `splitk`
+  // ways (block = slice * tile_span + local tile; the meet's tile id is the
+  // local index, so the slots and counters cover tile_span tiles).
+  int tile_end, tile_base, tile_span;
   // Completion signals (W4 only; sig == nullptr = off; parallel/overlap.py
   // signalled pieces). Output tile rows are grouped into slots of sig_rows
   // tile rows, sig_slots per batch element. A tile's C leaves write-through

@@ -307,9 +307,11 @@ static bool w4s_auto(const Problem& p) {
   return p.cus == 0 && w4s_fits(p) && tiles_of(p, kMfmaW4) >= 2LL * device_cus();
 }
 
-static double plan_cost(const Problem& p, int kernel, int S) {
+// Model time (us) of `kernel` over T of the problem's tiles (T < 0: all of
+// them), each split S ways along K.
+static double plan_cost_tiles(const Problem& p, int kernel, int S, long long T) {
   const KernelModel& m = model_of(kernel);
-  const long long T = tiles_of(p, kernel);
+  if (T < 0) T = tiles_of(p, kernel);
   const int nk = ktiles(p);
   const int per = (nk + S - 1) / S;
   const long long slots = (long long)(p.cus > 0 ? p.cus : device_cus()) * m.occ;
@@ -321,6 +323,8 @@ static double plan_cost(const Problem& p, int kernel, int S) {
   if (S > 1) t += (double)T * (S - 1) * 2.0 * m.bm * m.bn * 4.0 / kSlabBw + kMeetUs;
   return t;
 }
+
+static double plan_cost(const Problem& p, int kernel, int S) { return plan_cost_tiles(p, kernel, S, -1); }
 
 static bool split_ok(const Problem& p, int kernel, int S) {
   if (kernel == kFp8W4) return S == fp8_split(p);  // its measured rule (fp8_split)
@@ -411,9 +415,19 @@ int choose_splitk(const Problem& p, int kernel) {
 // launch -> tail, hipBLASLt; profiles/r2_fp8_tail_probe.jsonl): 6144^3 196.9
 // -> 175.2 (187.6), 6000^2 x 6144 183.9 -> 177.4 (191.0), 7168^3 278.2 ->
 // 269.1 (314.9).
+//
+// fp8 also has a tile-range form (GemmArgs::tile_end / tile_base / tile_span):
+// the first launch covers the first whole waves of map_tile's tile order
+// (tiles_dp = k x CUs tiles, fp8 W4S or W4) and the second the remaining
+// tiles, each split S ways, as one wave. Rows cannot always cut the grid at a
+// wave boundary (6144^3: 24 x 24 tiles, no row count gives 256 or 512 tiles);
+// tiles always can. Priced like the row form, taken when it is the cheaper of
+// the two; PDMB_TILE_TAIL=0 disables it (A/B, read per call).
 struct TailPlan {
-  int m1 = 0;  // rows of the first (unsplit) launch; 0 = one launch
-  int S = 1;   // K slices of the tail launch
+  int m1 = 0;        // rows of the first (unsplit) launch; 0 = one launch (row form)
+  int S = 1;         // K slices of the tail launch
+  int tiles_dp = 0;  // tile-range form: tiles of the first launch (> 0), rest split S ways
+  bool active() const { return m1 > 0 || tiles_dp > 0; }
 };
 
 static int tail_kernel(const Problem& p) { return p.dtype == kFP8 ? kFp8W4 : kMfmaW4; }
@@ -429,6 +443,26 @@ static TailPlan tail_plan(const Problem& p, int kernel) {
   const long long slots = device_cus();
   const int tm = (p.M + 255) / 256, tn = (p.N + 255) / 256, batch = p.batch < 1 ? 1 : p.batch;
   double bc = whole.cost * 0.97;
+  if (p.dtype == kFP8) {  // tile-range form: whole waves, then the rest split S ways
+    const char* env = std::getenv("PDMB_TILE_TAIL");
+    const long long T = (long long)tm * tn * batch;
+    const int nk = ktiles(p);
+    for (long long dp = slots; dp < T && !(env && env[0] == '0'); dp += slots) {
+      const long long rest = T - dp;
+      const double c1 = plan_cost_tiles(p, kFp8W4, 1, dp);
+      for (int S : {2, 4, 8}) {
+        const int per = (nk + S - 1) / S;
+        if (rest * S > slots || per < 8 || (S - 1) * per >= nk || rest > kMaxSplitTiles) continue;
+        const double c = c1 + plan_cost_tiles(p, kFp8W4, S, rest);
+        if (c < bc) {
+          bc = c;
+          best = TailPlan{};
+          best.tiles_dp = (int)dp;
+          best.S = S;
+        }
+      }
+    }
+  }
   for (int r = 1; r < tm; ++r) {  // r tail tile rows
     Problem a = p, b = p;
     a.M = (tm - r) * 256;
@@ -439,6 +473,7 @@ static TailPlan tail_plan(const Problem& p, int kernel) {
       const double c = c1 + plan_cost(b, kw, S);
       if (c < bc) {
         bc = c;
+        best = TailPlan{};
         best.m1 = a.M;
         best.S = S;
       }
@@ -468,12 +503,13 @@ PlanInfo plan_info(const Problem& p, int kernel) {
   const TailPlan t = tail_plan(p, kernel);
   r.tail_m1 = t.m1;
   r.tail_S = t.S;
+  r.tail_tiles_dp = t.tiles_dp;
   return r;
 }
 
-std::pair<int, int> tail_split(const Problem& p, int kernel) {
+TailSplit tail_split(const Problem& p, int kernel) {
   const TailPlan t = tail_plan(p, kernel);
-  return {t.m1, t.S};
+  return {t.m1, t.S, t.tiles_dp};
 }
 
 // fp8 W4 split-K (gemm_fp8.hip): grids of 256x256 tiles that fill at most
@@ -805,6 +841,15 @@ static Problem batch_elem(const Problem& p, int b) {
   return q;
 }
 
+// Split-K slots of a tail plan's second launch.
+static size_t tail_bytes(const Problem& p, const TailPlan& t) {
+  if (t.tiles_dp > 0) {
+    const long long T = tiles_of(p, kFp8W4);
+    return (size_t)(T - t.tiles_dp) * t.S * 256 * 256 * sizeof(float);
+  }
+  return splitk_bytes(tail_part(p, t), tail_kernel(p), t.S);
+}
+
 size_t gemm_workspace_bytes(const Problem& p, int kernel) {
   if (!wants_padding(p, kernel) && batch_split(p, kernel)) return gemm_workspace_bytes(batch_elem(p, 0), kAuto);
   if (p.sig) {
@@ -816,12 +861,12 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel) {
     const size_t copies = d.a_bytes + d.b_bytes + d.c_bytes;
     const int k = resolve_kernel(d.q, kAuto);
     const TailPlan t = tail_plan(d.q, kAuto);
-    if (t.m1 > 0) return copies + splitk_bytes(tail_part(d.q, t), tail_kernel(d.q), t.S);
+    if (t.active()) return copies + tail_bytes(d.q, t);
     return copies + (is_tiled(k) ? splitk_bytes(d.q, k, plan(d.q, k).splitk) : 0);
   }
   const int k = resolve_kernel(p, kernel);
   const TailPlan t = tail_plan(p, kernel);
-  if (t.m1 > 0) return splitk_bytes(tail_part(p, t), tail_kernel(p), t.S);  // the first launch is unsplit
+  if (t.active()) return tail_bytes(p, t);  // the first launch is unsplit
   if (is_tiled(k)) return splitk_bytes(p, k, plan(p, k).splitk);
   if (k == kFp8W4) return fp8_split_bytes(p, fp8_split(p));
   return is_experiment(k) ? experiment_workspace_bytes(p, k) : 0;
@@ -831,9 +876,25 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel) {
 // stream has no split-K counters yet inside a graph capture, or the workspace
 // was sized for another plan).
 static bool gemm_tail(const Problem& p, const TailPlan& t, hipStream_t stream, hipError_t* e) {
+  if (!p.workspace || p.workspace_bytes < tail_bytes(p, t) || !stream_counters(stream)) return false;
+  if (t.tiles_dp > 0) {  // fp8 tile-range form (gemm_fp8.hip GemmArgs::tile_end / tile_span)
+    GemmArgs d = to_args(p);
+    d.splitk = 1;
+    d.tile_end = t.tiles_dp;
+    const bool s_fits = gemm_fp8_w4s_fits(d) && device_cus() % 8 == 0;
+    if (s_fits) d.pers_grid = (device_cus() / 8) * 8;
+    *e = gemm_fp8_launch(d, s_fits ? 2 : 1, stream);
+    if (*e != hipSuccess) return true;
+    GemmArgs r = to_args(p);
+    r.splitk = t.S;
+    r.tile_base = t.tiles_dp;
+    r.tile_span = (int)(tiles_of(p, kFp8W4) - t.tiles_dp);
+    r.part = (float*)p.workspace;
+    r.flags = stream_counters(stream);
+    *e = gemm_fp8_launch(r, 1, stream);
+    return true;
+  }
   const Problem b = tail_part(p, t);
-  if (!p.workspace || p.workspace_bytes < splitk_bytes(b, tail_kernel(p), t.S) || !stream_counters(stream))
-    return false;
   Problem a = p;
   a.M = t.m1;
   if (p.dtype == kFP8) {  // both launches through the fp8 cases of gemm()
@@ -885,7 +946,7 @@ static hipError_t gemm_padded(const Problem& p, hipStream_t stream, int* used) {
   Problem qt = q;  // the tail plan's split slots follow the copies too
   qt.workspace = part;
   qt.workspace_bytes = part_bytes;
-  if (!(t.m1 > 0 && gemm_tail(qt, t, stream, &e)))
+  if (!(t.active() && gemm_tail(qt, t, stream, &e)))
     e = k == kF32_256s ? gemm_f32_256_launch(a, 1, stream)
       : is_tiled(k) ? tiled_launch(q, k, a, part, part_bytes, stream)
                      : gemm256_launch(q.dtype, a, 4, stream);
@@ -953,7 +1014,7 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
   if (p.K > 0) {
     const TailPlan t = tail_plan(p, kernel);
     hipError_t e = hipSuccess;
-    if (t.m1 > 0 && gemm_tail(p, t, stream, &e)) return e;
+    if (t.active() && gemm_tail(p, t, stream, &e)) return e;
   }
   GemmArgs a = to_args(p);
   if (p.K == 0) {

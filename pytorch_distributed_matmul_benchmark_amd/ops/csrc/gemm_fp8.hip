@@ -494,14 +494,26 @@ __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4(GemmArgs a) {
   if constexpr (TRACE) tr.t[0] = tile_clock();
 
   int bz, tm, tn;
-  map_tile(a, blockIdx.x, bz, tm, tn, SUB);
   // Split-K (grids that under-fill the CUs): the grid's "batch" is batch x S
   // with the slice innermost, as in gemm_w4.hip; slice s runs K-tiles
   // [s * kt_per, +kt_per) and the slices meet in the epilogue (splitk.h).
+  // A tile-range launch (GemmArgs::tile_span) instead maps block b to local
+  // tile b % span of the range and slice b / span: a tile's slices share the
+  // XCD (b % 8), so their meet stays in one L2.
   int slice = 0;
-  if (a.splitk > 1) {
-    slice = bz % a.splitk;
-    bz /= a.splitk;
+  long long meet_tile;
+  if (a.tile_span > 0) {
+    const int local = blockIdx.x % a.tile_span;
+    slice = blockIdx.x / a.tile_span;
+    map_tile(a, a.tile_base + local, bz, tm, tn, SUB);
+    meet_tile = local;
+  } else {
+    map_tile(a, blockIdx.x, bz, tm, tn, SUB);
+    if (a.splitk > 1) {
+      slice = bz % a.splitk;
+      bz /= a.splitk;
+    }
+    meet_tile = ((long long)bz * a.tiles_m + tm) * a.tiles_n + tn;
   }
   const int kt0 = slice * a.kt_per;
   const int m0 = tm * BM, n0 = tn * BN;
@@ -603,8 +615,7 @@ __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4(GemmArgs a) {
   // Split-K: only the last slice of a tile to arrive writes C, summing the
   // slices' fp32 slots (unscaled) block row by block row (splitk.h).
   SplitSlots sl;
-  if (split && !splitk_meet<8, 8, NT4>(a, smem, ((long long)bz * a.tiles_m + tm) * a.tiles_n + tn,
-                                       slice, acc, sl))
+  if (split && !splitk_meet<8, 8, NT4>(a, smem, meet_tile, slice, acc, sl))
     return;
   // Epilogue through LDS as whole rows (common.h store_block16), masked at
   // M / N; every DMA landed and every fragment read done before any wave
@@ -715,7 +726,8 @@ __device__ __forceinline__ void ktile_w4s(const Ctx4& c, const char* smem, u32x4
 template <bool NTS = true>  // NTS: non-temporal C stores (false: A/B kFp8W4STS)
 __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4s(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE4 + 4 * kEpiBuf];
-  const int T = a.tiles_m * a.tiles_n * a.batch;
+  // tile_end > 0: the whole-wave part of a tile-range tail plan
+  const int T = a.tile_end > 0 ? a.tile_end : a.tiles_m * a.tiles_n * a.batch;
   const int G = gridDim.x;
   int vb = blockIdx.x;
   const int lane = threadIdx.x & 63;
@@ -881,16 +893,21 @@ hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream) {
   a.tiles_n = (a.N + k8::BN - 1) / k8::BN;
   a.supertile = choose_supertile(a.tiles_m, a.tiles_n);
   const int S = variant == 1 && a.splitk > 1 ? a.splitk : 1;  // split-K: the W4 kernel only
+  const long long all_tiles = (long long)a.tiles_m * a.tiles_n * a.batch;
+  if (a.tile_span < 0 || a.tile_base < 0 || a.tile_end < 0 || a.tile_end > all_tiles ||
+      (a.tile_span > 0 && (variant != 1 || (long long)a.tile_base + a.tile_span > all_tiles)) ||
+      (a.tile_end > 0 && a.tile_span > 0))
+    return hipErrorInvalidValue;
+  const long long tiles = a.tile_span > 0 ? a.tile_span : a.tile_end > 0 ? a.tile_end : all_tiles;
   if (S > 1) {
     const int nk = a.K / k8::BK;
     a.kt_per = (nk + S - 1) / S;
-    if ((S - 1) * a.kt_per >= nk || !a.part || !a.flags ||
-        (long long)a.tiles_m * a.tiles_n * a.batch > kMaxSplitTiles)
+    if ((S - 1) * a.kt_per >= nk || !a.part || !a.flags || tiles > kMaxSplitTiles)
       return hipErrorInvalidValue;  // every slice must own >= 1 K-tile
   } else {
     a.splitk = 1;
   }
-  const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch * S;
+  const long long nblocks = tiles * S;
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
   const dim3 grid((unsigned)nblocks);

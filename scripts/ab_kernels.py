@@ -7,6 +7,7 @@ equal to the first kernel's. The arm ``torch`` is the vendor library
 
     python scripts/ab_kernels.py --kernels mfma256c,x_noprio --sizes 8192 16384 --rounds 5
     python scripts/ab_kernels.py --kernels auto,auto:1,torch ...    # "kernel:S": split-K S (1 = off)
+    python scripts/ab_kernels.py --kernels auto,auto@PDMB_TILE_TAIL=0,torch ...  # "@VAR=VAL": env for that arm
     python scripts/ab_kernels.py --kernels fp8_w4,torch --dtype float8_e4m3fn \
         --shapes 16384,16384,2048 16384,16384,16384      # M,N,K (K sweeps: per-tile overhead)
 """
@@ -57,18 +58,40 @@ def main():
                 return torch._scaled_mm(A, B, one, one, out_dtype=torch.bfloat16, out=out)
             return torch.matmul(A, B, out=out)
 
-        def arm(k):  # "kernel" or "kernel:S" (S = K slices: split-K forced / off with 1)
+        def arm(k):  # "kernel", "kernel:S" (S = K slices: split-K forced / off with 1),
+            # either with "@VAR=VAL" (an environment switch the dispatcher reads per call)
+            k, _, env = k.partition("@")
             name, _, S = k.partition(":")
-            return name, int(S or 0)
+            return name, int(S or 0), env
+
+        class envset:  # the arm's environment switch for the duration of its calls
+            def __init__(self, env):
+                self.kv = env.split("=", 1) if env else None
+
+            def __enter__(self):
+                if self.kv:
+                    self.old = os.environ.get(self.kv[0])
+                    os.environ[self.kv[0]] = self.kv[1]
+
+            def __exit__(self, *exc):
+                if self.kv:
+                    if self.old is None:
+                        os.environ.pop(self.kv[0], None)
+                    else:
+                        os.environ[self.kv[0]] = self.old
 
         def run(k):
-            name, S = arm(k)
-            return vendor() if k == "torch" else gemm.matmul(A, B, kernel=name, splitk=S)
+            if k == "torch":
+                return vendor()
+            name, S, env = arm(k)
+            with envset(env):
+                return gemm.matmul(A, B, kernel=name, splitk=S)
 
         def bench(k, iters):
             if k != "torch":
-                name, S = arm(k)
-                return gemm.bench_matmul(A, B, C, iters, 2, kernel=name, splitk=S) / iters
+                name, S, env = arm(k)
+                with envset(env):
+                    return gemm.bench_matmul(A, B, C, iters, 2, kernel=name, splitk=S) / iters
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             vendor(C)
             e0.record()

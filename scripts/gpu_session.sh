@@ -98,6 +98,11 @@ run_stage() {
               --rounds 3 --shapes 6144,6144,6144 6000,6000,6144 7168,7168,7168 4096,4096,4096 \
               8192,2048,8192 10240,10240,10240 16384,16384,16384 &&
             grep '^{' "$OUT/ab_fp8.log" > "$OUT/ab_fp8.jsonl" ;;
+    ab_fp8_tail) step ab_fp8_tail 900 python scripts/ab_kernels.py --dtype float8_e4m3fn \
+                   --kernels auto,auto@PDMB_TILE_TAIL=0,torch --rounds 5 --shapes 6144,6144,6144 \
+                   6000,6000,6144 7168,7168,7168 4608,4608,3072 10240,10240,10240 4096,4096,4096 \
+                   8192,2048,8192 16384,16384,16384 &&
+                 grep '^{' "$OUT/ab_fp8_tail.log" > "$OUT/ab_fp8_tail.jsonl" ;;
     race) step race 600 python scripts/race_screen.py --reps 200 && grep '^{' "$OUT/race.log" > "$OUT/race.jsonl" ;;
     tests_fp8) step tests_fp8 600 $PYT tests/test_fp8_gpu.py -m gpu ;;
     tests_comm) step tests_comm 1000 $PYT tests/test_ipc_gpu.py tests/test_reduce_gpu.py \

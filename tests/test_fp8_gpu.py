@@ -293,20 +293,30 @@ def test_fp8_tile_family_edge_tiles(kernel, M, N, K, splitk):
     assert torch.isnan(big[:, N:]).all() and torch.isnan(big[M:]).all()
 
 
-@pytest.mark.parametrize("M,N,K", [(6144, 6144, 6144), (6000, 6000, 6144), (7168, 7168, 1024)])
-def test_fp8_wave_tail_split(M, N, K):
+@pytest.mark.parametrize("M,N,K,form", [(6144, 6144, 6144, None), (6000, 6000, 6144, None),
+                                        (7168, 7168, 1024, None), (7168, 7168, 7168, None),
+                                        (6144, 6144, 6144, "rows"), (6000, 6000, 6144, "rows")])
+def test_fp8_wave_tail_split(M, N, K, form, monkeypatch):
     """fp8 wave-quantisation tail (gemm_dispatch.cpp tail_plan on fp8 W4): the
-    whole-wave rows as one fp8 W4 / W4S launch, the last tile rows split-K in a
+    whole waves as one fp8 W4 / W4S launch — whole tile rows, or (tile-range
+    form) the first k x 256 tiles of the tile order — and the rest split-K in a
     second; exact on small integers (alpha folded in), nothing written outside
-    C, the same bits every launch and under graph replay."""
+    C, the same bits every launch and under graph replay. form "rows": the
+    tile-range form disabled (PDMB_TILE_TAIL=0), the row form runs."""
+    if form == "rows":
+        monkeypatch.setenv("PDMB_TILE_TAIL", "0")
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     Af, Bf = _ints((M, K), g, -2, 3), _ints((K, N), g, -2, 3)
     A8, B8 = Af.to(FP8), _colmajor(Bf.to(FP8))
     big = torch.full((M + 16, N + 24), float("nan"), device="cuda", dtype=torch.bfloat16)
     out = big[:M, :N]
-    m1, S = gemm.tail_split_for(A8, B8, out)
-    if K == 6144:
-        assert 0 < m1 < M and m1 % 256 == 0 and S in (2, 4), (m1, S)
+    m1, S, t1 = gemm.tail_split_for(A8, B8, out)
+    if K >= 6144:
+        assert (0 < m1 < M and m1 % 256 == 0) != (t1 > 0) and S in (2, 4, 8), (m1, S, t1)
+    if form == "rows":
+        assert t1 == 0
+    elif K >= 6144:  # 24 x 24 / 28 x 28 tiles: no row count cuts a whole wave, tiles do
+        assert t1 > 0 and t1 % 256 == 0, (m1, S, t1)
     gemm.matmul(A8, B8, out=out, alpha=0.5)
     ref = (0.5 * (Af.double() @ Bf.double())).to(torch.bfloat16)
     assert torch.equal(out, ref)

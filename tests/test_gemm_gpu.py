@@ -457,8 +457,8 @@ def test_auto_wave_tail_split(M, N, K):
     B = torch.randint(-3, 4, (K, N), device="cuda", generator=g).to(dt)
     big = torch.full((M + 16, N + 24), float("nan"), device="cuda", dtype=dt)
     out = big[:M, :N]
-    m1, S = gemm.tail_split_for(A, B, out)
-    assert 0 < m1 < M and m1 % 256 == 0 and S in (2, 4), (m1, S)
+    m1, S, t1 = gemm.tail_split_for(A, B, out)
+    assert 0 < m1 < M and m1 % 256 == 0 and S in (2, 4) and t1 == 0, (m1, S, t1)
     gemm.matmul(A, B, out=out)
     ref = (A.double() @ B.double()).to(dt)
     assert torch.equal(out, ref)
@@ -490,10 +490,10 @@ def test_no_tail_split_where_it_does_not_pay():
         A = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
         B = torch.empty(K, N, device="cuda", dtype=torch.bfloat16)
         return gemm.tail_split_for(A, B, **kw)
-    assert tail(5000, 5000, 5056) == (0, 1)      # no split of the last rows fills the chip
-    assert tail(16384, 16384, 16384) == (0, 1)   # whole waves
-    assert tail(8192, 1024, 8192) == (0, 1)      # under-filled: the planner's split / small tiles
-    assert tail(6000, 6000, 6144, kernel="w4") == (0, 1)  # explicit kernels run as asked
+    assert tail(5000, 5000, 5056) == (0, 1, 0)      # no split of the last rows fills the chip
+    assert tail(16384, 16384, 16384) == (0, 1, 0)   # whole waves
+    assert tail(8192, 1024, 8192) == (0, 1, 0)      # under-filled: the planner's split / small tiles
+    assert tail(6000, 6000, 6144, kernel="w4") == (0, 1, 0)  # explicit kernels run as asked
 
 
 def test_w4_rejects_unaligned_n():

@@ -20,7 +20,7 @@ def C():
 
 
 def plan(C, dt, M, N, K, b=1, kernel=0, cus=0):
-    k, S, cost, m1, tS = C.plan_shape(dt, M, N, K, b, kernel, cus)
+    k, S, cost, m1, tS, t1 = C.plan_shape(dt, M, N, K, b, kernel, cus)
     return C.kernel_name(k), S, cost, (m1, tS)
 
 
