@@ -122,7 +122,7 @@ int choose_splitk(const Problem& p, int kernel);
 
 // Wave-quantisation tail (gemm_dispatch.cpp tail_plan): {M1, S, 0} when auto
 // runs rows [0, M1) as one launch and rows [M1, M) split S ways as a second;
-// {0, S, T1} (fp8 tile-range form) when it runs the first T1 tiles of its tile
+// {0, S, T1} (tile-range form) when it runs the first T1 tiles of its tile
 // order as one launch and the rest split S ways; {0, 1, 0}: one launch.
 struct TailSplit {
   int m1, S, tiles_dp;

@@ -228,7 +228,7 @@ int64_t splitk_for(const at::Tensor& A, const at::Tensor& B, c10::optional<at::T
 }
 
 // {M1, S, T1}: auto runs rows [0, M1) unsplit and [M1, M) split S ways, or
-// (fp8 tile-range form) tiles [0, T1) unsplit and the rest split S ways;
+// (tile-range form) tiles [0, T1) unsplit and the rest split S ways;
 // {0, 1, 0}: one launch.
 std::tuple<int64_t, int64_t, int64_t> tail_split_for(const at::Tensor& A, const at::Tensor& B,
                                                      c10::optional<at::Tensor> C, int64_t kernel,

@@ -416,9 +416,9 @@ int choose_splitk(const Problem& p, int kernel) {
 // -> 175.2 (187.6), 6000^2 x 6144 183.9 -> 177.4 (191.0), 7168^3 278.2 ->
 // 269.1 (314.9).
 //
-// fp8 also has a tile-range form (GemmArgs::tile_end / tile_base / tile_span):
-// the first launch covers the first whole waves of map_tile's tile order
-// (tiles_dp = k x CUs tiles, fp8 W4S or W4) and the second the remaining
+// The tile-range form (GemmArgs::tile_end / tile_base / tile_span): the first
+// launch covers the first whole waves of map_tile's tile order (tiles_dp =
+// k x CUs tiles, W4S or W4, fp8 W4S or W4) and the second the remaining
 // tiles, each split S ways, as one wave. Rows cannot always cut the grid at a
 // wave boundary (6144^3: 24 x 24 tiles, no row count gives 256 or 512 tiles);
 // tiles always can. Priced like the row form, taken when it is the cheaper of
@@ -443,17 +443,17 @@ static TailPlan tail_plan(const Problem& p, int kernel) {
   const long long slots = device_cus();
   const int tm = (p.M + 255) / 256, tn = (p.N + 255) / 256, batch = p.batch < 1 ? 1 : p.batch;
   double bc = whole.cost * 0.97;
-  if (p.dtype == kFP8) {  // tile-range form: whole waves, then the rest split S ways
+  {  // tile-range form: whole waves, then the rest split S ways
     const char* env = std::getenv("PDMB_TILE_TAIL");
     const long long T = (long long)tm * tn * batch;
     const int nk = ktiles(p);
     for (long long dp = slots; dp < T && !(env && env[0] == '0'); dp += slots) {
       const long long rest = T - dp;
-      const double c1 = plan_cost_tiles(p, kFp8W4, 1, dp);
+      const double c1 = plan_cost_tiles(p, kw, 1, dp);
       for (int S : {2, 4, 8}) {
         const int per = (nk + S - 1) / S;
         if (rest * S > slots || per < 8 || (S - 1) * per >= nk || rest > kMaxSplitTiles) continue;
-        const double c = c1 + plan_cost_tiles(p, kFp8W4, S, rest);
+        const double c = c1 + plan_cost_tiles(p, kw, S, rest);
         if (c < bc) {
           bc = c;
           best = TailPlan{};
@@ -844,7 +844,7 @@ static Problem batch_elem(const Problem& p, int b) {
 // Split-K slots of a tail plan's second launch.
 static size_t tail_bytes(const Problem& p, const TailPlan& t) {
   if (t.tiles_dp > 0) {
-    const long long T = tiles_of(p, kFp8W4);
+    const long long T = tiles_of(p, tail_kernel(p));
     return (size_t)(T - t.tiles_dp) * t.S * 256 * 256 * sizeof(float);
   }
   return splitk_bytes(tail_part(p, t), tail_kernel(p), t.S);
@@ -877,21 +877,29 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel) {
 // was sized for another plan).
 static bool gemm_tail(const Problem& p, const TailPlan& t, hipStream_t stream, hipError_t* e) {
   if (!p.workspace || p.workspace_bytes < tail_bytes(p, t) || !stream_counters(stream)) return false;
-  if (t.tiles_dp > 0) {  // fp8 tile-range form (gemm_fp8.hip GemmArgs::tile_end / tile_span)
+  if (t.tiles_dp > 0) {  // tile-range form (GemmArgs::tile_end / tile_span)
+    const int G = (device_cus() / 8) * 8;
     GemmArgs d = to_args(p);
     d.splitk = 1;
     d.tile_end = t.tiles_dp;
-    const bool s_fits = gemm_fp8_w4s_fits(d) && device_cus() % 8 == 0;
-    if (s_fits) d.pers_grid = (device_cus() / 8) * 8;
-    *e = gemm_fp8_launch(d, s_fits ? 2 : 1, stream);
-    if (*e != hipSuccess) return true;
     GemmArgs r = to_args(p);
     r.splitk = t.S;
     r.tile_base = t.tiles_dp;
-    r.tile_span = (int)(tiles_of(p, kFp8W4) - t.tiles_dp);
+    r.tile_span = (int)(tiles_of(p, tail_kernel(p)) - t.tiles_dp);
     r.part = (float*)p.workspace;
     r.flags = stream_counters(stream);
-    *e = gemm_fp8_launch(r, 1, stream);
+    if (p.dtype == kFP8) {
+      const bool s_fits = gemm_fp8_w4s_fits(d) && device_cus() % 8 == 0;
+      if (s_fits) d.pers_grid = G;
+      *e = gemm_fp8_launch(d, s_fits ? 2 : 1, stream);
+      if (*e == hipSuccess) *e = gemm_fp8_launch(r, 1, stream);
+      return true;
+    }
+    // bf16 / fp16: W4S over the whole waves where it streams >= 2 tiles per CU
+    const bool s = w4s_fits(p) && t.tiles_dp >= 2LL * device_cus();
+    if (s) d.pers_grid = G;
+    *e = gemm_w4_launch(p.dtype, d, stream, s ? 7 : 0);
+    if (*e == hipSuccess) *e = gemm_w4_launch(p.dtype, r, stream, 0);
     return true;
   }
   const Problem b = tail_part(p, t);

@@ -279,14 +279,26 @@ __device__ __forceinline__ unsigned w4_tile(const GemmArgs& a, char* smem, int v
   }
 
   int bz, tm, tn;
-  map_tile(a, vb, bz, tm, tn, SUB);
   // Split-K: the grid's "batch" is batch x S with the slice innermost, so
   // one slice of every tile is a contiguous block range (map_tile's grouped
-  // order) and each workgroup runs K-tiles [kt0, kt0 + nk) of its tile.
+  // order) and each workgroup runs K-tiles [kt0, kt0 + nk) of its tile. A
+  // tile-range launch (GemmArgs::tile_span, the wave-quantisation tail) maps
+  // block vb to local tile vb % span of the range and slice vb / span (a
+  // tile's slices share the XCD, vb % 8, so their meet stays in one L2).
   int slice = 0;
-  if (!PERS && a.splitk > 1) {
-    slice = bz % a.splitk;
-    bz /= a.splitk;
+  long long meet_tile;
+  if (!PERS && a.tile_span > 0) {
+    const int local = vb % a.tile_span;
+    slice = vb / a.tile_span;
+    map_tile(a, a.tile_base + local, bz, tm, tn, SUB);
+    meet_tile = local;
+  } else {
+    map_tile(a, vb, bz, tm, tn, SUB);
+    if (!PERS && a.splitk > 1) {
+      slice = bz % a.splitk;
+      bz /= a.splitk;
+    }
+    meet_tile = ((long long)bz * a.tiles_m + tm) * a.tiles_n + tn;
   }
   const int kt0 = slice * a.kt_per;
   const int m0 = tm * BM, n0 = tn * BN;
@@ -407,8 +419,7 @@ __device__ __forceinline__ unsigned w4_tile(const GemmArgs& a, char* smem, int v
   // other slices' fp32 slots block row by block row while storing, so no
   // more than 2 x 8 fragments are live in VGPRs (splitk.h).
   SplitSlots sl;
-  if (split && !splitk_meet<8, 8, NT>(a, smem, ((long long)bz * a.tiles_m + tm) * a.tiles_n + tn,
-                                      slice, acc, sl))
+  if (split && !splitk_meet<8, 8, NT>(a, smem, meet_tile, slice, acc, sl))
     return PERS ? pre : 0u;
 
   // Epilogue: acc[i][j] holds C^T of a 16x16 tile (lane: row l16, columns
@@ -622,7 +633,8 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4s(GemmArgs a) {
   TileTrace tr;
   if constexpr (TRACE) tr.t[0] = tile_clock();
   constexpr int IL = 64;
-  const int T = a.tiles_m * a.tiles_n * a.batch;
+  // tile_end > 0: the whole-wave part of a tile-range tail plan
+  const int T = a.tile_end > 0 ? a.tile_end : a.tiles_m * a.tiles_n * a.batch;
   const int G = gridDim.x;
   int vb = blockIdx.x;
   const int lane = threadIdx.x & 63;
@@ -852,11 +864,18 @@ hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
   a.tiles_m = (a.M + kw4::BM - 1) / kw4::BM;  // edge tiles: masked epilogue
   a.tiles_n = (a.N + kw4::BN - 1) / kw4::BN;
   const int S = a.splitk > 1 ? a.splitk : 1;
+  const long long all_tiles = (long long)a.tiles_m * a.tiles_n * a.batch;
+  // tile-range launches (GemmArgs::tile_end / tile_span): plain W4 (sub 0) for
+  // a range, plain W4 or W4S (sub 7) for the leading whole waves
+  if (a.tile_span < 0 || a.tile_base < 0 || a.tile_end < 0 || a.tile_end > all_tiles ||
+      (a.tile_span > 0 && (sub != 0 || a.sig || (long long)a.tile_base + a.tile_span > all_tiles)) ||
+      (a.tile_end > 0 && (a.tile_span > 0 || a.sig || (sub != 0 && sub != 7))))
+    return hipErrorInvalidValue;
+  const long long tiles = a.tile_span > 0 ? a.tile_span : a.tile_end > 0 ? a.tile_end : all_tiles;
   if (S > 1) {
     const int nk = a.K / kw4::BK;
     a.kt_per = (nk + S - 1) / S;
-    if ((S - 1) * a.kt_per >= nk || !a.part || !a.flags ||
-        (long long)a.tiles_m * a.tiles_n * a.batch > kMaxSplitTiles)
+    if ((S - 1) * a.kt_per >= nk || !a.part || !a.flags || tiles > kMaxSplitTiles)
       return hipErrorInvalidValue;  // every slice must own >= 1 K-tile
   } else {
     a.splitk = 1;
@@ -864,7 +883,7 @@ hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
   // The grid's batch is batch x S (slice innermost); the XCD-aware order is
   // chosen from the per-element tile grid as before.
   a.supertile = choose_supertile(a.tiles_m, a.tiles_n);
-  const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch * S;
+  const long long nblocks = tiles * S;
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
   const dim3 grid((unsigned)nblocks), block(kw4::NT);

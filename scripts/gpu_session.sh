@@ -103,6 +103,12 @@ run_stage() {
                    6000,6000,6144 7168,7168,7168 4608,4608,3072 10240,10240,10240 4096,4096,4096 \
                    8192,2048,8192 16384,16384,16384 &&
                  grep '^{' "$OUT/ab_fp8_tail.log" > "$OUT/ab_fp8_tail.jsonl" ;;
+    ab_bf16_tail) step ab_bf16_tail 900 python scripts/ab_kernels.py --dtype bfloat16 \
+                    --kernels auto,auto@PDMB_TILE_TAIL=0,torch --rounds 5 --shapes 6144,6144,6144 \
+                    6000,6000,6144 7168,7168,7168 10000,10000,10048 10240,10240,10240 16384,16384,16384 &&
+                  grep '^{' "$OUT/ab_bf16_tail.log" > "$OUT/ab_bf16_tail.jsonl" ;;
+    race_tails) step race_tails 600 python scripts/race_screen.py --tails --reps 50 &&
+                grep '^{' "$OUT/race_tails.log" > "$OUT/race_tails.jsonl" ;;
     race) step race 600 python scripts/race_screen.py --reps 200 && grep '^{' "$OUT/race.log" > "$OUT/race.jsonl" ;;
     tests_fp8) step tests_fp8 600 $PYT tests/test_fp8_gpu.py -m gpu ;;
     tests_comm) step tests_comm 1000 $PYT tests/test_ipc_gpu.py tests/test_reduce_gpu.py \

@@ -6,6 +6,7 @@ bit for bit); prints one JSON line per case with the number of bad runs and the
 first bad element (row, column, got, want) if any.
 
     python scripts/race_screen.py [--reps 200] [--kernels f32_t128x2,f32_t128,t128x2]
+    python scripts/race_screen.py --tails [--reps 50]   # auto's two-launch tail plans (bf16, fp8)
 """
 import argparse
 import json
@@ -20,31 +21,48 @@ from pytorch_distributed_matmul_benchmark_amd.ops import gemm  # noqa: E402
 
 SHAPES = [(256, 256, 32), (256, 256, 64), (256, 256, 96), (256, 256, 128), (512, 768, 192),
           (1024, 1024, 1024)]
+# --tails: auto's wave-quantisation tail plans (a whole-wave launch, then a
+# split-K launch whose slices meet in-kernel): the tile-range form on these
+TAIL_SHAPES = [(6144, 6144, 6144), (6000, 6000, 6144), (7168, 7168, 7168)]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--kernels", default="f32_t128x2,f32_t128,f32_256s,t128x2,t128")
+    ap.add_argument("--tails", action="store_true",
+                    help="screen auto's tail plans (bf16 and fp8, TAIL_SHAPES) instead")
     a = ap.parse_args()
-    for kern in a.kernels.split(","):
-        dt = torch.float32 if kern.startswith("f32") else torch.bfloat16
-        for m, n, k in SHAPES:
+    cases = ([(kd, shp) for kd in ("auto:bfloat16", "auto:float8_e4m3fn") for shp in TAIL_SHAPES]
+             if a.tails else [(kern, shp) for kern in a.kernels.split(",") for shp in SHAPES])
+    for kern, (m, n, k) in cases:
+        kern, _, dname = kern.partition(":")
+        dt = getattr(torch, dname) if dname else (torch.float32 if kern.startswith("f32") else torch.bfloat16)
+        fp8 = dt == gemm.FP8
+        S = 0 if kern == "auto" else 1
+        if True:
             g = torch.Generator(device="cuda").manual_seed(m + 3 * n + k)
-            A = torch.randint(-3, 4, (m, k), device="cuda", generator=g).to(dt)
-            B = torch.randint(-3, 4, (k, n), device="cuda", generator=g).to(dt)
-            want = torch.matmul(A.double(), B.double())
-            if dt != torch.float32:
-                want = want.to(dt).double()  # bf16 output: exact for these magnitudes (|C| <= 9 k)
-            C = torch.empty(m, n, device="cuda", dtype=dt)
+            lo, hi = (-2, 3) if fp8 else (-3, 4)
+            Af = torch.randint(lo, hi, (m, k), device="cuda", generator=g).float()
+            Bf = torch.randint(lo, hi, (k, n), device="cuda", generator=g).float()
+            if fp8:  # e4m3 operands (exact small integers), B column-major, bf16 C
+                A, B = Af.to(dt), Bf.t().contiguous().to(dt).t()
+            else:
+                A, B = Af.to(dt), Bf.to(dt)
+            want = torch.matmul(Af.double(), Bf.double())
+            odt = gemm.out_dtype(dt)
+            if odt != torch.float32:
+                want = want.to(odt).double()  # the fp32-exact sum rounded once, as the kernel does
+            C = torch.empty(m, n, device="cuda", dtype=odt)
             try:
-                gemm.matmul(A, B, out=C, kernel=kern, splitk=1)
+                gemm.matmul(A, B, out=C, kernel=kern, splitk=S)
             except (RuntimeError, ValueError):
                 continue  # the kernel does not take this shape (bf16 K % 64)
             bad, first = 0, None
+            plan = list(gemm.tail_split_for(A, B, C)) if kern == "auto" else None
             for _ in range(a.reps):
                 C.fill_(float("nan"))
-                gemm.matmul(A, B, out=C, kernel=kern, splitk=1)
+                gemm.matmul(A, B, out=C, kernel=kern, splitk=S)
                 d = C.double() != want
                 if bool(d.any()):
                     bad += 1
@@ -53,8 +71,9 @@ def main():
                         first = {"row": idx[0], "col": idx[1], "got": C[idx[0], idx[1]].item(),
                                  "want": want[idx[0], idx[1]].item(), "n_bad": int(d.sum().item())}
             torch.cuda.synchronize()
-            print(json.dumps({"kernel": kern, "m": m, "n": n, "k": k, "reps": a.reps, "bad_runs": bad,
-                              "first_bad": first}), flush=True)
+            print(json.dumps({"kernel": kern, "dtype": str(dt).replace("torch.", ""), "m": m, "n": n,
+                              "k": k, "reps": a.reps, "bad_runs": bad, "first_bad": first,
+                              **({"tail_split": plan} if plan else {})}), flush=True)
 
 
 if __name__ == "__main__":

@@ -446,11 +446,18 @@ def test_tile_family_edge_tiles_masked(kernel, M, N, K, splitk):
     assert torch.isnan(big[:, N:]).all() and torch.isnan(big[M:]).all()
 
 
-@pytest.mark.parametrize("M,N,K", [(6000, 6000, 6144), (10000, 10000, 10048), (6144, 6144, 6144)])
-def test_auto_wave_tail_split(M, N, K):
-    """Auto's wave-quantisation tail: rows [0, M1) as one W4 launch, the last
-    tile rows split-K in a second. Exact small integers, nothing written past
-    N in a wider row or past M, the same bits under graph replay."""
+@pytest.mark.parametrize("M,N,K,form", [(6000, 6000, 6144, "tiles"), (10000, 10000, 10048, "tiles"),
+                                        (6144, 6144, 6144, "tiles"), (7168, 7168, 7168, "tiles"),
+                                        (6000, 6000, 6144, "rows"), (10000, 10000, 10048, "rows"),
+                                        (6144, 6144, 6144, "rows")])
+def test_auto_wave_tail_split(M, N, K, form, monkeypatch):
+    """Auto's wave-quantisation tail: the whole waves as one W4 / W4S launch —
+    the first k x 256 tiles of the tile order ("tiles", the default form) or
+    whole tile rows ("rows": PDMB_TILE_TAIL=0) — and the rest split-K in a
+    second. Exact small integers, nothing written past N in a wider row or
+    past M, the same bits under graph replay."""
+    if form == "rows":
+        monkeypatch.setenv("PDMB_TILE_TAIL", "0")
     dt = torch.bfloat16
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     A = torch.randint(-3, 4, (M, K), device="cuda", generator=g).to(dt)
@@ -458,7 +465,10 @@ def test_auto_wave_tail_split(M, N, K):
     big = torch.full((M + 16, N + 24), float("nan"), device="cuda", dtype=dt)
     out = big[:M, :N]
     m1, S, t1 = gemm.tail_split_for(A, B, out)
-    assert 0 < m1 < M and m1 % 256 == 0 and S in (2, 4) and t1 == 0, (m1, S, t1)
+    if form == "rows":
+        assert 0 < m1 < M and m1 % 256 == 0 and S in (2, 4) and t1 == 0, (m1, S, t1)
+    else:
+        assert m1 == 0 and t1 > 0 and t1 % 256 == 0 and S in (2, 4, 8), (m1, S, t1)
     gemm.matmul(A, B, out=out)
     ref = (A.double() @ B.double()).to(dt)
     assert torch.equal(out, ref)

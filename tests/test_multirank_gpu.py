@@ -143,8 +143,11 @@ def test_two_ranks_overlap_check_catches_a_skipped_wait(gather, chunks, tmp_path
     assert rec["plan"]["source"] == "measured"
     assert rec["signalled"] == (chunks == "2"), rec["plan"]
     assert len(rec["checked_units"]) == 2
-    out = _run(2, "matmul_scaling_benchmark.py", *args,
-               env={"PDMB_TEST_SKIP_READY_WAIT": "20000000"})
+    # the delay must outlast one gloo collective (tens of ms through the host):
+    # a signalled unit's collective is issued behind the previous unit's, which
+    # blocks this host thread under gloo, so a short delay would end first
+    cycles = "20000000" if chunks == "1" else "800000000"
+    out = _run(2, "matmul_scaling_benchmark.py", *args, env={"PDMB_TEST_SKIP_READY_WAIT": cycles})
     assert "FAIL" in out and "ERROR" not in out
 
 
