@@ -74,7 +74,7 @@ from pytorch_distributed_matmul_benchmark_amd.parallel.dist import (  # noqa: E4
     setup_distributed, verify_collectives)
 from pytorch_distributed_matmul_benchmark_amd.parallel.overlap import (  # noqa: E402
     BidirRing, OverlapPipeline, all_gather_now, all_reduce_now, compute_ctx, gather_fn, make_gatherer,
-    measured_plan, reduce_fn, compute_stream)
+    measured_plan, pick_collective, reduce_fn, compute_stream)
 from pytorch_distributed_matmul_benchmark_amd.parallel.partition import (  # noqa: E402
     column_shard, global_batch, local_batch)
 from pytorch_distributed_matmul_benchmark_amd.utils.telemetry import (  # noqa: E402
@@ -109,6 +109,7 @@ class Workload:
         self.split = None                # serialized modes: [(ev0, ev_compute, ev_comm)] per timed step
         self.recording = False
         self.plan = None
+        self.coll_choice = None          # --allreduce / --allgather auto: the measured choice
         self.pipe = None
         self.step = None                 # set below, or by _pipeline
         self._closers = []               # collective teardown (IpcGather.close), run by close()
@@ -135,8 +136,9 @@ class Workload:
             lb, gb = local_batch(ws), global_batch(ws)
             A = self._rnd(lb, n, n, seed=2 * ctx.rank)
             B = self._rnd(lb, n, n, seed=2 * ctx.rank + 1, b=True)
-            # --allreduce ipc: peers pull chunks straight out of C (IPC-exportable allocations)
-            alloc = ((lambda *shape: ipc_empty(shape, odt, dev)) if a.allreduce == "ipc"
+            # --allreduce ipc / auto: peers may pull chunks straight out of C
+            # (IPC-exportable allocations)
+            alloc = ((lambda *shape: ipc_empty(shape, odt, dev)) if a.allreduce in ("ipc", "auto")
                      else (lambda *shape: torch.empty(*shape, device=dev, dtype=odt)))
             C = alloc(lb, n, n)
             self.kernel = self._label(A, B, C)
@@ -146,18 +148,17 @@ class Workload:
                          [(A[0], B[0], C[0]), (A[0], B[0], alloc(n, n))])
                 cs = CommStream(dev)
                 srcs = [C] + ([units[1][2]] if lb == 1 else [])
-                peer = make_gatherer(a.allreduce, dev, srcs, comm=cs)
+                impl, peer = self._collective(a.allreduce, "all_reduce", units[0][2], srcs, cs)
                 self._closers.append(getattr(peer, "close", None))
-                ar = reduce_fn(a.allreduce, peer)
+                ar = reduce_fn(impl, peer)
 
                 def coll(r, p, s, e, after, done):
                     ar(units[r][2][s:e], after=after, done=done)
                 self._pipeline(a, units, coll, lb, "all_reduce", n * n * C.element_size(), cs, peer,
-                               probe=lambda s, e: ar(units[0][2][s:e]))
+                               probe=lambda s, e: ar(units[0][2][s:e]), impl=impl)
             else:
                 self._serial_split()
-                cs = (make_gatherer(a.allreduce, dev, [C]) if a.allreduce != "rccl" and ws > 1
-                      else None)
+                impl, cs = self._collective(a.allreduce, "all_reduce", C[0], [C], None)
                 self._closers.append(getattr(cs, "close", None))
 
                 def step():
@@ -165,7 +166,7 @@ class Workload:
                     self._mm(A, B, C)
                     self._seg(1)
                     if ws > 1:
-                        all_reduce_now(C, a.allreduce, cs)
+                        all_reduce_now(C, impl, cs)
                     self._seg(2)
             self.flops = flop_gemm * gb
             self.global_batch, self.parallelism = gb, f"dp{ws}"
@@ -177,18 +178,18 @@ class Workload:
                   else torch.zeros(n, sh.padded, device=dev, dtype=dt))
             Bl[:, :sh.width].copy_(Bg[:, sh.start:sh.stop])
             del Bg
-            # --allgather ipc: peers pull their blocks out of Cl over xGMI peer
-            # memory, so the outputs live in IPC-exportable allocations
-            alloc = ((lambda: ipc_empty((n, sh.padded), odt, dev)) if a.allgather == "ipc"
+            # --allgather ipc / auto: peers may pull their blocks out of Cl over
+            # xGMI peer memory, so the outputs live in IPC-exportable allocations
+            alloc = ((lambda: ipc_empty((n, sh.padded), odt, dev)) if a.allgather in ("ipc", "auto")
                      else (lambda: torch.empty(n, sh.padded, device=dev, dtype=odt)))
             Cl = alloc()
             self.kernel = self._label(A, Bl, Cl)
             if overlap:
                 units = [(A, Bl, Cl), (A, Bl, alloc())]
                 cs = CommStream(dev)
-                gath = make_gatherer(a.allgather, dev, [u[2] for u in units], comm=cs)
+                impl, gath = self._collective(a.allgather, "all_gather", Cl, [u[2] for u in units], cs)
                 self._closers.append(getattr(gath, "close", None))
-                g = gather_fn(a.allgather, gath)
+                g = gather_fn(impl, gath)
                 self._gathered = {}
 
                 def coll(r, p, s, e, after, done):
@@ -204,12 +205,11 @@ class Workload:
                         probe_out[e - s] = torch.empty(ws * (e - s), sh.padded, device=dev, dtype=odt)
                     g(probe_out[e - s], units[0][2][s:e])
                 self._pipeline(a, units, coll, 1, "all_gather", n * sh.padded * Cl.element_size(),
-                               cs, gath, probe=probe)
+                               cs, gath, probe=probe, impl=impl)
                 probe_out.clear()
             else:
                 gathered = torch.empty(ws * n, sh.padded, device=dev, dtype=odt)
-                cs = (make_gatherer(a.allgather, dev, [Cl]) if a.allgather != "rccl" and ws > 1
-                      else None)
+                impl, cs = self._collective(a.allgather, "all_gather", Cl, [Cl], None)
                 self._closers.append(getattr(cs, "close", None))
                 self._serial_split()
 
@@ -218,7 +218,7 @@ class Workload:
                     self._mm(A, Bl, Cl)
                     self._seg(1)
                     if ws > 1:
-                        all_gather_now(gathered, Cl, a.allgather, cs)
+                        all_gather_now(gathered, Cl, impl, cs)
                     self._seg(2)
             self.flops = flop_gemm
             self.global_batch, self.parallelism = 1, f"tp{ws}"
@@ -255,8 +255,28 @@ class Workload:
         if self.step is None:
             self.step = step
 
+    # -- collectives -------------------------------------------------------------
+    def _collective(self, impl, kind, t, sources, cs):
+        """(implementation, comm object) for ``--allreduce`` / ``--allgather``
+        ``impl``: ``auto`` times RCCL, the direct P2P exchange and the
+        peer-memory pull on this job's ranks and keeps the fastest
+        (parallel/overlap.py pick_collective; the times go into the JSON as
+        ``collective``); otherwise the named one (``rccl`` on the current
+        stream needs no object unless an overlap's comm stream is given)."""
+        ws, dev = self.ctx.world_size, self.ctx.device
+        if ws <= 1:
+            return ("rccl" if impl == "auto" else impl), cs
+        if impl == "auto":
+            impl, obj, times = pick_collective(self.ctx, kind, t, sources, comm=cs)
+            self.coll_choice = {"kind": kind, "chosen": impl, "us": times}
+            return impl, obj
+        if impl == "rccl" and cs is None:
+            return impl, None
+        return impl, make_gatherer(impl, dev, sources, comm=cs)
+
     # -- overlap ---------------------------------------------------------------
-    def _pipeline(self, a, units, coll, per_step, kind, payload, cs, gath=None, probe=None):
+    def _pipeline(self, a, units, coll, per_step, kind, payload, cs, gath=None, probe=None,
+                  impl=None):
         """The overlapped step: plan (parallel/overlap.py measured_plan: this
         job's own GEMM and collective times, MAX over ranks; ``probe(s, e)``
         issues one collective of rows [s, e) of ring slot 0), then an
@@ -267,9 +287,7 @@ class Workload:
                                   steps=max(a.extra_steps, 1), compute=self.comp,
                                   owner=self._mask, comm=cs)
         if not self.plan.overlap:  # the planner refuses a losing overlap: serialize
-            self.step = self._serial_fallback(units, per_step, kind,
-                                              a.allreduce if kind == "all_reduce" else a.allgather,
-                                              gath)
+            self.step = self._serial_fallback(units, per_step, kind, impl, gath)
             return
         self.pipe = OverlapPipeline(self._mm, units, coll, self.ctx.device, self.plan,
                                     per_step=per_step, compute=self.comp, owner=self._mask, comm=cs)
@@ -588,6 +606,8 @@ def _measure(a, ctx, mode: str, overlap: bool, warmup: int, steps: int, key: str
                 host_issue_ms_per_step=round(max(gather_scalars(ctx, tel["host_issue_ms"])) / steps, 4))
     if comp is not None:
         info["compute_ms"], info["comm_ms"] = round(comp, 4), round(comm, 4)
+    if w.coll_choice is not None:
+        info["collective"] = w.coll_choice
     if w.plan is not None:
         info["plan"] = w.plan.as_dict()
         info["plan"]["signalled"] = bool(w.pipe is not None and w.pipe.signalled)
@@ -649,11 +669,14 @@ def main() -> int:
     ap.add_argument("--comm-cus", type=int, default=0,
                     help="overlap: CUs kept free of GEMM workgroups for RCCL (CU-masked "
                          "compute stream; 0 = no mask)")
-    ap.add_argument("--allreduce", default="rccl", choices=["rccl", "direct", "ipc"],
-                    help="batch_parallel all-reduce: RCCL, or a two-shot exchange over P2P links "
-                         "(reduce-scatter group, native fp32 sum, all-gather group)")
-    ap.add_argument("--allgather", default="rccl", choices=["rccl", "direct", "ipc"],
-                    help="matrix_parallel all-gather: RCCL, or direct P2P to every peer at once")
+    ap.add_argument("--allreduce", default="rccl", choices=["rccl", "direct", "ipc", "auto"],
+                    help="batch_parallel all-reduce: RCCL, a two-shot exchange over P2P links "
+                         "(reduce-scatter group, native fp32 sum, all-gather group), the same "
+                         "over xGMI peer memory (ipc), or auto: the fastest of the three, timed "
+                         "on the job's ranks")
+    ap.add_argument("--allgather", default="rccl", choices=["rccl", "direct", "ipc", "auto"],
+                    help="matrix_parallel all-gather: RCCL, direct P2P to every peer at once, "
+                         "a pull over xGMI peer memory (ipc), or auto: the fastest, timed")
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: torch.matmul + gloo, to exercise the multi-rank path without a GPU")

@@ -32,7 +32,7 @@ import torch
 from ..parallel.comm import CommStream, current_stream
 from ..parallel.ipc import ipc_empty
 from ..parallel.overlap import (OverlapPipeline, all_reduce_now, compute_ctx, compute_stream,
-                                make_gatherer, measured_plan, reduce_fn)
+                                make_gatherer, measured_plan, pick_collective, reduce_fn)
 from ..parallel.dist import DistContext
 from ..parallel.partition import global_batch, local_batch
 from ..utils.metrics import gemm_flops, tflops_from
@@ -47,8 +47,8 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     lb = local_batch(ws, w.batch)
     A = randn((lb, n, n), w, dev, seed=2 * (w.seed + ctx.rank))
     B = randn((lb, n, n), w, dev, seed=2 * (w.seed + ctx.rank) + 1, operand="B")
-    # --allreduce ipc: peers pull chunks straight out of C (IPC-exportable allocations)
-    alloc = ((lambda *shape: ipc_empty(shape, out_dtype(w), dev)) if w.allreduce == "ipc"
+    # --allreduce ipc / auto: peers may pull chunks straight out of C (IPC-exportable allocations)
+    alloc = ((lambda *shape: ipc_empty(shape, out_dtype(w), dev)) if w.allreduce in ("ipc", "auto")
              else (lambda *shape: torch.empty(shape, device=dev, dtype=out_dtype(w))))
     C = alloc(lb, n, n)
     mm = gemm_fn(w, dev)
@@ -56,9 +56,9 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     distributed = ctx.is_distributed
     flops = gemm_flops(n, n, n, lb)
 
-    def reduce_all():  # `direct` (the collective's comm object) is bound below
+    def reduce_all():  # `impl` / `direct` (the collective and its comm object) are bound below
         if distributed:
-            all_reduce_now(C, w.allreduce, direct)
+            all_reduce_now(C, impl, direct)
 
     extra = {"global_batch": gb, "local_batch": lb, "overlap": bool(w.overlap and distributed),
              "allreduce": w.allreduce}
@@ -67,12 +67,19 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
              [(A[0], B[0], C[0]), (A[0], B[0], alloc(n, n))])
     cs = CommStream(dev)
     # the collective's comm object: the CommStream, or (--allreduce ipc on GPUs)
-    # an IpcGather with every output buffer registered
-    direct = (make_gatherer(w.allreduce, dev, [C] + ([units[1][2]] if lb == 1 else []), comm=cs)
-              if w.allreduce != "rccl" and distributed else None)
+    # an IpcGather with every output buffer registered; auto: the fastest of
+    # rccl / direct / ipc on this job's ranks (pick_collective)
+    srcs = [C] + ([units[1][2]] if lb == 1 else [])
+    impl = w.allreduce
+    if impl == "auto" and distributed:
+        impl, direct, times = pick_collective(ctx, "all_reduce", units[0][2], srcs, comm=cs)
+        extra["allreduce"], extra["collective_us"] = f"auto:{impl}", times
+    else:
+        impl = "rccl" if impl == "auto" else impl
+        direct = make_gatherer(impl, dev, srcs, comm=cs) if impl != "rccl" and distributed else None
     compute, owner = (compute_stream(dev, w.comm_cus) if (w.overlap and distributed)
                       else (current_stream(dev), None))
-    ar = reduce_fn(w.allreduce, direct if direct is not None else cs)
+    ar = reduce_fn(impl, direct if direct is not None else cs)
     if w.overlap and distributed:
         # priced from this job's own GEMM and all-reduce times (MAX over ranks)
         plan = measured_plan(units, ctx, "all_reduce", n * n * C.element_size(), mm,

@@ -23,21 +23,22 @@ from .common import (ModeResult, Workload, align_ranks, allreduced_relerr, gemm_
 
 def run(w: Workload, ctx: DistContext) -> ModeResult:
     dev, n, ws = ctx.device, w.n, ctx.world_size
+    impl = "rccl" if w.allreduce == "auto" else w.allreduce  # auto: batch_parallel only
     A = randn((n, n), w, dev, seed=2 * (w.seed + ctx.rank))
     B = randn((n, n), w, dev, seed=2 * (w.seed + ctx.rank) + 1, operand="B")
     # --allreduce ipc: peers pull chunks straight out of C (IPC-exportable allocation)
-    C = (ipc_empty((n, n), out_dtype(w), dev) if w.allreduce == "ipc"
+    C = (ipc_empty((n, n), out_dtype(w), dev) if impl == "ipc"
          else torch.empty((n, n), device=dev, dtype=out_dtype(w)))
     mm = gemm_fn(w, dev)
     label = kernel_label(w, A, B, C)
     distributed = ctx.is_distributed
     # the collective's comm object: a CommStream (direct) or an IpcGather (ipc)
-    direct = make_gatherer(w.allreduce, dev, [C]) if w.allreduce != "rccl" and distributed else None
+    direct = make_gatherer(impl, dev, [C]) if impl != "rccl" and distributed else None
 
     def step():
         mm(A, B, C)
         if distributed:
-            all_reduce_now(C, w.allreduce, direct)
+            all_reduce_now(C, impl, direct)
 
     warmup(step, w, ctx)
     align_ranks(ctx)
@@ -48,7 +49,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         mm(A, B, C)
         seg.mark("compute", st)
         if distributed:
-            all_reduce_now(C, w.allreduce, direct)
+            all_reduce_now(C, impl, direct)
         seg.mark("comm", st)
     tot = seg.totals_ms()
     it = max(w.iters, 1)
@@ -58,7 +59,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
                      flops_local=flops, flops_total=flops * ws,
                      tflops=tflops_from(flops, comp / 1e3), compute_ms=comp, comm_ms=comm,
                      compute_only_tflops=tflops_from(flops, comp / 1e3), kernel=label,
-                     extra={"allreduce": w.allreduce})
+                     extra={"allreduce": impl})
     if w.check:
         res.relerr = allreduced_relerr(ctx, A, B, C)
     if hasattr(direct, "close"):  # IpcGather: unmap the peers' buffers before anyone frees

@@ -36,7 +36,7 @@ import torch
 from ..parallel.comm import CommStream, current_stream
 from ..parallel.ipc import ipc_empty
 from ..parallel.overlap import (OverlapPipeline, all_gather_now, compute_ctx, compute_stream,
-                                gather_fn, make_gatherer, measured_plan)
+                                gather_fn, make_gatherer, measured_plan, pick_collective)
 from ..parallel.dist import DistContext
 from ..parallel.partition import column_shard
 from ..utils.metrics import gemm_flops, tflops_from
@@ -89,7 +89,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     A, B_local, sh = make_operands(w, ctx)
     # --allgather ipc: peers pull their blocks straight out of C_local, so the
     # outputs live in IPC-exportable allocations (parallel/ipc.py)
-    alloc = ((lambda: ipc_empty((n, sh.padded), out_dtype(w), dev)) if w.allgather == "ipc"
+    alloc = ((lambda: ipc_empty((n, sh.padded), out_dtype(w), dev)) if w.allgather in ("ipc", "auto")
              else (lambda: torch.empty((n, sh.padded), device=dev, dtype=out_dtype(w))))
     C_local = alloc()
     mm = gemm_fn(w, dev)
@@ -100,10 +100,22 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     units = [(A, B_local, C_local), (A, B_local, alloc())]
     plan = None
     compute, owner = compute_stream(dev, w.comm_cus) if w.overlap else (current_stream(dev), None)
+    impl = w.allgather
+
+    def gatherer(sources, comm):
+        """(impl, comm object) — auto: the fastest of rccl / direct / ipc, timed here."""
+        if impl == "auto":
+            chosen, obj, times = pick_collective(ctx, "all_gather", C_local, sources, comm=comm)
+            extra["allgather"], extra["collective_us"] = f"auto:{chosen}", times
+            return chosen, obj
+        if impl == "rccl" and comm is None:
+            return impl, None
+        return impl, make_gatherer(impl, dev, sources, comm=comm)
+
     if w.overlap:
         cs = CommStream(dev)
-        gath = make_gatherer(w.allgather, dev, [u[2] for u in units], comm=cs)
-        g = gather_fn(w.allgather, gath)
+        impl, gath = gatherer([u[2] for u in units], cs)
+        g = gather_fn(impl, gath)
         probe_out = {}
 
         def probe(s, e):  # one piece's all-gather, into a scratch gather buffer
@@ -126,10 +138,10 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         if w.overlap:  # the planner serialized: the gatherer built for it is the one
             cs = gath
         else:
-            cs = make_gatherer(w.allgather, dev, [C_local]) if w.allgather != "rccl" else None
+            impl, cs = gatherer([C_local], None)
 
         def comm():
-            all_gather_now(gathered, C_local, w.allgather, cs)
+            all_gather_now(gathered, C_local, impl, cs)
 
         def serial_step():
             mm(A, B_local, C_local)

@@ -49,11 +49,12 @@ def run(w: Workload, ctx: DistContext, mode: str = "overlap", depth: int = None)
     if mode not in DEPTH:
         raise ValueError(f"unknown overlap mode {mode!r}")
     dev, n, ws = ctx.device, w.n, ctx.world_size
+    impl = "rccl" if w.allreduce == "auto" else w.allreduce  # auto: batch_parallel only
     depth = DEPTH[mode] if depth is None else max(1, int(depth))
     As = [randn((n, n), w, dev, seed=100 * (w.seed + ctx.rank) + 2 * i) for i in range(depth)]
     Bs = [randn((n, n), w, dev, seed=100 * (w.seed + ctx.rank) + 2 * i + 1, operand="B") for i in range(depth)]
     # --allreduce ipc: peers pull chunks straight out of the C ring (IPC-exportable)
-    Cs = [ipc_empty((n, n), out_dtype(w), dev) if w.allreduce == "ipc"
+    Cs = [ipc_empty((n, n), out_dtype(w), dev) if impl == "ipc"
           else torch.empty((n, n), device=dev, dtype=out_dtype(w)) for _ in range(depth)]
     mm = gemm_fn(w, dev)
     distributed = ctx.is_distributed
@@ -62,7 +63,7 @@ def run(w: Workload, ctx: DistContext, mode: str = "overlap", depth: int = None)
     # the collective's comm object: the CommStream, or (ipc on GPUs) an IpcGather
     # with every ring buffer registered
     cs = CommStream(dev)
-    comm = make_gatherer(w.allreduce, dev, Cs, comm=cs) if distributed and w.allreduce != "rccl" else cs
+    comm = make_gatherer(impl, dev, Cs, comm=cs) if distributed and impl != "rccl" else cs
 
     used = [True] + [False] * (depth - 1)
     if depth == 1 or not distributed:
@@ -70,10 +71,10 @@ def run(w: Workload, ctx: DistContext, mode: str = "overlap", depth: int = None)
             for _ in range(k):
                 mm(As[0], Bs[0], Cs[0])
                 if distributed:
-                    all_reduce_now(Cs[0], w.allreduce, comm)
+                    all_reduce_now(Cs[0], impl, comm)
         finish = (lambda: None)
     else:
-        ar = reduce_fn(w.allreduce, comm)
+        ar = reduce_fn(impl, comm)
         ready = [new_event(dev) for _ in range(depth)]
         done = [new_event(dev) for _ in range(depth)]
         used[0] = False

@@ -10,6 +10,7 @@
 
 #include <chrono>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 
 #include <cstdlib>
@@ -1172,16 +1173,31 @@ void signal_set(Signal* s, int slot, unsigned value) {
   __atomic_store_n((volatile unsigned*)s->host + slot, value, __ATOMIC_RELEASE);
 }
 
+// Spins (pause) for the first kSpinUs — a piece's flag usually turns within
+// tens of us of the wait starting, and this latency delays that piece's
+// collective — then sleeps in growing steps up to kSleepMaxUs, so a rank
+// waiting out a long GEMM does not hold a host core next to RCCL's proxy
+// threads (8 ranks = 8 cores otherwise).
 bool signal_wait(const Signal* s, int slot, unsigned epoch, double timeout_s) {
   if (!s || slot < 0 || slot >= s->slots) return false;
+  constexpr double kSpinUs = 200.0;
+  constexpr int kSleepMaxUs = 50;
   const auto t0 = std::chrono::steady_clock::now();
+  int nap = 2;
+  bool napping = false;
   for (unsigned spin = 0;; ++spin) {
     if ((int)(signal_flag(s, slot) - epoch) >= 0) return true;
-    if ((spin & 1023) == 1023) {
+    if (napping || (spin & 255) == 255) {
       const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       if (el > timeout_s) return false;
+      napping = el * 1e6 > kSpinUs;
     }
-    __builtin_ia32_pause();
+    if (napping) {
+      std::this_thread::sleep_for(std::chrono::microseconds(nap));
+      nap = nap * 2 > kSleepMaxUs ? kSleepMaxUs : nap * 2;
+    } else {
+      __builtin_ia32_pause();
+    }
   }
 }
 

@@ -192,7 +192,7 @@ class SignalSet:
     def flag(self, slot: int) -> int:
         return int(self._C.signal_flag(self.handle, slot))
 
-    def wait(self, slot: int, epoch: int, timeout_s: float = 120.0) -> None:
+    def wait(self, slot: int, epoch: int, timeout_s: float = 30.0) -> None:
         if not self._C.signal_wait(self.handle, int(slot), int(epoch), float(timeout_s)):
             raise TimeoutError(f"GEMM completion signal: slot {slot} did not reach epoch {epoch} "
                                f"within {timeout_s:.0f} s (flag {self.flag(slot)})")

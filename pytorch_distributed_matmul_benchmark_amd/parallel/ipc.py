@@ -118,10 +118,30 @@ class IpcGather:
         """Export ``src`` and map every peer's corresponding buffer (collective)."""
         assert src.is_cuda and src.storage_offset() == 0, "register an ipc_empty tensor"
         mod = _mod()
-        mine = mod.ipc_handle(src)
+        try:
+            mine = mod.ipc_handle(src)
+        except Exception as e:  # still join the exchange below, so no peer is left waiting
+            mine, why = None, e
         handles: List[Optional[bytes]] = [None] * self.ws
         dist.all_gather_object(handles, mine, group=self.group)
-        peers = {r: mod.ipc_open(h, self.dev_index) for r, h in enumerate(handles) if r != self.me}
+        if any(h is None for h in handles):
+            raise RuntimeError(f"IpcGather: a rank could not export its buffer"
+                               f"{f' ({why!r})' if mine is None else ''}")
+        peers, err = {}, None
+        try:
+            for r, h in enumerate(handles):
+                if r != self.me:
+                    peers[r] = mod.ipc_open(h, self.dev_index)
+        except Exception as e:
+            err = e
+        oks: List[Optional[bool]] = [None] * self.ws  # every rank fails together, or none does
+        dist.all_gather_object(oks, err is None, group=self.group)
+        if not all(oks):
+            for addr in peers.values():
+                mod.ipc_close(addr, self.dev_index)
+            raise RuntimeError(f"IpcGather: mapping a peer's buffer failed on rank(s) "
+                               f"{[r for r, ok in enumerate(oks) if not ok]}"
+                               f"{f' ({err!r})' if err is not None else ''}")
         self.bufs.append((src.data_ptr(), src.untyped_storage().nbytes(), peers))
 
     @property
@@ -252,12 +272,15 @@ class IpcGather:
         else:
             dist.all_reduce(self.flag, group=self.group)
 
-    def close(self) -> None:
+    def close(self, barrier: bool = True) -> None:
+        """Unmap the peers' buffers, then (``barrier``) wait for every rank to
+        have done so; ``barrier=False`` when not every rank holds a gatherer
+        (the caller runs a common barrier instead)."""
         mod = _mod()
         torch.cuda.synchronize(self.device)
         for _, _, peers in self.bufs:
             for addr in peers.values():
                 mod.ipc_close(addr, self.dev_index)
         self.bufs = []
-        if self.ws > 1:
+        if barrier and self.ws > 1:
             dist.barrier(group=self.group)

@@ -441,7 +441,7 @@ class OverlapPipeline:
     def __init__(self, mm: Callable, units: Sequence[Tuple], collective: Callable,
                  device: torch.device, plan: OverlapPlan, per_step: int = 1,
                  compute=None, owner=None, comm: Optional[CommStream] = None,
-                 timeout_s: float = 120.0, operands: Optional[Callable[[int], Tuple]] = None):
+                 timeout_s: float = 30.0, operands: Optional[Callable[[int], Tuple]] = None):
         from ..ops import gemm
 
         self.mm, self.units, self.collective = mm, list(units), collective
@@ -593,8 +593,12 @@ def make_gatherer(impl: str, device: torch.device, sources=(), comm: Optional[Co
     cs = comm or CommStream(device)
     if impl == "ipc" and device.type == "cuda":
         ig = IpcGather(cs)
-        for src in sources:
-            ig.register(src)
+        try:
+            for src in sources:
+                ig.register(src)  # fails on every rank together (IpcGather.register)
+        except Exception:
+            ig.close(barrier=False)  # unmap what the earlier buffers mapped
+            raise
         return ig
     return cs
 
@@ -648,3 +652,69 @@ def all_reduce_now(t: torch.Tensor, impl: str = "rccl", comm=None) -> None:
     reduce_fn(impl, comm)(t, after=ready, done=done)
     if cur is not None:
         cur.wait_event(done)
+
+
+COLLECTIVE_IMPLS = ("rccl", "direct", "ipc")
+
+
+def pick_collective(ctx, kind: str, t: torch.Tensor, sources=(), comm: Optional[CommStream] = None,
+                    reps: int = 3, candidates: Optional[Sequence[str]] = None):
+    """``--allreduce auto`` / ``--allgather auto``: time one whole collective of
+    ``t`` (all_reduce: in place; all_gather: ``t`` is this rank's block) with
+    every implementation on this job's own ranks — RCCL's, the direct P2P
+    exchange, and (GPU tensors) the peer-memory pull with ``sources``
+    registered — each after one untimed call and a barrier, MAX over ranks,
+    and keep the fastest. A candidate that fails on any rank is dropped on
+    every rank. Returns ``(impl, comm_object, {impl: us or None})``; the comm
+    object is what ``make_gatherer(impl, ...)`` would have built (on ``comm``),
+    the losers' are closed. Collective: every rank must call it."""
+    import time
+
+    from .dist import all_ok, barrier, reduce_scalar
+
+    dev = t.device
+    cuda = dev.type == "cuda"
+    cands = list(candidates or (COLLECTIVE_IMPLS if cuda else ("rccl", "direct")))
+    out = (torch.empty((ctx.world_size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+           if kind == "all_gather" else None)
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize(dev)
+
+    def call(impl, g):
+        if kind == "all_reduce":
+            all_reduce_now(t, impl, g)
+        else:
+            all_gather_now(out, t, impl, g)
+
+    times, objs = {}, {}
+    for impl in cands:
+        g, err = None, None
+        try:
+            g = make_gatherer(impl, dev, sources, comm=comm or CommStream(dev))
+            call(impl, g)
+            sync()
+        except Exception as e:  # e.g. no peer access: this candidate is out, on every rank
+            err = f"{type(e).__name__}: {e}"
+        if not all_ok(ctx, err is None):
+            times[impl] = None
+            if g is not None and hasattr(g, "close"):
+                g.close(barrier=False)
+            barrier(ctx)
+            continue
+        barrier(ctx)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            call(impl, g)
+        sync()
+        times[impl] = reduce_scalar(ctx, (time.perf_counter() - t0) * 1e6 / reps, "max")
+        objs[impl] = g
+    ok = {k: v for k, v in times.items() if v is not None}
+    if not ok:
+        raise RuntimeError(f"no {kind} implementation ran on every rank: {times}")
+    best = min(ok, key=ok.get)
+    for impl, g in objs.items():
+        if impl != best and hasattr(g, "close"):
+            g.close()
+    return best, objs[best], {k: (round(v, 1) if v is not None else None) for k, v in times.items()}

@@ -90,18 +90,21 @@ def build_parser(kind: str) -> argparse.ArgumentParser:
                    help="--overlap: collective pieces per GEMM, each started by the GEMM's own "
                         "tile-completion signals (0: the overlap planner's choice; 1: whole "
                         "collectives pipelined across GEMMs)")
-    g.add_argument("--allgather", default="rccl", choices=["rccl", "direct", "ipc"],
+    g.add_argument("--allgather", default="rccl", choices=["rccl", "direct", "ipc", "auto"],
                    help="matrix_parallel all-gather: RCCL's all_gather_into_tensor; direct: one "
                         "batched P2P group sending this rank's shard to every peer at once (each "
                         "over its own xGMI link on a fully connected node); ipc: every rank pulls "
-                        "the peers' shards out of their memory (hipIpc mappings) with DMA-engine "
-                        "copies, one stream per peer, no CUs (CPU tensors: as direct)")
-    g.add_argument("--allreduce", default="rccl", choices=["rccl", "direct", "ipc"],
+                        "the peers' shards out of their memory (hipIpc mappings) in one kernel "
+                        "launch (CPU tensors: as direct); auto: the fastest of the three, timed on "
+                        "the job's own ranks")
+    g.add_argument("--allreduce", default="rccl", choices=["rccl", "direct", "ipc", "auto"],
                    help="batch_parallel / data_parallel / overlap all-reduce: RCCL's all_reduce; "
                         "direct: a two-shot exchange over point-to-point links (reduce-scatter as one "
                         "batched P2P group, native fp32-accumulating sum, all-gather as another); "
-                        "ipc (batch_parallel on GPUs): the same two shots as pulls out of the peers' "
-                        "memory (hipIpc mappings, DMA-engine copies, no CUs); elsewhere as direct")
+                        "ipc (GPUs): the same two shots read out of the peers' memory (hipIpc "
+                        "mappings; the sum reads every peer's chunk in place); elsewhere as direct; "
+                        "auto (batch_parallel): the fastest of the three, timed on the job's ranks "
+                        "(other modes: rccl)")
     g.add_argument("--comm-cus", type=int, default=0,
                    help="--overlap: CUs kept free of GEMM workgroups for RCCL (CU-masked "
                         "compute stream, spread over the 8 XCDs; 0 = no mask)")

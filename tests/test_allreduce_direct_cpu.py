@@ -180,5 +180,32 @@ def test_overlap_ipc_allreduce_uses_the_peer_path():
     from pytorch_distributed_matmul_benchmark_amd.models import data_parallel, overlap
 
     src = inspect.getsource(overlap.run)
-    assert "reduce_fn(w.allreduce, comm)" in src and "cs.all_reduce_direct if" not in src
-    assert "make_gatherer(w.allreduce" in inspect.getsource(data_parallel.run)
+    assert "reduce_fn(impl, comm)" in src and "cs.all_reduce_direct if" not in src
+    assert "make_gatherer(impl" in inspect.getsource(data_parallel.run)
+
+
+def test_auto_collective_is_measured_and_agreed():
+    """--allreduce auto / --allgather auto (parallel/overlap.py pick_collective):
+    every candidate that runs is timed on the job's ranks (MAX over ranks), the
+    fastest is used, and the mode still checks out; bench.py reports the
+    choice and the times per mode."""
+    import json
+
+    for mode, flag in (("batch_parallel", "--allreduce"), ("matrix_parallel", "--allgather")):
+        for extra in ([], ["--overlap", "--chunks", "1"]):
+            out = _torchrun(2, "matmul_scaling_benchmark.py", "--device", "cpu", "--sizes", "192",
+                            "--iterations", "2", "--warmup", "1", "--dtype", "float32", "--mode",
+                            mode, flag, "auto", "--check", *extra)
+            assert "PASS" in out and "FAIL" not in out and "ERROR" not in out, (mode, extra)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--gpus", "2",
+                        "--size", "128", "--steps", "2", "--warmup", "1", "--extra-steps", "2",
+                        "--extra-warmup", "1", "--allgather", "auto", "--allreduce", "auto"],
+                       capture_output=True, text=True, timeout=300, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    for key in ("batch_parallel", "batch_parallel+overlap", "matrix_parallel", "matrix_parallel+overlap"):
+        m = d["modes"][key]
+        assert m and m["value"] > 0, key
+        c = m["collective"]
+        assert c["chosen"] in ("rccl", "direct") and set(c["us"]) == {"rccl", "direct"}, (key, c)
+        assert c["us"][c["chosen"]] == min(v for v in c["us"].values() if v is not None)
