@@ -89,6 +89,17 @@ DTYPES = {"bfloat16": torch.bfloat16, "float16": torch.float16, "float32": torch
           "float8_e4m3fn": torch.float8_e4m3fn}
 
 
+def collective_impl(flag, overlap: bool) -> str:
+    """``--allreduce`` / ``--allgather`` as given, or by default: RCCL for the
+    serialized modes (the reference's NCCL call, matmul_scaling_benchmark.py:
+    150 / :221, so those numbers stay reference-comparable) and ``auto`` for the
+    overlapped ones (the fastest of RCCL / direct / peer-memory, timed on the
+    job's own ranks: the MI355X-native schedule)."""
+    if flag:
+        return flag
+    return "auto" if overlap else "rccl"
+
+
 class Workload:
     """Operands + one timed ``step()`` of a scaling mode on this rank.
 
@@ -138,7 +149,8 @@ class Workload:
             B = self._rnd(lb, n, n, seed=2 * ctx.rank + 1, b=True)
             # --allreduce ipc / auto: peers may pull chunks straight out of C
             # (IPC-exportable allocations)
-            alloc = ((lambda *shape: ipc_empty(shape, odt, dev)) if a.allreduce in ("ipc", "auto")
+            ar_impl = collective_impl(a.allreduce, overlap)
+            alloc = ((lambda *shape: ipc_empty(shape, odt, dev)) if ar_impl in ("ipc", "auto")
                      else (lambda *shape: torch.empty(*shape, device=dev, dtype=odt)))
             C = alloc(lb, n, n)
             self.kernel = self._label(A, B, C)
@@ -148,7 +160,7 @@ class Workload:
                          [(A[0], B[0], C[0]), (A[0], B[0], alloc(n, n))])
                 cs = CommStream(dev)
                 srcs = [C] + ([units[1][2]] if lb == 1 else [])
-                impl, peer = self._collective(a.allreduce, "all_reduce", units[0][2], srcs, cs)
+                impl, peer = self._collective(ar_impl, "all_reduce", units[0][2], srcs, cs)
                 self._closers.append(getattr(peer, "close", None))
                 ar = reduce_fn(impl, peer)
 
@@ -158,7 +170,7 @@ class Workload:
                                probe=lambda s, e: ar(units[0][2][s:e]), impl=impl)
             else:
                 self._serial_split()
-                impl, cs = self._collective(a.allreduce, "all_reduce", C[0], [C], None)
+                impl, cs = self._collective(ar_impl, "all_reduce", C[0], [C], None)
                 self._closers.append(getattr(cs, "close", None))
 
                 def step():
@@ -180,14 +192,15 @@ class Workload:
             del Bg
             # --allgather ipc / auto: peers may pull their blocks out of Cl over
             # xGMI peer memory, so the outputs live in IPC-exportable allocations
-            alloc = ((lambda: ipc_empty((n, sh.padded), odt, dev)) if a.allgather in ("ipc", "auto")
+            ag_impl = collective_impl(a.allgather, overlap)
+            alloc = ((lambda: ipc_empty((n, sh.padded), odt, dev)) if ag_impl in ("ipc", "auto")
                      else (lambda: torch.empty(n, sh.padded, device=dev, dtype=odt)))
             Cl = alloc()
             self.kernel = self._label(A, Bl, Cl)
             if overlap:
                 units = [(A, Bl, Cl), (A, Bl, alloc())]
                 cs = CommStream(dev)
-                impl, gath = self._collective(a.allgather, "all_gather", Cl, [u[2] for u in units], cs)
+                impl, gath = self._collective(ag_impl, "all_gather", Cl, [u[2] for u in units], cs)
                 self._closers.append(getattr(gath, "close", None))
                 g = gather_fn(impl, gath)
                 self._gathered = {}
@@ -209,7 +222,7 @@ class Workload:
                 probe_out.clear()
             else:
                 gathered = torch.empty(ws * n, sh.padded, device=dev, dtype=odt)
-                impl, cs = self._collective(a.allgather, "all_gather", Cl, [Cl], None)
+                impl, cs = self._collective(ag_impl, "all_gather", Cl, [Cl], None)
                 self._closers.append(getattr(cs, "close", None))
                 self._serial_split()
 
@@ -669,14 +682,15 @@ def main() -> int:
     ap.add_argument("--comm-cus", type=int, default=0,
                     help="overlap: CUs kept free of GEMM workgroups for RCCL (CU-masked "
                          "compute stream; 0 = no mask)")
-    ap.add_argument("--allreduce", default="rccl", choices=["rccl", "direct", "ipc", "auto"],
+    ap.add_argument("--allreduce", default=None, choices=["rccl", "direct", "ipc", "auto"],
                     help="batch_parallel all-reduce: RCCL, a two-shot exchange over P2P links "
                          "(reduce-scatter group, native fp32 sum, all-gather group), the same "
                          "over xGMI peer memory (ipc), or auto: the fastest of the three, timed "
-                         "on the job's ranks")
-    ap.add_argument("--allgather", default="rccl", choices=["rccl", "direct", "ipc", "auto"],
+                         "on the job's ranks (default: rccl serialized, auto overlapped)")
+    ap.add_argument("--allgather", default=None, choices=["rccl", "direct", "ipc", "auto"],
                     help="matrix_parallel all-gather: RCCL, direct P2P to every peer at once, "
-                         "a pull over xGMI peer memory (ipc), or auto: the fastest, timed")
+                         "a pull over xGMI peer memory (ipc), or auto: the fastest, timed "
+                         "(default: rccl serialized, auto overlapped)")
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: torch.matmul + gloo, to exercise the multi-rank path without a GPU")
@@ -758,7 +772,8 @@ def main() -> int:
                        "parallelism": head["parallelism"], "mode": a.mode,
                        "overlap": bool(a.overlap), "backend": a.backend, "kernel": head["kernel"]},
             "dist_backend": ctx.backend,
-            "collectives": {"all_reduce": a.allreduce, "all_gather": a.allgather},
+            "collectives": {"all_reduce": a.allreduce or "rccl serialized, auto overlapped",
+                            "all_gather": a.allgather or "rccl serialized, auto overlapped"},
             "world_size_seen": dist.get_world_size() if ctx.is_distributed else 1,
             "rccl_version": _rccl_version(ctx),
             "collectives_verified": verified,
