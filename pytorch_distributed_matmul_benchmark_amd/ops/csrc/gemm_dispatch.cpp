@@ -423,7 +423,7 @@ int choose_splitk(const Problem& p, int kernel) {
 // tiles, each split S ways, as one wave. Rows cannot always cut the grid at a
 // wave boundary (6144^3: 24 x 24 tiles, no row count gives 256 or 512 tiles);
 // tiles always can. Priced like the row form, taken when it is the cheaper of
-// the two; PDMB_TILE_TAIL=0 disables it (A/B, read per call).
+// the two; PDMB_TILE_TAIL=0 disables it, =S forces S (A/B, read per call).
 struct TailPlan {
   int m1 = 0;        // rows of the first (unsplit) launch; 0 = one launch (row form)
   int S = 1;         // K slices of the tail launch
@@ -445,16 +445,21 @@ static TailPlan tail_plan(const Problem& p, int kernel) {
   const int tm = (p.M + 255) / 256, tn = (p.N + 255) / 256, batch = p.batch < 1 ? 1 : p.batch;
   double bc = whole.cost * 0.97;
   {  // tile-range form: whole waves, then the rest split S ways
+    // PDMB_TILE_TAIL (read per call, A/B): 0 = off; 2 / 4 / 8 = only that S, priced
+    // as if free (forced wherever the form is feasible)
     const char* env = std::getenv("PDMB_TILE_TAIL");
+    int force = env ? std::atoi(env) : -1;
+    if (force != 0 && force != 2 && force != 4 && force != 8) force = -1;
     const long long T = (long long)tm * tn * batch;
     const int nk = ktiles(p);
-    for (long long dp = slots; dp < T && !(env && env[0] == '0'); dp += slots) {
+    for (long long dp = slots; dp < T && force != 0; dp += slots) {
       const long long rest = T - dp;
       const double c1 = plan_cost_tiles(p, kw, 1, dp);
       for (int S : {2, 4, 8}) {
         const int per = (nk + S - 1) / S;
         if (rest * S > slots || per < 8 || (S - 1) * per >= nk || rest > kMaxSplitTiles) continue;
-        const double c = c1 + plan_cost_tiles(p, kw, S, rest);
+        if (force > 0 && S != force) continue;
+        const double c = force > 0 ? -1.0 : c1 + plan_cost_tiles(p, kw, S, rest);
         if (c < bc) {
           bc = c;
           best = TailPlan{};

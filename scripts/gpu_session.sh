@@ -99,12 +99,14 @@ run_stage() {
               8192,2048,8192 10240,10240,10240 16384,16384,16384 &&
             grep '^{' "$OUT/ab_fp8.log" > "$OUT/ab_fp8.jsonl" ;;
     ab_fp8_tail) step ab_fp8_tail 900 python scripts/ab_kernels.py --dtype float8_e4m3fn \
-                   --kernels auto,auto@PDMB_TILE_TAIL=0,torch --rounds 5 --shapes 6144,6144,6144 \
+                   --kernels auto,auto@PDMB_TILE_TAIL=0,auto@PDMB_TILE_TAIL=2,auto@PDMB_TILE_TAIL=4,torch \
+                   --rounds 5 --shapes 6144,6144,6144 \
                    6000,6000,6144 7168,7168,7168 4608,4608,3072 10240,10240,10240 4096,4096,4096 \
                    8192,2048,8192 16384,16384,16384 &&
                  grep '^{' "$OUT/ab_fp8_tail.log" > "$OUT/ab_fp8_tail.jsonl" ;;
     ab_bf16_tail) step ab_bf16_tail 900 python scripts/ab_kernels.py --dtype bfloat16 \
-                    --kernels auto,auto@PDMB_TILE_TAIL=0,torch --rounds 5 --shapes 6144,6144,6144 \
+                    --kernels auto,auto@PDMB_TILE_TAIL=0,auto@PDMB_TILE_TAIL=2,auto@PDMB_TILE_TAIL=4,torch \
+                   --rounds 5 --shapes 6144,6144,6144 \
                     6000,6000,6144 7168,7168,7168 10000,10000,10048 10240,10240,10240 16384,16384,16384 &&
                   grep '^{' "$OUT/ab_bf16_tail.log" > "$OUT/ab_bf16_tail.jsonl" ;;
     race_tails) step race_tails 600 python scripts/race_screen.py --tails --reps 50 &&
@@ -120,6 +122,10 @@ run_stage() {
                     cat "$OUT/mask_probe_k${k}_${occ// /}.log" >> "$OUT/mask_probe.jsonl"
                   done
                 done ;;
+    peer_copy) step peer_copy 300 python scripts/peer_copy_bench.py &&
+               grep '^{' "$OUT/peer_copy.log" > "$OUT/peer_copy.jsonl" ;;
+    rocprof_peer_copy) step rocprof_peer_copy 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/rocprof_pc" -o pc -- \
+                         python3 scripts/peer_copy_bench.py --arms sdma:2,kernel:32 --rounds 2 --iters 3 ;;
     queue_probe) step queue_probe 300 python scripts/queue_probe.py &&
                  grep '^{' "$OUT/queue_probe.log" > "$OUT/queue_probe.jsonl" ;;
     reduce_bench) step reduce_bench 300 python scripts/reduce_bench.py &&
