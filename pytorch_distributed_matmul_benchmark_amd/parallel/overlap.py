@@ -689,19 +689,29 @@ def pick_collective(ctx, kind: str, t: torch.Tensor, sources=(), comm: Optional[
             all_gather_now(out, t, impl, g)
 
     times, objs = {}, {}
+
+    def drop(impl, g):  # the candidate is out, on every rank
+        times[impl] = None
+        if g is not None and hasattr(g, "close"):
+            g.close(barrier=False)
+        barrier(ctx)
+
     for impl in cands:
         g, err = None, None
-        try:
+        try:  # built everywhere before any rank enters its collective
             g = make_gatherer(impl, dev, sources, comm=comm or CommStream(dev))
-            call(impl, g)
-            sync()
-        except Exception as e:  # e.g. no peer access: this candidate is out, on every rank
+        except Exception as e:  # e.g. no peer access
             err = f"{type(e).__name__}: {e}"
         if not all_ok(ctx, err is None):
-            times[impl] = None
-            if g is not None and hasattr(g, "close"):
-                g.close(barrier=False)
-            barrier(ctx)
+            drop(impl, g)
+            continue
+        try:
+            call(impl, g)
+            sync()
+        except Exception as e:
+            err = f"{type(e).__name__}: {e}"
+        if not all_ok(ctx, err is None):
+            drop(impl, g)
             continue
         barrier(ctx)
         t0 = time.perf_counter()

@@ -209,3 +209,43 @@ def test_auto_collective_is_measured_and_agreed():
         c = m["collective"]
         assert c["chosen"] in ("rccl", "direct") and set(c["us"]) == {"rccl", "direct"}, (key, c)
         assert c["us"][c["chosen"]] == min(v for v in c["us"].values() if v is not None)
+
+
+def _pick_worker(rank, ws, port, outdir):
+    import json as _json
+
+    from pytorch_distributed_matmul_benchmark_amd.parallel import overlap as O
+    from pytorch_distributed_matmul_benchmark_amd.parallel.dist import DistContext
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    ctx = DistContext(rank=rank, world_size=ws, local_rank=rank, device=torch.device("cpu"), backend="gloo")
+    real = O.make_gatherer
+
+    def flaky(impl, device, sources=(), comm=None):  # "direct" cannot be built on rank 1
+        if impl == "direct" and rank == 1:
+            raise RuntimeError("no P2P here")
+        return real(impl, device, sources, comm)
+
+    O.make_gatherer = flaky
+    t = torch.full((1000,), float(rank + 1))
+    impl, obj, times = O.pick_collective(ctx, "all_reduce", t, [], reps=2)
+    out = torch.empty(ws * 10)
+    gimpl, _, gtimes = O.pick_collective(ctx, "all_gather", torch.full((10,), float(rank)), [], reps=2)
+    with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
+        _json.dump({"impl": impl, "times": times, "gimpl": gimpl, "gtimes": gtimes}, f)
+    dist.destroy_process_group()
+
+
+def test_pick_collective_drops_a_candidate_that_fails_on_one_rank(tmp_path):
+    """pick_collective: a candidate that fails on ANY rank is dropped on EVERY
+    rank (times None), no rank hangs, and all ranks agree on the choice."""
+    import json as _json
+
+    ws = 3
+    mp.spawn(_pick_worker, args=(ws, _port(), str(tmp_path)), nprocs=ws, join=True)
+    res = [_json.load(open(tmp_path / f"r{r}.json")) for r in range(ws)]
+    for r in res:
+        assert r["impl"] == "rccl" and r["times"]["direct"] is None and r["times"]["rccl"] > 0
+        assert r["gimpl"] == "rccl" and r["gtimes"]["direct"] is None
+    assert len({_json.dumps(r, sort_keys=True) for r in res}) == 1  # identical on every rank
