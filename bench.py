@@ -505,6 +505,12 @@ def _self_launch(a) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def _phase(ctx, key: str, phase: str) -> None:
+    """Diagnostics (PDMB_BENCH_TRACE=1): each rank's mode / phase on stderr."""
+    if os.environ.get("PDMB_BENCH_TRACE") == "1":
+        print(f"[rank {ctx.rank}] {key}: {phase}", file=sys.stderr, flush=True)
+
+
 def _fault(ctx, key: str, phase: str) -> None:
     """Fault injection for the failure-agreement tests: ``PDMB_BENCH_FAULT=
     rank:mode:phase`` (mode ``*`` = any; phase ``setup`` | ``timed``) raises
@@ -583,6 +589,7 @@ def _measure(a, ctx, mode: str, overlap: bool, warmup: int, steps: int, key: str
     """Build (agreed across ranks) and time one workload. Returns
     ``(tflops, seconds, info)`` or ``(None, None, error_string)``."""
     w, err = None, None
+    _phase(ctx, key, "setup")
     try:
         _fault(ctx, key, "setup")
         w = Workload(a, ctx, mode, overlap, batch=batch)
@@ -597,10 +604,13 @@ def _measure(a, ctx, mode: str, overlap: bool, warmup: int, steps: int, key: str
         return None, None, err or "failed on another rank"
     try:
         _fault(ctx, key, "timed")
+        _phase(ctx, key, "warm")
         wms = w.warm(warmup, warmup_ms)
+        _phase(ctx, key, "timed")
         el, mine, tel = w.timed(steps)
     except Exception as e:
         _die(ctx, key, e)
+    _phase(ctx, key, "close")
     v = w.flops * steps / el / 1e12 if el > 0 else 0.0
     # per-rank rate: this rank's share of the FLOPs over its own wall time
     share = w.flops / ctx.world_size if mode in ("independent", "batch_parallel") else w.flops

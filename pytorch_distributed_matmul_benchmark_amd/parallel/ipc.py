@@ -85,6 +85,17 @@ def engine() -> str:
     return e
 
 
+_TRACE = os.environ.get("PDMB_IPC_TRACE") == "1"
+
+
+def _trace(msg: str) -> None:
+    """Diagnostics (PDMB_IPC_TRACE=1): one line per IPC operation on stderr."""
+    if _TRACE:
+        import sys
+
+        print(f"[ipc pid {os.getpid()}] {msg}", file=sys.stderr, flush=True)
+
+
 def blocks_per_peer() -> int:
     return int(os.environ.get("PDMB_IPC_BLOCKS", "0"))  # 0: the kernel's default (32)
 
@@ -143,6 +154,8 @@ class IpcGather:
                                f"{[r for r, ok in enumerate(oks) if not ok]}"
                                f"{f' ({err!r})' if err is not None else ''}")
         self.bufs.append((src.data_ptr(), src.untyped_storage().nbytes(), peers))
+        _trace(f"rank {self.me} register {src.data_ptr():#x} +{src.untyped_storage().nbytes()} "
+               f"peers {{{', '.join(f'{r}: {a:#x}' for r, a in peers.items())}}}")
 
     @property
     def npeers(self) -> int:
@@ -168,6 +181,7 @@ class IpcGather:
             return
         mod = _mod()
         cs = self.cs.stream
+        _trace(f"rank {self.me} pull " + ", ".join(f"{d.data_ptr():#x}<-{a:#x}+{d.nbytes}" for d, a in jobs))
         if self.engine == "kernel":
             mod.peer_copy([d for d, _ in jobs], [a for _, a in jobs], self.blocks)
             return
@@ -248,6 +262,8 @@ class IpcGather:
                 if self.engine == "kernel":
                     # pull and sum fused: this chunk of every rank's t, read in place
                     addrs = [self._peer_addr(t, r) + bounds[self.me][0] * es for r in range(self.ws)]
+                    _trace(f"rank {self.me} reduce {mine.data_ptr():#x}+{mine.nbytes} <- "
+                           + ", ".join(f"{a:#x}" for a in addrs))
                     mod.reduce_sum_addrs(mine, addrs, 0)
                 else:
                     scratch = self.cs._scratch(t, (self.ws - 1) * chunk)
@@ -278,6 +294,7 @@ class IpcGather:
         (the caller runs a common barrier instead)."""
         mod = _mod()
         torch.cuda.synchronize(self.device)
+        _trace(f"rank {self.me} close {len(self.bufs)} buffer(s)")
         for _, _, peers in self.bufs:
             for addr in peers.values():
                 mod.ipc_close(addr, self.dev_index)

@@ -478,6 +478,33 @@ def test_auto_wave_tail_split(M, N, K, form, monkeypatch):
     assert torch.equal(C2, ref)
 
 
+@pytest.mark.parametrize("dtype", ["bfloat16", "float8_e4m3fn"])
+def test_batched_tile_range_tail(dtype):
+    """The tile-range tail over a batch (5120^3 x 2: 800 tiles = 768 in whole
+    waves + 32 split-K; the tile order runs across batch elements): exact on
+    small integers for every element, nothing written outside C."""
+    dt = getattr(torch, dtype)
+    fp8 = dt == gemm.FP8
+    M = N = K = 5120
+    g = torch.Generator(device="cuda").manual_seed(77)
+    lo, hi = (-2, 3) if fp8 else (-3, 4)
+    Af = torch.randint(lo, hi, (2, M, K), device="cuda", generator=g).float()
+    Bf = torch.randint(lo, hi, (2, K, N), device="cuda", generator=g).float()
+    if fp8:
+        A, B = Af.to(dt), Bf.transpose(-1, -2).contiguous().to(dt).transpose(-1, -2)
+    else:
+        A, B = Af.to(dt), Bf.to(dt)
+    odt = gemm.out_dtype(dt)
+    big = torch.full((2, M + 8, N + 16), float("nan"), device="cuda", dtype=odt)
+    out = big[:, :M, :N]
+    m1, S, t1 = gemm.tail_split_for(A, B, out)
+    assert m1 == 0 and t1 == 768 and S > 1, (m1, S, t1)
+    gemm.matmul(A, B, out=out)
+    ref = torch.matmul(Af.double(), Bf.double()).to(odt)
+    assert torch.equal(out, ref)
+    assert torch.isnan(big[:, :, N:]).all() and torch.isnan(big[:, M:]).all()
+
+
 @pytest.mark.parametrize("M,N,K", [(6000, 6000, 6100), (6000, 5996, 6144)])
 def test_padded_wave_tail_split(M, N, K):
     """The padded fast path (K or N off the granule) runs the padded problem with
