@@ -74,7 +74,7 @@ from pytorch_distributed_matmul_benchmark_amd.parallel.dist import (  # noqa: E4
     setup_distributed, verify_collectives)
 from pytorch_distributed_matmul_benchmark_amd.parallel.overlap import (  # noqa: E402
     BidirRing, OverlapPipeline, all_gather_now, all_reduce_now, compute_ctx, gather_fn, make_gatherer,
-    measured_plan, pick_collective, reduce_fn, compute_stream)
+    ipc_buffers, measured_plan, pick_collective, reduce_fn, compute_stream)
 from pytorch_distributed_matmul_benchmark_amd.parallel.partition import (  # noqa: E402
     column_shard, global_batch, local_batch)
 from pytorch_distributed_matmul_benchmark_amd.utils.telemetry import (  # noqa: E402
@@ -150,7 +150,7 @@ class Workload:
             # --allreduce ipc / auto: peers may pull chunks straight out of C
             # (IPC-exportable allocations)
             ar_impl = collective_impl(a.allreduce, overlap)
-            alloc = ((lambda *shape: ipc_empty(shape, odt, dev)) if ar_impl in ("ipc", "auto")
+            alloc = ((lambda *shape: ipc_empty(shape, odt, dev)) if ipc_buffers(ar_impl, dev)
                      else (lambda *shape: torch.empty(*shape, device=dev, dtype=odt)))
             C = alloc(lb, n, n)
             self.kernel = self._label(A, B, C)
@@ -193,7 +193,7 @@ class Workload:
             # --allgather ipc / auto: peers may pull their blocks out of Cl over
             # xGMI peer memory, so the outputs live in IPC-exportable allocations
             ag_impl = collective_impl(a.allgather, overlap)
-            alloc = ((lambda: ipc_empty((n, sh.padded), odt, dev)) if ag_impl in ("ipc", "auto")
+            alloc = ((lambda: ipc_empty((n, sh.padded), odt, dev)) if ipc_buffers(ag_impl, dev)
                      else (lambda: torch.empty(n, sh.padded, device=dev, dtype=odt)))
             Cl = alloc()
             self.kernel = self._label(A, Bl, Cl)

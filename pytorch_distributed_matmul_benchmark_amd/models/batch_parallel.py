@@ -32,7 +32,8 @@ import torch
 from ..parallel.comm import CommStream, current_stream
 from ..parallel.ipc import ipc_empty
 from ..parallel.overlap import (OverlapPipeline, all_reduce_now, compute_ctx, compute_stream,
-                                make_gatherer, measured_plan, pick_collective, reduce_fn)
+                                ipc_buffers, make_gatherer, measured_plan, pick_collective,
+                                reduce_fn)
 from ..parallel.dist import DistContext
 from ..parallel.partition import global_batch, local_batch
 from ..utils.metrics import gemm_flops, tflops_from
@@ -48,7 +49,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     A = randn((lb, n, n), w, dev, seed=2 * (w.seed + ctx.rank))
     B = randn((lb, n, n), w, dev, seed=2 * (w.seed + ctx.rank) + 1, operand="B")
     # --allreduce ipc / auto: peers may pull chunks straight out of C (IPC-exportable allocations)
-    alloc = ((lambda *shape: ipc_empty(shape, out_dtype(w), dev)) if w.allreduce in ("ipc", "auto")
+    alloc = ((lambda *shape: ipc_empty(shape, out_dtype(w), dev)) if ipc_buffers(w.allreduce, dev)
              else (lambda *shape: torch.empty(shape, device=dev, dtype=out_dtype(w))))
     C = alloc(lb, n, n)
     mm = gemm_fn(w, dev)

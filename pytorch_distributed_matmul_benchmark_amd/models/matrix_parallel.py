@@ -36,7 +36,8 @@ import torch
 from ..parallel.comm import CommStream, current_stream
 from ..parallel.ipc import ipc_empty
 from ..parallel.overlap import (OverlapPipeline, all_gather_now, compute_ctx, compute_stream,
-                                gather_fn, make_gatherer, measured_plan, pick_collective)
+                                gather_fn, ipc_buffers, make_gatherer, measured_plan,
+                                pick_collective)
 from ..parallel.dist import DistContext
 from ..parallel.partition import column_shard
 from ..utils.metrics import gemm_flops, tflops_from
@@ -89,7 +90,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     A, B_local, sh = make_operands(w, ctx)
     # --allgather ipc: peers pull their blocks straight out of C_local, so the
     # outputs live in IPC-exportable allocations (parallel/ipc.py)
-    alloc = ((lambda: ipc_empty((n, sh.padded), out_dtype(w), dev)) if w.allgather in ("ipc", "auto")
+    alloc = ((lambda: ipc_empty((n, sh.padded), out_dtype(w), dev)) if ipc_buffers(w.allgather, dev)
              else (lambda: torch.empty((n, sh.padded), device=dev, dtype=out_dtype(w))))
     C_local = alloc()
     mm = gemm_fn(w, dev)

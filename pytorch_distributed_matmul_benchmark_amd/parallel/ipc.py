@@ -42,8 +42,8 @@ peer's comm stream has passed the same point):
 ``register(src)`` exports ``src`` (an ``ipc_empty`` tensor: its own
 hipMalloc allocation) and maps every peer's counterpart (handles exchanged by
 a host all-gather of objects); every rank registers corresponding buffers in
-the same order. ``close()`` unmaps, then barriers, so no rank frees an
-exported buffer another rank still maps.
+the same order. Exported buffers and peer mappings live until the process
+exits (the arena below); ``close()`` drains and barriers.
 
 gloo rehearsals (ranks sharing one GPU) exchange handles the same way; a
 barrier becomes "drain the comm stream, then a host barrier". CPU tensors
@@ -67,11 +67,34 @@ def _mod():
     return _native.load(build_if_missing=False)
 
 
+# Process-lifetime IPC arena: every exported buffer this process allocates is
+# kept until the process exits, and every peer buffer it maps stays mapped
+# (opened once per handle). Freeing an exported buffer and unmapping peers'
+# between benchmark modes let the next mode's hipMalloc / hipIpcOpenMemHandle
+# land on the same virtual addresses again (seen in PDMB_IPC_TRACE runs), and
+# an 8-rank one-GPU rehearsal that churned them faulted once
+# (profiles/r4e_selflaunch8_chunks_fault.log); with no unmap / free before
+# exit there is no address reuse to race with. A benchmark process exports a
+# handful of buffers (about 1.2 GB at 16k, ws = 8).
+_ARENA: List[torch.Tensor] = []
+_MAPPED: Dict[Tuple[int, bytes], int] = {}  # (device, peer handle) -> mapped address
+
+
 def ipc_empty(shape, dtype: torch.dtype, device: torch.device) -> torch.Tensor:
-    """A GPU tensor in its own allocation (IPC-exportable); CPU: plain empty."""
+    """A GPU tensor in its own allocation (IPC-exportable), kept alive by the
+    process-lifetime arena; CPU: plain empty."""
     if device.type != "cuda":
         return torch.empty(shape, dtype=dtype, device=device)
-    return _mod().ipc_empty(list(shape), dtype, device.index if device.index is not None else 0)
+    t = _mod().ipc_empty(list(shape), dtype, device.index if device.index is not None else 0)
+    _ARENA.append(t)
+    return t
+
+
+def _open(mod, handle: bytes, dev_index: int) -> int:
+    key = (dev_index, handle)
+    if key not in _MAPPED:
+        _MAPPED[key] = mod.ipc_open(handle, dev_index)
+    return _MAPPED[key]
 
 
 ENGINES = ("kernel", "sdma")
@@ -142,14 +165,12 @@ class IpcGather:
         try:
             for r, h in enumerate(handles):
                 if r != self.me:
-                    peers[r] = mod.ipc_open(h, self.dev_index)
+                    peers[r] = _open(mod, h, self.dev_index)
         except Exception as e:
             err = e
         oks: List[Optional[bool]] = [None] * self.ws  # every rank fails together, or none does
         dist.all_gather_object(oks, err is None, group=self.group)
         if not all(oks):
-            for addr in peers.values():
-                mod.ipc_close(addr, self.dev_index)
             raise RuntimeError(f"IpcGather: mapping a peer's buffer failed on rank(s) "
                                f"{[r for r, ok in enumerate(oks) if not ok]}"
                                f"{f' ({err!r})' if err is not None else ''}")
@@ -289,15 +310,13 @@ class IpcGather:
             dist.all_reduce(self.flag, group=self.group)
 
     def close(self, barrier: bool = True) -> None:
-        """Unmap the peers' buffers, then (``barrier``) wait for every rank to
-        have done so; ``barrier=False`` when not every rank holds a gatherer
-        (the caller runs a common barrier instead)."""
-        mod = _mod()
+        """Finish with this gatherer: drain the device, then (``barrier``) wait
+        for every rank to have done so, so no rank's next mode starts while a
+        peer still pulls from this one's buffers; ``barrier=False`` when not
+        every rank holds a gatherer (the caller runs a common barrier). The
+        mappings themselves stay open for the process (the arena above)."""
         torch.cuda.synchronize(self.device)
         _trace(f"rank {self.me} close {len(self.bufs)} buffer(s)")
-        for _, _, peers in self.bufs:
-            for addr in peers.values():
-                mod.ipc_close(addr, self.dev_index)
         self.bufs = []
         if barrier and self.ws > 1:
             dist.barrier(group=self.group)

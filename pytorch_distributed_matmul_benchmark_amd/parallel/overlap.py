@@ -657,13 +657,31 @@ def all_reduce_now(t: torch.Tensor, impl: str = "rccl", comm=None) -> None:
 COLLECTIVE_IMPLS = ("rccl", "direct", "ipc")
 
 
+def auto_candidates(device: torch.device) -> Tuple[str, ...]:
+    """What ``auto`` times: RCCL's collective and the direct P2P exchange (both
+    RCCL kernels); the peer-memory pull joins with ``PDMB_AUTO_IPC=1`` (GPU
+    tensors) — it ran only with ranks sharing one GPU so far, where one
+    8-rank rehearsal faulted before the IPC arena (parallel/ipc.py), so it is
+    opt-in rather than something a default run might pick."""
+    if device.type == "cuda" and os.environ.get("PDMB_AUTO_IPC") == "1":
+        return COLLECTIVE_IMPLS
+    return ("rccl", "direct")
+
+
+def ipc_buffers(impl: str, device: torch.device) -> bool:
+    """Whether a mode's collective buffers must be IPC-exportable (``ipc_empty``):
+    ``--... ipc``, or ``auto`` with the peer-memory pull among its candidates."""
+    return device.type == "cuda" and (impl == "ipc" or (impl == "auto" and "ipc" in auto_candidates(device)))
+
+
 def pick_collective(ctx, kind: str, t: torch.Tensor, sources=(), comm: Optional[CommStream] = None,
                     reps: int = 3, candidates: Optional[Sequence[str]] = None):
     """``--allreduce auto`` / ``--allgather auto``: time one whole collective of
     ``t`` (all_reduce: in place; all_gather: ``t`` is this rank's block) with
-    every implementation on this job's own ranks — RCCL's, the direct P2P
-    exchange, and (GPU tensors) the peer-memory pull with ``sources``
-    registered — each after one untimed call and a barrier, MAX over ranks,
+    every candidate implementation on this job's own ranks (``auto_candidates``:
+    RCCL's, the direct P2P exchange, and with PDMB_AUTO_IPC=1 the peer-memory
+    pull with ``sources`` registered) — each after one untimed call and a
+    barrier, MAX over ranks,
     and keep the fastest. A candidate that fails on any rank is dropped on
     every rank. Returns ``(impl, comm_object, {impl: us or None})``; the comm
     object is what ``make_gatherer(impl, ...)`` would have built (on ``comm``),
@@ -674,7 +692,9 @@ def pick_collective(ctx, kind: str, t: torch.Tensor, sources=(), comm: Optional[
 
     dev = t.device
     cuda = dev.type == "cuda"
-    cands = list(candidates or (COLLECTIVE_IMPLS if cuda else ("rccl", "direct")))
+    if candidates is None:
+        candidates = auto_candidates(dev)
+    cands = list(candidates)
     out = (torch.empty((ctx.world_size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
            if kind == "all_gather" else None)
 
