@@ -17,6 +17,9 @@
 //     --lds / --threads: each workgroup's dynamic LDS and size — 147968 B and
 //       256 threads model W4S (one workgroup per CU: the LDS does not fit two)
 //     --spin-us: how long each workgroup holds its CU (default 20 us)
+//     --bits b0,b1,...: exactly these mask bits off (which XCD / CU a bit
+//       names: with the W4S occupancy and one workgroup per CU, the XCD that
+//       lost a CU shows a "late" workgroup)
 // Each workgroup also stamps its start / end (wall clock): "late" counts the
 // workgroups that started more than half a spin after the first one, i.e.
 // that queued behind another workgroup instead of finding a free CU — with
@@ -62,6 +65,7 @@ __global__ void __launch_bounds__(256) where(unsigned* out, int spin) {
 int main(int argc, char** argv) {
   int k = 8, nblocks = 0, lds = 0, threads = 64, spin_us = 20;
   const char* mode = "first";
+  std::vector<int> bits;  // --bits b0,b1,...: exactly these mask bits off (mode "bits")
   for (int i = 1; i + 1 < argc; i += 2) {
     if (!strcmp(argv[i], "--exclude")) k = atoi(argv[i + 1]);
     if (!strcmp(argv[i], "--mode")) mode = argv[i + 1];
@@ -69,6 +73,15 @@ int main(int argc, char** argv) {
     if (!strcmp(argv[i], "--lds")) lds = atoi(argv[i + 1]);
     if (!strcmp(argv[i], "--threads")) threads = atoi(argv[i + 1]);
     if (!strcmp(argv[i], "--spin-us")) spin_us = atoi(argv[i + 1]);
+    if (!strcmp(argv[i], "--bits")) {
+      mode = "bits";
+      for (const char* q = argv[i + 1]; *q;) {
+        bits.push_back(atoi(q));
+        while (*q && *q != ',') ++q;
+        if (*q == ',') ++q;
+      }
+      k = (int)bits.size();
+    }
   }
   if (threads < 64 || threads > 256 || threads % 64 || lds < 0 || lds > 160 * 1024 || spin_us < 1 ||
       spin_us > 100000) {
@@ -86,7 +99,11 @@ int main(int argc, char** argv) {
   std::vector<unsigned> mask((n + 31) / 32, 0);
   for (int i = 0; i < n; ++i) mask[i / 32] |= 1u << (i % 32);
   for (int j = 0; j < k && k > 0; ++j) {
-    const int bit = !strcmp(mode, "block") ? j * (n / k) : j;
+    const int bit = !strcmp(mode, "bits") ? bits[j] : !strcmp(mode, "block") ? j * (n / k) : j;
+    if (bit < 0 || bit >= n) {
+      fprintf(stderr, "mask bit %d outside [0, %d)\n", bit, n);
+      return 2;
+    }
     mask[bit / 32] &= ~(1u << (bit % 32));
   }
   hipStream_t s;

@@ -68,6 +68,8 @@ run_stage() {
     selflaunch8_ipc) step selflaunch8_ipc 500 python bench.py --gpus 8 --dist-backend gloo --size 4096 \
                        --steps 3 --warmup 1 --extra-steps 2 --extra-warmup 1 --allgather ipc --allreduce ipc &&
                      grep '^{' "$OUT/selflaunch8_ipc.log" > "$OUT/selflaunch8_ipc.json" ;;
+    selflaunch8_chunks_x2) run_stage selflaunch8_chunks && cp "$OUT/selflaunch8_chunks.json" "$OUT/selflaunch8_chunks_a.json" &&
+                           run_stage selflaunch8_chunks ;;
     selflaunch8_chunks) step selflaunch8_chunks 500 python bench.py --gpus 8 --dist-backend gloo --size 4096 \
                           --steps 3 --warmup 1 --extra-steps 2 --extra-warmup 1 --allgather ipc --allreduce ipc \
                           --mode matrix_parallel --overlap --chunks 2 &&
@@ -126,6 +128,11 @@ run_stage() {
                grep '^{' "$OUT/peer_copy.log" > "$OUT/peer_copy.jsonl" ;;
     rocprof_peer_copy) step rocprof_peer_copy 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/rocprof_pc" -o pc -- \
                          python3 scripts/peer_copy_bench.py --arms sdma:2,kernel:32 --rounds 2 --iters 3 ;;
+    mask_bits) P=pytorch_distributed_matmul_benchmark_amd/runtime/cu_mask_probe
+               for b in $(seq 0 31) 64 128 192 255; do
+                 step mask_bit_$b 30 $P --bits $b --blocks 256 --threads 256 --lds 147968 || return $?
+                 cat "$OUT/mask_bit_$b.log" >> "$OUT/mask_bits.jsonl"
+               done ;;
     queue_probe) step queue_probe 300 python scripts/queue_probe.py &&
                  grep '^{' "$OUT/queue_probe.log" > "$OUT/queue_probe.jsonl" ;;
     reduce_bench) step reduce_bench 300 python scripts/reduce_bench.py &&
