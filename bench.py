@@ -631,6 +631,8 @@ def _measure(a, ctx, mode: str, overlap: bool, warmup: int, steps: int, key: str
         info["compute_ms"], info["comm_ms"] = round(comp, 4), round(comm, 4)
     if w.coll_choice is not None:
         info["collective"] = w.coll_choice
+    if w._mask is not None:
+        info["comm_cus"] = len(w._mask.excluded)   # --comm-cus rounded to 4 per XCD
     if w.plan is not None:
         info["plan"] = w.plan.as_dict()
         info["plan"]["signalled"] = bool(w.pipe is not None and w.pipe.signalled)

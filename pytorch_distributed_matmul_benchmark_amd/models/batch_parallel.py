@@ -124,7 +124,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         extra["ring"] = len(units)
         extra["pieces"] = len(pipe.pieces)
         extra["signalled"] = pipe.signalled
-        extra["comm_cus"] = w.comm_cus
+        extra["comm_cus"] = len(owner.excluded) if owner is not None else 0
         label = ("pdmb_w4_nn (completion signals)" if pipe.signalled
                  else kernel_label(w, A[0], B[0], C[0], shared=True))
 

@@ -186,7 +186,7 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
                                owner=owner, comm=cs, operands=operands)
         extra["pieces"] = len(pipe.pieces)
         extra["signalled"] = pipe.signalled
-        extra["comm_cus"] = w.comm_cus
+        extra["comm_cus"] = len(owner.excluded) if owner is not None else 0
         label = ("pdmb_w4_nn (completion signals)" if pipe.signalled
                  else kernel_label(w, A, B_local, C_local, shared=True))
 

@@ -338,8 +338,31 @@ def _xcd_spread(ncu: int, k: int, nxcd: int = 8) -> List[int]:
     Checked on the hardware (runtime/cu_mask_probe.hip,
     profiles/r3zo_cu_mask_placement_probe.jsonl): with bits 0..k-1 off every
     XCD runs on 32 - k/8 CUs, and workgroups still go round-robin, 1/8 to each
-    XCD; clearing k bits of one residue class instead starves that one XCD."""
+    XCD; clearing k bits of one residue class instead starves that one XCD.
+    Round 4 re-checked the map bit by bit at W4S occupancy (one 147,968-byte
+    LDS workgroup per CU; profiles/r4i_cu_mask_bit_map.jsonl): clearing bit i
+    alone takes a CU from XCD i % 8 for every i in 0..31, 64, 128, 192, 255."""
     return list(range(min(max(k, 0), ncu)))
+
+
+# CUs a compute stream gives up at a time: 4 per XCD. A per-XCD count is not
+# enough — inside an XCD the dispatcher does not place workgroups on the free
+# CUs alone: with bits 0..7 or 0..15 off (1 or 2 CUs per XCD) a grid of one
+# workgroup per usable CU at one-workgroup-per-CU occupancy still stacks 8 / 12
+# workgroups behind others (start skew 41 us vs 21 us unmasked), while bits
+# 0..31 off leave 28 CUs per XCD and no workgroup late
+# (profiles/r4h_cu_mask_w4s_occupancy_probe.jsonl) — round 3's masked-W4S
+# collapse. A single cleared bit already makes 1-4 workgroups of its XCD late
+# (profiles/r4i_cu_mask_bit_map.jsonl).
+MASK_GRANULE = 32
+
+
+def round_comm_cus(k: int, ncu: int = 256) -> int:
+    """``--comm-cus k`` as the compute stream applies it: rounded up to whole
+    MASK_GRANULE steps (0 stays 0), at most ncu - MASK_GRANULE."""
+    if k <= 0:
+        return 0
+    return min(-(-k // MASK_GRANULE) * MASK_GRANULE, max(ncu - MASK_GRANULE, 0))
 
 
 class MaskedStream:
@@ -403,12 +426,14 @@ def compute_ctx(stream, owner):
 
 
 def compute_stream(device: torch.device, comm_cus: int = 0):
-    """(stream, owner): the current stream (comm_cus == 0) or a CU-masked one."""
+    """(stream, owner): the current stream (comm_cus == 0) or a CU-masked one
+    keeping ``round_comm_cus(comm_cus)`` CUs free (``owner.excluded``)."""
     if device.type != "cuda":
         return None, None
     if comm_cus <= 0:
         return torch.cuda.current_stream(device), None
-    ms = MaskedStream(device, comm_cus)
+    ncu = torch.cuda.get_device_properties(device).multi_processor_count
+    ms = MaskedStream(device, round_comm_cus(comm_cus, ncu))
     return ms.stream, ms
 
 

@@ -35,6 +35,24 @@ def _kernels(src, tmp_path=None, experiments=False):
     return out
 
 
+def _loops(body, min_mfma=1):
+    """(label, text) of every back edge's span (a branch to a label above it)
+    holding at least ``min_mfma`` MFMA instructions."""
+    lines = body.split("\n")
+    lab = {}
+    out = []
+    for i, line in enumerate(lines):
+        m = re.match(r"(\.LBB\w+):", line)
+        if m:
+            lab[m.group(1)] = i
+        m = re.search(r"s_cbranch_\w+ (\.LBB\w+)", line)
+        if m and lab.get(m.group(1), i) < i:
+            text = "\n".join(lines[lab[m.group(1)]:i])
+            if len(re.findall(r"v_mfma", text)) >= min_mfma:
+                out.append((m.group(1), text))
+    return out
+
+
 def test_bf16_lds_dma_kernel_stays_pipelined(tmp_path):
     ks = _kernels("gemm_mfma256.hip", tmp_path, experiments=True)  # SCHED 2 is an A/B build
     main = [k for k in ks if "gemm256_nn" in k and "ILi2ELi2ELb0E" in k]
@@ -88,12 +106,17 @@ def test_w4_kernel_agpr_accumulators_and_counted_waits(tmp_path):
         assert k["spill"] == 0 and k["lds"] == 2 * 65536 + 4 * 4224  # + fused epilogue buffers
         assert re.search(r"v_mfma_f32_16x16x32_\w+ a\[", b)  # accumulators live in AGPRs
         assert k["vgpr"] <= 256
-        loop = b[:b.find("global_atomic")]  # K-loop + drain; the split-K epilogue follows
         assert "global_atomic" in b  # the fused split-K meeting point is compiled in
-        # two drains, both outside the K-loop: before the separate epilogue, and at the
-        # fused last K-tile's exit (the MFMA-to-store path has none)
-        assert len(re.findall(r"s_waitcnt vmcnt\(0\)", loop)) == 2
-        assert len(re.findall(r"s_waitcnt vmcnt\(16\) lgkmcnt\(0\)", b)) >= 4
+        # the K-loop (the backward branch over 2 K-tiles' 256 MFMAs) drains nothing: its
+        # waits are the counted vmcnt(16) ones; the drains sit outside it (before the
+        # separate epilogue and at the fused last K-tile's exit). Found by its back edge,
+        # not by block order, which the compiler is free to change.
+        loops = _loops(b, min_mfma=256)
+        assert len(loops) == 1, [n for n, _ in loops]
+        body = loops[0][1]
+        assert not re.findall(r"s_waitcnt vmcnt\(0\)", body)
+        assert len(re.findall(r"s_waitcnt vmcnt\(16\) lgkmcnt\(0\)", body)) >= 4
+        assert len(re.findall(r"s_waitcnt vmcnt\(0\)", b)) >= 2
         # loop body: 2 K-tiles x 8 blocks x 16 MFMAs, one odd tail K-tile, the fused last K-tile
         assert len(re.findall(mfma, b)) == 4 * 128
         assert len(re.findall(r"buffer_load_dwordx4 .* lds", b)) >= 3 * 16
