@@ -126,6 +126,7 @@ int choose_splitk(const Problem& p, int kernel);
 // order as one launch and the rest split S ways; {0, 1, 0}: one launch.
 struct TailSplit {
   int m1, S, tiles_dp;
+  int sub;  // parts per 256x256 tile of a refined tail's second launch (1: split-K tail)
 };
 TailSplit tail_split(const Problem& p, int kernel);
 
@@ -140,7 +141,7 @@ int resolve_kernel(const Problem& p, int kernel);
 struct PlanInfo {
   int kernel, splitk;
   double cost_us;
-  int tail_m1, tail_S, tail_tiles_dp;
+  int tail_m1, tail_S, tail_tiles_dp, tail_sub;
 };
 PlanInfo plan_info(const Problem& p, int kernel);
 

@@ -227,22 +227,22 @@ int64_t splitk_for(const at::Tensor& A, const at::Tensor& B, c10::optional<at::T
   return pdmb::choose_splitk(p, (int)kernel);
 }
 
-// {M1, S, T1}: auto runs rows [0, M1) unsplit and [M1, M) split S ways, or
-// (tile-range form) tiles [0, T1) unsplit and the rest split S ways;
-// {0, 1, 0}: one launch.
-std::tuple<int64_t, int64_t, int64_t> tail_split_for(const at::Tensor& A, const at::Tensor& B,
+// {M1, S, T1, R}: auto runs rows [0, M1) unsplit and [M1, M) split S ways, or
+// (tile-range form) tiles [0, T1) unsplit and the rest split S ways — or, R > 1
+// (refined tail), cut into R smaller tiles each; {0, 1, 0, 1}: one launch.
+std::tuple<int64_t, int64_t, int64_t, int64_t> tail_split_for(const at::Tensor& A, const at::Tensor& B,
                                                      c10::optional<at::Tensor> C, int64_t kernel,
                                                      int64_t cus) {
   pdmb::Problem p = make_problem(A, B, opt(C));
   p.cus = (int)cus;
   const auto t = pdmb::tail_split(p, (int)kernel);
-  return {t.m1, t.S, t.tiles_dp};
+  return {t.m1, t.S, t.tiles_dp, t.sub};
 }
 
 // The planner's decision for a SHAPE (no tensors: contiguous operands at an
 // aligned stand-in address, so it runs without a GPU): (kernel id, split-K,
-// model cost us, tail M1, tail S, tail T1). dtype: 0 f32, 1 f16, 2 bf16, 3 fp8.
-std::tuple<int64_t, int64_t, double, int64_t, int64_t, int64_t> plan_shape(int64_t dtype, int64_t M, int64_t N,
+// model cost us, tail M1, tail S, tail T1, tail R). dtype: 0 f32, 1 f16, 2 bf16, 3 fp8.
+std::tuple<int64_t, int64_t, double, int64_t, int64_t, int64_t, int64_t> plan_shape(int64_t dtype, int64_t M, int64_t N,
                                                                   int64_t K, int64_t batch,
                                                                   int64_t kernel, int64_t cus) {
   pdmb::Problem p{};
@@ -260,7 +260,7 @@ std::tuple<int64_t, int64_t, double, int64_t, int64_t, int64_t> plan_shape(int64
   p.sC = M * N;
   p.cus = (int)cus;
   const pdmb::PlanInfo r = pdmb::plan_info(p, (int)kernel);
-  return {r.kernel, r.splitk, r.cost_us, r.tail_m1, r.tail_S, r.tail_tiles_dp};
+  return {r.kernel, r.splitk, r.cost_us, r.tail_m1, r.tail_S, r.tail_tiles_dp, r.tail_sub > 0 ? r.tail_sub : 1};
 }
 
 // Total milliseconds for `iters` timed launches (after `warmup`).
@@ -501,7 +501,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("splitk_for", &splitk_for, "W4 K slices for this problem (0: not W4)", py::arg("A"),
         py::arg("B"), py::arg("out") = py::none(), py::arg("kernel") = 0, py::arg("splitk") = 0,
         py::arg("cus") = 0);
-  m.def("tail_split_for", &tail_split_for, "auto's wave-quantisation tail {M1, S, T1} ({0, 1, 0}: none)",
+  m.def("tail_split_for", &tail_split_for, "auto's wave-quantisation tail {M1, S, T1, R} ({0, 1, 0, 1}: none)",
         py::arg("A"), py::arg("B"), py::arg("out") = py::none(), py::arg("kernel") = 0,
         py::arg("cus") = 0);
   m.def("bench", &bench, "native hipEvent timing loop; returns total ms", py::arg("A"),

@@ -424,12 +424,23 @@ int choose_splitk(const Problem& p, int kernel) {
 // wave boundary (6144^3: 24 x 24 tiles, no row count gives 256 or 512 tiles);
 // tiles always can. Priced like the row form, taken when it is the cheaper of
 // the two; PDMB_TILE_TAIL=0 disables it, =S forces S (A/B, read per call).
+//
+// Refined tail (round 4): the remaining (< one wave of) tiles are not split
+// along K but cut into the tile family's smaller tiles — 256x128 halves or
+// 128x128 quarters (gemm_tile.hip, tile_span over W4's tile order), each
+// running the whole K unsplit: no fp32 slabs to write and combine, which for
+// fp8 (half a bf16 tile's compute per output byte) costs as much as the
+// compute it saves. Priced by the same model; PDMB_TAIL_REFINE=0 disables,
+// =2 / =4 forces halves / quarters (A/B, read per call).
 struct TailPlan {
   int m1 = 0;        // rows of the first (unsplit) launch; 0 = one launch (row form)
   int S = 1;         // K slices of the tail launch
   int tiles_dp = 0;  // tile-range form: tiles of the first launch (> 0), rest split S ways
+  int sub = 0;       // refined tail: the tile-family kernel of the second launch (S == 1)
   bool active() const { return m1 > 0 || tiles_dp > 0; }
 };
+
+static int sub_parts(int kernel) { return kernel == kT128 || kernel == kFp8T128 ? 4 : 2; }
 
 static int tail_kernel(const Problem& p) { return p.dtype == kFP8 ? kFp8W4 : kMfmaW4; }
 
@@ -452,9 +463,27 @@ static TailPlan tail_plan(const Problem& p, int kernel) {
     if (force != 0 && force != 2 && force != 4 && force != 8) force = -1;
     const long long T = (long long)tm * tn * batch;
     const int nk = ktiles(p);
+    const char* renv = std::getenv("PDMB_TAIL_REFINE");
+    const int rforce = renv ? std::atoi(renv) : -1;
+    const bool fp8 = p.dtype == kFP8;
     for (long long dp = slots; dp < T && force != 0; dp += slots) {
       const long long rest = T - dp;
       const double c1 = plan_cost_tiles(p, kw, 1, dp);
+      if (rest < slots && rforce != 0 && force <= 0) {  // refined: the last partial wave in smaller tiles
+        for (int ks : {fp8 ? kFp8T256x128 : kT256x128, fp8 ? kFp8T128 : kT128}) {
+          const int R = sub_parts(ks);
+          if (rforce > 0 && R != rforce) continue;
+          if (!supports(p, ks)) continue;
+          const double c = rforce > 0 ? -1.0 : c1 + plan_cost_tiles(p, ks, 1, rest * R);
+          if (c < bc) {
+            bc = c;
+            best = TailPlan{};
+            best.tiles_dp = (int)dp;
+            best.sub = ks;
+          }
+        }
+      }
+      if (rforce > 0) continue;
       for (int S : {2, 4, 8}) {
         const int per = (nk + S - 1) / S;
         if (rest * S > slots || per < 8 || (S - 1) * per >= nk || rest > kMaxSplitTiles) continue;
@@ -469,6 +498,7 @@ static TailPlan tail_plan(const Problem& p, int kernel) {
       }
     }
   }
+  if (best.sub && bc < 0) return best;  // forced refined tail
   for (int r = 1; r < tm; ++r) {  // r tail tile rows
     Problem a = p, b = p;
     a.M = (tm - r) * 256;
@@ -510,12 +540,13 @@ PlanInfo plan_info(const Problem& p, int kernel) {
   r.tail_m1 = t.m1;
   r.tail_S = t.S;
   r.tail_tiles_dp = t.tiles_dp;
+  r.tail_sub = t.sub ? sub_parts(t.sub) : 1;
   return r;
 }
 
 TailSplit tail_split(const Problem& p, int kernel) {
   const TailPlan t = tail_plan(p, kernel);
-  return {t.m1, t.S, t.tiles_dp};
+  return {t.m1, t.S, t.tiles_dp, t.sub ? sub_parts(t.sub) : 1};
 }
 
 // fp8 W4 split-K (gemm_fp8.hip): grids of 256x256 tiles that fill at most
@@ -849,6 +880,7 @@ static Problem batch_elem(const Problem& p, int b) {
 
 // Split-K slots of a tail plan's second launch.
 static size_t tail_bytes(const Problem& p, const TailPlan& t) {
+  if (t.sub) return 0;  // refined: unsplit
   if (t.tiles_dp > 0) {
     const long long T = tiles_of(p, tail_kernel(p));
     return (size_t)(T - t.tiles_dp) * t.S * 256 * 256 * sizeof(float);
@@ -882,6 +914,27 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel) {
 // stream has no split-K counters yet inside a graph capture, or the workspace
 // was sized for another plan).
 static bool gemm_tail(const Problem& p, const TailPlan& t, hipStream_t stream, hipError_t* e) {
+  if (t.sub && t.tiles_dp > 0) {  // refined: whole waves, then the rest in the tile family's tiles
+    const int G = (device_cus() / 8) * 8;
+    GemmArgs d = to_args(p);
+    d.splitk = 1;
+    d.tile_end = t.tiles_dp;
+    GemmArgs r = to_args(p);
+    r.splitk = 1;
+    r.tile_base = t.tiles_dp;
+    r.tile_span = (int)(tiles_of(p, tail_kernel(p)) - t.tiles_dp);
+    if (p.dtype == kFP8) {
+      const bool s_fits = gemm_fp8_w4s_fits(d) && device_cus() % 8 == 0;
+      if (s_fits) d.pers_grid = G;
+      *e = gemm_fp8_launch(d, s_fits ? 2 : 1, stream);
+    } else {
+      const bool s = w4s_fits(p) && t.tiles_dp >= 2LL * device_cus();
+      if (s) d.pers_grid = G;
+      *e = gemm_w4_launch(p.dtype, d, stream, s ? 7 : 0);
+    }
+    if (*e == hipSuccess) *e = gemm_tile_launch(t.sub, p.dtype, r, stream);
+    return true;
+  }
   if (!p.workspace || p.workspace_bytes < tail_bytes(p, t) || !stream_counters(stream)) return false;
   if (t.tiles_dp > 0) {  // tile-range form (GemmArgs::tile_end / tile_span)
     const int G = (device_cus() / 8) * 8;

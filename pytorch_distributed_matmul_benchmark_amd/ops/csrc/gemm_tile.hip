@@ -328,11 +328,24 @@ __global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
   constexpr int MB = C::MB, NB = C::NB, NS = C::NS;
 
   int bz, tm, tn;
-  map_tile(a, blockIdx.x, bz, tm, tn);
   int slice = 0;  // split-K: grid batch = batch x S, slice innermost (as W4)
-  if (a.splitk > 1) {
-    slice = bz % a.splitk;
-    bz /= a.splitk;
+  if (a.tile_span > 0) {
+    // Refined wave-quantisation tail (gemm_dispatch.cpp tail_plan): the tiles
+    // [tile_base, +tile_span) of W4's 256x256 order (a.tiles_m / tiles_n /
+    // supertile describe that grid), each cut into R = (256/BM) x (256/BN) of
+    // this kernel's tiles; block b is part b / span of local tile b % span.
+    constexpr int RM = 256 / C::BM, RN = 256 / C::BN;
+    const int local = blockIdx.x % a.tile_span, part = blockIdx.x / a.tile_span;
+    map_tile(a, a.tile_base + local, bz, tm, tn);
+    tm = tm * RM + part / RN;
+    tn = tn * RN + part % RN;
+    if (tm * C::BM >= a.M || tn * C::BN >= a.N) return;  // a part past an edge tile's rows / columns
+  } else {
+    map_tile(a, blockIdx.x, bz, tm, tn);
+    if (a.splitk > 1) {
+      slice = bz % a.splitk;
+      bz /= a.splitk;
+    }
   }
   const int kt0 = slice * a.kt_per;
   const int m0 = tm * C::BM, n0 = tn * C::BN;
@@ -512,6 +525,24 @@ __global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
 
 template <class C, bool FUSED = true>
 hipError_t launch(int dt, GemmArgs a, hipStream_t stream) {
+  if (a.tile_end != 0 || a.tile_span < 0 || a.tile_base < 0) return hipErrorInvalidValue;
+  if (a.tile_span > 0) {  // refined tail: W4's 256x256 tile order, R parts per tile, unsplit
+    a.tiles_m = (a.M + 255) / 256;
+    a.tiles_n = (a.N + 255) / 256;
+    a.supertile = choose_supertile(a.tiles_m, a.tiles_n);
+    a.splitk = 1;
+    if ((long long)a.tile_base + a.tile_span > (long long)a.tiles_m * a.tiles_n * a.batch)
+      return hipErrorInvalidValue;
+    constexpr int R = (256 / C::BM) * (256 / C::BN);
+    const long long nb = (long long)a.tile_span * R;
+    if (nb > 0x7fffffffLL) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)nb), block(NT);
+    if (dt == kBF16) hipLaunchKernelGGL((gemm_tile_nn<kBF16, C, FUSED>), grid, block, 0, stream, a);
+    else if (dt == kF16) hipLaunchKernelGGL((gemm_tile_nn<kF16, C, FUSED>), grid, block, 0, stream, a);
+    else if constexpr (C::OCC == 1) hipLaunchKernelGGL((gemm_tile_nn<kFP8, C, FUSED>), grid, block, 0, stream, a);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   a.tiles_m = (a.M + C::BM - 1) / C::BM;  // edge tiles: masked epilogue
   a.tiles_n = (a.N + C::BN - 1) / C::BN;
   const int S = a.splitk > 1 ? a.splitk : 1;

@@ -331,17 +331,18 @@ def splitk_for(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = N
 
 def tail_split_for(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
                    kernel="auto") -> tuple:
-    """(M1, S, T1): auto runs rows [0, M1) as one W4 launch and the remaining
+    """(M1, S, T1, R): auto runs rows [0, M1) as one W4 launch and the remaining
     tile rows as a second, S-way split-K launch that fills the chip
-    (gemm_dispatch.cpp tail_plan), or — fp8's tile-range form, M1 = 0 — the
+    (gemm_dispatch.cpp tail_plan), or — the tile-range form, M1 = 0 — the
     first T1 tiles of its tile order (whole waves) as one launch and the rest
-    S-way split; (0, 1, 0) when the problem runs as one launch."""
+    S-way split, or (R > 1, refined tail) the rest cut into R smaller tiles of
+    the tile family, unsplit; (0, 1, 0, 1) when the problem runs as one launch."""
     if A.device.type != "cuda":
-        return (0, 1, 0)
+        return (0, 1, 0, 1)
     C = _native.load()
     A, B = _prep_pair(A, B)
-    m1, s, t1 = C.tail_split_for(A, B, out, _kid(kernel), _cus())
-    return (int(m1), int(s), int(t1))
+    m1, s, t1, r = C.tail_split_for(A, B, out, _kid(kernel), _cus())
+    return (int(m1), int(s), int(t1), int(r))
 
 
 def bench_matmul(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, iters: int,

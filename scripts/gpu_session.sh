@@ -111,6 +111,20 @@ run_stage() {
                    --rounds 5 --shapes 6144,6144,6144 \
                     6000,6000,6144 7168,7168,7168 10000,10000,10048 10240,10240,10240 16384,16384,16384 &&
                   grep '^{' "$OUT/ab_bf16_tail.log" > "$OUT/ab_bf16_tail.jsonl" ;;
+    tests_tails) step tests_tails 900 $PYT tests/test_gemm_gpu.py tests/test_fp8_gpu.py -m gpu \
+                   -k "tail or tile_range" ;;
+    ab_refine_fp8) step ab_refine_fp8 900 python scripts/ab_kernels.py --dtype float8_e4m3fn \
+                     --kernels auto,auto@PDMB_TAIL_REFINE=0,auto@PDMB_TAIL_REFINE=2,auto@PDMB_TAIL_REFINE=4,torch \
+                     --rounds 5 --shapes 6144,6144,6144 6000,6000,6144 7168,7168,7168 4608,4608,3072 \
+                     10240,10240,10240 5120,5120,5120 &&
+                   grep '^{' "$OUT/ab_refine_fp8.log" > "$OUT/ab_refine_fp8.jsonl" ;;
+    ab_refine_bf16) step ab_refine_bf16 900 python scripts/ab_kernels.py --dtype bfloat16 \
+                      --kernels auto,auto@PDMB_TAIL_REFINE=0,auto@PDMB_TAIL_REFINE=2,auto@PDMB_TAIL_REFINE=4,torch \
+                      --rounds 5 --shapes 6144,6144,6144 6000,6000,6144 7168,7168,7168 10000,10000,10048 \
+                      10240,10240,10240 5120,5120,5120 &&
+                    grep '^{' "$OUT/ab_refine_bf16.log" > "$OUT/ab_refine_bf16.jsonl" ;;
+    race_refine) step race_refine 600 env PDMB_TAIL_REFINE=4 python scripts/race_screen.py --tails --reps 50 &&
+                 grep '^{' "$OUT/race_refine.log" > "$OUT/race_refine.jsonl" ;;
     race_tails) step race_tails 600 python scripts/race_screen.py --tails --reps 50 &&
                 grep '^{' "$OUT/race_tails.log" > "$OUT/race_tails.jsonl" ;;
     race) step race 600 python scripts/race_screen.py --reps 200 && grep '^{' "$OUT/race.log" > "$OUT/race.jsonl" ;;

@@ -305,12 +305,13 @@ def test_fp8_wave_tail_split(M, N, K, form, monkeypatch):
     tile-range form disabled (PDMB_TILE_TAIL=0), the row form runs."""
     if form == "rows":
         monkeypatch.setenv("PDMB_TILE_TAIL", "0")
+    monkeypatch.setenv("PDMB_TAIL_REFINE", "0")  # the split-K forms (refined: test_gemm_gpu.py)
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     Af, Bf = _ints((M, K), g, -2, 3), _ints((K, N), g, -2, 3)
     A8, B8 = Af.to(FP8), _colmajor(Bf.to(FP8))
     big = torch.full((M + 16, N + 24), float("nan"), device="cuda", dtype=torch.bfloat16)
     out = big[:M, :N]
-    m1, S, t1 = gemm.tail_split_for(A8, B8, out)
+    m1, S, t1, _ = gemm.tail_split_for(A8, B8, out)
     if K >= 6144:
         assert (0 < m1 < M and m1 % 256 == 0) != (t1 > 0) and S in (2, 4, 8), (m1, S, t1)
     if form == "rows":

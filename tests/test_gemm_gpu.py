@@ -464,11 +464,13 @@ def test_auto_wave_tail_split(M, N, K, form, monkeypatch):
     B = torch.randint(-3, 4, (K, N), device="cuda", generator=g).to(dt)
     big = torch.full((M + 16, N + 24), float("nan"), device="cuda", dtype=dt)
     out = big[:M, :N]
-    m1, S, t1 = gemm.tail_split_for(A, B, out)
+    if form == "tiles":  # the split-K tile-range form (the refined one is tested below)
+        monkeypatch.setenv("PDMB_TAIL_REFINE", "0")
+    m1, S, t1, r = gemm.tail_split_for(A, B, out)
     if form == "rows":
-        assert 0 < m1 < M and m1 % 256 == 0 and S in (2, 4) and t1 == 0, (m1, S, t1)
+        assert 0 < m1 < M and m1 % 256 == 0 and S in (2, 4) and t1 == 0 and r == 1, (m1, S, t1, r)
     else:
-        assert m1 == 0 and t1 > 0 and t1 % 256 == 0 and S in (2, 4, 8), (m1, S, t1)
+        assert m1 == 0 and t1 > 0 and t1 % 256 == 0 and S in (2, 4, 8) and r == 1, (m1, S, t1, r)
     gemm.matmul(A, B, out=out)
     ref = (A.double() @ B.double()).to(dt)
     assert torch.equal(out, ref)
@@ -497,12 +499,45 @@ def test_batched_tile_range_tail(dtype):
     odt = gemm.out_dtype(dt)
     big = torch.full((2, M + 8, N + 16), float("nan"), device="cuda", dtype=odt)
     out = big[:, :M, :N]
-    m1, S, t1 = gemm.tail_split_for(A, B, out)
-    assert m1 == 0 and t1 == 768 and S > 1, (m1, S, t1)
+    m1, S, t1, r = gemm.tail_split_for(A, B, out)
+    assert m1 == 0 and t1 == 768 and (S > 1 or r > 1), (m1, S, t1, r)
     gemm.matmul(A, B, out=out)
     ref = torch.matmul(Af.double(), Bf.double()).to(odt)
     assert torch.equal(out, ref)
     assert torch.isnan(big[:, :, N:]).all() and torch.isnan(big[:, M:]).all()
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float8_e4m3fn"])
+@pytest.mark.parametrize("M,N,K,R", [(6144, 6144, 6144, 2), (6000, 6000, 6144, 2), (4608, 4608, 3072, 2),
+                                     (6000, 5888, 3072, 4), (6144, 6144, 3072, 4), (4608, 4608, 3072, 4)])
+def test_refined_wave_tail(dtype, M, N, K, R, monkeypatch):
+    """The refined tail (PDMB_TAIL_REFINE=R forces it): whole waves of 256x256
+    tiles as one launch, the remaining tiles of the same order cut into R
+    256x128 / 128x128 tiles of the tile family, unsplit — edge tiles (6000,
+    5888) included: exact on small integers, nothing written outside C,
+    the same bits under graph replay."""
+    monkeypatch.setenv("PDMB_TAIL_REFINE", str(R))
+    dt = getattr(torch, dtype)
+    fp8 = dt == gemm.FP8
+    if not fp8 and (M, N, K) == (4608, 4608, 3072):
+        pytest.skip("bf16 runs this grid as 256x128 tiles (no W4 waves to tail)")
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + R)
+    lo, hi = (-2, 3) if fp8 else (-3, 4)
+    Af = torch.randint(lo, hi, (M, K), device="cuda", generator=g).float()
+    Bf = torch.randint(lo, hi, (K, N), device="cuda", generator=g).float()
+    A = Af.to(dt)
+    B = Bf.t().contiguous().to(dt).t() if fp8 else Bf.to(dt)
+    big = torch.full((M + 16, N + 24), float("nan"), device="cuda", dtype=torch.bfloat16)
+    out = big[:M, :N]
+    m1, S, t1, r = gemm.tail_split_for(A, B, out)
+    assert m1 == 0 and S == 1 and t1 > 0 and t1 % 256 == 0 and r == R, (m1, S, t1, r)
+    gemm.matmul(A, B, out=out)
+    ref = (Af.double() @ Bf.double()).to(torch.bfloat16)
+    assert torch.equal(out, ref)
+    assert torch.isnan(big[:, N:]).all() and torch.isnan(big[M:]).all()
+    C2 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    assert gemm.bench_matmul(A, B, C2, 3, 1, graph=True) > 0
+    assert torch.equal(C2, ref)
 
 
 @pytest.mark.parametrize("M,N,K", [(6000, 6000, 6100), (6000, 5996, 6144)])
@@ -527,10 +562,9 @@ def test_no_tail_split_where_it_does_not_pay():
         A = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
         B = torch.empty(K, N, device="cuda", dtype=torch.bfloat16)
         return gemm.tail_split_for(A, B, **kw)
-    assert tail(5000, 5000, 5056) == (0, 1, 0)      # no split of the last rows fills the chip
-    assert tail(16384, 16384, 16384) == (0, 1, 0)   # whole waves
-    assert tail(8192, 1024, 8192) == (0, 1, 0)      # under-filled: the planner's split / small tiles
-    assert tail(6000, 6000, 6144, kernel="w4") == (0, 1, 0)  # explicit kernels run as asked
+    assert tail(16384, 16384, 16384) == (0, 1, 0, 1)   # whole waves
+    assert tail(8192, 1024, 8192) == (0, 1, 0, 1)      # under-filled: the planner's split / small tiles
+    assert tail(6000, 6000, 6144, kernel="w4") == (0, 1, 0, 1)  # explicit kernels run as asked
 
 
 def test_w4_rejects_unaligned_n():

@@ -20,8 +20,8 @@ def C():
 
 
 def plan(C, dt, M, N, K, b=1, kernel=0, cus=0):
-    k, S, cost, m1, tS, t1 = C.plan_shape(dt, M, N, K, b, kernel, cus)
-    return C.kernel_name(k), S, cost, (m1, tS, t1)
+    k, S, cost, m1, tS, t1, r = C.plan_shape(dt, M, N, K, b, kernel, cus)
+    return C.kernel_name(k), S, cost, (m1, tS, t1, r)
 
 
 @pytest.mark.parametrize("n", [4096, 8192, 16384])
@@ -77,8 +77,8 @@ def test_bf16_plans(C):
     assert plan(C, BF16, 16384, 16384, 16384, cus=-1)[0] == "pdmb_w4_nn"  # shared device
     k, S, _, _ = plan(C, BF16, 4096, 512, 4096)
     assert k in ("pdmb_t128_nn", "pdmb_t256x128_nn", "pdmb_t128x2_nn") or S > 1
-    m1, tS, t1 = plan(C, BF16, 6144, 6144, 6144)[3]  # wave-quantisation tail split:
-    assert tS > 1 and (m1 > 0 or t1 > 0)                # rows, or (round 4) whole tile waves
+    m1, tS, t1, r = plan(C, BF16, 6144, 6144, 6144)[3]  # wave-quantisation tail: rows, or
+    assert (m1 > 0 or t1 > 0) and (tS > 1 or r > 1)       # (round 4) whole tile waves + split / refined
 
 
 def test_fp8_plans(C):
