@@ -483,7 +483,7 @@ static TailPlan tail_plan(const Problem& p, int kernel) {
           }
         }
       }
-      if (rforce > 0) continue;
+      if (rforce > 0 || best.sub) continue;  // a refined tail that pays beats the split-K forms
       for (int S : {2, 4, 8}) {
         const int per = (nk + S - 1) / S;
         if (rest * S > slots || per < 8 || (S - 1) * per >= nk || rest > kMaxSplitTiles) continue;
@@ -498,7 +498,13 @@ static TailPlan tail_plan(const Problem& p, int kernel) {
       }
     }
   }
-  if (best.sub && bc < 0) return best;  // forced refined tail
+  // A refined tail that beats the single launch is taken over every split-K
+  // form, whatever their model price: in every same-process A/B so far it ran
+  // at least as fast (bf16 7168^3: 1474 vs 1429 TFLOPS for the S = 8 tile-range
+  // split the model preferred; fp8 6144^3 2976 vs 2608;
+  // profiles/r4k_*_refined_tail_ab.jsonl) — the model under-prices the split's
+  // slab traffic and short slices.
+  if (best.sub) return best;
   for (int r = 1; r < tm; ++r) {  // r tail tile rows
     Problem a = p, b = p;
     a.M = (tm - r) * 256;
