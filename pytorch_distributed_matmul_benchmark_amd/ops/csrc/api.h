@@ -185,4 +185,8 @@ hipError_t multi_copy(void* const* dsts, const void* const* srcs, const size_t* 
 // Diagnostic builds write per-wave stamps here (device memory; nullptr = off).
 void set_debug_buffer(void* p);
 
+// Stream-K slots per tile (the most workgroups any tile of a span-tile range
+// is shared by, G workgroups over span x nk K-tiles; gemm_fp8.hip gemm_fp8_sk).
+int fp8_sk_slots(long long span, int nk, long long G);
+
 }  // namespace pdmb

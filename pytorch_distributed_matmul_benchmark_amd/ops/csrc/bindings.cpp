@@ -260,7 +260,7 @@ std::tuple<int64_t, int64_t, double, int64_t, int64_t, int64_t, int64_t> plan_sh
   p.sC = M * N;
   p.cus = (int)cus;
   const pdmb::PlanInfo r = pdmb::plan_info(p, (int)kernel);
-  return {r.kernel, r.splitk, r.cost_us, r.tail_m1, r.tail_S, r.tail_tiles_dp, r.tail_sub > 0 ? r.tail_sub : 1};
+  return {r.kernel, r.splitk, r.cost_us, r.tail_m1, r.tail_S, r.tail_tiles_dp, r.tail_sub};
 }
 
 // Total milliseconds for `iters` timed launches (after `warmup`).

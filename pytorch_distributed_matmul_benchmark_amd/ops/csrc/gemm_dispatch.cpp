@@ -437,7 +437,8 @@ struct TailPlan {
   int S = 1;         // K slices of the tail launch
   int tiles_dp = 0;  // tile-range form: tiles of the first launch (> 0), rest split S ways
   int sub = 0;       // refined tail: the tile-family kernel of the second launch (S == 1)
-  bool active() const { return m1 > 0 || tiles_dp > 0; }
+  bool sk = false;   // stream-K (fp8): tiles [tiles_dp, T) as even K-tile shares, S slots per tile
+  bool active() const { return m1 > 0 || tiles_dp > 0 || sk; }
 };
 
 static int sub_parts(int kernel) { return kernel == kT128 || kernel == kFp8T128 ? 4 : 2; }
@@ -498,6 +499,29 @@ static TailPlan tail_plan(const Problem& p, int kernel) {
       }
     }
   }
+  // Stream-K (fp8, gemm_fp8_sk; PDMB_STREAMK=1 forces it, read per call — A/B
+  // until priced): the last 1-2 waves' tiles as G even shares of K-tiles.
+  if (p.dtype == kFP8) {
+    const char* senv = std::getenv("PDMB_STREAMK");
+    if (senv && std::atoi(senv) == 1 && device_cus() % 8 == 0) {
+      const long long T = (long long)tm * tn * batch;
+      const int nk = ktiles(p);
+      const long long G = slots;
+      long long dp = T > 2 * G ? (T / G - 1) * G : 0;  // whole waves before the last 1-2
+      if (T - dp >= 2 * G) dp += G;
+      const long long rest = T - dp;
+      if (rest >= 8 && rest / 8 * nk >= G / 8 && rest <= kMaxSplitTiles) {
+        const int smax = fp8_sk_slots(rest, nk, G);
+        if (smax >= 2 && smax <= 8) {
+          TailPlan k;
+          k.tiles_dp = (int)dp;
+          k.S = smax;
+          k.sk = true;
+          return k;
+        }
+      }
+    }
+  }
   // A refined tail that beats the single launch is taken over every split-K
   // form, whatever their model price: in every same-process A/B so far it ran
   // at least as fast (bf16 7168^3: 1474 vs 1429 TFLOPS for the S = 8 tile-range
@@ -546,13 +570,13 @@ PlanInfo plan_info(const Problem& p, int kernel) {
   r.tail_m1 = t.m1;
   r.tail_S = t.S;
   r.tail_tiles_dp = t.tiles_dp;
-  r.tail_sub = t.sub ? sub_parts(t.sub) : 1;
+  r.tail_sub = t.sk ? 0 : t.sub ? sub_parts(t.sub) : 1;
   return r;
 }
 
 TailSplit tail_split(const Problem& p, int kernel) {
   const TailPlan t = tail_plan(p, kernel);
-  return {t.m1, t.S, t.tiles_dp, t.sub ? sub_parts(t.sub) : 1};
+  return {t.m1, t.S, t.tiles_dp, t.sk ? 0 : t.sub ? sub_parts(t.sub) : 1};
 }
 
 // fp8 W4 split-K (gemm_fp8.hip): grids of 256x256 tiles that fill at most
@@ -887,6 +911,7 @@ static Problem batch_elem(const Problem& p, int b) {
 // Split-K slots of a tail plan's second launch.
 static size_t tail_bytes(const Problem& p, const TailPlan& t) {
   if (t.sub) return 0;  // refined: unsplit
+  if (t.sk) return (size_t)(tiles_of(p, tail_kernel(p)) - t.tiles_dp) * t.S * 256 * 256 * sizeof(float);
   if (t.tiles_dp > 0) {
     const long long T = tiles_of(p, tail_kernel(p));
     return (size_t)(T - t.tiles_dp) * t.S * 256 * 256 * sizeof(float);
@@ -942,6 +967,27 @@ static bool gemm_tail(const Problem& p, const TailPlan& t, hipStream_t stream, h
     return true;
   }
   if (!p.workspace || p.workspace_bytes < tail_bytes(p, t) || !stream_counters(stream)) return false;
+  if (t.sk) {  // fp8 stream-K: whole waves (if any), then the rest as G even K-tile shares
+    const int G = (device_cus() / 8) * 8;
+    *e = hipSuccess;
+    if (t.tiles_dp > 0) {
+      GemmArgs d = to_args(p);
+      d.splitk = 1;
+      d.tile_end = t.tiles_dp;
+      const bool s_fits = gemm_fp8_w4s_fits(d);
+      if (s_fits) d.pers_grid = G;
+      *e = gemm_fp8_launch(d, s_fits ? 2 : 1, stream);
+    }
+    GemmArgs r = to_args(p);
+    r.splitk = t.S;
+    r.tile_base = t.tiles_dp;
+    r.tile_span = (int)(tiles_of(p, tail_kernel(p)) - t.tiles_dp);
+    r.part = (float*)p.workspace;
+    r.flags = stream_counters(stream);
+    r.pers_grid = G;
+    if (*e == hipSuccess) *e = gemm_fp8_launch(r, 3, stream);
+    return true;
+  }
   if (t.tiles_dp > 0) {  // tile-range form (GemmArgs::tile_end / tile_span)
     const int G = (device_cus() / 8) * 8;
     GemmArgs d = to_args(p);

@@ -870,7 +870,158 @@ __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4s(GemmArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA in flight at exit
 }
 
+// ---- fp8 stream-K: tiles [tile_base, +tile_span) as one even share of K-tile
+// iterations per workgroup ---------------------------------------------------
+// For grids of ~1-2 waves of 256x256 tiles (5120^3: 400 tiles = 1.56 waves)
+// neither whole tiles nor a split / refined last wave balance the CUs: half of
+// them would still run two whole tiles. Here the L = span x nk K-tile
+// iterations of the range (map_tile's order, local tile-major) are cut into G
+// = gridDim.x equal contiguous shares (splitk.h sk_begin); workgroup w runs its
+// share as segments, one per tile it touches: the W4 K-loop over the
+// segment's K-range (c.nk = its K-tiles, descriptors based at its first
+// K-tile), then either the plain epilogue (a whole tile) or the stream-K meet
+// (splitk.h sk_meet: contributor index = w - first owner; the last to arrive
+// sums the slots in K order and stores C). a.splitk = slots per tile (the
+// most contributors any tile has, host-computed), a.part / a.flags as split-K.
+__global__ void __launch_bounds__(NT4, 1) gemm_fp8_sk(GemmArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE4];
+  // 32-bit share arithmetic (host: L x G < 2^31), kept in SGPRs: the 64-bit
+  // divisions run on the VALU, and their VGPR results pushed the kernel into
+  // scratch
+  // XCD-local shares: workgroup b runs on XCD b % 8 (dispatch round-robin), and
+  // map_tile gives XCD x the tiles of index = x mod 8, grouped so their A / B
+  // panels share that XCD's L2. So XCD x's G / 8 workgroups share out only
+  // its own tiles (local 8 j + x); one chip-wide share order mixed panels
+  // across XCDs and ran at ~half speed (profiles/r4m_fp8_stream_k_ab.jsonl).
+  const unsigned nk_all = (unsigned)(a.K / BK);
+  const unsigned xcd = blockIdx.x & 7, wi = blockIdx.x >> 3, G = gridDim.x >> 3;
+  const unsigned L = ((unsigned)a.tile_span - xcd + 7) / 8 * nk_all;  // this XCD's K-tile iterations
+  const unsigned hi = __builtin_amdgcn_readfirstlane((wi + 1) * L / G);
+  const int sc = __builtin_amdgcn_readfirstlane(kScaleOne);
+  for (unsigned it = __builtin_amdgcn_readfirstlane(wi * L / G); it < hi;) {
+    // Per-lane values are formed again in every segment from an opaque thread
+    // id: hoisted out of the loop they stayed live across the K-loop and spilled.
+    unsigned tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = (int)(tid & 63);
+    const int wu = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const int wr = wu >> 1, wc = wu & 1;
+    const int l16 = lane & 15, g = lane >> 4;
+    const int jx = __builtin_amdgcn_readfirstlane(it / nk_all);  // this XCD's jx-th tile
+    const int local = 8 * jx + (int)xcd;
+    const int kt0 = __builtin_amdgcn_readfirstlane(it - (unsigned)jx * nk_all);
+    const int cnt = __builtin_amdgcn_readfirstlane(min(hi - it, nk_all - (unsigned)kt0));
+    it += (unsigned)cnt;
+    int bz, tm, tn;
+    map_tile(a, a.tile_base + local, bz, tm, tn);
+    bz = __builtin_amdgcn_readfirstlane(bz);
+    tm = __builtin_amdgcn_readfirstlane(tm);
+    tn = __builtin_amdgcn_readfirstlane(tn);
+    const int m0 = tm * BM, n0 = tn * BN;
+
+    Ctx4 c;
+    c.wu = wu;
+    c.lds0 = (uint32_t)(size_t)((lds_void*)smem);
+    c.lda = a.lda;
+    c.ldb = a.ldb;
+    c.nk = cnt;
+    const long long k0 = (long long)kt0 * BK;
+    const char* Ab = (const char*)a.A + (long long)bz * a.sA + (long long)m0 * a.lda + k0;
+    const char* Bb = (const char*)a.B + (long long)bz * a.sB + (long long)n0 * a.ldb + k0;
+    c.ra = make_rsrc(Ab, (long long)(a.M - m0 - 1) * a.lda + a.K - k0);
+    c.rb = make_rsrc(Bb, (long long)(a.N - n0 - 1) * a.ldb + a.K - k0);
+    {
+      const int r = wu * 8 + (lane >> 3), lc8 = lane & 7;
+      c.voffA = (uint32_t)(r * a.lda + ((lc8 ^ swz(r)) * 16));
+      c.voffB = (uint32_t)(r * a.ldb + ((lc8 ^ swz(r)) * 16));
+      const int sw = swz(l16);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          uint32_t ao = (uint32_t)(st * STAGE4 + (wr * 128 + l16) * BK + (((2 * g + h) ^ sw) * 16));
+          uint32_t bo = (uint32_t)(st * STAGE4 + A_BYTES + (wc * 128 + l16) * BK + (((2 * g + h) ^ sw) * 16));
+          asm volatile("" : "+v"(ao), "+v"(bo));
+          c.aoff[st][h] = ao;
+          c.boff[st][h] = bo;
+        }
+      }
+    }
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // prologue and K-loop: gemm_fp8_w4's, over this segment's cnt K-tiles
+    const int nk = c.nk;
+    const int t1 = nk > 1 ? 1 : 0, t2 = nk > 2 ? 2 : nk - 1;
+#pragma unroll
+    for (int h = 0; h < 16; ++h) issue_piece(c, 0, 0, h);
+#pragma unroll
+    for (int h = 8; h < 16; ++h) issue_piece(c, STAGE4, t1, h);
+#pragma unroll
+    for (int h = 0; h < 8; ++h) issue_piece(c, STAGE4, t1, h);
+    asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+    i32x8 A[8], A7a, A7b, B0[8], B1[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      A[i] = frag(smem + i * 16 * BK, c.aoff[0]);
+      B0[i] = frag(smem + i * 16 * BK, c.boff[0]);
+    }
+    A7a = A[7];
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+    for (int h = 8; h < 16; ++h) issue_piece(c, 0, t2, h);
+    int t = 0;
+    for (; t + 1 < nk; t += 2) {
+      ktile_w4<0>(c, smem, t, acc, A, A7a, A7b, B0, B1, sc);
+      ktile_w4<STAGE4>(c, smem, t + 1, acc, A, A7b, A7a, B1, B0, sc);
+    }
+    if (t < nk) ktile_w4<0>(c, smem, t, acc, A, A7a, A7b, B0, B1, sc);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+
+    const bool whole = kt0 == 0 && (unsigned)cnt == nk_all;
+    SplitSlots sl;
+    int slot = 0, S = 1;
+    if (!whole) {
+      const unsigned tb = (unsigned)jx * nk_all;
+      // owner of iteration x: max w with w L / G <= x (splitk.h sk_owner)
+      const int first = __builtin_amdgcn_readfirstlane((int)(((tb + 1) * G + L - 1) / L) - 1);
+      const int last = __builtin_amdgcn_readfirstlane((int)(((tb + nk_all) * G + L - 1) / L) - 1);
+      S = last - first + 1;
+      slot = (int)wi - first;
+      unsigned tm2 = threadIdx.x;
+      asm volatile("" : "+v"(tm2));
+      if (!sk_meet<8, 8, NT4>(a, smem, local, slot, S, acc, sl, (int)tm2)) continue;
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    char* Cb = (char*)a.C + (long long)bz * a.sC * 2;
+    char* ebuf = smem + 1024 + wu * 2 * kEpiBuf;  // past sk_meet's ticket word
+    const bool interior = m0 + BM <= a.M && n0 + BN <= a.N;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      f32x4 v[8];
+      if (whole) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = acc[i][j];
+      } else {
+        sk_row<8, 8, NT4>(sl, slot, S, i, acc, v);
+      }
+      if (interior)
+        store_block16<kBF16, false, true, 8, true>(ebuf + (i & 1) * kEpiBuf, v, a.alpha, Cb, (long long)a.ldc * 2,
+                                                   m0 + wr * 128 + i * 16, n0 + wc * 128, a.M, a.N, lane);
+      else
+        store_block16<kBF16, true, true, 8, true>(ebuf + (i & 1) * kEpiBuf, v, a.alpha, Cb, (long long)a.ldc * 2,
+                                                  m0 + wr * 128 + i * 16, n0 + wc * 128, a.M, a.N, lane);
+    }
+    // the next segment's prologue refills the stages this epilogue staged through
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+}
+
 }  // namespace k8
+
+int fp8_sk_slots(long long span, int nk, long long G) { return sk_max_owners(span, nk, G); }
 
 bool gemm_fp8_w4s_fits(const GemmArgs& a) {
   const int nk = a.K / k8::BK;
@@ -895,9 +1046,19 @@ hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream) {
   const int S = variant == 1 && a.splitk > 1 ? a.splitk : 1;  // split-K: the W4 kernel only
   const long long all_tiles = (long long)a.tiles_m * a.tiles_n * a.batch;
   if (a.tile_span < 0 || a.tile_base < 0 || a.tile_end < 0 || a.tile_end > all_tiles ||
-      (a.tile_span > 0 && (variant != 1 || (long long)a.tile_base + a.tile_span > all_tiles)) ||
+      (a.tile_span > 0 && ((variant != 1 && variant != 3) || (long long)a.tile_base + a.tile_span > all_tiles)) ||
       (a.tile_end > 0 && a.tile_span > 0))
     return hipErrorInvalidValue;
+  if (variant == 3) {  // stream-K over a tile range (gemm_fp8_sk): grid pers_grid, a.splitk slots per tile
+    const long long L = (long long)a.tile_span * (a.K / k8::BK);
+    if (a.tile_span < 8 || a.pers_grid <= 0 || a.pers_grid % 8 || a.tile_span / 8 * (a.K / k8::BK) < a.pers_grid / 8 ||
+        L * (a.pers_grid + 1) >= (1LL << 31) ||
+        a.splitk < 2 || !a.part || !a.flags ||
+        a.tile_span > kMaxSplitTiles || sk_max_owners(a.tile_span, a.K / k8::BK, a.pers_grid) > a.splitk)
+      return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k8::gemm_fp8_sk, dim3((unsigned)a.pers_grid), dim3(k8::NT4), 0, stream, a);
+    return hipGetLastError();
+  }
   const long long tiles = a.tile_span > 0 ? a.tile_span : a.tile_end > 0 ? a.tile_end : all_tiles;
   if (S > 1) {
     const int nk = a.K / k8::BK;

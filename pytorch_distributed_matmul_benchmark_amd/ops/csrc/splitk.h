@@ -133,4 +133,104 @@ __device__ __forceinline__ void splitk_load_other(const SplitSlots& sl, int slic
                                                      16 /* sc1 */));
 }
 
+// ---- stream-K meet (gemm_fp8.hip gemm_fp8_sk) ------------------------------
+// The same hand-off with a per-tile contributor count: S workgroups (S <=
+// a.splitk, the slots per tile) each carry a K-range of the tile; `slot` is
+// the contributor's index in K order. Whoever arrives last sums the slots in
+// slot order (its own in its own place): bitwise reproducible. A contributor
+// that is not last stores and returns false; its workgroup goes on to its next
+// K-range — the last one waits only for contributors that already took a
+// ticket (past their K-loop), never for one that has not started. t: the
+// thread index (the caller's, formed where it wants it live).
+template <int MB, int NB, int NT>
+__device__ __forceinline__ bool sk_meet(const GemmArgs& a, char* smem, long long tile, int slot, int S,
+                                        f32x4 (&acc)[MB][NB], SplitSlots& out, int t) {
+  constexpr int NBLK = MB * NB;
+  unsigned* arrive = a.flags + 2 * tile;
+  unsigned* done = arrive + 1;
+  int* bcast = (int*)smem;
+  __syncthreads();  // every wave is past its last LDS read before smem is reused
+  if (t == 0)
+    bcast[0] = (int)__hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int ord = bcast[0];
+  const __amdgpu_buffer_rsrc_t rs = splitk_rsrc<NBLK, NT>(a, tile);
+  if (ord < S - 1) {
+#pragma unroll
+    for (int i = 0; i < MB; ++i)
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(u32x4, acc[i][j]), rs,
+            ((slot * NBLK + i * NB + j) * NT + t) * 16, 0, 16 /* sc1: write-through */);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains
+    __syncthreads();
+    if (t == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();  // bcast (LDS) is not rewritten before every wave has read it
+    return false;
+  }
+  if (t == 0) {
+    while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(S - 1))
+      __builtin_amdgcn_s_sleep(1);
+    __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __syncthreads();
+  out.rs = rs;
+  out.t = t;
+  return true;
+}
+
+// Block row i of a stream-K tile's sum over its S contributors, in slot order.
+template <int MB, int NB, int NT>
+__device__ __forceinline__ void sk_row(const SplitSlots& sl, int slot, int S, int i, const f32x4 (&acc)[MB][NB],
+                                       f32x4 (&v)[NB]) {
+  constexpr int NBLK = MB * NB;
+  for (int s = 0; s < S; ++s) {
+    f32x4 q[NB];
+    if (s == slot) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) q[j] = acc[i][j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        q[j] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                       sl.rs, ((s * NBLK + i * NB + j) * NT + sl.t) * 16, 0, 16 /* sc1 */));
+    }
+    if (s == 0) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) v[j] = q[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) v[j] += q[j];
+    }
+  }
+}
+
+// Stream-K partition of L = span x nk K-tile iterations over G workgroups:
+// workgroup w runs iterations [w L / G, (w + 1) L / G) (L >= G: every range is
+// non-empty). Contributors of local tile t: workgroups first .. last.
+__host__ __device__ __forceinline__ long long sk_begin(long long w, long long L, long long G) { return w * L / G; }
+__host__ __device__ __forceinline__ int sk_owner(long long x, long long L, long long G) {
+  // the workgroup whose range holds iteration x: max w with w L / G <= x
+  return (int)(((x + 1) * G + L - 1) / L - 1);
+}
+
+// The most contributors any tile of a stream-K range has (slots per tile):
+// G workgroups in 8 XCD groups of G / 8, XCD x sharing out the range's tiles
+// of index = x mod 8 (gemm_fp8.hip gemm_fp8_sk).
+inline int sk_max_owners(long long span, int nk, long long G) {
+  int m = 0;
+  for (long long x = 0; x < 8; ++x) {
+    const long long tx = (span - x + 7) / 8, L = tx * nk, g = G / 8;
+    for (long long t = 0; t < tx; ++t) {
+      const int c = sk_owner(t * nk + nk - 1, L, g) - sk_owner(t * nk, L, g) + 1;
+      m = c > m ? c : m;
+    }
+  }
+  return m;
+}
+
 }  // namespace pdmb

@@ -125,6 +125,13 @@ run_stage() {
                     grep '^{' "$OUT/ab_refine_bf16.log" > "$OUT/ab_refine_bf16.jsonl" ;;
     race_refine) step race_refine 600 env PDMB_TAIL_REFINE=4 python scripts/race_screen.py --tails --reps 50 &&
                  grep '^{' "$OUT/race_refine.log" > "$OUT/race_refine.jsonl" ;;
+    tests_sk) step tests_sk 600 $PYT tests/test_fp8_gpu.py -m gpu -k "stream_k" ;;
+    ab_sk) step ab_sk 900 python scripts/ab_kernels.py --dtype float8_e4m3fn \
+             --kernels auto,auto@PDMB_STREAMK=1,torch --rounds 5 --shapes 5120,5120,5120 4608,4608,3072 \
+             3072,3072,8192 3584,3584,4096 7168,7168,1024 6000,5888,3072 4352,4352,2048 &&
+           grep '^{' "$OUT/ab_sk.log" > "$OUT/ab_sk.jsonl" ;;
+    race_sk) step race_sk 600 env PDMB_STREAMK=1 python scripts/race_screen.py --tails --reps 50 &&
+             grep '^{' "$OUT/race_sk.log" > "$OUT/race_sk.jsonl" ;;
     race_tails) step race_tails 600 python scripts/race_screen.py --tails --reps 50 &&
                 grep '^{' "$OUT/race_tails.log" > "$OUT/race_tails.jsonl" ;;
     race) step race 600 python scripts/race_screen.py --reps 200 && grep '^{' "$OUT/race.log" > "$OUT/race.jsonl" ;;

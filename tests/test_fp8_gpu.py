@@ -327,3 +327,36 @@ def test_fp8_wave_tail_split(M, N, K, form, monkeypatch):
     C2 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     assert gemm.bench_matmul(A8, B8, C2, 3, 1, graph=True) > 0
     assert torch.equal(C2, (Af.double() @ Bf.double()).to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("shape", [(1, 5120, 5120, 5120), (1, 4608, 4608, 3072), (1, 6000, 5888, 3072),
+                                   (1, 7168, 7168, 1024), (2, 2560, 2560, 5120), (1, 3072, 3072, 8192)])
+def test_fp8_stream_k(shape, monkeypatch):
+    """fp8 stream-K (gemm_fp8_sk, forced by PDMB_STREAMK=1): the whole waves
+    before the last 1-2 as one launch (none below two waves), the rest as 256
+    equal shares of K-tiles — tiles shared by 2 or 3 workgroups meet in K order
+    (splitk.h sk_meet), edge tiles and a batch included. Exact on small
+    integers with alpha, nothing written outside C, the same bits every launch
+    and under graph replay."""
+    monkeypatch.setenv("PDMB_STREAMK", "1")
+    b, M, N, K = shape
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K + b)
+    Af = torch.randint(-2, 3, (b, M, K), device="cuda", generator=g).float()
+    Bf = torch.randint(-2, 3, (b, K, N), device="cuda", generator=g).float()
+    A8 = Af.to(FP8)
+    B8 = Bf.transpose(-1, -2).contiguous().to(FP8).transpose(-1, -2)
+    if b == 1:
+        A8, B8, Af, Bf = A8[0], B8[0], Af[0], Bf[0]
+    big = torch.full((b, M + 16, N + 24), float("nan"), device="cuda", dtype=torch.bfloat16)
+    out = big[:, :M, :N] if b > 1 else big[0, :M, :N]
+    m1, S, t1, r = gemm.tail_split_for(A8, B8, out)
+    assert m1 == 0 and r == 0 and 2 <= S <= 8 and t1 % 256 == 0, (m1, S, t1, r)
+    gemm.matmul(A8, B8, out=out, alpha=0.5)
+    ref = (0.5 * torch.matmul(Af.double(), Bf.double())).to(torch.bfloat16)
+    assert torch.equal(out, ref)
+    assert torch.isnan(big[..., N:]).all() and torch.isnan(big[:, M:]).all()
+    for _ in range(3):
+        assert torch.equal(gemm.matmul(A8, B8, alpha=0.5), ref)
+    C2 = torch.empty_like(ref)
+    assert gemm.bench_matmul(A8, B8, C2, 3, 1, graph=True) > 0
+    assert torch.equal(C2, torch.matmul(Af.double(), Bf.double()).to(torch.bfloat16))

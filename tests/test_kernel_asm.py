@@ -154,7 +154,27 @@ def test_default_build_has_no_experiment_kernels(tmp_path):
     assert ks and all("ELi3ELb0ELi0EE" in k for k in ks), sorted(ks)  # SCHED 3 only
     (tmp_path / "fp8").mkdir()
     ks = _kernels("gemm_fp8.hip", tmp_path / "fp8")
-    assert ks and all("gemm_fp8_w4ILi0ELi0E" in k or "gemm_fp8_w4s" in k for k in ks), sorted(ks)
+    assert ks and all("gemm_fp8_w4ILi0ELi0E" in k or "gemm_fp8_w4s" in k or "gemm_fp8_sk" in k
+                      for k in ks), sorted(ks)
+
+
+def test_fp8_stream_k_kernel(tmp_path):
+    """gemm_fp8_sk (stream-K over a tile range): no scratch (per-lane values are
+    formed per segment, share arithmetic stays scalar), AGPR accumulators, one
+    workgroup per CU, and its K-loop is W4's (counted vmcnt(16) waits at both
+    barriers of each K-tile, no drain inside)."""
+    ks = _kernels("gemm_fp8.hip", tmp_path)
+    name = [k for k in ks if "gemm_fp8_sk" in k]
+    assert name, sorted(ks)
+    k = ks[name[0]]
+    b = k["body"]
+    assert k["spill"] == 0 and "scratch_" not in b
+    assert k["lds"] == 2 * 65536
+    assert re.search(r"v_mfma_f32_16x16x128_f8f6f4 a\[", b)
+    loops = _loops(b, min_mfma=128)
+    inner = [t for _, t in loops if not re.findall(r"s_waitcnt vmcnt\(0\)", t)]
+    assert inner, [n for n, _ in loops]  # the 2-K-tile loop body, drain-free
+    assert len(re.findall(r"s_waitcnt vmcnt\(16\) lgkmcnt\(0\)", inner[0])) >= 4
 
 
 @pytest.mark.parametrize("src,pat,dts,zero_per_kt", [
