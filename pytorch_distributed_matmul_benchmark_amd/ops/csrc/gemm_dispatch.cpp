@@ -499,16 +499,20 @@ static TailPlan tail_plan(const Problem& p, int kernel) {
       }
     }
   }
-  // Stream-K (fp8, gemm_fp8_sk; PDMB_STREAMK=1 forces it, read per call — A/B
+  // Stream-K (fp8, gemm_fp8_sk; PDMB_STREAMK=1 / 2 force it, read per call — A/B
   // until priced): the last 1-2 waves' tiles as G even shares of K-tiles.
   if (p.dtype == kFP8) {
     const char* senv = std::getenv("PDMB_STREAMK");
-    if (senv && std::atoi(senv) == 1 && device_cus() % 8 == 0) {
+    const int mode = senv ? std::atoi(senv) : 0;
+    if ((mode == 1 || mode == 2) && device_cus() % 8 == 0) {
       const long long T = (long long)tm * tn * batch;
       const int nk = ktiles(p);
       const long long G = slots;
-      long long dp = T > 2 * G ? (T / G - 1) * G : 0;  // whole waves before the last 1-2
+      // 1: whole waves before the last 1-2 waves, those stream-K; 2: only the
+      // last partial wave stream-K (the whole waves run in lockstep first)
+      long long dp = T > 2 * G ? (T / G - 1) * G : 0;
       if (T - dp >= 2 * G) dp += G;
+      if (mode == 2) dp = T / G * G;
       const long long rest = T - dp;
       if (rest >= 8 && rest / 8 * nk >= G / 8 && rest <= kMaxSplitTiles) {
         const int smax = fp8_sk_slots(rest, nk, G);

@@ -127,7 +127,7 @@ run_stage() {
                  grep '^{' "$OUT/race_refine.log" > "$OUT/race_refine.jsonl" ;;
     tests_sk) step tests_sk 600 $PYT tests/test_fp8_gpu.py -m gpu -k "stream_k" ;;
     ab_sk) step ab_sk 900 python scripts/ab_kernels.py --dtype float8_e4m3fn \
-             --kernels auto,auto@PDMB_STREAMK=1,torch --rounds 5 --shapes 5120,5120,5120 4608,4608,3072 \
+             --kernels auto,auto@PDMB_STREAMK=1,auto@PDMB_STREAMK=2,torch --rounds 5 --shapes 5120,5120,5120 4608,4608,3072 \
              3072,3072,8192 3584,3584,4096 7168,7168,1024 6000,5888,3072 4352,4352,2048 &&
            grep '^{' "$OUT/ab_sk.log" > "$OUT/ab_sk.jsonl" ;;
     race_sk) step race_sk 600 env PDMB_STREAMK=1 python scripts/race_screen.py --tails --reps 50 &&
