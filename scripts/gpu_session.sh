@@ -48,6 +48,12 @@ run_stage() {
                      --sizes 4096 8192 16384 --rounds 5 --iters 10 || return $?
                    grep '^{' "$OUT/final_$dt.log" > "$OUT/final_$dt.jsonl"
                  done ;;
+    shard_table) for dt in bfloat16 float8_e4m3fn; do
+                   step shard_$dt 600 python scripts/ab_kernels.py --dtype $dt --kernels auto,torch --rounds 5 \
+                     --shapes 16384,2048,16384 8192,2048,8192 8192,1024,8192 4096,2048,4096 4096,1024,4096 \
+                     4096,512,4096 2048,2048,2048 || return $?
+                   grep '^{' "$OUT/shard_$dt.log" > "$OUT/shard_$dt.jsonl"
+                 done ;;
     pmc) (export OUT="$OUT/pmc"; mkdir -p "$OUT"; step pmc 1200 bash scripts/gpu_pmc.sh) ;;
     tests_signal) step tests_signal 600 $PYT tests/test_signal_gpu.py tests/test_overlap_gpu.py -m gpu ;;
     smoke) step smoke 180 python __graft_entry__.py smoke ;;
