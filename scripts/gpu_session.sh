@@ -138,6 +138,10 @@ run_stage() {
            grep '^{' "$OUT/ab_sk.log" > "$OUT/ab_sk.jsonl" ;;
     race_sk) step race_sk 600 env PDMB_STREAMK=1 python scripts/race_screen.py --tails --reps 50 &&
              grep '^{' "$OUT/race_sk.log" > "$OUT/race_sk.jsonl" ;;
+    ab_fp8_onewave) step ab_fp8_onewave 900 python scripts/ab_kernels.py --dtype float8_e4m3fn \
+                      --kernels auto,fp8_w4:2,fp8_w4:4,torch --rounds 5 \
+                      --shapes 4096,4096,4096 8192,2048,8192 16384,2048,16384 4096,8192,4096 &&
+                    grep '^{' "$OUT/ab_fp8_onewave.log" > "$OUT/ab_fp8_onewave.jsonl" ;;
     race_tails) step race_tails 600 python scripts/race_screen.py --tails --reps 50 &&
                 grep '^{' "$OUT/race_tails.log" > "$OUT/race_tails.jsonl" ;;
     race) step race 600 python scripts/race_screen.py --reps 200 && grep '^{' "$OUT/race.log" > "$OUT/race.jsonl" ;;

@@ -507,7 +507,7 @@ def test_batched_tile_range_tail(dtype):
     assert torch.isnan(big[:, :, N:]).all() and torch.isnan(big[:, M:]).all()
 
 
-@pytest.mark.parametrize("dtype", ["bfloat16", "float8_e4m3fn"])
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16", "float8_e4m3fn"])
 @pytest.mark.parametrize("M,N,K,R", [(6144, 6144, 6144, 2), (6000, 6000, 6144, 2), (4608, 4608, 3072, 2),
                                      (6000, 5888, 3072, 4), (6144, 6144, 3072, 4), (4608, 4608, 3072, 4)])
 def test_refined_wave_tail(dtype, M, N, K, R, monkeypatch):
@@ -519,7 +519,7 @@ def test_refined_wave_tail(dtype, M, N, K, R, monkeypatch):
     monkeypatch.setenv("PDMB_TAIL_REFINE", str(R))
     dt = getattr(torch, dtype)
     fp8 = dt == gemm.FP8
-    if not fp8 and (M, N, K) == (4608, 4608, 3072):
+    if not fp8 and (M, N, K) == (4608, 4608, 3072):  # bf16 / fp16
         pytest.skip("bf16 runs this grid as 256x128 tiles (no W4 waves to tail)")
     g = torch.Generator(device="cuda").manual_seed(M + N + K + R)
     lo, hi = (-2, 3) if fp8 else (-3, 4)
@@ -527,15 +527,16 @@ def test_refined_wave_tail(dtype, M, N, K, R, monkeypatch):
     Bf = torch.randint(lo, hi, (K, N), device="cuda", generator=g).float()
     A = Af.to(dt)
     B = Bf.t().contiguous().to(dt).t() if fp8 else Bf.to(dt)
-    big = torch.full((M + 16, N + 24), float("nan"), device="cuda", dtype=torch.bfloat16)
+    odt = gemm.out_dtype(dt)
+    big = torch.full((M + 16, N + 24), float("nan"), device="cuda", dtype=odt)
     out = big[:M, :N]
     m1, S, t1, r = gemm.tail_split_for(A, B, out)
     assert m1 == 0 and S == 1 and t1 > 0 and t1 % 256 == 0 and r == R, (m1, S, t1, r)
     gemm.matmul(A, B, out=out)
-    ref = (Af.double() @ Bf.double()).to(torch.bfloat16)
+    ref = (Af.double() @ Bf.double()).to(odt)
     assert torch.equal(out, ref)
     assert torch.isnan(big[:, N:]).all() and torch.isnan(big[M:]).all()
-    C2 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    C2 = torch.empty(M, N, device="cuda", dtype=odt)
     assert gemm.bench_matmul(A, B, C2, 3, 1, graph=True) > 0
     assert torch.equal(C2, ref)
 
