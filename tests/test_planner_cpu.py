@@ -92,3 +92,26 @@ def test_explicit_two_per_cu_fp32_tile_runs_any_grid(C):
     for shape in ((256, 256, 32), (128, 128, 64), (4096, 512, 4096)):
         k, S, _, _ = plan(C, F32, *shape, kernel=53)
         assert k == "pdmb_f32_t128x2_nn" and S >= 1, (shape, k, S)
+
+
+def test_refined_tail_plans(C, monkeypatch):
+    """The refined wave-quantisation tail (round 4): whole waves of 256^2 tiles,
+    then the last partial wave in 256x128 halves / 128x128 quarters, unsplit —
+    taken over the split-K forms wherever it beats the single launch (the
+    same-process A/B in profiles/r4k_*_refined_tail_ab.jsonl); PDMB_TAIL_REFINE=0
+    falls back to the split-K tile-range form; stream-K only when forced."""
+    monkeypatch.delenv("PDMB_TAIL_REFINE", raising=False)
+    monkeypatch.delenv("PDMB_STREAMK", raising=False)
+    FP8 = 3
+    assert plan(C, BF16, 6144, 6144, 6144)[3] == (0, 1, 512, 4)
+    assert plan(C, BF16, 7168, 7168, 7168)[3] == (0, 1, 768, 4)   # not the S = 8 split
+    assert plan(C, FP8, 6144, 6144, 6144)[3] == (0, 1, 512, 4)
+    assert plan(C, FP8, 4608, 4608, 3072)[3] == (0, 1, 256, 2)
+    assert plan(C, BF16, 16384, 16384, 16384)[3] == (0, 1, 0, 1)  # whole waves: one launch
+    monkeypatch.setenv("PDMB_TAIL_REFINE", "0")
+    m1, S, t1, r = plan(C, BF16, 6144, 6144, 6144)[3]
+    assert r == 1 and S > 1 and (m1 > 0 or t1 > 0)
+    monkeypatch.delenv("PDMB_TAIL_REFINE")
+    monkeypatch.setenv("PDMB_STREAMK", "1")
+    m1, S, t1, r = plan(C, FP8, 5120, 5120, 5120)[3]
+    assert (m1, t1, r) == (0, 0, 0) and S == 2
