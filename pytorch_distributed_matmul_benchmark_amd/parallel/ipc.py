@@ -52,6 +52,7 @@ have no peer memory: ``--allgather ipc`` runs the direct P2P exchange there
 """
 from __future__ import annotations
 
+import atexit
 import os
 from typing import Dict, List, Optional, Tuple
 
@@ -78,6 +79,35 @@ def _mod():
 # handful of buffers (about 1.2 GB at 16k, ws = 8).
 _ARENA: List[torch.Tensor] = []
 _MAPPED: Dict[Tuple[int, bytes], int] = {}  # (device, peer handle) -> mapped address
+
+
+def _release_arena() -> None:
+    """atexit: drain the devices, unmap every peer buffer and free the exported
+    ones while the HIP runtime is still whole, instead of leaving open peer
+    mappings to the runtime's static destructors. By exit every collective has
+    completed (the process group was torn down after a barrier); a peer that
+    still maps this process's memory keeps it alive (dma-buf IPC). (A 2-rank
+    run under rocprofv3 crashed in __cxa_finalize with or without IPC —
+    rocprofv3's shared output database, not this: per-process ``-o x_%pid%``
+    avoids it; profiles/r4t_rocprof_ipc2_exit_segv.log.)"""
+    if not (_MAPPED or _ARENA):
+        return
+    try:
+        mod = _mod()
+        for d in {dev for dev, _ in _MAPPED} | {t.device.index for t in _ARENA}:
+            torch.cuda.synchronize(d)
+        for (dev, _), addr in list(_MAPPED.items()):
+            try:
+                mod.ipc_close(addr, dev)
+            except Exception:
+                pass
+    except Exception:
+        pass
+    _MAPPED.clear()
+    _ARENA.clear()
+
+
+atexit.register(_release_arena)
 
 
 def ipc_empty(shape, dtype: torch.dtype, device: torch.device) -> torch.Tensor:
