@@ -945,6 +945,16 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel) {
   return is_experiment(k) ? experiment_workspace_bytes(p, k) : 0;
 }
 
+// fp8 whole-wave launch of a tail plan: W4S where it streams >= 2 tiles per CU
+// (as bf16's rule), else W4. PDMB_TAIL_DP_W4S=1 (A/B, read per call) takes W4S
+// wherever it fits, the round-3 rule.
+static bool fp8_dp_streams(const GemmArgs& d, long long tiles_dp) {
+  if (!gemm_fp8_w4s_fits(d) || device_cus() % 8 != 0) return false;
+  const char* env = std::getenv("PDMB_TAIL_DP_W4S");
+  if (env && std::atoi(env) == 1) return true;
+  return tiles_dp >= 2LL * device_cus();
+}
+
 // The two launches of a tail plan; false: run the problem as one launch (the
 // stream has no split-K counters yet inside a graph capture, or the workspace
 // was sized for another plan).
@@ -959,7 +969,7 @@ static bool gemm_tail(const Problem& p, const TailPlan& t, hipStream_t stream, h
     r.tile_base = t.tiles_dp;
     r.tile_span = (int)(tiles_of(p, tail_kernel(p)) - t.tiles_dp);
     if (p.dtype == kFP8) {
-      const bool s_fits = gemm_fp8_w4s_fits(d) && device_cus() % 8 == 0;
+      const bool s_fits = fp8_dp_streams(d, t.tiles_dp);
       if (s_fits) d.pers_grid = G;
       *e = gemm_fp8_launch(d, s_fits ? 2 : 1, stream);
     } else {
@@ -978,7 +988,7 @@ static bool gemm_tail(const Problem& p, const TailPlan& t, hipStream_t stream, h
       GemmArgs d = to_args(p);
       d.splitk = 1;
       d.tile_end = t.tiles_dp;
-      const bool s_fits = gemm_fp8_w4s_fits(d);
+      const bool s_fits = fp8_dp_streams(d, t.tiles_dp);
       if (s_fits) d.pers_grid = G;
       *e = gemm_fp8_launch(d, s_fits ? 2 : 1, stream);
     }
@@ -1004,7 +1014,7 @@ static bool gemm_tail(const Problem& p, const TailPlan& t, hipStream_t stream, h
     r.part = (float*)p.workspace;
     r.flags = stream_counters(stream);
     if (p.dtype == kFP8) {
-      const bool s_fits = gemm_fp8_w4s_fits(d) && device_cus() % 8 == 0;
+      const bool s_fits = fp8_dp_streams(d, t.tiles_dp);
       if (s_fits) d.pers_grid = G;
       *e = gemm_fp8_launch(d, s_fits ? 2 : 1, stream);
       if (*e == hipSuccess) *e = gemm_fp8_launch(r, 1, stream);

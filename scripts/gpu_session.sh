@@ -142,6 +142,10 @@ run_stage() {
                       --kernels auto,fp8_w4:2,fp8_w4:4,torch --rounds 5 \
                       --shapes 4096,4096,4096 8192,2048,8192 16384,2048,16384 4096,8192,4096 &&
                     grep '^{' "$OUT/ab_fp8_onewave.log" > "$OUT/ab_fp8_onewave.jsonl" ;;
+    ab_dp_w4s) step ab_dp_w4s 900 python scripts/ab_kernels.py --dtype float8_e4m3fn \
+                 --kernels auto,auto@PDMB_TAIL_DP_W4S=1,fp8_w4,fp8_w4s,torch --rounds 5 \
+                 --shapes 4608,4608,3072 4352,4352,2048 4096,4096,4096 8192,2048,8192 5120,5120,4096 &&
+               grep '^{' "$OUT/ab_dp_w4s.log" > "$OUT/ab_dp_w4s.jsonl" ;;
     race_tails) step race_tails 600 python scripts/race_screen.py --tails --reps 50 &&
                 grep '^{' "$OUT/race_tails.log" > "$OUT/race_tails.jsonl" ;;
     race) step race 600 python scripts/race_screen.py --reps 200 && grep '^{' "$OUT/race.log" > "$OUT/race.jsonl" ;;
