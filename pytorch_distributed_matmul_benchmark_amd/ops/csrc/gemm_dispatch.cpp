@@ -148,11 +148,15 @@ int resolve_kernel(const Problem& p, int kernel) {
     if (kernel == kFp8T128 || kernel == kFp8T256x128) return supports(p, kernel) ? kernel : -1;
     if (is_experiment(kernel)) return experiment_resolve_fp8(p, kernel, s_fits);
     if (kernel != kAuto) return kernel;
-    // the streaming kernel on a device of its own with >= 2 tiles per CU (as W4S)
+    // the streaming kernel on a device of its own with more than one wave of
+    // tiles (bf16's W4S waits for 2 per CU; fp8 measured ahead of W4 from 1.3
+    // per CU: 5120^2 x 4096 2592 vs 2546, 4608^2 x 3072 1977 vs 1960 TFLOPS, and
+    // behind at exactly one, 4096^3 2700 vs 2797; profiles/r4x_fp8_tail_dp_w4_vs_w4s_ab.jsonl)
     const long long T = (long long)(p.M / 256) * (p.N / 256) * (p.batch < 1 ? 1 : p.batch);
     if (s_fits && p.cus == 0 && T >= 2LL * device_cus()) return kFp8W4S;
     // otherwise the planner: fp8 W4 (edge tiles too) or the fp8 tile family
     const Plan pl = plan(p, kAuto);
+    if (pl.kernel == kFp8W4 && pl.splitk <= 1 && s_fits && p.cus == 0 && T > device_cus()) return kFp8W4S;
     return pl.kernel >= 0 ? pl.kernel : kFp8W4;
   }
   if (is_fp8_kernel(kernel)) return -1;

@@ -146,6 +146,9 @@ run_stage() {
                  --kernels auto,auto@PDMB_TAIL_DP_W4S=1,fp8_w4,fp8_w4s,torch --rounds 5 \
                  --shapes 4608,4608,3072 4352,4352,2048 4096,4096,4096 8192,2048,8192 5120,5120,4096 &&
                grep '^{' "$OUT/ab_dp_w4s.log" > "$OUT/ab_dp_w4s.jsonl" ;;
+    ab_fp8_mid) step ab_fp8_mid 900 python scripts/ab_kernels.py --dtype float8_e4m3fn --kernels auto,fp8_w4,torch \
+                  --rounds 5 --shapes 5120,5120,5120 5120,5120,4096 6144,4096,4096 4608,4608,3072 4096,4096,4096 &&
+                grep '^{' "$OUT/ab_fp8_mid.log" > "$OUT/ab_fp8_mid.jsonl" ;;
     race_tails) step race_tails 600 python scripts/race_screen.py --tails --reps 50 &&
                 grep '^{' "$OUT/race_tails.log" > "$OUT/race_tails.jsonl" ;;
     race) step race 600 python scripts/race_screen.py --reps 200 && grep '^{' "$OUT/race.log" > "$OUT/race.jsonl" ;;
