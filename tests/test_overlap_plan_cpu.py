@@ -26,7 +26,7 @@ def test_plan_never_predicts_worse_than_serial(ws, n):
             p = O.plan_overlap(n, cols, n, torch.bfloat16, ws, kind, payload, granule=granule)
             assert p.serial_us == pytest.approx(p.gemm_us + p.comm_us)
             if p.overlap:
-                assert p.overlap_us < 0.97 * p.serial_us
+                assert p.overlap_us < 0.98 * p.serial_us
                 assert p.pieces in p.candidates and p.overlap_us == min(p.candidates.values())
             else:
                 assert p.pieces == 1 and p.rows == 0
