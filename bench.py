@@ -93,8 +93,9 @@ def collective_impl(flag, overlap: bool) -> str:
     """``--allreduce`` / ``--allgather`` as given, or by default: RCCL for the
     serialized modes (the reference's NCCL call, matmul_scaling_benchmark.py:
     150 / :221, so those numbers stay reference-comparable) and ``auto`` for the
-    overlapped ones (the fastest of RCCL / direct / peer-memory, timed on the
-    job's own ranks: the MI355X-native schedule)."""
+    overlapped ones (the faster of RCCL / direct — plus the peer-memory pull
+    with PDMB_AUTO_IPC=1 — timed on the job's own ranks: the MI355X-native
+    schedule)."""
     if flag:
         return flag
     return "auto" if overlap else "rccl"
@@ -271,8 +272,9 @@ class Workload:
     # -- collectives -------------------------------------------------------------
     def _collective(self, impl, kind, t, sources, cs):
         """(implementation, comm object) for ``--allreduce`` / ``--allgather``
-        ``impl``: ``auto`` times RCCL, the direct P2P exchange and the
-        peer-memory pull on this job's ranks and keeps the fastest
+        ``impl``: ``auto`` times RCCL and the direct P2P exchange (and the
+        peer-memory pull with PDMB_AUTO_IPC=1) on this job's ranks and keeps
+        the fastest
         (parallel/overlap.py pick_collective; the times go into the JSON as
         ``collective``); otherwise the named one (``rccl`` on the current
         stream needs no object unless an overlap's comm stream is given)."""
