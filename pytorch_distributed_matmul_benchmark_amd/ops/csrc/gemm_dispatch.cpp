@@ -456,7 +456,13 @@ static TailPlan tail_plan(const Problem& p, int kernel) {
   const int kw = tail_kernel(p);
   if (resolve_kernel(p, kAuto) < 0 || !supports(p, kw)) return best;
   const Plan whole = plan(p, kAuto);  // the best single launch (W4 or a smaller tile)
-  if (whole.kernel != kw || whole.splitk != 1) return best;
+  // A refined tail can also beat a single launch of the tile family (bf16
+  // 6144 x 4096 x 4096: 768 256x128 tiles = 3 waves, vs one W4 wave + one wave
+  // of 256x128 halves); the split-K forms only ever replace a single W4 launch.
+  const bool whole_w4 = whole.kernel == kw && whole.splitk == 1;
+  const bool whole_tile = whole.splitk <= 1 && (whole.kernel == kT256x128 || whole.kernel == kT128 ||
+                                                whole.kernel == kFp8T256x128 || whole.kernel == kFp8T128);
+  if (!whole_w4 && !whole_tile) return best;
   const long long slots = device_cus();
   const int tm = (p.M + 255) / 256, tn = (p.N + 255) / 256, batch = p.batch < 1 ? 1 : p.batch;
   double bc = whole.cost * 0.97;
@@ -488,7 +494,7 @@ static TailPlan tail_plan(const Problem& p, int kernel) {
           }
         }
       }
-      if (rforce > 0 || best.sub) continue;  // a refined tail that pays beats the split-K forms
+      if (rforce > 0 || best.sub || !whole_w4) continue;  // a refined tail that pays beats the split-K forms
       for (int S : {2, 4, 8}) {
         const int per = (nk + S - 1) / S;
         if (rest * S > slots || per < 8 || (S - 1) * per >= nk || rest > kMaxSplitTiles) continue;
@@ -536,7 +542,7 @@ static TailPlan tail_plan(const Problem& p, int kernel) {
   // split the model preferred; fp8 6144^3 2976 vs 2608;
   // profiles/r4k_*_refined_tail_ab.jsonl) — the model under-prices the split's
   // slab traffic and short slices.
-  if (best.sub) return best;
+  if (best.sub || !whole_w4) return best;
   for (int r = 1; r < tm; ++r) {  // r tail tile rows
     Problem a = p, b = p;
     a.M = (tm - r) * 256;

@@ -149,6 +149,10 @@ run_stage() {
     ab_fp8_mid) step ab_fp8_mid 900 python scripts/ab_kernels.py --dtype float8_e4m3fn --kernels auto,fp8_w4,torch \
                   --rounds 5 --shapes 5120,5120,5120 5120,5120,4096 6144,4096,4096 4608,4608,3072 4096,4096,4096 &&
                 grep '^{' "$OUT/ab_fp8_mid.log" > "$OUT/ab_fp8_mid.jsonl" ;;
+    ab_refine_tile) step ab_refine_tile 900 python scripts/ab_kernels.py --dtype bfloat16 \
+                      --kernels auto,auto@PDMB_TAIL_REFINE=0,torch --rounds 5 --shapes 6144,4096,4096 \
+                      4608,4608,3072 3000,7000,5056 8192,3072,4096 4096,6144,4096 &&
+                    grep '^{' "$OUT/ab_refine_tile.log" > "$OUT/ab_refine_tile.jsonl" ;;
     race_tails) step race_tails 600 python scripts/race_screen.py --tails --reps 50 &&
                 grep '^{' "$OUT/race_tails.log" > "$OUT/race_tails.jsonl" ;;
     race) step race 600 python scripts/race_screen.py --reps 200 && grep '^{' "$OUT/race.log" > "$OUT/race.jsonl" ;;

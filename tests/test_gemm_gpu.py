@@ -509,18 +509,20 @@ def test_batched_tile_range_tail(dtype):
 
 @pytest.mark.parametrize("dtype", ["bfloat16", "float16", "float8_e4m3fn"])
 @pytest.mark.parametrize("M,N,K,R", [(6144, 6144, 6144, 2), (6000, 6000, 6144, 2), (4608, 4608, 3072, 2),
-                                     (6000, 5888, 3072, 4), (6144, 6144, 3072, 4), (4608, 4608, 3072, 4)])
+                                     (6000, 5888, 3072, 4), (6144, 6144, 3072, 4), (4608, 4608, 3072, 4),
+                                     (6144, 4096, 4096, 2), (3000, 7000, 5056, 2)])
 def test_refined_wave_tail(dtype, M, N, K, R, monkeypatch):
     """The refined tail (PDMB_TAIL_REFINE=R forces it): whole waves of 256x256
     tiles as one launch, the remaining tiles of the same order cut into R
     256x128 / 128x128 tiles of the tile family, unsplit — edge tiles (6000,
-    5888) included: exact on small integers, nothing written outside C,
+    5888; 3000 x 7000) included, and grids whose single launch would be the
+    tile family itself (bf16 6144 x 4096 x 4096, 4608^2 x 3072): exact on small integers, nothing written outside C,
     the same bits under graph replay."""
     monkeypatch.setenv("PDMB_TAIL_REFINE", str(R))
     dt = getattr(torch, dtype)
     fp8 = dt == gemm.FP8
-    if not fp8 and (M, N, K) == (4608, 4608, 3072):  # bf16 / fp16
-        pytest.skip("bf16 runs this grid as 256x128 tiles (no W4 waves to tail)")
+    if fp8 and K % 128:
+        pytest.skip("fp8 needs K % 128 == 0")
     g = torch.Generator(device="cuda").manual_seed(M + N + K + R)
     lo, hi = (-2, 3) if fp8 else (-3, 4)
     Af = torch.randint(lo, hi, (M, K), device="cuda", generator=g).float()
