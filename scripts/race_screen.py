@@ -23,7 +23,8 @@ SHAPES = [(256, 256, 32), (256, 256, 64), (256, 256, 96), (256, 256, 128), (512,
           (1024, 1024, 1024)]
 # --tails: auto's wave-quantisation tail plans (a whole-wave launch, then a
 # split-K launch whose slices meet in-kernel): the tile-range form on these
-TAIL_SHAPES = [(6144, 6144, 6144), (6000, 6000, 6144), (7168, 7168, 7168), (5120, 5120, 5120), (4608, 4608, 3072)]
+TAIL_SHAPES = [(6144, 6144, 6144), (6000, 6000, 6144), (7168, 7168, 7168), (5120, 5120, 5120), (4608, 4608, 3072),
+               (6144, 4096, 4096), (3000, 7000, 5056)]
 
 
 def main():
