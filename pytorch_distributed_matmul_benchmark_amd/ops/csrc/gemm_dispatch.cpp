@@ -436,6 +436,14 @@ int choose_splitk(const Problem& p, int kernel) {
 // fp8 (half a bf16 tile's compute per output byte) costs as much as the
 // compute it saves. Priced by the same model; PDMB_TAIL_REFINE=0 disables,
 // =2 / =4 forces halves / quarters (A/B, read per call).
+//
+// Decision order (tail_plan): a refined tail that beats the best single
+// launch — a W4 launch, or a tile-family one (bf16 6144 x 4096 x 4096 ran as
+// three waves of 256x128 tiles) — is taken outright; otherwise, against a W4
+// launch only, the tile-range split-K form and then the row form; the fp8
+// stream-K form only when PDMB_STREAMK forces it (measured slower everywhere,
+// profiles/r4o_fp8_stream_k_modes_ab.jsonl). The whole-wave launch streams
+// (W4S / fp8 W4S) only from two tiles per CU.
 struct TailPlan {
   int m1 = 0;        // rows of the first (unsplit) launch; 0 = one launch (row form)
   int S = 1;         // K slices of the tail launch
