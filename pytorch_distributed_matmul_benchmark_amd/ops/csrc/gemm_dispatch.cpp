@@ -450,16 +450,66 @@ struct TailPlan {
   int tiles_dp = 0;  // tile-range form: tiles of the first launch (> 0), rest split S ways
   int sub = 0;       // refined tail: the tile-family kernel of the second launch (S == 1)
   bool sk = false;   // stream-K (fp8): tiles [tiles_dp, T) as even K-tile shares, S slots per tile
+  int f32k = 0;      // exact fp32: the split tail's kernel (kF32T128 / kF32T128x2; 128x128 tiles)
   bool active() const { return m1 > 0 || tiles_dp > 0 || sk; }
 };
 
+// Exact fp32 (f32_t128x2, two 128x128 workgroups per CU: a wave is 2 x CUs
+// tiles): the whole waves as one launch, the remaining tiles split S ways as
+// one wave of f32_t128 (one workgroup per CU). Measured (TFLOPS, no tail ->
+// tail, hipBLASLt; profiles/r5f_f32_tail_ab.jsonl): 5120^3 137.6 -> 148.1
+// (143.3), 3072^3 125.8 -> 141.4 (136.2), 5120^2 x 2048 128.3 -> 144.2
+// (132.0), 7168^3 146.2 -> 149.6 (144.9), 9216^3 145.3 -> 150.4 (142.0). Priced against
+// the last partial wave as it runs unsplit — lightly loaded CUs, about one
+// f32_t128 tile time (plan() prices it as a full two-per-CU wave).
+// PDMB_TILE_TAIL=0 disables it (A/B).
+static TailPlan f32_tail_plan(const Problem& p) {
+  TailPlan best;
+  const char* env = std::getenv("PDMB_TILE_TAIL");
+  if (env && std::atoi(env) == 0) return best;
+  if (!supports(p, kF32T128) || !supports(p, kF32T128x2)) return best;
+  const Plan whole = plan(p, kAuto);  // the best single launch (possibly split: 5120^3 ran f32_t128 x 2)
+  if (whole.kernel != kF32T128x2 && whole.kernel != kF32T128) return best;
+  const long long cus = device_cus(), slots2 = 2 * cus;
+  const long long T = tiles_of(p, kF32T128x2);
+  const long long dp = T / slots2 * slots2, rest = T - dp;
+  if (dp == 0 || rest == 0 || rest > cus || rest > kMaxSplitTiles) return best;
+  const int nk = ktiles(p);
+  const double c1 = plan_cost_tiles(p, kF32T128x2, 1, dp);
+  double base = whole.cost;
+  if (whole.kernel == kF32T128x2 && whole.splitk <= 1)  // its light last wave
+    base = std::min(base, c1 + plan_cost_tiles(p, kF32T128, 1, rest));
+  double bc = base * 0.97;
+  // the tail on f32_t128 only: a split f32_t128x2 tail (4352^3: 132 tiles x 2)
+  // measured 3 % slower than no tail (profiles/r5f_f32_tail_ab.jsonl)
+  for (int k : {kF32T128}) {
+    const long long slots = cus * model_of(k).occ;
+    for (int S : {2, 4, 8}) {
+      const int per = (nk + S - 1) / S;
+      if (rest * S > slots || per < 8 || (S - 1) * per >= nk) continue;
+      const double c = c1 + plan_cost_tiles(p, k, S, rest);
+      if (c < bc) {
+        bc = c;
+        best = TailPlan{};
+        best.tiles_dp = (int)dp;
+        best.S = S;
+        best.f32k = k;
+      }
+    }
+  }
+  return best;
+}
+
 static int sub_parts(int kernel) { return kernel == kT128 || kernel == kFp8T128 ? 4 : 2; }
 
-static int tail_kernel(const Problem& p) { return p.dtype == kFP8 ? kFp8W4 : kMfmaW4; }
+static int tail_kernel(const Problem& p) {
+  return p.dtype == kFP8 ? kFp8W4 : p.dtype == kF32 ? kF32T128x2 : kMfmaW4;
+}
 
 static TailPlan tail_plan(const Problem& p, int kernel) {
   TailPlan best;
   if (kernel != kAuto || p.splitk != 0 || p.cus > 0 || p.sig) return best;
+  if (p.dtype == kF32 && p.K > 0) return f32_tail_plan(p);
   if ((p.dtype != kBF16 && p.dtype != kF16 && p.dtype != kFP8) || p.M <= 256 || p.K <= 0) return best;
   const int kw = tail_kernel(p);
   if (resolve_kernel(p, kAuto) < 0 || !supports(p, kw)) return best;
@@ -933,6 +983,7 @@ static Problem batch_elem(const Problem& p, int b) {
 // Split-K slots of a tail plan's second launch.
 static size_t tail_bytes(const Problem& p, const TailPlan& t) {
   if (t.sub) return 0;  // refined: unsplit
+  if (t.f32k) return (size_t)(tiles_of(p, kF32T128x2) - t.tiles_dp) * t.S * 128 * 128 * sizeof(float);
   if (t.sk) return (size_t)(tiles_of(p, tail_kernel(p)) - t.tiles_dp) * t.S * 256 * 256 * sizeof(float);
   if (t.tiles_dp > 0) {
     const long long T = tiles_of(p, tail_kernel(p));
@@ -999,6 +1050,20 @@ static bool gemm_tail(const Problem& p, const TailPlan& t, hipStream_t stream, h
     return true;
   }
   if (!p.workspace || p.workspace_bytes < tail_bytes(p, t) || !stream_counters(stream)) return false;
+  if (t.f32k) {  // exact fp32: whole two-per-CU waves, then the rest split S ways as one wave
+    GemmArgs d = to_args(p);
+    d.splitk = 1;
+    d.tile_end = t.tiles_dp;
+    GemmArgs r = to_args(p);
+    r.splitk = t.S;
+    r.tile_base = t.tiles_dp;
+    r.tile_span = (int)(tiles_of(p, kF32T128x2) - t.tiles_dp);
+    r.part = (float*)p.workspace;
+    r.flags = stream_counters(stream);
+    *e = gemm_f32_tile_launch(d, stream, 2);
+    if (*e == hipSuccess) *e = gemm_f32_tile_launch(r, stream, t.f32k == kF32T128x2 ? 2 : 0);
+    return true;
+  }
   if (t.sk) {  // fp8 stream-K: whole waves (if any), then the rest as G even K-tile shares
     const int G = (device_cus() / 8) * 8;
     *e = hipSuccess;

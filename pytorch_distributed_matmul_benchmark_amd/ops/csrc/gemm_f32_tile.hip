@@ -215,11 +215,22 @@ __global__ void __launch_bounds__(NT, NS == 2 ? 2 : 1) gemm_f32_t128(GemmArgs a)
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
   int bz, tm, tn;
-  map_tile(a, blockIdx.x, bz, tm, tn);
   int slice = 0;  // split-K: grid batch = batch x S, slice innermost (as W4)
-  if (a.splitk > 1) {
-    slice = bz % a.splitk;
-    bz /= a.splitk;
+  long long meet_tile;
+  if (a.tile_span > 0) {
+    // the split tail of a tile-range plan (gemm_dispatch.cpp tail_plan): local
+    // tile b % span of [tile_base, +span) in map_tile's order, slice b / span
+    const int local = blockIdx.x % a.tile_span;
+    slice = blockIdx.x / a.tile_span;
+    map_tile(a, a.tile_base + local, bz, tm, tn);
+    meet_tile = local;
+  } else {
+    map_tile(a, blockIdx.x, bz, tm, tn);
+    if (a.splitk > 1) {
+      slice = bz % a.splitk;
+      bz /= a.splitk;
+    }
+    meet_tile = ((long long)bz * a.tiles_m + tm) * a.tiles_n + tn;
   }
   const int kt0 = slice * a.kt_per;
   const int m0 = tm * BM, n0 = tn * BN;
@@ -318,8 +329,7 @@ __global__ void __launch_bounds__(NT, NS == 2 ? 2 : 1) gemm_f32_t128(GemmArgs a)
 
   SplitSlots sl;
   const bool split = a.splitk > 1;
-  if (split && !splitk_meet<MB, NB, NT>(a, smem, ((long long)bz * a.tiles_m + tm) * a.tiles_n + tn,
-                                        slice, acc, sl))
+  if (split && !splitk_meet<MB, NB, NT>(a, smem, meet_tile, slice, acc, sl))
     return;
 
   // Epilogue through LDS as whole 256-B rows (common.h store_block16_f32),
@@ -385,21 +395,30 @@ bool gemm_f32_tile_supported(const GemmArgs& a, size_t align_a, size_t align_b, 
 // a.splitk > 1: split-K with a.part / a.flags (gemm_dispatch.cpp f32 planner).
 // variant 0: kF32T128 (4 stages, b128 B reads); 2: kF32T128x2 (2 stages, two
 // workgroups per CU); experiment builds: 1 = b32 B reads (round 3's first version).
+// Tile-range launches (gemm_dispatch.cpp tail_plan, as gemm_w4.hip's):
+// tile_end > 0 runs tiles [0, tile_end) of map_tile's order unsplit (the
+// whole waves); tile_span > 0 runs tiles [tile_base, +span), each split
+// a.splitk ways (the meet's tile id is the local index).
 hipError_t gemm_f32_tile_launch(GemmArgs a, hipStream_t stream, int variant) {
   a.tiles_m = (a.M + kf32t::BM - 1) / kf32t::BM;
   a.tiles_n = (a.N + kf32t::BN - 1) / kf32t::BN;
   a.supertile = choose_supertile(a.tiles_m, a.tiles_n);
   const int S = a.splitk > 1 ? a.splitk : 1;
+  const long long all_tiles = (long long)a.tiles_m * a.tiles_n * a.batch;
+  if (a.tile_span < 0 || a.tile_base < 0 || a.tile_end < 0 || a.tile_end > all_tiles ||
+      (a.tile_end > 0 && (a.tile_span > 0 || S > 1)) ||
+      (a.tile_span > 0 && (long long)a.tile_base + a.tile_span > all_tiles))
+    return hipErrorInvalidValue;
+  const long long tiles = a.tile_span > 0 ? a.tile_span : a.tile_end > 0 ? a.tile_end : all_tiles;
   if (S > 1) {
     const int nk = a.K / kf32t::BK;
     a.kt_per = (nk + S - 1) / S;
-    if ((S - 1) * a.kt_per >= nk || !a.part || !a.flags ||
-        (long long)a.tiles_m * a.tiles_n * a.batch > kMaxSplitTiles)
+    if ((S - 1) * a.kt_per >= nk || !a.part || !a.flags || tiles > kMaxSplitTiles)
       return hipErrorInvalidValue;  // every slice must own >= 1 K-tile
   } else {
     a.splitk = 1;
   }
-  const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch * S;
+  const long long nblocks = tiles * S;
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
 #ifdef PDMB_EXPERIMENTS

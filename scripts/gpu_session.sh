@@ -153,6 +153,11 @@ run_stage() {
                       --kernels auto,auto@PDMB_TAIL_REFINE=0,torch --rounds 5 --shapes 6144,4096,4096 \
                       4608,4608,3072 3000,7000,5056 8192,3072,4096 4096,6144,4096 &&
                     grep '^{' "$OUT/ab_refine_tile.log" > "$OUT/ab_refine_tile.jsonl" ;;
+    tests_f32_tail) step tests_f32_tail 600 $PYT tests/test_gemm_gpu.py -m gpu -k "f32_wave_tail" ;;
+    ab_f32_tail) step ab_f32_tail 900 python scripts/ab_kernels.py --dtype float32 \
+                   --kernels auto,auto@PDMB_TILE_TAIL=0,torch --rounds 3 --iters 5 --shapes 5120,5120,5120 \
+                   7168,7168,7168 9216,9216,9216 3072,3072,3072 5120,5120,2048 4352,4352,4352 7168,7168,1024 &&
+                 grep '^{' "$OUT/ab_f32_tail.log" > "$OUT/ab_f32_tail.jsonl" ;;
     race_tails) step race_tails 600 python scripts/race_screen.py --tails --reps 50 &&
                 grep '^{' "$OUT/race_tails.log" > "$OUT/race_tails.jsonl" ;;
     race) step race 600 python scripts/race_screen.py --reps 200 && grep '^{' "$OUT/race.log" > "$OUT/race.jsonl" ;;

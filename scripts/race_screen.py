@@ -25,6 +25,8 @@ SHAPES = [(256, 256, 32), (256, 256, 64), (256, 256, 96), (256, 256, 128), (512,
 # split-K launch whose slices meet in-kernel): the tile-range form on these
 TAIL_SHAPES = [(6144, 6144, 6144), (6000, 6000, 6144), (7168, 7168, 7168), (5120, 5120, 5120), (4608, 4608, 3072),
                (6144, 4096, 4096), (3000, 7000, 5056)]
+# exact fp32's tail (whole two-per-CU waves, then an f32_t128 split-K wave)
+F32_TAIL_SHAPES = [(3072, 3072, 3072), (5120, 5120, 2048), (7168, 7168, 1024)]
 
 
 def main():
@@ -35,6 +37,7 @@ def main():
                     help="screen auto's tail plans (bf16 and fp8, TAIL_SHAPES) instead")
     a = ap.parse_args()
     cases = ([(kd, shp) for kd in ("auto:bfloat16", "auto:float8_e4m3fn") for shp in TAIL_SHAPES]
+             + [("auto:float32", shp) for shp in F32_TAIL_SHAPES]
              if a.tails else [(kern, shp) for kern in a.kernels.split(",") for shp in SHAPES])
     for kern, (m, n, k) in cases:
         kern, _, dname = kern.partition(":")

@@ -543,6 +543,30 @@ def test_refined_wave_tail(dtype, M, N, K, R, monkeypatch):
     assert torch.equal(C2, ref)
 
 
+@pytest.mark.parametrize("M,N,K", [(3072, 3072, 3072), (5120, 5120, 2048), (5120, 5120, 5120),
+                                   (7168, 7168, 1024)])
+def test_f32_wave_tail_split(M, N, K):
+    """Exact fp32 tail (gemm_dispatch.cpp f32_tail_plan): the whole two-per-CU
+    waves of 128x128 tiles as one f32_t128x2 launch (tile_end), the remaining
+    tiles split S ways as one wave of f32_t128 (tile_span, meeting in-launch): exact on small integers, nothing written outside C, the same
+    bits under graph replay."""
+    dt = torch.float32
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    A = torch.randint(-3, 4, (M, K), device="cuda", generator=g).to(dt)
+    B = torch.randint(-3, 4, (K, N), device="cuda", generator=g).to(dt)
+    m1, S, t1, r = gemm.tail_split_for(A, B)
+    assert m1 == 0 and t1 > 0 and t1 % 512 == 0 and S > 1 and r == 1, (m1, S, t1, r)
+    big = torch.full((M + 16, N + 24), float("nan"), device="cuda", dtype=dt)
+    out = big[:M, :N]
+    gemm.matmul(A, B, out=out)
+    ref = (A.double() @ B.double()).to(dt)
+    assert torch.equal(out, ref)
+    assert torch.isnan(big[:, N:]).all() and torch.isnan(big[M:]).all()
+    C2 = torch.empty(M, N, device="cuda", dtype=dt)
+    assert gemm.bench_matmul(A, B, C2, 3, 1, graph=True) > 0
+    assert torch.equal(C2, ref)
+
+
 @pytest.mark.parametrize("M,N,K", [(6000, 6000, 6100), (6000, 5996, 6144)])
 def test_padded_wave_tail_split(M, N, K):
     """The padded fast path (K or N off the granule) runs the padded problem with
