@@ -443,7 +443,8 @@ int choose_splitk(const Problem& p, int kernel) {
 // launch only, the tile-range split-K form and then the row form; the fp8
 // stream-K form only when PDMB_STREAMK forces it (measured slower everywhere,
 // profiles/r4o_fp8_stream_k_modes_ab.jsonl). The whole-wave launch streams
-// (W4S / fp8 W4S) only from two tiles per CU.
+// (W4S / fp8 W4S) only from two tiles per CU. Exact fp32 has its own split
+// form (f32_tail_plan below).
 struct TailPlan {
   int m1 = 0;        // rows of the first (unsplit) launch; 0 = one launch (row form)
   int S = 1;         // K slices of the tail launch

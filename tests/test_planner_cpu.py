@@ -115,3 +115,17 @@ def test_refined_tail_plans(C, monkeypatch):
     monkeypatch.setenv("PDMB_STREAMK", "1")
     m1, S, t1, r = plan(C, FP8, 5120, 5120, 5120)[3]
     assert (m1, t1, r) == (0, 0, 0) and S == 2
+
+
+def test_f32_tail_plans(C, monkeypatch):
+    """Exact fp32's tail: whole two-per-CU waves of 128^2 tiles, then the rest
+    split-K as one f32_t128 wave, where the light last wave would idle most CUs
+    (profiles/r5g_f32_tail_ab.jsonl); none on whole waves or a full last wave."""
+    monkeypatch.delenv("PDMB_TILE_TAIL", raising=False)
+    F32 = 0
+    assert plan(C, F32, 5120, 5120, 5120)[3] == (0, 4, 1536, 1)
+    assert plan(C, F32, 3072, 3072, 3072)[3] == (0, 4, 512, 1)
+    assert plan(C, F32, 16384, 16384, 16384)[3] == (0, 1, 0, 1)
+    assert plan(C, F32, 6144, 6144, 6144)[3] == (0, 1, 0, 1)   # last wave half full: no split pays
+    monkeypatch.setenv("PDMB_TILE_TAIL", "0")
+    assert plan(C, F32, 5120, 5120, 5120)[3] == (0, 1, 0, 1)
