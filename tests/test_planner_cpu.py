@@ -129,3 +129,21 @@ def test_f32_tail_plans(C, monkeypatch):
     assert plan(C, F32, 6144, 6144, 6144)[3] == (0, 1, 0, 1)   # last wave half full: no split pays
     monkeypatch.setenv("PDMB_TILE_TAIL", "0")
     assert plan(C, F32, 5120, 5120, 5120)[3] == (0, 1, 0, 1)
+
+
+def test_plan_report_script(C, monkeypatch):
+    """scripts/plan_report.py: the planner's choice and tail form per shape."""
+    import importlib.util
+    import os
+
+    monkeypatch.delenv("PDMB_TAIL_REFINE", raising=False)
+    monkeypatch.delenv("PDMB_STREAMK", raising=False)
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts", "plan_report.py")
+    spec = importlib.util.spec_from_file_location("plan_report", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    rows = mod.report(C, "bfloat16", [(6144, 6144, 6144), (16384, 16384, 16384)])
+    assert rows[0]["tail"] == "tiles 512 / refined x4" and rows[0]["kernel"] == "pdmb_w4s"
+    assert rows[1]["tail"] == "-"
+    assert mod.report(C, "float32", [(5120, 5120, 5120)])[0]["tail"] == "tiles 1536 / split 4"
+    assert mod.tail_form(2048, 2, 0, 1) == "rows 2048 / split 2"
