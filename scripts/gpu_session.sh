@@ -158,6 +158,8 @@ run_stage() {
                    --kernels auto,auto@PDMB_TILE_TAIL=0,torch --rounds 3 --iters 5 --shapes 5120,5120,5120 \
                    7168,7168,7168 9216,9216,9216 3072,3072,3072 5120,5120,2048 4352,4352,4352 7168,7168,1024 &&
                  grep '^{' "$OUT/ab_f32_tail.log" > "$OUT/ab_f32_tail.jsonl" ;;
+    shape_fuzz) step shape_fuzz 900 python scripts/shape_fuzz.py --count 40 --seed 1 &&
+                grep '^{' "$OUT/shape_fuzz.log" > "$OUT/shape_fuzz.jsonl" ;;
     race_tails) step race_tails 600 python scripts/race_screen.py --tails --reps 50 &&
                 grep '^{' "$OUT/race_tails.log" > "$OUT/race_tails.jsonl" ;;
     race) step race 600 python scripts/race_screen.py --reps 200 && grep '^{' "$OUT/race.log" > "$OUT/race.jsonl" ;;
