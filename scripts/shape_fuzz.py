@@ -4,8 +4,9 @@ split-K, W4 / W4S, the tail forms, the padded path): per dtype, ``--count``
 shapes drawn from the sizes each dtype's fast path takes (and some it does not,
 which go through the padded path or refuse), small-integer operands whose
 products and sums are exact in fp32, compared with the float64 product rounded
-once to the output dtype. One JSON line per shape; exit status 1 on any
-mismatch.
+once to the output dtype; a share of the shapes batched (2 or 3 GEMMs: the
+tile order runs across the batch). One JSON line per shape; exit status 1 on
+any mismatch.
 
     python scripts/shape_fuzz.py [--count 40] [--seed 1] [--max 7000]
 """
@@ -40,6 +41,7 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--max", type=int, default=7000)
     ap.add_argument("--dtypes", default=",".join(DTYPES))
+    ap.add_argument("--batch-frac", type=float, default=0.2, help="share of batched (bmm) shapes")
     a = ap.parse_args()
     rng = random.Random(a.seed)
     bad = 0
@@ -48,16 +50,18 @@ def main() -> int:
         fp8 = dt == gemm.FP8
         for _ in range(a.count):
             m, n, k = draw(rng, dname, a.max)
-            g = torch.Generator(device="cuda").manual_seed(m * 7 + n * 3 + k)
+            b = rng.choice((2, 3)) if rng.random() < a.batch_frac else 0  # 0: 2-D operands
+            lead = (b,) if b else ()
+            g = torch.Generator(device="cuda").manual_seed(m * 7 + n * 3 + k + b)
             lo, hi = (-2, 3) if fp8 else (-3, 4)
-            Af = torch.randint(lo, hi, (m, k), device="cuda", generator=g).float()
-            Bf = torch.randint(lo, hi, (k, n), device="cuda", generator=g).float()
+            Af = torch.randint(lo, hi, (*lead, m, k), device="cuda", generator=g).float()
+            Bf = torch.randint(lo, hi, (*lead, k, n), device="cuda", generator=g).float()
             if fp8:
-                A, B = Af.to(dt), Bf.t().contiguous().to(dt).t()
+                A, B = Af.to(dt), Bf.transpose(-1, -2).contiguous().to(dt).transpose(-1, -2)
             else:
                 A, B = Af.to(dt), Bf.to(dt)
             odt = gemm.out_dtype(dt)
-            rec = {"dtype": dname, "m": m, "n": n, "k": k}
+            rec = {"dtype": dname, "m": m, "n": n, "k": k, "batch": b}
             try:
                 rec["kernel"] = gemm.kernel_for(A, B)
                 rec["tail"] = list(gemm.tail_split_for(A, B))
@@ -66,14 +70,14 @@ def main() -> int:
                 rec["refused"] = str(e)[:80]
                 print(json.dumps(rec), flush=True)
                 continue
-            want = (Af.double() @ Bf.double()).to(odt)
+            want = torch.matmul(Af.double(), Bf.double()).to(odt)
             d = C != want
             rec["ok"] = not bool(d.any())
             if not rec["ok"]:
                 bad += 1
                 idx = d.nonzero()[0].tolist()
-                rec["first_bad"] = {"row": idx[0], "col": idx[1], "got": C[idx[0], idx[1]].item(),
-                                    "want": want[idx[0], idx[1]].item(), "n_bad": int(d.sum().item())}
+                rec["first_bad"] = {"index": idx, "got": C[tuple(idx)].item(),
+                                    "want": want[tuple(idx)].item(), "n_bad": int(d.sum().item())}
             print(json.dumps(rec), flush=True)
             del A, B, C, Af, Bf, want
     print(json.dumps({"summary": True, "bad": bad}), flush=True)
