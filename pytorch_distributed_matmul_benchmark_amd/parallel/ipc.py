@@ -264,11 +264,9 @@ class IpcGather:
                 cs.wait_event(after)
             if not self._skip_b0:
                 self._barrier()  # B0: every rank's block is final
-            if self.engine == "sdma":
-                blocks[self.me].copy_(inp)
-                jobs = []
-            else:
-                jobs = [(blocks[self.me], inp.data_ptr())]
+            # this rank's own block goes through the same engine (sdma: a NoCU
+            # copy; a torch copy_ would be the runtime's blit kernel)
+            jobs = [(blocks[self.me], inp.data_ptr())]
             jobs += [(blocks[p], self._peer_addr(inp, p))
                      for p in ((self.me + d) % self.ws for d in range(1, self.ws))]
             self._pull(jobs)
