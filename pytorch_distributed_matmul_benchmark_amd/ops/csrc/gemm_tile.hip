@@ -537,10 +537,18 @@ hipError_t launch(int dt, GemmArgs a, hipStream_t stream) {
     const long long nb = (long long)a.tile_span * R;
     if (nb > 0x7fffffffLL) return hipErrorInvalidValue;
     const dim3 grid((unsigned)nb), block(NT);
-    if (dt == kBF16) hipLaunchKernelGGL((gemm_tile_nn<kBF16, C, FUSED>), grid, block, 0, stream, a);
-    else if (dt == kF16) hipLaunchKernelGGL((gemm_tile_nn<kF16, C, FUSED>), grid, block, 0, stream, a);
-    else if constexpr (C::OCC == 1) hipLaunchKernelGGL((gemm_tile_nn<kFP8, C, FUSED>), grid, block, 0, stream, a);
-    else return hipErrorInvalidValue;
+    if (dt == kBF16) {
+      hipLaunchKernelGGL((gemm_tile_nn<kBF16, C, FUSED>), grid, block, 0, stream, a);
+    } else if (dt == kF16) {
+      hipLaunchKernelGGL((gemm_tile_nn<kF16, C, FUSED>), grid, block, 0, stream, a);
+    } else if (dt == kFP8) {
+      if constexpr (C::OCC == 1)
+        hipLaunchKernelGGL((gemm_tile_nn<kFP8, C, FUSED>), grid, block, 0, stream, a);
+      else
+        return hipErrorInvalidValue;
+    } else {
+      return hipErrorInvalidValue;
+    }
     return hipGetLastError();
   }
   a.tiles_m = (a.M + C::BM - 1) / C::BM;  // edge tiles: masked epilogue
