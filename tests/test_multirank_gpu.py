@@ -151,6 +151,18 @@ def test_two_ranks_overlap_check_catches_a_skipped_wait(gather, chunks, tmp_path
     assert "FAIL" in out and "ERROR" not in out
 
 
+@pytest.mark.parametrize("gather", ["rccl", "direct", "ipc"])
+def test_eight_ranks_overlap_check_catches_a_skipped_wait(gather, tmp_path):
+    """The negative control at ws = 8 (8 gloo ranks sharing the GPU): the same
+    overlapped, checked matrix_parallel run FAILs its check when the collectives
+    are issued without their producer dependency. (Its PASS half at ws = 8 is
+    test_eight_ranks_scaling_overlap_checked.)"""
+    args = ["--sizes", "4096", "--iterations", "3", "--warmup", "1", "--mode", "matrix_parallel",
+            "--overlap", "--chunks", "1", "--check", "--allgather", gather]
+    out = _run(8, "matmul_scaling_benchmark.py", *args, env={"PDMB_TEST_SKIP_READY_WAIT": "20000000"})
+    assert "FAIL" in out and "ERROR" not in out
+
+
 # ---- the ws = 8 job shapes on real HIP (8 gloo ranks sharing the GPU) ---------
 def _bench8(*extra):
     env = dict(os.environ)
