@@ -163,6 +163,17 @@ def test_eight_ranks_overlap_check_catches_a_skipped_wait(gather, tmp_path):
     assert "FAIL" in out and "ERROR" not in out
 
 
+def test_eight_ranks_signalled_check_catches_a_skipped_wait():
+    """ws = 8, signalled pieces (16384: the 16384 x 2048 shard GEMM spans two
+    256-workgroup rounds, --chunks 2) through the ipc all-gather: without the
+    producer dependency the check FAILs (its PASS half:
+    test_eight_ranks_scaling_overlap_checked[matrix_parallel-16384-...])."""
+    out = _run(8, "matmul_scaling_benchmark.py", "--sizes", "16384", "--iterations", "2", "--warmup", "1",
+               "--mode", "matrix_parallel", "--overlap", "--chunks", "2", "--check", "--allgather", "ipc",
+               env={"PDMB_TEST_SKIP_READY_WAIT": "800000000"})
+    assert "FAIL" in out and "ERROR" not in out
+
+
 # ---- the ws = 8 job shapes on real HIP (8 gloo ranks sharing the GPU) ---------
 def _bench8(*extra):
     env = dict(os.environ)
