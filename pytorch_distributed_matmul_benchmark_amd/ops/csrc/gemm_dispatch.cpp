@@ -185,6 +185,13 @@ int resolve_kernel(const Problem& p, int kernel) {
       if (!f32fast) return kGeneric;
       {
         const Plan pl = plan(p, kAuto);
+        // Exactly one wave of 256x256 tiles on a long K: the 8-wave f32_256s
+        // measured 1.0-1.3 % ahead of f32_t128x2 (1024 x 16384 x 16384 152.1
+        // vs 150.1, 4096^2 x 14336 152.3 vs 150.8; profiles/r6f_f32_long_k_arms_ab.jsonl)
+        if (pl.kernel == kF32T128x2 && pl.splitk <= 1 && p.cus == 0 && p.K >= 8192 &&
+            (long long)(p.M / 256) * (p.N / 256) * (p.batch < 1 ? 1 : p.batch) == device_cus() &&
+            p.M % 256 == 0 && p.N % 256 == 0)
+          return kF32_256s;
         return pl.kernel >= 0 ? pl.kernel : kF32_256s;
       }
     case kGeneric: return kGeneric;

@@ -147,3 +147,13 @@ def test_plan_report_script(C, monkeypatch):
     assert rows[1]["tail"] == "-"
     assert mod.report(C, "float32", [(5120, 5120, 5120)])[0]["tail"] == "tiles 1536 / split 4"
     assert mod.tail_form(2048, 2, 0, 1) == "rows 2048 / split 2"
+
+
+def test_f32_long_k_one_wave_runs_256s(C):
+    """Exactly one wave of 256x256 tiles on a long K runs the 8-wave f32_256s
+    (measured 0.1-1.6 % ahead of f32_t128x2 there, profiles/r6g_f32_long_k_rule_ab.jsonl);
+    shorter K or more waves keep f32_t128x2."""
+    assert plan(C, 0, 1024, 16384, 16384)[0] == "pdmb_f32_256s_nn"
+    assert plan(C, 0, 4096, 4096, 14336)[0] == "pdmb_f32_256s_nn"
+    assert plan(C, 0, 4096, 4096, 4096)[0] == "pdmb_f32_t128x2_nn"
+    assert plan(C, 0, 8192, 8192, 28672)[0] == "pdmb_f32_t128x2_nn"
