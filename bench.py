@@ -77,6 +77,7 @@ from pytorch_distributed_matmul_benchmark_amd.parallel.overlap import (  # noqa:
     ipc_buffers, measured_plan, pick_collective, reduce_fn, compute_stream)
 from pytorch_distributed_matmul_benchmark_amd.parallel.partition import (  # noqa: E402
     column_shard, global_batch, local_batch)
+from pytorch_distributed_matmul_benchmark_amd.utils import testhooks  # noqa: E402
 from pytorch_distributed_matmul_benchmark_amd.utils.telemetry import (  # noqa: E402
     ClockSampler, visible_gpus)
 
@@ -214,12 +215,15 @@ class Workload:
                     g(self._gathered[key], units[r][2][s:e], after=after, done=done)
                 probe_out = {}
 
-                def probe(s, e):  # one piece's all-gather into a scratch gather buffer
+                def prepare(s, e):  # the probe's scratch gather buffer (agreed before any collective)
                     if e - s not in probe_out:
                         probe_out[e - s] = torch.empty(ws * (e - s), sh.padded, device=dev, dtype=odt)
+
+                def probe(s, e):  # one piece's all-gather into that buffer
+                    prepare(s, e)
                     g(probe_out[e - s], units[0][2][s:e])
                 self._pipeline(a, units, coll, 1, "all_gather", n * sh.padded * Cl.element_size(),
-                               cs, gath, probe=probe, impl=impl)
+                               cs, gath, probe=probe, impl=impl, prepare=prepare)
                 probe_out.clear()
             else:
                 gathered = torch.empty(ws * n, sh.padded, device=dev, dtype=odt)
@@ -282,8 +286,9 @@ class Workload:
         if ws <= 1:
             return ("rccl" if impl == "auto" else impl), cs
         if impl == "auto":
-            impl, obj, times = pick_collective(self.ctx, kind, t, sources, comm=cs)
-            self.coll_choice = {"kind": kind, "chosen": impl, "us": times}
+            spread = {}
+            impl, obj, times = pick_collective(self.ctx, kind, t, sources, comm=cs, spread_out=spread)
+            self.coll_choice = {"kind": kind, "chosen": impl, "us": times, "spread_us": spread}
             return impl, obj
         if impl == "rccl" and cs is None:
             return impl, None
@@ -291,7 +296,7 @@ class Workload:
 
     # -- overlap ---------------------------------------------------------------
     def _pipeline(self, a, units, coll, per_step, kind, payload, cs, gath=None, probe=None,
-                  impl=None):
+                  impl=None, prepare=None):
         """The overlapped step: plan (parallel/overlap.py measured_plan: this
         job's own GEMM and collective times, MAX over ranks; ``probe(s, e)``
         issues one collective of rows [s, e) of ring slot 0), then an
@@ -300,7 +305,7 @@ class Workload:
         self.plan = measured_plan(units, self.ctx, kind, payload, self._mm, probe,
                                   native=self.backend == "native", requested=a.chunks,
                                   steps=max(a.extra_steps, 1), compute=self.comp,
-                                  owner=self._mask, comm=cs)
+                                  owner=self._mask, comm=cs, piece_prepare=prepare)
         if not self.plan.overlap:  # the planner refuses a losing overlap: serialize
             self.step = self._serial_fallback(units, per_step, kind, impl, gath)
             return
@@ -725,6 +730,11 @@ def main() -> int:
                     help="skip the in-job rank-0-alone references (scaling_efficiency = null at N > 1)")
     a = ap.parse_args()
 
+    hooks = testhooks.active()
+    if hooks:  # negative-control fault injection (racy collectives): never a measurement
+        print(f"bench.py: refusing to run with test-only fault injection set: {', '.join(hooks)}",
+              file=sys.stderr, flush=True)
+        return 2
     if "WORLD_SIZE" not in os.environ:
         if a.gpus > 1:
             return _self_launch(a)

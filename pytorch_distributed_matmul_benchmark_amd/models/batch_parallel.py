@@ -73,8 +73,11 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     srcs = [C] + ([units[1][2]] if lb == 1 else [])
     impl = w.allreduce
     if impl == "auto" and distributed:
-        impl, direct, times = pick_collective(ctx, "all_reduce", units[0][2], srcs, comm=cs)
+        spread = {}
+        impl, direct, times = pick_collective(ctx, "all_reduce", units[0][2], srcs, comm=cs,
+                                              spread_out=spread)
         extra["allreduce"], extra["collective_us"] = f"auto:{impl}", times
+        extra["collective_spread_us"] = spread
     else:
         impl = "rccl" if impl == "auto" else impl
         direct = make_gatherer(impl, dev, srcs, comm=cs) if impl != "rccl" and distributed else None

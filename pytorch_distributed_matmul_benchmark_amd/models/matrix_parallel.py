@@ -106,8 +106,11 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
     def gatherer(sources, comm):
         """(impl, comm object) — auto: the fastest of rccl / direct / ipc, timed here."""
         if impl == "auto":
-            chosen, obj, times = pick_collective(ctx, "all_gather", C_local, sources, comm=comm)
+            spread = {}
+            chosen, obj, times = pick_collective(ctx, "all_gather", C_local, sources, comm=comm,
+                                                 spread_out=spread)
             extra["allgather"], extra["collective_us"] = f"auto:{chosen}", times
+            extra["collective_spread_us"] = spread
             return chosen, obj
         if impl == "rccl" and comm is None:
             return impl, None
@@ -119,15 +122,19 @@ def run(w: Workload, ctx: DistContext) -> ModeResult:
         g = gather_fn(impl, gath)
         probe_out = {}
 
-        def probe(s, e):  # one piece's all-gather, into a scratch gather buffer
+        def prepare(s, e):  # the probe's scratch gather buffer (agreed before any collective)
             if e - s not in probe_out:
                 probe_out[e - s] = torch.empty((ws * (e - s), sh.padded), device=dev,
                                                dtype=out_dtype(w))
+
+        def probe(s, e):  # one piece's all-gather, into that buffer
+            prepare(s, e)
             g(probe_out[e - s], units[0][2][s:e])
         # priced from this job's own GEMM and all-gather times (MAX over ranks)
         plan = measured_plan(units, ctx, "all_gather", n * sh.padded * C_local.element_size(), mm,
                              probe, native=w.backend == "native", requested=w.chunks,
-                             steps=max(w.iters, 1), compute=compute, owner=owner, comm=cs)
+                             steps=max(w.iters, 1), compute=compute, owner=owner, comm=cs,
+                             piece_prepare=prepare)
         del probe_out
         extra["plan"] = plan.as_dict()
 

@@ -5,9 +5,12 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <tuple>
+#include <vector>
 
 #include "api.h"
 
@@ -349,8 +352,36 @@ void reduce_sum(const at::Tensor& out, const std::vector<at::Tensor>& srcs) {
 }
 
 // ---- xGMI peer memory (parallel/ipc.py IpcGather) --------------------------
-// A tensor in its own hipMalloc allocation (so its IPC handle maps exactly
-// it, offset 0), freed by hipFree when the last torch reference goes.
+// IPC-exportable tensors come from a process-lifetime pool (the "arena"):
+// every buffer is its own hipMalloc allocation (so its IPC handle maps exactly
+// it, offset 0) and is never freed before exit — when its last torch
+// reference goes it returns to the pool and the next ipc_empty of the same
+// size and device takes it again. Its IPC handle is made once and cached.
+// Why: with buffers freed and re-allocated between benchmark modes, handle
+// bytes, buffer addresses and peer mappings are all reused
+// (scripts/ipc_handle_probe.py records which), so a mapping or a cache entry
+// that outlives its buffer can name memory that is gone
+// (docs/ARCHITECTURE.md "IPC fault"). With the pool, one handle always means
+// one live buffer, and a peer's mapping of it stays valid for the process.
+// PDMB_IPC_ARENA=0 (tests, diagnosis) restores hipFree on release and a
+// fresh handle per call.
+struct IpcBuf {
+  void* p;
+  size_t bytes;
+  int dev;
+  bool in_use;
+  std::string handle;  // cached hipIpcMemHandle_t bytes ("" until first export)
+};
+std::mutex g_ipc_mu;
+std::vector<IpcBuf>& ipc_pool() {
+  static std::vector<IpcBuf>* v = new std::vector<IpcBuf>();  // never destroyed: the runtime may go first
+  return *v;
+}
+bool ipc_arena() {
+  const char* e = std::getenv("PDMB_IPC_ARENA");
+  return !(e && std::string(e) == "0");
+}
+
 at::Tensor ipc_empty(std::vector<int64_t> shape, at::ScalarType dtype, int64_t device) {
   c10::hip::HIPGuard guard((c10::DeviceIndex)device);
   int64_t n = 1;
@@ -359,12 +390,35 @@ at::Tensor ipc_empty(std::vector<int64_t> shape, at::ScalarType dtype, int64_t d
     n *= d;
   }
   const size_t bytes = std::max<size_t>((size_t)n * c10::elementSize(dtype), 256);
-  void* p = nullptr;
-  check_hip(hipMalloc(&p, bytes), "hipMalloc (ipc_empty)");
   const int dev = (int)device;
+  const bool arena = ipc_arena();
+  void* p = nullptr;
+  if (arena) {
+    std::lock_guard<std::mutex> lk(g_ipc_mu);
+    for (auto& b : ipc_pool()) {
+      if (!b.in_use && b.bytes == bytes && b.dev == dev) {
+        b.in_use = true;
+        p = b.p;
+        break;
+      }
+    }
+  }
+  if (!p) {
+    check_hip(hipMalloc(&p, bytes), "hipMalloc (ipc_empty)");
+    if (arena) {
+      std::lock_guard<std::mutex> lk(g_ipc_mu);
+      ipc_pool().push_back({p, bytes, dev, true, std::string()});
+    }
+  }
   return at::from_blob(
       p, shape,
-      [dev](void* q) {
+      [dev, arena](void* q) {
+        if (arena) {  // back to the pool: still allocated, still exported, handle unchanged
+          std::lock_guard<std::mutex> lk(g_ipc_mu);
+          for (auto& b : ipc_pool())
+            if (b.p == q) b.in_use = false;
+          return;
+        }
         int cur = 0;
         (void)hipGetDevice(&cur);
         (void)hipSetDevice(dev);
@@ -374,8 +428,19 @@ at::Tensor ipc_empty(std::vector<int64_t> shape, at::ScalarType dtype, int64_t d
       at::TensorOptions().dtype(dtype).device(at::Device(at::kCUDA, (c10::DeviceIndex)device)));
 }
 
+// (buffers in the pool, of them in use, bytes held)
+std::tuple<int64_t, int64_t, int64_t> ipc_pool_stats() {
+  std::lock_guard<std::mutex> lk(g_ipc_mu);
+  int64_t used = 0, bytes = 0;
+  for (const auto& b : ipc_pool()) {
+    used += b.in_use;
+    bytes += (int64_t)b.bytes;
+  }
+  return {(int64_t)ipc_pool().size(), used, bytes};
+}
+
 // The IPC handle of an ipc_empty tensor (its data pointer must be the base
-// of its allocation).
+// of its allocation); a pooled buffer's handle is made once and reused.
 py::bytes ipc_handle(const at::Tensor& t) {
   TORCH_CHECK(t.is_cuda(), "pdmb: ipc_handle needs a GPU tensor");
   c10::hip::HIPGuard guard(t.device().index());
@@ -384,9 +449,35 @@ py::bytes ipc_handle(const at::Tensor& t) {
   check_hip(hipMemGetAddressRange(&base, &size, t.data_ptr()), "hipMemGetAddressRange");
   TORCH_CHECK(base == t.data_ptr(), "pdmb: ipc_handle: the tensor must start its own allocation "
               "(allocate it with ipc_empty)");
+  {
+    std::lock_guard<std::mutex> lk(g_ipc_mu);
+    for (const auto& b : ipc_pool())
+      if (b.p == base && !b.handle.empty()) return py::bytes(b.handle);
+  }
   hipIpcMemHandle_t h;
   check_hip(hipIpcGetMemHandle(&h, base), "hipIpcGetMemHandle");
-  return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+  std::string hs(reinterpret_cast<const char*>(&h), sizeof(h));
+  {
+    std::lock_guard<std::mutex> lk(g_ipc_mu);
+    for (auto& b : ipc_pool())
+      if (b.p == base) b.handle = hs;
+  }
+  return py::bytes(hs);
+}
+
+// (base, size) of the live allocation or peer mapping that holds `addr` in
+// this process (hipMemGetAddressRange); raises if none does — an address of
+// a closed mapping or a freed buffer (parallel/ipc.py PDMB_IPC_CHECK=1
+// checks every pull's source and destination range against it on the host,
+// before the launch).
+std::tuple<int64_t, int64_t> ipc_range(int64_t addr, int64_t device) {
+  c10::hip::HIPGuard guard((c10::DeviceIndex)device);
+  void* base = nullptr;
+  size_t size = 0;
+  const hipError_t e = hipMemGetAddressRange(&base, &size, (void*)(uintptr_t)addr);
+  TORCH_CHECK(e == hipSuccess, "pdmb: ipc_range: ", std::hex, "0x", addr, std::dec,
+              " is not inside a live allocation or mapping of this process (", hipGetErrorString(e), ")");
+  return {(int64_t)(uintptr_t)base, (int64_t)size};
 }
 
 // Map a peer's allocation into this process (device `device`); returns the
@@ -516,6 +607,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ipc_empty", &ipc_empty, "tensor in its own hipMalloc allocation (IPC-exportable)",
         py::arg("shape"), py::arg("dtype"), py::arg("device"));
   m.def("ipc_handle", &ipc_handle, py::arg("t"));
+  m.def("ipc_pool_stats", &ipc_pool_stats, "(pooled IPC buffers, in use, bytes)");
+  m.def("ipc_range", &ipc_range, "(base, size) of the allocation / mapping holding addr",
+        py::arg("addr"), py::arg("device"));
   m.def("ipc_open", &ipc_open, py::arg("handle"), py::arg("device"));
   m.def("ipc_close", &ipc_close, py::arg("ptr"), py::arg("device"));
   m.def("copy_from_peer", &copy_from_peer, py::arg("dst"), py::arg("src_addr"), py::arg("sdma") = true);

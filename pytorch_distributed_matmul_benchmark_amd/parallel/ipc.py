@@ -68,33 +68,40 @@ def _mod():
     return _native.load(build_if_missing=False)
 
 
-# Process-lifetime IPC arena: every exported buffer this process allocates is
-# kept until the process exits, and every peer buffer it maps stays mapped
-# (opened once per handle). Freeing an exported buffer and unmapping peers'
-# between benchmark modes let the next mode's hipMalloc / hipIpcOpenMemHandle
-# land on the same virtual addresses again (seen in PDMB_IPC_TRACE runs), and
-# an 8-rank one-GPU rehearsal that churned them faulted once
-# (profiles/r4e_selflaunch8_chunks_fault.log); with no unmap / free before
-# exit there is no address reuse to race with. A benchmark process exports a
-# handful of buffers (about 1.2 GB at 16k, ws = 8).
-_ARENA: List[torch.Tensor] = []
-_MAPPED: Dict[Tuple[int, bytes], int] = {}  # (device, peer handle) -> mapped address
+# Process-lifetime IPC arena (default; PDMB_IPC_ARENA=0 bypasses it): the
+# native pool (ops/csrc bindings.cpp ``ipc_empty``) never frees an exported
+# buffer before exit — a released one returns to the pool and is handed out
+# again for the next buffer of its size, under the same cached handle — and
+# every peer buffer this process maps stays mapped, opened once per handle
+# (``_MAPPED``). So one handle always names one live buffer, a peer's mapping
+# of it never goes stale, and nothing is unmapped or freed between benchmark
+# modes. The pool holds each distinct (size, device) a process ever exported
+# at once — a mode's ring and output buffers, re-used by later modes and
+# sweep sizes of the same shapes; a sweep over N sizes holds the buffers of
+# all N (about 1.2 GB per size at 16k, ws = 8). With the arena bypassed
+# (diagnosis / tests), ``close()`` unmaps this gatherer's peer buffers and a
+# released buffer is hipFree'd: the pre-arena behaviour.
+_MAPPED: Dict[Tuple[int, bytes], int] = {}  # arena: (device, peer handle) -> mapped address
+
+
+def arena() -> bool:
+    return os.environ.get("PDMB_IPC_ARENA", "1") != "0"
 
 
 def _release_arena() -> None:
-    """atexit: drain the devices, unmap every peer buffer and free the exported
-    ones while the HIP runtime is still whole, instead of leaving open peer
-    mappings to the runtime's static destructors. By exit every collective has
-    completed (the process group was torn down after a barrier); a peer that
-    still maps this process's memory keeps it alive (dma-buf IPC). (A 2-rank
-    run under rocprofv3 crashed in __cxa_finalize with or without IPC —
-    rocprofv3's shared output database, not this: per-process ``-o x_%pid%``
-    avoids it; profiles/r4t_rocprof_ipc2_exit_segv.log.)"""
-    if not (_MAPPED or _ARENA):
+    """atexit: drain the devices and unmap every peer buffer while the HIP
+    runtime is still whole, instead of leaving open peer mappings to the
+    runtime's static destructors. By exit every collective has completed (the
+    process group was torn down after a barrier); a peer that still maps this
+    process's memory keeps it alive (dma-buf IPC). (A 2-rank run under
+    rocprofv3 crashed in __cxa_finalize with or without IPC — rocprofv3's
+    shared output database, not this: per-process ``-o x_%pid%`` avoids it;
+    profiles/r4t_rocprof_ipc2_exit_segv.log.)"""
+    if not _MAPPED:
         return
     try:
         mod = _mod()
-        for d in {dev for dev, _ in _MAPPED} | {t.device.index for t in _ARENA}:
+        for d in {dev for dev, _ in _MAPPED}:
             torch.cuda.synchronize(d)
         for (dev, _), addr in list(_MAPPED.items()):
             try:
@@ -104,27 +111,32 @@ def _release_arena() -> None:
     except Exception:
         pass
     _MAPPED.clear()
-    _ARENA.clear()
 
 
 atexit.register(_release_arena)
 
 
 def ipc_empty(shape, dtype: torch.dtype, device: torch.device) -> torch.Tensor:
-    """A GPU tensor in its own allocation (IPC-exportable), kept alive by the
-    process-lifetime arena; CPU: plain empty."""
+    """A GPU tensor in its own allocation (IPC-exportable), from the
+    process-lifetime pool (above); CPU: plain empty."""
     if device.type != "cuda":
         return torch.empty(shape, dtype=dtype, device=device)
-    t = _mod().ipc_empty(list(shape), dtype, device.index if device.index is not None else 0)
-    _ARENA.append(t)
-    return t
+    return _mod().ipc_empty(list(shape), dtype, device.index if device.index is not None else 0)
 
 
 def _open(mod, handle: bytes, dev_index: int) -> int:
+    if not arena():
+        return mod.ipc_open(handle, dev_index)
     key = (dev_index, handle)
     if key not in _MAPPED:
         _MAPPED[key] = mod.ipc_open(handle, dev_index)
     return _MAPPED[key]
+
+
+def checking() -> bool:
+    """PDMB_IPC_CHECK=1: every pull / in-place sum is bounds-checked on the host
+    before its launch (``IpcGather._check``)."""
+    return os.environ.get("PDMB_IPC_CHECK") == "1"
 
 
 ENGINES = ("kernel", "sdma")
@@ -168,8 +180,10 @@ class IpcGather:
         if self.engine not in ENGINES:
             raise ValueError(f"IpcGather engine {self.engine!r}: one of {ENGINES}")
         self.blocks = blocks_per_peer()
-        # registered buffers: (local base address, bytes) -> {peer rank: mapped address}
-        self.bufs: List[Tuple[int, int, Dict[int, int]]] = []
+        # registered buffers: (local base address, bytes, {peer rank: mapped
+        # address}, {peer rank: the peer's buffer bytes})
+        self.bufs: List[Tuple[int, int, Dict[int, int], Dict[int, int]]] = []
+        self.check = checking()
         self.copy_streams = ([torch.cuda.Stream(device=self.device)
                               for _ in range(min(COPY_STREAMS, max(self.ws - 1, 0)))]
                              if self.engine == "sdma" else [])
@@ -182,31 +196,37 @@ class IpcGather:
         """Export ``src`` and map every peer's corresponding buffer (collective)."""
         assert src.is_cuda and src.storage_offset() == 0, "register an ipc_empty tensor"
         mod = _mod()
+        nbytes = src.untyped_storage().nbytes()
         try:
-            mine = mod.ipc_handle(src)
+            mine = (mod.ipc_handle(src), nbytes)
         except Exception as e:  # still join the exchange below, so no peer is left waiting
             mine, why = None, e
-        handles: List[Optional[bytes]] = [None] * self.ws
+        handles: List[Optional[Tuple[bytes, int]]] = [None] * self.ws
         dist.all_gather_object(handles, mine, group=self.group)
         if any(h is None for h in handles):
             raise RuntimeError(f"IpcGather: a rank could not export its buffer"
                                f"{f' ({why!r})' if mine is None else ''}")
-        peers, err = {}, None
+        peers, sizes, err = {}, {}, None
         try:
-            for r, h in enumerate(handles):
+            for r, (h, nb) in enumerate(handles):
                 if r != self.me:
                     peers[r] = _open(mod, h, self.dev_index)
+                    sizes[r] = nb
         except Exception as e:
             err = e
         oks: List[Optional[bool]] = [None] * self.ws  # every rank fails together, or none does
         dist.all_gather_object(oks, err is None, group=self.group)
         if not all(oks):
+            if not arena():
+                for a in peers.values():
+                    mod.ipc_close(a, self.dev_index)
             raise RuntimeError(f"IpcGather: mapping a peer's buffer failed on rank(s) "
                                f"{[r for r, ok in enumerate(oks) if not ok]}"
                                f"{f' ({err!r})' if err is not None else ''}")
-        self.bufs.append((src.data_ptr(), src.untyped_storage().nbytes(), peers))
-        _trace(f"rank {self.me} register {src.data_ptr():#x} +{src.untyped_storage().nbytes()} "
-               f"peers {{{', '.join(f'{r}: {a:#x}' for r, a in peers.items())}}}")
+        self.bufs.append((src.data_ptr(), nbytes, peers, sizes))
+        _trace(f"rank {self.me} register {src.data_ptr():#x} +{nbytes} handle "
+               f"{handles[self.me][0][:16].hex()} peers "
+               f"{{{', '.join(f'{r}: {a:#x}+{sizes[r]}' for r, a in peers.items())}}}")
 
     @property
     def npeers(self) -> int:
@@ -218,10 +238,50 @@ class IpcGather:
         p = t.data_ptr()
         if peer == self.me:
             return p
-        for base, nbytes, peers in self.bufs:
+        for base, nbytes, peers, _ in self.bufs:
             if base <= p and p + t.nbytes <= base + nbytes:
                 return peers[peer] + (p - base)
         raise ValueError("IpcGather: the input is not inside a registered buffer")
+
+    def _check(self, what: str, dst: torch.Tensor, src: int, nbytes: int) -> None:
+        """PDMB_IPC_CHECK=1 (host side, before the launch): ``src`` +
+        ``nbytes`` must lie inside one registered peer extent (the peer's own
+        buffer size, exchanged at registration) — or inside this rank's own
+        registered buffer — and both ranges inside a live allocation /
+        mapping of this process (ops ``ipc_range``: a closed mapping or a
+        freed buffer is refused); a violation names the peer, the offset and
+        the extent."""
+        mod = _mod()
+        where = None
+        for base, nb, peers, sizes in self.bufs:
+            if base <= src and src + nbytes <= base + nb:
+                where = (self.me, src - base, nb)
+                break
+            for r, a in peers.items():
+                if a <= src < a + sizes[r]:
+                    if src + nbytes > a + sizes[r]:
+                        raise RuntimeError(
+                            f"IpcGather[{what}]: pull of {nbytes} B from peer {r} at offset "
+                            f"{src - a} runs past its buffer (extent {sizes[r]} B)")
+                    where = (r, src - a, sizes[r])
+                    break
+            if where:
+                break
+        if where is None and nbytes:
+            raise RuntimeError(f"IpcGather[{what}]: source {src:#x} (+{nbytes} B) is in no registered "
+                               f"buffer of this rank or any peer")
+        for addr, n, label in ((src, nbytes, f"source (peer {where[0]}, offset {where[1]}, "
+                                             f"extent {where[2]})" if where else "source"),
+                               (dst.data_ptr(), dst.nbytes, "destination")):
+            if not n:
+                continue
+            try:
+                b, sz = mod.ipc_range(addr, self.dev_index)
+            except RuntimeError as e:
+                raise RuntimeError(f"IpcGather[{what}]: {label} {addr:#x} +{n} B: {e}") from None
+            if addr + n > b + sz:
+                raise RuntimeError(f"IpcGather[{what}]: {label} {addr:#x} +{n} B runs past its "
+                                   f"allocation [{b:#x}, +{sz})")
 
     def _pull(self, jobs) -> None:
         """Issue ``jobs`` [(dst tensor, src address)] on the comm stream (kernel
@@ -233,6 +293,9 @@ class IpcGather:
         mod = _mod()
         cs = self.cs.stream
         _trace(f"rank {self.me} pull " + ", ".join(f"{d.data_ptr():#x}<-{a:#x}+{d.nbytes}" for d, a in jobs))
+        if self.check:
+            for d, a in jobs:
+                self._check("pull", d, a, d.nbytes)
         if self.engine == "kernel":
             mod.peer_copy([d for d, _ in jobs], [a for _, a in jobs], self.blocks)
             return
@@ -313,6 +376,9 @@ class IpcGather:
                     addrs = [self._peer_addr(t, r) + bounds[self.me][0] * es for r in range(self.ws)]
                     _trace(f"rank {self.me} reduce {mine.data_ptr():#x}+{mine.nbytes} <- "
                            + ", ".join(f"{a:#x}" for a in addrs))
+                    if self.check:
+                        for a in addrs:
+                            self._check("reduce", mine, a, mine.nbytes)
                     mod.reduce_sum_addrs(mine, addrs, 0)
                 else:
                     scratch = self.cs._scratch(t, (self.ws - 1) * chunk)
@@ -341,10 +407,17 @@ class IpcGather:
         """Finish with this gatherer: drain the device, then (``barrier``) wait
         for every rank to have done so, so no rank's next mode starts while a
         peer still pulls from this one's buffers; ``barrier=False`` when not
-        every rank holds a gatherer (the caller runs a common barrier). The
-        mappings themselves stay open for the process (the arena above)."""
+        every rank holds a gatherer (the caller runs a common barrier). With
+        the arena the mappings stay open for the process; bypassed
+        (PDMB_IPC_ARENA=0), this gatherer's peer mappings are closed here,
+        after the drain and before the barrier (the pre-arena order)."""
         torch.cuda.synchronize(self.device)
         _trace(f"rank {self.me} close {len(self.bufs)} buffer(s)")
+        if not arena():
+            mod = _mod()
+            for _, _, peers, _ in self.bufs:
+                for a in peers.values():
+                    mod.ipc_close(a, self.dev_index)
         self.bufs = []
         if barrier and self.ws > 1:
             dist.barrier(group=self.group)

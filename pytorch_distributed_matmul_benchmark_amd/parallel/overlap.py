@@ -119,6 +119,17 @@ class OverlapPlan:
     # over ranks, measured_plan); "model": the GEMM and busBW tables above
     source: str = "model"
     piece_us: Dict[int, float] = field(default_factory=dict)  # measured: one piece's collective, per P
+    # measured: the unit's GEMM while one piece of the P-piece cut runs beside
+    # it on the comm stream (``gemm_shared_us``: P = 1, the whole collective),
+    # and the slowdown share that implies (``cu_share_p[P]`` = (G'_P - G) /
+    # min(G, piece_P): the fraction of the overlapped GEMM time the
+    # collective costs; ``cu_share``: P = 1); model: None and RCCL_CU_SHARE
+    gemm_shared_us: Optional[float] = None
+    cu_share: float = RCCL_CU_SHARE
+    cu_share_p: Dict[int, float] = field(default_factory=dict)
+    # measured: [min, max] over reps and ranks of every timed value (the
+    # planner itself uses the median of each rank's reps, MAX over ranks)
+    spread_us: Dict[str, List[float]] = field(default_factory=dict)
 
     def as_dict(self) -> dict:
         d = asdict(self)
@@ -126,6 +137,11 @@ class OverlapPlan:
         d["piece_us"] = {str(k): round(v, 1) for k, v in self.piece_us.items()}
         for k in ("gemm_us", "comm_us", "serial_us", "overlap_us"):
             d[k] = round(d[k], 1)
+        if d["gemm_shared_us"] is not None:
+            d["gemm_shared_us"] = round(d["gemm_shared_us"], 1)
+        d["cu_share"] = round(d["cu_share"], 4)
+        d["cu_share_p"] = {str(k): round(v, 4) for k, v in self.cu_share_p.items()}
+        d["spread_us"] = {k: [round(x, 1) for x in v] for k, v in self.spread_us.items()}
         return d
 
 
@@ -135,7 +151,9 @@ def plan_overlap(m: int, n: int, k: int, dtype: torch.dtype, ws: int, kind: str,
                  comm_time_us: Optional[float] = None,
                  piece_us: float = COLLECTIVE_LAT_US + PIECE_HOST_US,
                  piece_time_us: Optional[Dict[int, float]] = None,
-                 source: str = "model") -> OverlapPlan:
+                 source: str = "model", gemm_shared_us: Optional[float] = None,
+                 spread_us: Optional[Dict[str, List[float]]] = None,
+                 shared_time_us: Optional[Dict[int, float]] = None) -> OverlapPlan:
     """Choose how a unit (one [m, k] @ [k, n] GEMM whose output's collective
     follows) overlaps: serialize, pipeline whole collectives across units
     (pieces = 1), or start P row pieces as the GEMM's tiles finish (P > 1,
@@ -144,11 +162,18 @@ def plan_overlap(m: int, n: int, k: int, dtype: torch.dtype, ws: int, kind: str,
 
         serial      = G + C
         overlap(P)  = max(G', C') + min(G', C') / P / steps
-        G'          = G + RCCL_CU_SHARE * min(G, C')
+        G'          = G + s * min(G, C')
         C'          = C + (P - 1) * piece_us   (per extra collective call)
 
     (the steady state is the slower of the two streams; what is exposed once
-    per timed region is the faster stream's first / last piece).
+    per timed region is the faster stream's first / last piece). ``s`` is the
+    share of the overlapped GEMM time the collective beside it costs:
+    measured per piece count (``shared_time_us[P]`` = the GEMM timed while
+    one piece of the P-piece cut runs beside it: s_P = (G'_P - G) /
+    min(G, piece_P), clamped to [0, 1] — a small piece can disturb the GEMM
+    less per microsecond than a whole collective, e.g. when its bytes stay
+    in the MALL; ``gemm_shared_us`` alone stands for P = 1 and every P) or the
+    RCCL_CU_SHARE guess.
 
     ``requested`` > 0 is an explicit request: P = ``requested`` (clamped to
     what the granule allows), overlapped even where the model predicts a
@@ -166,16 +191,28 @@ def plan_overlap(m: int, n: int, k: int, dtype: torch.dtype, ws: int, kind: str,
     units = tm // granule if granule > 0 else 1
     choices = piece_choices(m, granule, requested)
     measured = dict(piece_time_us or {})
+    shared = dict(shared_time_us or {})
+    if gemm_shared_us is not None:
+        shared.setdefault(1, gemm_shared_us)
+    elif 1 in shared:
+        gemm_shared_us = shared[1]
+
+    def share_of(Gs: float, piece: float) -> float:
+        return min(max((Gs - G) / min(G, piece), 0.0), 1.0) if min(G, piece) > 0 else 0.0
+
+    shares = {P: share_of(v, measured.get(P, C) if P > 1 else C) for P, v in shared.items()}
+    share = shares.get(1, RCCL_CU_SHARE)
 
     def cost(P: int) -> float:
         Cp = P * measured[P] if P in measured else C + (P - 1) * piece_us
-        Gp = G + RCCL_CU_SHARE * min(G, Cp)
+        Gp = G + shares.get(P, share) * min(G, Cp)
         return max(Gp, Cp) + min(Gp, Cp) / P / max(steps, 1)
 
     cands = {P: cost(P) for P in choices}
     best = min(cands, key=lambda P: (cands[P], P))
     ov = cands[best]
-    kw = dict(candidates=cands, source=source, piece_us=measured)
+    kw = dict(candidates=cands, source=source, piece_us=measured, gemm_shared_us=gemm_shared_us,
+              cu_share=share, cu_share_p=shares, spread_us=dict(spread_us or {}))
     if C <= 0.0:
         return OverlapPlan(False, 1, 0, G, C, serial, serial, reason="no collective (ws = 1)", **kw)
     if ov >= serial * 0.98 and requested <= 0:
@@ -237,7 +274,8 @@ def plan_for_units(units: Sequence[Tuple], ws: int, kind: str, payload_bytes: fl
 def measured_plan(units: Sequence[Tuple], ctx, kind: str, payload_bytes: float, mm: Callable,
                   piece_collective: Callable[[int, int], None], *, native: bool = True,
                   requested: int = 0, steps: int = 10, compute=None, owner=None,
-                  comm: Optional[CommStream] = None, reps: int = 3) -> OverlapPlan:
+                  comm: Optional[CommStream] = None, reps: int = 5,
+                  piece_prepare: Optional[Callable[[int, int], None]] = None) -> OverlapPlan:
     """``plan_overlap`` from times measured on this job's own ranks — the
     reference judges its serialized and overlapped modes by measured time
     (backup/matmul_overlap_benchmark.py:155-164, matmul_scaling_benchmark.py:
@@ -250,14 +288,27 @@ def measured_plan(units: Sequence[Tuple], ctx, kind: str, payload_bytes: float, 
       * C(P) for every piece count P the planner may choose: one collective
         of the first piece's rows, ``piece_collective(start, stop)`` (the
         mode's own collective — RCCL / direct / ipc — on ring slot 0, issued
-        on the comm stream), ``reps`` times after a barrier, host-timed
+        on the comm stream), ``reps`` times after a barrier, each host-timed
         until the comm stream drains (so a piece's host issue cost counts);
-      * every value is the MAX over ranks, so all ranks hold the same plan.
+      * G'(P): the same GEMM, ``reps`` times, each while one piece of the
+        P-piece cut (P = 1: the whole collective) runs beside it on the comm
+        stream (the GEMM issued first, the piece right behind it) — the
+        GEMM's measured slowdown next to the collective, which replaces the
+        RCCL_CU_SHARE guess;
+      * each value is the median of this rank's reps, then the MAX over
+        ranks, so all ranks hold the same plan and one slow rep on one rank
+        does not set it; ``spread_us`` records [min, max] over reps and ranks.
 
-    Only the GEMM's slowdown while a collective runs beside it
-    (``RCCL_CU_SHARE``) stays modelled. If measuring fails on any rank the
-    model plan (``plan_for_units``) is returned, ``source == "model"``.
-    Collective: every rank must call it."""
+    Every phase is agreed across ranks before the next one starts (``all_ok``
+    after the GEMM timing and after each P's local preparation —
+    ``piece_prepare(start, stop)``: buffer allocation and the like, no
+    collective — before that P's first collective): a rank whose
+    GEMM or preparation fails never leaves its peers inside a collective it
+    skips; on any failure every rank returns the model plan
+    (``plan_for_units``), ``source == "model"``. (A collective that itself
+    raises on one rank only cannot be agreed on; the phases before it are
+    what can fail alone.) Collective: every rank must call it."""
+    import statistics
     import time
 
     from .dist import all_ok, barrier, reduce_scalar
@@ -274,56 +325,97 @@ def measured_plan(units: Sequence[Tuple], ctx, kind: str, payload_bytes: float, 
         choices = [1] + choices
     cuda = dev.type == "cuda"
     cs = comm or CommStream(dev)
-    err = None
-    G, piece = 0.0, {}
-    try:
-        def sync():
-            if cuda:
-                torch.cuda.synchronize(dev)
+    reps = max(int(reps), 1)
+    samples: Dict[str, List[float]] = {}
 
-        # GEMM: events on the compute stream, in the pipeline's issue context
+    def sync():
+        if cuda:
+            torch.cuda.synchronize(dev)
+
+    def gemm_reps(beside: Optional[int]) -> List[float]:
+        """``reps`` GEMM times (us) on the compute stream; ``beside``: issue a
+        collective of rows [0, beside) right behind each GEMM."""
+        out = []
+        for _ in range(reps):
+            if cuda:
+                cur = compute if compute is not None else torch.cuda.current_stream(dev)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                with compute_ctx(compute, owner):
+                    e0.record(cur)
+                    mm(A, B, C)
+                    e1.record(cur)
+                if beside is not None:
+                    piece_collective(0, beside)
+                    cs.synchronize()
+                e1.synchronize()
+                out.append(e0.elapsed_time(e1) * 1e3)
+            else:
+                t0 = time.perf_counter()
+                mm(A, B, C)
+                out.append((time.perf_counter() - t0) * 1e6)
+                if beside is not None:
+                    piece_collective(0, beside)
+            sync()
+        return out
+
+    def phase(name: str, fn) -> bool:
+        """Run one measuring phase on this rank, then agree (collective)."""
+        err = None
+        try:
+            samples[name] = fn()
+        except Exception as e:  # a failed measurement falls back to the model, on every rank alike
+            err = f"{type(e).__name__}: {e}"
+        if not all_ok(ctx, err is None):
+            model.reason += f" (measuring failed in {name}: {err or 'on another rank'})"
+            return False
+        return True
+
+    def warm_gemm():
         sync()
         with compute_ctx(compute, owner):
             mm(A, B, C)  # first launch outside the timing (kernel selection, workspace)
         sync()
-        if cuda:
-            cur = compute if compute is not None else torch.cuda.current_stream(dev)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            with compute_ctx(compute, owner):
-                e0.record(cur)
-                for _ in range(reps):
-                    mm(A, B, C)
-                e1.record(cur)
-            e1.synchronize()
-            G = e0.elapsed_time(e1) * 1e3 / reps
-        else:
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                mm(A, B, C)
-            G = (time.perf_counter() - t0) * 1e6 / reps
-        # collectives: one piece per candidate P, after a barrier
-        for P in choices:
-            span = piece_span(m, granule, P)
-            piece_collective(0, span)  # untimed first call (buffers, communicator paths)
-            cs.synchronize()
-            sync()
-            barrier(ctx)
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                piece_collective(0, span)
-            cs.synchronize()
-            sync()
-            piece[P] = (time.perf_counter() - t0) * 1e6 / reps
-    except Exception as e:  # a failed measurement falls back to the model, on every rank alike
-        err = f"{type(e).__name__}: {e}"
-    if not all_ok(ctx, err is None):
-        model.reason += f" (measuring failed: {err or 'on another rank'})"
+        return gemm_reps(None)
+
+    if not phase("gemm", warm_gemm):
         return model
-    G = reduce_scalar(ctx, G, "max")
-    piece = {P: reduce_scalar(ctx, v, "max") for P, v in sorted(piece.items())}
+
+    def coll_reps(span: int) -> List[float]:
+        piece_collective(0, span)  # untimed first call (buffers, communicator paths)
+        cs.synchronize()
+        sync()
+        barrier(ctx)
+        out = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            piece_collective(0, span)
+            cs.synchronize()
+            sync()
+            out.append((time.perf_counter() - t0) * 1e6)
+        return out
+
+    for P in choices:
+        span = piece_span(m, granule, P)
+        if piece_prepare is not None and not phase(f"prepare{P}", lambda: [piece_prepare(0, span)]):
+            return model
+        if not phase(f"piece{P}", lambda: coll_reps(span)):
+            return model
+    for P in choices:
+        if not phase(f"gemm_shared{P}", lambda: gemm_reps(piece_span(m, granule, P))):
+            return model
+
+    def agreed(name: str) -> float:
+        return reduce_scalar(ctx, statistics.median(samples[name]), "max")
+
+    spread = {k: [reduce_scalar(ctx, min(v), "min"), reduce_scalar(ctx, max(v), "max")]
+              for k, v in sorted(samples.items()) if not k.startswith("prepare")}
+    G = agreed("gemm")
+    piece = {P: agreed(f"piece{P}") for P in sorted(choices)}
+    Gs = {P: agreed(f"gemm_shared{P}") for P in sorted(choices)}
     return plan_overlap(m, C.shape[-1], A.shape[-1], A.dtype, ws, kind, payload_bytes,
                         granule=granule, steps=steps, requested=requested, gemm_time_us=G,
-                        comm_time_us=piece[1], piece_time_us=piece, source="measured")
+                        comm_time_us=piece[1], piece_time_us=piece, source="measured",
+                        shared_time_us=Gs, spread_us=spread)
 
 
 def piece_rows(m: int, rows: int) -> List[Tuple[int, int]]:
@@ -702,17 +794,20 @@ def ipc_buffers(impl: str, device: torch.device) -> bool:
 
 
 def pick_collective(ctx, kind: str, t: torch.Tensor, sources=(), comm: Optional[CommStream] = None,
-                    reps: int = 3, candidates: Optional[Sequence[str]] = None):
+                    reps: int = 5, candidates: Optional[Sequence[str]] = None,
+                    spread_out: Optional[Dict[str, List[float]]] = None):
     """``--allreduce auto`` / ``--allgather auto``: time one whole collective of
     ``t`` (all_reduce: in place; all_gather: ``t`` is this rank's block) with
     every candidate implementation on this job's own ranks (``auto_candidates``:
     RCCL's, the direct P2P exchange, and with PDMB_AUTO_IPC=1 the peer-memory
     pull with ``sources`` registered) — each after one untimed call and a
-    barrier, MAX over ranks,
-    and keep the fastest. A candidate that fails on any rank is dropped on
+    barrier, ``reps`` reps each timed alone, the median of a rank's reps and
+    the MAX over ranks (``spread_out``, if given, receives [min, max] over reps
+    and ranks per candidate) — and keep the fastest. A candidate that fails on any rank is dropped on
     every rank. Returns ``(impl, comm_object, {impl: us or None})``; the comm
     object is what ``make_gatherer(impl, ...)`` would have built (on ``comm``),
     the losers' are closed. Collective: every rank must call it."""
+    import statistics
     import time
 
     from .dist import all_ok, barrier, reduce_scalar
@@ -735,7 +830,7 @@ def pick_collective(ctx, kind: str, t: torch.Tensor, sources=(), comm: Optional[
         else:
             all_gather_now(out, t, impl, g)
 
-    times, objs = {}, {}
+    times, objs, spread = {}, {}, {}
 
     def drop(impl, g):  # the candidate is out, on every rank
         times[impl] = None
@@ -761,11 +856,15 @@ def pick_collective(ctx, kind: str, t: torch.Tensor, sources=(), comm: Optional[
             drop(impl, g)
             continue
         barrier(ctx)
-        t0 = time.perf_counter()
+        reps_us = []
         for _ in range(reps):
+            t0 = time.perf_counter()
             call(impl, g)
-        sync()
-        times[impl] = reduce_scalar(ctx, (time.perf_counter() - t0) * 1e6 / reps, "max")
+            sync()
+            reps_us.append((time.perf_counter() - t0) * 1e6)
+        # median of this rank's reps, MAX over ranks; [min, max] over reps and ranks
+        times[impl] = reduce_scalar(ctx, statistics.median(reps_us), "max")
+        spread[impl] = [reduce_scalar(ctx, min(reps_us), "min"), reduce_scalar(ctx, max(reps_us), "max")]
         objs[impl] = g
     ok = {k: v for k, v in times.items() if v is not None}
     if not ok:
@@ -774,4 +873,6 @@ def pick_collective(ctx, kind: str, t: torch.Tensor, sources=(), comm: Optional[
     for impl, g in objs.items():
         if impl != best and hasattr(g, "close"):
             g.close()
+    if spread_out is not None:
+        spread_out.update({k: [round(x, 1) for x in v] for k, v in spread.items()})
     return best, objs[best], {k: (round(v, 1) if v is not None else None) for k, v in times.items()}

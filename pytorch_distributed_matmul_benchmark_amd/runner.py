@@ -37,6 +37,7 @@ from .utils.metrics import (balance_efficiency, bytes_per_element, dtype_from_na
                             overlap_efficiency, peak_for_device, percent_of_peak,
                             scaling_efficiency, square_flops, tflops_from)
 from .utils.report import Reporter, device_banner
+from .utils import testhooks
 from .utils.timing import marker
 
 KINDS = {
@@ -351,6 +352,10 @@ def run_benchmarks(kind: str, ctx: DistContext, rep: Reporter, args) -> List[Dic
         rep.line(f"  - Collective: {coll} (backend {dist_backend_name()})")
     rep.line(f"  - Iterations per test: {args.iterations}")
     rep.line(f"  - Warmup iterations: {args.warmup}")
+    hooks = testhooks.active()
+    if hooks:  # negative-control fault injection: not a measurement
+        rep.line(f"  - WARNING: test-only fault injection active ({', '.join(hooks)}): "
+                 "collectives may race; timings are not measurements")
     rep.line(f"{'=' * k['width']}\n")
     out = []
     done = _completed(args, kind, mode, ctx) if getattr(args, "resume", False) else set()
@@ -399,6 +404,8 @@ def run_benchmarks(kind: str, ctx: DistContext, rep: Reporter, args) -> List[Dic
                    "backend": args.backend, "iterations": args.iterations,
                    "warmup": args.warmup, "tflops_rank0": res.tflops, "kernel": res.kernel,
                    "flops_per_iter_total": res.flops_total, **agg, **extra, **res.extra}
+            if hooks:
+                rec["test_hooks"] = hooks
             rep.record(rec)
             out.append(rec)
         del res

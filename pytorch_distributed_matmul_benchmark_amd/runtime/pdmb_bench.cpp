@@ -494,7 +494,8 @@ void run_rank(int rank, const Opts& o, int n, ncclComm_t comm, Barrier& bar, Res
     // transfer of a group has its own xGMI link on a fully connected node.
     auto ar_chunk = [&](size_t count) { return ((count + ws - 1) / ws + 63) / 64 * 64; };  // 16-B aligned chunks
     const size_t ar_chunk_max = ar_chunk(lb * mat);
-    Buf ARs((o.direct_ar || o.peer_ar) && ws > 1 ? (size_t)(ws - 1) * ar_chunk_max * oes : 0);
+    // landing slots for the direct exchange only (the ipc form sums in place)
+    Buf ARs(o.direct_ar && ws > 1 ? (size_t)(ws - 1) * ar_chunk_max * oes : 0);
     // --allreduce ipc (parallel/ipc.py IpcGather.all_reduce, kernel engine):
     // the same two shots read straight out of the peers' C / C2 (direct peer
     // access between this process's GPUs) from the comm stream — the chunk's

@@ -203,6 +203,9 @@ def main():
                    "tflops_in_schedule": {k: round(flops / v / 1e9, 1) for k, v in best.items()
                                           if k.startswith("pipe_")},
                    "best_arm": arm_best, "planner": chosen, "plan": plan.as_dict(),
+                   # the GEMM's measured slowdown beside one whole proxy collective
+                   "gemm_shared_over_gemm": (round(plan.gemm_shared_us / plan.gemm_us, 4)
+                                             if plan.gemm_shared_us else None),
                    "plan_model": model.as_dict(),
                    "planner_vs_best": round(best.get(chosen, S) / best[arm_best], 4)}
             print(json.dumps(rec), flush=True)

@@ -11,9 +11,37 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "slow: long-running test")
+    config.addinivalue_line("markers", "experiments: A/B or diagnostic kernels that only a "
+                                       "PDMB_EXPERIMENTS=1 build carries (deselected otherwise)")
 
 
+def _experiment_kernels():
+    try:
+        from pytorch_distributed_matmul_benchmark_amd.ops.gemm import EXPERIMENT_KERNELS
+
+        return set(EXPERIMENT_KERNELS)
+    except Exception:  # pragma: no cover
+        return set()
+
+
+@pytest.hookimpl(tryfirst=True)
 def pytest_collection_modifyitems(config, items):
+    # Experiment-kernel cases (a ``kernel`` parameter naming an experiment
+    # kernel, or an explicit ``experiments`` mark) run only against a
+    # PDMB_EXPERIMENTS=1 build: deselected otherwise, so the shipping build's
+    # ``-m gpu`` run reports only real skips. Runs before -m filtering, so
+    # ``-m "gpu and experiments"`` selects them on an experiment build.
+    exp = _experiment_kernels()
+    for item in items:
+        cs = getattr(item, "callspec", None)
+        k = cs.params.get("kernel") if cs is not None else None
+        if isinstance(k, str) and k in exp:
+            item.add_marker(pytest.mark.experiments)
+    if os.environ.get("PDMB_EXPERIMENTS") != "1":
+        drop = [it for it in items if it.get_closest_marker("experiments") is not None]
+        if drop:
+            config.hook.pytest_deselected(items=drop)
+            items[:] = [it for it in items if it.get_closest_marker("experiments") is None]
     try:
         import torch
 

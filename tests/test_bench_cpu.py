@@ -159,6 +159,17 @@ def test_bench_world_size_mismatch_is_an_error():
     assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
 
 
+def test_bench_refuses_test_fault_injection():
+    """A PDMB_TEST_* negative-control switch (racy collectives) never yields a
+    driver line (such a run must not pass for a measurement)."""
+    env = dict(os.environ, PDMB_TEST_SKIP_READY_WAIT="1000")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu",
+                        "--size", "64", "--steps", "1", "--warmup", "0"], capture_output=True,
+                       text=True, timeout=120, cwd="/tmp", env=env)
+    assert r.returncode == 2 and "PDMB_TEST_SKIP_READY_WAIT" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
 def test_bench_setup_failure_on_one_rank_is_agreed():
     """A secondary mode that fails to set up on rank 1 only becomes an "error"
     entry on rank 0's line; the headline and the other modes still report."""

@@ -102,6 +102,7 @@ def test_fp8_race_screen(kernel):
         assert torch.equal(gemm.matmul(A8, B8, alpha=sa * sb, kernel=kernel), ref)
 
 
+@pytest.mark.experiments
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (1000, 1052, 384), (2304, 2048, 1024),
                                    (512, 512, 384)])
 def test_fp8_8wave_kernel_exact(M, N, K):
@@ -329,9 +330,14 @@ def test_fp8_wave_tail_split(M, N, K, form, monkeypatch):
     assert torch.equal(C2, (Af.double() @ Bf.double()).to(torch.bfloat16))
 
 
-@pytest.mark.parametrize("shape", [(1, 5120, 5120, 5120), (1, 4608, 4608, 3072), (1, 6000, 5888, 3072),
-                                   (1, 7168, 7168, 1024), (2, 2560, 2560, 5120), (1, 3072, 3072, 8192)])
-@pytest.mark.parametrize("mode", ["1", "2"])
+SK_SHAPES = [(1, 5120, 5120, 5120), (1, 4608, 4608, 3072), (1, 6000, 5888, 3072),
+             (1, 7168, 7168, 1024), (2, 2560, 2560, 5120), (1, 3072, 3072, 8192)]
+
+
+# mode 2 on 7168^2 x 1024 is not generated: 16 tiles left after the whole
+# waves, fewer K-tiles than workgroups per XCD
+@pytest.mark.parametrize("shape,mode", [(s, m) for m in ("1", "2") for s in SK_SHAPES
+                                        if not (m == "2" and s == (1, 7168, 7168, 1024))])
 def test_fp8_stream_k(shape, mode, monkeypatch):
     """fp8 stream-K (gemm_fp8_sk, forced by PDMB_STREAMK=1): the whole waves
     before the last 1-2 as one launch (none below two waves), the rest as 256
@@ -340,8 +346,6 @@ def test_fp8_stream_k(shape, mode, monkeypatch):
     integers with alpha, nothing written outside C, the same bits every launch
     and under graph replay."""
     monkeypatch.setenv("PDMB_STREAMK", mode)  # 2: only the last partial wave stream-K
-    if mode == "2" and shape == (1, 7168, 7168, 1024):
-        pytest.skip("16 tiles left after the whole waves: fewer K-tiles than workgroups per XCD")
     b, M, N, K = shape
     g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K + b)
     Af = torch.randint(-2, 3, (b, M, K), device="cuda", generator=g).float()

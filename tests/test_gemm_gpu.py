@@ -507,10 +507,14 @@ def test_batched_tile_range_tail(dtype):
     assert torch.isnan(big[:, :, N:]).all() and torch.isnan(big[:, M:]).all()
 
 
-@pytest.mark.parametrize("dtype", ["bfloat16", "float16", "float8_e4m3fn"])
-@pytest.mark.parametrize("M,N,K,R", [(6144, 6144, 6144, 2), (6000, 6000, 6144, 2), (4608, 4608, 3072, 2),
-                                     (6000, 5888, 3072, 4), (6144, 6144, 3072, 4), (4608, 4608, 3072, 4),
-                                     (6144, 4096, 4096, 2), (3000, 7000, 5056, 2)])
+REFINED_SHAPES = [(6144, 6144, 6144, 2), (6000, 6000, 6144, 2), (4608, 4608, 3072, 2),
+                  (6000, 5888, 3072, 4), (6144, 6144, 3072, 4), (4608, 4608, 3072, 4),
+                  (6144, 4096, 4096, 2), (3000, 7000, 5056, 2)]
+
+
+@pytest.mark.parametrize("dtype,M,N,K,R", [(d,) + s for d in ("bfloat16", "float16", "float8_e4m3fn")
+                                           for s in REFINED_SHAPES
+                                           if not (d == "float8_e4m3fn" and s[2] % 128)])  # fp8: K % 128
 def test_refined_wave_tail(dtype, M, N, K, R, monkeypatch):
     """The refined tail (PDMB_TAIL_REFINE=R forces it): whole waves of 256x256
     tiles as one launch, the remaining tiles of the same order cut into R
@@ -521,8 +525,6 @@ def test_refined_wave_tail(dtype, M, N, K, R, monkeypatch):
     monkeypatch.setenv("PDMB_TAIL_REFINE", str(R))
     dt = getattr(torch, dtype)
     fp8 = dt == gemm.FP8
-    if fp8 and K % 128:
-        pytest.skip("fp8 needs K % 128 == 0")
     g = torch.Generator(device="cuda").manual_seed(M + N + K + R)
     lo, hi = (-2, 3) if fp8 else (-3, 4)
     Af = torch.randint(lo, hi, (M, K), device="cuda", generator=g).float()
@@ -630,21 +632,27 @@ def test_thin_grid_supertiles_exact(M, N, batch, kernel, dtype):
 # ---- under-filled grids: T128 (128x128 tiles) and W4 / T128 split-K ----
 # (matrix_parallel column shards at ws >= 4: 4096 x 512, 8192 x 1024; 2048^3)
 
-@pytest.mark.parametrize("kernel", ["w4", "t256x128", "t128", "t128x2"])
-@pytest.mark.parametrize("M,N,K,b,splitk", [
+WHOLE_TILE_SHAPES = [
     (2048, 2048, 2048, 1, 0), (4096, 512, 4096, 1, 0), (8192, 1024, 8192, 1, 2),
     (1024, 1024, 4096, 1, 2), (1024, 1024, 4096, 1, 4), (1024, 1024, 4096, 1, 8),
     (512, 512, 2048, 2, 4), (1024, 768, 832, 1, 4), (4096, 512, 4096, 1, 1),
-    (256, 256, 64, 1, 0), (512, 768, 320, 3, 0)])
+    (256, 256, 64, 1, 0), (512, 768, 320, 3, 0)]
+
+
+def _whole_tile_fits(kernel, M, N):
+    """W4 needs M, N % 256; T256x128 needs M % 256 (the other combinations are
+    not generated, rather than skipped)."""
+    return not ((kernel == "w4" and (M % 256 or N % 256)) or (kernel == "t256x128" and M % 256))
+
+
+@pytest.mark.parametrize("kernel,M,N,K,b,splitk", [
+    (k,) + s for k in ("w4", "t256x128", "t128", "t128x2") for s in WHOLE_TILE_SHAPES
+    if _whole_tile_fits(k, s[0], s[1])])
 @pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
 def test_whole_tile_kernels_exact(kernel, M, N, K, b, splitk, dtype):
     """Integer data keeps every fp32 slice partial and their sum exact: the
     (split) result equals the fp64 product rounded once (K = 832 leaves the
     last of 4 slices one K-tile; K = 64 is a one-K-tile prologue/tail)."""
-    if kernel == "w4" and (M % 256 or N % 256):
-        pytest.skip("W4 needs M, N % 256")
-    if kernel == "t256x128" and M % 256:
-        pytest.skip("T256x128 needs M % 256")
     dt = DT[dtype]
     g = torch.Generator(device="cuda").manual_seed(M + N + K + splitk)
     A = torch.randint(-3, 4, (b, M, K), device="cuda", generator=g).to(dt)
@@ -712,6 +720,7 @@ def test_tile_family_matches_w4_bitwise_unsplit():
         assert torch.equal(gemm.matmul(A, B, kernel=k, splitk=1), ref), k
 
 
+@pytest.mark.experiments
 @pytest.mark.parametrize("b,M,N,K", [(1, 256, 256, 64), (1, 256, 512, 128), (1, 2304, 1280, 192),
                                      (3, 1024, 768, 256), (1, 4096, 4096, 512), (1, 8192, 2048, 128)])
 def test_persistent_w4_matches_w4_bitwise(b, M, N, K):
@@ -752,6 +761,7 @@ def test_streaming_w4s_matches_w4_bitwise(b, M, N, K):
         assert torch.equal(out, ref)
 
 
+@pytest.mark.experiments
 @pytest.mark.parametrize("b,M,N,K", [(1, 4096, 4096, 512), (2, 4096, 8192, 384), (1, 8192, 8192, 384),
                                      (1, 16384, 2048, 384)])
 def test_streaming_w4s_rot_matches_w4_bitwise(b, M, N, K):
@@ -780,6 +790,7 @@ def test_streaming_w4s_fp16_exact():
         gemm.matmul(A[:, :960], B[:960], kernel="w4s")
 
 
+@pytest.mark.experiments
 def test_persistent_w4_streams_graph_and_cu_budget():
     """Queues are per stream: persistent launches on two streams at once stay
     exact; a graph replays exactly; a CU-masked stream (fewer workgroups than

@@ -179,3 +179,172 @@ def test_round_comm_cus_whole_granules():
     assert round_comm_cus(0) == 0 and round_comm_cus(-4) == 0
     assert round_comm_cus(1) == 32 and round_comm_cus(8) == 32 and round_comm_cus(32) == 32
     assert round_comm_cus(33) == 64 and round_comm_cus(1000) == 224
+
+
+def test_measured_plan_measures_the_gemm_beside_the_collective():
+    """G' (VERDICT r4 #2): measured_plan times the unit's GEMM while a whole
+    collective runs beside it and prices the overlap with that slowdown
+    instead of the RCCL_CU_SHARE guess. Mock: a GEMM issued right behind a
+    collective takes twice as long (4 -> 8 ms), so the measured share is
+    (8 - 4) / min(4, 6) = 1 and the P = 1 candidate is max(G + min(G, C), C)
+    + min(...) / steps."""
+    import time
+
+    from pytorch_distributed_matmul_benchmark_amd.parallel.dist import DistContext
+
+    m = 64
+    A = torch.randn(m, m)
+    units = [(A, A, torch.empty(m, m)) for _ in range(2)]
+    ctx = DistContext(rank=0, world_size=2, local_rank=0, device=torch.device("cpu"))
+    beside = [False]
+
+    def mm(x, y, out):
+        time.sleep(0.008 if beside[0] else 0.004)
+        beside[0] = False
+
+    def coll(s, e):
+        time.sleep(0.006)
+        beside[0] = True
+
+    p = O.measured_plan(units, ctx, "all_reduce", m * m * 4, mm, coll, steps=10, reps=5)
+    assert p.source == "measured" and p.gemm_shared_us is not None
+    assert p.gemm_shared_us > 1.5 * p.gemm_us
+    assert 0.5 < p.cu_share <= 1.0
+    G, C, s = p.gemm_us, p.comm_us, p.cu_share
+    Gp = G + s * min(G, C)
+    assert p.candidates[1] == pytest.approx(max(Gp, C) + min(Gp, C) / 10, rel=1e-6)
+    assert p.cu_share_p == {1: p.cu_share}
+    d = p.as_dict()
+    assert {"gemm", "gemm_shared1", "piece1"} <= set(d["spread_us"])
+    assert all(lo <= hi for lo, hi in d["spread_us"].values())
+    assert d["gemm_shared_us"] == round(p.gemm_shared_us, 1)
+    # the model fallback keeps the guess
+    q = O.plan_overlap(16384, 2048, 16384, torch.bfloat16, 8, "all_gather", 16384 * 2048 * 2)
+    assert q.gemm_shared_us is None and q.cu_share == O.RCCL_CU_SHARE
+
+
+def test_plan_share_is_clamped():
+    kw = dict(gemm_time_us=1000.0, comm_time_us=500.0, source="measured")
+    fast = O.plan_overlap(4096, 4096, 4096, torch.bfloat16, 8, "all_reduce", 0.0,
+                          gemm_shared_us=900.0, **kw)  # noise below G: no negative share
+    assert fast.cu_share == 0.0
+    slow = O.plan_overlap(4096, 4096, 4096, torch.bfloat16, 8, "all_reduce", 0.0,
+                          gemm_shared_us=5000.0, **kw)
+    assert slow.cu_share == 1.0 and not slow.overlap  # overlap can only tie serial: refused
+    # per piece count: a small piece that barely disturbs the GEMM makes P = 4 win
+    per = O.plan_overlap(16384, 16384, 16384, torch.bfloat16, 8, "all_reduce", 0.0, granule=16,
+                         steps=10, gemm_time_us=5700.0, comm_time_us=930.0, source="measured",
+                         piece_time_us={1: 930.0, 2: 283.0, 4: 152.0},
+                         shared_time_us={1: 6040.0, 2: 5800.0, 4: 5720.0})
+    assert per.cu_share_p[1] == pytest.approx(340 / 930) and per.cu_share_p[4] == pytest.approx(20 / 152)
+    assert per.pieces == 4 and per.gemm_shared_us == 6040.0
+
+
+def _fail_worker(rank, ws, port, where, outdir):
+    """One rank (1) fails in measured_plan's ``where`` phase; every rank must
+    return the model plan without hanging."""
+    import json as _json
+    import os as _os
+
+    import torch.distributed as dist
+
+    from pytorch_distributed_matmul_benchmark_amd.parallel import overlap as O
+    from pytorch_distributed_matmul_benchmark_amd.parallel.dist import DistContext
+
+    _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    ctx = DistContext(rank=rank, world_size=ws, local_rank=rank, device=torch.device("cpu"),
+                      backend="gloo")
+    m = 64
+    A = torch.randn(m, m)
+    units = [(A, A, torch.empty(m, m)) for _ in range(2)]
+    t = torch.ones(m, m)
+    calls = {"mm": 0}
+
+    def mm(x, y, out):
+        calls["mm"] += 1
+        if where == "gemm" and rank == 1:
+            raise RuntimeError("injected GEMM failure")
+        torch.matmul(x, y, out=out)
+
+    def prepare(s, e):  # the probe's local setup (e.g. its gather buffer): no collective
+        if where == "prepare" and rank == 1:
+            raise RuntimeError("injected allocation failure")
+
+    def coll(s, e):
+        dist.all_reduce(t[s:e].contiguous())
+
+    p = O.measured_plan(units, ctx, "all_reduce", m * m * 4, mm, coll, steps=10, reps=2,
+                        piece_prepare=prepare)
+    dist.barrier()  # every rank got here: nobody is left inside a collective
+    with open(_os.path.join(outdir, f"r{rank}.json"), "w") as f:
+        _json.dump({"source": p.source, "reason": p.reason}, f)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ws", [2, 8])
+@pytest.mark.parametrize("where", ["gemm", "prepare"])
+def test_measured_plan_one_rank_failure_is_agreed(ws, where, tmp_path):
+    import json as _json
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_fail_worker, args=(ws, port, where, str(tmp_path)), nprocs=ws, join=True)
+    res = [_json.load(open(tmp_path / f"r{r}.json")) for r in range(ws)]
+    for r in res:
+        assert r["source"] == "model" and "measuring failed" in r["reason"], r
+
+
+def _plan_worker(rank, ws, port, outdir):
+    """measured_plan over a real gloo group: the shared-GEMM field and the
+    spread are agreed (identical on every rank)."""
+    import json as _json
+    import os as _os
+
+    import torch.distributed as dist
+
+    from pytorch_distributed_matmul_benchmark_amd.parallel import overlap as O
+    from pytorch_distributed_matmul_benchmark_amd.parallel.dist import DistContext
+
+    _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    ctx = DistContext(rank=rank, world_size=ws, local_rank=rank, device=torch.device("cpu"),
+                      backend="gloo")
+    m = 128
+    A = torch.randn(m, m)
+    units = [(A, A, torch.empty(m, m)) for _ in range(2)]
+    t = torch.ones(1 << 16)
+
+    def mm(x, y, out):
+        torch.matmul(x, y, out=out)
+
+    p = O.measured_plan(units, ctx, "all_reduce", m * m * 4, mm, lambda s, e: dist.all_reduce(t),
+                        steps=10, reps=3)
+    with open(_os.path.join(outdir, f"r{rank}.json"), "w") as f:
+        _json.dump(p.as_dict(), f, sort_keys=True)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ws", [2, 8])
+def test_measured_plan_shared_gemm_field_agreed(ws, tmp_path):
+    import json as _json
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_plan_worker, args=(ws, port, str(tmp_path)), nprocs=ws, join=True)
+    res = [open(tmp_path / f"r{r}.json").read() for r in range(ws)]
+    assert len(set(res)) == 1  # the same plan on every rank
+    d = _json.loads(res[0])
+    assert d["source"] == "measured" and d["gemm_shared_us"] is not None
+    assert 0.0 <= d["cu_share"] <= 1.0 and set(d["spread_us"]) == {"gemm", "gemm_shared1", "piece1"}
+    G, C, s = d["gemm_us"], d["comm_us"], d["cu_share"]
+    Gp = G + s * min(G, C)
+    assert d["candidates"]["1"] == pytest.approx(max(Gp, C) + min(Gp, C) / 10, abs=0.2)
