@@ -94,9 +94,8 @@ def collective_impl(flag, overlap: bool) -> str:
     """``--allreduce`` / ``--allgather`` as given, or by default: RCCL for the
     serialized modes (the reference's NCCL call, matmul_scaling_benchmark.py:
     150 / :221, so those numbers stay reference-comparable) and ``auto`` for the
-    overlapped ones (the faster of RCCL / direct — plus the peer-memory pull
-    with PDMB_AUTO_IPC=1 — timed on the job's own ranks: the MI355X-native
-    schedule)."""
+    overlapped ones (the fastest of RCCL / direct / the peer-memory pull,
+    timed on the job's own ranks: the MI355X-native schedule)."""
     if flag:
         return flag
     return "auto" if overlap else "rccl"
@@ -276,9 +275,8 @@ class Workload:
     # -- collectives -------------------------------------------------------------
     def _collective(self, impl, kind, t, sources, cs):
         """(implementation, comm object) for ``--allreduce`` / ``--allgather``
-        ``impl``: ``auto`` times RCCL and the direct P2P exchange (and the
-        peer-memory pull with PDMB_AUTO_IPC=1) on this job's ranks and keeps
-        the fastest
+        ``impl``: ``auto`` times RCCL, the direct P2P exchange and the
+        peer-memory pull on this job's ranks and keeps the fastest
         (parallel/overlap.py pick_collective; the times go into the JSON as
         ``collective``); otherwise the named one (``rccl`` on the current
         stream needs no object unless an overlap's comm stream is given)."""
@@ -289,10 +287,15 @@ class Workload:
             spread = {}
             impl, obj, times = pick_collective(self.ctx, kind, t, sources, comm=cs, spread_out=spread)
             self.coll_choice = {"kind": kind, "chosen": impl, "us": times, "spread_us": spread}
+            if impl == "ipc":  # which pull engine ran (parallel/ipc.py PDMB_IPC_ENGINE)
+                self.coll_choice["ipc_engine"] = getattr(obj, "engine", None)
             return impl, obj
         if impl == "rccl" and cs is None:
             return impl, None
-        return impl, make_gatherer(impl, dev, sources, comm=cs)
+        obj = make_gatherer(impl, dev, sources, comm=cs)
+        if impl == "ipc" and hasattr(obj, "engine"):
+            self.coll_choice = {"kind": kind, "chosen": impl, "us": None, "ipc_engine": obj.engine}
+        return impl, obj
 
     # -- overlap ---------------------------------------------------------------
     def _pipeline(self, a, units, coll, per_step, kind, payload, cs, gath=None, probe=None,

@@ -333,29 +333,32 @@ def measured_plan(units: Sequence[Tuple], ctx, kind: str, payload_bytes: float, 
             torch.cuda.synchronize(dev)
 
     def gemm_reps(beside: Optional[int]) -> List[float]:
-        """``reps`` GEMM times (us) on the compute stream; ``beside``: issue a
-        collective of rows [0, beside) right behind each GEMM."""
+        """``reps`` GEMM times (us) on the compute stream, issued back to back
+        (the pipeline's steady state; each timed by its own event pair, so a
+        host gap between launches is not counted); ``beside``: a collective
+        of rows [0, beside) issued right behind each GEMM, which it overlaps."""
         out = []
-        for _ in range(reps):
-            if cuda:
-                cur = compute if compute is not None else torch.cuda.current_stream(dev)
+        if cuda:
+            cur = compute if compute is not None else torch.cuda.current_stream(dev)
+            evs = []
+            for _ in range(reps):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 with compute_ctx(compute, owner):
                     e0.record(cur)
                     mm(A, B, C)
                     e1.record(cur)
+                evs.append((e0, e1))
                 if beside is not None:
                     piece_collective(0, beside)
-                    cs.synchronize()
-                e1.synchronize()
-                out.append(e0.elapsed_time(e1) * 1e3)
-            else:
-                t0 = time.perf_counter()
-                mm(A, B, C)
-                out.append((time.perf_counter() - t0) * 1e6)
-                if beside is not None:
-                    piece_collective(0, beside)
+            cs.synchronize()
             sync()
+            return [e0.elapsed_time(e1) * 1e3 for e0, e1 in evs]
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            mm(A, B, C)
+            out.append((time.perf_counter() - t0) * 1e6)
+            if beside is not None:
+                piece_collective(0, beside)
         return out
 
     def phase(name: str, fn) -> bool:
@@ -777,12 +780,16 @@ COLLECTIVE_IMPLS = ("rccl", "direct", "ipc")
 
 
 def auto_candidates(device: torch.device) -> Tuple[str, ...]:
-    """What ``auto`` times: RCCL's collective and the direct P2P exchange (both
-    RCCL kernels); the peer-memory pull joins with ``PDMB_AUTO_IPC=1`` (GPU
-    tensors) — it ran only with ranks sharing one GPU so far, where one
-    8-rank rehearsal faulted before the IPC arena (parallel/ipc.py), so it is
-    opt-in rather than something a default run might pick."""
-    if device.type == "cuda" and os.environ.get("PDMB_AUTO_IPC") == "1":
+    """What ``auto`` times: RCCL's collective, the direct P2P exchange (both
+    RCCL kernels) and, on GPU tensors, the peer-memory pull (parallel/ipc.py).
+    The pull had been opt-in since an 8-rank one-GPU rehearsal faulted in
+    round 4; its cause class is now pinned (docs/ARCHITECTURE.md "IPC fault":
+    handles re-issued for re-allocated addresses and stale imports, measured
+    by scripts/ipc_handle_probe.py) and closed by the buffer pool, the churn
+    runs clean with every pull bounds-checked (tests/test_multirank_gpu.py
+    test_ipc_churn_register_close_free), so it is a default candidate again;
+    ``PDMB_AUTO_IPC=0`` leaves it out."""
+    if device.type == "cuda" and os.environ.get("PDMB_AUTO_IPC", "1") != "0":
         return COLLECTIVE_IMPLS
     return ("rccl", "direct")
 
@@ -799,8 +806,8 @@ def pick_collective(ctx, kind: str, t: torch.Tensor, sources=(), comm: Optional[
     """``--allreduce auto`` / ``--allgather auto``: time one whole collective of
     ``t`` (all_reduce: in place; all_gather: ``t`` is this rank's block) with
     every candidate implementation on this job's own ranks (``auto_candidates``:
-    RCCL's, the direct P2P exchange, and with PDMB_AUTO_IPC=1 the peer-memory
-    pull with ``sources`` registered) — each after one untimed call and a
+    RCCL's, the direct P2P exchange, and on GPUs the peer-memory pull with
+    ``sources`` registered) — each after one untimed call and a
     barrier, ``reps`` reps each timed alone, the median of a rank's reps and
     the MAX over ranks (``spread_out``, if given, receives [min, max] over reps
     and ranks per candidate) — and keep the fastest. A candidate that fails on any rank is dropped on

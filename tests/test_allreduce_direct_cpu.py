@@ -209,6 +209,8 @@ def test_auto_collective_is_measured_and_agreed():
         c = m["collective"]
         assert c["chosen"] in ("rccl", "direct") and set(c["us"]) == {"rccl", "direct"}, (key, c)
         assert c["us"][c["chosen"]] == min(v for v in c["us"].values() if v is not None)
+        assert set(c["spread_us"]) == set(c["us"])  # [min, max] over reps and ranks
+        assert all(lo <= c["us"][k] <= hi for k, (lo, hi) in c["spread_us"].items())
 
 
 def _pick_worker(rank, ws, port, outdir):

@@ -138,3 +138,27 @@ def test_rank_stream_set_has_no_false_queue_dependency():
     assert r.returncode == 0, r.stderr[-2000:]
     d = __import__("json").loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["gate_was_closed"] and d["free"], d
+
+
+def test_ipc_handle_reuse_and_the_pool():
+    """scripts/ipc_handle_probe.py (two processes): with hipFree between
+    exports (PDMB_IPC_ARENA=0) a buffer re-allocated at the freed address is
+    exported under the same handle bytes, and — what made the pre-arena churn
+    unsafe — a peer still holding the old import gets that stale mapping back
+    (recorded, profiles/r7c_ipc_handle_probe.jsonl). The pool (default) hands
+    the same live buffer back under the same handle while the peer keeps its
+    mapping: every read current."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "ipc_handle_probe.py"),
+                        "--trials", "3"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    recs = [__import__("json").loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    trials = [x for x in recs if "trial" in x]
+    bypass = [x for x in trials if not x["arena"]]
+    pool = [x for x in trials if x["arena"]]
+    # equal-size churn, child closing first: handles repeat with the address, reads are current
+    same_size = [x for x in bypass[1:3]]
+    assert all(x["same_handle_as_prev"] == x["same_ptr_as_prev"] for x in same_size), same_size
+    assert all(x.get("read_ok") for x in bypass[:3]), bypass[:3]
+    # the pool: same buffer, same handle, the peer's open mapping reads the new bytes
+    assert len(pool) == 3 and all(x.get("read_ok") for x in pool), pool
+    assert all(x["same_ptr_as_prev"] and x["same_handle_as_prev"] for x in pool[1:]), pool

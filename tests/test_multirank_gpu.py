@@ -200,6 +200,9 @@ def test_eight_ranks_self_launch_bench(extra):
     shapes (local batch 1 with a two-slot ring, 512-column shards at 4096):
     every mode runs, with measured overlap plans."""
     d = _bench8(*extra)
+    if not extra:  # auto on the overlapped modes: all three candidates timed, ipc included
+        colls = [m["collective"] for m in d["modes"].values() if m.get("collective")]
+        assert colls and all(set(c["us"]) == {"rccl", "direct", "ipc"} for c in colls), colls
     plans = [m["plan"] for m in d["modes"].values() if m.get("plan")]
     plans += [d["config"]["overlap_plan"]] if "overlap_plan" in d["config"] else []
     assert plans and all(p["source"] == "measured" for p in plans), plans
