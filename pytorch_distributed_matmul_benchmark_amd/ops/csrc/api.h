@@ -26,6 +26,10 @@ enum Kernel : int {
   kFp8T256x128 = 42,  // gemm_tile.hip fp8: 256x128 tile, 4 waves x 128x64, split-K (M % 256, N % 128)
   kF32T128 = 51,      // gemm_f32_tile.hip: exact fp32, 128x128 tile, 4 waves x 64x64, split-K (any M, N % 4)
   kF32T128x2 = 53,    // kF32T128 on 2 LDS stages, two workgroups per CU (grids of >= 2 tiles per CU)
+  kT192 = 60,         // gemm_tile.hip: bf16/fp16 NN, 192x192 tile, 4 waves x 96x96, 3-stage ring, split-K
+  kT192x128 = 61,     // gemm_tile.hip: bf16/fp16 NN, 192x128 tile, 4 waves x 96x64, 3-stage ring, split-K
+  kFp8T192 = 62,      // gemm_tile.hip fp8: 192x192 tile, 4 waves x 96x96, split-K
+  kFp8T192x128 = 63,  // gemm_tile.hip fp8: 192x128 tile, 4 waves x 96x64, split-K
 };
 
 // Experiment / diagnostic kernel ids (A/B and timing-only builds) live in

@@ -152,9 +152,11 @@ __device__ __forceinline__ void signal_tile(const GemmArgs& a, int bz, int tm) {
 // rows: a quarter of the requests, all of them whole lines.
 // Buffer rows are NB * 32 + 8 bytes (W4: 264): the b64 writes (16 lanes =
 // 16 rows, 2 banks each) and the b128 reads (16 B chunks of whole rows)
-// are conflict-free for NB = 8 and NB = 4.
+// are conflict-free for NB = 8 and NB = 4. NB = 6 (the 192-column tiles of
+// gemm_tile.hip): rows of NB * 32 + 16 = 208 B, 52 dwords, put the 16 rows'
+// b64 writes on 16 distinct 4-bank slots (52 r mod 64, r < 16).
 template <int NB>
-constexpr int epi_pitch() { return NB * 32 + 8; }
+constexpr int epi_pitch() { return NB * 32 + (NB % 4 ? 16 : 8); }
 template <int NB = 8>
 constexpr int epi_buf() { return 16 * epi_pitch<NB>(); }
 constexpr int kEpiPitch = epi_pitch<8>();
@@ -180,7 +182,8 @@ __device__ __forceinline__ void store_block16(char* buf, const f32x4 (&v)[NB], f
                                               int lane) {
   constexpr int P = epi_pitch<NB>();
   constexpr int CPR = NB * 2;    // 16-B chunks per row
-  constexpr int RPI = 64 / CPR;  // rows per read instruction
+  constexpr int NR = 16 * CPR / 64;  // read instructions: chunk q = lane + 64 r is row q / CPR
+  static_assert(16 * CPR % 64 == 0, "whole 16-row blocks per read round");
   const int l16 = lane & 15, g = lane >> 4;
   typedef __attribute__((address_space(3))) char lds_char;
   lds_char* lb = (lds_char*)(lds_void*)buf;
@@ -196,16 +199,16 @@ __device__ __forceinline__ void store_block16(char* buf, const f32x4 (&v)[NB], f
     }
     *(lds_u32x2*)(lb + l16 * P + (j * 16 + 4 * g) * 2) = w;
   }
-  const int rl = lane / CPR, ch = lane % CPR;
   if constexpr (WT) {
     // one descriptor per 16-row block (uniform base; offsets < 16 rows x ldc_b)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         C + (long long)row0 * ldc_b + (long long)col0 * 2, 0, 0x7fffffff, 0x00020000);
 #pragma unroll
-    for (int r = 0; r < 16 / RPI; ++r) {
-      const u32x4 x = *(lds_u32x4_t*)(lb + (RPI * r + rl) * P + ch * 16);
-      const int row = row0 + RPI * r + rl, col = col0 + 8 * ch;
-      const int off = (RPI * r + rl) * (int)ldc_b + ch * 16;
+    for (int r = 0; r < NR; ++r) {
+      const int q = lane + 64 * r, rl = q / CPR, ch = q % CPR;
+      const u32x4 x = *(lds_u32x4_t*)(lb + rl * P + ch * 16);
+      const int row = row0 + rl, col = col0 + 8 * ch;
+      const int off = rl * (int)ldc_b + ch * 16;
       if (!MASK || (row < M && col + 8 <= N)) {
         __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 16 /* sc1 */);
       } else if (row < M && col + 4 <= N) {
@@ -215,9 +218,10 @@ __device__ __forceinline__ void store_block16(char* buf, const f32x4 (&v)[NB], f
     return;
   }
 #pragma unroll
-  for (int r = 0; r < 16 / RPI; ++r) {
-    const u32x4 x = *(lds_u32x4_t*)(lb + (RPI * r + rl) * P + ch * 16);
-    const int row = row0 + RPI * r + rl, col = col0 + 8 * ch;
+  for (int r = 0; r < NR; ++r) {
+    const int q = lane + 64 * r, rl = q / CPR, ch = q % CPR;
+    const u32x4 x = *(lds_u32x4_t*)(lb + rl * P + ch * 16);
+    const int row = row0 + rl, col = col0 + 8 * ch;
     char* p = C + (long long)row * ldc_b + (long long)col * 2;
     if constexpr (MASK) {
       if (row < M) {

@@ -119,7 +119,8 @@ static const char* experiment_name(int) { return "auto"; }
 #endif
 
 static bool is_fp8_kernel(int k) {
-  return k == kFp8W4 || k == kFp8W4S || k == kFp8T128 || k == kFp8T256x128 || experiment_is_fp8(k);
+  return k == kFp8W4 || k == kFp8W4S || k == kFp8T128 || k == kFp8T256x128 || k == kFp8T192 ||
+         k == kFp8T192x128 || experiment_is_fp8(k);
 }
 
 static int device_cus();
@@ -136,7 +137,9 @@ struct Plan {
 };
 static Plan plan(const Problem& p, int kernel);
 
-int resolve_kernel(const Problem& p, int kernel) {
+// The kernel of the whole-problem plan (resolve_kernel without relabelling a
+// refined wave-quantisation tail; tail_plan asks this one).
+static int resolve_core(const Problem& p, int kernel) {
   if (is_experiment(kernel) && !experiments_built()) return -1;
   const GemmArgs a = to_args(p);
   if (p.dtype == kFP8) {  // fp8 kernels only; no generic / padded fallback
@@ -145,7 +148,8 @@ int resolve_kernel(const Problem& p, int kernel) {
       return -1;
     const bool s_fits = gemm_fp8_w4s_fits(a) && device_cus() % 8 == 0;
     if (kernel == kFp8W4S) return s_fits ? kernel : -1;
-    if (kernel == kFp8T128 || kernel == kFp8T256x128) return supports(p, kernel) ? kernel : -1;
+    if (kernel == kFp8T128 || kernel == kFp8T256x128 || kernel == kFp8T192 || kernel == kFp8T192x128)
+      return supports(p, kernel) ? kernel : -1;
     if (is_experiment(kernel)) return experiment_resolve_fp8(p, kernel, s_fits);
     if (kernel != kAuto) return kernel;
     // the streaming kernel on a device of its own with more than one wave of
@@ -164,6 +168,7 @@ int resolve_kernel(const Problem& p, int kernel) {
   const bool w4 = gemm_w4_supported(p.dtype, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   const bool t128 = gemm_tile_supported(p.dtype, 128, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   const bool t256 = gemm_tile_supported(p.dtype, 256, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
+  const bool t192 = gemm_tile_supported(p.dtype, 192, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   const bool f32fast = p.dtype == kF32 &&
                        gemm_f32_256_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   switch (kernel) {
@@ -173,7 +178,7 @@ int resolve_kernel(const Problem& p, int kernel) {
     // that fill the chip, T128 for under-filled ones: plan()), SCHED 3 for
     // edge tiles.
     case kAuto:
-      if (w4 || t128 || t256) {
+      if (w4 || t128 || t256 || t192) {
         const Plan pl = plan(p, kAuto);
         return pl.kernel == kMfmaW4 && pl.splitk == 1 && w4s_auto(p) ? kMfmaW4S : pl.kernel;
       }
@@ -201,6 +206,8 @@ int resolve_kernel(const Problem& p, int kernel) {
     case kT128: return t128 ? kT128 : -1;
     case kT128x2: return t128 ? kT128x2 : -1;  // shares T128's constraints
     case kT256x128: return t256 ? kT256x128 : -1;
+    case kT192: return t192 ? kT192 : -1;
+    case kT192x128: return t192 ? kT192x128 : -1;
     case kF32_256s: return f32fast ? kF32_256s : -1;
     case kF32W4: return f32fast ? kF32W4 : -1;  // same constraints as f32_256
     case kF32T128: return p.dtype == kF32 && supports(p, kF32T128) ? kF32T128 : -1;
@@ -269,6 +276,16 @@ static constexpr KernelModel kModels[] = {
     {kF32_256s, 256, 256, 1, 7.1, 2, 1},
     {kF32T128, 128, 128, 1, 1.81, 2, 8},
     {kF32W4, 256, 256, 1, 7.1, 2, 8},
+    // round 5: 192-row tiles (first estimated from the T256x128 rate per MFMA,
+    // 72 / 48 MFMAs per wave per K-tile against its 64; calibrated on the first
+    // A/B, profiles/r7e_t192_ab_*.jsonl: bf16 3072^3 46 us = 48 K-tiles x 0.87
+    // + 4, 6144^3 340 us = 4 waves x (96 x 0.84 + 4); fp8 3072^3 23.9 us = 24 x
+    // 0.83 + 4; T192x128 2304^2 x 4096 40.9 us = 64 x 0.61 x boost + 4).
+    // Listed last: the incumbents keep ties.
+    {kT192, 192, 192, 1, 0.86, 0, 8},
+    {kT192x128, 192, 128, 1, 0.60, 0, 8},
+    {kFp8T192, 192, 192, 1, 0.83, 1, 8},
+    {kFp8T192x128, 192, 128, 1, 0.60, 1, 8},
 };
 static int dt_class(const Problem& p) { return p.dtype == kFP8 ? 1 : p.dtype == kF32 ? 2 : 0; }
 static constexpr double kFixedUs = 4.0;   // launch + prologue + epilogue
@@ -361,13 +378,19 @@ static bool supports(const Problem& p, int kernel) {
 
 // `kernel`: kAuto (choose), or one of kMfmaW4 / kT256x128 / kT128 / kT128x2
 // (choose only the split). p.splitk > 0 fixes the split.
+static bool is_t192(int k) { return k == kT192 || k == kT192x128 || k == kFp8T192 || k == kFp8T192x128; }
+
 static Plan plan(const Problem& p, int kernel) {
   Plan best{-1, 1};
   double bc = 1e300;
   bool any = false;
   static const int kS[] = {1, 2, 4, 8};
+  // PDMB_T192=0 (read per call; A/B): auto leaves the 192-row tiles out
+  const char* t192env = std::getenv("PDMB_T192");
+  const bool no192 = kernel == kAuto && t192env && std::atoi(t192env) == 0;
   for (const KernelModel& m : kModels) {
     if (kernel != kAuto && kernel != m.kernel) continue;
+    if (no192 && is_t192(m.kernel)) continue;
     if (m.cls != dt_class(p) || !supports(p, m.kernel)) continue;
     any = true;
     for (int S : kS) {
@@ -399,7 +422,8 @@ static Plan plan(const Problem& p, int kernel) {
 
 static bool is_tiled(int k) {
   return k == kMfmaW4 || k == kT128 || k == kT128x2 || k == kT256x128 || k == kFp8T128 || k == kFp8T256x128 ||
-         k == kF32W4 || k == kF32T128 || k == kF32T128x2;
+         k == kF32W4 || k == kF32T128 || k == kF32T128x2 || k == kT192 || k == kT192x128 || k == kFp8T192 ||
+         k == kFp8T192x128;
 }
 
 int choose_splitk(const Problem& p, int kernel) {
@@ -520,14 +544,16 @@ static TailPlan tail_plan(const Problem& p, int kernel) {
   if (p.dtype == kF32 && p.K > 0) return f32_tail_plan(p);
   if ((p.dtype != kBF16 && p.dtype != kF16 && p.dtype != kFP8) || p.M <= 256 || p.K <= 0) return best;
   const int kw = tail_kernel(p);
-  if (resolve_kernel(p, kAuto) < 0 || !supports(p, kw)) return best;
+  if (resolve_core(p, kAuto) < 0 || !supports(p, kw)) return best;
   const Plan whole = plan(p, kAuto);  // the best single launch (W4 or a smaller tile)
   // A refined tail can also beat a single launch of the tile family (bf16
   // 6144 x 4096 x 4096: 768 256x128 tiles = 3 waves, vs one W4 wave + one wave
   // of 256x128 halves); the split-K forms only ever replace a single W4 launch.
   const bool whole_w4 = whole.kernel == kw && whole.splitk == 1;
   const bool whole_tile = whole.splitk <= 1 && (whole.kernel == kT256x128 || whole.kernel == kT128 ||
-                                                whole.kernel == kFp8T256x128 || whole.kernel == kFp8T128);
+                                                whole.kernel == kFp8T256x128 || whole.kernel == kFp8T128 ||
+                                                whole.kernel == kT192 || whole.kernel == kT192x128 ||
+                                                whole.kernel == kFp8T192 || whole.kernel == kFp8T192x128);
   if (!whole_w4 && !whole_tile) return best;
   const long long slots = device_cus();
   const int tm = (p.M + 255) / 256, tn = (p.N + 255) / 256, batch = p.batch < 1 ? 1 : p.batch;
@@ -1032,6 +1058,19 @@ static bool fp8_dp_streams(const GemmArgs& d, long long tiles_dp) {
   return tiles_dp >= 2LL * device_cus();
 }
 
+// Which kernel `kernel` resolves to. Auto whose whole-problem plan is a
+// 192-row tile launch but whose refined tail beats it (6144^3: four waves of
+// 192x192 tiles vs two W4S waves + 256x128 halves) runs the tail: report its
+// first, whole-wave launch, as for a W4 plan.
+int resolve_kernel(const Problem& p, int kernel) {
+  const int k = resolve_core(p, kernel);
+  if (kernel != kAuto || !is_t192(k) || p.K <= 0) return k;
+  const TailPlan t = tail_plan(p, kAuto);
+  if (!t.active() || !t.sub) return k;
+  if (p.dtype == kFP8) return fp8_dp_streams(to_args(p), t.tiles_dp) ? kFp8W4S : kFp8W4;
+  return w4s_fits(p) && t.tiles_dp >= 2LL * device_cus() ? kMfmaW4S : kMfmaW4;
+}
+
 // The two launches of a tail plan; false: run the problem as one launch (the
 // stream has no split-K counters yet inside a graph capture, or the workspace
 // was sized for another plan).
@@ -1279,7 +1318,11 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kT128x2:
     case kT256x128:
     case kFp8T128:
-    case kFp8T256x128: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream);
+    case kFp8T256x128:
+    case kT192:
+    case kT192x128:
+    case kFp8T192:
+    case kFp8T192x128: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream);
     case kMfmaW4S: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 7);
     case kF32_256s: return gemm_f32_256_launch(a, 1, stream);
     case kF32W4:
@@ -1445,6 +1488,10 @@ const char* kernel_name(int kernel) {
     case kT128: return "pdmb_t128_nn";
     case kT128x2: return "pdmb_t128x2_nn";
     case kT256x128: return "pdmb_t256x128_nn";
+    case kT192: return "pdmb_t192_nn";
+    case kT192x128: return "pdmb_t192x128_nn";
+    case kFp8T192: return "pdmb_fp8_t192_nt";
+    case kFp8T192x128: return "pdmb_fp8_t192x128_nt";
     case kF32W4: return "pdmb_f32_w4_nn";
     case kF32T128: return "pdmb_f32_t128_nn";
     case kF32T128x2: return "pdmb_f32_t128x2_nn";

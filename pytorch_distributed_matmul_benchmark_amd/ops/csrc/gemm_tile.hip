@@ -66,21 +66,29 @@ constexpr int NT = 256;
 template <int BM_, int BN_, int NS_, int OCC_>
 struct Cfg {
   static constexpr int BM = BM_, BN = BN_, NS = NS_, OCC = OCC_;
-  static_assert(BN == 128, "B image: one 256-B row of 128 columns per k");
-  static_assert(BM == 128 || BM == 256, "A image rows");
+  static_assert(BN == 128 || BN == 192, "B image: 128 columns per k, or three 64-column panels");
+  static_assert(BM == 128 || BM == 192 || BM == 256, "A image rows");
   static_assert(NS >= 2 && NS <= 4, "ring depth");
+  // bf16 / fp16 B image of a 192-column tile: three 64-column panels (below)
+  static constexpr bool PANEL = BN == 192;
   static constexpr int MB = BM / 32, NB = BN / 32;       // 16x16 blocks per wave (2 x 2 waves)
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BK * BN * 2;
   static constexpr int STAGE = A_BYTES + B_BYTES;
   static constexpr int PA = A_BYTES / 4096, PB = B_BYTES / 4096;  // 1 KiB pieces per wave
   static constexpr int P = PA + PB;
   static constexpr int G = MB * NB * 2;                  // MFMAs (gaps) per K-tile per wave
-  static_assert(NS * STAGE <= 160 * 1024 / OCC, "LDS");
+  // the stages, plus (one workgroup per CU) the fused epilogue's wave buffers
+  static_assert(NS * STAGE + (OCC == 1 ? 4 * epi_buf<NB>() : 0) <= 160 * 1024 / OCC, "LDS");
 };
 
 using CfgT128 = Cfg<128, 128, 4, 1>;
 using CfgT128x2 = Cfg<128, 128, 2, 2>;
 using CfgT256x128 = Cfg<256, 128, 3, 1>;
+// Round 5: 192-row tiles for grids that no 256- or 128-tile cuts into whole
+// waves — 3072^2 is 16 x 16 192x192 tiles (one wave of 256 CUs; 144 W4 tiles
+// fill 56 %), 2304^2 is 12 x 18 192x128 tiles (84 %; 81 W4 tiles fill 32 %).
+using CfgT192 = Cfg<192, 192, 3, 1>;
+using CfgT192x128 = Cfg<192, 128, 3, 1>;
 
 // Item schedule of one K-tile: which load follows MFMA `gap`. Three classes —
 // B fragment halves (2 NB, each two ds_read_b64_tr_b16), A fragment halves
@@ -191,6 +199,17 @@ __device__ __forceinline__ u32x4 b_rsrc(const Ctx<C>& c, int tile) {
 // (h-PA)*16 + wu*4 + [0,4) (4 x 256 B). The swizzles depend on (row >> 1) & 7
 // (A) and k & 11 (B) only, which those row offsets leave alone, so one
 // per-lane offset serves every piece.
+//
+// PANEL (BN = 192, bf16 / fp16): B is three images of 64 columns, [64 k][128
+// B] each (panel p: columns 64p .. 64p+63 at A_BYTES + 8 KiB p), 32-B unit v
+// (16 columns) of row k holding column unit v ^ s(k), s(k) = ((k >> 1) & 1) |
+// ((k >> 3) & 1) << 1. A 128-B row pitch puts rows of one parity on one half of
+// the 64 banks; a ds_read_b64_tr_b16 half-wave reads rows 8g + q4 (g = 0, 1;
+// q4 = 0..3), i.e. four rows per parity, which s(k) sends to four different
+// units: 64 distinct banks, conflict-free. DMA pieces: 8-row groups r of one
+// panel (1 KiB each); wave wu takes r = wu and wu + 4 of all three panels, so
+// (r & 1) — bit 3 of k — is the wave's own and one per-lane offset serves all
+// six pieces.
 template <int DT, class C>
 __device__ __forceinline__ void issue_piece(const Ctx<C>& c, u32x4 rb, uint32_t so, int tile, int h) {
   if constexpr (DT == kFP8) {  // A / Bt rows h' * 32 + wu * 8 + [0,8), K at tile * 128 B
@@ -203,6 +222,10 @@ __device__ __forceinline__ void issue_piece(const Ctx<C>& c, u32x4 rb, uint32_t 
   } else if (h < C::PA) {
     dma16_m0(c.ra, c.voffA, (uint32_t)tile * (BK * 2) + (uint32_t)(h * 32 * c.lda2),
              c.lds0 + so + (h * 32 + c.wu * 8) * 128);
+  } else if constexpr (C::PANEL) {
+    const int kb = h - C::PA, pn = kb >> 1, r = c.wu + 4 * (kb & 1);  // panel, 8-row group
+    dma16_m0(rb, c.voffB, (uint32_t)(r * 8 * c.ldb2 + pn * 128),
+             c.lds0 + so + C::A_BYTES + pn * 8192 + r * 1024);
   } else {
     const int kb = h - C::PA;
     dma16_m0(rb, c.voffB, (uint32_t)(kb * 16 * c.ldb2),
@@ -215,12 +238,14 @@ __device__ __forceinline__ s16x8 frag_a(const char* smem, uint32_t off, int m) {
   return *(const lds_s16x8*)(smem + m * 16 * 128 + off);
 }
 
-// B fragment half ks of block j (16 output columns): two transposed reads.
+// B fragment half ks of block j (16 output columns): two transposed reads
+// (rows 4 apart; PANEL: 128-B rows within the block's panel, which `off` holds).
 template <class C>
 __device__ __forceinline__ s16x8 frag_b(const char* smem, uint32_t off, int ks) {
-  const char* p = smem + C::A_BYTES + ks * 32 * 256 + off;
+  constexpr int RP = C::PANEL ? 128 : 256;  // B image row pitch
+  const char* p = smem + C::A_BYTES + ks * 32 * RP + off;
   s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p + 4 * 256));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p + 4 * RP));
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
@@ -393,14 +418,21 @@ __global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
     c.b_bytes = ((long long)(a.kb - k0 - 1) * a.ldb + (a.N - n0)) * 2;
     const int r = wu * 8 + (lane >> 3), lc8 = lane & 7;  // row of A piece 0
     c.voffA = (uint32_t)(r * c.lda2 + ((lc8 ^ ((r >> 1) & 7)) * 16));
-    const int lr16 = lane >> 4, lc16 = lane & 15;
-    const int k = wu * 4 + lr16;  // k row of B piece 0
-    const int s = (k & 3) | (((k >> 3) & 1) << 2);
-    const int n = ((lc16 >> 1) ^ s) * 16 + (lc16 & 1) * 8;  // column of this lane's 16 B
-    c.voffB = (uint32_t)(k * c.ldb2 + n * 2);
+    if constexpr (C::PANEL) {  // row lane >> 3 of an 8-row group (group parity wu & 1)
+      const int kr = lane >> 3;
+      const int s = ((kr >> 1) & 1) | ((wu & 1) << 1);
+      const int n = ((lc8 >> 1) ^ s) * 16 + (lc8 & 1) * 8;  // column (within the panel) of this lane's 16 B
+      c.voffB = (uint32_t)(kr * c.ldb2 + n * 2);
+    } else {
+      const int lr16 = lane >> 4, lc16 = lane & 15;
+      const int k = wu * 4 + lr16;  // k row of B piece 0
+      const int s = (k & 3) | (((k >> 3) & 1) << 2);
+      const int n = ((lc16 >> 1) ^ s) * 16 + (lc16 & 1) * 8;  // column of this lane's 16 B
+      c.voffB = (uint32_t)(k * c.ldb2 + n * 2);
+    }
     const int swA = (l16 >> 1) & 7;
     const int q4 = l16 >> 2, p4 = l16 & 3;
-    const int sB = q4 | ((g & 1) << 2);
+    const int sB = C::PANEL ? (((q4 >> 1) & 1) | ((g & 1) << 1)) : (q4 | ((g & 1) << 2));
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       uint32_t ao = (uint32_t)((wr * (C::BM / 2) + l16) * 128 + (((4 * ks + g) ^ swA) * 16));
@@ -410,7 +442,8 @@ __global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const int u = NB * wc + j;  // 32-B unit = columns 16u .. 16u+15 of the tile
-      uint32_t bo = (uint32_t)((8 * g + q4) * 256 + ((u ^ sB) * 32) + p4 * 8);
+      uint32_t bo = C::PANEL ? (uint32_t)((u >> 2) * 8192 + (8 * g + q4) * 128 + (((u & 3) ^ sB) * 32) + p4 * 8)
+                             : (uint32_t)((8 * g + q4) * 256 + ((u ^ sB) * 32) + p4 * 8);
       asm volatile("" : "+v"(bo));
       c.boff[j] = bo;
     }
@@ -526,6 +559,7 @@ __global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
 template <class C, bool FUSED = true>
 hipError_t launch(int dt, GemmArgs a, hipStream_t stream) {
   if (a.tile_end != 0 || a.tile_span < 0 || a.tile_base < 0) return hipErrorInvalidValue;
+  if (a.tile_span > 0 && (256 % C::BM || 256 % C::BN)) return hipErrorInvalidValue;  // no whole parts
   if (a.tile_span > 0) {  // refined tail: W4's 256x256 tile order, R parts per tile, unsplit
     a.tiles_m = (a.M + 255) / 256;
     a.tiles_n = (a.N + 255) / 256;
@@ -583,7 +617,7 @@ hipError_t launch(int dt, GemmArgs a, hipStream_t stream) {
 
 }  // namespace ktile
 
-// bm x 128 tiles (bm = 128 or 256).
+// bm x 128 / bm x 192 tiles (bm = 128, 192 or 256).
 bool gemm_tile_supported(int dt, int bm, const GemmArgs& a, size_t align_a, size_t align_b,
                          size_t align_c) {
   // Edge tiles (M % bm, N % 128): rows of A (and fp8's Bt) past M / N load
@@ -615,9 +649,10 @@ bool gemm_tile_supported(int dt, int bm, const GemmArgs& a, size_t align_a, size
   return true;
 }
 
-// kernel: kT128 | kT128x2 | kT256x128 (bf16 / fp16), kFp8T128 | kFp8T256x128 (fp8)
+// kernel: kT128 | kT128x2 | kT256x128 | kT192 | kT192x128 (bf16 / fp16),
+// kFp8T128 | kFp8T256x128 | kFp8T192 | kFp8T192x128 (fp8)
 hipError_t gemm_tile_launch(int kernel, int dt, GemmArgs a, hipStream_t stream) {
-  bool fp8 = kernel == kFp8T128 || kernel == kFp8T256x128;
+  bool fp8 = kernel == kFp8T128 || kernel == kFp8T256x128 || kernel == kFp8T192 || kernel == kFp8T192x128;
 #ifdef PDMB_EXPERIMENTS
   fp8 = fp8 || kernel == kFp8T128Unfused;
 #endif
@@ -632,6 +667,10 @@ hipError_t gemm_tile_launch(int kernel, int dt, GemmArgs a, hipStream_t stream) 
     case kT128: return ktile::launch<ktile::CfgT128>(dt, a, stream);
     case kT128x2: return ktile::launch<ktile::CfgT128x2>(dt, a, stream);
     case kT256x128: return ktile::launch<ktile::CfgT256x128>(dt, a, stream);
+    case kT192: return ktile::launch<ktile::CfgT192>(dt, a, stream);
+    case kT192x128: return ktile::launch<ktile::CfgT192x128>(dt, a, stream);
+    case kFp8T192: return ktile::launch<ktile::CfgT192>(dt, a, stream);
+    case kFp8T192x128: return ktile::launch<ktile::CfgT192x128>(dt, a, stream);
     default: return hipErrorInvalidValue;
   }
 }

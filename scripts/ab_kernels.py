@@ -10,6 +10,15 @@ equal to the first kernel's. The arm ``torch`` is the vendor library
     python scripts/ab_kernels.py --kernels auto,auto@PDMB_TILE_TAIL=0,torch ...  # "@VAR=VAL": env for that arm
     python scripts/ab_kernels.py --kernels fp8_w4,torch --dtype float8_e4m3fn \
         --shapes 16384,16384,2048 16384,16384,16384      # M,N,K (K sweeps: per-tile overhead)
+    python scripts/ab_kernels.py --kernels auto,torch --shapes 3072,3072,3072 --sessions 3
+
+``--sessions N`` (one session is not a result on GEMMs of tens
+of microseconds, whose same-process A/B swung ~9 % between sessions): the
+whole A/B runs in N fresh processes one after another; each prints its
+per-kernel lines (``session``: i), then one summary line per (shape, kernel)
+gives the median over sessions of the per-session medians, the min / max
+session median and the ratio to the last kernel's (the vendor arm when it is
+listed last) per session — the cross-session figures README / BASELINE cite.
 """
 import argparse
 import json
@@ -33,7 +42,11 @@ def main():
     ap.add_argument("--dtype", default="bfloat16")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--sessions", type=int, default=1,
+                    help="repeat the whole A/B in this many fresh processes and summarise")
     a = ap.parse_args()
+    if a.sessions > 1:
+        return sessions(a)
     ks = a.kernels.split(",")
     dt = getattr(torch, a.dtype)
     shapes = ([tuple(int(v) for v in s.split(",")) for s in a.shapes] if a.shapes
@@ -129,5 +142,46 @@ def main():
         torch.cuda.empty_cache()
 
 
+def sessions(a) -> int:
+    """Run the A/B in ``a.sessions`` fresh child processes and summarise."""
+    import subprocess
+
+    argv = [x for x in sys.argv[1:]]
+    i = argv.index("--sessions")
+    del argv[i:i + 2]
+    runs = []
+    for sid in range(a.sessions):
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), *argv], capture_output=True,
+                           text=True)
+        if r.returncode != 0:
+            sys.stderr.write(r.stderr[-3000:])
+            return r.returncode
+        recs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+        for d in recs:
+            d["session"] = sid
+            print(json.dumps(d), flush=True)
+        runs.append(recs)
+    kernels = a.kernels.split(",")
+    last = kernels[-1]
+    keys = [(d.get("m"), d["n"], d.get("k"), d.get("batch"), d["kernel"]) for d in runs[0]]
+    for key in keys:
+        meds, ratios = [], []
+        for recs in runs:
+            by = {(d.get("m"), d["n"], d.get("k"), d.get("batch"), d["kernel"]): d for d in recs}
+            meds.append(by[key]["median_tflops"])
+            ref = by.get(key[:4] + (last,))
+            if ref:
+                ratios.append(by[key]["median_tflops"] / ref["median_tflops"])
+        m, n, k, b, kern = key
+        print(json.dumps({"summary": True, "n": n, **({"m": m, "k": k} if m is not None else {}),
+                          **({"batch": b} if b else {}), "kernel": kern, "sessions": len(meds),
+                          "session_medians": meds, "median_tflops": round(statistics.median(meds), 1),
+                          "min_session": min(meds), "max_session": max(meds),
+                          "ratio_vs": last, "ratio_per_session": [round(x, 4) for x in ratios],
+                          "ratio_median": round(statistics.median(ratios), 4) if ratios else None}),
+              flush=True)
+    return 0
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -20,7 +20,7 @@ import torch  # noqa: E402
 from pytorch_distributed_matmul_benchmark_amd.ops import gemm  # noqa: E402
 
 SHAPES = [(256, 256, 32), (256, 256, 64), (256, 256, 96), (256, 256, 128), (512, 768, 192),
-          (1024, 1024, 1024)]
+          (1024, 1024, 1024), (3072, 3072, 1024), (2304, 2304, 1024)]
 # --tails: auto's wave-quantisation tail plans (a whole-wave launch, then a
 # split-K launch whose slices meet in-kernel): the tile-range form on these
 TAIL_SHAPES = [(6144, 6144, 6144), (6000, 6000, 6144), (7168, 7168, 7168), (5120, 5120, 5120), (4608, 4608, 3072),

@@ -208,7 +208,7 @@ def test_fp8_splitk_exact(M, N, K, splitk):
 
 
 # ---- fp8 tile family (gemm_tile.hip, DT = kFP8): under-filled fp8 grids ----
-@pytest.mark.parametrize("kernel", ["fp8_t128", "fp8_t256x128"])
+@pytest.mark.parametrize("kernel", ["fp8_t128", "fp8_t256x128", "fp8_t192", "fp8_t192x128"])
 @pytest.mark.parametrize("M,N,K,splitk", [(256, 128, 128, 1), (512, 384, 256, 1), (2048, 2048, 2048, 1),
                                           (4096, 512, 4096, 0), (4096, 512, 4096, 2), (2048, 1024, 4096, 4),
                                           (1024, 16384, 256, 1), (16384, 1024, 256, 1), (768, 640, 1152, 2)])
@@ -230,7 +230,7 @@ def test_fp8_tile_family_exact(kernel, M, N, K, splitk):
         assert torch.equal(C, ref)
 
 
-@pytest.mark.parametrize("kernel", ["fp8_t128", "fp8_t256x128"])
+@pytest.mark.parametrize("kernel", ["fp8_t128", "fp8_t256x128", "fp8_t192", "fp8_t192x128"])
 def test_fp8_tile_family_matches_w4_bitwise(kernel):
     """Unsplit, a block's K-tiles go through the same one-MFMA-per-128-K chain
     as in fp8 W4: bitwise equal on random operands, batched too."""

@@ -428,7 +428,7 @@ def test_w4_edge_tiles_masked(dtype, b, M, N, K, splitk):
     assert torch.isnan(big[..., :M, N:]).all() and torch.isnan(big[..., M:, :]).all()
 
 
-@pytest.mark.parametrize("kernel", ["t128", "t256x128", "t128x2"])
+@pytest.mark.parametrize("kernel", ["t128", "t256x128", "t128x2", "t192", "t192x128"])
 @pytest.mark.parametrize("M,N,K,splitk", [(300, 520, 256, 1), (1000, 1000, 512, 1), (3000, 7000, 512, 1),
                                          (700, 264, 2048, 2)])
 def test_tile_family_edge_tiles_masked(kernel, M, N, K, splitk):
@@ -1050,3 +1050,70 @@ def test_batched_streaming_gemm_runs_per_element(dtype, bcast):
     out = torch.empty_like(C)
     gemm.bench_matmul(A8, B8, out, iters=2, warmup=1)
     assert torch.equal(out, C)
+
+
+
+# ---- 192-row tiles (round 5): T192 (192x192, B as three 64-column panels) and
+# T192x128 — the grids no 256- / 128-tile cuts into whole waves -----------------
+@pytest.mark.parametrize("kernel", ["t192", "t192x128"])
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+@pytest.mark.parametrize("b,M,N,K,splitk", [(1, 3072, 3072, 1024, 1), (1, 2304, 2304, 768, 1),
+                                            (1, 192, 192, 64, 1), (1, 384, 576, 128, 1),
+                                            (2, 576, 384, 320, 1), (1, 1920, 1152, 2048, 2),
+                                            (1, 768, 768, 4096, 4), (1, 1000, 1048, 704, 1)])
+def test_t192_exact_small_integers(kernel, dtype, b, M, N, K, splitk):
+    """Exact on small integers (every fp32 partial sum exact): one and several
+    tiles, batched, split-K 2 / 4 (odd K-tile counts), edge tiles in M and N
+    (1000 x 1048), K of one K-tile; nothing written outside C."""
+    dt = DT[dtype]
+    g = torch.Generator(device="cuda").manual_seed(b * 11 + M + 3 * N + K + splitk)
+    A = torch.randint(-3, 4, (b, M, K), device="cuda", generator=g).to(dt)
+    B = torch.randint(-3, 4, (b, K, N), device="cuda", generator=g).to(dt)
+    big = torch.full((b, M + 8, N + 24), float("nan"), device="cuda", dtype=dt)
+    out = big[:, :M, :N]
+    if b == 1:
+        A, B, out = A[0], B[0], out[0]
+    assert gemm.kernel_for(A, B, out, kernel=kernel) == f"pdmb_{kernel}_nn"
+    assert gemm.splitk_for(A, B, out, kernel=kernel, splitk=splitk) == splitk
+    for _ in range(2):  # split-K counters re-zeroed by every launch
+        gemm.matmul(A, B, out=out, kernel=kernel, splitk=splitk)
+        assert torch.equal(out, (A.double() @ B.double()).to(dt))
+    assert torch.isnan(big[..., :M, N:]).all() and torch.isnan(big[..., M:, :]).all()
+
+
+@pytest.mark.parametrize("kernel", ["t192", "t192x128"])
+def test_t192_identity_asymmetric_and_bitwise_w4(kernel):
+    """A = I with an asymmetric B (catches a column permutation of the panel
+    image or the epilogue), and on random data unsplit bitwise equal to W4 (the
+    same MFMA chain per output block)."""
+    n = 768
+    I = torch.eye(n, device="cuda", dtype=torch.bfloat16)
+    Bs = ((torch.arange(n * 1152, device="cuda").view(n, 1152) * 7) % 97).to(torch.bfloat16)
+    assert torch.equal(gemm.matmul(I, Bs, kernel=kernel), Bs)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    A = torch.randn(1536, 2048, device="cuda", dtype=torch.bfloat16, generator=g)
+    B = torch.randn(2048, 1536, device="cuda", dtype=torch.bfloat16, generator=g)
+    ref = gemm.matmul(A, B, kernel="w4", splitk=1)
+    assert torch.equal(gemm.matmul(A, B, kernel=kernel, splitk=1), ref)
+
+
+@pytest.mark.parametrize("kernel", ["t192", "t192x128"])
+def test_t192_race_screen(kernel):
+    torch.manual_seed(31)
+    A = torch.randn(3072, 3072, device="cuda", dtype=torch.bfloat16)
+    B = torch.randn(3072, 3072, device="cuda", dtype=torch.bfloat16)
+    ref = gemm.matmul(A, B, kernel=kernel)
+    assert _relerr(ref, _ref(A, B)) < TOL[torch.bfloat16]
+    for _ in range(20):
+        assert torch.equal(gemm.matmul(A, B, kernel=kernel), ref)
+
+
+def test_t192_is_auto_on_one_wave_grids():
+    """3072^2 is one wave of 192x192 tiles (144 256-tiles fill 56 % of the
+    CUs) and 2304^2 84 % of one of 192x128: auto takes the 192-row tiles there
+    and keeps W4S / W4 where 256-tiles fill the chip."""
+    mk = lambda m, n, k: (torch.empty(m, k, device="cuda", dtype=torch.bfloat16),
+                          torch.empty(k, n, device="cuda", dtype=torch.bfloat16))
+    assert gemm.kernel_for(*mk(3072, 3072, 3072)) == "pdmb_t192_nn"
+    assert gemm.kernel_for(*mk(2304, 2304, 4096)) == "pdmb_t192x128_nn"
+    assert gemm.kernel_for(*mk(16384, 16384, 16384)) == "pdmb_w4s"

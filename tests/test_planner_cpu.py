@@ -109,8 +109,10 @@ def test_refined_tail_plans(C, monkeypatch):
     assert plan(C, FP8, 4608, 4608, 3072)[3] == (0, 1, 256, 2)
     assert plan(C, BF16, 16384, 16384, 16384)[3] == (0, 1, 0, 1)  # whole waves: one launch
     monkeypatch.setenv("PDMB_TAIL_REFINE", "0")
-    m1, S, t1, r = plan(C, BF16, 6144, 6144, 6144)[3]
-    assert r == 1 and S > 1 and (m1 > 0 or t1 > 0)
+    k, _, _, (m1, S, t1, r) = plan(C, BF16, 6144, 6144, 6144)
+    # without the refined tail: the split-K tail over W4, or (round 5) one
+    # launch of 192x192 tiles — 6144^3 is exactly 4 waves of them
+    assert r == 1 and ((S > 1 and (m1 > 0 or t1 > 0)) or (k == "pdmb_t192_nn" and (m1, t1) == (0, 0)))
     monkeypatch.delenv("PDMB_TAIL_REFINE")
     monkeypatch.setenv("PDMB_STREAMK", "1")
     m1, S, t1, r = plan(C, FP8, 5120, 5120, 5120)[3]
@@ -157,3 +159,19 @@ def test_f32_long_k_one_wave_runs_256s(C):
     assert plan(C, 0, 4096, 4096, 14336)[0] == "pdmb_f32_256s_nn"
     assert plan(C, 0, 4096, 4096, 4096)[0] == "pdmb_f32_t128x2_nn"
     assert plan(C, 0, 8192, 8192, 28672)[0] == "pdmb_f32_t128x2_nn"
+
+
+def test_t192_plans(C, monkeypatch):
+    """Round 5: the 192-row tiles where no 256- / 128-tile cuts the grid into
+    whole waves (3072^2: one wave of 192x192; 2304^2: 84 % of one of 192x128;
+    measured 1260 / 1078 TF vs hipBLASLt 1067 / 965, profiles/r7e_t192_ab_bf16.jsonl),
+    W4S / W4 where 256-tiles fill the chip, and PDMB_T192=0 leaves them out."""
+    monkeypatch.delenv("PDMB_T192", raising=False)
+    assert plan(C, BF16, 3072, 3072, 3072)[0] == "pdmb_t192_nn"
+    assert plan(C, BF16, 2304, 2304, 4096)[0] == "pdmb_t192x128_nn"
+    assert plan(C, FP8, 3072, 3072, 3072)[0] == "pdmb_fp8_t192_nt"
+    assert plan(C, BF16, 16384, 16384, 16384)[0] == "pdmb_w4s"
+    assert plan(C, BF16, 8192, 8192, 8192)[0] == "pdmb_w4s"
+    monkeypatch.setenv("PDMB_T192", "0")
+    assert "192" not in plan(C, BF16, 3072, 3072, 3072)[0]
+    assert "192" not in plan(C, FP8, 2304, 2304, 4096)[0]
