@@ -44,6 +44,11 @@ enum ExperimentKernel : int {
   kF32T128B32 = 52,      // kF32T128 with one b32 LDS read per B operand (round 3's first version)
   kF32W4B32 = 54,        // kF32W4 with one b32 LDS read per B operand (round 2's version)
   kF32_256p = 55,        // kF32_256s with software-pipelined fragments and a mid-tile barrier
+  // W4S power attribution (timing only, wrong results; scripts/power_attrib.py):
+  kMfmaW4SNoFrag = 56,   // no LDS fragment reads (MFMAs re-use their registers)
+  kMfmaW4SNoDma = 57,    // no LDS-DMA refills in the K-loop
+  kMfmaW4SNoEpi = 58,    // no C stores (no-access loads in their place)
+  kMfmaW4SMfmaOnly = 59, // neither fragment reads nor refills: MFMAs, waits, barriers
 };
 
 }  // namespace pdmb

@@ -22,7 +22,8 @@ static bool is_experiment(int k) {
     case kFp8W4Tall: case kFp8W4Wide: case kFp8W4Scaled: case kFp8W4Trace: case kMfmaW4Trace:
     case kFp8W4TS: case kFp8W4STS: case kMfmaW4STS: case kF32_256sDirect: case kFp8W4Unfused:
     case kT128Unfused: case kFp8T128Unfused: case kMfmaW4Unfused: case kF32T128B32:
-    case kF32W4B32: case kF32_256p:
+    case kF32W4B32: case kF32_256p: case kMfmaW4SNoFrag: case kMfmaW4SNoDma: case kMfmaW4SNoEpi:
+    case kMfmaW4SMfmaOnly:
       return true;
     default:
       return false;
@@ -55,6 +56,7 @@ static int experiment_resolve(const Problem& p, int kernel, bool fast, bool w4, 
     case kMfmaW4PersTrace:
       return (p.dtype == kBF16 && w4) ? kernel : -1;
     case kMfmaW4STrace: case kMfmaW4SRot: case kMfmaW4SRotTrace: case kMfmaW4STS:
+    case kMfmaW4SNoFrag: case kMfmaW4SNoDma: case kMfmaW4SNoEpi: case kMfmaW4SMfmaOnly:
       return (p.dtype == kBF16 && w4 && w4s_fits(p)) ? kernel : -1;
     case kMfmaW4Pers: return w4 ? kernel : -1;  // bf16 and fp16
     default: return -1;
@@ -91,6 +93,10 @@ static hipError_t experiment_launch(const Problem& p, int k, const GemmArgs& a, 
       return gemm_fp8_launch(s, 17, stream);
     }
     case kMfmaW4STS: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 11);
+    case kMfmaW4SNoFrag: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 13);
+    case kMfmaW4SNoDma: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 14);
+    case kMfmaW4SNoEpi: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 15);
+    case kMfmaW4SMfmaOnly: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 16);
     case kMfma256: return gemm256_launch(p.dtype, a, 0, stream);
     case kMfma256b: return gemm256_launch(p.dtype, a, 1, stream);
     case kMfma256c: return gemm256_launch(p.dtype, a, 2, stream);
@@ -148,6 +154,10 @@ static const char* experiment_name(int kernel) {
     case kF32T128B32: return "pdmb_f32_t128_b32";
     case kF32W4B32: return "pdmb_f32_w4_b32";
     case kFp8W4Trace: return "pdmb_fp8_w4_nt_trace";
+    case kMfmaW4SNoFrag: return "pdmb_w4s_diag_nofrag";
+    case kMfmaW4SNoDma: return "pdmb_w4s_diag_nodma";
+    case kMfmaW4SNoEpi: return "pdmb_w4s_diag_noepi";
+    case kMfmaW4SMfmaOnly: return "pdmb_w4s_diag_mfma_only";
     default: return "auto";
   }
 }

@@ -577,7 +577,11 @@ __device__ __forceinline__ u32x4 src_b(const Src& s, int kt, int ldb2) {
 // byte offset kaT; B of "t+3": descriptor rbT at its K-tile) and wait counts
 // (W0 at Bar0, W1 at Bar_mid); otherwise ktile<DT, 64, SO> item for item.
 // ZERO (K-tile 0 of a tile): the first MFMA of every accumulator takes C = 0.
-template <int DT, int SO, int W0, int W1, bool ZERO = false>
+// DIAG (timing-only experiment builds, WRONG results; the power attribution
+// of VERDICT r4 #8, scripts/power_attrib.py): bit 0 drops the fragment reads
+// (the MFMAs keep re-using the registers they hold), bit 1 the LDS-DMA refills;
+// every MFMA, wait and barrier stays.
+template <int DT, int SO, int W0, int W1, bool ZERO = false, int DIAG = 0>
 __device__ __forceinline__ void ktile_s(const Ctx& c, const char* smem, u32x4 raT, uint32_t kaT,
                                         u32x4 rbT, f32x4 (&acc)[8][8], Frag (&A)[8], Frag& A7c,
                                         Frag& A7n, Frag (&Bc)[8], Frag (&Bn)[8]) {
@@ -601,7 +605,11 @@ __device__ __forceinline__ void ktile_s(const Ctx& c, const char* smem, u32x4 ra
       else
         mfma_acc<DT>(acc[mi][ni], Bc[ni].k[ks], mi == 7 ? A7c.k[ks] : A[mi].k[ks]);
       const int it = kItems[mi][gap];
-      if (it == 1) {
+      if ((DIAG & 2) && it == 1) {
+        // no refill (timing-only)
+      } else if ((DIAG & 1) && it >= 100) {
+        // no fragment read (timing-only)
+      } else if (it == 1) {
         const int h = piece_of(mi, gap);
         if (h < 8) {
           dma16_at(raT, c.voffA, kaT + (uint32_t)(h * 32 * c.lda2), c.lds0w, SO + h * 32 * 128);
@@ -627,7 +635,10 @@ __device__ __forceinline__ void ktile_s(const Ctx& c, const char* smem, u32x4 ra
 
 // TRACE (kMfmaW4STrace): each workgroup stamps its start and end (after the
 // final drain) into the tile-trace row blockIdx.x, for the per-XCD tail.
-template <int DT, int TRACE = 0, bool NTS = true>  // NTS: non-temporal C stores (false: A/B)
+// DIAG: ktile_s's bits, plus bit 2: no C stores — 32 out-of-range LDS-DMA
+// loads per wave in their place, as before the first tile, so every vmcnt
+// wait counts the same (timing-only, WRONG results).
+template <int DT, int TRACE = 0, bool NTS = true, int DIAG = 0>  // NTS: non-temporal C stores (false: A/B)
 __global__ void __launch_bounds__(NT, 1) gemm_w4s(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 4 * kEpiBuf];
   TileTrace tr;
@@ -780,24 +791,25 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4s(GemmArgs a) {
     // DMAs they wait for), then pairs whose DMA targets stay in this tile
     // (W4's instruction mix: no selects), then the last two pairs, whose
     // targets cross into the next tile (nk >= 6: host-checked).
-    ktile_s<DT, 0, 48, 48, true>(c, smem, cur.ra, 2 * (BK * 2), src_b(cur, 3, c.ldb2), acc, A, A7a,
-                                 A7b, B0, B1);
-    ktile_s<DT, STAGE, 48, 16>(c, smem, cur.ra, 3 * (BK * 2), src_b(cur, 4, c.ldb2), acc, A, A7b, A7a,
-                               B1, B0);
+    constexpr int KD = DIAG & 3;
+    ktile_s<DT, 0, 48, 48, true, KD>(c, smem, cur.ra, 2 * (BK * 2), src_b(cur, 3, c.ldb2), acc, A, A7a,
+                                     A7b, B0, B1);
+    ktile_s<DT, STAGE, 48, 16, false, KD>(c, smem, cur.ra, 3 * (BK * 2), src_b(cur, 4, c.ldb2), acc, A,
+                                          A7b, A7a, B1, B0);
     int t = 2;
     for (; t + 4 < nk; t += 2) {
-      ktile_s<DT, 0, 16, 16>(c, smem, cur.ra, (uint32_t)(t + 2) * (BK * 2), src_b(cur, t + 3, c.ldb2),
-                             acc, A, A7a, A7b, B0, B1);
-      ktile_s<DT, STAGE, 16, 16>(c, smem, cur.ra, (uint32_t)(t + 3) * (BK * 2),
-                                 src_b(cur, t + 4, c.ldb2), acc, A, A7b, A7a, B1, B0);
+      ktile_s<DT, 0, 16, 16, false, KD>(c, smem, cur.ra, (uint32_t)(t + 2) * (BK * 2),
+                                        src_b(cur, t + 3, c.ldb2), acc, A, A7a, A7b, B0, B1);
+      ktile_s<DT, STAGE, 16, 16, false, KD>(c, smem, cur.ra, (uint32_t)(t + 3) * (BK * 2),
+                                            src_b(cur, t + 4, c.ldb2), acc, A, A7b, A7a, B1, B0);
     }
     for (; t < nk; t += 2) {
       u32x4 ra;
       uint32_t ka;
       tgt_a(t + 2, ra, ka);
-      ktile_s<DT, 0, 16, 16>(c, smem, ra, ka, tgt_b(t + 3), acc, A, A7a, A7b, B0, B1);
+      ktile_s<DT, 0, 16, 16, false, KD>(c, smem, ra, ka, tgt_b(t + 3), acc, A, A7a, A7b, B0, B1);
       tgt_a(t + 3, ra, ka);
-      ktile_s<DT, STAGE, 16, 16>(c, smem, ra, ka, tgt_b(t + 4), acc, A, A7b, A7a, B1, B0);
+      ktile_s<DT, STAGE, 16, 16, false, KD>(c, smem, ra, ka, tgt_b(t + 4), acc, A, A7b, A7a, B1, B0);
     }
     // The last MFMAs write their AGPRs before the epilogue reads them (asm
     // MFMAs are invisible to hipcc's hazard recognizer).
@@ -809,14 +821,27 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4s(GemmArgs a) {
     unsigned all = ~0u;
     asm volatile("" : "+s"(all));  // per tile, so the mbcnt is not hoisted either
     const int eln = (int)__builtin_amdgcn_mbcnt_hi(all, __builtin_amdgcn_mbcnt_lo(all, 0u));
+    if constexpr (DIAG & 4) {  // timing-only: 32 no-access loads for the 32 stores
+      u32x4 nul;
+      nul.x = 0u;
+      nul.y = 0u;
+      nul.z = 0u;
+      nul.w = 0x00020000u;
+      const uint32_t eb = c.lds0 + 2 * STAGE + wu * kEpiBuf;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      f32x4 v[8];
+      for (int i = 0; i < 32; ++i) dma16_m0(nul, 0u, 0u, eb);
+      (void)Cb;
+      (void)eln;
+    } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = acc[i][j];
-      store_block16<DT, false, false, 8, NTS>(ebuf, v, 1.0f, Cb, (long long)a.ldc * 2,
-                                              tm * BM + wr * 128 + i * 16, tn * BN + wc * 128, a.M,
-                                              a.N, eln);
+      for (int i = 0; i < 8; ++i) {
+        f32x4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = acc[i][j];
+        store_block16<DT, false, false, 8, NTS>(ebuf, v, 1.0f, Cb, (long long)a.ldc * 2,
+                                                tm * BM + wr * 128 + i * 16, tn * BN + wc * 128, a.M,
+                                                a.N, eln);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
     if (!more) break;
@@ -937,6 +962,17 @@ hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
     if (a.supertile == 1) a.supertile = 6;
     const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
     hipLaunchKernelGGL((kw4::gemm_w4s<kBF16, 1>), pg, block, 0, stream, a);
+    return hipGetLastError();
+  }
+  if (sub >= 13 && sub <= 16) {  // W4S power attribution (timing-only): DIAG 1, 2, 4, 3
+    if (S > 1 || a.pers_grid <= 0 || a.pers_grid % 8 || (a.K / kw4::BK) % 2 || a.K / kw4::BK < 6 ||
+        dt != kBF16)
+      return hipErrorInvalidValue;
+    const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
+    if (sub == 13) hipLaunchKernelGGL((kw4::gemm_w4s<kBF16, 0, true, 1>), pg, block, 0, stream, a);
+    if (sub == 14) hipLaunchKernelGGL((kw4::gemm_w4s<kBF16, 0, true, 2>), pg, block, 0, stream, a);
+    if (sub == 15) hipLaunchKernelGGL((kw4::gemm_w4s<kBF16, 0, true, 4>), pg, block, 0, stream, a);
+    if (sub == 16) hipLaunchKernelGGL((kw4::gemm_w4s<kBF16, 0, true, 3>), pg, block, 0, stream, a);
     return hipGetLastError();
   }
   if (sub == 8) {  // W4S with per-workgroup start / end stamps
