@@ -10,7 +10,8 @@ KS=${KS:-auto}
 pass() {
   local name=$1; shift
   timeout -k 10 240 rocprofv3 --kernel-trace "$@" --output-format csv -d $OUT/$name -o run -- \
-      python3 scripts/prof_gemm_arms.py --n $N --reps 3 --kernels $KS --dtype ${DT:-bfloat16} > $OUT/$name.log 2>&1
+      python3 scripts/prof_gemm_arms.py --n $N --reps ${REPS:-3} --kernels $KS --dtype ${DT:-bfloat16} \
+      ${SHAPE:+--shape $SHAPE} > $OUT/$name.log 2>&1
   local rc=$?
   echo "pass $name rc=$rc"
   case $rc in 124|134|137|139) exit $rc;; esac

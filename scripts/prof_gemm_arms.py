@@ -24,24 +24,26 @@ def main():
     ap.add_argument("--dtype", default="bfloat16")
     ap.add_argument("--kernels", default="auto", help="comma list of native kernels")
     ap.add_argument("--no-torch", action="store_true")
+    ap.add_argument("--shape", default=None, help="M,N,K (instead of the square --n)")
     a = ap.parse_args()
     dt = getattr(torch, a.dtype)
     n = a.n
+    m, nn, kk = (int(x) for x in a.shape.split(",")) if a.shape else (n, n, n)
     torch.manual_seed(0)
     if dt == torch.float8_e4m3fn:  # per-tensor scaled e4m3, B column-major; torch arm = _scaled_mm
-        A, _ = gemm.fp8_quantize(torch.randn(n, n, device="cuda"))
-        B, _ = gemm.fp8_quantize(torch.randn(n, n, device="cuda"), colmajor=True)
+        A, _ = gemm.fp8_quantize(torch.randn(m, kk, device="cuda"))
+        B, _ = gemm.fp8_quantize(torch.randn(kk, nn, device="cuda"), colmajor=True)
         one = torch.ones((), device="cuda")
 
         def torch_mm(A, B, out):
             torch._scaled_mm(A, B, scale_a=one, scale_b=one, out_dtype=torch.bfloat16)
     else:
-        A = torch.randn(n, n, device="cuda", dtype=dt)
-        B = torch.randn(n, n, device="cuda", dtype=dt)
+        A = torch.randn(m, kk, device="cuda", dtype=dt)
+        B = torch.randn(kk, nn, device="cuda", dtype=dt)
 
         def torch_mm(A, B, out):
             torch.matmul(A, B, out=out)
-    C = torch.empty(n, n, device="cuda", dtype=gemm.out_dtype(dt))
+    C = torch.empty(m, nn, device="cuda", dtype=gemm.out_dtype(dt))
     ks = a.kernels.split(",")
     for _ in range(2):  # warm (clocks, caches, code objects)
         for k in ks:

@@ -8,7 +8,8 @@ from pytorch_distributed_matmul_benchmark_amd.ops import gemm
 
 pytestmark = pytest.mark.gpu
 FP8 = torch.float8_e4m3fn
-FP8_KERNELS = ("pdmb_fp8_w4_nt", "pdmb_fp8_w4s", "pdmb_fp8_t128_nt", "pdmb_fp8_t256x128_nt")
+FP8_KERNELS = ("pdmb_fp8_w4_nt", "pdmb_fp8_w4s", "pdmb_fp8_t128_nt", "pdmb_fp8_t256x128_nt",
+               "pdmb_fp8_t192_nt", "pdmb_fp8_t192x128_nt")
 
 
 def _ints(shape, g, lo=-3, hi=4):

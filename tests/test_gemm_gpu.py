@@ -32,7 +32,8 @@ def test_native_extension_is_loaded():
 FAST = ["mfma256d", "mfma256", "mfma256b", "mfma256c"]
 
 
-TILED = ("pdmb_w4_nn", "pdmb_t256x128_nn", "pdmb_t128_nn", "pdmb_t128x2_nn", "pdmb_w4s")
+TILED = ("pdmb_w4_nn", "pdmb_t256x128_nn", "pdmb_t128_nn", "pdmb_t128x2_nn", "pdmb_w4s",
+         "pdmb_t192_nn", "pdmb_t192x128_nn")
 F32 = ("pdmb_f32_256s_nn", "pdmb_f32_w4_nn", "pdmb_f32_t128_nn", "pdmb_f32_t128x2_nn")
 
 

@@ -70,7 +70,8 @@ def test_torchrun_rccl_single_rank(mode, extra):
                 "--check", *extra])
     assert "Results for 2048x2048" in out and "PASS" in out
     assert "FAIL" not in out and "ERROR" not in out
-    assert any(k in out for k in ("pdmb_w4_nn", "pdmb_w4s", "pdmb_t128", "pdmb_t256x128", "pdmb_mfma256"))
+    assert any(k in out for k in ("pdmb_w4_nn", "pdmb_w4s", "pdmb_t128", "pdmb_t256x128", "pdmb_t192",
+                                 "pdmb_mfma256"))
 
 
 def test_bench_json_contract():
