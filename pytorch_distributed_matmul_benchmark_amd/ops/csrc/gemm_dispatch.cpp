@@ -263,6 +263,7 @@ struct KernelModel {
   double kt;
   int cls;   // 0: bf16 / fp16, 1: fp8, 2: fp32
   int maxS;  // largest split-K (1: the kernel does not split)
+  double kt2 = 0.0;  // per K-tile on grids of two or more waves (0: kt)
 };
 static constexpr KernelModel kModels[] = {
     {kMfmaW4, 256, 256, 1, 1.42, 0, 8},
@@ -281,11 +282,14 @@ static constexpr KernelModel kModels[] = {
     // A/B, profiles/r7e_t192_ab_*.jsonl: bf16 3072^3 46 us = 48 K-tiles x 0.87
     // + 4, 6144^3 340 us = 4 waves x (96 x 0.84 + 4); fp8 3072^3 23.9 us = 24 x
     // 0.83 + 4; T192x128 2304^2 x 4096 40.9 us = 64 x 0.61 x boost + 4).
-    // Listed last: the incumbents keep ties.
+    // Listed last: the incumbents keep ties. T192x128 runs slower per K-tile
+    // past one wave (profiles/r7j_t192_ab_bf16.jsonl: 1024 x 9216 x 16384 332 us
+    // over 2 waves, 2560 x 4608 x 16384 341 us, 2304 x 8192 x 16384 530 us over
+    // 3 waves: 0.65-0.67 per K-tile, where it lost 7-8 % to W4 on the first two).
     {kT192, 192, 192, 1, 0.86, 0, 8},
-    {kT192x128, 192, 128, 1, 0.60, 0, 8},
+    {kT192x128, 192, 128, 1, 0.60, 0, 8, 0.67},
     {kFp8T192, 192, 192, 1, 0.83, 1, 8},
-    {kFp8T192x128, 192, 128, 1, 0.60, 1, 8},
+    {kFp8T192x128, 192, 128, 1, 0.60, 1, 8, 0.67},
 };
 static int dt_class(const Problem& p) { return p.dtype == kFP8 ? 1 : p.dtype == kF32 ? 2 : 0; }
 static constexpr double kFixedUs = 4.0;   // launch + prologue + epilogue
@@ -348,7 +352,8 @@ static double plan_cost_tiles(const Problem& p, int kernel, int S, long long T) 
   const long long waves = (units + slots - 1) / slots;
   const double busy = (double)units / (double)(waves * slots);
   const double boost = m.cls == 2 ? 1.0 : 0.62 + 0.38 * busy;  // power headroom (not fp32)
-  double t = (double)waves * (per * m.kt * boost + kFixedUs);
+  const double kt = waves > 1 && m.kt2 > 0 ? m.kt2 : m.kt;
+  double t = (double)waves * (per * kt * boost + kFixedUs);
   if (S > 1) t += (double)T * (S - 1) * 2.0 * m.bm * m.bn * 4.0 / kSlabBw + kMeetUs;
   return t;
 }

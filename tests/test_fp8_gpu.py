@@ -308,6 +308,7 @@ def test_fp8_wave_tail_split(M, N, K, form, monkeypatch):
     if form == "rows":
         monkeypatch.setenv("PDMB_TILE_TAIL", "0")
     monkeypatch.setenv("PDMB_TAIL_REFINE", "0")  # the split-K forms (refined: test_gemm_gpu.py)
+    monkeypatch.setenv("PDMB_T192", "0")  # else a whole 192-row tile plan beats the split forms
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     Af, Bf = _ints((M, K), g, -2, 3), _ints((K, N), g, -2, 3)
     A8, B8 = Af.to(FP8), _colmajor(Bf.to(FP8))

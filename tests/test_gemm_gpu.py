@@ -459,6 +459,7 @@ def test_auto_wave_tail_split(M, N, K, form, monkeypatch):
     past M, the same bits under graph replay."""
     if form == "rows":
         monkeypatch.setenv("PDMB_TILE_TAIL", "0")
+    monkeypatch.setenv("PDMB_T192", "0")  # else a whole 192-row tile plan beats the split forms
     dt = torch.bfloat16
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     A = torch.randint(-3, 4, (M, K), device="cuda", generator=g).to(dt)

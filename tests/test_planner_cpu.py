@@ -175,3 +175,14 @@ def test_t192_plans(C, monkeypatch):
     monkeypatch.setenv("PDMB_T192", "0")
     assert "192" not in plan(C, BF16, 3072, 3072, 3072)[0]
     assert "192" not in plan(C, FP8, 2304, 2304, 4096)[0]
+
+
+def test_t192x128_multi_wave_rate(C, monkeypatch):
+    """T192x128 is priced slower per K-tile past one wave (kModels kt2; measured
+    0.65-0.67 us vs 0.61 on one wave, profiles/r7j_t192_ab_bf16.jsonl): the two
+    two-wave grids where it lost 7-8 % to W4 go back to W4, one-wave grids keep it."""
+    monkeypatch.delenv("PDMB_T192", raising=False)
+    for shape in ((1024, 9216, 16384), (2560, 4608, 16384)):
+        assert "192" not in plan(C, BF16, *shape)[0], shape
+    for shape in ((2048, 2304, 4096), (3072, 1536, 4096), (4608, 1024, 4096)):
+        assert plan(C, BF16, *shape)[0] == "pdmb_t192x128_nn", shape
