@@ -62,7 +62,7 @@ run_stage() {
                  grep '^{' "$OUT/bench_quick.log" > "$OUT/bench_quick.json" ;;
     overlap_proxy) step overlap_proxy 900 python scripts/overlap_proxy.py &&
                    grep '^{' "$OUT/overlap_proxy.log" > "$OUT/overlap_proxy.jsonl" ;;
-    rocprof_bench) step rocprof_bench 400 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof" -o bench -- \
+    rocprof_bench) step rocprof_bench 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/rocprof" -o bench -- \
                      python3 bench.py --steps 20 --warmup 5 ;;
     selflaunch2) step selflaunch2 400 python bench.py --gpus 2 --dist-backend gloo --size 4096 --steps 3 \
                    --warmup 1 --extra-steps 2 --extra-warmup 1 ;;

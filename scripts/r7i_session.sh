@@ -12,6 +12,6 @@ echo "== bench $(date +%T)"
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $OUT/bench.log 2>&1 || exit $?
 grep '^{' $OUT/bench.log > $OUT/bench.json; cut -c1-400 $OUT/bench.json
 echo "== rocprof $(date +%T)"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/rocprof -o bench -- python3 bench.py --steps 20 --warmup 5 --extra-steps 0 > $OUT/rocprof.log 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/rocprof -o bench -- python3 bench.py --steps 20 --warmup 5 --extra-steps 0 > $OUT/rocprof.log 2>&1 || exit $?
 find $OUT/rocprof -name "*kernel_stats.csv" | head -2
 echo "== done $(date +%T)"
