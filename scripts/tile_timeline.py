@@ -68,6 +68,10 @@ def analyse(tr: torch.Tensor) -> dict:
     for r in rows:
         per_xcd.setdefault(r[5] & 0xF, []).append(r[3])
     xcd_end = {x: statistics.median(v) - t0 for x, v in sorted(per_xcd.items())}
+    per_xcd_loop, per_xcd_start = {}, {}
+    for r in rows:
+        per_xcd_loop.setdefault(r[5] & 0xF, []).append(r[2] - r[1])
+        per_xcd_start.setdefault(r[5] & 0xF, []).append(r[1] - t0)
 
     def us(x):
         return round(x * TICK_US, 2)
@@ -84,6 +88,10 @@ def analyse(tr: torch.Tensor) -> dict:
         "tail_us": us(max(ends) - statistics.median(ends)),
         # median end of each XCD's workgroups: XCDs that run faster idle at the end
         "xcd_end_us": [us(v) for v in xcd_end.values()],
+        # per XCD: median K-loop time and median time its K-loops started
+        "xcd_loop_us": [us(statistics.median(v)) for _, v in sorted(per_xcd_loop.items())],
+        "xcd_loop_start_us": [us(statistics.median(v)) for _, v in sorted(per_xcd_start.items())],
+        "loop_min_us": us(min(loop)), "loop_max_us": us(max(loop)),
         "xcd_idle_frac": round(sum(max(xcd_end.values()) - v for v in xcd_end.values())
                                / (len(xcd_end) * max(xcd_end.values())), 4),
     }
