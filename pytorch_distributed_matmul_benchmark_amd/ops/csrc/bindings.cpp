@@ -403,7 +403,13 @@ at::Tensor ipc_empty(std::vector<int64_t> shape, at::ScalarType dtype, int64_t d
       }
     }
   }
-  if (!p) {
+  if (p) {
+    // A released buffer returns to the pool when its last torch reference
+    // goes, which can be before this device's queued work on it has run
+    // (hipFree would have synchronized): drain the device before handing it
+    // out again. Setup-time only (ipc_empty is never called in a timed loop).
+    check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize (ipc_empty reuse)");
+  } else {
     check_hip(hipMalloc(&p, bytes), "hipMalloc (ipc_empty)");
     if (arena) {
       std::lock_guard<std::mutex> lk(g_ipc_mu);
