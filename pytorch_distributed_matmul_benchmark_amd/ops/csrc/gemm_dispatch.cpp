@@ -212,6 +212,7 @@ static int resolve_core(const Problem& p, int kernel) {
     case kF32W4: return f32fast ? kF32W4 : -1;  // same constraints as f32_256
     case kF32T128: return p.dtype == kF32 && supports(p, kF32T128) ? kF32T128 : -1;
     case kF32T128x2: return p.dtype == kF32 && supports(p, kF32T128) ? kF32T128x2 : -1;
+    case kF32T64: return p.dtype == kF32 && supports(p, kF32T64) ? kF32T64 : -1;
     default:
       return is_experiment(kernel) ? experiment_resolve(p, kernel, fast, w4, t128, f32fast) : -1;
   }
@@ -290,6 +291,14 @@ static constexpr KernelModel kModels[] = {
     {kT192x128, 192, 128, 1, 0.60, 0, 8, 0.67},
     {kFp8T192, 192, 192, 1, 0.83, 1, 8},
     {kFp8T192x128, 192, 128, 1, 0.60, 1, 8, 0.67},
+    // round 5: the exact-fp32 64x128 tile for shard grids that a 128x128 tile
+    // fills only by splitting K (4096 x 512 x 4096: 128 tiles x 2 slices; 256
+    // 64x128 tiles run unsplit). 0.92 us per K-tile (half a T128 K-tile's
+    // MFMAs at 2 % below its rate: one barrier per 2048 MFMA cycles instead of
+    // 4096), fit to 4096 x {512, 1024} x 4096 and 2048 x 1024 x 2048
+    // (profiles/r7p_f32_t64_ab.jsonl: 140.6 vs 139.0 TF for f32_t128 x 2 at
+    // 4096 x 512 x 4096, 136.2 vs 127.7 at 2048 x 1024 x 2048).
+    {kF32T64, 64, 128, 1, 0.92, 2, 8},
 };
 static int dt_class(const Problem& p) { return p.dtype == kFP8 ? 1 : p.dtype == kF32 ? 2 : 0; }
 static constexpr double kFixedUs = 4.0;   // launch + prologue + epilogue
@@ -376,7 +385,7 @@ static bool supports(const Problem& p, int kernel) {
   if (kernel == kFp8W4) return gemm_fp8_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   if (kernel == kF32_256s || kernel == kF32W4)
     return p.dtype == kF32 && gemm_f32_256_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
-  if (kernel == kF32T128 || kernel == kF32T128x2)
+  if (kernel == kF32T128 || kernel == kF32T128x2 || kernel == kF32T64)
     return p.dtype == kF32 && gemm_f32_tile_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   return gemm_tile_supported(p.dtype, model_of(kernel).bm, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
 }
@@ -393,9 +402,13 @@ static Plan plan(const Problem& p, int kernel) {
   // PDMB_T192=0 (read per call; A/B): auto leaves the 192-row tiles out
   const char* t192env = std::getenv("PDMB_T192");
   const bool no192 = kernel == kAuto && t192env && std::atoi(t192env) == 0;
+  // PDMB_F32T64=0 (read per call; A/B): auto leaves the 64x128 fp32 tile out
+  const char* t64env = std::getenv("PDMB_F32T64");
+  const bool no64 = kernel == kAuto && t64env && std::atoi(t64env) == 0;
   for (const KernelModel& m : kModels) {
     if (kernel != kAuto && kernel != m.kernel) continue;
     if (no192 && is_t192(m.kernel)) continue;
+    if (no64 && m.kernel == kF32T64) continue;
     if (m.cls != dt_class(p) || !supports(p, m.kernel)) continue;
     any = true;
     for (int S : kS) {
@@ -410,6 +423,13 @@ static Plan plan(const Problem& p, int kernel) {
       // on any grid.
       if (kernel == kAuto && m.cls == 2 && m.occ > 1 &&
           tiles_of(p, m.kernel) < (long long)(p.cus > 0 ? p.cus : device_cus()) * m.occ)
+        continue;
+      // f32_t64 only within one wave: past it, it measured 3-4 % behind
+      // f32_t128 / f32_t128x2 (2048^3 138.0 vs 143.4, 8192 x 512 x 8192 143.6
+      // vs 148.0; profiles/r7p_f32_t64_ab.jsonl), and the fp32 tail plan
+      // (f32_tail_plan) prices the multi-wave grids against f32_t128x2.
+      if (kernel == kAuto && m.kernel == kF32T64 &&
+          tiles_of(p, m.kernel) > (long long)(p.cus > 0 ? p.cus : device_cus()))
         continue;
       const double c = plan_cost(p, m.kernel, S);
       if (c < bc * 0.97) {  // a different choice only for a clear win
@@ -428,7 +448,7 @@ static Plan plan(const Problem& p, int kernel) {
 static bool is_tiled(int k) {
   return k == kMfmaW4 || k == kT128 || k == kT128x2 || k == kT256x128 || k == kFp8T128 || k == kFp8T256x128 ||
          k == kF32W4 || k == kF32T128 || k == kF32T128x2 || k == kT192 || k == kT192x128 || k == kFp8T192 ||
-         k == kFp8T192x128;
+         k == kFp8T192x128 || k == kF32T64;
 }
 
 int choose_splitk(const Problem& p, int kernel) {
@@ -830,7 +850,7 @@ static hipError_t tiled_launch(const Problem& p, int k, GemmArgs a, void* part, 
     }
   }
   if (k == kF32W4) return gemm_f32_w4_launch(a, stream, sub);  // sub: the variant (experiments)
-  if (k == kF32T128 || k == kF32T128x2) return gemm_f32_tile_launch(a, stream, sub);  // sub: the variant
+  if (k == kF32T128 || k == kF32T128x2 || k == kF32T64) return gemm_f32_tile_launch(a, stream, sub);  // sub: the variant
   return k == kMfmaW4 ? gemm_w4_launch(p.dtype, a, stream, sub) : gemm_tile_launch(k, p.dtype, a, stream);
 }
 
@@ -1334,6 +1354,7 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kF32W4:
     case kF32T128: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream);
     case kF32T128x2: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream, 2);
+    case kF32T64: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream, 3);
     default:
       if (is_experiment(k)) return experiment_launch(p, k, a, stream);
       return gemm_generic_launch(p.dtype, a, generic_vec_ok(p), stream);
@@ -1500,6 +1521,7 @@ const char* kernel_name(int kernel) {
     case kFp8T192x128: return "pdmb_fp8_t192x128_nt";
     case kF32W4: return "pdmb_f32_w4_nn";
     case kF32T128: return "pdmb_f32_t128_nn";
+    case kF32T64: return "pdmb_f32_t64_nn";
     case kF32T128x2: return "pdmb_f32_t128x2_nn";
     default: return is_experiment(kernel) ? experiment_name(kernel) : "auto";
   }

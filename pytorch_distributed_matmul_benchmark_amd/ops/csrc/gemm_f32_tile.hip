@@ -41,13 +41,24 @@
 namespace pdmb {
 namespace kf32t {
 
-constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
-constexpr int MB = 4, NB = 4;                 // 16x16 blocks per wave
-constexpr int A_BYTES = BM * BK * 4;          // 16 KiB
+constexpr int BN = 128, BK = 32, NT = 256;
+constexpr int NB = 4;                         // 16x16 column blocks per wave
 constexpr int B_BYTES = BK * BN * 4;          // 16 KiB
-constexpr int STAGE = A_BYTES + B_BYTES;      // 32 KiB
-constexpr int P = 8;                          // DMA pieces per wave per K-tile (4 A + 4 B)
-constexpr int G = 2 * 4 * MB * NB;            // MFMAs per K-tile per wave (kb, e, mi, ni) = 128
+// Tile rows: 128 (kF32T128 / kF32T128x2) or 64 (kF32T64, round 5: a 64x128
+// tile, 4 waves x 32x64). The B image, its DMA pieces and the b128 B reads
+// are the same for both; A has BM / 32 pieces per wave and MB = BM / 32 row
+// blocks per wave.
+template <int BM_>
+struct Sh {
+  static constexpr int BM = BM_;
+  static_assert(BM == 64 || BM == 128, "tile rows");
+  static constexpr int MB = BM / 32;                  // 16x16 row blocks per wave
+  static constexpr int A_BYTES = BM * BK * 4;         // 16 / 8 KiB
+  static constexpr int STAGE = A_BYTES + B_BYTES;     // 32 / 24 KiB
+  static constexpr int PA = BM / 32;                  // A DMA pieces per wave per K-tile
+  static constexpr int P = PA + 4;                    // + 4 B pieces
+  static constexpr int G = 2 * 4 * MB * NB;           // MFMAs per K-tile per wave (kb, e, mi, ni)
+};
 typedef __attribute__((address_space(3))) f32x4 lds_f32x4;
 typedef __attribute__((address_space(3))) float lds_f32;
 
@@ -80,11 +91,12 @@ __device__ __forceinline__ void wait_barrier() {
 // else 32 b32, 2 kb x 4 ni x 4 e) and 8 DMA pieces spread Bresenham-style
 // over the 128 MFMA gaps, at most one per gap. Encoding: 0 none; 1 + piece;
 // 100 + B read q; 200 + A read q.
-template <bool BV>
+template <class H, bool BV>
 struct Sched {
+  static constexpr int G = H::G;
   int item[G];
   constexpr Sched() : item() {
-    const int T[3] = {BV ? 8 : 32, 8, P};
+    const int T[3] = {BV ? 8 : 32, 2 * H::MB, H::P};
     int n[3] = {0, 0, 0};
     for (int g = 0; g < G; ++g) {
       int best = -1, bd = 0;
@@ -120,13 +132,13 @@ constexpr int kBSwz = BV ? 0 : 4;
 // group uses output column 16 g + 4 r + ni of the wave's 64 (a column
 // permutation undone by the epilogue), so one read feeds four MFMAs. Else
 // b[kb][ni][e] = B[k][16 ni + l16] (one b32 read per MFMA operand).
-template <bool BV>
+template <int MB, bool BV>
 struct Frag {
   f32x4 a[2][MB];      // [kb][mi]
   float b[2][NB][4];   // [kb][ni][e]
 };
-template <>
-struct Frag<true> {
+template <int MB>
+struct Frag<MB, true> {
   f32x4 a[2][MB];      // [kb][mi]
   f32x4 b4[2][4];      // [kb][e], lanes ni
 };
@@ -152,29 +164,32 @@ __device__ __forceinline__ u32x4 b_rsrc(const Ctx& c, int tile) {
   return make_rsrc(c.Bb + off, c.b_bytes - off);
 }
 
-// DMA piece h (0..7) of K-tile `tile` into the stage at byte offset `so`.
-// h < 4: A rows 32 h + 8 wu + [0, 8) (8 x 128 B). h >= 4: B k-rows k0, k0 + 1
-// with k0 = 16 ((h-4) >> 1) + 4 wu + 2 ((h-4) & 1) (2 x 512 B).
+// DMA piece h (0..P-1) of K-tile `tile` into the stage at byte offset `so`.
+// h < PA: A rows 32 h + 8 wu + [0, 8) (8 x 128 B). h >= PA: B k-rows k0,
+// k0 + 1 with k0 = 16 (j >> 1) + 4 wu + 2 (j & 1), j = h - PA (2 x 512 B).
+template <class H>
 __device__ __forceinline__ void issue_piece(const Ctx& c, u32x4 rb, uint32_t so, int tile, int h) {
-  if (h < 4) {
+  if (h < H::PA) {
     dma16_m0(c.ra, c.voffA, (uint32_t)tile * (BK * 4) + (uint32_t)(h * 32 * c.lda4),
              c.lds0 + so + (h * 32 + c.wu * 8) * 128);
   } else {
-    const int j = h - 4;
+    const int j = h - H::PA;
     const int k0 = 16 * (j >> 1) + 4 * c.wu + 2 * (j & 1);
-    dma16_m0(rb, c.voffB, (uint32_t)(k0 * c.ldb4), c.lds0 + so + A_BYTES + k0 * 512);
+    dma16_m0(rb, c.voffB, (uint32_t)(k0 * c.ldb4), c.lds0 + so + H::A_BYTES + k0 * 512);
   }
 }
 
-// One K-tile: 128 MFMAs on `cur` (tile t), reading tile t+1's fragments into
+// One K-tile: G MFMAs on `cur` (tile t), reading tile t+1's fragments into
 // `nxt` from stage `sn`, DMA of tile t + NS into stage `sc`.
-template <int NS, bool BV>
+template <class H, int NS, bool BV>
 __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, uint32_t sc, uint32_t sn,
-                                      f32x4 (&acc)[MB][NB], const Frag<BV>& cur, Frag<BV>& nxt) {
-  constexpr Sched<BV> S{};
+                                      f32x4 (&acc)[H::MB][NB], const Frag<H::MB, BV>& cur,
+                                      Frag<H::MB, BV>& nxt) {
+  constexpr int MB = H::MB, G = H::G;
+  constexpr Sched<H, BV> S{};
   const int td = t + NS < c.nk ? t + NS : c.nk - 1;  // clamped tail DMAs (harmless re-reads)
   const u32x4 rb = b_rsrc(c, td);
-  wait_lgkm_barrier<P * (NS - 2)>();
+  wait_lgkm_barrier<H::P * (NS - 2)>();
   __builtin_amdgcn_sched_barrier(0);
   uint32_t ab[2], bb[NB];
 #pragma unroll
@@ -183,14 +198,14 @@ __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, uin
   for (int ni = 0; ni < NB; ++ni) bb[ni] = c.bbase[ni] + sn;
 #pragma unroll
   for (int gap = 0; gap < G; ++gap) {
-    const int kb = gap >> 6, e = (gap >> 4) & 3, mi = (gap >> 2) & 3, ni = gap & 3;
+    const int ni = gap % NB, mi = (gap / NB) % MB, e = (gap / (NB * MB)) % 4, kb = gap / (NB * MB * 4);
     if constexpr (BV)
       mfma(acc[mi][ni], cur.b4[kb][e][ni], cur.a[kb][mi][e]);
     else
       mfma(acc[mi][ni], cur.b[kb][ni][e], cur.a[kb][mi][e]);
     const int it = S.item[gap];
     if (it >= 200) {
-      const int q = it - 200, qk = q >> 2, qm = q & 3;
+      const int q = it - 200, qk = q / MB, qm = q % MB;
       nxt.a[qk][qm] = *(const lds_f32x4*)(smem + ab[qk] + qm * 2048);
     } else if (it >= 100) {
       if constexpr (BV) {
@@ -201,7 +216,7 @@ __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, uin
         nxt.b[qk][qn][qe] = *(const lds_f32*)(smem + bb[qn] + qk * 8192 + qe * 512);
       }
     } else if (it >= 1) {
-      issue_piece(c, rb, sc, td, it - 1);
+      issue_piece<H>(c, rb, sc, td, it - 1);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -209,8 +224,11 @@ __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, uin
 
 // NS: LDS stages (4: 128 KiB, one workgroup per CU; 2: 64 KiB, two per CU).
 // BV: b128 B reads (column-permuted MFMAs) instead of b32 ones.
-template <int NS, bool BV>
+// BM: tile rows (128, or 64 for kF32T64: 4 x 24 KiB stages).
+template <int NS, bool BV, int BM = 128>
 __global__ void __launch_bounds__(NT, NS == 2 ? 2 : 1) gemm_f32_t128(GemmArgs a) {
+  using H = Sh<BM>;
+  constexpr int MB = H::MB, P = H::P, STAGE = H::STAGE;
   constexpr int LDS_BYTES = NS * STAGE;
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
@@ -261,7 +279,7 @@ __global__ void __launch_bounds__(NT, NS == 2 ? 2 : 1) gemm_f32_t128(GemmArgs a)
     // the b32 reads, and global chunk lane & 31 (no swizzle) for the b128 reads
     // (see kBSwz)
     c.voffB = (uint32_t)((lane >> 5) * c.ldb4 + (((lane & 31) ^ (kBSwz<BV> * wu)) * 16));
-    const int rr = wr * 64 + l16;  // + 16 mi: same swizzle
+    const int rr = wr * (BM / 2) + l16;  // + 16 mi: same swizzle
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
       uint32_t ao = (uint32_t)(rr * 128 + (((kb * 4 + g) ^ ((rr >> 1) & 7)) * 16));
@@ -273,7 +291,7 @@ __global__ void __launch_bounds__(NT, NS == 2 ? 2 : 1) gemm_f32_t128(GemmArgs a)
       // BV: chunk wc * 16 + l16 (columns wc * 64 + 4 l16 .. + 3), bbase[0] only
       const int col = BV ? wc * 64 + 4 * l16 : wc * 64 + ni * 16 + l16;
       const int ch = (col >> 2) ^ (kBSwz<BV> * g);
-      uint32_t bo = (uint32_t)(A_BYTES + 4 * g * 512 + ch * 16 + (col & 3) * 4);
+      uint32_t bo = (uint32_t)(H::A_BYTES + 4 * g * 512 + ch * 16 + (col & 3) * 4);
       asm volatile("" : "+v"(bo));
       c.bbase[ni] = bo;
       if (BV) break;
@@ -294,10 +312,10 @@ __global__ void __launch_bounds__(NT, NS == 2 ? 2 : 1) gemm_f32_t128(GemmArgs a)
     const int tl = st < nk ? st : nk - 1;
     const u32x4 rb = b_rsrc(c, tl);
 #pragma unroll
-    for (int h = 0; h < P; ++h) issue_piece(c, rb, st * STAGE, tl, h);
+    for (int h = 0; h < P; ++h) issue_piece<H>(c, rb, st * STAGE, tl, h);
   }
   wait_barrier<P * (NS - 1)>();
-  Frag<BV> F0, F1;
+  Frag<MB, BV> F0, F1;
 #pragma unroll
   for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
@@ -317,12 +335,12 @@ __global__ void __launch_bounds__(NT, NS == 2 ? 2 : 1) gemm_f32_t128(GemmArgs a)
   // stage (t+1) % NS, refills stage t % NS with tile t + NS.
   int t = 0;
   for (; t + 1 < nk; t += 2) {
-    ktile<NS>(c, smem, t, (uint32_t)((t % NS) * STAGE), (uint32_t)(((t + 1) % NS) * STAGE), acc, F0, F1);
-    ktile<NS>(c, smem, t + 1, (uint32_t)(((t + 1) % NS) * STAGE), (uint32_t)(((t + 2) % NS) * STAGE), acc,
-              F1, F0);
+    ktile<H, NS>(c, smem, t, (uint32_t)((t % NS) * STAGE), (uint32_t)(((t + 1) % NS) * STAGE), acc, F0, F1);
+    ktile<H, NS>(c, smem, t + 1, (uint32_t)(((t + 1) % NS) * STAGE), (uint32_t)(((t + 2) % NS) * STAGE), acc,
+                 F1, F0);
   }
   if (t < nk)  // odd count: the last tile (its "next" reads are clamped re-reads)
-    ktile<NS>(c, smem, t, (uint32_t)((t % NS) * STAGE), (uint32_t)((t % NS) * STAGE), acc, F0, F1);
+    ktile<H, NS>(c, smem, t, (uint32_t)((t % NS) * STAGE), (uint32_t)((t % NS) * STAGE), acc, F0, F1);
   // Drain the tail DMAs and give the last MFMAs time to write their AGPRs
   // (asm MFMAs are invisible to hipcc's hazard recognizer).
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
@@ -367,7 +385,7 @@ __global__ void __launch_bounds__(NT, NS == 2 ? 2 : 1) gemm_f32_t128(GemmArgs a)
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = w[r];
     }
-    const int row0 = m0 + wr * 64 + mi * 16, col0 = n0 + wc * 64;
+    const int row0 = m0 + wr * (BM / 2) + mi * 16, col0 = n0 + wc * 64;
     if (interior)
       store_block16_f32<false, NB, BV>(ebuf, v, Cb, (long long)a.ldc * 4, row0, col0, a.M, a.N, lane);
     else
@@ -400,7 +418,8 @@ bool gemm_f32_tile_supported(const GemmArgs& a, size_t align_a, size_t align_b, 
 // whole waves); tile_span > 0 runs tiles [tile_base, +span), each split
 // a.splitk ways (the meet's tile id is the local index).
 hipError_t gemm_f32_tile_launch(GemmArgs a, hipStream_t stream, int variant) {
-  a.tiles_m = (a.M + kf32t::BM - 1) / kf32t::BM;
+  const int bm = variant == 3 ? 64 : 128;  // 3: kF32T64
+  a.tiles_m = (a.M + bm - 1) / bm;
   a.tiles_n = (a.N + kf32t::BN - 1) / kf32t::BN;
   a.supertile = choose_supertile(a.tiles_m, a.tiles_n);
   const int S = a.splitk > 1 ? a.splitk : 1;
@@ -427,6 +446,10 @@ hipError_t gemm_f32_tile_launch(GemmArgs a, hipStream_t stream, int variant) {
     return hipGetLastError();
   }
 #endif
+  if (variant == 3) {  // kF32T64: 64x128 tiles, 4 stages, one workgroup per CU
+    hipLaunchKernelGGL((kf32t::gemm_f32_t128<4, true, 64>), dim3((unsigned)nblocks), dim3(kf32t::NT), 0, stream, a);
+    return hipGetLastError();
+  }
   if (variant == 2) {  // kF32T128x2
     hipLaunchKernelGGL((kf32t::gemm_f32_t128<2, true>), dim3((unsigned)nblocks), dim3(kf32t::NT), 0, stream, a);
     return hipGetLastError();

@@ -34,7 +34,7 @@ FAST = ["mfma256d", "mfma256", "mfma256b", "mfma256c"]
 
 TILED = ("pdmb_w4_nn", "pdmb_t256x128_nn", "pdmb_t128_nn", "pdmb_t128x2_nn", "pdmb_w4s",
          "pdmb_t192_nn", "pdmb_t192x128_nn")
-F32 = ("pdmb_f32_256s_nn", "pdmb_f32_w4_nn", "pdmb_f32_t128_nn", "pdmb_f32_t128x2_nn")
+F32 = ("pdmb_f32_256s_nn", "pdmb_f32_w4_nn", "pdmb_f32_t128_nn", "pdmb_f32_t128x2_nn", "pdmb_f32_t64_nn")
 
 
 def _need(kernel):
@@ -205,13 +205,14 @@ def test_race_screen_repeated_runs(kernel):
 @pytest.mark.parametrize("M,N,K", [(256, 256, 32), (512, 768, 96), (1000, 1052, 320),
                                    (300, 200, 64), (2304, 2048, 1024)])
 @pytest.mark.parametrize("kernel", ["f32_256", "f32_256s", "f32_w4", "x_f32_256s_direct", "f32_t128",
-                                    "f32_t128x2", "x_f32_w4_b32", "x_f32_t128_b32"])
+                                    "f32_t128x2", "x_f32_w4_b32", "x_f32_t128_b32", "f32_t64"])
 def test_f32_256_exact_and_random(M, N, K, kernel):
     _need(kernel)
     g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
     A = torch.randint(-3, 4, (M, K), device="cuda", generator=g).float()
     B = torch.randint(-3, 4, (K, N), device="cuda", generator=g).float()
-    assert gemm.kernel_for(A, B, kernel=kernel).startswith(("pdmb_f32_256", "pdmb_f32_w4", "pdmb_f32_t128"))
+    assert gemm.kernel_for(A, B, kernel=kernel).startswith(("pdmb_f32_256", "pdmb_f32_w4", "pdmb_f32_t128",
+                                                            "pdmb_f32_t64"))
     C = gemm.matmul(A, B, kernel=kernel)
     assert torch.equal(C.double(), _ref(A, B))  # small integers: exact in fp32
     A = torch.randn(M, K, device="cuda", generator=g)
@@ -220,7 +221,7 @@ def test_f32_256_exact_and_random(M, N, K, kernel):
     assert _relerr(C, _ref(A, B)) < TOL[torch.float32]
 
 
-@pytest.mark.parametrize("kernel", ["f32_w4", "f32_t128"])
+@pytest.mark.parametrize("kernel", ["f32_w4", "f32_t128", "f32_t64"])
 @pytest.mark.parametrize("M,N,K,splitk,split", [(4096, 1024, 4096, 0, None), (4096, 2048, 4096, 0, None),
                                                 (2048, 2048, 2048, 0, None), (1000, 1052, 4096, 0, True),
                                                 (512, 512, 1024, 2, True), (4096, 4096, 4096, 0, False),
@@ -254,7 +255,7 @@ def test_f32_splitk_exact(kernel, M, N, K, splitk, split):
     assert torch.equal(gemm.matmul(A, B, kernel=kernel, splitk=splitk), C)
 
 
-F32_T128_ARMS = ["f32_t128", "f32_t128x2", "x_f32_t128_b32"]
+F32_T128_ARMS = ["f32_t128", "f32_t128x2", "x_f32_t128_b32", "f32_t64"]
 
 
 @pytest.mark.parametrize("M,N,K,b", [(128, 128, 32, 1), (256, 384, 96, 1), (1000, 1052, 320, 1),
@@ -264,7 +265,7 @@ F32_T128_ARMS = ["f32_t128", "f32_t128x2", "x_f32_t128_b32"]
 def test_f32_t128_exact_identity_and_batched(M, N, K, b, kernel):
     """The 128x128 exact-fp32 tile (gemm_f32_tile.hip; shipping: b128 B reads
     with column-permuted MFMAs; experiment arms: b32 B reads, 2 stages x 2
-    workgroups per CU): small integers exact (every fp32 partial sum exact),
+    workgroups per CU) and its 64x128 form (f32_t64): small integers exact (every fp32 partial sum exact),
     A = I with an asymmetric B (catches a column permutation the epilogue
     fails to undo), batched, edge tiles in M and N, one-K-tile problems."""
     _need(kernel)

@@ -32,11 +32,13 @@ def test_f32_shards_fill_the_chip(C, n, ws):
     wave, and the under-filled 4096 shards go to the small tile or a split W4."""
     shard = n // ws
     k, S, cost, _ = plan(C, F32, n, shard, n)
-    bm = 128 if k in ("pdmb_f32_t128_nn", "pdmb_f32_t128x2_nn") else 256
-    units = -(-n // bm) * -(-shard // bm) * max(S, 1)
+    bm, bn = {"pdmb_f32_t128_nn": (128, 128), "pdmb_f32_t128x2_nn": (128, 128),
+              "pdmb_f32_t64_nn": (64, 128)}.get(k, (256, 256))
+    units = -(-n // bm) * -(-shard // bn) * max(S, 1)
     assert units >= 192, (n, ws, k, S)
     if n == 4096:
-        assert k in ("pdmb_f32_t128_nn", "pdmb_f32_t128x2_nn") or (k == "pdmb_f32_w4_nn" and S > 1)
+        assert k in ("pdmb_f32_t128_nn", "pdmb_f32_t128x2_nn", "pdmb_f32_t64_nn") or (
+            k == "pdmb_f32_w4_nn" and S > 1)
 
 
 def test_f32_full_grids_take_two_128_tiles_per_cu(C):
@@ -186,3 +188,14 @@ def test_t192x128_multi_wave_rate(C, monkeypatch):
         assert "192" not in plan(C, BF16, *shape)[0], shape
     for shape in ((2048, 2304, 4096), (3072, 1536, 4096), (4608, 1024, 4096)):
         assert plan(C, BF16, *shape)[0] == "pdmb_t192x128_nn", shape
+
+
+def test_f32_t64_plans(C):
+    """Round 5: the 64x128 exact-fp32 tile where 128x128 tiles fill the chip
+    only by splitting K (4096 x 512 x 4096, the ws = 8 shard at 4k: 256 tiles
+    unsplit; 2048 x 1024 x 2048) — measured ahead of f32_t128 there
+    (profiles/r7p_f32_t64_ab.jsonl) — and never where f32_t128 runs a whole wave."""
+    assert plan(C, F32, 4096, 512, 4096)[:2] == ("pdmb_f32_t64_nn", 1)
+    assert plan(C, F32, 2048, 1024, 2048)[0] == "pdmb_f32_t64_nn"
+    for shape in ((4096, 1024, 4096), (2048, 2048, 2048), (8192, 512, 8192), (8192, 1024, 8192)):
+        assert plan(C, F32, *shape)[0] != "pdmb_f32_t64_nn", shape
