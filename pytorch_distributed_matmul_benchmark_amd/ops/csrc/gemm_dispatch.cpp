@@ -398,21 +398,42 @@ static Plan plan(const Problem& p, int kernel) {
   Plan best{-1, 1};
   double bc = 1e300;
   bool any = false;
-  static const int kS[] = {1, 2, 4, 8};
+  // Pass 0 prices the power-of-two splits; pass 1 the 3-way split, which then
+  // replaces the best of pass 0 only by a clear win (the plans of every grid
+  // it does not win stay as they were).
+  static const int kS0[] = {1, 2, 4, 8}, kS1[] = {3};
+  // PDMB_SPLIT3=0 (read per call; A/B): auto leaves the 3-way split out
+  const char* s3env = std::getenv("PDMB_SPLIT3");
+  const bool no3 = s3env && std::atoi(s3env) == 0;
   // PDMB_T192=0 (read per call; A/B): auto leaves the 192-row tiles out
   const char* t192env = std::getenv("PDMB_T192");
   const bool no192 = kernel == kAuto && t192env && std::atoi(t192env) == 0;
   // PDMB_F32T64=0 (read per call; A/B): auto leaves the 64x128 fp32 tile out
   const char* t64env = std::getenv("PDMB_F32T64");
   const bool no64 = kernel == kAuto && t64env && std::atoi(t64env) == 0;
+  for (int pass = 0; pass < 2; ++pass)
   for (const KernelModel& m : kModels) {
     if (kernel != kAuto && kernel != m.kernel) continue;
     if (no192 && is_t192(m.kernel)) continue;
     if (no64 && m.kernel == kF32T64) continue;
     if (m.cls != dt_class(p) || !supports(p, m.kernel)) continue;
     any = true;
-    for (int S : kS) {
+    const int* Ss = pass ? kS1 : kS0;
+    const int nS = pass ? 1 : 4;
+    for (int si = 0; si < nS; ++si) {
+      const int S = Ss[si];
       if (S > 4 && p.splitk != S) continue;
+      // The 3-way split (round 5; profiles/r7r_split3_ab_*.jsonl): 256 / 3
+      // slices fill a wave that 2 or 4 leave a quarter empty or over-full
+      // (bf16 2560 x 4096 x 16384 1238 vs 1091 TF, fp32 2560 x 256 x 8192 119.5
+      // vs 84.3). Auto takes it only with >= 32 K-tiles per slice — its
+      // reducer reads two slots per row with no row-ahead prefetch (S == 2 has
+      // one): bf16 1024^2 x 4096 (22 K-tiles per slice) ran 25.5 us vs 21.9 at
+      // S = 2 — and not on the 256^2 fp32 tile (fp32 2560 x 2048 x 4096 on
+      // f32_w4 129.0 vs 132.4 for f32_t128 x 4).
+      if (S == 3 && p.splitk != 3 &&
+          (no3 || (ktiles(p) + 2) / 3 < 32 || m.kernel == kF32W4))
+        continue;
       if (p.splitk > 0 && S != p.splitk) continue;
       if (!split_ok(p, m.kernel, S)) continue;
       // auto takes a two-per-CU fp32 tile only on grids whose tiles (not split

@@ -212,7 +212,8 @@ def test_fp8_splitk_exact(M, N, K, splitk):
 @pytest.mark.parametrize("kernel", ["fp8_t128", "fp8_t256x128", "fp8_t192", "fp8_t192x128"])
 @pytest.mark.parametrize("M,N,K,splitk", [(256, 128, 128, 1), (512, 384, 256, 1), (2048, 2048, 2048, 1),
                                           (4096, 512, 4096, 0), (4096, 512, 4096, 2), (2048, 1024, 4096, 4),
-                                          (1024, 16384, 256, 1), (16384, 1024, 256, 1), (768, 640, 1152, 2)])
+                                          (1024, 16384, 256, 1), (16384, 1024, 256, 1), (768, 640, 1152, 2),
+                                          (2048, 1024, 4096, 3)])
 def test_fp8_tile_family_exact(kernel, M, N, K, splitk):
     """fp8 T128 / T256x128 (A / Bt images with the fp8 swizzle, one 16x16x128
     MFMA per block per K-tile, alpha in the LDS-staged epilogue) on exact small

@@ -199,3 +199,19 @@ def test_f32_t64_plans(C):
     assert plan(C, F32, 2048, 1024, 2048)[0] == "pdmb_f32_t64_nn"
     for shape in ((4096, 1024, 4096), (2048, 2048, 2048), (8192, 512, 8192), (8192, 1024, 8192)):
         assert plan(C, F32, *shape)[0] != "pdmb_f32_t64_nn", shape
+
+
+def test_split3_plans(C, monkeypatch):
+    """Round 5: the 3-way split-K, priced after the power-of-two splits and
+    taken only by a clear win with >= 32 K-tiles per slice (and not on the
+    256^2 fp32 tile): measured ahead on these grids (profiles/r7r_split3_ab_*.jsonl),
+    left out where it lost (bf16 1024^2 x 4096, fp32 2560 x 2048 x 4096)."""
+    monkeypatch.delenv("PDMB_SPLIT3", raising=False)
+    assert plan(C, BF16, 2560, 4096, 16384)[:2] == ("pdmb_w4_nn", 3)
+    assert plan(C, BF16, 5120, 2048, 16384)[:2] == ("pdmb_w4_nn", 3)
+    assert plan(C, F32, 2560, 256, 8192)[1] == 3
+    assert plan(C, F32, 1536, 1536, 4096)[1] == 3
+    assert plan(C, BF16, 1024, 1024, 4096)[1] != 3
+    assert plan(C, F32, 2560, 2048, 4096)[1] != 3
+    monkeypatch.setenv("PDMB_SPLIT3", "0")
+    assert plan(C, BF16, 2560, 4096, 16384)[1] != 3
