@@ -398,10 +398,12 @@ static Plan plan(const Problem& p, int kernel) {
   Plan best{-1, 1};
   double bc = 1e300;
   bool any = false;
-  // Pass 0 prices the power-of-two splits; pass 1 the 3-way split, which then
-  // replaces the best of pass 0 only by a clear win (the plans of every grid
-  // it does not win stay as they were).
-  static const int kS0[] = {1, 2, 4, 8}, kS1[] = {3};
+  // Pass 0 prices the power-of-two splits; pass 1 the 3- (5-, 6-) way
+  // splits, whose cheapest plan then replaces the best of pass 0 only by a
+  // clear win (the plans of every grid it does not win stay as they were).
+  Plan alt{-1, 1};
+  double ac = 1e300;
+  static const int kS0[] = {1, 2, 4, 8}, kS1[] = {3, 5, 6};
   // PDMB_SPLIT3=0 (read per call; A/B): auto leaves the 3-way split out
   const char* s3env = std::getenv("PDMB_SPLIT3");
   const bool no3 = s3env && std::atoi(s3env) == 0;
@@ -419,10 +421,21 @@ static Plan plan(const Problem& p, int kernel) {
     if (m.cls != dt_class(p) || !supports(p, m.kernel)) continue;
     any = true;
     const int* Ss = pass ? kS1 : kS0;
-    const int nS = pass ? 1 : 4;
+    const int nS = pass ? 3 : 4;
     for (int si = 0; si < nS; ++si) {
       const int S = Ss[si];
-      if (S > 4 && p.splitk != S) continue;
+      // 5- / 6-way (round 5): exact fp32 only — its K-tiles carry 4x the MFMA
+      // time of bf16's, so the longer meet pays: fp32 1024 x 256 x 16384 92.8
+      // vs 68.2 TF, 512 x 6400 x 16384 136.4 vs 115.8, all six grids tried
+      // ahead; on bf16 two of six lost (2560 x 256 x 16384 515 vs 543;
+      // profiles/r7u_split56_ab_*.jsonl). PDMB_SPLIT56=0 leaves them out (A/B).
+      if ((S == 5 || S == 6) && p.splitk != S) {
+        const char* e56 = std::getenv("PDMB_SPLIT56");
+        if ((e56 && std::atoi(e56) == 0) || m.cls != 2 || (ktiles(p) + S - 1) / S < 32 || m.kernel == kF32W4)
+          continue;
+      } else if (S > 4 && p.splitk != S) {
+        continue;
+      }
       // The 3-way split (round 5; profiles/r7r_split3_ab_*.jsonl): 256 / 3
       // slices fill a wave that 2 or 4 leave a quarter empty or over-full
       // (bf16 2560 x 4096 x 16384 1238 vs 1091 TF, fp32 2560 x 256 x 8192 119.5
@@ -453,12 +466,18 @@ static Plan plan(const Problem& p, int kernel) {
           tiles_of(p, m.kernel) > (long long)(p.cus > 0 ? p.cus : device_cus()))
         continue;
       const double c = plan_cost(p, m.kernel, S);
-      if (c < bc * 0.97) {  // a different choice only for a clear win
+      if (pass) {  // the cheapest non-power-of-two plan, compared with pass 0's below
+        if (c < ac) {
+          ac = c;
+          alt = Plan{m.kernel, S, c};
+        }
+      } else if (c < bc * 0.97) {  // a different choice only for a clear win
         bc = c;
         best = Plan{m.kernel, S, c};
       }
     }
   }
+  if (alt.kernel >= 0 && ac < bc * 0.97) best = alt;
   if (best.kernel < 0 && any)  // the requested split is impossible for this K
     for (const KernelModel& m : kModels)
       if ((kernel == kAuto || kernel == m.kernel) && m.cls == dt_class(p) && supports(p, m.kernel))

@@ -227,7 +227,8 @@ def test_f32_256_exact_and_random(M, N, K, kernel):
                                                 (2048, 2048, 2048, 0, None), (1000, 1052, 4096, 0, True),
                                                 (512, 512, 1024, 2, True), (4096, 4096, 4096, 0, False),
                                                 (1000, 1052, 4096, 4, True), (700, 300, 2048, 8, True),
-                                                (1000, 1052, 4096, 3, True)])
+                                                (1000, 1052, 4096, 3, True), (1000, 300, 8192, 5, True),
+                                                (700, 300, 8192, 6, True)])
 def test_f32_splitk_exact(kernel, M, N, K, splitk, split):
     """Exact-fp32 W4 / T128 split-K for under-filled grids (matrix_parallel's
     fp32 shards): slices meet in-launch (splitk.h), edge tiles masked; exact on
@@ -698,7 +699,8 @@ def test_auto_plan_for_shard_shapes():
 @pytest.mark.parametrize("kernel,M,N,K,splitk", [
     ("auto", 8192, 1024, 8192, 0), ("auto", 2048, 2048, 2048, 0), ("t128", 4096, 512, 4096, 2),
     ("w4", 4096, 512, 4096, 8), ("t128", 4096, 4096, 4096, 1), ("t256x128", 4096, 2048, 4096, 1),
-    ("t256x128", 2048, 1024, 8192, 4), ("t128", 2560, 512, 8192, 3), ("w4", 2560, 4096, 16384, 3)])
+    ("t256x128", 2048, 1024, 8192, 4), ("t128", 2560, 512, 8192, 3), ("w4", 2560, 4096, 16384, 3),
+    ("t128", 1024, 256, 16384, 6), ("w4", 512, 5632, 16384, 5)])
 def test_tiled_random_and_bitwise_repeatable(kernel, M, N, K, splitk):
     """Random data vs fp64, and a race screen for the LDS-DMA ring and the
     split-K meeting: the slices meet in a fixed order, so every launch is

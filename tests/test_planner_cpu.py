@@ -215,3 +215,14 @@ def test_split3_plans(C, monkeypatch):
     assert plan(C, F32, 2560, 2048, 4096)[1] != 3
     monkeypatch.setenv("PDMB_SPLIT3", "0")
     assert plan(C, BF16, 2560, 4096, 16384)[1] != 3
+
+
+def test_split56_fp32_only(C, monkeypatch):
+    """Round 5: 5- / 6-way splits for exact fp32 only (measured ahead on six
+    fp32 grids, mixed on bf16; profiles/r7u_split56_ab_*.jsonl)."""
+    monkeypatch.delenv("PDMB_SPLIT56", raising=False)
+    assert plan(C, F32, 1024, 256, 16384)[1] in (5, 6)
+    assert plan(C, F32, 512, 6400, 16384)[1] in (5, 6)
+    assert plan(C, BF16, 2560, 256, 16384)[1] not in (5, 6)
+    monkeypatch.setenv("PDMB_SPLIT56", "0")
+    assert plan(C, F32, 1024, 256, 16384)[1] not in (5, 6)
