@@ -30,7 +30,7 @@ import torch
 from .models import (DISTRIBUTED_MODES, EXTRA_SCALING_MODES, OVERLAP_MODES, SCALING_MODES,
                      ModeResult, Workload, run_mode)
 from .models.common import tolerance
-from .ops.gemm import out_dtype as _gemm_out_dtype
+from .ops.gemm import KERNELS as _GEMM_KERNELS, out_dtype as _gemm_out_dtype
 from .parallel.dist import (DistContext, all_ok, barrier, cleanup_distributed, reduce_scalar,
                             setup_distributed, verify_collectives)
 from .utils.metrics import (balance_efficiency, bytes_per_element, dtype_from_name, dtype_name,
@@ -78,9 +78,7 @@ def build_parser(kind: str) -> argparse.ArgumentParser:
     g.add_argument("--backend", default="native", choices=["native", "torch"],
                    help="GEMM implementation on GPU: native gfx950 MFMA kernels (default) or "
                         "torch.matmul/hipBLASLt for A/B comparison")
-    g.add_argument("--kernel", default="auto",
-                   choices=["auto", "w4", "w4s", "t128", "t128x2", "t256x128", "mfma256d", "generic",
-                            "f32_w4", "f32_256s", "fp8_w4", "fp8_w4s"],
+    g.add_argument("--kernel", default="auto", choices=list(_GEMM_KERNELS),
                    help="native kernel selection (shipping kernels; A/B kernels need a "
                         "PDMB_EXPERIMENTS=1 build and scripts/ab_kernels.py)")
     g.add_argument("--batch", type=int, default=4,
