@@ -7,6 +7,7 @@ first bad element (row, column, got, want) if any.
 
     python scripts/race_screen.py [--reps 200] [--kernels f32_t128x2,f32_t128,t128x2]
     python scripts/race_screen.py --tails [--reps 50]   # auto's two-launch tail plans (bf16, fp8)
+    python scripts/race_screen.py --splits [--reps 50]  # round 5: auto's 3- / 5- / 6-way splits, f32_t64
 """
 import argparse
 import json
@@ -27,6 +28,13 @@ TAIL_SHAPES = [(6144, 6144, 6144), (6000, 6000, 6144), (7168, 7168, 7168), (5120
                (6144, 4096, 4096), (3000, 7000, 5056)]
 # exact fp32's tail (whole two-per-CU waves, then an f32_t128 split-K wave)
 F32_TAIL_SHAPES = [(3072, 3072, 3072), (5120, 5120, 2048), (7168, 7168, 1024)]
+# --splits (round 5): grids auto runs with a 3-way (bf16, fp32) or 5- / 6-way
+# (fp32) split-K, and on the 64x128 fp32 tile
+SPLIT_CASES = [("auto:bfloat16", (2560, 4096, 16384)), ("auto:bfloat16", (4608, 2048, 16384)),
+               ("auto:bfloat16", (2560, 512, 8192)), ("auto:bfloat16", (3584, 2560, 16384)),
+               ("auto:float32", (2560, 256, 8192)), ("auto:float32", (1536, 1536, 4096)),
+               ("auto:float32", (1024, 256, 16384)), ("auto:float32", (512, 6400, 16384)),
+               ("auto:float32", (4096, 512, 4096)), ("auto:float32", (2048, 512, 2048))]
 
 
 def main():
@@ -35,10 +43,16 @@ def main():
     ap.add_argument("--kernels", default="f32_t128x2,f32_t128,f32_256s,t128x2,t128")
     ap.add_argument("--tails", action="store_true",
                     help="screen auto's tail plans (bf16 and fp8, TAIL_SHAPES) instead")
+    ap.add_argument("--splits", action="store_true",
+                    help="screen auto's non-power-of-two split plans (SPLIT_CASES) instead")
     a = ap.parse_args()
-    cases = ([(kd, shp) for kd in ("auto:bfloat16", "auto:float8_e4m3fn") for shp in TAIL_SHAPES]
-             + [("auto:float32", shp) for shp in F32_TAIL_SHAPES]
-             if a.tails else [(kern, shp) for kern in a.kernels.split(",") for shp in SHAPES])
+    if a.splits:
+        cases = SPLIT_CASES
+    elif a.tails:
+        cases = ([(kd, shp) for kd in ("auto:bfloat16", "auto:float8_e4m3fn") for shp in TAIL_SHAPES]
+                 + [("auto:float32", shp) for shp in F32_TAIL_SHAPES])
+    else:
+        cases = [(kern, shp) for kern in a.kernels.split(",") for shp in SHAPES]
     for kern, (m, n, k) in cases:
         kern, _, dname = kern.partition(":")
         dt = getattr(torch, dname) if dname else (torch.float32 if kern.startswith("f32") else torch.bfloat16)
@@ -64,6 +78,8 @@ def main():
                 continue  # the kernel does not take this shape (bf16 K % 64)
             bad, first = 0, None
             plan = list(gemm.tail_split_for(A, B, C)) if kern == "auto" else None
+            split = {"kernel_run": gemm.kernel_for(A, B, C), "splitk": gemm.splitk_for(A, B, C)} \
+                if kern == "auto" and a.splits else {}
             for _ in range(a.reps):
                 C.fill_(float("nan"))
                 gemm.matmul(A, B, out=C, kernel=kern, splitk=S)
@@ -77,7 +93,7 @@ def main():
             torch.cuda.synchronize()
             print(json.dumps({"kernel": kern, "dtype": str(dt).replace("torch.", ""), "m": m, "n": n,
                               "k": k, "reps": a.reps, "bad_runs": bad, "first_bad": first,
-                              **({"tail_split": plan} if plan else {})}), flush=True)
+                              **({"tail_split": plan} if plan else {}), **split}), flush=True)
 
 
 if __name__ == "__main__":
