@@ -545,6 +545,10 @@ static Plan plan_uncached(const Problem& p, int kernel) {
       // one): bf16 1024^2 x 4096 (22 K-tiles per slice) ran 25.5 us vs 21.9 at
       // S = 2 — and not on the 256^2 fp32 tile (fp32 2560 x 2048 x 4096 on
       // f32_w4 129.0 vs 132.4 for f32_t128 x 4).
+      // (The T128 / 4-stage fp32 reducers now prefetch both other slots at
+      // S = 3, splitk_load_others3: +7 % on bf16 2560 x 512 x 8192, but with
+      // 22 K-tiles per slice S = 3 still lost to S = 2 on two of three bf16
+      // grids, profiles/r7z_split3_prefetch_ab_*.jsonl — the 32 stays.)
       if (S == 3 && p.splitk != 3 &&
           (no3 || (ktiles(p) + 2) / 3 < 32 || m.kernel == kF32W4))
         continue;

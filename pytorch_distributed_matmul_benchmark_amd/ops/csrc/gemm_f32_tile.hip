@@ -362,8 +362,11 @@ __global__ void __launch_bounds__(NT, NS == 2 ? 2 : 1) gemm_f32_t128(GemmArgs a)
   // MFMAs of the odd-count last K-tile (wrong results at K / 32 odd, found by
   // scripts/race_screen.py; tests/test_mfma_hazards.py now screens for it).
   const bool pf2 = NS == 4 && split && a.splitk == 2 && a.meet_prefetch;
+  const bool pf3 = NS == 4 && split && a.splitk == 3 && a.meet_prefetch;  // splitk_load_others3
   f32x4 qa[NB], qb[NB];
+  f32x4 ta[2][NB], tb[2][NB];
   if (pf2) splitk_load_other<MB, NB, NT>(sl, slice, 0, qa);
+  if (pf3) splitk_load_others3<MB, NB, NT>(sl, slice, 0, ta);
 #pragma unroll
   for (int mi = 0; mi < MB; ++mi) {
     f32x4 v[NB];
@@ -375,6 +378,9 @@ __global__ void __launch_bounds__(NT, NS == 2 ? 2 : 1) gemm_f32_t128(GemmArgs a)
       const f32x4(&q)[NB] = (mi & 1) ? qb : qa;
 #pragma unroll
       for (int j = 0; j < NB; ++j) v[j] = acc[mi][j] + q[j];
+    } else if (pf3) {
+      if (mi + 1 < MB) splitk_load_others3<MB, NB, NT>(sl, slice, mi + 1, (mi & 1) ? ta : tb);
+      splitk_sum3<NB>(slice, acc[mi], (mi & 1) ? tb : ta, v);
     } else {
       splitk_row<MB, NB, NT>(a, sl, slice, mi, acc, v);
     }

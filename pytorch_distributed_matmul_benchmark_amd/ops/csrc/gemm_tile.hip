@@ -523,9 +523,17 @@ __global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
   char* Cb = (char*)a.C + (long long)bz * a.sC * 2;
   char* ebuf = smem + 1024 + wu * 2 * epi_buf<NB>();  // past splitk_meet's ticket word
   // S == 2: the other slice's rows prefetched a row ahead (splitk.h splitk_load_other)
+  // S == 3: both other slices' rows, a row ahead (splitk_load_others3) — in
+  // T128 only: its 4 x 4 blocks leave the registers (358 VGPRs, no spills);
+  // in T256x128, T128x2 and T192 the two extra row buffers spilled.
+  constexpr bool kPf3 = C::BM == 128 && C::BN == 128 && C::NS == 4;
   const bool pf2 = split && a.splitk == 2 && a.meet_prefetch;
+  const bool pf3 = kPf3 && split && a.splitk == 3 && a.meet_prefetch;
   f32x4 qa[NB], qb[NB];
+  f32x4 ta[2][NB], tb[2][NB];
   if (pf2) splitk_load_other<MB, NB, NT>(sl, slice, 0, qa);
+  if constexpr (kPf3)
+    if (pf3) splitk_load_others3<MB, NB, NT>(sl, slice, 0, ta);
 #pragma unroll
   for (int i = 0; i < MB; ++i) {
     f32x4 v[NB];
@@ -537,6 +545,11 @@ __global__ void __launch_bounds__(NT, C::OCC) gemm_tile_nn(GemmArgs a) {
       const f32x4(&q)[NB] = (i & 1) ? qb : qa;
 #pragma unroll
       for (int j = 0; j < NB; ++j) v[j] = acc[i][j] + q[j];
+    } else if (kPf3 && pf3) {
+      if constexpr (kPf3) {
+        if (i + 1 < MB) splitk_load_others3<MB, NB, NT>(sl, slice, i + 1, (i & 1) ? ta : tb);
+        splitk_sum3<NB>(slice, acc[i], (i & 1) ? tb : ta, v);
+      }
     } else {
       splitk_row<MB, NB, NT>(a, sl, slice, i, acc, v);
     }

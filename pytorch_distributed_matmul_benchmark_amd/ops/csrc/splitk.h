@@ -133,6 +133,32 @@ __device__ __forceinline__ void splitk_load_other(const SplitSlots& sl, int slic
                                                      16 /* sc1 */));
 }
 
+// S == 3 (round 5; GemmArgs::meet_prefetch): both other slices' block row i,
+// issued a row ahead of their use, q[0] = the lower slot, q[1] = the higher.
+// The sum stays in slot order — (x0 + x1) + x2 with this slice's registers in
+// its own place — so it is bitwise equal to splitk_row (splitk_sum3).
+template <int MB, int NB, int NT>
+__device__ __forceinline__ void splitk_load_others3(const SplitSlots& sl, int slice, int i, f32x4 (&q)[2][NB]) {
+  constexpr int NBLK = MB * NB;
+  const int o0 = slice == 0 ? 1 : 0, o1 = slice == 2 ? 1 : 2;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    q[0][j] = __builtin_bit_cast(
+        f32x4, __builtin_amdgcn_raw_buffer_load_b128(sl.rs, ((o0 * NBLK + i * NB + j) * NT + sl.t) * 16, 0,
+                                                     16 /* sc1 */));
+    q[1][j] = __builtin_bit_cast(
+        f32x4, __builtin_amdgcn_raw_buffer_load_b128(sl.rs, ((o1 * NBLK + i * NB + j) * NT + sl.t) * 16, 0,
+                                                     16 /* sc1 */));
+  }
+}
+template <int NB>
+__device__ __forceinline__ void splitk_sum3(int slice, const f32x4 (&own)[NB], const f32x4 (&q)[2][NB],
+                                            f32x4 (&v)[NB]) {
+#pragma unroll
+  for (int j = 0; j < NB; ++j)  // fp32 addition commutes: (own + q0) == (q0 + own) bit for bit
+    v[j] = slice == 2 ? (q[0][j] + q[1][j]) + own[j] : (own[j] + q[0][j]) + q[1][j];
+}
+
 // ---- stream-K meet (gemm_fp8.hip gemm_fp8_sk) ------------------------------
 // The same hand-off with a per-tile contributor count: S workgroups (S <=
 // a.splitk, the slots per tile) each carry a K-range of the tile; `slot` is

@@ -1124,3 +1124,26 @@ def test_t192_is_auto_on_one_wave_grids():
     assert gemm.kernel_for(*mk(3072, 3072, 3072)) == "pdmb_t192_nn"
     assert gemm.kernel_for(*mk(2304, 2304, 4096)) == "pdmb_t192x128_nn"
     assert gemm.kernel_for(*mk(16384, 16384, 16384)) == "pdmb_w4s"
+
+
+@pytest.mark.parametrize("kernel,M,N,K,dt", [("t128", 1024, 1024, 4096, "bfloat16"), ("t128", 700, 264, 2048, "bfloat16"),
+                                            ("f32_t128", 1000, 1052, 4096, "float32"),
+                                            ("f32_t64", 700, 300, 2048, "float32")])
+def test_split3_prefetch_bitwise(kernel, M, N, K, dt, monkeypatch):
+    """Round 5: the 3-way reducer's row-ahead prefetch of both other slots
+    (splitk.h splitk_load_others3; T128 and the 4-stage fp32 tiles) sums in
+    slot order, so it is bitwise equal to the row-by-row reducer
+    (PDMB_SPLITK_PREFETCH=0) on random data, and exact on small integers."""
+    d = DT[dt]
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    A = torch.randn(M, K, device="cuda", generator=g).to(d)
+    B = torch.randn(K, N, device="cuda", generator=g).to(d)
+    C1 = gemm.matmul(A, B, kernel=kernel, splitk=3)
+    monkeypatch.setenv("PDMB_SPLITK_PREFETCH", "0")
+    C0 = gemm.matmul(A, B, kernel=kernel, splitk=3)
+    monkeypatch.delenv("PDMB_SPLITK_PREFETCH")
+    assert torch.equal(C1, C0)
+    Ai = torch.randint(-3, 4, (M, K), device="cuda", generator=g).to(d)
+    Bi = torch.randint(-3, 4, (K, N), device="cuda", generator=g).to(d)
+    C = gemm.matmul(Ai, Bi, kernel=kernel, splitk=3)
+    assert torch.equal(C.double(), (Ai.double() @ Bi.double()).to(d).double())
