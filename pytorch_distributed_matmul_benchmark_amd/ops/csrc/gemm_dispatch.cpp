@@ -371,6 +371,18 @@ static bool w4s_auto(const Problem& p) {
   return p.cus == 0 && w4s_fits(p) && tiles_of(p, kMfmaW4) >= 2LL * device_cus();
 }
 
+// f32_t128x2 split into slices on a grid of fewer than two tiles per CU
+// (plan_uncached takes it there from 3 slices per CU: PDMB_F32X2SPLIT=0 turns
+// that off, A/B, read per call).
+static constexpr double kF32X2AloneKt = 1.9;
+static bool f32x2_split_on() {
+  const char* e = std::getenv("PDMB_F32X2SPLIT");
+  return !(e && std::atoi(e) == 0);
+}
+static bool f32x2_split_grid(const Problem& p, const KernelModel& m, int S, long long T) {
+  return m.kernel == kF32T128x2 && S > 1 && T < 2LL * (p.cus > 0 ? p.cus : device_cus()) && f32x2_split_on();
+}
+
 // Model time (us) of `kernel` over T of the problem's tiles (T < 0: all of
 // them), each split S ways along K.
 static double plan_cost_tiles(const Problem& p, int kernel, int S, long long T) {
@@ -385,6 +397,19 @@ static double plan_cost_tiles(const Problem& p, int kernel, int S, long long T) 
   const double boost = m.cls == 2 ? 1.0 : 0.62 + 0.38 * busy;  // power headroom (not fp32)
   const double kt = waves > 1 && m.kt2 > 0 ? m.kt2 : m.kt;
   double t = (double)waves * (per * kt * boost + kFixedUs);
+  if (f32x2_split_grid(p, m, S, T)) {
+    // Split slices of a grid with fewer tiles than two per CU (round 5): the
+    // hardware hands each CU its next slice as one finishes, so a CU runs
+    // n = ceil(units / CUs) slices, in pairs at the co-resident rate and the
+    // odd one alone (kF32X2AloneKt; alone it measured 1.84-1.85 us per
+    // K-tile) — not whole two-per-CU waves. It still overprices the split arms
+    // the rule admits by 3-30 % (profiles/r7ad_f32_small_split_arms.jsonl: a
+    // slice's meet overlaps its co-resident slice's loop, the slab term does
+    // not know), so auto takes them only where they are clearly cheaper.
+    const long long cus = p.cus > 0 ? p.cus : device_cus();
+    const long long n = (units + cus - 1) / cus;
+    t = (double)(n / 2) * (per * kt + kFixedUs) + (double)(n % 2) * (per * kF32X2AloneKt + kFixedUs);
+  }
   if (S > 1) t += (double)T * (S - 1) * 2.0 * m.bm * m.bn * 4.0 / kSlabBw + kMeetUs;
   return t;
 }
@@ -496,6 +521,16 @@ static Plan plan(const Problem& p, int kernel) {
 }
 
 static Plan plan_uncached(const Problem& p, int kernel) {
+  // The launch re-plans the split of the kernel auto resolved to with that
+  // kernel fixed (tiled_launch). Auto takes f32_t128x2 on a grid of fewer than
+  // two tiles per CU only split >= 3 slices per CU (below), a rule the fixed
+  // plan does not apply (an explicit request runs it on any grid): there the
+  // fixed plan is auto's own.
+  if (kernel == kF32T128x2 && p.splitk == 0 && p.dtype == kF32 && f32x2_split_on() &&
+      tiles_of(p, kF32T128x2) < 2LL * (p.cus > 0 ? p.cus : device_cus())) {
+    const Plan a = plan(p, kAuto);
+    if (a.kernel == kF32T128x2) return a;
+  }
   Plan best{-1, 1};
   double bc = 1e300;
   bool any = false;
@@ -530,8 +565,16 @@ static Plan plan_uncached(const Problem& p, int kernel) {
       // vs 68.2 TF, 512 x 6400 x 16384 136.4 vs 115.8, all six grids tried
       // ahead; on bf16 two of six lost (2560 x 256 x 16384 515 vs 543;
       // profiles/r7u_split56_ab_*.jsonl). PDMB_SPLIT56=0 leaves them out (A/B).
-      if ((S == 5 || S == 6) && p.splitk != S) {
-        const char* e56 = std::getenv("PDMB_SPLIT56");
+      // 8-way (round 5), the same rule, on the exact-fp32 64x128 tile only:
+      // 1024 x 256 x 16384 113.5 vs 95.2 TF at 6 ways, 256 x 512 x 16384 58.8
+      // vs 48.2, 1024 x 256 x 8192 91.4 vs 81.2; on the 128x128 tiles it lost
+      // (512 x 1024 x 16384 f32_t128 x 8 123.3 vs 131.9 for f32_t64 x 4, 512 x
+      // 9216 x 16384 f32_t128x2 x 8 137.6 vs 142.3 at 6 ways;
+      // profiles/r7ae_f32_split8_x2split_ab.jsonl, confirmed with settled arms
+      // on 5 more f32_t64 grids: +1.5 to +20 %, r7af_f32_planner_confirm_settled.jsonl).
+      // PDMB_SPLIT8=0 leaves it out.
+      if ((S == 5 || S == 6 || (S == 8 && m.kernel == kF32T64)) && p.splitk != S) {
+        const char* e56 = std::getenv(S == 8 ? "PDMB_SPLIT8" : "PDMB_SPLIT56");
         if ((e56 && std::atoi(e56) == 0) || m.cls != 2 || (ktiles(p) + S - 1) / S < 32 || m.kernel == kF32W4)
           continue;
       } else if (S > 4 && p.splitk != S) {
@@ -560,8 +603,18 @@ static Plan plan_uncached(const Problem& p, int kernel) {
       // 4-stage tile on 4096 x 1024 x 4096 and 2048^3 (142.3 / 138.3 vs 146.5 /
       // 143.8 TF, profiles/r3_f32_t128x2_ab.jsonl). An explicit request runs it
       // on any grid.
+      // Round 5: split into >= 3 slices per CU it does run there — a CU's
+      // co-resident slices hide each other's prologue, epilogue and meet:
+      // 2560 x 2048 x 4096 303.6 us as f32_t128x2 x 4 vs 324.0 for f32_t128 x 4
+      // (profiles/r7ad_f32_small_split_arms.jsonl); auto vs PDMB_F32X2SPLIT=0 on
+      // 20 grids it changes, settled arms, two sessions: -0.5 to +19 %, median
+      // +3.3 % (r7af_f32_planner_confirm_settled.jsonl; priced per CU, see
+      // f32x2_split_grid; the launch's re-plan with the kernel fixed returns
+      // this plan, see the top). PDMB_F32X2SPLIT=0 leaves it out (A/B).
       if (kernel == kAuto && m.cls == 2 && m.occ > 1 &&
-          tiles_of(p, m.kernel) < (long long)(p.cus > 0 ? p.cus : device_cus()) * m.occ)
+          tiles_of(p, m.kernel) < (long long)(p.cus > 0 ? p.cus : device_cus()) * m.occ &&
+          !(f32x2_split_on() && S > 1 &&
+            tiles_of(p, m.kernel) * S >= 3LL * (p.cus > 0 ? p.cus : device_cus())))
         continue;
       // f32_t64 only within one wave: past it, it measured 3-4 % behind
       // f32_t128 / f32_t128x2 (2048^3 138.0 vs 143.4, 8192 x 512 x 8192 143.6

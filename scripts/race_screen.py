@@ -34,7 +34,11 @@ SPLIT_CASES = [("auto:bfloat16", (2560, 4096, 16384)), ("auto:bfloat16", (4608, 
                ("auto:bfloat16", (2560, 512, 8192)), ("auto:bfloat16", (3584, 2560, 16384)),
                ("auto:float32", (2560, 256, 8192)), ("auto:float32", (1536, 1536, 4096)),
                ("auto:float32", (1024, 256, 16384)), ("auto:float32", (512, 6400, 16384)),
-               ("auto:float32", (4096, 512, 4096)), ("auto:float32", (2048, 512, 2048))]
+               ("auto:float32", (4096, 512, 4096)), ("auto:float32", (2048, 512, 2048)),
+               # round 5: split f32_t128x2 on < 2 tiles per CU, 8-way f32_t64
+               ("auto:float32", (2560, 2048, 4096)), ("auto:float32", (3072, 1536, 2048)),
+               ("auto:float32", (6144, 768, 16384)), ("auto:float32", (1000, 3000, 4096)),
+               ("auto:float32", (768, 256, 16384)), ("auto:float32", (256, 768, 8192))]
 
 
 def main():

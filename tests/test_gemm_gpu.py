@@ -258,6 +258,33 @@ def test_f32_splitk_exact(kernel, M, N, K, splitk, split):
     assert torch.equal(gemm.matmul(A, B, kernel=kernel, splitk=splitk), C)
 
 
+@pytest.mark.parametrize("M,N,K,kernel,S", [(2560, 2048, 4096, "f32_t128x2", 4), (1024, 256, 16384, "f32_t64", 8),
+                                             (512, 12288, 2048, "f32_t128x2", 2), (1000, 3000, 4096, None, None)])
+def test_f32_auto_x2_split_and_split8_exact(M, N, K, kernel, S, monkeypatch):
+    """Round 5 planner: auto runs f32_t128x2 split >= 3 slices per CU on grids
+    of < 2 tiles per CU, and 8-way fp32 splits (test_planner_cpu.py). The plan
+    auto prices is the one that launches; exact on small integers (edges
+    masked), bitwise repeatable on random data."""
+    monkeypatch.delenv("PDMB_F32X2SPLIT", raising=False)
+    monkeypatch.delenv("PDMB_SPLIT8", raising=False)
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    A = torch.randint(-3, 4, (M, K), device="cuda", generator=g).float()
+    B = torch.randint(-3, 4, (K, N), device="cuda", generator=g).float()
+    if kernel:
+        assert gemm.kernel_for(A, B) == f"pdmb_{kernel}_nn"
+        assert gemm.splitk_for(A, B) == S
+    big = torch.full((M + 8, N + 12), float("nan"), device="cuda")
+    gemm.matmul(A, B, out=big[:M, :N])
+    assert torch.equal(big[:M, :N].double(), _ref(A, B))
+    assert torch.isnan(big[:, N:]).all() and torch.isnan(big[M:]).all()
+    A = torch.randn(M, K, device="cuda", generator=g)
+    B = torch.randn(K, N, device="cuda", generator=g)
+    C = gemm.matmul(A, B)
+    assert _relerr(C, _ref(A, B)) < TOL[torch.float32]
+    for _ in range(5):
+        assert torch.equal(gemm.matmul(A, B), C)
+
+
 F32_T128_ARMS = ["f32_t128", "f32_t128x2", "x_f32_t128_b32", "f32_t64"]
 
 

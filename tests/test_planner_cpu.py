@@ -221,8 +221,44 @@ def test_split56_fp32_only(C, monkeypatch):
     """Round 5: 5- / 6-way splits for exact fp32 only (measured ahead on six
     fp32 grids, mixed on bf16; profiles/r7u_split56_ab_*.jsonl)."""
     monkeypatch.delenv("PDMB_SPLIT56", raising=False)
+    monkeypatch.setenv("PDMB_SPLIT8", "0")  # (8 ways takes the first grid since, test_split8_*)
     assert plan(C, F32, 1024, 256, 16384)[1] in (5, 6)
     assert plan(C, F32, 512, 6400, 16384)[1] in (5, 6)
     assert plan(C, BF16, 2560, 256, 16384)[1] not in (5, 6)
     monkeypatch.setenv("PDMB_SPLIT56", "0")
     assert plan(C, F32, 1024, 256, 16384)[1] not in (5, 6)
+
+
+def test_split8_fp32_only(C, monkeypatch):
+    """Round 5: the 8-way split under the 5- / 6-way rule (exact fp32 only,
+    >= 32 K-tiles per slice): 1024 x 256 x 16384 on f32_t64 x 8 ran 81.5 us vs
+    96.9 at 6 ways (profiles/r7ad_f32_small_split_arms.jsonl); PDMB_SPLIT8=0
+    leaves it out; bf16 / fp8 auto never splits 8 ways."""
+    monkeypatch.delenv("PDMB_SPLIT8", raising=False)
+    assert plan(C, F32, 1024, 256, 16384)[:2] == ("pdmb_f32_t64_nn", 8)
+    assert plan(C, F32, 1024, 256, 4096)[1] != 8  # 16 K-tiles per slice
+    for dt in (BF16, FP8):
+        for shape in ((1024, 256, 16384), (256, 256, 16384), (2048, 1024, 16384)):
+            assert plan(C, dt, *shape)[1] != 8, (dt, shape)
+    monkeypatch.setenv("PDMB_SPLIT8", "0")
+    assert plan(C, F32, 1024, 256, 16384)[1] != 8
+
+
+def test_f32_x2_split_on_small_grids(C, monkeypatch):
+    """Round 5: f32_t128x2 split into >= 3 slices per CU on a grid of fewer than
+    two 128x128 tiles per CU (2560 x 2048 x 4096: 320 tiles x 4 ran 303.6 us vs
+    324.0 for f32_t128 x 4, profiles/r7ad_f32_small_split_arms.jsonl), never
+    2 or fewer slices per CU there; an explicit f32_t128x2 request gets auto's
+    split (the launch re-plans with the kernel fixed); PDMB_F32X2SPLIT=0 turns
+    it off."""
+    monkeypatch.delenv("PDMB_F32X2SPLIT", raising=False)
+    assert plan(C, F32, 2560, 2048, 4096)[:2] == ("pdmb_f32_t128x2_nn", 4)
+    assert plan(C, F32, 2560, 2048, 4096, kernel=53)[:2] == ("pdmb_f32_t128x2_nn", 4)
+    for shape in ((4096, 1024, 4096), (2048, 2048, 2048), (1536, 1536, 4096), (768, 9216, 4096),
+                  (512, 12288, 4096), (1536, 5120, 4096), (2560, 512, 8192)):
+        k, S, _, _ = plan(C, F32, *shape)
+        tiles = -(-shape[0] // 128) * -(-shape[1] // 128)
+        if k == "pdmb_f32_t128x2_nn" and tiles < 512:
+            assert S > 1 and tiles * S >= 768, (shape, S)
+    monkeypatch.setenv("PDMB_F32X2SPLIT", "0")
+    assert plan(C, F32, 2560, 2048, 4096)[0] == "pdmb_f32_t128_nn"
