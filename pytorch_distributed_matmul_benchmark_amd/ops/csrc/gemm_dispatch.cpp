@@ -383,6 +383,12 @@ static bool f32x2_split_grid(const Problem& p, const KernelModel& m, int S, long
   return m.kernel == kF32T128x2 && S > 1 && T < 2LL * (p.cus > 0 ? p.cus : device_cus()) && f32x2_split_on();
 }
 
+static constexpr double kSlotLatUs = 4.5;
+static bool split_slot_lat_on() {
+  const char* e = std::getenv("PDMB_SPLIT_SLOT_LAT");
+  return !(e && std::atoi(e) == 0);
+}
+
 // Model time (us) of `kernel` over T of the problem's tiles (T < 0: all of
 // them), each split S ways along K.
 static double plan_cost_tiles(const Problem& p, int kernel, int S, long long T) {
@@ -411,6 +417,16 @@ static double plan_cost_tiles(const Problem& p, int kernel, int S, long long T) 
     t = (double)(n / 2) * (per * kt + kFixedUs) + (double)(n % 2) * (per * kF32X2AloneKt + kFixedUs);
   }
   if (S > 1) t += (double)T * (S - 1) * 2.0 * m.bm * m.bn * 4.0 / kSlabBw + kMeetUs;
+  // bf16 / fp16 grids of <= 64 tiles split >= 4 ways into slices of <= 32
+  // K-tiles (round 5): the slab term, sized for the chip's bandwidth, misses
+  // the reducer's latency there — every slot past the second costs ~4.5 us
+  // (forced arms, profiles/r7ai_bf16_small_arms.jsonl: T128 x 4 ran 6.8-9.5 us
+  // over the model on 1024^2 x 8192, 512 x 2048 x 8192, 768^2 x 8192, where
+  // x 3 ran 14-17 % faster). Auto vs the term off on 13 grids of 4-64 tiles
+  // it changes, settled arms, two sessions: +1 to +20 %, median +4.5 %, bf16 and
+  // fp16 alike (profiles/r7aj_*_split_slot_latency_ab.jsonl).
+  // PDMB_SPLIT_SLOT_LAT=0 leaves it out (A/B).
+  if (S >= 4 && m.cls == 0 && T <= 64 && per <= 32 && split_slot_lat_on()) t += (S - 2) * kSlotLatUs;
   return t;
 }
 

@@ -262,3 +262,19 @@ def test_f32_x2_split_on_small_grids(C, monkeypatch):
             assert S > 1 and tiles * S >= 768, (shape, S)
     monkeypatch.setenv("PDMB_F32X2SPLIT", "0")
     assert plan(C, F32, 2560, 2048, 4096)[0] == "pdmb_f32_t128_nn"
+
+
+def test_split_slot_latency_small_bf16_grids(C, monkeypatch):
+    """Round 5: bf16 / fp16 grids of <= 64 tiles split >= 4 ways into short
+    slices pay a reducer latency the slab term misses; with it, auto moves
+    1024^2 x 8192 / 512 x 2048 x 8192 / 768^2 x 8192 from T128 x 4 to x 3
+    (+14-17 %, profiles/r7aj_*_split_slot_latency_ab.jsonl); off with
+    PDMB_SPLIT_SLOT_LAT=0; fp32 and fp8 plans unchanged."""
+    monkeypatch.delenv("PDMB_SPLIT_SLOT_LAT", raising=False)
+    for dt in (BF16, F16):
+        for shape in ((1024, 1024, 8192), (512, 2048, 8192), (768, 768, 8192)):
+            assert plan(C, dt, *shape)[:2] == ("pdmb_t128_nn", 3), (dt, shape)
+    other = {(dt, s): plan(C, dt, *s)[:2] for dt in (F32, FP8) for s in ((1024, 1024, 8192), (512, 512, 8192))}
+    monkeypatch.setenv("PDMB_SPLIT_SLOT_LAT", "0")
+    assert plan(C, BF16, 1024, 1024, 8192)[:2] == ("pdmb_t128_nn", 4)
+    assert other == {(dt, s): plan(C, dt, *s)[:2] for (dt, s) in other}
