@@ -383,6 +383,10 @@ static bool f32x2_split_grid(const Problem& p, const KernelModel& m, int S, long
   return m.kernel == kF32T128x2 && S > 1 && T < 2LL * (p.cus > 0 ? p.cus : device_cus()) && f32x2_split_on();
 }
 
+static bool split3_small_on() {
+  const char* e = std::getenv("PDMB_SPLIT3_SMALL");
+  return !(e && std::atoi(e) == 0);
+}
 static constexpr double kSlotLatUs = 4.5;
 static bool split_slot_lat_on() {
   const char* e = std::getenv("PDMB_SPLIT_SLOT_LAT");
@@ -608,8 +612,19 @@ static Plan plan_uncached(const Problem& p, int kernel) {
       // S = 3, splitk_load_others3: +7 % on bf16 2560 x 512 x 8192, but with
       // 22 K-tiles per slice S = 3 still lost to S = 2 on two of three bf16
       // grids, profiles/r7z_split3_prefetch_ab_*.jsonl — the 32 stays.)
+      // ... except on bf16 / fp16 grids of <= 36 128^2 tiles, where T128 x 3
+      // (whose reducer prefetches both other slots) measured ahead of x 2 with
+      // 11-22 K-tiles per slice: 768^2 x 4096 249.4 vs 234.6 TF, 512 x 1024 x
+      // 4096 231.4 vs 215.2, 384 x 768 x 4096 132.6 vs 122.1
+      // (profiles/r7aj_*_split_slot_latency_ab.jsonl forced arms; at 64 tiles
+      // it was mixed, r7ai). Auto vs the rule off on 16 grids it changes, bf16
+      // and fp16, settled arms, two sessions: all 32 gain, +0.9 to +13.7 %,
+      // median +7.5 % (r7ak_*_split3_small_ab.jsonl). PDMB_SPLIT3_SMALL=0
+      // leaves it out (A/B).
+      const bool s3small = m.kernel == kT128 && tiles_of(p, m.kernel) <= 36 && (ktiles(p) + 2) / 3 >= 8 &&
+                           split3_small_on();
       if (S == 3 && p.splitk != 3 &&
-          (no3 || (ktiles(p) + 2) / 3 < 32 || m.kernel == kF32W4))
+          (no3 || ((ktiles(p) + 2) / 3 < 32 && !s3small) || m.kernel == kF32W4))
         continue;
       if (p.splitk > 0 && S != p.splitk) continue;
       if (!split_ok(p, m.kernel, S)) continue;

@@ -278,3 +278,17 @@ def test_split_slot_latency_small_bf16_grids(C, monkeypatch):
     monkeypatch.setenv("PDMB_SPLIT_SLOT_LAT", "0")
     assert plan(C, BF16, 1024, 1024, 8192)[:2] == ("pdmb_t128_nn", 4)
     assert other == {(dt, s): plan(C, dt, *s)[:2] for (dt, s) in other}
+
+
+def test_split3_small_bf16_grids(C, monkeypatch):
+    """Round 5: T128 x 3 on bf16 / fp16 grids of <= 36 tiles below the 32
+    K-tiles-per-slice minimum (its reducer prefetches both other slots;
+    profiles/r7aj_*, r7ak_*); PDMB_SPLIT3_SMALL=0 restores the minimum; not on
+    grids of more tiles, nor on fp8 (its own 32 K-tile minimum)."""
+    monkeypatch.delenv("PDMB_SPLIT3_SMALL", raising=False)
+    for dt in (BF16, F16):
+        assert plan(C, dt, 768, 768, 4096)[:2] == ("pdmb_t128_nn", 3)
+    assert plan(C, BF16, 1024, 1024, 4096)[1] != 3  # 64 tiles: mixed, left out
+    assert plan(C, FP8, 768, 768, 4096)[1] != 3  # 11 fp8 K-tiles per slice
+    monkeypatch.setenv("PDMB_SPLIT3_SMALL", "0")
+    assert plan(C, BF16, 768, 768, 4096)[1] != 3
