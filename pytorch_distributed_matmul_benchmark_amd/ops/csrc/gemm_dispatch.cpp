@@ -421,16 +421,18 @@ static double plan_cost_tiles(const Problem& p, int kernel, int S, long long T) 
     t = (double)(n / 2) * (per * kt + kFixedUs) + (double)(n % 2) * (per * kF32X2AloneKt + kFixedUs);
   }
   if (S > 1) t += (double)T * (S - 1) * 2.0 * m.bm * m.bn * 4.0 / kSlabBw + kMeetUs;
-  // bf16 / fp16 grids of <= 64 tiles split >= 4 ways into slices of <= 32
-  // K-tiles (round 5): the slab term, sized for the chip's bandwidth, misses
+  // bf16 / fp16 / fp8 grids of <= 64 tiles split >= 4 ways into slices of <=
+  // 32 K-tiles (round 5): the slab term, sized for the chip's bandwidth, misses
   // the reducer's latency there — every slot past the second costs ~4.5 us
   // (forced arms, profiles/r7ai_bf16_small_arms.jsonl: T128 x 4 ran 6.8-9.5 us
   // over the model on 1024^2 x 8192, 512 x 2048 x 8192, 768^2 x 8192, where
   // x 3 ran 14-17 % faster). Auto vs the term off on 13 grids of 4-64 tiles
   // it changes, settled arms, two sessions: +1 to +20 %, median +4.5 %, bf16 and
-  // fp16 alike (profiles/r7aj_*_split_slot_latency_ab.jsonl).
+  // fp16 alike (profiles/r7aj_*_split_slot_latency_ab.jsonl); fp8, 16 grids it
+  // moves off T128 x 4, with the x 3 rule below: all gain, +7 to +40 %
+  // (r7am_fp8_small_rules_ab.jsonl).
   // PDMB_SPLIT_SLOT_LAT=0 leaves it out (A/B).
-  if (S >= 4 && m.cls == 0 && T <= 64 && per <= 32 && split_slot_lat_on()) t += (S - 2) * kSlotLatUs;
+  if (S >= 4 && m.cls != 2 && T <= 64 && per <= 32 && split_slot_lat_on()) t += (S - 2) * kSlotLatUs;
   return t;
 }
 
@@ -612,7 +614,7 @@ static Plan plan_uncached(const Problem& p, int kernel) {
       // S = 3, splitk_load_others3: +7 % on bf16 2560 x 512 x 8192, but with
       // 22 K-tiles per slice S = 3 still lost to S = 2 on two of three bf16
       // grids, profiles/r7z_split3_prefetch_ab_*.jsonl — the 32 stays.)
-      // ... except on bf16 / fp16 grids of <= 36 128^2 tiles, where T128 x 3
+      // ... except on grids of <= 36 128^2 tiles, where T128 x 3
       // (whose reducer prefetches both other slots) measured ahead of x 2 with
       // 11-22 K-tiles per slice: 768^2 x 4096 249.4 vs 234.6 TF, 512 x 1024 x
       // 4096 231.4 vs 215.2, 384 x 768 x 4096 132.6 vs 122.1
@@ -621,8 +623,11 @@ static Plan plan_uncached(const Problem& p, int kernel) {
       // and fp16, settled arms, two sessions: all 32 gain, +0.9 to +13.7 %,
       // median +7.5 % (r7ak_*_split3_small_ab.jsonl). PDMB_SPLIT3_SMALL=0
       // leaves it out (A/B).
-      const bool s3small = m.kernel == kT128 && tiles_of(p, m.kernel) <= 36 && (ktiles(p) + 2) / 3 >= 8 &&
-                           split3_small_on();
+      // fp8 T128 (round 5, the same A/B, r7am_fp8_small_rules_ab.jsonl) from 16
+      // K-tiles per slice: with 11 it lost (1024 x 256 x 4096 159.4 vs 172.3
+      // unsplit); with 22, +4 to +8 % over x 2 on five grids.
+      const bool s3small = (m.kernel == kT128 || m.kernel == kFp8T128) && tiles_of(p, m.kernel) <= 36 &&
+                           (ktiles(p) + 2) / 3 >= (m.kernel == kFp8T128 ? 16 : 8) && split3_small_on();
       if (S == 3 && p.splitk != 3 &&
           (no3 || ((ktiles(p) + 2) / 3 < 32 && !s3small) || m.kernel == kF32W4))
         continue;

@@ -38,7 +38,11 @@ SPLIT_CASES = [("auto:bfloat16", (2560, 4096, 16384)), ("auto:bfloat16", (4608, 
                # round 5: split f32_t128x2 on < 2 tiles per CU, 8-way f32_t64
                ("auto:float32", (2560, 2048, 4096)), ("auto:float32", (3072, 1536, 2048)),
                ("auto:float32", (6144, 768, 16384)), ("auto:float32", (1000, 3000, 4096)),
-               ("auto:float32", (768, 256, 16384)), ("auto:float32", (256, 768, 8192))]
+               ("auto:float32", (768, 256, 16384)), ("auto:float32", (256, 768, 8192)),
+               # round 5: small-grid split rules (T128 x 3 below 32 K-tiles per slice)
+               ("auto:bfloat16", (768, 768, 4096)), ("auto:float16", (256, 768, 2048)),
+               ("auto:bfloat16", (1024, 1024, 8192)), ("auto:float8_e4m3fn", (768, 768, 8192)),
+               ("auto:float8_e4m3fn", (1000, 260, 8192))]
 
 
 def main():

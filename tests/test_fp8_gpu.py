@@ -208,6 +208,27 @@ def test_fp8_splitk_exact(M, N, K, splitk):
         assert torch.equal(C, (0.5 * (Af.double() @ Bf.double())).to(torch.bfloat16))
 
 
+@pytest.mark.parametrize("M,N,K,S", [(768, 768, 8192, 3), (512, 512, 8192, 3), (1024, 768, 8192, 2),
+                                     (1000, 260, 8192, None)])
+def test_fp8_small_grid_split_plans_exact(M, N, K, S, monkeypatch):
+    """Round 5 small-grid split rules (reducer-latency term, T128 x 3 below 32
+    K-tiles per slice) on fp8 T128: the plan auto prices is the one launched;
+    exact on small integers with masked edges; bitwise repeatable."""
+    monkeypatch.delenv("PDMB_SPLIT_SLOT_LAT", raising=False)
+    monkeypatch.delenv("PDMB_SPLIT3_SMALL", raising=False)
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    Af, Bf = _ints((M, K), g, -2, 3), _ints((K, N), g, -2, 3)
+    A8, B8 = Af.to(FP8), _colmajor(Bf.to(FP8))
+    if S is not None:
+        assert gemm.kernel_for(A8, B8) == "pdmb_fp8_t128_nt"
+        assert gemm.splitk_for(A8, B8) == S
+    ref = (0.5 * (Af.double() @ Bf.double())).to(torch.bfloat16)
+    C = gemm.matmul(A8, B8, alpha=0.5)
+    assert torch.equal(C, ref)
+    for _ in range(5):
+        assert torch.equal(gemm.matmul(A8, B8, alpha=0.5), C)
+
+
 # ---- fp8 tile family (gemm_tile.hip, DT = kFP8): under-filled fp8 grids ----
 @pytest.mark.parametrize("kernel", ["fp8_t128", "fp8_t256x128", "fp8_t192", "fp8_t192x128"])
 @pytest.mark.parametrize("M,N,K,splitk", [(256, 128, 128, 1), (512, 384, 256, 1), (2048, 2048, 2048, 1),

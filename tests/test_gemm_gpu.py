@@ -285,6 +285,34 @@ def test_f32_auto_x2_split_and_split8_exact(M, N, K, kernel, S, monkeypatch):
         assert torch.equal(gemm.matmul(A, B), C)
 
 
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+@pytest.mark.parametrize("M,N,K,S", [(768, 768, 4096, 3), (1024, 1024, 8192, 3), (256, 768, 2048, 3),
+                                     (700, 304, 4096, 3)])
+def test_small_grid_split_plans_exact(dtype, M, N, K, S, monkeypatch):
+    """Round 5 small-grid split rules (reducer-latency term, T128 x 3 below 32
+    K-tiles per slice; test_planner_cpu.py): the plan auto prices is the one
+    launched; exact on small integers with masked edges; bitwise repeatable."""
+    monkeypatch.delenv("PDMB_SPLIT_SLOT_LAT", raising=False)
+    monkeypatch.delenv("PDMB_SPLIT3_SMALL", raising=False)
+    dt = getattr(torch, dtype)
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    A = torch.randint(-3, 4, (M, K), device="cuda", generator=g).to(dt)
+    B = torch.randint(-3, 4, (K, N), device="cuda", generator=g).to(dt)
+    if S is not None:
+        assert gemm.kernel_for(A, B) == "pdmb_t128_nn"
+        assert gemm.splitk_for(A, B) == S
+    big = torch.full((M + 8, N + 12), float("nan"), device="cuda", dtype=dt)
+    gemm.matmul(A, B, out=big[:M, :N])
+    assert torch.equal(big[:M, :N], (A.double() @ B.double()).to(dt))
+    assert torch.isnan(big[:, N:]).all() and torch.isnan(big[M:]).all()
+    A = torch.randn(M, K, device="cuda", generator=g).to(dt)
+    B = torch.randn(K, N, device="cuda", generator=g).to(dt)
+    C = gemm.matmul(A, B)
+    assert _relerr(C, _ref(A, B)) < TOL[dt]
+    for _ in range(5):
+        assert torch.equal(gemm.matmul(A, B), C)
+
+
 F32_T128_ARMS = ["f32_t128", "f32_t128x2", "x_f32_t128_b32", "f32_t64"]
 
 
