@@ -235,6 +235,7 @@ static int resolve_core(const Problem& p, int kernel) {
     case kF32T128: return p.dtype == kF32 && supports(p, kF32T128) ? kF32T128 : -1;
     case kF32T128x2: return p.dtype == kF32 && supports(p, kF32T128) ? kF32T128x2 : -1;
     case kF32T64: return p.dtype == kF32 && supports(p, kF32T64) ? kF32T64 : -1;
+    case kF32T64x2: return p.dtype == kF32 && supports(p, kF32T64) ? kF32T64x2 : -1;
     default:
       return is_experiment(kernel) ? experiment_resolve(p, kernel, fast, w4, t128, f32fast) : -1;
   }
@@ -321,6 +322,12 @@ static constexpr KernelModel kModels[] = {
     // (profiles/r7p_f32_t64_ab.jsonl: 140.6 vs 139.0 TF for f32_t128 x 2 at
     // 4096 x 512 x 4096, 136.2 vs 127.7 at 2048 x 1024 x 2048).
     {kF32T64, 64, 128, 1, 0.92, 2, 8},
+    // round 5: f32_t64 on 2 stages, two workgroups per CU: 1.80 us per K-tile
+    // of a co-resident pair, 0.95 alone (split slices priced per CU on any
+    // grid, f32x2_split_grid); its split arms fit within 0.9-1.3x
+    // (profiles/r7ao_f32_t64x2_arms.jsonl). Auto vs PDMB_F32T64X2=0 on 21 small
+    // grids it changes: median +6.1 %, -0.5 to +37 % (r7ap_f32_t64x2_auto_ab.jsonl).
+    {kF32T64x2, 64, 128, 2, 1.80, 2, 8},
 };
 static int dt_class(const Problem& p) { return p.dtype == kFP8 ? 1 : p.dtype == kF32 ? 2 : 0; }
 static constexpr double kFixedUs = 4.0;   // launch + prologue + epilogue
@@ -380,6 +387,7 @@ static bool f32x2_split_on() {
   return !(e && std::atoi(e) == 0);
 }
 static bool f32x2_split_grid(const Problem& p, const KernelModel& m, int S, long long T) {
+  if (m.kernel == kF32T64x2) return S > 1;  // any grid (its plans date from this model)
   return m.kernel == kF32T128x2 && S > 1 && T < 2LL * (p.cus > 0 ? p.cus : device_cus()) && f32x2_split_on();
 }
 
@@ -418,7 +426,8 @@ static double plan_cost_tiles(const Problem& p, int kernel, int S, long long T) 
     // not know), so auto takes them only where they are clearly cheaper.
     const long long cus = p.cus > 0 ? p.cus : device_cus();
     const long long n = (units + cus - 1) / cus;
-    t = (double)(n / 2) * (per * kt + kFixedUs) + (double)(n % 2) * (per * kF32X2AloneKt + kFixedUs);
+    const double alone = m.kernel == kF32T64x2 ? kF32X2AloneKt / 2.0 : kF32X2AloneKt;
+    t = (double)(n / 2) * (per * kt + kFixedUs) + (double)(n % 2) * (per * alone + kFixedUs);
   }
   if (S > 1) t += (double)T * (S - 1) * 2.0 * m.bm * m.bn * 4.0 / kSlabBw + kMeetUs;
   // bf16 / fp16 / fp8 grids of <= 64 tiles split >= 4 ways into slices of <=
@@ -454,7 +463,7 @@ static bool supports(const Problem& p, int kernel) {
   if (kernel == kFp8W4) return gemm_fp8_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   if (kernel == kF32_256s || kernel == kF32W4)
     return p.dtype == kF32 && gemm_f32_256_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
-  if (kernel == kF32T128 || kernel == kF32T128x2 || kernel == kF32T64)
+  if (kernel == kF32T128 || kernel == kF32T128x2 || kernel == kF32T64 || kernel == kF32T64x2)
     return p.dtype == kF32 && gemm_f32_tile_supported(a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
   return gemm_tile_supported(p.dtype, model_of(kernel).bm, a, (size_t)p.A, (size_t)p.B, (size_t)p.C);
 }
@@ -548,10 +557,10 @@ static Plan plan_uncached(const Problem& p, int kernel) {
   // two tiles per CU only split >= 3 slices per CU (below), a rule the fixed
   // plan does not apply (an explicit request runs it on any grid): there the
   // fixed plan is auto's own.
-  if (kernel == kF32T128x2 && p.splitk == 0 && p.dtype == kF32 && f32x2_split_on() &&
-      tiles_of(p, kF32T128x2) < 2LL * (p.cus > 0 ? p.cus : device_cus())) {
+  if ((kernel == kF32T128x2 || kernel == kF32T64x2) && p.splitk == 0 && p.dtype == kF32 && f32x2_split_on() &&
+      tiles_of(p, kernel) < 2LL * (p.cus > 0 ? p.cus : device_cus())) {
     const Plan a = plan(p, kAuto);
-    if (a.kernel == kF32T128x2) return a;
+    if (a.kernel == kernel) return a;
   }
   Plan best{-1, 1};
   double bc = 1e300;
@@ -571,11 +580,19 @@ static Plan plan_uncached(const Problem& p, int kernel) {
   // PDMB_F32T64=0 (read per call; A/B): auto leaves the 64x128 fp32 tile out
   const char* t64env = std::getenv("PDMB_F32T64");
   const bool no64 = kernel == kAuto && t64env && std::atoi(t64env) == 0;
+  // PDMB_F32T64X2=0 (read per call; A/B): auto leaves f32_t64x2 out
+  const char* t64x2env = std::getenv("PDMB_F32T64X2");
+  const bool t64x2_on = !(t64x2env && std::atoi(t64x2env) == 0);
   for (int pass = 0; pass < 2; ++pass)
   for (const KernelModel& m : kModels) {
     if (kernel != kAuto && kernel != m.kernel) continue;
     if (no192 && is_t192(m.kernel)) continue;
     if (no64 && m.kernel == kF32T64) continue;
+    // f32_t64x2 in auto only where the 128x128 tiles number fewer than two per
+    // CU (the full grids keep their measured f32_t128x2 / tail plans)
+    if (kernel == kAuto && m.kernel == kF32T64x2 &&
+        (!t64x2_on || tiles_of(p, kF32T128x2) >= 2LL * (p.cus > 0 ? p.cus : device_cus())))
+      continue;
     if (m.cls != dt_class(p) || !supports(p, m.kernel)) continue;
     any = true;
     const int* Ss = pass ? kS1 : kS0;
@@ -682,7 +699,7 @@ static Plan plan_uncached(const Problem& p, int kernel) {
 static bool is_tiled(int k) {
   return k == kMfmaW4 || k == kT128 || k == kT128x2 || k == kT256x128 || k == kFp8T128 || k == kFp8T256x128 ||
          k == kF32W4 || k == kF32T128 || k == kF32T128x2 || k == kT192 || k == kT192x128 || k == kFp8T192 ||
-         k == kFp8T192x128 || k == kF32T64;
+         k == kFp8T192x128 || k == kF32T64 || k == kF32T64x2;
 }
 
 int choose_splitk(const Problem& p, int kernel) {
@@ -1096,7 +1113,7 @@ static hipError_t tiled_launch(const Problem& p, int k, GemmArgs a, void* part, 
     }
   }
   if (k == kF32W4) return gemm_f32_w4_launch(a, stream, sub);  // sub: the variant (experiments)
-  if (k == kF32T128 || k == kF32T128x2 || k == kF32T64) return gemm_f32_tile_launch(a, stream, sub);  // sub: the variant
+  if (k == kF32T128 || k == kF32T128x2 || k == kF32T64 || k == kF32T64x2) return gemm_f32_tile_launch(a, stream, sub);  // sub: the variant
   return k == kMfmaW4 ? gemm_w4_launch(p.dtype, a, stream, sub) : gemm_tile_launch(k, p.dtype, a, stream);
 }
 
@@ -1601,6 +1618,7 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kF32T128: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream);
     case kF32T128x2: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream, 2);
     case kF32T64: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream, 3);
+    case kF32T64x2: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream, 4);
     default:
       if (is_experiment(k)) return experiment_launch(p, k, a, stream);
       return gemm_generic_launch(p.dtype, a, generic_vec_ok(p), stream);
@@ -1768,6 +1786,7 @@ const char* kernel_name(int kernel) {
     case kF32W4: return "pdmb_f32_w4_nn";
     case kF32T128: return "pdmb_f32_t128_nn";
     case kF32T64: return "pdmb_f32_t64_nn";
+    case kF32T64x2: return "pdmb_f32_t64x2_nn";
     case kF32T128x2: return "pdmb_f32_t128x2_nn";
     default: return is_experiment(kernel) ? experiment_name(kernel) : "auto";
   }

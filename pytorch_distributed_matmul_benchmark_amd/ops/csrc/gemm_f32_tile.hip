@@ -424,7 +424,7 @@ bool gemm_f32_tile_supported(const GemmArgs& a, size_t align_a, size_t align_b, 
 // whole waves); tile_span > 0 runs tiles [tile_base, +span), each split
 // a.splitk ways (the meet's tile id is the local index).
 hipError_t gemm_f32_tile_launch(GemmArgs a, hipStream_t stream, int variant) {
-  const int bm = variant == 3 ? 64 : 128;  // 3: kF32T64
+  const int bm = variant == 3 || variant == 4 ? 64 : 128;  // 3: kF32T64, 4: kF32T64x2
   a.tiles_m = (a.M + bm - 1) / bm;
   a.tiles_n = (a.N + kf32t::BN - 1) / kf32t::BN;
   a.supertile = choose_supertile(a.tiles_m, a.tiles_n);
@@ -454,6 +454,10 @@ hipError_t gemm_f32_tile_launch(GemmArgs a, hipStream_t stream, int variant) {
 #endif
   if (variant == 3) {  // kF32T64: 64x128 tiles, 4 stages, one workgroup per CU
     hipLaunchKernelGGL((kf32t::gemm_f32_t128<4, true, 64>), dim3((unsigned)nblocks), dim3(kf32t::NT), 0, stream, a);
+    return hipGetLastError();
+  }
+  if (variant == 4) {  // kF32T64x2: 64x128 tiles, 2 stages, two workgroups per CU
+    hipLaunchKernelGGL((kf32t::gemm_f32_t128<2, true, 64>), dim3((unsigned)nblocks), dim3(kf32t::NT), 0, stream, a);
     return hipGetLastError();
   }
   if (variant == 2) {  // kF32T128x2

@@ -8,7 +8,7 @@ T128x2 / T192 / T192x128, split-K) for grids that under-fill the 256 CUs or
 that only 192-row tiles cut into whole waves, SCHED 3 of
 ``gemm_mfma256.hip`` for edge tiles the others do not take; exact fp32 on
 ``gemm_f32_tile.hip`` (f32_t128x2 on grids of >= 2 tiles per CU, f32_t128
-split-K below that, f32_t64 = 64x128 tiles where they fill the chip unsplit), ``gemm_f32_256.hip`` and ``gemm_f32_w4.hip`` (split-K)
+split-K below that, f32_t64 = 64x128 tiles where they fill the chip unsplit, f32_t64x2 = those two per CU, split), ``gemm_f32_256.hip`` and ``gemm_f32_w4.hip`` (split-K)
 as the planner prices them; fp8 e4m3 on ``gemm_fp8.hip`` and
 the fp8 tile family; ``gemm_generic.hip`` for anything else. Large problems
 whose K / N / alignment miss the LDS-DMA granule are zero-padded onto the
@@ -38,7 +38,8 @@ from . import _native
 KERNELS = {"auto": 0, "generic": 2, "f32_256s": 7, "mfma256d": 9, "fp8_w4": 16, "w4": 21,
            "t128": 26, "t128x2": 27, "t256x128": 28, "f32_w4": 29, "w4s": 36, "fp8_w4s": 37,
            "fp8_t128": 41, "fp8_t256x128": 42, "f32_t128": 51, "f32_t128x2": 53,
-           "t192": 60, "t192x128": 61, "fp8_t192": 62, "fp8_t192x128": 63, "f32_t64": 64}
+           "t192": 60, "t192x128": 61, "fp8_t192": 62, "fp8_t192x128": 63, "f32_t64": 64,
+           "f32_t64x2": 65}
 # A/B and timing-only diagnostic kernels (api.h ``ExperimentKernel``): accepted
 # only by a library built with ``PDMB_EXPERIMENTS=1``; ``diag_*`` ones skip waits
 # or data movement on purpose and compute WRONG results.
@@ -62,7 +63,7 @@ KERNEL_NAMES = {0: "auto", 2: "pdmb_generic_nn", 7: "pdmb_f32_256s_nn", 9: "pdmb
                 37: "pdmb_fp8_w4s", 41: "pdmb_fp8_t128_nt", 42: "pdmb_fp8_t256x128_nt",
                 51: "pdmb_f32_t128_nn", 53: "pdmb_f32_t128x2_nn", 60: "pdmb_t192_nn",
                 61: "pdmb_t192x128_nn", 62: "pdmb_fp8_t192_nt", 63: "pdmb_fp8_t192x128_nt",
-                64: "pdmb_f32_t64_nn",
+                64: "pdmb_f32_t64_nn", 65: "pdmb_f32_t64x2_nn",
                 1: "pdmb_mfma256_nn",
                 3: "pdmb_mfma256b_nn", 4: "pdmb_mfma256c_nn", 5: "pdmb_mfma256c_stamp",
                 6: "pdmb_f32_256_nn", 15: "pdmb_fp8_256_nt", -1: "unsupported"}

@@ -42,7 +42,10 @@ SPLIT_CASES = [("auto:bfloat16", (2560, 4096, 16384)), ("auto:bfloat16", (4608, 
                # round 5: small-grid split rules (T128 x 3 below 32 K-tiles per slice)
                ("auto:bfloat16", (768, 768, 4096)), ("auto:float16", (256, 768, 2048)),
                ("auto:bfloat16", (1024, 1024, 8192)), ("auto:float8_e4m3fn", (768, 768, 8192)),
-               ("auto:float8_e4m3fn", (1000, 260, 8192))]
+               ("auto:float8_e4m3fn", (1000, 260, 8192)),
+               # round 5: f32_t64x2 split on small fp32 grids
+               ("auto:float32", (1536, 3072, 1024)), ("auto:float32", (1536, 1536, 4096)),
+               ("auto:float32", (9216, 256, 16384))]
 
 
 def main():

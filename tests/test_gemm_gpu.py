@@ -34,7 +34,8 @@ FAST = ["mfma256d", "mfma256", "mfma256b", "mfma256c"]
 
 TILED = ("pdmb_w4_nn", "pdmb_t256x128_nn", "pdmb_t128_nn", "pdmb_t128x2_nn", "pdmb_w4s",
          "pdmb_t192_nn", "pdmb_t192x128_nn")
-F32 = ("pdmb_f32_256s_nn", "pdmb_f32_w4_nn", "pdmb_f32_t128_nn", "pdmb_f32_t128x2_nn", "pdmb_f32_t64_nn")
+F32 = ("pdmb_f32_256s_nn", "pdmb_f32_w4_nn", "pdmb_f32_t128_nn", "pdmb_f32_t128x2_nn", "pdmb_f32_t64_nn",
+       "pdmb_f32_t64x2_nn")
 
 
 def _need(kernel):
@@ -163,8 +164,8 @@ def test_fp32_exact_mfma_path():
     A = torch.randn(512, 512, device="cuda", dtype=torch.float32)
     B = torch.randn(512, 512, device="cuda", dtype=torch.float32)
     # 4 256-tiles: a smaller fp32 tile (128x128, or 64x128 since round 5)
-    assert gemm.kernel_for(A, B) in ("pdmb_f32_t128_nn", "pdmb_f32_t64_nn")
-    for k in ("auto", "generic", "f32_256s", "f32_w4", "f32_t128", "f32_t64"):
+    assert gemm.kernel_for(A, B) in ("pdmb_f32_t128_nn", "pdmb_f32_t64_nn", "pdmb_f32_t64x2_nn")
+    for k in ("auto", "generic", "f32_256s", "f32_w4", "f32_t128", "f32_t64", "f32_t64x2"):
         C = gemm.matmul(A, B, kernel=k)
         assert _relerr(C, _ref(A, B)) < TOL[torch.float32]
 
@@ -206,7 +207,7 @@ def test_race_screen_repeated_runs(kernel):
 @pytest.mark.parametrize("M,N,K", [(256, 256, 32), (512, 768, 96), (1000, 1052, 320),
                                    (300, 200, 64), (2304, 2048, 1024)])
 @pytest.mark.parametrize("kernel", ["f32_256", "f32_256s", "f32_w4", "x_f32_256s_direct", "f32_t128",
-                                    "f32_t128x2", "x_f32_w4_b32", "x_f32_t128_b32", "f32_t64"])
+                                    "f32_t128x2", "x_f32_w4_b32", "x_f32_t128_b32", "f32_t64", "f32_t64x2"])
 def test_f32_256_exact_and_random(M, N, K, kernel):
     _need(kernel)
     g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
@@ -222,7 +223,7 @@ def test_f32_256_exact_and_random(M, N, K, kernel):
     assert _relerr(C, _ref(A, B)) < TOL[torch.float32]
 
 
-@pytest.mark.parametrize("kernel", ["f32_w4", "f32_t128", "f32_t64"])
+@pytest.mark.parametrize("kernel", ["f32_w4", "f32_t128", "f32_t64", "f32_t64x2"])
 @pytest.mark.parametrize("M,N,K,splitk,split", [(4096, 1024, 4096, 0, None), (4096, 2048, 4096, 0, None),
                                                 (2048, 2048, 2048, 0, None), (1000, 1052, 4096, 0, True),
                                                 (512, 512, 1024, 2, True), (4096, 4096, 4096, 0, False),
@@ -258,11 +259,13 @@ def test_f32_splitk_exact(kernel, M, N, K, splitk, split):
     assert torch.equal(gemm.matmul(A, B, kernel=kernel, splitk=splitk), C)
 
 
-@pytest.mark.parametrize("M,N,K,kernel,S", [(2560, 2048, 4096, "f32_t128x2", 4), (1024, 256, 16384, "f32_t64", 8),
-                                             (512, 12288, 2048, "f32_t128x2", 2), (1000, 3000, 4096, None, None)])
+@pytest.mark.parametrize("M,N,K,kernel,S", [(2560, 2048, 4096, "f32_t64x2", 2), (1024, 256, 16384, "f32_t64", 8),
+                                             (512, 12288, 2048, "f32_t128x2", 2), (1000, 3000, 4096, None, None),
+                                             (1536, 3072, 1024, "f32_t64x2", 2), (1536, 1536, 4096, "f32_t64x2", 4)])
 def test_f32_auto_x2_split_and_split8_exact(M, N, K, kernel, S, monkeypatch):
     """Round 5 planner: auto runs f32_t128x2 split >= 3 slices per CU on grids
-    of < 2 tiles per CU, and 8-way fp32 splits (test_planner_cpu.py). The plan
+    of < 2 tiles per CU, f32_t64x2 split there, and 8-way fp32 splits
+    (test_planner_cpu.py). The plan
     auto prices is the one that launches; exact on small integers (edges
     masked), bitwise repeatable on random data."""
     monkeypatch.delenv("PDMB_F32X2SPLIT", raising=False)
@@ -313,7 +316,7 @@ def test_small_grid_split_plans_exact(dtype, M, N, K, S, monkeypatch):
         assert torch.equal(gemm.matmul(A, B), C)
 
 
-F32_T128_ARMS = ["f32_t128", "f32_t128x2", "x_f32_t128_b32", "f32_t64"]
+F32_T128_ARMS = ["f32_t128", "f32_t128x2", "x_f32_t128_b32", "f32_t64", "f32_t64x2"]
 
 
 @pytest.mark.parametrize("M,N,K,b", [(128, 128, 32, 1), (256, 384, 96, 1), (1000, 1052, 320, 1),

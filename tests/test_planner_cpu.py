@@ -33,11 +33,11 @@ def test_f32_shards_fill_the_chip(C, n, ws):
     shard = n // ws
     k, S, cost, _ = plan(C, F32, n, shard, n)
     bm, bn = {"pdmb_f32_t128_nn": (128, 128), "pdmb_f32_t128x2_nn": (128, 128),
-              "pdmb_f32_t64_nn": (64, 128)}.get(k, (256, 256))
+              "pdmb_f32_t64_nn": (64, 128), "pdmb_f32_t64x2_nn": (64, 128)}.get(k, (256, 256))
     units = -(-n // bm) * -(-shard // bn) * max(S, 1)
     assert units >= 192, (n, ws, k, S)
     if n == 4096:
-        assert k in ("pdmb_f32_t128_nn", "pdmb_f32_t128x2_nn", "pdmb_f32_t64_nn") or (
+        assert k in ("pdmb_f32_t128_nn", "pdmb_f32_t128x2_nn", "pdmb_f32_t64_nn", "pdmb_f32_t64x2_nn") or (
             k == "pdmb_f32_w4_nn" and S > 1)
 
 
@@ -207,6 +207,7 @@ def test_split3_plans(C, monkeypatch):
     256^2 fp32 tile): measured ahead on these grids (profiles/r7r_split3_ab_*.jsonl),
     left out where it lost (bf16 1024^2 x 4096, fp32 2560 x 2048 x 4096)."""
     monkeypatch.delenv("PDMB_SPLIT3", raising=False)
+    monkeypatch.setenv("PDMB_F32T64X2", "0")  # (f32_t64x2 takes 1536^2 x 4096 since)
     assert plan(C, BF16, 2560, 4096, 16384)[:2] == ("pdmb_w4_nn", 3)
     assert plan(C, BF16, 5120, 2048, 16384)[:2] == ("pdmb_w4_nn", 3)
     assert plan(C, F32, 2560, 256, 8192)[1] == 3
@@ -252,6 +253,7 @@ def test_f32_x2_split_on_small_grids(C, monkeypatch):
     split (the launch re-plans with the kernel fixed); PDMB_F32X2SPLIT=0 turns
     it off."""
     monkeypatch.delenv("PDMB_F32X2SPLIT", raising=False)
+    monkeypatch.setenv("PDMB_F32T64X2", "0")  # (f32_t64x2 takes 2560 x 2048 x 4096 since)
     assert plan(C, F32, 2560, 2048, 4096)[:2] == ("pdmb_f32_t128x2_nn", 4)
     assert plan(C, F32, 2560, 2048, 4096, kernel=53)[:2] == ("pdmb_f32_t128x2_nn", 4)
     for shape in ((4096, 1024, 4096), (2048, 2048, 2048), (1536, 1536, 4096), (768, 9216, 4096),
@@ -293,3 +295,20 @@ def test_split3_small_bf16_grids(C, monkeypatch):
     assert plan(C, FP8, 768, 768, 8192)[:2] == ("pdmb_fp8_t128_nt", 3)  # 22: ahead
     monkeypatch.setenv("PDMB_SPLIT3_SMALL", "0")
     assert plan(C, BF16, 768, 768, 4096)[1] != 3
+
+
+def test_f32_t64x2_plans(C, monkeypatch):
+    """Round 5: f32_t64x2 (the 64x128 exact-fp32 tile on 2 stages, two per CU),
+    split, on fp32 grids of fewer than two 128x128 tiles per CU: auto vs
+    PDMB_F32T64X2=0 on 21 grids, median +6.1 %, up to +37 %
+    (profiles/r7ap_f32_t64x2_auto_ab.jsonl); the full grids keep their plans
+    (5120^3: f32_t128x2 waves + split tail)."""
+    monkeypatch.delenv("PDMB_F32T64X2", raising=False)
+    assert plan(C, F32, 1536, 3072, 1024)[:2] == ("pdmb_f32_t64x2_nn", 2)
+    assert plan(C, F32, 1536, 1536, 4096)[:2] == ("pdmb_f32_t64x2_nn", 4)
+    assert plan(C, F32, 1536, 3072, 1024, kernel=65)[:2] == ("pdmb_f32_t64x2_nn", 2)  # fixed = auto's
+    for shape in ((4096, 4096, 4096), (8192, 8192, 8192), (5120, 5120, 5120), (16384, 1024, 16384)):
+        assert plan(C, F32, *shape)[0] != "pdmb_f32_t64x2_nn", shape
+    assert plan(C, F32, 5120, 5120, 5120)[3] == (0, 4, 1536, 1)
+    monkeypatch.setenv("PDMB_F32T64X2", "0")
+    assert plan(C, F32, 1536, 3072, 1024)[0] != "pdmb_f32_t64x2_nn"
