@@ -381,6 +381,10 @@ static bool w4s_auto(const Problem& p) {
 // f32_t128x2 split into slices on a grid of fewer than two tiles per CU
 // (plan_uncached takes it there from 3 slices per CU: PDMB_F32X2SPLIT=0 turns
 // that off, A/B, read per call).
+static bool t64x2_full_on() {  // PDMB_F32T64X2_FULL=0: f32_t64x2 only on the small grids (A/B)
+  const char* e = std::getenv("PDMB_F32T64X2_FULL");
+  return !(e && std::atoi(e) == 0);
+}
 static constexpr double kF32X2AloneKt = 1.9;
 static bool f32x2_split_on() {
   const char* e = std::getenv("PDMB_F32X2SPLIT");
@@ -551,14 +555,22 @@ static Plan plan(const Problem& p, int kernel) {
   return r;
 }
 
+// kAuto without f32_t64x2 on the full grids: the baseline f32_tail_plan
+// weighs its split tail against (the tails were measured against those plans).
+constexpr int kAutoNoT64x2Full = -7;
+
 static Plan plan_uncached(const Problem& p, int kernel) {
+  const bool no_t64x2_full = kernel == kAutoNoT64x2Full;
+  if (no_t64x2_full) kernel = kAuto;
   // The launch re-plans the split of the kernel auto resolved to with that
   // kernel fixed (tiled_launch). Auto takes f32_t128x2 on a grid of fewer than
   // two tiles per CU only split >= 3 slices per CU (below), a rule the fixed
   // plan does not apply (an explicit request runs it on any grid): there the
   // fixed plan is auto's own.
-  if ((kernel == kF32T128x2 || kernel == kF32T64x2) && p.splitk == 0 && p.dtype == kF32 && f32x2_split_on() &&
-      tiles_of(p, kernel) < 2LL * (p.cus > 0 ? p.cus : device_cus())) {
+  // (f32_t64x2: on every grid — auto takes it only split on the full grids.)
+  if (((kernel == kF32T128x2 && f32x2_split_on() && tiles_of(p, kernel) < 2LL * (p.cus > 0 ? p.cus : device_cus())) ||
+       kernel == kF32T64x2) &&
+      p.splitk == 0 && p.dtype == kF32) {
     const Plan a = plan(p, kAuto);
     if (a.kernel == kernel) return a;
   }
@@ -590,8 +602,8 @@ static Plan plan_uncached(const Problem& p, int kernel) {
     if (no64 && m.kernel == kF32T64) continue;
     // f32_t64x2 in auto only where the 128x128 tiles number fewer than two per
     // CU (the full grids keep their measured f32_t128x2 / tail plans)
-    if (kernel == kAuto && m.kernel == kF32T64x2 &&
-        (!t64x2_on || tiles_of(p, kF32T128x2) >= 2LL * (p.cus > 0 ? p.cus : device_cus())))
+    const bool full_grid = tiles_of(p, kF32T128x2) >= 2LL * (p.cus > 0 ? p.cus : device_cus());
+    if (kernel == kAuto && m.kernel == kF32T64x2 && (!t64x2_on || (full_grid && (no_t64x2_full || !t64x2_full_on()))))
       continue;
     if (m.cls != dt_class(p) || !supports(p, m.kernel)) continue;
     any = true;
@@ -648,6 +660,17 @@ static Plan plan_uncached(const Problem& p, int kernel) {
       if (S == 3 && p.splitk != 3 &&
           (no3 || ((ktiles(p) + 2) / 3 < 32 && !s3small) || m.kernel == kF32W4))
         continue;
+      // f32_t64x2 on the full fp32 grids (round 5): split only — unsplit it lost
+      // (3072 x 3584 x 4096 130.1 vs 144.4 TF for f32_t128x2 x 3), split 2 ways it
+      // gained on the grids without a split tail (4608^2 x 4096 143.2 vs 127.2,
+      // 5120 x 2560 x 8192 143.6 vs 130.4; profiles/r7as_f32_t64x2_full_ab.jsonl).
+      // Grids with an fp32 split tail keep it (f32_tail_plan's baseline leaves
+      // these plans out: on them t64x2 x 2 measured -1.7 to +0.9 %). The rule as
+      // built, auto vs PDMB_F32T64X2_FULL=0 on 16 of the 31 non-tail grids of a
+      // 784-grid scan it changes: -2.3 to +19.4 %, median +2.3 %
+      // (r7at_f32_t64x2_full_rule_ab.jsonl; the two losses are 3072 x 3584 x
+      // 4096 and its transpose, where f32_t128x2 x 3 stays 2 % ahead).
+      if (kernel == kAuto && m.kernel == kF32T64x2 && full_grid && S < 2) continue;
       if (p.splitk > 0 && S != p.splitk) continue;
       if (!split_ok(p, m.kernel, S)) continue;
       // auto takes a two-per-CU fp32 tile only on grids whose tiles (not split
@@ -776,7 +799,7 @@ static TailPlan f32_tail_plan(const Problem& p) {
   const char* env = std::getenv("PDMB_TILE_TAIL");
   if (env && std::atoi(env) == 0) return best;
   if (!supports(p, kF32T128) || !supports(p, kF32T128x2)) return best;
-  const Plan whole = plan(p, kAuto);  // the best single launch (possibly split: 5120^3 ran f32_t128 x 2)
+  const Plan whole = plan(p, kAutoNoT64x2Full);  // the best single launch (possibly split: 5120^3 ran f32_t128 x 2)
   if (whole.kernel != kF32T128x2 && whole.kernel != kF32T128) return best;
   const long long cus = device_cus(), slots2 = 2 * cus;
   const long long T = tiles_of(p, kF32T128x2);

@@ -307,8 +307,13 @@ def test_f32_t64x2_plans(C, monkeypatch):
     assert plan(C, F32, 1536, 3072, 1024)[:2] == ("pdmb_f32_t64x2_nn", 2)
     assert plan(C, F32, 1536, 1536, 4096)[:2] == ("pdmb_f32_t64x2_nn", 4)
     assert plan(C, F32, 1536, 3072, 1024, kernel=65)[:2] == ("pdmb_f32_t64x2_nn", 2)  # fixed = auto's
-    for shape in ((4096, 4096, 4096), (8192, 8192, 8192), (5120, 5120, 5120), (16384, 1024, 16384)):
+    for shape in ((4096, 4096, 4096), (8192, 8192, 8192), (16384, 16384, 16384), (16384, 1024, 16384)):
         assert plan(C, F32, *shape)[0] != "pdmb_f32_t64x2_nn", shape
-    assert plan(C, F32, 5120, 5120, 5120)[3] == (0, 4, 1536, 1)
+    assert plan(C, F32, 5120, 5120, 5120)[3] == (0, 4, 1536, 1)  # its split tail stays
+    # full grids without a split tail: split 2 ways (r7as), never unsplit
+    assert plan(C, F32, 4608, 4608, 4096)[:2] == ("pdmb_f32_t64x2_nn", 2)
+    assert plan(C, F32, 3072, 3584, 4096)[1] != 1 or plan(C, F32, 3072, 3584, 4096)[0] != "pdmb_f32_t64x2_nn"
+    monkeypatch.setenv("PDMB_F32T64X2_FULL", "0")
+    assert plan(C, F32, 4608, 4608, 4096)[0] != "pdmb_f32_t64x2_nn"
     monkeypatch.setenv("PDMB_F32T64X2", "0")
     assert plan(C, F32, 1536, 3072, 1024)[0] != "pdmb_f32_t64x2_nn"
