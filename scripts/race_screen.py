@@ -45,7 +45,8 @@ SPLIT_CASES = [("auto:bfloat16", (2560, 4096, 16384)), ("auto:bfloat16", (4608, 
                ("auto:float8_e4m3fn", (1000, 260, 8192)),
                # round 5: f32_t64x2 split on small fp32 grids
                ("auto:float32", (1536, 3072, 1024)), ("auto:float32", (1536, 1536, 4096)),
-               ("auto:float32", (9216, 256, 16384))]
+               ("auto:float32", (9216, 256, 16384)), ("auto:float32", (3584, 3584, 2048)),
+               ("auto:float32", (4608, 4608, 4096))]
 
 
 def main():

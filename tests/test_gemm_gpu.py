@@ -261,7 +261,8 @@ def test_f32_splitk_exact(kernel, M, N, K, splitk, split):
 
 @pytest.mark.parametrize("M,N,K,kernel,S", [(2560, 2048, 4096, "f32_t64x2", 2), (1024, 256, 16384, "f32_t64", 8),
                                              (512, 12288, 2048, "f32_t128x2", 2), (1000, 3000, 4096, None, None),
-                                             (1536, 3072, 1024, "f32_t64x2", 2), (1536, 1536, 4096, "f32_t64x2", 4)])
+                                             (1536, 3072, 1024, "f32_t64x2", 2), (1536, 1536, 4096, "f32_t64x2", 4),
+                                             (3584, 3584, 2048, "f32_t64x2", 2), (4608, 4608, 4096, "f32_t64x2", 2)])
 def test_f32_auto_x2_split_and_split8_exact(M, N, K, kernel, S, monkeypatch):
     """Round 5 planner: auto runs f32_t128x2 split >= 3 slices per CU on grids
     of < 2 tiles per CU, f32_t64x2 split there, and 8-way fp32 splits
