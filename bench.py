@@ -107,8 +107,12 @@ class Workload:
     ``batch`` (independent only): GEMMs per step (a bmm), the rank-0-alone
     reference of batch_parallel's local batch."""
 
-    def __init__(self, a, ctx, mode: str, overlap: bool, batch: int = 1):
+    def __init__(self, a, ctx, mode: str, overlap: bool, batch: int = 1,
+                 test_corrupt_rank: int | None = None):
         self.ctx, self.mode, self.overlap = ctx, mode, overlap
+        # tests only (the per-mode check's negative control): verify() damages
+        # one checked output on this rank before comparing; never set by main()
+        self._test_corrupt_rank = test_corrupt_rank
         self.cuda = ctx.device.type == "cuda"
         self.dt = DTYPES[a.dtype]
         self.backend = a.backend
@@ -125,6 +129,9 @@ class Workload:
         self.pipe = None
         self.step = None                 # set below, or by _pipeline
         self._closers = []               # collective teardown (IpcGather.close), run by close()
+        self._negate = []                # verify(): operands whose sign the check step flips
+        self._targets = lambda: []       # verify(): what the check step's outputs must satisfy
+        self._fallback_gathered = {}     # serialized fallback's all-gather outputs, by ring slot
         comp = torch.cuda.current_stream(dev) if self.cuda else None
         self._mask = None
         if overlap and self.cuda and a.comm_cus > 0 and mode in ("batch_parallel", "matrix_parallel",
@@ -142,6 +149,9 @@ class Workload:
 
             def step():
                 self._mm(A, B, C)
+            self._negate = [A]
+            self._targets = lambda: ([("gemm", A[i], B[i], C[i]) for i in sorted({0, batch - 1})]
+                                     if batch > 1 else [("gemm", A, B, C)])
             self.flops = flop_gemm * ws * batch
             self.global_batch, self.parallelism = ws * batch, f"independent{ws}"
         elif mode == "batch_parallel":
@@ -155,6 +165,7 @@ class Workload:
                      else (lambda *shape: torch.empty(*shape, device=dev, dtype=odt)))
             C = alloc(lb, n, n)
             self.kernel = self._label(A, B, C)
+            self._negate = [A]
             if overlap:
                 # ring over the batch's own outputs; one element: a second C (reference C1/C2)
                 units = ([(A[b], B[b], C[b]) for b in range(lb)] if lb >= 2 else
@@ -169,6 +180,7 @@ class Workload:
                     ar(units[r][2][s:e], after=after, done=done)
                 self._pipeline(a, units, coll, lb, "all_reduce", n * n * C.element_size(), cs, peer,
                                probe=lambda s, e: ar(units[0][2][s:e]), impl=impl)
+                self._targets = lambda: [("reduce", *units[r]) for r in self._last_slots(lb)]
             else:
                 self._serial_split()
                 impl, cs = self._collective(ar_impl, "all_reduce", C[0], [C], None)
@@ -181,6 +193,7 @@ class Workload:
                     if ws > 1:
                         all_reduce_now(C, impl, cs)
                     self._seg(2)
+                self._targets = lambda: [("reduce", A[b], B[b], C[b]) for b in sorted({0, lb - 1})]
             self.flops = flop_gemm * gb
             self.global_batch, self.parallelism = gb, f"dp{ws}"
         elif mode == "matrix_parallel":
@@ -198,6 +211,7 @@ class Workload:
                      else (lambda: torch.empty(n, sh.padded, device=dev, dtype=odt)))
             Cl = alloc()
             self.kernel = self._label(A, Bl, Cl)
+            self._negate = [A]
             if overlap:
                 units = [(A, Bl, Cl), (A, Bl, alloc())]
                 cs = CommStream(dev)
@@ -224,6 +238,18 @@ class Workload:
                 self._pipeline(a, units, coll, 1, "all_gather", n * sh.padded * Cl.element_size(),
                                cs, gath, probe=probe, impl=impl, prepare=prepare)
                 probe_out.clear()
+
+                def targets():
+                    out = []
+                    for r in self._last_slots(1):
+                        out.append(("gemm", A, Bl, units[r][2]))
+                        if self.pipe is not None:
+                            out += [("gather", units[r][2][s:e], self._gathered[(r, p)])
+                                    for p, (s, e) in enumerate(self.pipe.pieces)]
+                        elif r in self._fallback_gathered:
+                            out.append(("gather", units[r][2], self._fallback_gathered[r]))
+                    return out
+                self._targets = targets
             else:
                 gathered = torch.empty(ws * n, sh.padded, device=dev, dtype=odt)
                 impl, cs = self._collective(ag_impl, "all_gather", Cl, [Cl], None)
@@ -237,6 +263,8 @@ class Workload:
                     if ws > 1:
                         all_gather_now(gathered, Cl, impl, cs)
                     self._seg(2)
+                self._targets = lambda: [("gemm", A, Bl, Cl)] + ([("gather", Cl, gathered)] if ws > 1
+                                                                  else [])
             self.flops = flop_gemm
             self.global_batch, self.parallelism = 1, f"tp{ws}"
         elif mode == "ring_parallel":
@@ -326,7 +354,7 @@ class Workload:
     def _serial_fallback(self, units, per_step, kind, impl, gath=None):
         """The serialized step over the same units (collective on the current stream)."""
         ws, dev = self.ctx.world_size, self.ctx.device
-        gathered = {}
+        gathered = self._fallback_gathered
         cs = gath if gath is not None else (CommStream(dev) if impl != "rccl" else None)
 
         def step():
@@ -471,6 +499,100 @@ class Workload:
         tel["host_issue_ms"] = issued * 1e3
         return elapsed, mine, tel
 
+    # -- the per-mode check -------------------------------------------------------
+    def _last_slots(self, per_step: int):
+        """Ring slots the most recent step wrote: the pipeline's last
+        ``per_step`` units, or (serialized fallback) slots 0..per_step-1."""
+        if self.pipe is not None:
+            k = self.pipe.k
+            return [u % self.pipe.R for u in range(max(k - per_step, 0), k)]
+        return list(range(per_step))
+
+    def verify(self) -> dict:
+        """Check the data of one more step, run AFTER the timed region
+        (parallel/verify.py; the reference's validate_result intent,
+        matmul_scaling_benchmark.py:240-249, applied to every mode's output and
+        collective). The A operands' signs are flipped first (exact in every
+        dtype), so this step's products are the exact negation of every earlier
+        step's: a collective that delivered a stale buffer — a peer's previous
+        output, a ring slot not yet rewritten — is off by twice the value and
+        fails. Per target of the step:
+
+          * ``gemm``: 24 sampled rows of C against an fp32 recompute of A @ B;
+          * ``reduce`` (batch_parallel): the same rows of the reduced C against
+            the fp32 all-reduce (torch.distributed) of every rank's fp32
+            recompute, and the reduced C's digest identical on every rank;
+          * ``gather`` (matrix_parallel): every block of the gathered output
+            bitwise equal (parallel/verify.py ``digest``) to its producer rank's
+            local C.
+
+        Collective (every rank runs the same targets). Returns ``{"check":
+        "pass" | "fail" | "skipped", "check_detail": ...}``, agreed across ranks."""
+        from pytorch_distributed_matmul_benchmark_amd.parallel.verify import (
+            REL_TOL, digest, flip_sign_, ref_rows, rows_error, rows_of, sample_rows)
+
+        ctx, ws = self.ctx, self.ctx.world_size
+        if self.mode == "ring_parallel":
+            return {"check": "skipped", "check_detail": "ring_parallel: no per-mode check"}
+        for x in self._negate:
+            flip_sign_(x)
+        self.step()
+        self.finish()
+        self._sync()
+        corrupt = self._test_corrupt_rank is not None and self._test_corrupt_rank == ctx.rank
+        worst, fails = {}, []
+
+        def note(key, err, tol):
+            worst[key] = max(worst.get(key, 0.0), err)
+            if not err <= tol:
+                fails.append(f"{key} error {err:.3g} > {tol:.3g}")
+
+        def gathered_digests(d: int):
+            if not ctx.is_distributed:
+                return [d]
+            t = torch.tensor([d], dtype=torch.int64, device=ctx.device)
+            out = torch.empty(ws, dtype=torch.int64, device=ctx.device)
+            dist.all_gather_into_tensor(out, t)
+            return [int(v) for v in out.tolist()]
+
+        for kind, *ops in self._targets():
+            if kind in ("gemm", "reduce"):
+                A, B, C = ops
+                if corrupt:
+                    C.view(-1)[0] = 1e4  # row 0 is always sampled
+                    corrupt = False
+                rows = sample_rows(C.shape[0])
+                pre = ref_rows(A, B, rows)
+                tol = REL_TOL.get(C.dtype, 2.0 ** -6)
+                if kind == "gemm":
+                    note("gemm", rows_error(rows_of(C, rows), pre), tol)
+                    continue
+                both = torch.stack([pre, pre.abs()])
+                if ctx.is_distributed:
+                    dist.all_reduce(both)
+                note("reduce", rows_error(rows_of(C, rows), both[0], both[1]), tol * (ws + 2) / 4)
+                ds = gathered_digests(digest(C))
+                if len(set(ds)) != 1:
+                    fails.append("reduced output differs between ranks")
+            else:  # gather
+                local, gathered = ops
+                if corrupt:
+                    gathered.view(-1)[0] += 1
+                    corrupt = False
+                ds = gathered_digests(digest(local))
+                rows = local.shape[0]
+                bad = [j for j in range(ws) if digest(gathered[j * rows:(j + 1) * rows]) != ds[j]]
+                worst["gather_blocks_wrong"] = worst.get("gather_blocks_wrong", 0) + len(bad)
+                if bad:
+                    fails.append(f"gathered blocks of ranks {bad} differ from their producers")
+        ok = all_ok(ctx, not fails)
+        detail = {k: (round(v, 6) if isinstance(v, float) else v) for k, v in worst.items()}
+        if fails:
+            detail["failed"] = fails[:4]
+        elif not ok:
+            detail["failed"] = ["on another rank"]
+        return {"check": "pass" if ok else "fail", "check_detail": detail}
+
     def close(self):
         if self.pipe is not None:
             self.pipe.close()
@@ -595,14 +717,16 @@ def _die(ctx, key: str, exc: BaseException) -> None:
 
 
 def _measure(a, ctx, mode: str, overlap: bool, warmup: int, steps: int, key: str,
-             warmup_ms: float = 0.0, batch: int = 1):
-    """Build (agreed across ranks) and time one workload. Returns
-    ``(tflops, seconds, info)`` or ``(None, None, error_string)``."""
+             warmup_ms: float = 0.0, batch: int = 1, test_corrupt_rank: int | None = None):
+    """Build (agreed across ranks), time, then check (``Workload.verify``,
+    outside the timed region) one workload. Returns ``(tflops, seconds,
+    info)`` — ``info["check"]`` is "pass" / "fail" / "skipped" — or ``(None,
+    None, error_string)``."""
     w, err = None, None
     _phase(ctx, key, "setup")
     try:
         _fault(ctx, key, "setup")
-        w = Workload(a, ctx, mode, overlap, batch=batch)
+        w = Workload(a, ctx, mode, overlap, batch=batch, test_corrupt_rank=test_corrupt_rank)
     except Exception as e:  # OOM, unsupported shape, ...: every rank skips together
         err = f"{type(e).__name__}: {e}"
         print(f"[rank {ctx.rank}] {key} setup failed: {err}", file=sys.stderr, flush=True)
@@ -618,6 +742,10 @@ def _measure(a, ctx, mode: str, overlap: bool, warmup: int, steps: int, key: str
         wms = w.warm(warmup, warmup_ms)
         _phase(ctx, key, "timed")
         el, mine, tel = w.timed(steps)
+        _phase(ctx, key, "check")
+        t_check = time.perf_counter()
+        checked = w.verify()
+        checked["check_s"] = round(time.perf_counter() - t_check, 3)
     except Exception as e:
         _die(ctx, key, e)
     _phase(ctx, key, "close")
@@ -636,7 +764,8 @@ def _measure(a, ctx, mode: str, overlap: bool, warmup: int, steps: int, key: str
                 sclk_mhz_min_over_ranks=(round(min(clocks), 1) if min(clocks) > 0 else None),
                 # host enqueue time per step (rank max) against ms_per_step: a host-bound
                 # schedule shows host_issue close to the step time with the GPU waiting
-                host_issue_ms_per_step=round(max(gather_scalars(ctx, tel["host_issue_ms"])) / steps, 4))
+                host_issue_ms_per_step=round(max(gather_scalars(ctx, tel["host_issue_ms"])) / steps, 4),
+                **checked)
     if comp is not None:
         info["compute_ms"], info["comm_ms"] = round(comp, 4), round(comm, 4)
     if w.coll_choice is not None:
@@ -686,7 +815,7 @@ def _rccl_version(ctx):
         return None
 
 
-def main() -> int:
+def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -731,7 +860,11 @@ def main() -> int:
                          "secondary modes run longer than this (0: no limit)")
     ap.add_argument("--no-scaling-ref", action="store_true",
                     help="skip the in-job rank-0-alone references (scaling_efficiency = null at N > 1)")
-    a = ap.parse_args()
+    return ap
+
+
+def main() -> int:
+    a = build_parser().parse_args()
 
     hooks = testhooks.active()
     if hooks:  # negative-control fault injection (racy collectives): never a measurement
@@ -781,9 +914,11 @@ def main() -> int:
         return round(v / (ws * ref), 4) if ref and v is not None else None
 
     modes = {}
+    # a failed output check voids the number (Workload.verify: the step's data)
+    head_ok = head.get("check") != "fail"
     if ctx.is_main:
         out = {
-            "metric": METRIC, "value": round(value, 4), "unit": "TFLOPS",
+            "metric": METRIC, "value": round(value, 4) if head_ok else None, "unit": "TFLOPS",
             "n_gpus": ws, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms_step, 4), "higher_is_better": True,
             "scaling": "strong" if a.mode in ("matrix_parallel", "ring_parallel") else "weak",
@@ -804,6 +939,8 @@ def main() -> int:
             "world_size_seen": dist.get_world_size() if ctx.is_distributed else 1,
             "rccl_version": _rccl_version(ctx),
             "collectives_verified": verified,
+            # the headline step's own output, checked after the timed region
+            "check": head["check"], "check_detail": head["check_detail"],
             "per_rank_tflops": head["per_rank_tflops"],
             # medians of a 5 ms amdsmi poll over the timed region, with the sample counts
             "sclk_mhz": head["sclk_mhz"], "power_w": head["power_w"],
@@ -849,15 +986,19 @@ def main() -> int:
                 if v is None:
                     modes[key] = {"error": info}
                     continue
-                modes[key] = {"value": round(v, 4), "ms_per_step": round(el / a.extra_steps * 1e3, 4),
+                if info.get("check") == "fail":  # checked wrong: no number for this mode
+                    v = None
+                modes[key] = {"value": round(v, 4) if v is not None else None,
+                              "ms_per_step": round(el / a.extra_steps * 1e3, 4),
                               "steps": a.extra_steps, "warmup": a.extra_warmup,
                               "scaling": "strong" if family == "matrix_parallel" else "weak",
-                              "vs_baseline": vs_base(family, v), "scaling_efficiency": eff(v, ref),
+                              "vs_baseline": vs_base(family, v),
+                              "scaling_efficiency": eff(v, ref) if v is not None else None,
                               "ref_tflops_rank0_alone": round(ref, 4) if ref else None, **info}
 
     _Pending.emit()
     cleanup_distributed()
-    return 0
+    return 0 if head_ok else 1
 
 
 if __name__ == "__main__":

@@ -39,6 +39,24 @@ peer's comm stream has passed the same point):
     order of that chunk of every rank's ``t`` -> B1 (every chunk reduced) ->
     pull every peer's reduced chunk into place -> B2.
 
+Visibility of a peer's data (why the kernel engine's plain loads are used):
+every pull is a NEW kernel launch that starts after B0 has completed on
+this rank, and B0 completes only after every peer's comm stream passed its
+own B0, which is queued behind that peer's producer kernel. A producer's
+writes leave its XCD L2s at the end of its kernel: the per-XCD L2s are not
+coherent even within one GPU (docs/guides: MI355X_MICROARCH "Workgroup
+dispatch ... inter-workgroup visibility"), so the end-of-kernel release
+writes dirty lines back to memory for any later kernel on another XCD, the
+same write-back a peer's xGMI read relies on; the pulling kernel's own
+start-of-kernel acquire leaves no stale line in its L1/L2. So no in-kernel
+fence or system-scope load is needed — one hand-off per kernel boundary,
+nothing spins on a flag. This is an argument from the single-GPU memory
+model, not a measurement across two physical GPUs: the pull stays out of
+``auto`` by default (parallel/overlap.py ``auto_candidates``), and whenever it
+runs, ``pick_collective`` has first checked it bitwise on two rank-coded
+payloads in a row and bench.py checks every mode's delivered data
+(parallel/verify.py), so a stale pull is reported, never timed as correct.
+
 ``register(src)`` exports ``src`` (an ``ipc_empty`` tensor: its own
 hipMalloc allocation) and maps every peer's counterpart (handles exchanged by
 a host all-gather of objects); every rank registers corresponding buffers in
@@ -254,7 +272,11 @@ class IpcGather:
         mod = _mod()
         where = None
         for base, nb, peers, sizes in self.bufs:
-            if base <= src and src + nbytes <= base + nb:
+            if base <= src < base + nb:
+                if src + nbytes > base + nb:
+                    raise RuntimeError(
+                        f"IpcGather[{what}]: read of {nbytes} B from this rank ({self.me}) at offset "
+                        f"{src - base} runs past its own buffer (extent {nb} B)")
                 where = (self.me, src - base, nb)
                 break
             for r, a in peers.items():

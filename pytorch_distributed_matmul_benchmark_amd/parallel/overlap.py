@@ -780,16 +780,16 @@ COLLECTIVE_IMPLS = ("rccl", "direct", "ipc")
 
 
 def auto_candidates(device: torch.device) -> Tuple[str, ...]:
-    """What ``auto`` times: RCCL's collective, the direct P2P exchange (both
-    RCCL kernels) and, on GPU tensors, the peer-memory pull (parallel/ipc.py).
-    The pull had been opt-in since an 8-rank one-GPU rehearsal faulted in
-    round 4; its cause class is now pinned (docs/ARCHITECTURE.md "IPC fault":
-    handles re-issued for re-allocated addresses and stale imports, measured
-    by scripts/ipc_handle_probe.py) and closed by the buffer pool, the churn
-    runs clean with every pull bounds-checked (tests/test_multirank_gpu.py
-    test_ipc_churn_register_close_free), so it is a default candidate again;
-    ``PDMB_AUTO_IPC=0`` leaves it out."""
-    if device.type == "cuda" and os.environ.get("PDMB_AUTO_IPC", "1") != "0":
+    """What ``auto`` times: RCCL's collective and the direct P2P exchange (both
+    RCCL kernels); the peer-memory pull (parallel/ipc.py) joins only with
+    ``PDMB_AUTO_IPC=1``. Every pull it has ever made ran between ranks that
+    share ONE GPU (gloo rehearsals): no byte has crossed xGMI between two
+    physical devices yet, and a hipErrorIllegalAddress inside a peer pull
+    would take every rank down rather than drop the candidate. Once a 2- or
+    8-GPU run of the overlapped modes has passed its checks with it
+    (``check_collective`` below and bench.py's per-mode check), it can be a
+    default candidate again."""
+    if device.type == "cuda" and os.environ.get("PDMB_AUTO_IPC", "0") == "1":
         return COLLECTIVE_IMPLS
     return ("rccl", "direct")
 
@@ -802,22 +802,30 @@ def ipc_buffers(impl: str, device: torch.device) -> bool:
 
 def pick_collective(ctx, kind: str, t: torch.Tensor, sources=(), comm: Optional[CommStream] = None,
                     reps: int = 5, candidates: Optional[Sequence[str]] = None,
-                    spread_out: Optional[Dict[str, List[float]]] = None):
+                    spread_out: Optional[Dict[str, List[float]]] = None,
+                    _test_corrupt: Optional[Callable[[str, torch.Tensor], None]] = None):
     """``--allreduce auto`` / ``--allgather auto``: time one whole collective of
     ``t`` (all_reduce: in place; all_gather: ``t`` is this rank's block) with
     every candidate implementation on this job's own ranks (``auto_candidates``:
-    RCCL's, the direct P2P exchange, and on GPUs the peer-memory pull with
-    ``sources`` registered) — each after one untimed call and a
-    barrier, ``reps`` reps each timed alone, the median of a rank's reps and
-    the MAX over ranks (``spread_out``, if given, receives [min, max] over reps
-    and ranks per candidate) — and keep the fastest. A candidate that fails on any rank is dropped on
-    every rank. Returns ``(impl, comm_object, {impl: us or None})``; the comm
-    object is what ``make_gatherer(impl, ...)`` would have built (on ``comm``),
-    the losers' are closed. Collective: every rank must call it."""
+    RCCL's, the direct P2P exchange, and with PDMB_AUTO_IPC=1 the peer-memory
+    pull with ``sources`` registered). Each candidate is first CHECKED: two
+    calls on rank-coded payloads (parallel/verify.py ``check_collective``),
+    compared bitwise with the expected gather / sum; a candidate wrong on any
+    rank is dropped on every rank and recorded as ``"wrong"``. Then it is
+    timed: ``reps`` reps after a barrier, each timed alone, the median of a
+    rank's reps and the MAX over ranks (``spread_out``, if given, receives
+    [min, max] over reps and ranks per candidate); the fastest is kept. A
+    candidate that raises on any rank is dropped on every rank (``None``).
+    ``t``'s contents are overwritten. Returns ``(impl, comm_object, {impl: us
+    | None | "wrong"})``; the comm object is what ``make_gatherer(impl, ...)``
+    would have built (on ``comm``), the losers' are closed. ``_test_corrupt
+    (impl, result)`` (tests only: the gate's negative control) damages a
+    checked result on the calling rank. Collective: every rank must call it."""
     import statistics
     import time
 
     from .dist import all_ok, barrier, reduce_scalar
+    from .verify import check_collective
 
     dev = t.device
     cuda = dev.type == "cuda"
@@ -854,13 +862,25 @@ def pick_collective(ctx, kind: str, t: torch.Tensor, sources=(), comm: Optional[
         if not all_ok(ctx, err is None):
             drop(impl, g)
             continue
+        wrong = None
         try:
-            call(impl, g)
-            sync()
+            corrupt = ((lambda res, _i=impl: _test_corrupt(_i, res)) if _test_corrupt is not None
+                       else None)
+            wrong = check_collective(kind, ctx.rank, ctx.world_size, t, out, lambda: call(impl, g),
+                                     sync, corrupt=corrupt)
         except Exception as e:
             err = f"{type(e).__name__}: {e}"
         if not all_ok(ctx, err is None):
             drop(impl, g)
+            continue
+        if not all_ok(ctx, wrong is None):
+            if wrong is not None:
+                import sys
+
+                print(f"[rank {ctx.rank}] {kind} candidate {impl!r} returned wrong data: {wrong}",
+                      file=sys.stderr, flush=True)
+            drop(impl, g)
+            times[impl] = "wrong"
             continue
         barrier(ctx)
         reps_us = []
@@ -873,13 +893,13 @@ def pick_collective(ctx, kind: str, t: torch.Tensor, sources=(), comm: Optional[
         times[impl] = reduce_scalar(ctx, statistics.median(reps_us), "max")
         spread[impl] = [reduce_scalar(ctx, min(reps_us), "min"), reduce_scalar(ctx, max(reps_us), "max")]
         objs[impl] = g
-    ok = {k: v for k, v in times.items() if v is not None}
+    ok = {k: v for k, v in times.items() if isinstance(v, float)}
     if not ok:
-        raise RuntimeError(f"no {kind} implementation ran on every rank: {times}")
+        raise RuntimeError(f"no {kind} implementation ran correctly on every rank: {times}")
     best = min(ok, key=ok.get)
     for impl, g in objs.items():
         if impl != best and hasattr(g, "close"):
             g.close()
     if spread_out is not None:
         spread_out.update({k: [round(x, 1) for x in v] for k, v in spread.items()})
-    return best, objs[best], {k: (round(v, 1) if v is not None else None) for k, v in times.items()}
+    return best, objs[best], {k: (round(v, 1) if isinstance(v, float) else v) for k, v in times.items()}

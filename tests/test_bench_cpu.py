@@ -93,8 +93,14 @@ def test_bench_eight_ranks_driver_form():
     assert d["config"]["parallelism"] == "independent8" and d["scaling_efficiency"] is not None
     assert set(d["modes"]) == {"batch_parallel", "batch_parallel+overlap", "matrix_parallel",
                                "matrix_parallel+overlap"}
+    assert d["check"] == "pass", d["check_detail"]
     for key, m in d["modes"].items():
         assert "error" not in m, (key, m)
+        # every mode's last step checked after its timed region (Workload.verify)
+        assert m["check"] == "pass", (key, m["check_detail"])
+        if key.endswith("+overlap"):
+            c = m["collective"]  # every auto candidate passed the payload gate and was timed
+            assert all(isinstance(v, float) for v in c["us"].values()), c
         gb = 8 if key.startswith("batch") else 1
         assert m["global_batch"] == gb and m["parallelism"] == ("dp8" if gb == 8 else "tp8")
         assert m["value"] == pytest.approx(2.0 * 128 ** 3 * gb / (m["ms_per_step"] / 1e3) / 1e12,

@@ -175,8 +175,8 @@ def test_eight_ranks_signalled_check_catches_a_skipped_wait():
 
 
 # ---- the ws = 8 job shapes on real HIP (8 gloo ranks sharing the GPU) ---------
-def _bench8(*extra):
-    env = dict(os.environ)
+def _bench8(*extra, env_extra=None):
+    env = dict(os.environ, **(env_extra or {}))
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "8", "--dist-backend", "gloo",
@@ -187,22 +187,27 @@ def _bench8(*extra):
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["n_gpus"] == 8 and d["world_size_seen"] == 8 and d["value"] > 0
     assert d["collectives_verified"] is True and "modes_incomplete" not in d
+    assert d["check"] == "pass", d["check_detail"]
     for key, m in d["modes"].items():
         assert m and "error" not in m and m["value"] > 0, (key, m)
+        assert m["check"] == "pass", (key, m["check_detail"])  # Workload.verify, after timing
     return d
 
 
-@pytest.mark.parametrize("extra", [[], ["--allgather", "ipc", "--allreduce", "ipc"],
-                                   ["--mode", "matrix_parallel", "--overlap", "--chunks", "2",
-                                    "--allgather", "ipc"]])
-def test_eight_ranks_self_launch_bench(extra):
+@pytest.mark.parametrize("extra,auto_ipc", [([], "0"), ([], "1"),
+                                            (["--allgather", "ipc", "--allreduce", "ipc"], "0"),
+                                            (["--mode", "matrix_parallel", "--overlap", "--chunks", "2",
+                                              "--allgather", "ipc"], "0")])
+def test_eight_ranks_self_launch_bench(extra, auto_ipc):
     """bench.py --gpus 8 through the self-launch path, the BASELINE ws = 8
     shapes (local batch 1 with a two-slot ring, 512-column shards at 4096):
-    every mode runs, with measured overlap plans."""
-    d = _bench8(*extra)
-    if not extra:  # auto on the overlapped modes: all three candidates timed, ipc included
+    every mode runs, with measured overlap plans, and passes its check."""
+    d = _bench8(*extra, env_extra={"PDMB_AUTO_IPC": auto_ipc})
+    if not extra:  # auto on the overlapped modes: every candidate checked, then timed
+        want = {"rccl", "direct", "ipc"} if auto_ipc == "1" else {"rccl", "direct"}
         colls = [m["collective"] for m in d["modes"].values() if m.get("collective")]
-        assert colls and all(set(c["us"]) == {"rccl", "direct", "ipc"} for c in colls), colls
+        assert colls and all(set(c["us"]) == want for c in colls), colls
+        assert all(isinstance(v, float) for c in colls for v in c["us"].values()), colls
     plans = [m["plan"] for m in d["modes"].values() if m.get("plan")]
     plans += [d["config"]["overlap_plan"]] if "overlap_plan" in d["config"] else []
     assert plans and all(p["source"] == "measured" for p in plans), plans

@@ -1,0 +1,223 @@
+"""The multi-rank self-checks (parallel/verify.py; VERDICT r5 "Next #1"):
+
+* pick_collective runs every candidate on rank-coded payloads and drops one
+  that returns wrong data on any rank, on every rank ("wrong" in its times);
+* bench.py's per-mode check (Workload.verify) reports pass on honest runs and
+  fail — with the mode's value nulled by main() — when one rank's output is
+  damaged (test constructor argument) or when a collective silently does
+  nothing in the check step (the stale-buffer case the sign flip exists for).
+
+gloo on CPU, world sizes 2 and 3 (8 in test_bench_cpu's driver-form run)."""
+import importlib.util
+import json
+import os
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+from conftest import free_port
+
+from pytorch_distributed_matmul_benchmark_amd.parallel import verify as V
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+# ---- single-process pieces ---------------------------------------------------------------
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("ws", [2, 8, 16])
+def test_payload_sums_are_exact(dtype, ws):
+    """Σ over ranks of the payload (and every partial sum) is an exact integer in the dtype."""
+    shape = (37, 70)
+    acc = torch.zeros(shape, dtype=dtype)
+    for r in range(ws):
+        p = V.payload(shape, r, 1, ws, dtype, torch.device("cpu"))
+        assert p.abs().max() <= V.payload_half(ws)
+        acc = acc + p  # rounded in the dtype at every step, like a ring reduction
+    assert torch.equal(acc, V.expected_sum(shape, 1, ws, dtype, torch.device("cpu")))
+
+
+def test_payload_blocks_differ_between_ranks_and_seeds():
+    dev = torch.device("cpu")
+    blocks = [V.payload((8, 16), r, 1, 8, torch.bfloat16, dev) for r in range(8)]
+    for i in range(8):
+        for j in range(i + 1, 8):
+            assert not torch.equal(blocks[i], blocks[j])
+    assert not torch.equal(V.payload((8, 16), 0, 1, 8, torch.float32, dev),
+                           V.payload((8, 16), 0, 2, 8, torch.float32, dev))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32, torch.float8_e4m3fn])
+def test_digest_is_exact_and_position_sensitive(dtype):
+    x = torch.randn(300, 129).to(dtype)
+    d = V.digest(x)
+    assert d == V.digest(x.clone())
+    y = x.clone()
+    y.view(-1)[1234] = (float(y.view(-1)[1234].float()) + 1.0) * 2.0
+    assert V.digest(y) != d
+    # swapping two distinct elements moves the weights: a permuted block is caught
+    z = x.clone().view(-1)
+    i, j = 5, 77
+    if float(z[i].float()) != float(z[j].float()):
+        z[i], z[j] = x.view(-1)[j], x.view(-1)[i]
+        assert V.digest(z.view_as(x)) != d
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32, torch.float8_e4m3fn])
+def test_flip_sign_is_exact_negation(dtype):
+    x = torch.randn(64, 33).to(dtype)
+    y = V.flip_sign_(x.clone())
+    assert torch.equal(y.float(), -x.float())
+    assert torch.equal(V.flip_sign_(y).float(), x.float())
+
+
+def test_ref_rows_and_sample_rows():
+    A, B = torch.randn(100, 50), torch.randn(50, 9000)
+    rows = V.sample_rows(100)
+    assert rows[0] == 0 and rows[-1] == 99 and len(rows) == 24
+    ref = V.ref_rows(A, B, rows)
+    assert torch.allclose(ref, (A @ B)[rows], atol=1e-4)
+    assert V.rows_error(V.rows_of(A @ B, rows), ref) < 1e-6
+    assert V.rows_error(V.rows_of(-(A @ B), rows), ref) > 1.0  # a sign-flipped (stale) block
+
+
+# ---- pick_collective's gate ---------------------------------------------------------------
+def _pick_worker(rank, ws, port, outdir, corrupt):
+    from pytorch_distributed_matmul_benchmark_amd.parallel import overlap as O
+    from pytorch_distributed_matmul_benchmark_amd.parallel.dist import DistContext
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    ctx = DistContext(rank=rank, world_size=ws, local_rank=rank, device=torch.device("cpu"),
+                      backend="gloo")
+
+    def damage(impl, res):  # rank 1 sees a wrong result from the corrupted candidates
+        if rank == 1 and impl in corrupt:
+            res.view(-1)[3] += 1
+
+    res = {}
+    for kind, t in (("all_reduce", torch.zeros(64, 33, dtype=torch.bfloat16)),
+                    ("all_gather", torch.zeros(16, 40, dtype=torch.float32))):
+        try:
+            impl, _, times = O.pick_collective(ctx, kind, t, [], reps=1, _test_corrupt=damage)
+            res[kind] = {"impl": impl, "times": times}
+        except RuntimeError as e:
+            res[kind] = {"error": str(e)}
+    with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
+        json.dump(res, f)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("corrupt", [[], ["direct"], ["rccl"], ["rccl", "direct"]])
+def test_pick_collective_drops_a_wrong_candidate(corrupt, tmp_path):
+    ws = 3
+    mp.spawn(_pick_worker, args=(ws, free_port(), str(tmp_path), corrupt), nprocs=ws, join=True)
+    res = [json.load(open(tmp_path / f"r{r}.json")) for r in range(ws)]
+    assert len({json.dumps(r, sort_keys=True, default=str).replace(" ", "") for r in
+                [{k: v.get("impl", v.get("error")) for k, v in x.items()} for x in res]}) == 1
+    for r in res:
+        for kind in ("all_reduce", "all_gather"):
+            got = r[kind]
+            if len(corrupt) == 2:
+                assert "error" in got and "ran correctly" in got["error"]
+                continue
+            assert got["impl"] not in corrupt
+            for impl in ("rccl", "direct"):
+                if impl in corrupt:
+                    assert got["times"][impl] == "wrong"
+                else:
+                    assert isinstance(got["times"][impl], float) and got["times"][impl] > 0
+
+
+# ---- bench.py's per-mode check --------------------------------------------------------------
+def _bench_module():
+    spec = importlib.util.spec_from_file_location("pdmb_bench_main", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+CASES = [("independent", False), ("batch_parallel", False), ("batch_parallel", True),
+         ("matrix_parallel", False), ("matrix_parallel", True)]
+
+
+def _check_worker(rank, ws, port, outdir, how, chunks):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(ws), LOCAL_RANK=str(rank))
+    bench = _bench_module()
+    ctx = bench.setup_distributed("cpu", timeout_s=120)
+    a = bench.build_parser().parse_args(["--device", "cpu", "--size", "96", "--chunks", str(chunks),
+                                         "--extra-steps", "1"])
+    if how == "stale":
+        # the check step's collective silently does nothing: the outputs still
+        # hold the previous (un-negated) step's data, or no peer's contribution
+        real_ar, real_ag, real_verify = bench.all_reduce_now, bench.all_gather_now, bench.Workload.verify
+        state = {"on": False}
+        bench.all_reduce_now = lambda *x, **k: None if state["on"] else real_ar(*x, **k)
+        bench.all_gather_now = lambda *x, **k: None if state["on"] else real_ag(*x, **k)
+
+        def verify(self):
+            state["on"] = True
+            try:
+                return real_verify(self)
+            finally:
+                state["on"] = False
+        bench.Workload.verify = verify
+    out = {}
+    for mode, ov in CASES:
+        if how == "stale" and (ov or mode == "independent"):
+            continue  # the stale switch covers the serialized collectives
+        v, el, info = bench._measure(a, ctx, mode, ov, 1, 2, mode + ("+overlap" if ov else ""),
+                                     test_corrupt_rank=1 if how == "corrupt" else None)
+        out[f"{mode}{'+overlap' if ov else ''}"] = {"check": info["check"],
+                                                    "detail": info["check_detail"]}
+    with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
+        json.dump(out, f)
+    bench.cleanup_distributed()
+
+
+@pytest.mark.parametrize("how,ws,chunks", [("honest", 2, 0), ("honest", 3, 2), ("corrupt", 2, 0),
+                                           ("corrupt", 3, 2), ("stale", 2, 0)])
+def test_bench_mode_check(how, ws, chunks, tmp_path):
+    mp.spawn(_check_worker, args=(ws, free_port(), str(tmp_path), how, chunks), nprocs=ws, join=True)
+    res = [json.load(open(tmp_path / f"r{r}.json")) for r in range(ws)]
+    for r in res:
+        assert {k: v["check"] for k, v in r.items()} == {k: v["check"] for k, v in res[0].items()}
+    want = "pass" if how == "honest" else "fail"
+    for key, v in res[0].items():
+        assert v["check"] == want, (key, v)
+    if how == "stale":
+        assert set(res[0]) == {"batch_parallel", "matrix_parallel"}
+
+
+def test_bench_line_nulls_a_failed_mode(monkeypatch):
+    """main(): a mode whose check fails reports value null (and no efficiency)."""
+    import subprocess
+    import sys
+
+    code = f"""
+import runpy, sys
+sys.path.insert(0, {ROOT!r})
+import importlib.util
+spec = importlib.util.spec_from_file_location("b", {os.path.join(ROOT, 'bench.py')!r})
+b = importlib.util.module_from_spec(spec); spec.loader.exec_module(b)
+real = b.Workload.verify
+def verify(self):
+    r = real(self)
+    if self.mode == "matrix_parallel":
+        r = dict(r, check="fail")
+    return r
+b.Workload.verify = verify
+sys.argv = ["bench.py", "--device", "cpu", "--size", "64", "--steps", "1", "--warmup", "0",
+            "--extra-steps", "1", "--extra-warmup", "0"]
+sys.exit(b.main())
+"""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       cwd="/tmp", env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["check"] == "pass" and d["value"] > 0
+    assert d["modes"]["matrix_parallel"]["value"] is None
+    assert d["modes"]["matrix_parallel"]["scaling_efficiency"] is None
+    assert d["modes"]["batch_parallel"]["value"] > 0 and d["modes"]["batch_parallel"]["check"] == "pass"
