@@ -637,10 +637,17 @@ def _self_launch(a) -> int:
     return subprocess.call(cmd, env=env)
 
 
+_T0 = time.perf_counter()
+
+
 def _phase(ctx, key: str, phase: str) -> None:
-    """Diagnostics (PDMB_BENCH_TRACE=1): each rank's mode / phase on stderr."""
+    """Diagnostics (PDMB_BENCH_TRACE=1): each rank's mode / phase on stderr,
+    with the seconds since start and this rank's peak device memory so far."""
     if os.environ.get("PDMB_BENCH_TRACE") == "1":
-        print(f"[rank {ctx.rank}] {key}: {phase}", file=sys.stderr, flush=True)
+        mem = (f" peak {torch.cuda.max_memory_allocated(ctx.device) / 2**30:.2f} GiB"
+               if ctx.device.type == "cuda" else "")
+        print(f"[rank {ctx.rank} +{time.perf_counter() - _T0:.1f}s] {key}: {phase}{mem}",
+              file=sys.stderr, flush=True)
 
 
 def _fault(ctx, key: str, phase: str) -> None:

@@ -42,6 +42,26 @@ hipError_t gemm_tile_launch(int kernel, int dt, GemmArgs a, hipStream_t stream);
 
 static unsigned long long* g_debug_buffer = nullptr;
 
+// The planner's A/B switches (PDMB_SPLIT3, PDMB_T192, PDMB_TILE_TAIL, ...:
+// each names one rule below and the measurement behind it). They are read
+// ONLY in a PDMB_EXPERIMENTS=1 build, where scripts/ab_kernels.py flips them
+// per call to price a rule against its absence. The shipping build ignores
+// the environment: every rule is fixed at its shipped value, so a plan
+// depends on the shape, layout, dtype and CU budget alone
+// (tests/test_golden_plans_cpu.py pins the reference shapes' plans).
+// ab_switch(name) = the variable's integer value, or -1 when it is unset
+// (always -1 in the shipping build).
+static int ab_switch(const char* name) {
+#ifdef PDMB_EXPERIMENTS
+  const char* e = std::getenv(name);
+  return e && e[0] ? std::atoi(e) : -1;
+#else
+  (void)name;
+  return -1;
+#endif
+}
+static bool ab_off(const char* name) { return ab_switch(name) == 0; }  // "=0 leaves the rule out"
+
 void set_debug_buffer(void* p) { g_debug_buffer = (unsigned long long*)p; }
 
 // The problem's shape / layout fields only (the planner's supports() checks:
@@ -84,10 +104,8 @@ static GemmArgs to_args(const Problem& p) {
   a.kb = p.kb > 0 && p.kb < p.K ? p.kb : p.K;
   a.dbg = g_debug_buffer;
   a.alpha = p.alpha;
-  {  // read per launch, so an in-process A/B can flip it (scripts/ab_kernels.py)
-    const char* e = std::getenv("PDMB_SPLITK_PREFETCH");
-    a.meet_prefetch = (e && e[0] == '0') ? 0 : 1;
-  }
+  // read per launch, so an in-process A/B can flip it (scripts/ab_kernels.py)
+  a.meet_prefetch = ab_off("PDMB_SPLITK_PREFETCH") ? 0 : 1;
   if (p.sig) {
     a.sig = p.sig->dev;
     a.sig_host = p.sig->host_dev;
@@ -382,28 +400,18 @@ static bool w4s_auto(const Problem& p) {
 // (plan_uncached takes it there from 3 slices per CU: PDMB_F32X2SPLIT=0 turns
 // that off, A/B, read per call).
 static bool t64x2_full_on() {  // PDMB_F32T64X2_FULL=0: f32_t64x2 only on the small grids (A/B)
-  const char* e = std::getenv("PDMB_F32T64X2_FULL");
-  return !(e && std::atoi(e) == 0);
+  return !ab_off("PDMB_F32T64X2_FULL");
 }
 static constexpr double kF32X2AloneKt = 1.9;
-static bool f32x2_split_on() {
-  const char* e = std::getenv("PDMB_F32X2SPLIT");
-  return !(e && std::atoi(e) == 0);
-}
+static bool f32x2_split_on() { return !ab_off("PDMB_F32X2SPLIT"); }
 static bool f32x2_split_grid(const Problem& p, const KernelModel& m, int S, long long T) {
   if (m.kernel == kF32T64x2) return S > 1;  // any grid (its plans date from this model)
   return m.kernel == kF32T128x2 && S > 1 && T < 2LL * (p.cus > 0 ? p.cus : device_cus()) && f32x2_split_on();
 }
 
-static bool split3_small_on() {
-  const char* e = std::getenv("PDMB_SPLIT3_SMALL");
-  return !(e && std::atoi(e) == 0);
-}
+static bool split3_small_on() { return !ab_off("PDMB_SPLIT3_SMALL"); }
 static constexpr double kSlotLatUs = 4.5;
-static bool split_slot_lat_on() {
-  const char* e = std::getenv("PDMB_SPLIT_SLOT_LAT");
-  return !(e && std::atoi(e) == 0);
-}
+static bool split_slot_lat_on() { return !ab_off("PDMB_SPLIT_SLOT_LAT"); }
 
 // Model time (us) of `kernel` over T of the problem's tiles (T < 0: all of
 // them), each split S ways along K.
@@ -478,15 +486,20 @@ static bool is_t192(int k) { return k == kT192 || k == kT192x128 || k == kFp8T19
 
 // ---- planner memo -------------------------------------------------------------
 // plan() and tail_plan() are pure functions of the problem's shape and layout,
-// the CU budget, the requested kernel and the A/B switches in the environment.
+// the CU budget, the requested kernel and (experiments build only) the A/B
+// switches in the environment.
 // One GEMM call asks them several times (resolve, split, workspace size,
 // launch, and tail_plan's own sub-plans): ~8 us of host time per call at
 // 1024^3 on the GPU box's host (profiles/r7w_host_overhead.jsonl). Per-thread
-// memo keyed by exactly those inputs; the environment enters as a hash of
-// every PDMB_* variable (one pass over environ), so a switch flipped between
-// calls (scripts/ab_kernels.py arms, tests) takes effect at once.
+// memo keyed by exactly those inputs; in a PDMB_EXPERIMENTS=1 build the
+// environment enters as a hash of every PDMB_* variable (one pass over
+// environ), so a switch flipped between calls (scripts/ab_kernels.py arms)
+// takes effect at once; the shipping build hashes nothing.
 extern "C" char** environ;
 static uint64_t pdmb_env_hash() {
+#ifndef PDMB_EXPERIMENTS
+  return 0;  // the shipping planner reads no environment (ab_switch)
+#else
   uint64_t h = 1469598103934665603ull;
   for (char** e = environ; e && *e; ++e) {
     const char* v = *e;
@@ -495,6 +508,7 @@ static uint64_t pdmb_env_hash() {
     h = (h ^ 0xffu) * 1099511628211ull;
   }
   return h;
+#endif
 }
 struct MemoKey {
   int what, kernel, dtype, M, N, K, lda, ldb, ldc, batch, splitk, cus, kb, sig, dev_cus;
@@ -584,17 +598,13 @@ static Plan plan_uncached(const Problem& p, int kernel) {
   double ac = 1e300;
   static const int kS0[] = {1, 2, 4, 8}, kS1[] = {3, 5, 6};
   // PDMB_SPLIT3=0 (read per call; A/B): auto leaves the 3-way split out
-  const char* s3env = std::getenv("PDMB_SPLIT3");
-  const bool no3 = s3env && std::atoi(s3env) == 0;
+  const bool no3 = ab_off("PDMB_SPLIT3");
   // PDMB_T192=0 (read per call; A/B): auto leaves the 192-row tiles out
-  const char* t192env = std::getenv("PDMB_T192");
-  const bool no192 = kernel == kAuto && t192env && std::atoi(t192env) == 0;
+  const bool no192 = kernel == kAuto && ab_off("PDMB_T192");
   // PDMB_F32T64=0 (read per call; A/B): auto leaves the 64x128 fp32 tile out
-  const char* t64env = std::getenv("PDMB_F32T64");
-  const bool no64 = kernel == kAuto && t64env && std::atoi(t64env) == 0;
+  const bool no64 = kernel == kAuto && ab_off("PDMB_F32T64");
   // PDMB_F32T64X2=0 (read per call; A/B): auto leaves f32_t64x2 out
-  const char* t64x2env = std::getenv("PDMB_F32T64X2");
-  const bool t64x2_on = !(t64x2env && std::atoi(t64x2env) == 0);
+  const bool t64x2_on = !ab_off("PDMB_F32T64X2");
   for (int pass = 0; pass < 2; ++pass)
   for (const KernelModel& m : kModels) {
     if (kernel != kAuto && kernel != m.kernel) continue;
@@ -625,8 +635,7 @@ static Plan plan_uncached(const Problem& p, int kernel) {
       // on 5 more f32_t64 grids: +1.5 to +20 %, r7af_f32_planner_confirm_settled.jsonl).
       // PDMB_SPLIT8=0 leaves it out.
       if ((S == 5 || S == 6 || (S == 8 && m.kernel == kF32T64)) && p.splitk != S) {
-        const char* e56 = std::getenv(S == 8 ? "PDMB_SPLIT8" : "PDMB_SPLIT56");
-        if ((e56 && std::atoi(e56) == 0) || m.cls != 2 || (ktiles(p) + S - 1) / S < 32 || m.kernel == kF32W4)
+        if (ab_off(S == 8 ? "PDMB_SPLIT8" : "PDMB_SPLIT56") || m.cls != 2 || (ktiles(p) + S - 1) / S < 32 || m.kernel == kF32W4)
           continue;
       } else if (S > 4 && p.splitk != S) {
         continue;
@@ -796,8 +805,7 @@ struct TailPlan {
 // PDMB_TILE_TAIL=0 disables it (A/B).
 static TailPlan f32_tail_plan(const Problem& p) {
   TailPlan best;
-  const char* env = std::getenv("PDMB_TILE_TAIL");
-  if (env && std::atoi(env) == 0) return best;
+  if (ab_off("PDMB_TILE_TAIL")) return best;
   if (!supports(p, kF32T128) || !supports(p, kF32T128x2)) return best;
   const Plan whole = plan(p, kAutoNoT64x2Full);  // the best single launch (possibly split: 5120^3 ran f32_t128 x 2)
   if (whole.kernel != kF32T128x2 && whole.kernel != kF32T128) return best;
@@ -872,13 +880,11 @@ static TailPlan tail_plan_uncached(const Problem& p, int kernel) {
   {  // tile-range form: whole waves, then the rest split S ways
     // PDMB_TILE_TAIL (read per call, A/B): 0 = off; 2 / 4 / 8 = only that S, priced
     // as if free (forced wherever the form is feasible)
-    const char* env = std::getenv("PDMB_TILE_TAIL");
-    int force = env ? std::atoi(env) : -1;
+    int force = ab_switch("PDMB_TILE_TAIL");
     if (force != 0 && force != 2 && force != 4 && force != 8) force = -1;
     const long long T = (long long)tm * tn * batch;
     const int nk = ktiles(p);
-    const char* renv = std::getenv("PDMB_TAIL_REFINE");
-    const int rforce = renv ? std::atoi(renv) : -1;
+    const int rforce = ab_switch("PDMB_TAIL_REFINE");
     const bool fp8 = p.dtype == kFP8;
     for (long long dp = slots; dp < T && force != 0; dp += slots) {
       const long long rest = T - dp;
@@ -915,8 +921,7 @@ static TailPlan tail_plan_uncached(const Problem& p, int kernel) {
   // Stream-K (fp8, gemm_fp8_sk; PDMB_STREAMK=1 / 2 force it, read per call — A/B
   // until priced): the last 1-2 waves' tiles as G even shares of K-tiles.
   if (p.dtype == kFP8) {
-    const char* senv = std::getenv("PDMB_STREAMK");
-    const int mode = senv ? std::atoi(senv) : 0;
+    const int mode = ab_switch("PDMB_STREAMK");
     if ((mode == 1 || mode == 2) && device_cus() % 8 == 0) {
       const long long T = (long long)tm * tn * batch;
       const int nk = ktiles(p);
@@ -1365,8 +1370,7 @@ size_t gemm_workspace_bytes(const Problem& p, int kernel) {
 // wherever it fits, the round-3 rule.
 static bool fp8_dp_streams(const GemmArgs& d, long long tiles_dp) {
   if (!gemm_fp8_w4s_fits(d) || device_cus() % 8 != 0) return false;
-  const char* env = std::getenv("PDMB_TAIL_DP_W4S");
-  if (env && std::atoi(env) == 1) return true;
+  if (ab_switch("PDMB_TAIL_DP_W4S") == 1) return true;
   return tiles_dp >= 2LL * device_cus();
 }
 

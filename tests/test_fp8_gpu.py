@@ -317,10 +317,11 @@ def test_fp8_tile_family_edge_tiles(kernel, M, N, K, splitk):
     assert torch.isnan(big[:, N:]).all() and torch.isnan(big[M:]).all()
 
 
+@pytest.mark.experiments
 @pytest.mark.parametrize("M,N,K,form", [(6144, 6144, 6144, None), (6000, 6000, 6144, None),
                                         (7168, 7168, 1024, None), (7168, 7168, 7168, None),
                                         (6144, 6144, 6144, "rows"), (6000, 6000, 6144, "rows")])
-def test_fp8_wave_tail_split(M, N, K, form, monkeypatch):
+def test_fp8_wave_tail_split(M, N, K, form, monkeypatch):  # forced forms: experiments build
     """fp8 wave-quantisation tail (gemm_dispatch.cpp tail_plan on fp8 W4): the
     whole waves as one fp8 W4 / W4S launch — whole tile rows, or (tile-range
     form) the first k x 256 tiles of the tile order — and the rest split-K in a
@@ -358,6 +359,7 @@ SK_SHAPES = [(1, 5120, 5120, 5120), (1, 4608, 4608, 3072), (1, 6000, 5888, 3072)
              (1, 7168, 7168, 1024), (2, 2560, 2560, 5120), (1, 3072, 3072, 8192)]
 
 
+@pytest.mark.experiments
 # mode 2 on 7168^2 x 1024 is not generated: 16 tiles left after the whole
 # waves, fewer K-tiles than workgroups per XCD
 @pytest.mark.parametrize("shape,mode", [(s, m) for m in ("1", "2") for s in SK_SHAPES

@@ -510,6 +510,11 @@ def test_tile_family_edge_tiles_masked(kernel, M, N, K, splitk):
     assert torch.isnan(big[:, N:]).all() and torch.isnan(big[M:]).all()
 
 
+# Forced tail forms (PDMB_TILE_TAIL / PDMB_TAIL_REFINE / PDMB_T192): the
+# planner reads those A/B switches only in a PDMB_EXPERIMENTS=1 build, so these
+# run there; test_shipping_tail_plans_exact covers the tails the shipping
+# planner chooses by itself.
+@pytest.mark.experiments
 @pytest.mark.parametrize("M,N,K,form", [(6000, 6000, 6144, "tiles"), (10000, 10000, 10048, "tiles"),
                                         (6144, 6144, 6144, "tiles"), (7168, 7168, 7168, "tiles"),
                                         (6000, 6000, 6144, "rows"), (10000, 10000, 10048, "rows"),
@@ -577,6 +582,7 @@ REFINED_SHAPES = [(6144, 6144, 6144, 2), (6000, 6000, 6144, 2), (4608, 4608, 307
                   (6144, 4096, 4096, 2), (3000, 7000, 5056, 2)]
 
 
+@pytest.mark.experiments  # PDMB_TAIL_REFINE=R forces the form (experiments build)
 @pytest.mark.parametrize("dtype,M,N,K,R", [(d,) + s for d in ("bfloat16", "float16", "float8_e4m3fn")
                                            for s in REFINED_SHAPES
                                            if not (d == "float8_e4m3fn" and s[2] % 128)])  # fp8: K % 128
@@ -1185,6 +1191,7 @@ def test_t192_is_auto_on_one_wave_grids():
     assert gemm.kernel_for(*mk(16384, 16384, 16384)) == "pdmb_w4s"
 
 
+@pytest.mark.experiments  # PDMB_SPLITK_PREFETCH=0: the experiments build reads it
 @pytest.mark.parametrize("kernel,M,N,K,dt", [("t128", 1024, 1024, 4096, "bfloat16"), ("t128", 700, 264, 2048, "bfloat16"),
                                             ("f32_t128", 1000, 1052, 4096, "float32"),
                                             ("f32_t64", 700, 300, 2048, "float32")])
@@ -1206,3 +1213,38 @@ def test_split3_prefetch_bitwise(kernel, M, N, K, dt, monkeypatch):
     Bi = torch.randint(-3, 4, (K, N), device="cuda", generator=g).to(d)
     C = gemm.matmul(Ai, Bi, kernel=kernel, splitk=3)
     assert torch.equal(C.double(), (Ai.double() @ Bi.double()).to(d).double())
+
+
+# The wave-quantisation tails the SHIPPING planner picks by itself (refined
+# halves / quarters for bf16 / fp16 / fp8; the split f32_t128 tail for exact
+# fp32), batched grids included: exact on small integers, nothing written
+# outside C.
+SHIPPING_TAILS = [("bfloat16", 1, 6144, 6144, 6144), ("bfloat16", 2, 6144, 6144, 6144),
+                  ("bfloat16", 1, 6000, 6000, 6144), ("bfloat16", 1, 4608, 4608, 3072),
+                  ("bfloat16", 1, 3000, 7000, 5056), ("float16", 2, 6000, 5888, 3072),
+                  ("float16", 1, 7168, 7168, 1024), ("float8_e4m3fn", 1, 6144, 6144, 6144),
+                  ("float8_e4m3fn", 1, 6000, 6000, 6144), ("float8_e4m3fn", 2, 6000, 5888, 3072),
+                  ("float32", 1, 5120, 5120, 5120), ("float32", 1, 3072, 3072, 3072),
+                  ("float32", 1, 6000, 5888, 3072), ("float32", 2, 4608, 4608, 3072)]
+
+
+@pytest.mark.parametrize("dtype,b,M,N,K", SHIPPING_TAILS)
+def test_shipping_tail_plans_exact(dtype, b, M, N, K):
+    dt = getattr(torch, dtype)
+    fp8 = dt == gemm.FP8
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + b)
+    lo, hi = (-2, 3) if fp8 else (-3, 4)
+    Af = torch.randint(lo, hi, (b, M, K), device="cuda", generator=g).float()
+    Bf = torch.randint(lo, hi, (b, K, N), device="cuda", generator=g).float()
+    A = Af.to(dt)
+    B = Bf.transpose(-1, -2).contiguous().to(dt).transpose(-1, -2) if fp8 else Bf.to(dt)
+    if b == 1:
+        A, B, Af, Bf = A[0], B[0], Af[0], Bf[0]
+    odt = gemm.out_dtype(dt)
+    big = torch.full((b, M + 16, N + 24), float("nan"), device="cuda", dtype=odt)
+    out = big[:, :M, :N] if b > 1 else big[0, :M, :N]
+    m1, S, t1, r = gemm.tail_split_for(A, B, out)
+    assert t1 > 0 and m1 == 0 and (r > 1 or S > 1), (m1, S, t1, r)  # a tail is planned
+    gemm.matmul(A, B, out=out)
+    assert torch.equal(out, torch.matmul(Af.double(), Bf.double()).to(odt))
+    assert torch.isnan(big[..., N:]).all() and torch.isnan(big[:, M:]).all()

@@ -19,6 +19,16 @@ def C():
         pytest.skip(f"native extension not built: {e}")
 
 
+def ab(C, monkeypatch, name, value) -> bool:
+    """Set one of the planner's A/B switches; True if this build reads it. Only
+    a PDMB_EXPERIMENTS=1 build does (gemm_dispatch.cpp ab_switch): in the
+    shipping build the rule stays on, so the "switch off" halves below run
+    on experiment builds only (tests/test_golden_plans_cpu.py checks that the
+    shipping build ignores every switch)."""
+    monkeypatch.setenv(name, value)
+    return bool(C.EXPERIMENTS)
+
+
 def plan(C, dt, M, N, K, b=1, kernel=0, cus=0):
     k, S, cost, m1, tS, t1, r = C.plan_shape(dt, M, N, K, b, kernel, cus)
     return C.kernel_name(k), S, cost, (m1, tS, t1, r)
@@ -110,15 +120,15 @@ def test_refined_tail_plans(C, monkeypatch):
     assert plan(C, FP8, 6144, 6144, 6144)[3] == (0, 1, 512, 4)
     assert plan(C, FP8, 4608, 4608, 3072)[3] == (0, 1, 256, 2)
     assert plan(C, BF16, 16384, 16384, 16384)[3] == (0, 1, 0, 1)  # whole waves: one launch
-    monkeypatch.setenv("PDMB_TAIL_REFINE", "0")
-    k, _, _, (m1, S, t1, r) = plan(C, BF16, 6144, 6144, 6144)
-    # without the refined tail: the split-K tail over W4, or (round 5) one
-    # launch of 192x192 tiles — 6144^3 is exactly 4 waves of them
-    assert r == 1 and ((S > 1 and (m1 > 0 or t1 > 0)) or (k == "pdmb_t192_nn" and (m1, t1) == (0, 0)))
-    monkeypatch.delenv("PDMB_TAIL_REFINE")
-    monkeypatch.setenv("PDMB_STREAMK", "1")
-    m1, S, t1, r = plan(C, FP8, 5120, 5120, 5120)[3]
-    assert (m1, t1, r) == (0, 0, 0) and S == 2
+    if ab(C, monkeypatch, "PDMB_TAIL_REFINE", "0"):
+        k, _, _, (m1, S, t1, r) = plan(C, BF16, 6144, 6144, 6144)
+        # without the refined tail: the split-K tail over W4, or (round 5) one
+        # launch of 192x192 tiles — 6144^3 is exactly 4 waves of them
+        assert r == 1 and ((S > 1 and (m1 > 0 or t1 > 0)) or (k == "pdmb_t192_nn" and (m1, t1) == (0, 0)))
+        monkeypatch.delenv("PDMB_TAIL_REFINE")
+        monkeypatch.setenv("PDMB_STREAMK", "1")
+        m1, S, t1, r = plan(C, FP8, 5120, 5120, 5120)[3]
+        assert (m1, t1, r) == (0, 0, 0) and S == 2
 
 
 def test_f32_tail_plans(C, monkeypatch):
@@ -131,8 +141,8 @@ def test_f32_tail_plans(C, monkeypatch):
     assert plan(C, F32, 3072, 3072, 3072)[3] == (0, 4, 512, 1)
     assert plan(C, F32, 16384, 16384, 16384)[3] == (0, 1, 0, 1)
     assert plan(C, F32, 6144, 6144, 6144)[3] == (0, 1, 0, 1)   # last wave half full: no split pays
-    monkeypatch.setenv("PDMB_TILE_TAIL", "0")
-    assert plan(C, F32, 5120, 5120, 5120)[3] == (0, 1, 0, 1)
+    if ab(C, monkeypatch, "PDMB_TILE_TAIL", "0"):
+        assert plan(C, F32, 5120, 5120, 5120)[3] == (0, 1, 0, 1)
 
 
 def test_plan_report_script(C, monkeypatch):
@@ -174,9 +184,9 @@ def test_t192_plans(C, monkeypatch):
     assert plan(C, FP8, 3072, 3072, 3072)[0] == "pdmb_fp8_t192_nt"
     assert plan(C, BF16, 16384, 16384, 16384)[0] == "pdmb_w4s"
     assert plan(C, BF16, 8192, 8192, 8192)[0] == "pdmb_w4s"
-    monkeypatch.setenv("PDMB_T192", "0")
-    assert "192" not in plan(C, BF16, 3072, 3072, 3072)[0]
-    assert "192" not in plan(C, FP8, 2304, 2304, 4096)[0]
+    if ab(C, monkeypatch, "PDMB_T192", "0"):
+        assert "192" not in plan(C, BF16, 3072, 3072, 3072)[0]
+        assert "192" not in plan(C, FP8, 2304, 2304, 4096)[0]
 
 
 def test_t192x128_multi_wave_rate(C, monkeypatch):
@@ -207,27 +217,27 @@ def test_split3_plans(C, monkeypatch):
     256^2 fp32 tile): measured ahead on these grids (profiles/r7r_split3_ab_*.jsonl),
     left out where it lost (bf16 1024^2 x 4096, fp32 2560 x 2048 x 4096)."""
     monkeypatch.delenv("PDMB_SPLIT3", raising=False)
-    monkeypatch.setenv("PDMB_F32T64X2", "0")  # (f32_t64x2 takes 1536^2 x 4096 since)
     assert plan(C, BF16, 2560, 4096, 16384)[:2] == ("pdmb_w4_nn", 3)
     assert plan(C, BF16, 5120, 2048, 16384)[:2] == ("pdmb_w4_nn", 3)
-    assert plan(C, F32, 2560, 256, 8192)[1] == 3
-    assert plan(C, F32, 1536, 1536, 4096)[1] == 3
     assert plan(C, BF16, 1024, 1024, 4096)[1] != 3
-    assert plan(C, F32, 2560, 2048, 4096)[1] != 3
-    monkeypatch.setenv("PDMB_SPLIT3", "0")
-    assert plan(C, BF16, 2560, 4096, 16384)[1] != 3
+    if ab(C, monkeypatch, "PDMB_F32T64X2", "0"):  # (f32_t64x2 takes 1536^2 x 4096 since)
+        assert plan(C, F32, 2560, 256, 8192)[1] == 3
+        assert plan(C, F32, 1536, 1536, 4096)[1] == 3
+        assert plan(C, F32, 2560, 2048, 4096)[1] != 3
+        monkeypatch.setenv("PDMB_SPLIT3", "0")
+        assert plan(C, BF16, 2560, 4096, 16384)[1] != 3
 
 
 def test_split56_fp32_only(C, monkeypatch):
     """Round 5: 5- / 6-way splits for exact fp32 only (measured ahead on six
     fp32 grids, mixed on bf16; profiles/r7u_split56_ab_*.jsonl)."""
     monkeypatch.delenv("PDMB_SPLIT56", raising=False)
-    monkeypatch.setenv("PDMB_SPLIT8", "0")  # (8 ways takes the first grid since, test_split8_*)
-    assert plan(C, F32, 1024, 256, 16384)[1] in (5, 6)
     assert plan(C, F32, 512, 6400, 16384)[1] in (5, 6)
     assert plan(C, BF16, 2560, 256, 16384)[1] not in (5, 6)
-    monkeypatch.setenv("PDMB_SPLIT56", "0")
-    assert plan(C, F32, 1024, 256, 16384)[1] not in (5, 6)
+    if ab(C, monkeypatch, "PDMB_SPLIT8", "0"):  # (8 ways takes the first grid since, test_split8_*)
+        assert plan(C, F32, 1024, 256, 16384)[1] in (5, 6)
+        monkeypatch.setenv("PDMB_SPLIT56", "0")
+        assert plan(C, F32, 1024, 256, 16384)[1] not in (5, 6)
 
 
 def test_split8_fp32_only(C, monkeypatch):
@@ -241,8 +251,8 @@ def test_split8_fp32_only(C, monkeypatch):
     for dt in (BF16, FP8):
         for shape in ((1024, 256, 16384), (256, 256, 16384), (2048, 1024, 16384)):
             assert plan(C, dt, *shape)[1] != 8, (dt, shape)
-    monkeypatch.setenv("PDMB_SPLIT8", "0")
-    assert plan(C, F32, 1024, 256, 16384)[1] != 8
+    if ab(C, monkeypatch, "PDMB_SPLIT8", "0"):
+        assert plan(C, F32, 1024, 256, 16384)[1] != 8
 
 
 def test_f32_x2_split_on_small_grids(C, monkeypatch):
@@ -253,17 +263,17 @@ def test_f32_x2_split_on_small_grids(C, monkeypatch):
     split (the launch re-plans with the kernel fixed); PDMB_F32X2SPLIT=0 turns
     it off."""
     monkeypatch.delenv("PDMB_F32X2SPLIT", raising=False)
-    monkeypatch.setenv("PDMB_F32T64X2", "0")  # (f32_t64x2 takes 2560 x 2048 x 4096 since)
-    assert plan(C, F32, 2560, 2048, 4096)[:2] == ("pdmb_f32_t128x2_nn", 4)
-    assert plan(C, F32, 2560, 2048, 4096, kernel=53)[:2] == ("pdmb_f32_t128x2_nn", 4)
-    for shape in ((4096, 1024, 4096), (2048, 2048, 2048), (1536, 1536, 4096), (768, 9216, 4096),
-                  (512, 12288, 4096), (1536, 5120, 4096), (2560, 512, 8192)):
-        k, S, _, _ = plan(C, F32, *shape)
-        tiles = -(-shape[0] // 128) * -(-shape[1] // 128)
-        if k == "pdmb_f32_t128x2_nn" and tiles < 512:
-            assert S > 1 and tiles * S >= 768, (shape, S)
-    monkeypatch.setenv("PDMB_F32X2SPLIT", "0")
-    assert plan(C, F32, 2560, 2048, 4096)[0] == "pdmb_f32_t128_nn"
+    if ab(C, monkeypatch, "PDMB_F32T64X2", "0"):  # (f32_t64x2 takes 2560 x 2048 x 4096 since)
+        assert plan(C, F32, 2560, 2048, 4096)[:2] == ("pdmb_f32_t128x2_nn", 4)
+        assert plan(C, F32, 2560, 2048, 4096, kernel=53)[:2] == ("pdmb_f32_t128x2_nn", 4)
+        for shape in ((4096, 1024, 4096), (2048, 2048, 2048), (1536, 1536, 4096), (768, 9216, 4096),
+                      (512, 12288, 4096), (1536, 5120, 4096), (2560, 512, 8192)):
+            k, S, _, _ = plan(C, F32, *shape)
+            tiles = -(-shape[0] // 128) * -(-shape[1] // 128)
+            if k == "pdmb_f32_t128x2_nn" and tiles < 512:
+                assert S > 1 and tiles * S >= 768, (shape, S)
+        monkeypatch.setenv("PDMB_F32X2SPLIT", "0")
+        assert plan(C, F32, 2560, 2048, 4096)[0] == "pdmb_f32_t128_nn"
 
 
 def test_split_slot_latency_small_bf16_grids(C, monkeypatch):
@@ -277,9 +287,9 @@ def test_split_slot_latency_small_bf16_grids(C, monkeypatch):
         for shape in ((1024, 1024, 8192), (512, 2048, 8192), (768, 768, 8192)):
             assert plan(C, dt, *shape)[:2] == ("pdmb_t128_nn", 3), (dt, shape)
     other = {(F32, s): plan(C, F32, *s)[:2] for s in ((1024, 1024, 8192), (512, 512, 8192))}
-    monkeypatch.setenv("PDMB_SPLIT_SLOT_LAT", "0")
-    assert plan(C, BF16, 1024, 1024, 8192)[:2] == ("pdmb_t128_nn", 4)
-    assert other == {(dt, s): plan(C, dt, *s)[:2] for (dt, s) in other}
+    if ab(C, monkeypatch, "PDMB_SPLIT_SLOT_LAT", "0"):
+        assert plan(C, BF16, 1024, 1024, 8192)[:2] == ("pdmb_t128_nn", 4)
+        assert other == {(dt, s): plan(C, dt, *s)[:2] for (dt, s) in other}
 
 
 def test_split3_small_bf16_grids(C, monkeypatch):
@@ -293,8 +303,8 @@ def test_split3_small_bf16_grids(C, monkeypatch):
     assert plan(C, BF16, 1024, 1024, 4096)[1] != 3  # 64 tiles: mixed, left out
     assert plan(C, FP8, 768, 768, 4096)[1] != 3  # 11 fp8 K-tiles per slice: lost (r7am)
     assert plan(C, FP8, 768, 768, 8192)[:2] == ("pdmb_fp8_t128_nt", 3)  # 22: ahead
-    monkeypatch.setenv("PDMB_SPLIT3_SMALL", "0")
-    assert plan(C, BF16, 768, 768, 4096)[1] != 3
+    if ab(C, monkeypatch, "PDMB_SPLIT3_SMALL", "0"):
+        assert plan(C, BF16, 768, 768, 4096)[1] != 3
 
 
 def test_f32_t64x2_plans(C, monkeypatch):
@@ -313,7 +323,7 @@ def test_f32_t64x2_plans(C, monkeypatch):
     # full grids without a split tail: split 2 ways (r7as), never unsplit
     assert plan(C, F32, 4608, 4608, 4096)[:2] == ("pdmb_f32_t64x2_nn", 2)
     assert plan(C, F32, 3072, 3584, 4096)[1] != 1 or plan(C, F32, 3072, 3584, 4096)[0] != "pdmb_f32_t64x2_nn"
-    monkeypatch.setenv("PDMB_F32T64X2_FULL", "0")
-    assert plan(C, F32, 4608, 4608, 4096)[0] != "pdmb_f32_t64x2_nn"
-    monkeypatch.setenv("PDMB_F32T64X2", "0")
-    assert plan(C, F32, 1536, 3072, 1024)[0] != "pdmb_f32_t64x2_nn"
+    if ab(C, monkeypatch, "PDMB_F32T64X2_FULL", "0"):
+        assert plan(C, F32, 4608, 4608, 4096)[0] != "pdmb_f32_t64x2_nn"
+        monkeypatch.setenv("PDMB_F32T64X2", "0")
+        assert plan(C, F32, 1536, 3072, 1024)[0] != "pdmb_f32_t64x2_nn"
