@@ -721,6 +721,18 @@ static Plan plan_uncached(const Problem& p, int kernel) {
     }
   }
   if (alt.kernel >= 0 && ac < bc * 0.97) best = alt;
+  // f32_t64x2 on a full grid is the newcomer there, so it never wins on the
+  // hysteresis alone: the best plan without it (the 3-way split included)
+  // keeps the grid unless f32_t64x2 is priced strictly cheaper. Round 5 took
+  // 3072 x 3584 x 4096 (and its transpose) from f32_t128x2 x 3 (model 671 us)
+  // to f32_t64x2 x 2 (687 us) because pass 1 needs a 3 % win, and measured
+  // 141.6 vs 144.7 TF (profiles/r7at_f32_t64x2_full_rule_table.txt); the 14
+  // grids it gained on are priced cheaper with it and keep it.
+  if (kernel == kAuto && !no_t64x2_full && best.kernel == kF32T64x2 && p.splitk == 0 &&
+      tiles_of(p, kF32T128x2) >= 2LL * (p.cus > 0 ? p.cus : device_cus())) {
+    const Plan base = plan(p, kAutoNoT64x2Full);
+    if (base.kernel >= 0 && base.cost <= best.cost) best = base;
+  }
   if (best.kernel < 0 && any)  // the requested split is impossible for this K
     for (const KernelModel& m : kModels)
       if ((kernel == kAuto || kernel == m.kernel) && m.cls == dt_class(p) && supports(p, m.kernel))

@@ -323,6 +323,10 @@ def test_f32_t64x2_plans(C, monkeypatch):
     # full grids without a split tail: split 2 ways (r7as), never unsplit
     assert plan(C, F32, 4608, 4608, 4096)[:2] == ("pdmb_f32_t64x2_nn", 2)
     assert plan(C, F32, 3072, 3584, 4096)[1] != 1 or plan(C, F32, 3072, 3584, 4096)[0] != "pdmb_f32_t64x2_nn"
+    # round 6: never on the hysteresis alone — the grids where f32_t128x2 x 3 is
+    # priced cheaper (and measured 2 % ahead, r7at) keep it
+    for shape in ((3072, 3584, 4096), (3584, 3072, 4096), (3072, 3584, 16384)):
+        assert plan(C, F32, *shape)[:2] == ("pdmb_f32_t128x2_nn", 3), shape
     if ab(C, monkeypatch, "PDMB_F32T64X2_FULL", "0"):
         assert plan(C, F32, 4608, 4608, 4096)[0] != "pdmb_f32_t64x2_nn"
         monkeypatch.setenv("PDMB_F32T64X2", "0")
