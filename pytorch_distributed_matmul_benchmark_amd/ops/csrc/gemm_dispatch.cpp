@@ -1618,7 +1618,12 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     }
     return hipSuccess;
   }
-  switch (k) {
+  // One launch of the whole problem: the whole-problem plan's kernel. (k may be
+  // the renamed first launch of a refined tail, resolve_kernel; that tail form
+  // needs no workspace and never declines, but if a tail did, the launch here
+  // is the plan the planner priced, not the renamed kernel. ADVICE r5.)
+  const int kw = resolve_core(p, kernel);
+  switch (kw) {
     case kFp8W4: {
       GemmArgs s = a;
       s.splitk = 1;
@@ -1650,16 +1655,16 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kT192:
     case kT192x128:
     case kFp8T192:
-    case kFp8T192x128: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream);
+    case kFp8T192x128: return tiled_launch(p, kw, a, p.workspace, p.workspace_bytes, stream);
     case kMfmaW4S: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 7);
     case kF32_256s: return gemm_f32_256_launch(a, 1, stream);
     case kF32W4:
-    case kF32T128: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream);
-    case kF32T128x2: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream, 2);
-    case kF32T64: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream, 3);
-    case kF32T64x2: return tiled_launch(p, k, a, p.workspace, p.workspace_bytes, stream, 4);
+    case kF32T128: return tiled_launch(p, kw, a, p.workspace, p.workspace_bytes, stream);
+    case kF32T128x2: return tiled_launch(p, kw, a, p.workspace, p.workspace_bytes, stream, 2);
+    case kF32T64: return tiled_launch(p, kw, a, p.workspace, p.workspace_bytes, stream, 3);
+    case kF32T64x2: return tiled_launch(p, kw, a, p.workspace, p.workspace_bytes, stream, 4);
     default:
-      if (is_experiment(k)) return experiment_launch(p, k, a, stream);
+      if (is_experiment(kw)) return experiment_launch(p, kw, a, stream);
       return gemm_generic_launch(p.dtype, a, generic_vec_ok(p), stream);
   }
 }

@@ -643,8 +643,11 @@ bool gemm_tile_supported(int dt, int bm, const GemmArgs& a, size_t align_a, size
     if (a.lda < a.K || a.ldb < a.K || a.ldc < a.N) return false;
     if (a.batch > 1 && (a.sA % 16 || a.sB % 16 || a.sC % 4)) return false;
     if (align_a % 16 || align_b % 16 || align_c % 8) return false;
-    // 32-bit offsets: rows up to bm-1 (A) / 127 (Bt) plus the K byte offset.
-    if ((long long)bm * a.lda + a.K >= (1LL << 31) || (long long)128 * a.ldb + a.K >= (1LL << 31))
+    // 32-bit offsets: rows up to bm-1 (A) / the tile's last Bt row plus the K
+    // byte offset. The 192-column fp8 tile (T192, BN = 192) reads Bt rows up
+    // to 191; bm = 192 covers both 192-row tiles, so it is bounded by 192.
+    const long long bt_rows = bm == 192 ? 192 : 128;
+    if ((long long)bm * a.lda + a.K >= (1LL << 31) || bt_rows * a.ldb + a.K >= (1LL << 31))
       return false;
     return true;
   }

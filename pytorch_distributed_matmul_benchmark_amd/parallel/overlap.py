@@ -50,7 +50,7 @@ from .partition import ceil_div
 
 # ---- the planner -------------------------------------------------------------
 # GEMM rate (TFLOPS) of a full grid per dtype on one MI355X, measured
-# (README.md headline table: W4 / W4S 16k bf16 1526, fp16 ~ bf16, exact
+# (docs/HISTORY.md headline table: W4 / W4S 16k bf16 1526, fp16 ~ bf16, exact
 # fp32 152, fp8 3300); an under-filled grid runs at the fraction of the
 # 256 CUs its 256x256 tiles fill (split-K recovers part: floor 0.6).
 GEMM_TFLOPS = {torch.bfloat16: 1500.0, torch.float16: 1500.0, torch.float32: 150.0,
@@ -130,6 +130,9 @@ class OverlapPlan:
     # measured: [min, max] over reps and ranks of every timed value (the
     # planner itself uses the median of each rank's reps, MAX over ranks)
     spread_us: Dict[str, List[float]] = field(default_factory=dict)
+    # measured: wall time spent measuring, MAX over ranks (the
+    # setup cost every overlapped mode and sweep size pays on every rank)
+    planner_s: float = 0.0
 
     def as_dict(self) -> dict:
         d = asdict(self)
@@ -142,6 +145,7 @@ class OverlapPlan:
         d["cu_share"] = round(d["cu_share"], 4)
         d["cu_share_p"] = {str(k): round(v, 4) for k, v in self.cu_share_p.items()}
         d["spread_us"] = {k: [round(x, 1) for x in v] for k, v in self.spread_us.items()}
+        d["planner_s"] = round(d["planner_s"], 3)
         return d
 
 
@@ -313,6 +317,7 @@ def measured_plan(units: Sequence[Tuple], ctx, kind: str, payload_bytes: float, 
 
     from .dist import all_ok, barrier, reduce_scalar
 
+    t_start = time.perf_counter()
     A, B, C = units[0]
     m, ws, dev = C.shape[-2], ctx.world_size, C.device
     granule = _granule(units, native, owner)
@@ -415,10 +420,12 @@ def measured_plan(units: Sequence[Tuple], ctx, kind: str, payload_bytes: float, 
     G = agreed("gemm")
     piece = {P: agreed(f"piece{P}") for P in sorted(choices)}
     Gs = {P: agreed(f"gemm_shared{P}") for P in sorted(choices)}
-    return plan_overlap(m, C.shape[-1], A.shape[-1], A.dtype, ws, kind, payload_bytes,
-                        granule=granule, steps=steps, requested=requested, gemm_time_us=G,
-                        comm_time_us=piece[1], piece_time_us=piece, source="measured",
-                        shared_time_us=Gs, spread_us=spread)
+    out = plan_overlap(m, C.shape[-1], A.shape[-1], A.dtype, ws, kind, payload_bytes,
+                       granule=granule, steps=steps, requested=requested, gemm_time_us=G,
+                       comm_time_us=piece[1], piece_time_us=piece, source="measured",
+                       shared_time_us=Gs, spread_us=spread)
+    out.planner_s = reduce_scalar(ctx, time.perf_counter() - t_start, "max")  # agreed: MAX over ranks
+    return out
 
 
 def piece_rows(m: int, rows: int) -> List[Tuple[int, int]]:
