@@ -408,11 +408,20 @@ __host__ __device__ __forceinline__ void map_tile(const GemmArgs& a, int b, int&
     // supertile 6: mode 1 with the XCD -> block position rotated by one per
     // round, so every XCD visits every position of the 16 x 16 round (A/B)
     const int x = a.supertile == 6 ? ((b & 7) + round) & 7 : b & 7;
-    const int st_n = a.tiles_n >> 4;
-    const int st_per_b = (a.tiles_m >> 4) * st_n;
+    const int st_n = a.tiles_n >> 4, st_m = a.tiles_m >> 4;
+    const int st_per_b = st_m * st_n;
     bz = round / st_per_b;
     const int s = round - bz * st_per_b;
-    const int sr = s / st_n, sc = s - sr * st_n;
+    int sr = s / st_n, sc = s - sr * st_n;
+    // round-order A/Bs (experiments; the Infinity Cache reuse of the panels
+    // between consecutive rounds): 7 = snake (odd super-tile rows sweep N
+    // backwards, so a row change re-reads the B panels just used), 8 = the
+    // super-tiles sweep M fastest (B panels stay, A panels change)
+    if (a.supertile == 7 && (sr & 1)) sc = st_n - 1 - sc;
+    if (a.supertile == 8) {
+      sc = s / st_m;
+      sr = s - sc * st_m;
+    }
     if (sub == 2) {  // XCD sub-block 2 (M) x 16 (N)
       tm = (sr << 4) + (x << 1) + (i >> 4);
       tn = (sc << 4) + (i & 15);

@@ -49,6 +49,12 @@ enum ExperimentKernel : int {
   kMfmaW4SNoDma = 57,    // no LDS-DMA refills in the K-loop
   kMfmaW4SNoEpi = 58,    // no C stores (no-access loads in their place)
   kMfmaW4SMfmaOnly = 59, // neither fragment reads nor refills: MFMAs, waits, barriers
+  // W4S tile orders (round 6, VERDICT r5 #6: does the clock follow the L2 /
+  // Infinity Cache hit rate?), the shipping K-loop with another map_tile order:
+  kMfmaW4STall = 70,     // XCD sub-block 8 x 4 (12 panels per K-step, A-heavy)
+  kMfmaW4SWide = 71,     // XCD sub-block 2 x 16 (18 panels per K-step: lower L2 hit)
+  kMfmaW4SSnake = 72,    // 16 x 16 rounds in snake order (odd rows sweep N backwards)
+  kMfmaW4SMcol = 73,     // 16 x 16 rounds sweeping M fastest
 };
 
 }  // namespace pdmb

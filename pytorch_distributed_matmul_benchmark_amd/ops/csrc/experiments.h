@@ -23,7 +23,7 @@ static bool is_experiment(int k) {
     case kFp8W4TS: case kFp8W4STS: case kMfmaW4STS: case kF32_256sDirect: case kFp8W4Unfused:
     case kT128Unfused: case kFp8T128Unfused: case kMfmaW4Unfused: case kF32T128B32:
     case kF32W4B32: case kF32_256p: case kMfmaW4SNoFrag: case kMfmaW4SNoDma: case kMfmaW4SNoEpi:
-    case kMfmaW4SMfmaOnly:
+    case kMfmaW4SMfmaOnly: case kMfmaW4STall: case kMfmaW4SWide: case kMfmaW4SSnake: case kMfmaW4SMcol:
       return true;
     default:
       return false;
@@ -57,6 +57,7 @@ static int experiment_resolve(const Problem& p, int kernel, bool fast, bool w4, 
       return (p.dtype == kBF16 && w4) ? kernel : -1;
     case kMfmaW4STrace: case kMfmaW4SRot: case kMfmaW4SRotTrace: case kMfmaW4STS:
     case kMfmaW4SNoFrag: case kMfmaW4SNoDma: case kMfmaW4SNoEpi: case kMfmaW4SMfmaOnly:
+    case kMfmaW4STall: case kMfmaW4SWide: case kMfmaW4SSnake: case kMfmaW4SMcol:
       return (p.dtype == kBF16 && w4 && w4s_fits(p)) ? kernel : -1;
     case kMfmaW4Pers: return w4 ? kernel : -1;  // bf16 and fp16
     default: return -1;
@@ -97,6 +98,10 @@ static hipError_t experiment_launch(const Problem& p, int k, const GemmArgs& a, 
     case kMfmaW4SNoDma: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 14);
     case kMfmaW4SNoEpi: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 15);
     case kMfmaW4SMfmaOnly: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 16);
+    case kMfmaW4STall: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 17);
+    case kMfmaW4SWide: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 18);
+    case kMfmaW4SSnake: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 19);
+    case kMfmaW4SMcol: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 20);
     case kMfma256: return gemm256_launch(p.dtype, a, 0, stream);
     case kMfma256b: return gemm256_launch(p.dtype, a, 1, stream);
     case kMfma256c: return gemm256_launch(p.dtype, a, 2, stream);
@@ -158,6 +163,10 @@ static const char* experiment_name(int kernel) {
     case kMfmaW4SNoDma: return "pdmb_w4s_diag_nodma";
     case kMfmaW4SNoEpi: return "pdmb_w4s_diag_noepi";
     case kMfmaW4SMfmaOnly: return "pdmb_w4s_diag_mfma_only";
+    case kMfmaW4STall: return "pdmb_w4s_tall";
+    case kMfmaW4SWide: return "pdmb_w4s_wide";
+    case kMfmaW4SSnake: return "pdmb_w4s_snake";
+    case kMfmaW4SMcol: return "pdmb_w4s_mcol";
     default: return "auto";
   }
 }

@@ -1135,7 +1135,7 @@ static hipError_t tiled_launch(const Problem& p, int k, GemmArgs a, void* part, 
     }
   }
   a.splitk = S;
-  if ((sub >= 7 && sub <= 11) || (sub >= 13 && sub <= 16)) {  // W4S (13-16: power diag), unsplit, one
+  if ((sub >= 7 && sub <= 11) || (sub >= 13 && sub <= 20)) {  // W4S (13-16: power diag, 17-20: tile order), unsplit, one
                                                               // workgroup per usable CU (a multiple of 8)
     if (S > 1) {
       sub = 0;

@@ -638,7 +638,9 @@ __device__ __forceinline__ void ktile_s(const Ctx& c, const char* smem, u32x4 ra
 // DIAG: ktile_s's bits, plus bit 2: no C stores — 32 out-of-range LDS-DMA
 // loads per wave in their place, as before the first tile, so every vmcnt
 // wait counts the same (timing-only, WRONG results).
-template <int DT, int TRACE = 0, bool NTS = true, int DIAG = 0>  // NTS: non-temporal C stores (false: A/B)
+// SUB: map_tile's XCD sub-block shape (0 = 4 x 8; 1 = 8 x 4 and 2 = 2 x 16 are
+// the tile-order A/Bs of kMfmaW4STall / kMfmaW4SWide).
+template <int DT, int TRACE = 0, bool NTS = true, int DIAG = 0, int SUB = 0>  // NTS: non-temporal C stores (false: A/B)
 __global__ void __launch_bounds__(NT, 1) gemm_w4s(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 4 * kEpiBuf];
   TileTrace tr;
@@ -692,12 +694,12 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4s(GemmArgs a) {
   const int nk = c.nk;
 
   int bz, tm, tn;
-  map_tile(a, vb, bz, tm, tn);
+  map_tile(a, vb, bz, tm, tn, SUB);
   Src cur = tile_src(a, bz, tm, tn);
   int nvb = vb + G, nbz = bz, ntm = tm, ntn = tn;
   Src nxt = cur;
   if (nvb < T) {
-    map_tile(a, nvb, nbz, ntm, ntn);
+    map_tile(a, nvb, nbz, ntm, ntn, SUB);
     nxt = tile_src(a, nbz, ntm, ntn);
   }
 
@@ -852,7 +854,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4s(GemmArgs a) {
     cur = nxt;
     nvb = vb + G;
     if (nvb < T) {
-      map_tile(a, nvb, nbz, ntm, ntn);
+      map_tile(a, nvb, nbz, ntm, ntn, SUB);
       nxt = tile_src(a, nbz, ntm, ntn);
     }
   }
@@ -973,6 +975,19 @@ hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
     if (sub == 14) hipLaunchKernelGGL((kw4::gemm_w4s<kBF16, 0, true, 2>), pg, block, 0, stream, a);
     if (sub == 15) hipLaunchKernelGGL((kw4::gemm_w4s<kBF16, 0, true, 4>), pg, block, 0, stream, a);
     if (sub == 16) hipLaunchKernelGGL((kw4::gemm_w4s<kBF16, 0, true, 3>), pg, block, 0, stream, a);
+    return hipGetLastError();
+  }
+  if (sub >= 17 && sub <= 20) {  // W4S tile-order A/Bs: 8x4 / 2x16 sub-blocks, snake / M-fastest rounds
+    if (S > 1 || a.pers_grid <= 0 || a.pers_grid % 8 || (a.K / kw4::BK) % 2 || a.K / kw4::BK < 6 ||
+        dt != kBF16)
+      return hipErrorInvalidValue;
+    const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
+    if (sub == 17) hipLaunchKernelGGL((kw4::gemm_w4s<kBF16, 0, true, 0, 1>), pg, block, 0, stream, a);
+    if (sub == 18) hipLaunchKernelGGL((kw4::gemm_w4s<kBF16, 0, true, 0, 2>), pg, block, 0, stream, a);
+    if (sub == 19 || sub == 20) {
+      if (a.supertile == 1) a.supertile = sub == 19 ? 7 : 8;
+      hipLaunchKernelGGL((kw4::gemm_w4s<kBF16>), pg, block, 0, stream, a);
+    }
     return hipGetLastError();
   }
   if (sub == 8) {  // W4S with per-workgroup start / end stamps
