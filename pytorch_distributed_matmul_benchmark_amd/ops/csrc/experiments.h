@@ -24,6 +24,7 @@ static bool is_experiment(int k) {
     case kT128Unfused: case kFp8T128Unfused: case kMfmaW4Unfused: case kF32T128B32:
     case kF32W4B32: case kF32_256p: case kMfmaW4SNoFrag: case kMfmaW4SNoDma: case kMfmaW4SNoEpi:
     case kMfmaW4SMfmaOnly: case kMfmaW4STall: case kMfmaW4SWide: case kMfmaW4SSnake: case kMfmaW4SMcol:
+    case kFp8W4SK4: case kFp8W4SK4TS:
       return true;
     default:
       return false;
@@ -33,11 +34,13 @@ static bool is_experiment(int k) {
 static bool experiment_is_fp8(int k) {
   return k == kFp8 || k == kFp8W4TS || k == kFp8W4STS || k == kFp8W4Unfused || k == kFp8T128Unfused ||
          k == kFp8W4Diag || k == kFp8W4Diag2 || k == kFp8W4Diag3 || k == kFp8W4Tall || k == kFp8W4Wide ||
-         k == kFp8W4Scaled || k == kFp8W4Trace;
+         k == kFp8W4Scaled || k == kFp8W4Trace || k == kFp8W4SK4 || k == kFp8W4SK4TS;
 }
 
 static int experiment_resolve_fp8(const Problem& p, int kernel, bool s_fits) {
   if (kernel == kFp8W4STS) return s_fits ? kernel : -1;
+  if (kernel == kFp8W4SK4 || kernel == kFp8W4SK4TS)
+    return gemm_fp8_w4s_k4_fits(shape_args(p)) && device_cus() % 8 == 0 ? kernel : -1;
   if (kernel == kFp8T128Unfused) return supports(p, kFp8T128) ? kernel : -1;
   return kernel;
 }
@@ -92,6 +95,13 @@ static hipError_t experiment_launch(const Problem& p, int k, const GemmArgs& a, 
       GemmArgs s = a;
       s.pers_grid = ((p.cus > 0 ? p.cus : device_cus()) / 8) * 8;
       return gemm_fp8_launch(s, 17, stream);
+    }
+    case kFp8W4SK4:
+    case kFp8W4SK4TS: {
+      GemmArgs s = a;
+      s.splitk = 1;
+      s.pers_grid = ((p.cus > 0 ? p.cus : device_cus()) / 8) * 8;
+      return gemm_fp8_launch(s, k == kFp8W4SK4 ? 19 : 20, stream);
     }
     case kMfmaW4STS: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 11);
     case kMfmaW4SNoFrag: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 13);
@@ -167,6 +177,8 @@ static const char* experiment_name(int kernel) {
     case kMfmaW4SWide: return "pdmb_w4s_wide";
     case kMfmaW4SSnake: return "pdmb_w4s_snake";
     case kMfmaW4SMcol: return "pdmb_w4s_mcol";
+    case kFp8W4SK4: return "pdmb_fp8_w4s_k4";
+    case kFp8W4SK4TS: return "pdmb_fp8_w4s_k4_tstore";
     default: return "auto";
   }
 }

@@ -34,6 +34,7 @@ hipError_t gemm_f32_tile_launch(GemmArgs a, hipStream_t stream, int variant);
 bool gemm_fp8_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream);
 bool gemm_fp8_w4s_fits(const GemmArgs& a);
+bool gemm_fp8_w4s_k4_fits(const GemmArgs& a);
 bool gemm_w4_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub = 0);
 bool gemm_tile_supported(int dt, int bm, const GemmArgs& a, size_t align_a, size_t align_b,

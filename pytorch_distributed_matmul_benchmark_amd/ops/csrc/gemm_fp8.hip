@@ -723,7 +723,11 @@ __device__ __forceinline__ void ktile_w4s(const Ctx4& c, const char* smem, u32x4
   }
 }
 
-template <bool NTS = true>  // NTS: non-temporal C stores (false: A/B kFp8W4STS)
+// K4 (experiments: kFp8W4SK4 / kFp8W4SK4TS): also nk == 4 (K = 512). With four
+// K-tiles the first pair is already the pair whose second K-tile fetches the
+// next tile's B(0) (item t + 4 = nk), so its DMA targets go through the same
+// selects as the last pair's; nk >= 6 never reaches the next tile there.
+template <bool NTS = true, bool K4 = false>  // NTS: non-temporal C stores (false: A/B kFp8W4STS)
 __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4s(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE4 + 4 * kEpiBuf];
   // tile_end > 0: the whole-wave part of a tile-range tail plan
@@ -824,9 +828,20 @@ __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4s(GemmArgs a) {
       r.w = rc.w;
       ko = (uint32_t)k * BK;
     };
-    ktile_w4s<0, 48, 48, true>(c, smem, cur.ra, 2 * BK, cur.rb, 3 * BK, lds0w, acc, A, A7a, A7b, B0, B1);
-    ktile_w4s<STAGE4, 48, 16, false>(c, smem, cur.ra, 3 * BK, cur.rb, 4 * BK, lds0w, acc, A, A7b, A7a,
-                                     B1, B0);
+    if constexpr (K4) {
+      u32x4 ra, rb;
+      uint32_t ka, kb;
+      tgt(2, cur.ra, nxt.ra, ra, ka);
+      tgt(3, cur.rb, nxt.rb, rb, kb);
+      ktile_w4s<0, 48, 48, true>(c, smem, ra, ka, rb, kb, lds0w, acc, A, A7a, A7b, B0, B1);
+      tgt(3, cur.ra, nxt.ra, ra, ka);
+      tgt(4, cur.rb, nxt.rb, rb, kb);
+      ktile_w4s<STAGE4, 48, 16, false>(c, smem, ra, ka, rb, kb, lds0w, acc, A, A7b, A7a, B1, B0);
+    } else {
+      ktile_w4s<0, 48, 48, true>(c, smem, cur.ra, 2 * BK, cur.rb, 3 * BK, lds0w, acc, A, A7a, A7b, B0, B1);
+      ktile_w4s<STAGE4, 48, 16, false>(c, smem, cur.ra, 3 * BK, cur.rb, 4 * BK, lds0w, acc, A, A7b, A7a,
+                                       B1, B0);
+    }
     int t = 2;
     for (; t + 4 < nk; t += 2) {
       ktile_w4s<0, 16, 16, false>(c, smem, cur.ra, (uint32_t)(t + 2) * BK, cur.rb, (uint32_t)(t + 3) * BK,
@@ -1028,6 +1043,11 @@ bool gemm_fp8_w4s_fits(const GemmArgs& a) {
   return a.M % k8::BM == 0 && a.N % k8::BN == 0 && a.K % (2 * k8::BK) == 0 && nk >= 6;
 }
 
+bool gemm_fp8_w4s_k4_fits(const GemmArgs& a) {  // the K4 variant: nk even, >= 4
+  const int nk = a.K / k8::BK;
+  return a.M % k8::BM == 0 && a.N % k8::BN == 0 && a.K % (2 * k8::BK) == 0 && nk >= 4;
+}
+
 bool gemm_fp8_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c) {
   if (a.K % 128 != 0 || a.K <= 0 || a.N % 4 != 0 || a.M <= 0 || a.N <= 0) return false;
   if (a.lda % 16 || a.ldb % 16 || a.ldc % 4) return false;
@@ -1105,6 +1125,14 @@ hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream) {
     if (!gemm_fp8_w4s_fits(a) || a.pers_grid <= 0 || a.pers_grid % 8) return hipErrorInvalidValue;
     const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
     hipLaunchKernelGGL(k8::gemm_fp8_w4s<false>, pg, dim3(k8::NT4), 0, stream, a);
+  }
+  else if (variant == 19 || variant == 20) {  // kFp8W4SK4 / kFp8W4SK4TS: W4S down to nk == 4
+    if (!gemm_fp8_w4s_k4_fits(a) || a.pers_grid <= 0 || a.pers_grid % 8) return hipErrorInvalidValue;
+    const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
+    if (variant == 19)
+      hipLaunchKernelGGL((k8::gemm_fp8_w4s<true, true>), pg, dim3(k8::NT4), 0, stream, a);
+    else
+      hipLaunchKernelGGL((k8::gemm_fp8_w4s<false, true>), pg, dim3(k8::NT4), 0, stream, a);
   }
   else
     hipLaunchKernelGGL(k8::gemm_fp8_nt, grid, dim3(k8::NTHREADS), 0, stream, a);

@@ -5,6 +5,12 @@ utilisation (SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs × cycles)), L2 hit rate,
 LDS bank conflicts and wave stall split. Markdown to stdout.
 
     python scripts/pmc_summary.py gpurun_out/pmc
+    python scripts/pmc_summary.py gpurun_out/pmc --cycle w4s,x_w4s_snake,torch
+
+``--cycle``: label every GEMM dispatch by its position in the launch order
+instead of by kernel name (scripts/prof_gemm_arms.py issues its arms in one
+fixed cycle, the torch arm last): arms that run the same kernel template with
+another runtime argument (a tile order) are told apart.
 """
 import collections
 import csv
@@ -19,7 +25,7 @@ def short(k):
     return k.replace("void ", "").split("(")[0]
 
 
-def main(d):
+def main(d, cycle=None):
     cnt = collections.defaultdict(lambda: collections.defaultdict(list))
     dur = collections.defaultdict(list)
     for p in sorted(os.listdir(d)):
@@ -27,10 +33,13 @@ def main(d):
         if not os.path.exists(f):
             continue
         seen = set()
-        for r in csv.DictReader(open(f)):
+        rows = [r for r in csv.DictReader(open(f))
+                if "distribution" not in r["Kernel_Name"] and "fillBuffer" not in r["Kernel_Name"]]
+        order = {did: i for i, did in enumerate(sorted({int(r["Dispatch_Id"]) for r in rows}))}
+        for r in rows:
             k = r["Kernel_Name"]
-            if "distribution" in k or "fillBuffer" in k:
-                continue
+            if cycle:
+                k = cycle[order[int(r["Dispatch_Id"])] % len(cycle)]
             cnt[short(k)][r["Counter_Name"]].append(float(r["Counter_Value"]))
             key = (r["Dispatch_Id"], p)
             if key not in seen:
@@ -57,4 +66,9 @@ def main(d):
 
 
 if __name__ == "__main__":
-    sys.exit(main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"))
+    args = [x for x in sys.argv[1:] if not x.startswith("--cycle")]
+    cyc = None
+    if "--cycle" in sys.argv:
+        cyc = sys.argv[sys.argv.index("--cycle") + 1].split(",")
+        args = [x for x in args if x != sys.argv[sys.argv.index("--cycle") + 1]]
+    sys.exit(main(args[0] if args else "gpurun_out/pmc", cyc))
