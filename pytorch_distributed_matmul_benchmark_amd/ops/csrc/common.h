@@ -412,16 +412,21 @@ __host__ __device__ __forceinline__ void map_tile(const GemmArgs& a, int b, int&
     const int st_per_b = st_m * st_n;
     bz = round / st_per_b;
     const int s = round - bz * st_per_b;
+#ifdef PDMB_EXPERIMENTS
     int sr = s / st_n, sc = s - sr * st_n;
-    // round-order A/Bs (experiments; the Infinity Cache reuse of the panels
-    // between consecutive rounds): 7 = snake (odd super-tile rows sweep N
-    // backwards, so a row change re-reads the B panels just used), 8 = the
-    // super-tiles sweep M fastest (B panels stay, A panels change)
+    // round-order A/Bs (experiments build only; the Infinity Cache reuse of
+    // the panels between consecutive rounds, profiles/r8c_*: no effect): 7 =
+    // snake (odd super-tile rows sweep N backwards), 8 = the super-tiles
+    // sweep M fastest
     if (a.supertile == 7 && (sr & 1)) sc = st_n - 1 - sc;
     if (a.supertile == 8) {
       sc = s / st_m;
       sr = s - sc * st_m;
     }
+#else
+    (void)st_m;
+    const int sr = s / st_n, sc = s - sr * st_n;
+#endif
     if (sub == 2) {  // XCD sub-block 2 (M) x 16 (N)
       tm = (sr << 4) + (x << 1) + (i >> 4);
       tn = (sc << 4) + (i & 15);

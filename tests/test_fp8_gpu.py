@@ -170,6 +170,27 @@ def test_fp8_streaming_w4s_matches_w4_bitwise(batch, M, N, K):
         assert torch.equal(out, ref)
 
 
+@pytest.mark.parametrize("kernel", ["x_fp8_w4s_k4", "x_fp8_w4s_k4_tstore"])
+@pytest.mark.parametrize("batch,M,N,K", [(1, 4096, 4096, 512), (1, 8192, 8192, 512), (2, 2048, 2048, 512),
+                                         (1, 16384, 2048, 512), (1, 2048, 16384, 512), (1, 256, 256, 512),
+                                         (1, 8192, 4096, 1024), (1, 4096, 4096, 768)])
+def test_fp8_w4s_k4_matches_w4_bitwise(kernel, batch, M, N, K):
+    """fp8 W4S down to four K-tiles (round 6, K4: the first pair's DMA targets
+    through the same selects as the last pair's; at K = 512 the first pair
+    already fetches the next tile's B(0)): bitwise equal to fp8 W4 with alpha,
+    one and many tiles per CU, thin grids, batches, K = 512 / 768 / 1024."""
+    g = torch.Generator(device="cuda").manual_seed(7 * batch + M + 3 * N + K)
+    A = torch.randn(batch, M, K, device="cuda", generator=g).to(FP8)
+    B = _colmajor(torch.randn(batch, K, N, device="cuda", generator=g).to(FP8))
+    if batch == 1:
+        A, B = A[0], B[0]
+    ref = gemm.matmul(A, B, kernel="fp8_w4", alpha=0.5)
+    for _ in range(2):
+        out = torch.full_like(ref, float("nan"))
+        gemm.matmul(A, B, out=out, kernel=kernel, alpha=0.5)
+        assert torch.equal(out, ref)
+
+
 def test_fp8_w4s_plan_and_refusals():
     g = torch.Generator(device="cuda").manual_seed(9)
 
