@@ -655,7 +655,7 @@ __global__ void __launch_bounds__(NT4, 1) gemm_fp8_w4(GemmArgs a) {
 // next tile's first two K-tiles wait vmcnt(16 + 32), the first tile issues
 // 32 out-of-range LDS-DMA loads in the stores' place, and every MFMA of
 // K-tile 0 (one per accumulator: K = 128 per MFMA) starts from C = 0.
-// Interior tiles only (M, N % 256), K % 256 == 0, K >= 768; static tiles
+// Interior tiles only (M, N % 256), K % 256 == 0, K >= 512 (K = 512: the K4 form); static tiles
 // b, b + G, ... (G = grid, a multiple of 8) on a device the GEMM has to itself.
 __device__ __forceinline__ void mfma_f8_zero(f32x4& acc, const i32x8& a, const i32x8& b) {
   asm volatile("v_mfma_f32_16x16x128_f8f6f4 %0, %1, %2, 0" : "=&a"(acc) : "v"(a), "v"(b));
@@ -723,7 +723,8 @@ __device__ __forceinline__ void ktile_w4s(const Ctx4& c, const char* smem, u32x4
   }
 }
 
-// K4 (experiments: kFp8W4SK4 / kFp8W4SK4TS): also nk == 4 (K = 512). With four
+// K4 (nk == 4, K = 512, shipping; kFp8W4SK4 / kFp8W4SK4TS force it on any
+// even nk >= 4 for A/B): with four
 // K-tiles the first pair is already the pair whose second K-tile fetches the
 // next tile's B(0) (item t + 4 = nk), so its DMA targets go through the same
 // selects as the last pair's; nk >= 6 never reaches the next tile there.
@@ -1038,9 +1039,10 @@ __global__ void __launch_bounds__(NT4, 1) gemm_fp8_sk(GemmArgs a) {
 
 int fp8_sk_slots(long long span, int nk, long long G) { return sk_max_owners(span, nk, G); }
 
+// nk even and >= 4 (round 6: K = 512 runs the K4 form, below; before, nk >= 6)
 bool gemm_fp8_w4s_fits(const GemmArgs& a) {
   const int nk = a.K / k8::BK;
-  return a.M % k8::BM == 0 && a.N % k8::BN == 0 && a.K % (2 * k8::BK) == 0 && nk >= 6;
+  return a.M % k8::BM == 0 && a.N % k8::BN == 0 && a.K % (2 * k8::BK) == 0 && nk >= 4;
 }
 
 bool gemm_fp8_w4s_k4_fits(const GemmArgs& a) {  // the K4 variant: nk even, >= 4
@@ -1099,7 +1101,16 @@ hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream) {
   if (variant == 2) {  // kFp8W4S: streaming persistent (host: gemm_fp8_w4s_fits, pers_grid % 8 == 0)
     if (!gemm_fp8_w4s_fits(a) || a.pers_grid <= 0 || a.pers_grid % 8) return hipErrorInvalidValue;
     const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
-    hipLaunchKernelGGL(k8::gemm_fp8_w4s<true>, pg, dim3(k8::NT4), 0, stream, a);
+    // K = 512 (four K-tiles): the K4 form. Measured against fp8 W4, which
+    // cannot overlap a tile's C stores with anything (settled, two sessions,
+    // profiles/r8d/ab_fp8_k512_summary.jsonl): 16384^2 x 512 1544 vs 1328 TF
+    // (hipBLASLt 1553), 8192^2 x 512 1551 vs 1398 (1511), 16384 x 8192 x 512
+    // 1567 vs 1418 (1544). From six K-tiles on, the K4 form measured within
+    // +-2 % of the plain one either way (r8e), so those keep the plain W4S.
+    if (a.K / k8::BK < 6)
+      hipLaunchKernelGGL((k8::gemm_fp8_w4s<true, true>), pg, dim3(k8::NT4), 0, stream, a);
+    else
+      hipLaunchKernelGGL(k8::gemm_fp8_w4s<true>, pg, dim3(k8::NT4), 0, stream, a);
     return hipGetLastError();
   }
 #ifdef PDMB_EXPERIMENTS

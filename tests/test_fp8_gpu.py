@@ -152,12 +152,13 @@ def test_fp8_thin_supertiles_exact(M, N, batch):
 
 @pytest.mark.parametrize("batch,M,N,K", [(1, 256, 256, 768), (1, 1024, 2048, 1024), (1, 4096, 4096, 768),
                                          (1, 8192, 4096, 1024), (2, 2048, 2048, 768), (1, 16384, 2048, 768),
-                                         (1, 2048, 16384, 768)])
+                                         (1, 2048, 16384, 768), (1, 8192, 8192, 512), (2, 4096, 2048, 512),
+                                         (1, 16384, 2048, 512), (1, 256, 512, 512)])
 def test_fp8_streaming_w4s_matches_w4_bitwise(batch, M, N, K):
     """fp8 W4S (one K-tile stream per CU, epilogue overlapped with the next
     tile's first DMAs, C = 0 MFMA starts): the same accumulation order as the
     W4 fp8 kernel, so bitwise equal, for one and several tiles per CU, uneven
-    tile counts, thin grids and batches."""
+    tile counts, thin grids and batches; K = 512 runs the K4 form (round 6)."""
     g = torch.Generator(device="cuda").manual_seed(batch + M + 3 * N + K)
     A = torch.randn(batch, M, K, device="cuda", generator=g).to(FP8)
     B = _colmajor(torch.randn(batch, K, N, device="cuda", generator=g).to(FP8))
@@ -207,6 +208,14 @@ def test_fp8_w4s_plan_and_refusals():
     with pytest.raises(RuntimeError):
         gemm.matmul(A, B, kernel="fp8_w4s")
     A, B = ops(8192, 8192, 640)  # K / 128 odd
+    assert gemm.kernel_for(A, B) == "pdmb_fp8_w4_nt"
+    with pytest.raises(RuntimeError):
+        gemm.matmul(A, B, kernel="fp8_w4s")
+    A, B = ops(8192, 8192, 512)  # four K-tiles (round 6): W4S's K4 form
+    assert gemm.kernel_for(A, B) == "pdmb_fp8_w4s"
+    A, B = ops(4096, 4096, 512)  # one tile per CU: W4
+    assert gemm.kernel_for(A, B) == "pdmb_fp8_w4_nt"
+    A, B = ops(8192, 8192, 256)  # two K-tiles: no stream
     assert gemm.kernel_for(A, B) == "pdmb_fp8_w4_nt"
     with pytest.raises(RuntimeError):
         gemm.matmul(A, B, kernel="fp8_w4s")

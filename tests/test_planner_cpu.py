@@ -189,6 +189,18 @@ def test_t192_plans(C, monkeypatch):
         assert "192" not in plan(C, FP8, 2304, 2304, 4096)[0]
 
 
+def test_fp8_short_k_streams(C):
+    """Round 6: fp8 W4S down to four K-tiles (K = 512, the K4 form), measured
+    1.15x fp8 W4 and at hipBLASLt's rate on the write-bound short-K grids
+    (profiles/r8d/ab_fp8_k512_summary.jsonl); one tile per CU keeps W4, two
+    K-tiles cannot stream."""
+    FP8 = 3
+    for shape in ((16384, 16384, 512), (8192, 8192, 512), (16384, 8192, 512), (16384, 16384, 1024)):
+        assert plan(C, FP8, *shape)[0] == "pdmb_fp8_w4s", shape
+    assert plan(C, FP8, 4096, 4096, 512)[0] == "pdmb_fp8_w4_nt"
+    assert plan(C, FP8, 8192, 8192, 256)[0] != "pdmb_fp8_w4s"
+
+
 def test_t192x128_multi_wave_rate(C, monkeypatch):
     """T192x128 is priced slower per K-tile past one wave (kModels kt2; measured
     0.65-0.67 us vs 0.61 on one wave, profiles/r7j_t192_ab_bf16.jsonl): the two
