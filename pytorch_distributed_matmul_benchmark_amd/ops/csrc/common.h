@@ -388,12 +388,20 @@ inline int choose_supertile(int tiles_m, int tiles_n) {
 __host__ __device__ __forceinline__ void map_tile(const GemmArgs& a, int b, int& bz, int& tm, int& tn,
                                                   int sub = 0) {
   const int tpb = a.tiles_m * a.tiles_n;
-  if (a.supertile >= 2 && a.supertile <= 5) {
+#ifdef PDMB_EXPERIMENTS
+  // 9 (experiments, round 6): the 32 x 8 round of mode 3 as an 8 x 1 XCD grid
+  // of 4 x 8 blocks (each XCD spans the grid's 8 tile columns: 4 A + 8 B
+  // panels per K-step instead of mode 3's 8 A + 4 B)
+  const bool thin = (a.supertile >= 2 && a.supertile <= 5) || a.supertile == 9;
+#else
+  const bool thin = a.supertile >= 2 && a.supertile <= 5;
+#endif
+  if (thin) {
     const int x = b & 7, j = b >> 3;
     const int round = j >> 5, i = j & 31;
     const int st = a.supertile;
     const int xn = st == 2 ? 4 : st == 3 ? 2 : st == 4 ? 8 : 1;  // XCD grid columns
-    const int bn = (st == 2 || st == 4) ? 8 : 4, bm = 32 / bn;  // XCD block
+    const int bn = (st == 2 || st == 4 || st == 9) ? 8 : 4, bm = 32 / bn;  // XCD block
     const int SM = (8 / xn) * bm, SN = xn * bn;                   // round shape in tiles
     const int st_n = a.tiles_n / SN;
     const int st_per_b = (a.tiles_m / SM) * st_n;

@@ -59,6 +59,12 @@ enum ExperimentKernel : int {
   // shipping W4S runs it at nk == 4 only, K = 512)
   kFp8W4SK4 = 74,
   kFp8W4SK4TS = 75,      // the same with plain (temporal) C stores
+  // thin grids (tiles_n = 8: the ws = 8 shards at 16k / 8k): mode 3's 32 x 8
+  // round as an 8 x 1 XCD grid of 4 x 8 blocks (supertile 9)
+  kMfmaW4SSt9 = 76,
+  kMfmaW4St9 = 77,
+  kFp8W4SSt9 = 78,
+  kFp8W4St9 = 79,
 };
 
 }  // namespace pdmb

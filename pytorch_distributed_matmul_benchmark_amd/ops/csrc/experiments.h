@@ -24,7 +24,7 @@ static bool is_experiment(int k) {
     case kT128Unfused: case kFp8T128Unfused: case kMfmaW4Unfused: case kF32T128B32:
     case kF32W4B32: case kF32_256p: case kMfmaW4SNoFrag: case kMfmaW4SNoDma: case kMfmaW4SNoEpi:
     case kMfmaW4SMfmaOnly: case kMfmaW4STall: case kMfmaW4SWide: case kMfmaW4SSnake: case kMfmaW4SMcol:
-    case kFp8W4SK4: case kFp8W4SK4TS:
+    case kFp8W4SK4: case kFp8W4SK4TS: case kMfmaW4SSt9: case kMfmaW4St9: case kFp8W4SSt9: case kFp8W4St9:
       return true;
     default:
       return false;
@@ -34,11 +34,14 @@ static bool is_experiment(int k) {
 static bool experiment_is_fp8(int k) {
   return k == kFp8 || k == kFp8W4TS || k == kFp8W4STS || k == kFp8W4Unfused || k == kFp8T128Unfused ||
          k == kFp8W4Diag || k == kFp8W4Diag2 || k == kFp8W4Diag3 || k == kFp8W4Tall || k == kFp8W4Wide ||
-         k == kFp8W4Scaled || k == kFp8W4Trace || k == kFp8W4SK4 || k == kFp8W4SK4TS;
+         k == kFp8W4Scaled || k == kFp8W4Trace || k == kFp8W4SK4 || k == kFp8W4SK4TS || k == kFp8W4SSt9 ||
+         k == kFp8W4St9;
 }
 
 static int experiment_resolve_fp8(const Problem& p, int kernel, bool s_fits) {
   if (kernel == kFp8W4STS) return s_fits ? kernel : -1;
+  if (kernel == kFp8W4SSt9) return s_fits ? kernel : -1;
+  if (kernel == kFp8W4St9) return kernel;
   if (kernel == kFp8W4SK4 || kernel == kFp8W4SK4TS)
     return gemm_fp8_w4s_k4_fits(shape_args(p)) && device_cus() % 8 == 0 ? kernel : -1;
   if (kernel == kFp8T128Unfused) return supports(p, kFp8T128) ? kernel : -1;
@@ -60,8 +63,9 @@ static int experiment_resolve(const Problem& p, int kernel, bool fast, bool w4, 
       return (p.dtype == kBF16 && w4) ? kernel : -1;
     case kMfmaW4STrace: case kMfmaW4SRot: case kMfmaW4SRotTrace: case kMfmaW4STS:
     case kMfmaW4SNoFrag: case kMfmaW4SNoDma: case kMfmaW4SNoEpi: case kMfmaW4SMfmaOnly:
-    case kMfmaW4STall: case kMfmaW4SWide: case kMfmaW4SSnake: case kMfmaW4SMcol:
+    case kMfmaW4STall: case kMfmaW4SWide: case kMfmaW4SSnake: case kMfmaW4SMcol: case kMfmaW4SSt9:
       return (p.dtype == kBF16 && w4 && w4s_fits(p)) ? kernel : -1;
+    case kMfmaW4St9: return (p.dtype == kBF16 && w4) ? kernel : -1;
     case kMfmaW4Pers: return w4 ? kernel : -1;  // bf16 and fp16
     default: return -1;
   }
@@ -112,6 +116,23 @@ static hipError_t experiment_launch(const Problem& p, int k, const GemmArgs& a, 
     case kMfmaW4SWide: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 18);
     case kMfmaW4SSnake: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 19);
     case kMfmaW4SMcol: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 20);
+    case kMfmaW4SSt9: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 21);
+    case kMfmaW4St9: {
+      GemmArgs s = a;
+      s.splitk = 1;
+      return gemm_w4_launch(p.dtype, s, stream, 22);
+    }
+    case kFp8W4SSt9: {
+      GemmArgs s = a;
+      s.splitk = 1;
+      s.pers_grid = ((p.cus > 0 ? p.cus : device_cus()) / 8) * 8;
+      return gemm_fp8_launch(s, 21, stream);
+    }
+    case kFp8W4St9: {
+      GemmArgs s = a;
+      s.splitk = 1;
+      return gemm_fp8_launch(s, 22, stream);
+    }
     case kMfma256: return gemm256_launch(p.dtype, a, 0, stream);
     case kMfma256b: return gemm256_launch(p.dtype, a, 1, stream);
     case kMfma256c: return gemm256_launch(p.dtype, a, 2, stream);
@@ -179,6 +200,10 @@ static const char* experiment_name(int kernel) {
     case kMfmaW4SMcol: return "pdmb_w4s_mcol";
     case kFp8W4SK4: return "pdmb_fp8_w4s_k4";
     case kFp8W4SK4TS: return "pdmb_fp8_w4s_k4_tstore";
+    case kMfmaW4SSt9: return "pdmb_w4s_st9";
+    case kMfmaW4St9: return "pdmb_w4_nn_st9";
+    case kFp8W4SSt9: return "pdmb_fp8_w4s_st9";
+    case kFp8W4St9: return "pdmb_fp8_w4_nt_st9";
     default: return "auto";
   }
 }

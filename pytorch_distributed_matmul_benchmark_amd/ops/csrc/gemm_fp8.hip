@@ -1137,6 +1137,20 @@ hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream) {
     const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
     hipLaunchKernelGGL(k8::gemm_fp8_w4s<false>, pg, dim3(k8::NT4), 0, stream, a);
   }
+  else if (variant == 21 || variant == 22) {  // fp8 W4S / W4 with mode 3's rounds as supertile 9
+    if (a.supertile == 3) a.supertile = 9;
+    if (variant == 22) {
+      if (S > 1) return hipErrorInvalidValue;
+      hipLaunchKernelGGL(k8::gemm_fp8_w4<0>, grid, dim3(k8::NT4), 0, stream, a);
+    } else {
+      if (!gemm_fp8_w4s_fits(a) || a.pers_grid <= 0 || a.pers_grid % 8) return hipErrorInvalidValue;
+      const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
+      if (a.K / k8::BK < 6)
+        hipLaunchKernelGGL((k8::gemm_fp8_w4s<true, true>), pg, dim3(k8::NT4), 0, stream, a);
+      else
+        hipLaunchKernelGGL(k8::gemm_fp8_w4s<true>, pg, dim3(k8::NT4), 0, stream, a);
+    }
+  }
   else if (variant == 19 || variant == 20) {  // kFp8W4SK4 / kFp8W4SK4TS: W4S down to nk == 4
     if (!gemm_fp8_w4s_k4_fits(a) || a.pers_grid <= 0 || a.pers_grid % 8) return hipErrorInvalidValue;
     const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));

@@ -977,6 +977,20 @@ hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
     if (sub == 16) hipLaunchKernelGGL((kw4::gemm_w4s<kBF16, 0, true, 3>), pg, block, 0, stream, a);
     return hipGetLastError();
   }
+  if (sub == 21 || sub == 22) {  // W4S / W4 with mode 3's rounds as an 8 x 1 XCD grid of 4 x 8 (supertile 9)
+    if (a.supertile == 3) a.supertile = 9;
+    if (sub == 22) {
+      if (S > 1 || dt != kBF16) return hipErrorInvalidValue;
+      hipLaunchKernelGGL(kw4::gemm_w4_nn<kBF16>, grid, block, 0, stream, a);
+      return hipGetLastError();
+    }
+    if (S > 1 || a.pers_grid <= 0 || a.pers_grid % 8 || (a.K / kw4::BK) % 2 || a.K / kw4::BK < 6 ||
+        dt != kBF16)
+      return hipErrorInvalidValue;
+    const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
+    hipLaunchKernelGGL((kw4::gemm_w4s<kBF16>), pg, block, 0, stream, a);
+    return hipGetLastError();
+  }
   if (sub >= 17 && sub <= 20) {  // W4S tile-order A/Bs: 8x4 / 2x16 sub-blocks, snake / M-fastest rounds
     if (S > 1 || a.pers_grid <= 0 || a.pers_grid % 8 || (a.K / kw4::BK) % 2 || a.K / kw4::BK < 6 ||
         dt != kBF16)

@@ -20,8 +20,9 @@ Here every number a multi-GPU run reports is checked:
   so an all-gather's blocks can be compared with their producers' local
   outputs across ranks bitwise without moving the tensors.
 * ``ref_rows`` / ``rows_error`` — sampled rows of a GEMM recomputed in fp32
-  (``torch.matmul`` of the upcast operands) against the kernel's output: the
-  GEMM side of bench.py's per-mode check (``Workload.verify``).
+  (broadcast products of the upcast operands summed over K: no library GEMM)
+  against the kernel's output: the GEMM side of bench.py's per-mode check
+  (``Workload.verify``).
 
 Nothing here runs inside a timed region.
 """
@@ -110,19 +111,25 @@ def sample_rows(m: int, count: int = 24) -> List[int]:
     return sorted({int(round(i * step)) for i in range(count)})
 
 
-def ref_rows(A: torch.Tensor, B: torch.Tensor, rows: Sequence[int], col_chunk: int = 4096) -> torch.Tensor:
+def ref_rows(A: torch.Tensor, B: torch.Tensor, rows: Sequence[int], budget_bytes: int = 256 << 20) -> torch.Tensor:
     """fp32 reference of rows ``rows`` of A @ B (A [m, k], B [k, n]; any
-    strides, fp8 included), computed in column chunks of B."""
+    strides, fp8 included) WITHOUT a library GEMM: broadcast products summed
+    over k (torch's elementwise and reduction kernels), in column chunks of B
+    that keep the [rows, k, chunk] product under ``budget_bytes``. A vendor GEMM
+    here would put a hipBLASLt kernel into every bench.py run, which the
+    provenance check (tests/test_provenance_gpu.py) forbids."""
     idx = torch.tensor(list(rows), device=A.device, dtype=torch.long)
     if A.element_size() == 1:  # fp8: gather the rows' bytes (index_select has no fp8 kernel)
         a = A.view(torch.uint8).index_select(0, idx).view(A.dtype).float()
     else:
         a = A.index_select(0, idx).float()
-    n = B.shape[-1]
+    k, n = B.shape[-2], B.shape[-1]
+    r = max(len(rows), 1)
+    chunk = max(1, min(n, budget_bytes // (4 * r * max(k, 1))))
     out = torch.empty(len(rows), n, device=A.device, dtype=torch.float32)
-    for s in range(0, n, col_chunk):
-        e = min(n, s + col_chunk)
-        out[:, s:e] = a @ B[:, s:e].float()
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        out[:, s:e] = (a.unsqueeze(2) * B[:, s:e].float().unsqueeze(0)).sum(dim=1)
     return out
 
 
