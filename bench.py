@@ -947,7 +947,7 @@ def main() -> int:
             "rccl_version": _rccl_version(ctx),
             "collectives_verified": verified,
             # the headline step's own output, checked after the timed region
-            "check": head["check"], "check_detail": head["check_detail"],
+            "check": head["check"], "check_detail": head["check_detail"], "check_s": head["check_s"],
             "per_rank_tflops": head["per_rank_tflops"],
             # medians of a 5 ms amdsmi poll over the timed region, with the sample counts
             "sclk_mhz": head["sclk_mhz"], "power_w": head["power_w"],

@@ -29,4 +29,7 @@ timeout -k 10 400 python scripts/ab_kernels.py --dtype float8_e4m3fn --rounds 4 
   > $OUT/ab_fp8_w4.jsonl 2> $OUT/ab_fp8_w4.err || exit $?
 grep '"summary"' $OUT/ab_fp8_w4.jsonl | cut -c1-200
 grep -h '"bitwise_eq_first": false' $OUT/ab_*.jsonl | grep -v torch | cut -c1-200
+echo "== counters $(date +%T)"
+timeout -s KILL 60 rocprofv3 -L > $OUT/counters.txt 2>&1; echo "list rc=$?"
+grep -o "SQ_INSTS_[A-Z0-9_]*" $OUT/counters.txt | sort -u | head -60
 echo "exit 0"
