@@ -65,6 +65,7 @@ enum ExperimentKernel : int {
   kMfmaW4St9 = 77,
   kFp8W4SSt9 = 78,
   kFp8W4St9 = 79,
+  kF32W4NB = 80,         // exact-fp32 W4 with a branch-free K-loop (round 6)
 };
 
 }  // namespace pdmb

@@ -25,6 +25,7 @@ static bool is_experiment(int k) {
     case kF32W4B32: case kF32_256p: case kMfmaW4SNoFrag: case kMfmaW4SNoDma: case kMfmaW4SNoEpi:
     case kMfmaW4SMfmaOnly: case kMfmaW4STall: case kMfmaW4SWide: case kMfmaW4SSnake: case kMfmaW4SMcol:
     case kFp8W4SK4: case kFp8W4SK4TS: case kMfmaW4SSt9: case kMfmaW4St9: case kFp8W4SSt9: case kFp8W4St9:
+    case kF32W4NB:
       return true;
     default:
       return false;
@@ -53,7 +54,7 @@ static int experiment_resolve(const Problem& p, int kernel, bool fast, bool w4, 
     case kF32_256: case kF32NoDma: case kF32_256sDirect: case kF32_256p: return f32fast ? kernel : -1;
     case kT128Unfused: return t128 ? kernel : -1;
     case kF32T128B32: return p.dtype == kF32 && supports(p, kF32T128) ? kernel : -1;
-    case kF32W4B32: return f32fast ? kernel : -1;
+    case kF32W4B32: case kF32W4NB: return f32fast ? kernel : -1;
     case kMfmaW4Unfused: return (p.dtype == kBF16 && w4) ? kernel : -1;
     case kMfma256: case kMfma256b: case kMfma256c: return fast ? kernel : -1;
     case kMfma256X1: case kMfma256X2: case kMfma256X4: case kMfma256Stamp:
@@ -76,7 +77,7 @@ static size_t experiment_workspace_bytes(const Problem& p, int k) {
       k == kMfmaW4Pers || k == kMfmaW4PersTrace)
     return splitk_bytes(p, kMfmaW4, plan(p, kMfmaW4).splitk);
   if (k == kF32T128B32) return splitk_bytes(p, kF32T128, plan(p, kF32T128).splitk);
-  if (k == kF32W4B32) return splitk_bytes(p, kF32W4, plan(p, kF32W4).splitk);
+  if (k == kF32W4B32 || k == kF32W4NB) return splitk_bytes(p, kF32W4, plan(p, kF32W4).splitk);
   return 0;
 }
 
@@ -152,6 +153,7 @@ static hipError_t experiment_launch(const Problem& p, int k, const GemmArgs& a, 
     case kF32_256p: return gemm_f32_256_launch(a, 11, stream);
     case kF32T128B32: return tiled_launch(p, kF32T128, a, p.workspace, p.workspace_bytes, stream, 1);
     case kF32W4B32: return tiled_launch(p, kF32W4, a, p.workspace, p.workspace_bytes, stream, 1);
+    case kF32W4NB: return tiled_launch(p, kF32W4, a, p.workspace, p.workspace_bytes, stream, 2);
     case kMfma256X1: case kMfma256X2: case kMfma256X4:
       return gemm256_launch(p.dtype, a, 10 + (k - kMfma256X1 + 1), stream);
     default: return hipErrorInvalidValue;
@@ -189,6 +191,7 @@ static const char* experiment_name(int kernel) {
     case kMfmaW4Unfused: return "pdmb_w4_nn_unfused";
     case kF32T128B32: return "pdmb_f32_t128_b32";
     case kF32W4B32: return "pdmb_f32_w4_b32";
+    case kF32W4NB: return "pdmb_f32_w4_nb";
     case kFp8W4Trace: return "pdmb_fp8_w4_nt_trace";
     case kMfmaW4SNoFrag: return "pdmb_w4s_diag_nofrag";
     case kMfmaW4SNoDma: return "pdmb_w4s_diag_nodma";

@@ -158,7 +158,16 @@ __device__ __forceinline__ void half_step(const Ctx& c, const char* smem, f32x4 
 }
 
 // BV: b128 B reads (column-permuted MFMAs) instead of b32 ones.
-template <bool BV>
+// NB (experiments, round 6: kF32W4NB): a branch-free K-loop. The shipping loop
+// skips the last two tiles' DMA pieces and the last tile's fragment reads
+// with runtime conditions: hipcc puts a branch around each of the 16 DMA
+// pieces and the reads, 32 branches per 512 MFMAs (PMC: 0.067 branches per
+// MFMA against hipBLASLt's 0.002, 95.4 % MFMA busy against its 98.9 %,
+// profiles/r8h_*). NB always issues all 16 pieces (the last two tiles
+// re-read their own K-tile into the stage they just released: harmless, as
+// W4's clamped tail DMAs) and always reads the next fragments (the last
+// tile's are never used).
+template <bool BV, bool NB = false>
 __global__ void __launch_bounds__(NT, 1) gemm_f32_w4(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
@@ -250,13 +259,16 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4(GemmArgs a) {
   for (int t = 0; t < nk; ++t) {
     const int s = t & 1;
     const bool more = t + 1 < nk, more2 = t + 2 < nk;
-    const int td = more2 ? t + 2 : t;  // the last two tiles issue no DMA (np = 0)
+    const int td = more2 ? t + 2 : t;  // the last two tiles issue no DMA (np = 0; NB: a re-read)
     const u32x4 ra = rsrc_a(td), rb = rsrc_b(td);
     half_step(c, smem, acc, h0, h1, s, 1, wr, wc, l16, g, ra, rb, s, 0, 0);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    half_step(c, smem, acc, h1, h0, s ^ 1, more ? 0 : -1, wr, wc, l16, g, ra, rb, s,
-              0, more2 ? 16 : 0);
+    if constexpr (NB)
+      half_step(c, smem, acc, h1, h0, s ^ 1, 0, wr, wc, l16, g, ra, rb, s, 0, 16);
+    else
+      half_step(c, smem, acc, h1, h0, s ^ 1, more ? 0 : -1, wr, wc, l16, g, ra, rb, s,
+                0, more2 ? 16 : 0);
   }
   // Give the last MFMAs time to write their AGPRs (asm MFMAs are invisible to
   // hipcc's hazard recognizer).
@@ -327,6 +339,11 @@ hipError_t gemm_f32_w4_launch(GemmArgs a, hipStream_t stream, int variant) {
 #ifdef PDMB_EXPERIMENTS
   if (variant == 1) {
     hipLaunchKernelGGL(kf32w4::gemm_f32_w4<false>, dim3((unsigned)nblocks), dim3(kf32w4::NT), 0, stream, a);
+    return hipGetLastError();
+  }
+  if (variant == 2) {  // kF32W4NB: the branch-free K-loop
+    hipLaunchKernelGGL((kf32w4::gemm_f32_w4<true, true>), dim3((unsigned)nblocks), dim3(kf32w4::NT), 0, stream,
+                       a);
     return hipGetLastError();
   }
 #endif

@@ -62,6 +62,18 @@ def main(d, cycle=None):
         split = "n/a" if wa is None else f"{wa / 1e9:.2f} : {wi / 1e9:.2f} : {ac / 1e9:.2f} (×1e9)"
         print(f"| `{k}` | {t:.0f} | {f(clk, '.3f')} | {f(util, '.1%')} | {f(l2, '.1%')} | "
               f"{f(bc, '.3g')} / {f(la, '.3g')} | {split} |")
+    if any(c.get("SQ_INSTS_MFMA") for c in cnt.values()):
+        print()
+        print("| kernel | MFMA insts | VALU / MFMA | SALU / MFMA | LDS / MFMA | SMEM / MFMA | VMEM / MFMA | BRANCH / MFMA |")
+        print("|---|---|---|---|---|---|---|---|")
+        for k, c in cnt.items():
+            med = lambda n: statistics.median(c[n][1:] if len(c[n]) > 2 else c[n]) if c.get(n) else None  # noqa: E731
+            mf = med("SQ_INSTS_MFMA")
+            if not mf:
+                continue
+            r = lambda n: "n/a" if med(n) is None else f"{med(n) / mf:.4f}"  # noqa: E731
+            print(f"| `{k}` | {mf:.4g} | {r('SQ_INSTS_VALU')} | {r('SQ_INSTS_SALU')} | {r('SQ_INSTS_LDS')} | "
+                  f"{r('SQ_INSTS_SMEM')} | {r('SQ_INSTS_VMEM')} | {r('SQ_INSTS_BRANCH')} |")
     return 0
 
 
