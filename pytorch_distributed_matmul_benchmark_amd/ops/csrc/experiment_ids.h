@@ -66,6 +66,17 @@ enum ExperimentKernel : int {
   kFp8W4SSt9 = 78,
   kFp8W4St9 = 79,
   kF32W4NB = 80,         // exact-fp32 W4 with a branch-free K-loop (round 6)
+  kF32W4NBP = 81,        // kF32W4NB with 1024-B B rows: conflict-free b128 B reads (round 6)
+  kF32W4NoDma = 82,      // timing-only kF32W4NBP diagnostics (WRONG results): no DMA refills,
+  kF32W4NoFrag = 83,     //   no fragment reads,
+  kF32W4MfmaBar = 84,    //   MFMAs and the mid-tile barrier only,
+  kF32W4MfmaOnly = 85,   //   MFMAs only
+  kF32W4Spread = 86,     // kF32W4NBP with the DMA pieces and fragment reads spread over each half,
+  kF32W4SpreadDma = 87,  //   the DMA pieces only,
+  kF32W4SpreadRd = 88,   //   the fragment reads only
+  kF32W4Lean = 89,       // kF32W4NBP with a third of the SALU per K-tile (descriptors built once)
+  kF32W4Lean2 = 90,      // kF32W4Lean without the s_nop per DMA piece
+  kF32W4S = 91,          // the streamed persistent form of kF32W4Lean2
 };
 
 }  // namespace pdmb

@@ -25,7 +25,9 @@ static bool is_experiment(int k) {
     case kF32W4B32: case kF32_256p: case kMfmaW4SNoFrag: case kMfmaW4SNoDma: case kMfmaW4SNoEpi:
     case kMfmaW4SMfmaOnly: case kMfmaW4STall: case kMfmaW4SWide: case kMfmaW4SSnake: case kMfmaW4SMcol:
     case kFp8W4SK4: case kFp8W4SK4TS: case kMfmaW4SSt9: case kMfmaW4St9: case kFp8W4SSt9: case kFp8W4St9:
-    case kF32W4NB:
+    case kF32W4NB: case kF32W4NBP: case kF32W4NoDma: case kF32W4NoFrag: case kF32W4MfmaBar:
+    case kF32W4MfmaOnly: case kF32W4Spread: case kF32W4SpreadDma: case kF32W4SpreadRd:
+    case kF32W4Lean: case kF32W4Lean2: case kF32W4S:
       return true;
     default:
       return false;
@@ -54,7 +56,15 @@ static int experiment_resolve(const Problem& p, int kernel, bool fast, bool w4, 
     case kF32_256: case kF32NoDma: case kF32_256sDirect: case kF32_256p: return f32fast ? kernel : -1;
     case kT128Unfused: return t128 ? kernel : -1;
     case kF32T128B32: return p.dtype == kF32 && supports(p, kF32T128) ? kernel : -1;
-    case kF32W4B32: case kF32W4NB: return f32fast ? kernel : -1;
+    case kF32W4B32: case kF32W4NB: case kF32W4NBP: case kF32W4NoDma: case kF32W4NoFrag:
+    case kF32W4MfmaBar: case kF32W4MfmaOnly: case kF32W4Spread: case kF32W4SpreadDma: case kF32W4SpreadRd:
+    case kF32W4Lean: case kF32W4Lean2:
+      return f32fast ? kernel : -1;
+    case kF32W4S:
+      return f32fast && (p.K / 32) % 2 == 0 && p.K / 32 >= 4 && p.M % 256 == 0 && p.N % 256 == 0 &&
+                     device_cus() % 8 == 0
+                 ? kernel
+                 : -1;
     case kMfmaW4Unfused: return (p.dtype == kBF16 && w4) ? kernel : -1;
     case kMfma256: case kMfma256b: case kMfma256c: return fast ? kernel : -1;
     case kMfma256X1: case kMfma256X2: case kMfma256X4: case kMfma256Stamp:
@@ -77,7 +87,7 @@ static size_t experiment_workspace_bytes(const Problem& p, int k) {
       k == kMfmaW4Pers || k == kMfmaW4PersTrace)
     return splitk_bytes(p, kMfmaW4, plan(p, kMfmaW4).splitk);
   if (k == kF32T128B32) return splitk_bytes(p, kF32T128, plan(p, kF32T128).splitk);
-  if (k == kF32W4B32 || k == kF32W4NB) return splitk_bytes(p, kF32W4, plan(p, kF32W4).splitk);
+  if (k == kF32W4B32 || (k >= kF32W4NB && k <= kF32W4Lean2)) return splitk_bytes(p, kF32W4, plan(p, kF32W4).splitk);
   return 0;
 }
 
@@ -154,6 +164,19 @@ static hipError_t experiment_launch(const Problem& p, int k, const GemmArgs& a, 
     case kF32T128B32: return tiled_launch(p, kF32T128, a, p.workspace, p.workspace_bytes, stream, 1);
     case kF32W4B32: return tiled_launch(p, kF32W4, a, p.workspace, p.workspace_bytes, stream, 1);
     case kF32W4NB: return tiled_launch(p, kF32W4, a, p.workspace, p.workspace_bytes, stream, 2);
+    case kF32W4NBP: return tiled_launch(p, kF32W4, a, p.workspace, p.workspace_bytes, stream, 3);
+    case kF32W4NoDma: case kF32W4NoFrag: case kF32W4MfmaBar: case kF32W4MfmaOnly:
+      return tiled_launch(p, kF32W4, a, p.workspace, p.workspace_bytes, stream, 4 + (k - kF32W4NoDma));
+    case kF32W4Spread: case kF32W4SpreadDma: case kF32W4SpreadRd:
+      return tiled_launch(p, kF32W4, a, p.workspace, p.workspace_bytes, stream, 8 + (k - kF32W4Spread));
+    case kF32W4Lean: return tiled_launch(p, kF32W4, a, p.workspace, p.workspace_bytes, stream, 11);
+    case kF32W4Lean2: return tiled_launch(p, kF32W4, a, p.workspace, p.workspace_bytes, stream, 12);
+    case kF32W4S: {
+      GemmArgs s = a;
+      s.splitk = 1;
+      s.pers_grid = ((p.cus > 0 ? p.cus : device_cus()) / 8) * 8;
+      return gemm_f32_w4_launch(s, stream, 14);
+    }
     case kMfma256X1: case kMfma256X2: case kMfma256X4:
       return gemm256_launch(p.dtype, a, 10 + (k - kMfma256X1 + 1), stream);
     default: return hipErrorInvalidValue;
@@ -192,6 +215,17 @@ static const char* experiment_name(int kernel) {
     case kF32T128B32: return "pdmb_f32_t128_b32";
     case kF32W4B32: return "pdmb_f32_w4_b32";
     case kF32W4NB: return "pdmb_f32_w4_nb";
+    case kF32W4NBP: return "pdmb_f32_w4_nbp";
+    case kF32W4NoDma: return "pdmb_f32_w4_diag_nodma";
+    case kF32W4NoFrag: return "pdmb_f32_w4_diag_nofrag";
+    case kF32W4MfmaBar: return "pdmb_f32_w4_diag_mfma_bar";
+    case kF32W4MfmaOnly: return "pdmb_f32_w4_diag_mfma_only";
+    case kF32W4Spread: return "pdmb_f32_w4_spread";
+    case kF32W4SpreadDma: return "pdmb_f32_w4_spread_dma";
+    case kF32W4SpreadRd: return "pdmb_f32_w4_spread_rd";
+    case kF32W4Lean: return "pdmb_f32_w4_lean";
+    case kF32W4Lean2: return "pdmb_f32_w4_lean2";
+    case kF32W4S: return "pdmb_f32_w4s";
     case kFp8W4Trace: return "pdmb_fp8_w4_nt_trace";
     case kMfmaW4SNoFrag: return "pdmb_w4s_diag_nofrag";
     case kMfmaW4SNoDma: return "pdmb_w4s_diag_nodma";

@@ -39,13 +39,27 @@ namespace kf32w4 {
 
 constexpr int BM = 256, BN = 256, BK = 32, NT = 256;
 constexpr int A_BYTES = BM * BK * 4;      // 32 KiB
-constexpr int B_PITCH = (BN + 4) * 4;     // 1040 B per k-row
-constexpr int B_BYTES = BK * B_PITCH;     // 33,280 B
-constexpr int STAGE = A_BYTES + B_BYTES;  // 66,048 B (16-B multiple)
-constexpr int LDS_BYTES = 2 * STAGE;      // 132,096 B
+// B k-row pitch: 1040 B (BP false) or 1024 B (BP, experiments: kF32W4NBP).
+// With 1040-B rows the b128 B reads of lane groups g and g + 1 (k-rows 4
+// apart = 4160 B, 64 B mod the 256-B bank row) overlap on 4 bank quads in
+// every ds_read_b128 lane group ({0-3,12-15} of g against {4-11} of g + 1,
+// MI355X_MICROARCH.md LDS table): 2-way, 4 extra cycles per read, exactly
+// the 5.4e8 conflict cycles of profiles/r8h_*; 1024-B rows put a group's 16
+// lanes on 16 distinct quads (gemm_f32_tile.hip kBSwz). The pad only helps
+// the b32 reads (BV false).
+template <bool BP>
+constexpr int b_pitch() { return BP ? BN * 4 : (BN + 4) * 4; }
+template <bool BP>
+constexpr int stage_bytes() { return A_BYTES + BK * b_pitch<BP>(); }  // 66,048 / 65,536 B
+constexpr int B_PITCH = b_pitch<false>();
+constexpr int STAGE = stage_bytes<false>();
+constexpr int LDS_BYTES = 2 * STAGE;      // 132,096 B (the BP stages fit in it)
 
 __device__ __forceinline__ void mfma(f32x4& acc, float b, float a) {
   asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+}
+__device__ __forceinline__ void mfma_zero(f32x4& acc, float b, float a) {
+  asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, 0" : "=&a"(acc) : "v"(b), "v"(a));
 }
 
 // LDS-DMA with a scalar offset; M0 is clobbered (declared), not saved.
@@ -56,6 +70,31 @@ __device__ __forceinline__ void dma16_m0(u32x4 rsrc, uint32_t voff, uint32_t sof
       "buffer_load_dwordx4 %0, %1, %2 offen lds"
       :
       : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds)
+      : "memory", "m0");
+}
+
+// LN (experiments): M0 = an SGPR stage base + the piece's constant LDS
+// offset in one SALU (the plain form computes the address, then moves it).
+__device__ __forceinline__ void dma16_m0i(u32x4 rsrc, uint32_t voff, uint32_t soff, uint32_t base, int imm) {
+  asm volatile(
+      "s_add_u32 m0, %3, %4\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %0, %1, %2 offen lds"
+      :
+      : "v"(voff), "s"(rsrc), "s"(soff), "s"(base), "i"(imm)
+      : "memory", "m0");
+}
+
+// LN >= 2 (experiments): the DMA piece fused with its gap's MFMA, which is
+// the one wait state the M0 write needs before the LDS-DMA (no s_nop).
+__device__ __forceinline__ void mfma_dma(f32x4& acc, float b, float a, u32x4 rsrc, uint32_t voff,
+                                         uint32_t soff, uint32_t base, int imm) {
+  asm volatile(
+      "s_add_u32 m0, %5, %6\n\t"
+      "v_mfma_f32_16x16x4_f32 %0, %1, %2, %0\n\t"
+      "buffer_load_dwordx4 %3, %4, %7 offen lds"
+      : "+a"(acc)
+      : "v"(b), "v"(a), "v"(voff), "s"(rsrc), "s"(base), "i"(imm), "s"(soff)
       : "memory", "m0");
 }
 
@@ -87,46 +126,70 @@ struct Half<true> {
 // DMA piece h (0..15) of K-tile `tile` into stage `stg`: h < 8: A rows
 // (h*4 + wu)*8 + [0,8) (8 x 128 B); h >= 8: B k-row (h-8)*4 + wu (1 KiB).
 // A's swizzle depends on (r >> 1) & 7, which the h*32-row offset keeps.
+template <bool BP>
 __device__ __forceinline__ void issue_piece(const Ctx& c, u32x4 ra, u32x4 rb, int stg, int h) {
+  constexpr int ST = stage_bytes<BP>();
   if (h < 8) {
     dma16_m0(ra, c.voffA, (uint32_t)(h * 32 * c.lda4),
-             c.lds0 + stg * STAGE + ((h * 4 + c.wu) * 8) * 128);
+             c.lds0 + stg * ST + ((h * 4 + c.wu) * 8) * 128);
   } else {
     const int kr = (h - 8) * 4 + c.wu;
-    dma16_m0(rb, c.voffB, (uint32_t)((h - 8) * 4 * c.ldb4), c.lds0 + stg * STAGE + A_BYTES + kr * B_PITCH);
+    dma16_m0(rb, c.voffB, (uint32_t)((h - 8) * 4 * c.ldb4), c.lds0 + stg * ST + A_BYTES + kr * b_pitch<BP>());
   }
+}
+
+// LN (experiments): piece h of the K-tile whose A / B voffsets are vA / vB (the
+// K-tile offset rides in the voffset, so the descriptors are the slice's, set
+// once), into the stage at LDS byte `base`.
+template <bool BP>
+__device__ __forceinline__ void issue_piece_ln(const Ctx& c, u32x4 ra, u32x4 rb, uint32_t vA, uint32_t vB,
+                                               uint32_t base, int h) {
+  static_assert(BP, "LN: the A piece and B k-row wave offsets are both wu * 1 KiB");
+  if (h < 8)  // A rows (h * 4 + wu) * 8 + [0, 8): wu * 1 KiB rides in `base`
+    dma16_m0i(ra, vA, (uint32_t)(h * 32 * c.lda4), base, h * 4096);
+  else  // B k-row (h - 8) * 4 + wu
+    dma16_m0i(rb, vB, (uint32_t)((h - 8) * 4 * c.ldb4), base, A_BYTES + (h - 8) * 4 * 1024);
 }
 
 // Fragment reads of 16-k block kb from stage stg. mi / ni index the wave's
 // 8 row blocks / 8 column blocks; each is issued separately so the schedule
 // can place it in an MFMA gap.
+template <bool BP>
 __device__ __forceinline__ f32x4 read_a(const char* smem, int stg, int kb, int mi, int wr, int l16,
                                         int g) {
   const int r = wr * 128 + mi * 16 + l16;
   const int ch = (kb * 4 + g) ^ ((r >> 1) & 7);
-  return *(const f32x4*)(smem + stg * STAGE + r * 128 + ch * 16);
+  return *(const f32x4*)(smem + stg * stage_bytes<BP>() + r * 128 + ch * 16);
 }
+template <bool BP>
 __device__ __forceinline__ float read_b(const char* smem, int stg, int kb, int ni, int e, int wc,
                                         int l16, int g) {
   const int k = kb * 16 + 4 * g + e;
   const int col = wc * 128 + ni * 16 + l16;
-  return *(const float*)(smem + stg * STAGE + A_BYTES + k * B_PITCH + col * 4);
+  return *(const float*)(smem + stg * stage_bytes<BP>() + A_BYTES + k * b_pitch<BP>() + col * 4);
 }
+template <bool BP>
 __device__ __forceinline__ f32x4 read_b4(const char* smem, int stg, int kb, int h, int e, int wc,
                                          int l16, int g) {
   const int k = kb * 16 + 4 * g + e;
   const int col = wc * 128 + h * 64 + 4 * l16;
-  return *(const f32x4*)(smem + stg * STAGE + A_BYTES + k * B_PITCH + col * 4);
+  return *(const f32x4*)(smem + stg * stage_bytes<BP>() + A_BYTES + k * b_pitch<BP>() + col * 4);
 }
 
 // One 16-k half: 256 MFMAs from `cur`; in their gaps read the other half's
 // fragments into `nxt` (kb_next >= 0) and issue DMA pieces [p0, p0 + np) of
-// the next tile (one per 4 MFMAs from the start).
-template <bool BV>
+// the next tile (one per 4 MFMAs from the start). DG: the timing-only
+// diagnostic bits of gemm_f32_w4 (1: no DMA, 2: no fragment reads). SP
+// (experiments): bit 1 spreads the DMA pieces one per 16 MFMAs over the whole
+// half (instead of one per 4 over its first quarter), bit 2 the fragment reads
+// one per 12 over its first three quarters (the phases 15 mod 16 and 5 mod 12
+// never meet).
+template <bool BV, bool BP, int DG = 0, int SP = 0, int LN = 0, bool ZERO = false>
 __device__ __forceinline__ void half_step(const Ctx& c, const char* smem, f32x4 (&acc)[8][8],
                                           const Half<BV>& cur, Half<BV>& nxt, int stg_rd, int kb_next,
                                           int wr, int wc, int l16, int g, u32x4 ra, u32x4 rb,
-                                          int stg_dma, int p0, int np) {
+                                          int stg_dma, int p0, int np, uint32_t vA = 0, uint32_t vB = 0,
+                                          uint32_t mbase = 0) {
 #pragma unroll
   for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -134,23 +197,51 @@ __device__ __forceinline__ void half_step(const Ctx& c, const char* smem, f32x4 
 #pragma unroll
       for (int ni = 0; ni < 8; ++ni) {
         const int gap = (e * 8 + mi) * 8 + ni;  // 0..255
-        if constexpr (BV)
+        constexpr int DP = (SP & 1) ? 16 : 4, DR = (SP & 1) ? 15 : 3;  // DMA period / phase
+        constexpr int RP = (SP & 2) ? 12 : 4, RR = (SP & 2) ? 5 : 1;   // read period / phase
+        static_assert(!(SP & 2) || BV, "spread reads: b128 B reads only");
+        if constexpr (LN >= 2) {
+          static_assert(BV && BP && DG == 0, "LN 2: on the b128, 1 KiB-row kernel");
+          if (gap % DP == DR && gap / DP < np) {  // MFMA + DMA piece h in one asm block
+            const int h = p0 + gap / DP;
+            if (h < 8)
+              mfma_dma(acc[mi][ni], cur.b4[e][ni >> 2][ni & 3], cur.a[mi][e], ra, vA,
+                       (uint32_t)(h * 32 * c.lda4), mbase, h * 4096);
+            else
+              mfma_dma(acc[mi][ni], cur.b4[e][ni >> 2][ni & 3], cur.a[mi][e], rb, vB,
+                       (uint32_t)((h - 8) * 4 * c.ldb4), mbase, A_BYTES + (h - 8) * 4096);
+            __builtin_amdgcn_sched_barrier(0);
+            continue;
+          }
+        }
+        if constexpr (ZERO && BV) {  // a streamed tile's K-tile 0: e == 0 starts each accumulator
+          if (e == 0)
+            mfma_zero(acc[mi][ni], cur.b4[e][ni >> 2][ni & 3], cur.a[mi][e]);
+          else
+            mfma(acc[mi][ni], cur.b4[e][ni >> 2][ni & 3], cur.a[mi][e]);
+        } else if constexpr (BV) {
           mfma(acc[mi][ni], cur.b4[e][ni >> 2][ni & 3], cur.a[mi][e]);
-        else
+        } else {
           mfma(acc[mi][ni], cur.b[ni][e], cur.a[mi][e]);
-        if (gap % 4 == 3 && gap / 4 < np) {
-          issue_piece(c, ra, rb, stg_dma, p0 + gap / 4);
-        } else if (kb_next >= 0 && gap % 4 == 1 && gap / 4 < (BV ? 16 : 40)) {
-          // 8 A rows (b128) then the B reads (BV: 8 b128; else 32 b32), one per 4 MFMAs
-          const int q = gap / 4;
+        }
+        if (gap % DP == DR && gap / DP < np) {
+          if constexpr (DG & 1) continue;
+          if constexpr (LN)
+            issue_piece_ln<BP>(c, ra, rb, vA, vB, mbase, p0 + gap / DP);
+          else
+            issue_piece<BP>(c, ra, rb, stg_dma, p0 + gap / DP);
+        } else if (kb_next >= 0 && gap % RP == RR && gap / RP < (BV ? 16 : 40)) {
+          if constexpr (DG & 2) continue;
+          // 8 A rows (b128) then the B reads (BV: 8 b128; else 32 b32), one per RP MFMAs
+          const int q = gap / RP;
           if (q < 8) {
-            nxt.a[q] = read_a(smem, stg_rd, kb_next, q, wr, l16, g);
+            nxt.a[q] = read_a<BP>(smem, stg_rd, kb_next, q, wr, l16, g);
           } else if constexpr (BV) {
             const int e2 = (q - 8) >> 1, h2 = (q - 8) & 1;
-            nxt.b4[e2][h2] = read_b4(smem, stg_rd, kb_next, h2, e2, wc, l16, g);
+            nxt.b4[e2][h2] = read_b4<BP>(smem, stg_rd, kb_next, h2, e2, wc, l16, g);
           } else {
             const int e2 = (q - 8) >> 3, ni2 = (q - 8) & 7;
-            nxt.b[ni2][e2] = read_b(smem, stg_rd, kb_next, ni2, e2, wc, l16, g);
+            nxt.b[ni2][e2] = read_b<BP>(smem, stg_rd, kb_next, ni2, e2, wc, l16, g);
           }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -167,7 +258,22 @@ __device__ __forceinline__ void half_step(const Ctx& c, const char* smem, f32x4 
 // re-read their own K-tile into the stage they just released: harmless, as
 // W4's clamped tail DMAs) and always reads the next fragments (the last
 // tile's are never used).
-template <bool BV, bool NB = false>
+// DG (experiments, round 6: kF32W4NoDma ..., timing-only, WRONG results): bit 1
+// drops the DMA refills, bit 2 the fragment reads, bit 4 the mid-tile wait and
+// barrier — what costs the NB kernel its 97.3 % MFMA busy against hipBLASLt's
+// 98.7 % (profiles/r8l_*).
+// LN (experiments, kF32W4Lean): kF32W4NBP with a third of the SALU work per
+// K-tile: the slice's descriptors are built once and each K-tile's offset rides
+// in the voffsets (two VALU adds) instead of two new descriptors per K-tile
+// (~30 SALU), and M0 takes one SALU per piece (dma16_m0i). r8m: the DMA pieces
+// (with their SALU) cost 0.9 % MFMA busy and the fragment reads 0.6 %; the
+// kernel's 0.14 SALU per MFMA against hipBLASLt's 0.04 is the largest
+// instruction-mix difference left (profiles/r8i_fp32_instruction_mix.md).
+// LN 2 (kF32W4Lean2): also no s_nop per DMA piece (mfma_dma). (Unrolling the
+// K-loop by two to make each stage a constant made hipcc split an accumulator's
+// live range with v_accvgpr moves inside the loop — the hazard class
+// tests/test_mfma_hazards.py screens for — so it is not done.)
+template <bool BV, bool NB = false, bool BP = false, int DG = 0, int SP = 0, int LN = 0>
 __global__ void __launch_bounds__(NT, 1) gemm_f32_w4(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
@@ -226,12 +332,12 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4(GemmArgs a) {
   {
     const u32x4 ra = rsrc_a(0), rb = rsrc_b(0);
 #pragma unroll
-    for (int h = 0; h < 16; ++h) issue_piece(c, ra, rb, 0, h);
+    for (int h = 0; h < 16; ++h) issue_piece<BP>(c, ra, rb, 0, h);
   }
   if (nk > 1) {
     const u32x4 ra = rsrc_a(1), rb = rsrc_b(1);
 #pragma unroll
-    for (int h = 0; h < 16; ++h) issue_piece(c, ra, rb, 1, h);
+    for (int h = 0; h < 16; ++h) issue_piece<BP>(c, ra, rb, 1, h);
     asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
@@ -241,13 +347,13 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4(GemmArgs a) {
   for (int e = 0; e < 4; ++e) {  // in the order the MFMAs consume them
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi)
-      if (e == 0) h0.a[mi] = read_a(smem, 0, 0, mi, wr, l16, g);
+      if (e == 0) h0.a[mi] = read_a<BP>(smem, 0, 0, mi, wr, l16, g);
     if constexpr (BV) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) h0.b4[e][h] = read_b4(smem, 0, 0, h, e, wc, l16, g);
+      for (int h = 0; h < 2; ++h) h0.b4[e][h] = read_b4<BP>(smem, 0, 0, h, e, wc, l16, g);
     } else {
 #pragma unroll
-      for (int ni = 0; ni < 8; ++ni) h0.b[ni][e] = read_b(smem, 0, 0, ni, e, wc, l16, g);
+      for (int ni = 0; ni < 8; ++ni) h0.b[ni][e] = read_b<BP>(smem, 0, 0, ni, e, wc, l16, g);
     }
   }
   // K-tile t (stage s = t & 1; tile t+1 in s ^ 1 was issued a tile ago):
@@ -256,18 +362,31 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4(GemmArgs a) {
   //             s_barrier — so nobody waits at the top of a tile
   //   half 1: MFMAs from h1 | DMA tile t+2 into s | read half 0 of t+1 from
   //           s ^ 1 into h0
+  const u32x4 ra0 = rsrc_a(0), rb0 = rsrc_b(0);  // LN: built once
+  static_assert(!LN || (NB && BP && DG == 0), "LN: on the branch-free 1 KiB-row kernel");
   for (int t = 0; t < nk; ++t) {
     const int s = t & 1;
     const bool more = t + 1 < nk, more2 = t + 2 < nk;
     const int td = more2 ? t + 2 : t;  // the last two tiles issue no DMA (np = 0; NB: a re-read)
+    if constexpr (LN) {
+      // the slice's descriptors; this K-tile's offset in the voffsets
+      const uint32_t vA = c.voffA + (uint32_t)td * (BK * 4), vB = c.voffB + (uint32_t)td * (BK * c.ldb4);
+      const uint32_t mbase = c.lds0 + (uint32_t)s * stage_bytes<BP>() + (uint32_t)c.wu * 1024;
+      half_step<BV, BP, DG, SP, LN>(c, smem, acc, h0, h1, s, 1, wr, wc, l16, g, ra0, rb0, s, 0, 0);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      half_step<BV, BP, DG, SP, LN>(c, smem, acc, h1, h0, s ^ 1, 0, wr, wc, l16, g, ra0, rb0, s, 0, 16, vA, vB,
+                                    mbase);
+      continue;
+    }
     const u32x4 ra = rsrc_a(td), rb = rsrc_b(td);
-    half_step(c, smem, acc, h0, h1, s, 1, wr, wc, l16, g, ra, rb, s, 0, 0);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    half_step<BV, BP, DG, SP, LN>(c, smem, acc, h0, h1, s, 1, wr, wc, l16, g, ra, rb, s, 0, 0);
+    if constexpr (!(DG & 4)) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (NB)
-      half_step(c, smem, acc, h1, h0, s ^ 1, 0, wr, wc, l16, g, ra, rb, s, 0, 16);
+      half_step<BV, BP, DG, SP, LN>(c, smem, acc, h1, h0, s ^ 1, 0, wr, wc, l16, g, ra, rb, s, 0, 16);
     else
-      half_step(c, smem, acc, h1, h0, s ^ 1, more ? 0 : -1, wr, wc, l16, g, ra, rb, s,
+      half_step<BV, BP, DG, SP, LN>(c, smem, acc, h1, h0, s ^ 1, more ? 0 : -1, wr, wc, l16, g, ra, rb, s,
                 0, more2 ? 16 : 0);
   }
   // Give the last MFMAs time to write their AGPRs (asm MFMAs are invisible to
@@ -315,6 +434,195 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4(GemmArgs a) {
   }
 }
 
+// ---- f32_w4s: the streamed persistent form (round 6) ------
+// The lean2 K-loop (1 KiB B rows, descriptors per tile, M0 in one SALU, no
+// s_nop per DMA piece: 98.3 % MFMA busy against hipBLASLt's 98.9 %,
+// profiles/r8p_*) run as ONE K-tile stream per CU, as gemm_w4.hip's W4S does
+// for bf16: the DMA pieces that would fetch K-tiles nk, nk + 1 fetch K-tiles
+// 0, 1 of the CU's next tile, the last K-tile reads the next tile's first
+// fragments as usual, K-tile 0 starts the accumulators with C = 0 (no zeroing
+// pass), and the epilogue leaves through its own LDS region past the two
+// stages (16-row x 64-column blocks, 17 KiB for the four waves) while the
+// next tile's first K-tiles land. Its 64 stores per wave are not drained:
+// vmcnt counts loads, stores and LDS-DMA in issue order, so K-tile 0's
+// mid-tile wait is vmcnt(63) (the counter's largest value: K-tile 1 landed
+// once at most 63 younger stores remain); before the first tile 64 no-access
+// LDS-DMA loads stand in for them. That needs all 64 stores issued on every
+// tile, so only whole tiles run here (M, N multiples of 256: no masked store
+// can be skipped). Tiles are static (workgroup b: b, b + G, ...; G a multiple
+// of 8 keeps a tile on map_tile's XCD); no workgroup waits for another, so
+// residency is not required. Host: unsplit, K / 32 even and >= 4, M % 256 ==
+// N % 256 == 0, K * ldb * 4 < 2^31.
+constexpr int EPI4 = epi_buf_f32<4>();                        // 4352 B per wave
+constexpr int S_STAGE = stage_bytes<true>();                   // 65,536 B
+constexpr int S_LDS = 2 * S_STAGE + 4 * EPI4;                  // 148,480 B
+
+struct TileSrc {
+  u32x4 ra, rb;  // A at row m0 / B at column n0, both from K = 0, to the operand's end
+};
+
+__device__ __forceinline__ TileSrc f32_tile_src(const GemmArgs& a, int bz, int tm, int tn) {
+  const int m0 = tm * BM, n0 = tn * BN;
+  TileSrc t;
+  t.ra = make_rsrc((const char*)a.A + ((long long)bz * a.sA + (long long)m0 * a.lda) * 4,
+                   ((long long)(a.M - m0 - 1) * a.lda + a.K) * 4);
+  t.rb = make_rsrc((const char*)a.B + ((long long)bz * a.sB + n0) * 4,
+                   ((long long)(a.kb - 1) * a.ldb + (a.N - n0)) * 4);
+  return t;
+}
+
+template <int W>
+__device__ __forceinline__ void wait_vm_lgkm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(W) : "memory");
+}
+
+// One K-tile in stage S: half 0 from h0 (reading h1 of this K-tile from S);
+// the mid-tile wait (vmcnt(W): the next K-tile landed; lgkmcnt(0): S read);
+// half 1 from h1, refilling S with the K-tile two ahead (descriptors ra / rb,
+// voffsets vA / vB) and reading h0 of the next K-tile from S ^ 1.
+template <int W, bool ZERO>
+__device__ __forceinline__ void ktile_s(const Ctx& c, const char* smem, f32x4 (&acc)[8][8], Half<true>& h0,
+                                        Half<true>& h1, int S, int wr, int wc, int l16, int g, u32x4 ra,
+                                        u32x4 rb, uint32_t vA, uint32_t vB, uint32_t mbase) {
+  half_step<true, true, 0, 0, 2, ZERO>(c, smem, acc, h0, h1, S, 1, wr, wc, l16, g, ra, rb, S, 0, 0);
+  wait_vm_lgkm_barrier<W>();
+  __builtin_amdgcn_sched_barrier(0);
+  half_step<true, true, 0, 0, 2>(c, smem, acc, h1, h0, S ^ 1, 0, wr, wc, l16, g, ra, rb, S, 0, 16, vA, vB,
+                                 mbase);
+}
+
+__global__ void __launch_bounds__(NT, 1) gemm_f32_w4s(GemmArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[S_LDS];
+  const int T = a.tiles_m * a.tiles_n * a.batch;
+  const int G = gridDim.x;
+  int vb = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wu >> 1, wc = wu & 1;
+  const int l16 = lane & 15, g = lane >> 4;
+
+  Ctx c;
+  c.wu = wu;
+  c.lds0 = (uint32_t)(size_t)((lds_void*)smem);
+  c.lda4 = a.lda * 4;
+  c.ldb4 = a.ldb * 4;
+  c.nk = a.K / BK;
+  {
+    const int r = wu * 8 + (lane >> 3);  // row of A piece 0
+    c.voffA = (uint32_t)(r * c.lda4 + (((lane & 7) ^ ((r >> 1) & 7)) * 16));
+    c.voffB = (uint32_t)(wu * c.ldb4 + lane * 16);  // k-row wu of piece 8
+  }
+  const int nk = c.nk;
+  const uint32_t kA = BK * 4, kB = (uint32_t)(BK * c.ldb4);  // voffset steps per K-tile
+  const uint32_t mb0 = c.lds0 + (uint32_t)wu * 1024, mb1 = mb0 + S_STAGE;
+
+  int bz, tm, tn;
+  map_tile(a, vb, bz, tm, tn);
+  TileSrc cur = f32_tile_src(a, bz, tm, tn);
+  int nvb = vb + G, nbz = bz, ntm = tm, ntn = tn;
+  TileSrc nxt = cur;
+  if (nvb < T) {
+    map_tile(a, nvb, nbz, ntm, ntn);
+    nxt = f32_tile_src(a, nbz, ntm, ntn);
+  }
+
+  // Prologue of the first tile: K-tiles 0, 1 -> stages 0, 1; K-tile 0 landed
+  // everywhere; its first half's fragments.
+#pragma unroll
+  for (int h = 0; h < 16; ++h) issue_piece_ln<true>(c, cur.ra, cur.rb, c.voffA, c.voffB, mb0, h);
+#pragma unroll
+  for (int h = 0; h < 16; ++h) issue_piece_ln<true>(c, cur.ra, cur.rb, c.voffA + kA, c.voffB + kB, mb1, h);
+  asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+  Half<true> h0, h1;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+      if (e == 0) h0.a[mi] = read_a<true>(smem, 0, 0, mi, wr, l16, g);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) h0.b4[e][h] = read_b4<true>(smem, 0, 0, h, e, wc, l16, g);
+  }
+  char* ebuf = smem + 2 * S_STAGE + wu * EPI4;
+  {  // 64 no-access loads (num_records 0: zeros into this wave's epilogue buffer)
+    u32x4 nul;
+    nul.x = 0u;
+    nul.y = 0u;
+    nul.z = 0u;
+    nul.w = 0x00020000u;
+    const uint32_t eb = c.lds0 + 2 * S_STAGE + wu * EPI4;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) dma16_m0(nul, 0u, 0u, eb);
+  }
+
+  // Started by each tile's K-tile 0 (ZERO: C = 0 in the first MFMA of every
+  // accumulator). Zeroing them with v_accvgpr_write instead put each write 1-4
+  // instructions before the asm MFMA reading it: a VALU-write / MFMA-read
+  // hazard hipcc cannot see.
+  f32x4 acc[8][8];
+  for (;;) {
+    const bool more = nvb < T;
+    // K-tile 0 (stage 0): the 64 stores (or stand-ins) are younger than K-tile 1
+    ktile_s<63, true>(c, smem, acc, h0, h1, 0, wr, wc, l16, g, cur.ra, cur.rb, c.voffA + 2 * kA,
+                      c.voffB + 2 * kB, mb0);
+    int t = 1;
+    for (; t + 2 < nk; ++t)
+      ktile_s<0, false>(c, smem, acc, h0, h1, t & 1, wr, wc, l16, g, cur.ra, cur.rb,
+                        c.voffA + (uint32_t)(t + 2) * kA, c.voffB + (uint32_t)(t + 2) * kB, (t & 1) ? mb1 : mb0);
+    {
+      // K-tiles nk - 2 (stage 0), nk - 1 (stage 1): their refills are the next
+      // tile's K-tiles 0 and 1 — or, on the last tile, re-reads of this tile's
+      // last K-tile into stages nobody reads again
+      const u32x4 ra = more ? nxt.ra : cur.ra, rb = more ? nxt.rb : cur.rb;
+      const uint32_t k0 = more ? 0u : (uint32_t)(nk - 1), k1 = more ? 1u : (uint32_t)(nk - 1);
+      ktile_s<0, false>(c, smem, acc, h0, h1, 0, wr, wc, l16, g, ra, rb, c.voffA + k0 * kA, c.voffB + k0 * kB,
+                        mb0);
+      ktile_s<0, false>(c, smem, acc, h0, h1, 1, wr, wc, l16, g, ra, rb, c.voffA + k1 * kA, c.voffB + k1 * kB,
+                        mb1);
+    }
+    // The last MFMAs write their AGPRs before the epilogue reads them (asm
+    // MFMAs are invisible to hipcc's hazard recognizer). Every accumulator is
+    // an operand of the padding, so no register copy of one (the epilogue's
+    // regroup needs AGPR temporaries) can be placed before it.
+    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15"
+                 : "+a"(acc[0][0]), "+a"(acc[0][1]), "+a"(acc[0][2]), "+a"(acc[0][3]), "+a"(acc[0][4]),
+                   "+a"(acc[0][5]), "+a"(acc[0][6]), "+a"(acc[0][7])::"memory");
+#pragma unroll
+    for (int i = 1; i < 8; ++i)
+      asm volatile(""
+                   : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]), "+a"(acc[i][4]),
+                     "+a"(acc[i][5]), "+a"(acc[i][6]), "+a"(acc[i][7]));
+    __builtin_amdgcn_sched_barrier(0);
+    char* Cb = (char*)a.C + (long long)bz * a.sC * 4;
+    const int m0 = tm * BM, n0 = tn * BN;
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {  // acc[mi][4 h + j][r] is column 64 h + 16 g + 4 r + j: regroup by r
+        f32x4 w[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          w[r] = f32x4{acc[mi][4 * h][r], acc[mi][4 * h + 1][r], acc[mi][4 * h + 2][r], acc[mi][4 * h + 3][r]};
+        const int row0 = m0 + wr * 128 + mi * 16, col0 = n0 + wc * 128 + 64 * h;
+        store_block16_f32<false, 4, true>(ebuf, w, Cb, (long long)a.ldc * 4, row0, col0, a.M, a.N, lane);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (!more) break;
+    vb = nvb;
+    bz = nbz;
+    tm = ntm;
+    tn = ntn;
+    cur = nxt;
+    nvb = vb + G;
+    if (nvb < T) {
+      map_tile(a, nvb, nbz, ntm, ntn);
+      nxt = f32_tile_src(a, nbz, ntm, ntn);
+    }
+  }
+  // No LDS-DMA may still be writing when this workgroup's LDS is handed on.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 }  // namespace kf32w4
 
 // a.splitk > 1: split-K with a.part / a.flags (gemm_dispatch.cpp f32_split).
@@ -344,6 +652,41 @@ hipError_t gemm_f32_w4_launch(GemmArgs a, hipStream_t stream, int variant) {
   if (variant == 2) {  // kF32W4NB: the branch-free K-loop
     hipLaunchKernelGGL((kf32w4::gemm_f32_w4<true, true>), dim3((unsigned)nblocks), dim3(kf32w4::NT), 0, stream,
                        a);
+    return hipGetLastError();
+  }
+  if (variant == 3) {  // kF32W4NBP: branch-free, 1024-B B rows (conflict-free b128 reads)
+    hipLaunchKernelGGL((kf32w4::gemm_f32_w4<true, true, true>), dim3((unsigned)nblocks), dim3(kf32w4::NT), 0,
+                       stream, a);
+    return hipGetLastError();
+  }
+  if (variant >= 4 && variant <= 7) {  // timing-only diagnostics of kF32W4NBP (DG 1, 2, 3, 7)
+    auto k = variant == 4 ? kf32w4::gemm_f32_w4<true, true, true, 1>
+           : variant == 5 ? kf32w4::gemm_f32_w4<true, true, true, 2>
+           : variant == 6 ? kf32w4::gemm_f32_w4<true, true, true, 3>
+                          : kf32w4::gemm_f32_w4<true, true, true, 7>;
+    hipLaunchKernelGGL(k, dim3((unsigned)nblocks), dim3(kf32w4::NT), 0, stream, a);
+    return hipGetLastError();
+  }
+  if (variant == 14) {  // kF32W4S: the streamed persistent form (unsplit, pers_grid workgroups)
+    const int nk = a.K / kf32w4::BK;
+    if (S > 1 || a.pers_grid <= 0 || a.pers_grid % 8 || nk % 2 || nk < 4 || a.tile_span || a.tile_end ||
+        a.M % kf32w4::BM || a.N % kf32w4::BN || (long long)a.K * a.ldb * 4 >= (1LL << 31))
+      return hipErrorInvalidValue;
+    const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
+    hipLaunchKernelGGL(kf32w4::gemm_f32_w4s, pg, dim3(kf32w4::NT), 0, stream, a);
+    return hipGetLastError();
+  }
+  if (variant == 11 || variant == 12) {  // kF32W4Lean, kF32W4Lean2
+    auto k = variant == 11 ? kf32w4::gemm_f32_w4<true, true, true, 0, 0, 1>
+                           : kf32w4::gemm_f32_w4<true, true, true, 0, 0, 2>;
+    hipLaunchKernelGGL(k, dim3((unsigned)nblocks), dim3(kf32w4::NT), 0, stream, a);
+    return hipGetLastError();
+  }
+  if (variant >= 8 && variant <= 10) {  // kF32W4Spread*: kF32W4NBP with SP 3, 1, 2
+    auto k = variant == 8 ? kf32w4::gemm_f32_w4<true, true, true, 0, 3>
+           : variant == 9 ? kf32w4::gemm_f32_w4<true, true, true, 0, 1>
+                          : kf32w4::gemm_f32_w4<true, true, true, 0, 2>;
+    hipLaunchKernelGGL(k, dim3((unsigned)nblocks), dim3(kf32w4::NT), 0, stream, a);
     return hipGetLastError();
   }
 #endif

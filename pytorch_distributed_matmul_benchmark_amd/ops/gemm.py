@@ -59,7 +59,10 @@ EXPERIMENT_KERNELS = {"mfma256": 1, "mfma256b": 3, "mfma256c": 4, "mfma256c_stam
                       "diag_w4s_noepi": 58, "diag_w4s_mfma_only": 59, "x_w4s_tall": 70,
                       "x_w4s_wide": 71, "x_w4s_snake": 72, "x_w4s_mcol": 73,
                       "x_fp8_w4s_k4": 74, "x_fp8_w4s_k4_tstore": 75, "x_w4s_st9": 76,
-                      "x_w4_st9": 77, "x_fp8_w4s_st9": 78, "x_fp8_w4_st9": 79, "x_f32_w4_nb": 80}
+                      "x_w4_st9": 77, "x_fp8_w4s_st9": 78, "x_fp8_w4_st9": 79, "x_f32_w4_nb": 80, "x_f32_w4_nbp": 81,
+                      "diag_f32_w4_nodma": 82, "diag_f32_w4_nofrag": 83, "diag_f32_w4_mfma_bar": 84,
+                      "diag_f32_w4_mfma_only": 85, "x_f32_w4_spread": 86, "x_f32_w4_spread_dma": 87,
+                      "x_f32_w4_spread_rd": 88, "x_f32_w4_lean": 89, "x_f32_w4_lean2": 90, "x_f32_w4s": 91}
 KERNEL_NAMES = {0: "auto", 2: "pdmb_generic_nn", 7: "pdmb_f32_256s_nn", 9: "pdmb_mfma256d_nn",
                 16: "pdmb_fp8_w4_nt", 21: "pdmb_w4_nn", 26: "pdmb_t128_nn",
                 27: "pdmb_t128x2_nn", 28: "pdmb_t256x128_nn", 29: "pdmb_f32_w4_nn", 36: "pdmb_w4s",

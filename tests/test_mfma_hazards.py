@@ -128,3 +128,68 @@ def test_parked_accumulator_is_exempt():
 def test_no_valu_write_right_before_an_mfma_read(src):
     found = {name: h for name, body in _kernels(gfx950_asm(src)) if (h := hazards(body))}
     assert not found, {k[:90]: v[:3] for k, v in found.items()}
+
+
+# The other direction (round 6): an MFMA's result read by a VALU instruction
+# (v_accvgpr_read / v_accvgpr_mov of the accumulator, or any VALU source) too
+# soon after the MFMA that writes it. The streamed exact-fp32 kernel's epilogue
+# regroup first had hipcc copy an accumulator tuple ONE instruction after the
+# MFMA that wrote it (profiles/r8lq_fp32_lean_stream.md); every accumulator is
+# now an operand of the s_nop padding instead. The bound checked is 8 wait
+# states: the closest such read in the shipping build is the fp8 tile
+# family's epilogue at 8 (16x16x128 f8f6f4), 13 for its bf16 / fp16 members,
+# >= 25 everywhere else, and the tile family is exact on small integers on the
+# GPU (tests/test_fp8_gpu.py::test_fp8_tile_family_exact, test_gemm_gpu.py).
+NEED_RD = 8
+
+
+def _srcs(ins):
+    op = ins.split()[0]
+    return set().union(*(_regs(t) for t in ins[len(op):].split(",")[1:]))
+
+
+def read_hazards(body):
+    ins = _instructions(body)
+    bad = []
+    for i, line in enumerate(ins):
+        op = line.split()[0]
+        if not op.startswith("v_mfma"):
+            continue
+        dst = _dst(line)
+        states = 0
+        for j in range(i + 1, min(len(ins), i + 40)):
+            pj = ins[j].split()[0]
+            if pj in ("s_branch", "s_setpc_b64", "s_endpgm"):
+                break  # no fall-through: what follows is another block's code
+            if pj == "s_nop":
+                states += int(ins[j].split()[1], 0) + 1
+            else:
+                if pj.startswith("v_") and not pj.startswith("v_mfma") and _srcs(ins[j]) & dst:
+                    bad.append((line, ins[j], states))
+                    break
+                if pj.startswith("v_mfma") and _dst(ins[j]) & dst:
+                    break  # rewritten by the next MFMA (same-pipe ordering)
+                dst = dst - _dst(ins[j])  # overwritten: later reads see that value
+                if not dst:
+                    break
+                states += 1
+            if states >= NEED_RD:
+                break
+    return bad
+
+
+def test_detects_a_copy_right_after_the_mfma():
+    body = "\n".join(["\tv_mfma_f32_16x16x4_f32 a[240:243], v105, v69, a[240:243]", "\ts_nop 0",
+                      "\tv_accvgpr_read_b32 v88, a240"])
+    assert len(read_hazards(body)) == 1
+    ok = body.replace("\ts_nop 0", "\ts_nop 15")
+    assert read_hazards(ok) == []
+    # not reached by fall-through, or the register rewritten first: no hazard
+    assert read_hazards(body.replace("\ts_nop 0", "\ts_branch .LBB0_9\n.LBB0_8:")) == []
+    assert read_hazards(body.replace("\ts_nop 0", "\tv_accvgpr_write_b32 a240, 0")) == []
+
+
+@pytest.mark.parametrize("src", SOURCES)
+def test_no_valu_read_right_after_an_mfma_write(src):
+    found = {name: h for name, body in _kernels(gfx950_asm(src)) if (h := read_hazards(body))}
+    assert not found, {k[:90]: v[:3] for k, v in found.items()}
