@@ -176,6 +176,10 @@ def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -
     flags = f"arch={ARCH};experiments={int(experiments())}"
     if not flags_file.exists() or flags_file.read_text() != flags:
         force = True
+    # Until this build links, the objects may be a mix of flavours (a failed
+    # PDMB_EXPERIMENTS=1 build leaves its objects behind, newer than their
+    # sources): with no flags file, the next build of either flavour starts over.
+    flags_file.unlink(missing_ok=True)
     inc, libdirs = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
     import torch

@@ -573,6 +573,23 @@ void set_debug_buffer(c10::optional<at::Tensor> buf) {
   }
 }
 
+// Diagnostics: a host-mapped, coherent buffer that the stamping kernels of an
+// experiments build write with system-scope stores, readable by the host
+// WHILE a kernel runs (e.g. one that never finishes: scripts/w4s_hang_probe.py).
+int64_t host_stamp_alloc(int64_t bytes) {
+  void* p = nullptr;
+  check_hip(hipHostMalloc(&p, (size_t)bytes, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
+  memset(p, 0xff, (size_t)bytes);
+  pdmb::set_debug_buffer(p);
+  return (int64_t)(uintptr_t)p;
+}
+std::vector<int64_t> host_stamp_read(int64_t ptr, int64_t n) {
+  const volatile long long* q = (const volatile long long*)(uintptr_t)ptr;
+  std::vector<int64_t> out((size_t)n);
+  for (int64_t i = 0; i < n; ++i) out[(size_t)i] = q[i];
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -630,6 +647,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stream_cu_mask", &stream_cu_mask, py::arg("stream"), py::arg("device"));
   m.def("destroy_stream", &destroy_stream, py::arg("stream"));
   m.attr("EXPERIMENTS") = pdmb::experiments_built();
+  m.def("host_stamp_alloc", &host_stamp_alloc, py::arg("bytes"));
+  m.def("host_stamp_read", &host_stamp_read, py::arg("ptr"), py::arg("n"));
   m.attr("MAX_SPLIT_TILES") = pdmb::kMaxSplitTiles;
   m.attr("ARCH") = "gfx950";
 }

@@ -76,7 +76,12 @@ enum ExperimentKernel : int {
   kF32W4SpreadRd = 88,   //   the fragment reads only
   kF32W4Lean = 89,       // kF32W4NBP with a third of the SALU per K-tile (descriptors built once)
   kF32W4Lean2 = 90,      // kF32W4Lean without the s_nop per DMA piece
-  kF32W4S = 91,          // the streamed persistent form of kF32W4Lean2
+  kF32W4S = 91,          // the streamed persistent form of kF32W4Lean2 (hangs, see gemm_f32_w4.hip)
+  kF32T128Lean = 92,     // kF32T128 / kF32T128x2 / kF32T64 / kF32T64x2 with the W4 lean K-loop
+  kF32T128x2Lean = 93,   //   (descriptors built once per slice, K-tile offsets in the voffsets,
+  kF32T64Lean = 94,      //   M0 in one SALU, the DMA piece fused with its gap's MFMA; round 6)
+  kF32T64x2Lean = 95,
+  kF32W4SDbg = 96,       // f32_w4s stamping its progress into a host-mapped buffer (diagnostic)
 };
 
 }  // namespace pdmb

@@ -27,7 +27,8 @@ static bool is_experiment(int k) {
     case kFp8W4SK4: case kFp8W4SK4TS: case kMfmaW4SSt9: case kMfmaW4St9: case kFp8W4SSt9: case kFp8W4St9:
     case kF32W4NB: case kF32W4NBP: case kF32W4NoDma: case kF32W4NoFrag: case kF32W4MfmaBar:
     case kF32W4MfmaOnly: case kF32W4Spread: case kF32W4SpreadDma: case kF32W4SpreadRd:
-    case kF32W4Lean: case kF32W4Lean2: case kF32W4S:
+    case kF32W4Lean: case kF32W4Lean2: case kF32T128Lean: case kF32T128x2Lean: case kF32T64Lean:
+    case kF32T64x2Lean: case kF32W4S: case kF32W4SDbg:
       return true;
     default:
       return false;
@@ -51,20 +52,24 @@ static int experiment_resolve_fp8(const Problem& p, int kernel, bool s_fits) {
   return kernel;
 }
 
+// The shipping kernel whose plan (split) a lean fp32 tile arm runs.
+static int ln_base(int k) {
+  return k == kF32T128Lean ? kF32T128 : k == kF32T128x2Lean ? kF32T128x2 : k == kF32T64Lean ? kF32T64 : kF32T64x2;
+}
+
 static int experiment_resolve(const Problem& p, int kernel, bool fast, bool w4, bool t128, bool f32fast) {
   switch (kernel) {
     case kF32_256: case kF32NoDma: case kF32_256sDirect: case kF32_256p: return f32fast ? kernel : -1;
     case kT128Unfused: return t128 ? kernel : -1;
     case kF32T128B32: return p.dtype == kF32 && supports(p, kF32T128) ? kernel : -1;
+    case kF32W4S: case kF32W4SDbg:
+      return f32fast && gemm_f32_w4s_fits(shape_args(p)) && device_cus() % 8 == 0 ? kernel : -1;
+    case kF32T128Lean: case kF32T128x2Lean: case kF32T64Lean: case kF32T64x2Lean:
+      return p.dtype == kF32 && supports(p, kF32T128) && gemm_f32_tile_ln_fits(shape_args(p)) ? kernel : -1;
     case kF32W4B32: case kF32W4NB: case kF32W4NBP: case kF32W4NoDma: case kF32W4NoFrag:
     case kF32W4MfmaBar: case kF32W4MfmaOnly: case kF32W4Spread: case kF32W4SpreadDma: case kF32W4SpreadRd:
     case kF32W4Lean: case kF32W4Lean2:
       return f32fast ? kernel : -1;
-    case kF32W4S:
-      return f32fast && (p.K / 32) % 2 == 0 && p.K / 32 >= 4 && p.M % 256 == 0 && p.N % 256 == 0 &&
-                     device_cus() % 8 == 0
-                 ? kernel
-                 : -1;
     case kMfmaW4Unfused: return (p.dtype == kBF16 && w4) ? kernel : -1;
     case kMfma256: case kMfma256b: case kMfma256c: return fast ? kernel : -1;
     case kMfma256X1: case kMfma256X2: case kMfma256X4: case kMfma256Stamp:
@@ -87,6 +92,10 @@ static size_t experiment_workspace_bytes(const Problem& p, int k) {
       k == kMfmaW4Pers || k == kMfmaW4PersTrace)
     return splitk_bytes(p, kMfmaW4, plan(p, kMfmaW4).splitk);
   if (k == kF32T128B32) return splitk_bytes(p, kF32T128, plan(p, kF32T128).splitk);
+  if (k >= kF32T128Lean && k <= kF32T64x2Lean) {
+    const int base = ln_base(k);
+    return splitk_bytes(p, base, plan(p, base).splitk);
+  }
   if (k == kF32W4B32 || (k >= kF32W4NB && k <= kF32W4Lean2)) return splitk_bytes(p, kF32W4, plan(p, kF32W4).splitk);
   return 0;
 }
@@ -162,6 +171,14 @@ static hipError_t experiment_launch(const Problem& p, int k, const GemmArgs& a, 
     case kF32_256sDirect: return gemm_f32_256_launch(a, 10, stream);
     case kF32_256p: return gemm_f32_256_launch(a, 11, stream);
     case kF32T128B32: return tiled_launch(p, kF32T128, a, p.workspace, p.workspace_bytes, stream, 1);
+    case kF32W4S: case kF32W4SDbg: {
+      GemmArgs s = a;
+      s.splitk = 1;
+      s.pers_grid = ((p.cus > 0 ? p.cus : device_cus()) / 8) * 8;
+      return gemm_f32_w4_launch(s, stream, k == kF32W4S ? 14 : 15);
+    }
+    case kF32T128Lean: case kF32T128x2Lean: case kF32T64Lean: case kF32T64x2Lean:
+      return tiled_launch(p, ln_base(k), a, p.workspace, p.workspace_bytes, stream, 5 + (k - kF32T128Lean));
     case kF32W4B32: return tiled_launch(p, kF32W4, a, p.workspace, p.workspace_bytes, stream, 1);
     case kF32W4NB: return tiled_launch(p, kF32W4, a, p.workspace, p.workspace_bytes, stream, 2);
     case kF32W4NBP: return tiled_launch(p, kF32W4, a, p.workspace, p.workspace_bytes, stream, 3);
@@ -171,12 +188,6 @@ static hipError_t experiment_launch(const Problem& p, int k, const GemmArgs& a, 
       return tiled_launch(p, kF32W4, a, p.workspace, p.workspace_bytes, stream, 8 + (k - kF32W4Spread));
     case kF32W4Lean: return tiled_launch(p, kF32W4, a, p.workspace, p.workspace_bytes, stream, 11);
     case kF32W4Lean2: return tiled_launch(p, kF32W4, a, p.workspace, p.workspace_bytes, stream, 12);
-    case kF32W4S: {
-      GemmArgs s = a;
-      s.splitk = 1;
-      s.pers_grid = ((p.cus > 0 ? p.cus : device_cus()) / 8) * 8;
-      return gemm_f32_w4_launch(s, stream, 14);
-    }
     case kMfma256X1: case kMfma256X2: case kMfma256X4:
       return gemm256_launch(p.dtype, a, 10 + (k - kMfma256X1 + 1), stream);
     default: return hipErrorInvalidValue;
@@ -223,9 +234,14 @@ static const char* experiment_name(int kernel) {
     case kF32W4Spread: return "pdmb_f32_w4_spread";
     case kF32W4SpreadDma: return "pdmb_f32_w4_spread_dma";
     case kF32W4SpreadRd: return "pdmb_f32_w4_spread_rd";
+    case kF32T128Lean: return "pdmb_f32_t128_lean";
+    case kF32T128x2Lean: return "pdmb_f32_t128x2_lean";
+    case kF32T64Lean: return "pdmb_f32_t64_lean";
+    case kF32T64x2Lean: return "pdmb_f32_t64x2_lean";
+    case kF32W4S: return "pdmb_f32_w4s";
+    case kF32W4SDbg: return "pdmb_f32_w4s_dbg";
     case kF32W4Lean: return "pdmb_f32_w4_lean";
     case kF32W4Lean2: return "pdmb_f32_w4_lean2";
-    case kF32W4S: return "pdmb_f32_w4s";
     case kFp8W4Trace: return "pdmb_fp8_w4_nt_trace";
     case kMfmaW4SNoFrag: return "pdmb_w4s_diag_nofrag";
     case kMfmaW4SNoDma: return "pdmb_w4s_diag_nodma";

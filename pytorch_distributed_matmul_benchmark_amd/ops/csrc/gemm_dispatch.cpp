@@ -29,7 +29,9 @@ hipError_t gemm_generic_launch(int dt, GemmArgs a, bool vec, hipStream_t stream)
 bool gemm_f32_256_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 hipError_t gemm_f32_256_launch(GemmArgs a, int variant, hipStream_t stream);
 hipError_t gemm_f32_w4_launch(GemmArgs a, hipStream_t stream, int variant);
+bool gemm_f32_w4s_fits(const GemmArgs& a);  // experiments build: kF32W4S
 bool gemm_f32_tile_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
+bool gemm_f32_tile_ln_fits(const GemmArgs& a);
 hipError_t gemm_f32_tile_launch(GemmArgs a, hipStream_t stream, int variant);
 bool gemm_fp8_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream);

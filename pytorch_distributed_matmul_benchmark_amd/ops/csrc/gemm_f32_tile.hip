@@ -77,6 +77,22 @@ __device__ __forceinline__ void dma16_m0(u32x4 rsrc, uint32_t voff, uint32_t sof
       : "memory", "m0");
 }
 
+// LN (experiments, round 6): the DMA piece fused with its gap's MFMA — M0 =
+// an SGPR stage base + the piece's constant LDS offset in one SALU, and the
+// MFMA is the one wait state the M0 write needs before the LDS-DMA (no s_nop;
+// gemm_f32_w4.hip mfma_dma, which took the W4 loop from 97.0 to 98.3 % MFMA
+// busy, profiles/r8lq_fp32_lean_stream.md).
+__device__ __forceinline__ void mfma_dma(f32x4& acc, float b, float a, u32x4 rsrc, uint32_t voff, uint32_t soff,
+                                         uint32_t base, int imm) {
+  asm volatile(
+      "s_add_u32 m0, %5, %6\n\t"
+      "v_mfma_f32_16x16x4_f32 %0, %1, %2, %0\n\t"
+      "buffer_load_dwordx4 %3, %4, %7 offen lds"
+      : "+a"(acc)
+      : "v"(b), "v"(a), "v"(voff), "s"(rsrc), "s"(base), "i"(imm), "s"(soff)
+      : "memory", "m0", "scc");
+}
+
 template <int N>
 __device__ __forceinline__ void wait_lgkm_barrier() {
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
@@ -145,6 +161,7 @@ struct Frag<MB, true> {
 
 struct Ctx {
   u32x4 ra;             // A descriptor at this slice's first K
+  u32x4 rb0;            // LN: B descriptor at this slice's first K (built once)
   const char* Bb;       // B at this slice's first K row, column n0
   long long b_bytes;
   int lda4, ldb4, nk, wu;
@@ -181,14 +198,22 @@ __device__ __forceinline__ void issue_piece(const Ctx& c, u32x4 rb, uint32_t so,
 
 // One K-tile: G MFMAs on `cur` (tile t), reading tile t+1's fragments into
 // `nxt` from stage `sn`, DMA of tile t + NS into stage `sc`.
-template <class H, int NS, bool BV>
+// LN (experiments): the slice's descriptors are built once and the K-tile's
+// offset rides in the voffsets (one VALU add each) instead of a new B
+// descriptor per K-tile (~15 SALU: a 64-bit multiply, the extent, clamps), and
+// each piece issues as mfma_dma.
+template <class H, int NS, bool BV, bool LN = false>
 __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, uint32_t sc, uint32_t sn,
                                       f32x4 (&acc)[H::MB][NB], const Frag<H::MB, BV>& cur,
                                       Frag<H::MB, BV>& nxt) {
   constexpr int MB = H::MB, G = H::G;
   constexpr Sched<H, BV> S{};
   const int td = t + NS < c.nk ? t + NS : c.nk - 1;  // clamped tail DMAs (harmless re-reads)
-  const u32x4 rb = b_rsrc(c, td);
+  const u32x4 rb = LN ? c.rb0 : b_rsrc(c, td);
+  // LN: this K-tile's voffsets and the stage's M0 bases (A pieces at h * 4096 +
+  // wu * 1024, B k-row pairs at A_BYTES + (16 (j >> 1) + 2 (j & 1)) * 512 + wu * 2048)
+  const uint32_t vA = c.voffA + (uint32_t)td * (BK * 4), vB = c.voffB + (uint32_t)td * (uint32_t)(BK * c.ldb4);
+  const uint32_t mA = c.lds0 + sc + (uint32_t)c.wu * 1024, mB = c.lds0 + sc + (uint32_t)c.wu * 2048;
   wait_lgkm_barrier<H::P * (NS - 2)>();
   __builtin_amdgcn_sched_barrier(0);
   uint32_t ab[2], bb[NB];
@@ -196,14 +221,29 @@ __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, uin
   for (int kb = 0; kb < 2; ++kb) ab[kb] = c.abase[kb] + sn;
 #pragma unroll
   for (int ni = 0; ni < NB; ++ni) bb[ni] = c.bbase[ni] + sn;
-#pragma unroll
-  for (int gap = 0; gap < G; ++gap) {
+  auto step = [&](const int gap) __attribute__((always_inline)) {
     const int ni = gap % NB, mi = (gap / NB) % MB, e = (gap / (NB * MB)) % 4, kb = gap / (NB * MB * 4);
+    const int it = S.item[gap];
+    if constexpr (LN) {
+      static_assert(BV, "LN: the b128 kernel");
+      if (it >= 1 && it < 100) {  // the gap's MFMA and DMA piece h in one asm block
+        const int h = it - 1;
+        if (h < H::PA) {
+          mfma_dma(acc[mi][ni], cur.b4[kb][e][ni], cur.a[kb][mi][e], c.ra, vA, (uint32_t)(h * 32 * c.lda4), mA,
+                   h * 4096);
+        } else {
+          const int j = h - H::PA, kr = 16 * (j >> 1) + 2 * (j & 1);
+          mfma_dma(acc[mi][ni], cur.b4[kb][e][ni], cur.a[kb][mi][e], rb, vB, (uint32_t)((kr + 4 * c.wu) * c.ldb4),
+                   mB, H::A_BYTES + kr * 512);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        return;
+      }
+    }
     if constexpr (BV)
       mfma(acc[mi][ni], cur.b4[kb][e][ni], cur.a[kb][mi][e]);
     else
       mfma(acc[mi][ni], cur.b[kb][ni][e], cur.a[kb][mi][e]);
-    const int it = S.item[gap];
     if (it >= 200) {
       const int q = it - 200, qk = q / MB, qm = q % MB;
       nxt.a[qk][qm] = *(const lds_f32x4*)(smem + ab[qk] + qm * 2048);
@@ -219,13 +259,31 @@ __device__ __forceinline__ void ktile(const Ctx& c, const char* smem, int t, uin
       issue_piece<H>(c, rb, sc, td, it - 1);
     }
     __builtin_amdgcn_sched_barrier(0);
+  };
+  if constexpr (LN) {
+    // loops of 32 gaps: one loop of 128 fused gaps passes the unroller's size
+    // limit, and a rolled loop cannot give the pieces constant M0 offsets
+    // (the "i" operands)
+#pragma unroll
+    for (int gap = 0; gap < 32; ++gap) step(gap);
+#pragma unroll
+    for (int gap = 32; gap < 64; ++gap) step(gap);
+    if constexpr (G == 128) {
+#pragma unroll
+      for (int gap = 64; gap < 96; ++gap) step(gap);
+#pragma unroll
+      for (int gap = 96; gap < 128; ++gap) step(gap);
+    }
+  } else {
+#pragma unroll
+    for (int gap = 0; gap < G; ++gap) step(gap);
   }
 }
 
 // NS: LDS stages (4: 128 KiB, one workgroup per CU; 2: 64 KiB, two per CU).
 // BV: b128 B reads (column-permuted MFMAs) instead of b32 ones.
 // BM: tile rows (128, or 64 for kF32T64: 4 x 24 KiB stages).
-template <int NS, bool BV, int BM = 128>
+template <int NS, bool BV, int BM = 128, bool LN = false>
 __global__ void __launch_bounds__(NT, NS == 2 ? 2 : 1) gemm_f32_t128(GemmArgs a) {
   using H = Sh<BM>;
   constexpr int MB = H::MB, P = H::P, STAGE = H::STAGE;
@@ -271,6 +329,7 @@ __global__ void __launch_bounds__(NT, NS == 2 ? 2 : 1) gemm_f32_t128(GemmArgs a)
                    ((long long)(a.M - m0 - 1) * a.lda + (a.K - k0)) * 4);
   c.Bb = (const char*)a.B + ((long long)bz * a.sB + k0 * a.ldb + n0) * 4;
   c.b_bytes = ((long long)(a.kb - k0 - 1) * a.ldb + (a.N - n0)) * 4;
+  if constexpr (LN) c.rb0 = b_rsrc(c, 0);
   {
     const int r = wu * 8 + (lane >> 3);  // row of A piece 0 (the swizzle is 32-row periodic)
     c.voffA = (uint32_t)(r * c.lda4 + (((lane & 7) ^ ((r >> 1) & 7)) * 16));
@@ -335,12 +394,13 @@ __global__ void __launch_bounds__(NT, NS == 2 ? 2 : 1) gemm_f32_t128(GemmArgs a)
   // stage (t+1) % NS, refills stage t % NS with tile t + NS.
   int t = 0;
   for (; t + 1 < nk; t += 2) {
-    ktile<H, NS>(c, smem, t, (uint32_t)((t % NS) * STAGE), (uint32_t)(((t + 1) % NS) * STAGE), acc, F0, F1);
-    ktile<H, NS>(c, smem, t + 1, (uint32_t)(((t + 1) % NS) * STAGE), (uint32_t)(((t + 2) % NS) * STAGE), acc,
-                 F1, F0);
+    ktile<H, NS, BV, LN>(c, smem, t, (uint32_t)((t % NS) * STAGE), (uint32_t)(((t + 1) % NS) * STAGE), acc, F0,
+                         F1);
+    ktile<H, NS, BV, LN>(c, smem, t + 1, (uint32_t)(((t + 1) % NS) * STAGE), (uint32_t)(((t + 2) % NS) * STAGE),
+                         acc, F1, F0);
   }
   if (t < nk)  // odd count: the last tile (its "next" reads are clamped re-reads)
-    ktile<H, NS>(c, smem, t, (uint32_t)((t % NS) * STAGE), (uint32_t)((t % NS) * STAGE), acc, F0, F1);
+    ktile<H, NS, BV, LN>(c, smem, t, (uint32_t)((t % NS) * STAGE), (uint32_t)((t % NS) * STAGE), acc, F0, F1);
   // Drain the tail DMAs and give the last MFMAs time to write their AGPRs
   // (asm MFMAs are invisible to hipcc's hazard recognizer).
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
@@ -416,6 +476,13 @@ bool gemm_f32_tile_supported(const GemmArgs& a, size_t align_a, size_t align_b, 
   return true;
 }
 
+// LN's 32-bit voffsets: the K-tile offset rides in them, so the whole K of A
+// (128 B per K-tile, plus 127 rows) and of B (K rows) must stay below 2^31.
+bool gemm_f32_tile_ln_fits(const GemmArgs& a) {
+  return (long long)128 * a.lda * 4 + (long long)a.K * 4 < (1LL << 31) &&
+         (long long)(a.K + 32) * a.ldb * 4 + 512 < (1LL << 31);
+}
+
 // a.splitk > 1: split-K with a.part / a.flags (gemm_dispatch.cpp f32 planner).
 // variant 0: kF32T128 (4 stages, b128 B reads); 2: kF32T128x2 (2 stages, two
 // workgroups per CU); experiment builds: 1 = b32 B reads (round 3's first version).
@@ -424,7 +491,7 @@ bool gemm_f32_tile_supported(const GemmArgs& a, size_t align_a, size_t align_b, 
 // whole waves); tile_span > 0 runs tiles [tile_base, +span), each split
 // a.splitk ways (the meet's tile id is the local index).
 hipError_t gemm_f32_tile_launch(GemmArgs a, hipStream_t stream, int variant) {
-  const int bm = variant == 3 || variant == 4 ? 64 : 128;  // 3: kF32T64, 4: kF32T64x2
+  const int bm = variant == 3 || variant == 4 || variant == 7 || variant == 8 ? 64 : 128;  // kF32T64 (x2)
   a.tiles_m = (a.M + bm - 1) / bm;
   a.tiles_n = (a.N + kf32t::BN - 1) / kf32t::BN;
   a.supertile = choose_supertile(a.tiles_m, a.tiles_n);
@@ -449,6 +516,15 @@ hipError_t gemm_f32_tile_launch(GemmArgs a, hipStream_t stream, int variant) {
 #ifdef PDMB_EXPERIMENTS
   if (variant == 1) {
     hipLaunchKernelGGL((kf32t::gemm_f32_t128<4, false>), dim3((unsigned)nblocks), dim3(kf32t::NT), 0, stream, a);
+    return hipGetLastError();
+  }
+  if (variant >= 5 && variant <= 8) {  // LN forms of kF32T128, kF32T128x2, kF32T64, kF32T64x2
+    if (!gemm_f32_tile_ln_fits(a)) return hipErrorInvalidValue;
+    auto k = variant == 5 ? kf32t::gemm_f32_t128<4, true, 128, true>
+           : variant == 6 ? kf32t::gemm_f32_t128<2, true, 128, true>
+           : variant == 7 ? kf32t::gemm_f32_t128<4, true, 64, true>
+                          : kf32t::gemm_f32_t128<2, true, 64, true>;
+    hipLaunchKernelGGL(k, dim3((unsigned)nblocks), dim3(kf32t::NT), 0, stream, a);
     return hipGetLastError();
   }
 #endif

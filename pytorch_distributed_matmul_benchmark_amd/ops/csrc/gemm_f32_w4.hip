@@ -82,7 +82,7 @@ __device__ __forceinline__ void dma16_m0i(u32x4 rsrc, uint32_t voff, uint32_t so
       "buffer_load_dwordx4 %0, %1, %2 offen lds"
       :
       : "v"(voff), "s"(rsrc), "s"(soff), "s"(base), "i"(imm)
-      : "memory", "m0");
+      : "memory", "m0", "scc");
 }
 
 // LN >= 2 (experiments): the DMA piece fused with its gap's MFMA, which is
@@ -95,7 +95,7 @@ __device__ __forceinline__ void mfma_dma(f32x4& acc, float b, float a, u32x4 rsr
       "buffer_load_dwordx4 %3, %4, %7 offen lds"
       : "+a"(acc)
       : "v"(b), "v"(a), "v"(voff), "s"(rsrc), "s"(base), "i"(imm), "s"(soff)
-      : "memory", "m0");
+      : "memory", "m0", "scc");
 }
 
 struct Ctx {
@@ -445,11 +445,19 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4(GemmArgs a) {
 // stages (16-row x 64-column blocks, 17 KiB for the four waves) while the
 // next tile's first K-tiles land. Its 64 stores per wave are not drained:
 // vmcnt counts loads, stores and LDS-DMA in issue order, so K-tile 0's
-// mid-tile wait is vmcnt(63) (the counter's largest value: K-tile 1 landed
-// once at most 63 younger stores remain); before the first tile 64 no-access
-// LDS-DMA loads stand in for them. That needs all 64 stores issued on every
-// tile, so only whole tiles run here (M, N multiples of 256: no masked store
-// can be skipped). Tiles are static (workgroup b: b, b + G, ...; G a multiple
+// mid-tile wait is vmcnt(47) (K-tile 1 landed once at most 47 younger stores
+// remain; the 16 refills that half issues then keep the count <= 63).
+// The count must NEVER pass 63, the counter's largest value: the hardware
+// does not hold back a 64th outstanding operation, and the counter wraps.
+// (The first form waited vmcnt(63) after 16 K-tile 1 pieces plus 64 stores,
+// or 64 no-access loads before the first tile: up to 80 outstanding. With
+// K-tile 1 slow to land — a cold first launch — that wrapped the counter and
+// a later wait never finished: the launch hung, r8s / r8t.) So the epilogue
+// waits vmcnt(43) before its last 20 stores (the 16 pieces of K-tile 1 and the
+// first store retired: at most 43 + 20 = 63), and the first tile starts with
+// both prologue stages landed. That needs all 64 stores issued on every tile,
+// so only whole tiles run here (M, N multiples of 256: no masked store can be
+// skipped). Tiles are static (workgroup b: b, b + G, ...; G a multiple
 // of 8 keeps a tile on map_tile's XCD); no workgroup waits for another, so
 // residency is not required. Host: unsplit, K / 32 even and >= 4, M % 256 ==
 // N % 256 == 0, K * ldb * 4 < 2^31.
@@ -491,6 +499,18 @@ __device__ __forceinline__ void ktile_s(const Ctx& c, const char* smem, f32x4 (&
                                  mbase);
 }
 
+// DBG (experiments, kF32W4SDbg): lane 0 of every wave stamps its progress
+// into a.dbg (host-mapped, coherent: read by the host while the kernel runs)
+// at slot (blockIdx.x * 4 + wave) * 4: [0] tiles finished, [1] phase
+// (1 prologue issued, 2 prologue landed, 3 K-tile 0 done, 4 K-loop done,
+// 5 epilogue done, 9 exit), [2] the last K-tile finished, [3] its tile index.
+__device__ __forceinline__ void dbg_stamp(const GemmArgs& a, int lane, int wu, int k, long long v) {
+  if (lane == 0)
+    __hip_atomic_store(a.dbg + ((long long)blockIdx.x * 4 + wu) * 4 + k, (unsigned long long)v, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <int DBG = 0>
 __global__ void __launch_bounds__(NT, 1) gemm_f32_w4s(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[S_LDS];
   const int T = a.tiles_m * a.tiles_n * a.batch;
@@ -532,6 +552,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4s(GemmArgs a) {
   for (int h = 0; h < 16; ++h) issue_piece_ln<true>(c, cur.ra, cur.rb, c.voffA, c.voffB, mb0, h);
 #pragma unroll
   for (int h = 0; h < 16; ++h) issue_piece_ln<true>(c, cur.ra, cur.rb, c.voffA + kA, c.voffB + kB, mb1, h);
+  if constexpr (DBG) dbg_stamp(a, lane, wu, 1, 1);
   asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
   Half<true> h0, h1;
 #pragma unroll
@@ -543,16 +564,11 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4s(GemmArgs a) {
     for (int h = 0; h < 2; ++h) h0.b4[e][h] = read_b4<true>(smem, 0, 0, h, e, wc, l16, g);
   }
   char* ebuf = smem + 2 * S_STAGE + wu * EPI4;
-  {  // 64 no-access loads (num_records 0: zeros into this wave's epilogue buffer)
-    u32x4 nul;
-    nul.x = 0u;
-    nul.y = 0u;
-    nul.z = 0u;
-    nul.w = 0x00020000u;
-    const uint32_t eb = c.lds0 + 2 * S_STAGE + wu * EPI4;
-#pragma unroll
-    for (int i = 0; i < 64; ++i) dma16_m0(nul, 0u, 0u, eb);
-  }
+  // K-tile 1 of the first tile landed too (K-tile 0's vmcnt(47) counts on
+  // nothing older than the stores being outstanding)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (DBG) dbg_stamp(a, lane, wu, 1, 2);
+  int ntiles = 0;
 
   // Started by each tile's K-tile 0 (ZERO: C = 0 in the first MFMA of every
   // accumulator). Zeroing them with v_accvgpr_write instead put each write 1-4
@@ -561,13 +577,19 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4s(GemmArgs a) {
   f32x4 acc[8][8];
   for (;;) {
     const bool more = nvb < T;
-    // K-tile 0 (stage 0): the 64 stores (or stand-ins) are younger than K-tile 1
-    ktile_s<63, true>(c, smem, acc, h0, h1, 0, wr, wc, l16, g, cur.ra, cur.rb, c.voffA + 2 * kA,
+    // K-tile 0 (stage 0): the epilogue's stores are younger than K-tile 1
+    ktile_s<47, true>(c, smem, acc, h0, h1, 0, wr, wc, l16, g, cur.ra, cur.rb, c.voffA + 2 * kA,
                       c.voffB + 2 * kB, mb0);
+    if constexpr (DBG) {
+      dbg_stamp(a, lane, wu, 1, 3);
+      dbg_stamp(a, lane, wu, 3, vb);
+    }
     int t = 1;
-    for (; t + 2 < nk; ++t)
+    for (; t + 2 < nk; ++t) {
       ktile_s<0, false>(c, smem, acc, h0, h1, t & 1, wr, wc, l16, g, cur.ra, cur.rb,
                         c.voffA + (uint32_t)(t + 2) * kA, c.voffB + (uint32_t)(t + 2) * kB, (t & 1) ? mb1 : mb0);
+      if constexpr (DBG) dbg_stamp(a, lane, wu, 2, t);
+    }
     {
       // K-tiles nk - 2 (stage 0), nk - 1 (stage 1): their refills are the next
       // tile's K-tiles 0 and 1 — or, on the last tile, re-reads of this tile's
@@ -579,6 +601,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4s(GemmArgs a) {
       ktile_s<0, false>(c, smem, acc, h0, h1, 1, wr, wc, l16, g, ra, rb, c.voffA + k1 * kA, c.voffB + k1 * kB,
                         mb1);
     }
+    if constexpr (DBG) dbg_stamp(a, lane, wu, 1, 4);
     // The last MFMAs write their AGPRs before the epilogue reads them (asm
     // MFMAs are invisible to hipcc's hazard recognizer). Every accumulator is
     // an operand of the padding, so no register copy of one (the epilogue's
@@ -598,6 +621,8 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4s(GemmArgs a) {
     for (int mi = 0; mi < 8; ++mi) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {  // acc[mi][4 h + j][r] is column 64 h + 16 g + 4 r + j: regroup by r
+        // 4 stores per block: before block 11 (stores 44..), at most 43 outstanding
+        if (mi * 2 + h == 11) asm volatile("s_waitcnt vmcnt(43)" ::: "memory");
         f32x4 w[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -607,6 +632,10 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4s(GemmArgs a) {
       }
     }
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (DBG) {
+      dbg_stamp(a, lane, wu, 1, 5);
+      dbg_stamp(a, lane, wu, 0, ++ntiles);
+    }
     if (!more) break;
     vb = nvb;
     bz = nbz;
@@ -621,12 +650,23 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4s(GemmArgs a) {
   }
   // No LDS-DMA may still be writing when this workgroup's LDS is handed on.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (DBG) dbg_stamp(a, lane, wu, 1, 9);
 }
 
 }  // namespace kf32w4
 
+// The streamed form's shape constraints (K-tiles even and >= 4, whole 256x256
+// tiles, 32-bit B offsets over the whole K); alignment as gemm_f32_256.
+bool gemm_f32_w4s_fits(const GemmArgs& a) {
+  const int nk = a.K / kf32w4::BK;
+  return a.K % kf32w4::BK == 0 && nk % 2 == 0 && nk >= 4 && a.M > 0 && a.N > 0 && a.M % kf32w4::BM == 0 &&
+         a.N % kf32w4::BN == 0 && (long long)a.K * a.ldb * 4 < (1LL << 31);
+}
+
 // a.splitk > 1: split-K with a.part / a.flags (gemm_dispatch.cpp f32_split).
-// variant 0: the shipping kernel (b128 B reads); 1 (experiment builds): b32 B reads.
+// variant 0: the shipping kernel (b128 B reads); experiment builds: 1.. the
+// A/B arms, 14 the streamed persistent form (kF32W4S, a.pers_grid workgroups),
+// 15 its stamping diagnostic.
 hipError_t gemm_f32_w4_launch(GemmArgs a, hipStream_t stream, int variant) {
   a.tiles_m = (a.M + kf32w4::BM - 1) / kf32w4::BM;
   a.tiles_n = (a.N + kf32w4::BN - 1) / kf32w4::BN;
@@ -644,6 +684,23 @@ hipError_t gemm_f32_w4_launch(GemmArgs a, hipStream_t stream, int variant) {
   const long long nblocks = (long long)a.tiles_m * a.tiles_n * a.batch * S;
   if (nblocks <= 0) return hipSuccess;
   if (nblocks > 0x7fffffffLL) return hipErrorInvalidValue;
+#ifdef PDMB_EXPERIMENTS
+  if (variant == 14) {  // kF32W4S: the streamed persistent form (unsplit, pers_grid workgroups)
+    if (S > 1 || !gemm_f32_w4s_fits(a) || a.pers_grid <= 0 || a.pers_grid % 8 || a.tile_span || a.tile_end)
+      return hipErrorInvalidValue;
+    const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
+    hipLaunchKernelGGL(kf32w4::gemm_f32_w4s<0>, pg, dim3(kf32w4::NT), 0, stream, a);
+    return hipGetLastError();
+  }
+  if (variant == 15) {  // kF32W4SDbg: the streamed form stamping its progress into a.dbg
+    if (S > 1 || !gemm_f32_w4s_fits(a) || a.pers_grid <= 0 || a.pers_grid % 8 || a.tile_span || a.tile_end ||
+        !a.dbg)
+      return hipErrorInvalidValue;
+    const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
+    hipLaunchKernelGGL(kf32w4::gemm_f32_w4s<1>, pg, dim3(kf32w4::NT), 0, stream, a);
+    return hipGetLastError();
+  }
+#endif
 #ifdef PDMB_EXPERIMENTS
   if (variant == 1) {
     hipLaunchKernelGGL(kf32w4::gemm_f32_w4<false>, dim3((unsigned)nblocks), dim3(kf32w4::NT), 0, stream, a);
@@ -665,15 +722,6 @@ hipError_t gemm_f32_w4_launch(GemmArgs a, hipStream_t stream, int variant) {
            : variant == 6 ? kf32w4::gemm_f32_w4<true, true, true, 3>
                           : kf32w4::gemm_f32_w4<true, true, true, 7>;
     hipLaunchKernelGGL(k, dim3((unsigned)nblocks), dim3(kf32w4::NT), 0, stream, a);
-    return hipGetLastError();
-  }
-  if (variant == 14) {  // kF32W4S: the streamed persistent form (unsplit, pers_grid workgroups)
-    const int nk = a.K / kf32w4::BK;
-    if (S > 1 || a.pers_grid <= 0 || a.pers_grid % 8 || nk % 2 || nk < 4 || a.tile_span || a.tile_end ||
-        a.M % kf32w4::BM || a.N % kf32w4::BN || (long long)a.K * a.ldb * 4 >= (1LL << 31))
-      return hipErrorInvalidValue;
-    const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
-    hipLaunchKernelGGL(kf32w4::gemm_f32_w4s, pg, dim3(kf32w4::NT), 0, stream, a);
     return hipGetLastError();
   }
   if (variant == 11 || variant == 12) {  // kF32W4Lean, kF32W4Lean2

@@ -317,7 +317,8 @@ def test_small_grid_split_plans_exact(dtype, M, N, K, S, monkeypatch):
         assert torch.equal(gemm.matmul(A, B), C)
 
 
-F32_T128_ARMS = ["f32_t128", "f32_t128x2", "x_f32_t128_b32", "f32_t64", "f32_t64x2"]
+F32_T128_ARMS = ["f32_t128", "f32_t128x2", "x_f32_t128_b32", "f32_t64", "f32_t64x2", "x_f32_t128_lean",
+                 "x_f32_t128x2_lean", "x_f32_t64_lean", "x_f32_t64x2_lean"]
 
 
 @pytest.mark.parametrize("M,N,K,b", [(128, 128, 32, 1), (256, 384, 96, 1), (1000, 1052, 320, 1),
@@ -372,6 +373,37 @@ def test_f32_256_identity_batched_and_shards():
     for r in range(4):  # matrix_parallel column shards (strided views)
         Bs = Bf[:, r * 256:(r + 1) * 256]
         assert _relerr(gemm.matmul(Af, Bs), _ref(Af, Bs)) < TOL[torch.float32]
+
+
+@pytest.mark.experiments
+@pytest.mark.parametrize("b,M,N,K,exact", [(1, 256, 256, 128, True), (1, 4096, 4096, 256, True),
+                                           (1, 8192, 8192, 512, False), (1, 5120, 3072, 1024, True),
+                                           (1, 9216, 6912, 640, True), (3, 1024, 1024, 512, True),
+                                           (1, 2304, 8960, 384, False), (1, 4352, 4608, 192, True)])
+def test_f32_w4s_exact_and_bitwise(b, M, N, K, exact):
+    """The streamed exact-fp32 kernel (x_f32_w4s, round 6, experiments build:
+    its first launches hung in 3 of 4 processes, gemm_f32_w4.hip): one K-tile stream per
+    CU over static tiles (1 to 10 tiles per workgroup, grids that are not whole
+    waves, a batch, the four-K-tile minimum). Small integers exact against
+    fp64 (a dropped, doubled or misplaced K-tile of the stream would show), and
+    bitwise equal to the unstreamed f32_w4 (the same per-element MFMA order)."""
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K + b)
+    sa, sb = ((b, M, K), (b, K, N)) if b > 1 else ((M, K), (K, N))
+    if exact:
+        A = torch.randint(-3, 4, sa, device="cuda", generator=g).float()
+        B = torch.randint(-3, 4, sb, device="cuda", generator=g).float()
+    else:
+        A = torch.randn(sa, device="cuda", generator=g)
+        B = torch.randn(sb, device="cuda", generator=g)
+    _need("x_f32_w4s")
+    assert gemm.kernel_for(A, B, kernel="x_f32_w4s") == "pdmb_f32_w4s"
+    C = gemm.matmul(A, B, kernel="x_f32_w4s")
+    R = torch.matmul(A.double(), B.double())
+    if exact:
+        assert torch.equal(C.double(), R)
+    else:
+        assert _relerr(C, R) < TOL[torch.float32]
+    assert torch.equal(C, gemm.matmul(A, B, kernel="f32_w4"))
 
 
 @pytest.mark.parametrize("kernel", ["f32_256", "f32_256s", "f32_w4", "f32_t128"])
