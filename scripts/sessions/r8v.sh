@@ -10,7 +10,10 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out/r8v; mkdir -p $OUT
-PDMB_EXPERIMENTS=1 timeout -k 10 900 python -m pytorch_distributed_matmul_benchmark_amd.ops.build --no-bench > $OUT/build.log 2>&1 || exit $?
+export PDMB_EXPERIMENTS=1
+timeout -k 10 900 python -m pytorch_distributed_matmul_benchmark_amd.ops.build --no-bench > $OUT/build.log 2>&1 || exit $?
+timeout -k 10 300 python scripts/check_f32_tile_lean.py > $OUT/check_lean.jsonl 2> $OUT/check_lean.err || { tail -5 $OUT/check_lean.jsonl; tail -5 $OUT/check_lean.err; exit 1; }
+tail -1 $OUT/check_lean.jsonl
 ab() {  # name, kernels, shapes...
   local n=$1 k=$2; shift 2
   timeout -k 10 500 python scripts/ab_kernels.py --dtype float32 --rounds 4 --iters 10 --settle 1 --sessions 2 \
