@@ -32,6 +32,7 @@ enum Kernel : int {
   kFp8T192x128 = 63,  // gemm_tile.hip fp8: 192x128 tile, 4 waves x 96x64, split-K
   kF32T64 = 64,       // gemm_f32_tile.hip: exact fp32, 64x128 tile, 4 waves x 32x64, split-K (any M, N % 4)
   kF32T64x2 = 65,     // kF32T64 on 2 LDS stages, two workgroups per CU
+  kF32W4L = 66,       // gemm_f32_w4.hip: exact-fp32 W4 on the lean K-loop (one whole wave of 256x256 tiles)
 };
 
 // Experiment / diagnostic kernel ids (A/B and timing-only builds) live in

@@ -30,6 +30,7 @@ bool gemm_f32_256_supported(const GemmArgs& a, size_t align_a, size_t align_b, s
 hipError_t gemm_f32_256_launch(GemmArgs a, int variant, hipStream_t stream);
 hipError_t gemm_f32_w4_launch(GemmArgs a, hipStream_t stream, int variant);
 bool gemm_f32_w4s_fits(const GemmArgs& a);  // experiments build: kF32W4S
+bool gemm_f32_w4l_fits(const GemmArgs& a);
 bool gemm_f32_tile_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 bool gemm_f32_tile_ln_fits(const GemmArgs& a);
 hipError_t gemm_f32_tile_launch(GemmArgs a, hipStream_t stream, int variant);
@@ -171,6 +172,8 @@ static int fp8_split(const Problem& p);
 static bool w4s_fits(const Problem& p);
 static bool w4s_auto(const Problem& p);
 static bool supports(const Problem& p, int kernel);
+struct Plan;
+static bool f32w4l_one_wave(const Problem& p, const GemmArgs& a, const Plan& pl);
 static int signal_kernel(const Problem& p, int kernel);
 
 struct Plan {
@@ -233,6 +236,12 @@ static int resolve_core(const Problem& p, int kernel) {
       if (!f32fast) return kGeneric;
       {
         const Plan pl = plan(p, kAuto);
+        // Exactly one whole wave of 256x256 tiles (round 6): the lean W4
+        // K-loop (f32_w4l: 98.3 % MFMA busy, profiles/r8lq_fp32_lean_stream.md)
+        // ahead of the plan it replaces, settled, two sessions: 8192 x 2048 x
+        // 8192 153.1 vs 149.8 (f32_256s), 4096^2 x 16384 153.3 vs 149.9
+        // (f32_256s), 4096^3 150.9 vs 150.2 (f32_t128x2); profiles/r8r/, r8q/.
+        if (f32w4l_one_wave(p, a, pl)) return kF32W4L;
         // Exactly one wave of 256x256 tiles on a long K: the 8-wave f32_256s
         // measured 1.0-1.3 % ahead of f32_t128x2 (1024 x 16384 x 16384 152.1
         // vs 150.1, 4096^2 x 14336 152.3 vs 150.8; profiles/r6f_f32_long_k_arms_ab.jsonl)
@@ -253,6 +262,7 @@ static int resolve_core(const Problem& p, int kernel) {
     case kT192x128: return t192 ? kT192x128 : -1;
     case kF32_256s: return f32fast ? kF32_256s : -1;
     case kF32W4: return f32fast ? kF32W4 : -1;  // same constraints as f32_256
+    case kF32W4L: return f32fast && gemm_f32_w4l_fits(a) && p.splitk <= 1 ? kF32W4L : -1;  // unsplit only
     case kF32T128: return p.dtype == kF32 && supports(p, kF32T128) ? kF32T128 : -1;
     case kF32T128x2: return p.dtype == kF32 && supports(p, kF32T128) ? kF32T128x2 : -1;
     case kF32T64: return p.dtype == kF32 && supports(p, kF32T64) ? kF32T64 : -1;
@@ -397,6 +407,16 @@ static bool w4s_fits(const Problem& p) {  // interior tiles only (its epilogue i
 }
 static bool w4s_auto(const Problem& p) {
   return p.cus == 0 && w4s_fits(p) && tiles_of(p, kMfmaW4) >= 2LL * device_cus();
+}
+
+// f32_w4l on exactly one whole wave of 256x256 tiles on a device of its own,
+// in place of an unsplit f32_t128x2 / f32_256s plan. (On more waves it led by
+// only 0.2-0.85 % and lost 1.4 % at 16384^2 x 1024, profiles/r8r/: not taken.)
+static bool f32w4l_one_wave(const Problem& p, const GemmArgs& a, const Plan& pl) {
+  if (p.cus != 0 || p.dtype != kF32 || pl.splitk > 1 || (pl.kernel != kF32T128x2 && pl.kernel != kF32_256s))
+    return false;
+  if (p.M % 256 || p.N % 256 || p.K < 4096 || !gemm_f32_w4l_fits(a)) return false;  // (measured from K = 4096)
+  return (long long)(p.M / 256) * (p.N / 256) * (p.batch < 1 ? 1 : p.batch) == device_cus();
 }
 
 // f32_t128x2 split into slices on a grid of fewer than two tiles per CU
@@ -751,7 +771,7 @@ static bool is_tiled(int k) {
 
 int choose_splitk(const Problem& p, int kernel) {
   const int k = resolve_kernel(p, kernel);
-  if (k == kMfmaW4S || k == kFp8W4S) return 1;
+  if (k == kMfmaW4S || k == kFp8W4S || k == kF32W4L) return 1;
   if (k == kFp8W4) return fp8_split(p);
   if (!is_tiled(k)) return 0;
   return plan(p, k).splitk;
@@ -1661,6 +1681,11 @@ hipError_t gemm(const Problem& p, int kernel, hipStream_t stream, int* used) {
     case kFp8T192x128: return tiled_launch(p, kw, a, p.workspace, p.workspace_bytes, stream);
     case kMfmaW4S: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 7);
     case kF32_256s: return gemm_f32_256_launch(a, 1, stream);
+    case kF32W4L: {
+      GemmArgs s = a;
+      s.splitk = 1;
+      return gemm_f32_w4_launch(s, stream, 16);
+    }
     case kF32W4:
     case kF32T128: return tiled_launch(p, kw, a, p.workspace, p.workspace_bytes, stream);
     case kF32T128x2: return tiled_launch(p, kw, a, p.workspace, p.workspace_bytes, stream, 2);
@@ -1831,6 +1856,7 @@ const char* kernel_name(int kernel) {
     case kFp8T192: return "pdmb_fp8_t192_nt";
     case kFp8T192x128: return "pdmb_fp8_t192x128_nt";
     case kF32W4: return "pdmb_f32_w4_nn";
+    case kF32W4L: return "pdmb_f32_w4l_nn";
     case kF32T128: return "pdmb_f32_t128_nn";
     case kF32T64: return "pdmb_f32_t64_nn";
     case kF32T64x2: return "pdmb_f32_t64x2_nn";

@@ -655,6 +655,13 @@ __global__ void __launch_bounds__(NT, 1) gemm_f32_w4s(GemmArgs a) {
 
 }  // namespace kf32w4
 
+// The lean K-loop's 32-bit voffsets carry the K-tile offset: A's 255 rows plus
+// its whole K, and B's whole K of rows, must stay below 2^31 bytes.
+bool gemm_f32_w4l_fits(const GemmArgs& a) {
+  return (long long)256 * a.lda * 4 + (long long)a.K * 4 < (1LL << 31) &&
+         (long long)(a.K + 32) * a.ldb * 4 + 1024 < (1LL << 31);
+}
+
 // The streamed form's shape constraints (K-tiles even and >= 4, whole 256x256
 // tiles, 32-bit B offsets over the whole K); alignment as gemm_f32_256.
 bool gemm_f32_w4s_fits(const GemmArgs& a) {
@@ -664,7 +671,9 @@ bool gemm_f32_w4s_fits(const GemmArgs& a) {
 }
 
 // a.splitk > 1: split-K with a.part / a.flags (gemm_dispatch.cpp f32_split).
-// variant 0: the shipping kernel (b128 B reads); experiment builds: 1.. the
+// variant 0: the shipping kernel (b128 B reads); 16: kF32W4L, the lean K-loop
+// (1 KiB B rows, branch-free, descriptors once per slice, no s_nop per DMA
+// piece: bitwise equal to variant 0); experiment builds: 1.. the
 // A/B arms, 14 the streamed persistent form (kF32W4S, a.pers_grid workgroups),
 // 15 its stamping diagnostic.
 hipError_t gemm_f32_w4_launch(GemmArgs a, hipStream_t stream, int variant) {
@@ -738,6 +747,12 @@ hipError_t gemm_f32_w4_launch(GemmArgs a, hipStream_t stream, int variant) {
     return hipGetLastError();
   }
 #endif
+  if (variant == 16) {  // kF32W4L: the lean K-loop (experiments' kF32W4Lean2), unsplit or split
+    if (!gemm_f32_w4l_fits(a)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((kf32w4::gemm_f32_w4<true, true, true, 0, 0, 2>), dim3((unsigned)nblocks), dim3(kf32w4::NT),
+                       0, stream, a);
+    return hipGetLastError();
+  }
   if (variant != 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(kf32w4::gemm_f32_w4<true>, dim3((unsigned)nblocks), dim3(kf32w4::NT), 0, stream, a);
   return hipGetLastError();

@@ -39,7 +39,7 @@ KERNELS = {"auto": 0, "generic": 2, "f32_256s": 7, "mfma256d": 9, "fp8_w4": 16, 
            "t128": 26, "t128x2": 27, "t256x128": 28, "f32_w4": 29, "w4s": 36, "fp8_w4s": 37,
            "fp8_t128": 41, "fp8_t256x128": 42, "f32_t128": 51, "f32_t128x2": 53,
            "t192": 60, "t192x128": 61, "fp8_t192": 62, "fp8_t192x128": 63, "f32_t64": 64,
-           "f32_t64x2": 65}
+           "f32_t64x2": 65, "f32_w4l": 66}
 # A/B and timing-only diagnostic kernels (api.h ``ExperimentKernel``): accepted
 # only by a library built with ``PDMB_EXPERIMENTS=1``; ``diag_*`` ones skip waits
 # or data movement on purpose and compute WRONG results.
@@ -71,7 +71,7 @@ KERNEL_NAMES = {0: "auto", 2: "pdmb_generic_nn", 7: "pdmb_f32_256s_nn", 9: "pdmb
                 37: "pdmb_fp8_w4s", 41: "pdmb_fp8_t128_nt", 42: "pdmb_fp8_t256x128_nt",
                 51: "pdmb_f32_t128_nn", 53: "pdmb_f32_t128x2_nn", 60: "pdmb_t192_nn",
                 61: "pdmb_t192x128_nn", 62: "pdmb_fp8_t192_nt", 63: "pdmb_fp8_t192x128_nt",
-                64: "pdmb_f32_t64_nn", 65: "pdmb_f32_t64x2_nn",
+                64: "pdmb_f32_t64_nn", 65: "pdmb_f32_t64x2_nn", 66: "pdmb_f32_w4l_nn",
                 1: "pdmb_mfma256_nn",
                 3: "pdmb_mfma256b_nn", 4: "pdmb_mfma256c_nn", 5: "pdmb_mfma256c_stamp",
                 6: "pdmb_f32_256_nn", 15: "pdmb_fp8_256_nt", -1: "unsupported"}

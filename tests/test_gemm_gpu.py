@@ -35,7 +35,7 @@ FAST = ["mfma256d", "mfma256", "mfma256b", "mfma256c"]
 TILED = ("pdmb_w4_nn", "pdmb_t256x128_nn", "pdmb_t128_nn", "pdmb_t128x2_nn", "pdmb_w4s",
          "pdmb_t192_nn", "pdmb_t192x128_nn")
 F32 = ("pdmb_f32_256s_nn", "pdmb_f32_w4_nn", "pdmb_f32_t128_nn", "pdmb_f32_t128x2_nn", "pdmb_f32_t64_nn",
-       "pdmb_f32_t64x2_nn")
+       "pdmb_f32_t64x2_nn", "pdmb_f32_w4l_nn")
 
 
 def _need(kernel):
@@ -207,7 +207,8 @@ def test_race_screen_repeated_runs(kernel):
 @pytest.mark.parametrize("M,N,K", [(256, 256, 32), (512, 768, 96), (1000, 1052, 320),
                                    (300, 200, 64), (2304, 2048, 1024)])
 @pytest.mark.parametrize("kernel", ["f32_256", "f32_256s", "f32_w4", "x_f32_256s_direct", "f32_t128",
-                                    "f32_t128x2", "x_f32_w4_b32", "x_f32_t128_b32", "f32_t64", "f32_t64x2"])
+                                    "f32_t128x2", "x_f32_w4_b32", "x_f32_t128_b32", "f32_t64", "f32_t64x2",
+                                    "f32_w4l"])
 def test_f32_256_exact_and_random(M, N, K, kernel):
     _need(kernel)
     g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
@@ -406,7 +407,32 @@ def test_f32_w4s_exact_and_bitwise(b, M, N, K, exact):
     assert torch.equal(C, gemm.matmul(A, B, kernel="f32_w4"))
 
 
-@pytest.mark.parametrize("kernel", ["f32_256", "f32_256s", "f32_w4", "f32_t128"])
+@pytest.mark.parametrize("b,M,N,K", [(1, 4096, 4096, 4096), (1, 8192, 2048, 8192), (1, 4096, 4096, 4128),
+                                     (4, 2048, 2048, 4096)])
+def test_f32_w4l_one_wave_auto_exact_and_bitwise(b, M, N, K):
+    """Round 6: exactly one whole wave of 256x256 fp32 tiles runs the lean W4
+    K-loop (f32_w4l); small integers exact against fp64 (K / 32 odd at 4128:
+    the branch-free loop's re-read tail), bitwise equal to f32_w4 (the same
+    per-element MFMA order), A = I with an asymmetric B, and repeatable."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + b)
+    sa, sb = ((b, M, K), (b, K, N)) if b > 1 else ((M, K), (K, N))
+    A = torch.randint(-3, 4, sa, device="cuda", generator=g).float()
+    B = torch.randint(-3, 4, sb, device="cuda", generator=g).float()
+    assert gemm.kernel_for(A, B) == "pdmb_f32_w4l_nn"
+    C = gemm.matmul(A, B)
+    assert torch.equal(C.double(), torch.matmul(A.double(), B.double()))
+    assert torch.equal(C, gemm.matmul(A, B, kernel="f32_w4"))
+    for _ in range(3):
+        assert torch.equal(gemm.matmul(A, B), C)
+    if b == 1 and M == N == K:
+        eye = torch.eye(M, device="cuda")
+        Bq = (torch.arange(M * M, device="cuda").view(M, M) % 97).float()
+        assert torch.equal(gemm.matmul(eye, Bq), Bq) and torch.equal(gemm.matmul(Bq, eye), Bq)
+    with pytest.raises(RuntimeError):
+        gemm.matmul(A, B, kernel="f32_w4l", splitk=2)  # unsplit only
+
+
+@pytest.mark.parametrize("kernel", ["f32_256", "f32_256s", "f32_w4", "f32_t128", "f32_w4l"])
 def test_f32_256_race_screen(kernel):
     _need(kernel)
     torch.manual_seed(11)

@@ -61,7 +61,7 @@ GOLDEN = {
     ("fp16", 16384, 2048, 16384, 1): ("w4s", 1, "w4_nn", 1),
     ("fp16", 16384, 16384, 16384, 2): ("w4s", 1, "w4_nn", 1),
     ("fp16", 16384, 16384, 16384, 4): ("w4s", 1, "w4_nn", 1),
-    ("fp32", 4096, 4096, 4096, 1): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
+    ("fp32", 4096, 4096, 4096, 1): ("f32_w4l_nn", 1, "f32_t128x2_nn", 1),
     ("fp32", 4096, 2048, 4096, 1): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
     ("fp32", 4096, 1024, 4096, 1): ("f32_t128_nn", 1, "f32_t128_nn", 1),
     ("fp32", 4096, 512, 4096, 1): ("f32_t64_nn", 1, "f32_t64_nn", 1),
@@ -69,7 +69,7 @@ GOLDEN = {
     ("fp32", 4096, 4096, 4096, 4): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
     ("fp32", 8192, 8192, 8192, 1): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
     ("fp32", 8192, 4096, 8192, 1): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
-    ("fp32", 8192, 2048, 8192, 1): ("f32_256s_nn", 0, "f32_t128x2_nn", 1),
+    ("fp32", 8192, 2048, 8192, 1): ("f32_w4l_nn", 1, "f32_t128x2_nn", 1),
     ("fp32", 8192, 1024, 8192, 1): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
     ("fp32", 8192, 8192, 8192, 2): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
     ("fp32", 8192, 8192, 8192, 4): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),

@@ -53,9 +53,17 @@ def test_f32_shards_fill_the_chip(C, n, ws):
 
 def test_f32_full_grids_take_two_128_tiles_per_cu(C):
     """Full fp32 grids run f32_t128x2 (measured ahead of f32_256s at 4k / 8k /
-    16k in the same process, profiles/r3i_f32_256p_ab.jsonl)."""
-    for n in (4096, 8192, 16384):
+    16k in the same process, profiles/r3i_f32_256p_ab.jsonl); exactly one whole
+    wave of 256x256 tiles alone on the device runs the lean W4 loop (round 6,
+    f32_w4l: 4096^3 150.9 vs 150.2, profiles/r8q/)."""
+    for n in (8192, 16384):
         assert plan(C, F32, n, n, n)[0] == "pdmb_f32_t128x2_nn"
+    assert plan(C, F32, 4096, 4096, 4096)[:2] == ("pdmb_f32_w4l_nn", 1)
+    assert plan(C, F32, 4096, 4096, 4096, cus=-1)[0] == "pdmb_f32_t128x2_nn"
+    assert plan(C, F32, 4096, 4096, 4096, b=2)[0] == "pdmb_f32_t128x2_nn"  # two waves
+    assert plan(C, F32, 4096, 4096, 4128)[0] == "pdmb_f32_w4l_nn"  # 129 K-tiles: the loop takes any count
+    for shape in ((4352, 3840, 4096), (4096, 2048, 4096), (4096, 4096, 2048)):
+        assert plan(C, F32, *shape)[0] != "pdmb_f32_w4l_nn", shape
 
 
 def test_f32_planner_prefers_cheaper_plan(C):
@@ -166,10 +174,13 @@ def test_plan_report_script(C, monkeypatch):
 def test_f32_long_k_one_wave_runs_256s(C):
     """Exactly one wave of 256x256 tiles on a long K runs the 8-wave f32_256s
     (measured 0.1-1.6 % ahead of f32_t128x2 there, profiles/r6g_f32_long_k_rule_ab.jsonl);
-    shorter K or more waves keep f32_t128x2."""
-    assert plan(C, 0, 1024, 16384, 16384)[0] == "pdmb_f32_256s_nn"
-    assert plan(C, 0, 4096, 4096, 14336)[0] == "pdmb_f32_256s_nn"
-    assert plan(C, 0, 4096, 4096, 4096)[0] == "pdmb_f32_t128x2_nn"
+    shorter K or more waves keep f32_t128x2. Round 6: the lean W4 loop (f32_w4l)
+    takes every such one-wave grid of whole tiles (8192 x 2048 x 8192 153.1 vs
+    149.8, 4096^2 x 16384 153.3 vs 149.9 TF, profiles/r8r/); f32_256s keeps
+    the edge-tile ones."""
+    assert plan(C, 0, 1024, 16384, 16384)[0] == "pdmb_f32_w4l_nn"
+    assert plan(C, 0, 4096, 4096, 14336)[0] == "pdmb_f32_w4l_nn"
+    assert plan(C, 0, 4096, 4096, 14336, cus=-1)[0] == "pdmb_f32_t128x2_nn"
     assert plan(C, 0, 8192, 8192, 28672)[0] == "pdmb_f32_t128x2_nn"
 
 
