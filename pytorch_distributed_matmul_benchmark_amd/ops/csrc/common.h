@@ -361,6 +361,24 @@ __device__ __forceinline__ void dma16_at(u32x4 rsrc, uint32_t voff, uint32_t sof
       : "memory", "m0", "scc");
 }
 
+// dma16_at with 4 wait states before the load (s_nop 3 for the s_nop 0):
+// 5 states from the end of any instruction before the statement. A VALU write
+// of an SGPR needs 5 wait states before a VMEM instruction reads it, and
+// hipcc, which pads its own loads (s_nop 3 after v_readfirstlane + s_mul),
+// cannot see the read inside this asm. In W4S and fp8 W4S it restores a few
+// spilled soffsets with v_readlane right before the first K-tiles' pieces of
+// a tile (round 6, tests/test_sgpr_vmem_hazard.py); those K-tiles use this.
+__device__ __forceinline__ void dma16_at_pad(u32x4 rsrc, uint32_t voff, uint32_t soff, uint32_t lds0w,
+                                             uint32_t off) {
+  asm volatile(
+      "s_add_u32 m0, %3, %4\n\t"
+      "s_nop 3\n\t"
+      "buffer_load_dwordx4 %0, %1, %2 offen lds"
+      :
+      : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds0w), "i"(off)
+      : "memory", "m0", "scc");
+}
+
 // ---- block -> output tile mapping -------------------------------------
 // Speed only (never correctness): workgroups are dealt round-robin over the
 // 8 XCDs (blocks b and b+8 share an XCD). In super-tile mode every "round"

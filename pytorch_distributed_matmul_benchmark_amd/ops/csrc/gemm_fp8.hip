@@ -706,11 +706,21 @@ __device__ __forceinline__ void ktile_w4s(const Ctx4& c, const char* smem, u32x4
       const int it = kW4Items[mi][ni];
       if (it == 1) {
         const int h = w4_piece(mi, ni);
-        if (h < 8)  // A of t+2 into S.A: rows (h*4 + wu)*8 + [0,8)
-          dma16_at(raT, c.voffA, kaT + (uint32_t)(h * 32 * c.lda), lds0w, SO + h * 4 * 8 * BK);
-        else  // B of t+3 into S^1.B
-          dma16_at(rbT, c.voffB, kbT + (uint32_t)((h - 8) * 32 * c.ldb), lds0w,
-                   SN + A_BYTES + (h - 8) * 4 * 8 * BK);
+        // the first two K-tiles of a tile (W0 48): soffsets hipcc may have just
+        // restored with v_readlane (common.h dma16_at_pad)
+        if (h < 8) {  // A of t+2 into S.A: rows (h*4 + wu)*8 + [0,8)
+          if constexpr (W0 == 48)
+            dma16_at_pad(raT, c.voffA, kaT + (uint32_t)(h * 32 * c.lda), lds0w, SO + h * 4 * 8 * BK);
+          else
+            dma16_at(raT, c.voffA, kaT + (uint32_t)(h * 32 * c.lda), lds0w, SO + h * 4 * 8 * BK);
+        } else {  // B of t+3 into S^1.B
+          if constexpr (W0 == 48)
+            dma16_at_pad(rbT, c.voffB, kbT + (uint32_t)((h - 8) * 32 * c.ldb), lds0w,
+                         SN + A_BYTES + (h - 8) * 4 * 8 * BK);
+          else
+            dma16_at(rbT, c.voffB, kbT + (uint32_t)((h - 8) * 32 * c.ldb), lds0w,
+                     SN + A_BYTES + (h - 8) * 4 * 8 * BK);
+        }
       } else if (it >= 10 && it < 20) {
         Bn[it - 10] = frag(smem + (it - 10) * 16 * BK, c.boff[SN / STAGE4]);
       } else if (it == 27) {

@@ -612,11 +612,20 @@ __device__ __forceinline__ void ktile_s(const Ctx& c, const char* smem, u32x4 ra
       } else if (it == 1) {
         const int h = piece_of(mi, gap);
         if (h < 8) {
-          dma16_at(raT, c.voffA, kaT + (uint32_t)(h * 32 * c.lda2), c.lds0w, SO + h * 32 * 128);
+          // the first two K-tiles of a tile (W0 48): soffsets hipcc may have
+          // just restored with v_readlane (common.h dma16_at_pad)
+          if constexpr (W0 == 48)
+            dma16_at_pad(raT, c.voffA, kaT + (uint32_t)(h * 32 * c.lda2), c.lds0w, SO + h * 32 * 128);
+          else
+            dma16_at(raT, c.voffA, kaT + (uint32_t)(h * 32 * c.lda2), c.lds0w, SO + h * 32 * 128);
         } else {
           const int nq = (h - 8) >> 2, kb = (h - 8) & 3;
-          dma16_at(rbT, c.voffB, (uint32_t)(kb * 16 * c.ldb2 + nq * IL * 2), c.lds0w,
-                   SN + A_BYTES + nq * BH_BYTES + kb * 16 * 256);
+          if constexpr (W0 == 48)
+            dma16_at_pad(rbT, c.voffB, (uint32_t)(kb * 16 * c.ldb2 + nq * IL * 2), c.lds0w,
+                         SN + A_BYTES + nq * BH_BYTES + kb * 16 * 256);
+          else
+            dma16_at(rbT, c.voffB, (uint32_t)(kb * 16 * c.ldb2 + nq * IL * 2), c.lds0w,
+                     SN + A_BYTES + nq * BH_BYTES + kb * 16 * 256);
         }
       } else if (it >= 100 && it < 200) {
         const int s = (it - 100) >> 1, h = (it - 100) & 1;
