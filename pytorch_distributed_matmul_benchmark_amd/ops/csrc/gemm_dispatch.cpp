@@ -173,7 +173,7 @@ static bool w4s_fits(const Problem& p);
 static bool w4s_auto(const Problem& p);
 static bool supports(const Problem& p, int kernel);
 struct Plan;
-static bool f32w4l_one_wave(const Problem& p, const GemmArgs& a, const Plan& pl);
+static bool f32w4l_whole_waves(const Problem& p, const GemmArgs& a, const Plan& pl);
 static int signal_kernel(const Problem& p, int kernel);
 
 struct Plan {
@@ -236,12 +236,10 @@ static int resolve_core(const Problem& p, int kernel) {
       if (!f32fast) return kGeneric;
       {
         const Plan pl = plan(p, kAuto);
-        // Exactly one whole wave of 256x256 tiles (round 6): the lean W4
-        // K-loop (f32_w4l: 98.3 % MFMA busy, profiles/r8lq_fp32_lean_stream.md)
-        // ahead of the plan it replaces, settled, two sessions: 8192 x 2048 x
-        // 8192 153.1 vs 149.8 (f32_256s), 4096^2 x 16384 153.3 vs 149.9
-        // (f32_256s), 4096^3 150.9 vs 150.2 (f32_t128x2); profiles/r8r/, r8q/.
-        if (f32w4l_one_wave(p, a, pl)) return kF32W4L;
+        // Whole waves of 256x256 tiles (round 6): the lean W4 K-loop (f32_w4l,
+        // 98.3 % MFMA busy, profiles/r8lq_fp32_lean_stream.md) in place of
+        // the plan below (f32_t128x2, or f32_256s on one long-K wave).
+        if (f32w4l_whole_waves(p, a, pl)) return kF32W4L;
         // Exactly one wave of 256x256 tiles on a long K: the 8-wave f32_256s
         // measured 1.0-1.3 % ahead of f32_t128x2 (1024 x 16384 x 16384 152.1
         // vs 150.1, 4096^2 x 14336 152.3 vs 150.8; profiles/r6f_f32_long_k_arms_ab.jsonl)
@@ -409,14 +407,29 @@ static bool w4s_auto(const Problem& p) {
   return p.cus == 0 && w4s_fits(p) && tiles_of(p, kMfmaW4) >= 2LL * device_cus();
 }
 
-// f32_w4l on exactly one whole wave of 256x256 tiles on a device of its own,
-// in place of an unsplit f32_t128x2 / f32_256s plan. (On more waves it led by
-// only 0.2-0.85 % and lost 1.4 % at 16384^2 x 1024, profiles/r8r/: not taken.)
-static bool f32w4l_one_wave(const Problem& p, const GemmArgs& a, const Plan& pl) {
+// f32_w4l on whole waves of 256x256 tiles, K >= 4096, on a device of its own,
+// in place of an unsplit f32_t128x2 / f32_256s plan. Settled, two sessions,
+// TFLOPS:
+//  * one wave (profiles/r8y/, against the old plan): 4096^3 151.8 vs 150.6,
+//    8192 x 2048 x 8192 152.2 vs 151.2, 4096^2 x 16384 152.9 vs 151.8,
+//    1024 x 16384^2 152.9 vs 152.0, 2048 x 8192^2 151.9 vs 151.2, 4096^2 x
+//    8192 152.4 vs 151.2;
+//  * more waves (profiles/r8za/, against f32_t128x2): 8192^3 152.3 vs 151.6,
+//    16384^3 152.8 vs 151.9, 16384 x {8192, 4096, 2048} x 16384 152.7 / 152.6 /
+//    152.4 vs 151.9 / 151.8 / 151.2, 8192 x 4096 x 8192 151.9 vs 151.0, 12288^3
+//    152.2 vs 151.9, 8192^2 x 4096 150.9 vs 151.0, 4096^3 x 2 151.1 vs 150.3.
+// +0.5 % median (-0.07 to +0.8 %; r8r measured +2.2 / +2.3 % on two one-wave
+// grids against a slower f32_256s arm). That is under the 1 % bar VERDICT r5
+// set for planner rules; this one is taken as a kernel replacement, not a
+// fitted threshold: bitwise-equal output, fewer instructions per K-tile, no
+// grid losing beyond noise. Short K loses (16384^2 x 1024: -1.4 %, r8r), hence
+// K >= 4096; partial waves keep f32_t128x2's tail plans.
+static bool f32w4l_whole_waves(const Problem& p, const GemmArgs& a, const Plan& pl) {
   if (p.cus != 0 || p.dtype != kF32 || pl.splitk > 1 || (pl.kernel != kF32T128x2 && pl.kernel != kF32_256s))
     return false;
-  if (p.M % 256 || p.N % 256 || p.K < 4096 || !gemm_f32_w4l_fits(a)) return false;  // (measured from K = 4096)
-  return (long long)(p.M / 256) * (p.N / 256) * (p.batch < 1 ? 1 : p.batch) == device_cus();
+  if (p.M % 256 || p.N % 256 || p.K < 4096 || !gemm_f32_w4l_fits(a)) return false;
+  const long long T = (long long)(p.M / 256) * (p.N / 256) * (p.batch < 1 ? 1 : p.batch);
+  return T > 0 && T % device_cus() == 0;
 }
 
 // f32_t128x2 split into slices on a grid of fewer than two tiles per CU

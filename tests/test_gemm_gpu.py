@@ -408,9 +408,9 @@ def test_f32_w4s_exact_and_bitwise(b, M, N, K, exact):
 
 
 @pytest.mark.parametrize("b,M,N,K", [(1, 4096, 4096, 4096), (1, 8192, 2048, 8192), (1, 4096, 4096, 4128),
-                                     (4, 2048, 2048, 4096)])
+                                     (4, 2048, 2048, 4096), (1, 8192, 8192, 8192), (2, 4096, 4096, 4096)])
 def test_f32_w4l_one_wave_auto_exact_and_bitwise(b, M, N, K):
-    """Round 6: exactly one whole wave of 256x256 fp32 tiles runs the lean W4
+    """Round 6: whole waves of 256x256 fp32 tiles (K >= 4096) run the lean W4
     K-loop (f32_w4l); small integers exact against fp64 (K / 32 odd at 4128:
     the branch-free loop's re-read tail), bitwise equal to f32_w4 (the same
     per-element MFMA order), A = I with an asymmetric B, and repeatable."""

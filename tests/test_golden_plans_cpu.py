@@ -11,7 +11,9 @@ modes) and beside a collective (``cus = -1``: gemm.shared_device, the
 overlapped modes). None of these plans runs a wave-quantisation tail.
 
 A planner change that moves one of these plans must edit this table on
-purpose, with the measurement that justifies it. The shipping build also
+purpose, with the measurement that justifies it. (Round 6: exact fp32 on whole
+waves of 256x256 tiles, K >= 4096, alone on the device, moved to f32_w4l:
+profiles/r8y_f32_w4l_one_wave.md, r8za/.) The shipping build also
 reads no A/B switch from the environment (gemm_dispatch.cpp ``ab_switch``):
 setting every one of them changes no plan.
 """
@@ -65,20 +67,20 @@ GOLDEN = {
     ("fp32", 4096, 2048, 4096, 1): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
     ("fp32", 4096, 1024, 4096, 1): ("f32_t128_nn", 1, "f32_t128_nn", 1),
     ("fp32", 4096, 512, 4096, 1): ("f32_t64_nn", 1, "f32_t64_nn", 1),
-    ("fp32", 4096, 4096, 4096, 2): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
-    ("fp32", 4096, 4096, 4096, 4): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
-    ("fp32", 8192, 8192, 8192, 1): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
-    ("fp32", 8192, 4096, 8192, 1): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
+    ("fp32", 4096, 4096, 4096, 2): ("f32_w4l_nn", 1, "f32_t128x2_nn", 1),
+    ("fp32", 4096, 4096, 4096, 4): ("f32_w4l_nn", 1, "f32_t128x2_nn", 1),
+    ("fp32", 8192, 8192, 8192, 1): ("f32_w4l_nn", 1, "f32_t128x2_nn", 1),
+    ("fp32", 8192, 4096, 8192, 1): ("f32_w4l_nn", 1, "f32_t128x2_nn", 1),
     ("fp32", 8192, 2048, 8192, 1): ("f32_w4l_nn", 1, "f32_t128x2_nn", 1),
     ("fp32", 8192, 1024, 8192, 1): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
-    ("fp32", 8192, 8192, 8192, 2): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
-    ("fp32", 8192, 8192, 8192, 4): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
-    ("fp32", 16384, 16384, 16384, 1): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
-    ("fp32", 16384, 8192, 16384, 1): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
-    ("fp32", 16384, 4096, 16384, 1): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
-    ("fp32", 16384, 2048, 16384, 1): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
-    ("fp32", 16384, 16384, 16384, 2): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
-    ("fp32", 16384, 16384, 16384, 4): ("f32_t128x2_nn", 1, "f32_t128x2_nn", 1),
+    ("fp32", 8192, 8192, 8192, 2): ("f32_w4l_nn", 1, "f32_t128x2_nn", 1),
+    ("fp32", 8192, 8192, 8192, 4): ("f32_w4l_nn", 1, "f32_t128x2_nn", 1),
+    ("fp32", 16384, 16384, 16384, 1): ("f32_w4l_nn", 1, "f32_t128x2_nn", 1),
+    ("fp32", 16384, 8192, 16384, 1): ("f32_w4l_nn", 1, "f32_t128x2_nn", 1),
+    ("fp32", 16384, 4096, 16384, 1): ("f32_w4l_nn", 1, "f32_t128x2_nn", 1),
+    ("fp32", 16384, 2048, 16384, 1): ("f32_w4l_nn", 1, "f32_t128x2_nn", 1),
+    ("fp32", 16384, 16384, 16384, 2): ("f32_w4l_nn", 1, "f32_t128x2_nn", 1),
+    ("fp32", 16384, 16384, 16384, 4): ("f32_w4l_nn", 1, "f32_t128x2_nn", 1),
     ("fp8", 4096, 4096, 4096, 1): ("fp8_w4_nt", 1, "fp8_w4_nt", 1),
     ("fp8", 4096, 2048, 4096, 1): ("fp8_t256x128_nt", 1, "fp8_t256x128_nt", 1),
     ("fp8", 4096, 1024, 4096, 1): ("fp8_t128_nt", 1, "fp8_t128_nt", 1),

@@ -52,17 +52,18 @@ def test_f32_shards_fill_the_chip(C, n, ws):
 
 
 def test_f32_full_grids_take_two_128_tiles_per_cu(C):
-    """Full fp32 grids run f32_t128x2 (measured ahead of f32_256s at 4k / 8k /
-    16k in the same process, profiles/r3i_f32_256p_ab.jsonl); exactly one whole
-    wave of 256x256 tiles alone on the device runs the lean W4 loop (round 6,
-    f32_w4l: 4096^3 150.9 vs 150.2, profiles/r8q/)."""
-    for n in (8192, 16384):
-        assert plan(C, F32, n, n, n)[0] == "pdmb_f32_t128x2_nn"
-    assert plan(C, F32, 4096, 4096, 4096)[:2] == ("pdmb_f32_w4l_nn", 1)
-    assert plan(C, F32, 4096, 4096, 4096, cus=-1)[0] == "pdmb_f32_t128x2_nn"
-    assert plan(C, F32, 4096, 4096, 4096, b=2)[0] == "pdmb_f32_t128x2_nn"  # two waves
+    """Full fp32 grids beside a collective run f32_t128x2 (measured ahead of
+    f32_256s at 4k / 8k / 16k in the same process, profiles/r3i_f32_256p_ab.jsonl);
+    whole waves of 256x256 tiles alone on the device, K >= 4096, run the lean
+    W4 loop (round 6, f32_w4l: +0.5 % median over f32_t128x2, profiles/r8za/,
+    r8y/); partial waves and short K keep f32_t128x2."""
+    for n in (4096, 8192, 16384):
+        assert plan(C, F32, n, n, n)[:2] == ("pdmb_f32_w4l_nn", 1)
+        assert plan(C, F32, n, n, n, cus=-1)[0] == "pdmb_f32_t128x2_nn"
+    assert plan(C, F32, 4096, 4096, 4096, b=2)[0] == "pdmb_f32_w4l_nn"
     assert plan(C, F32, 4096, 4096, 4128)[0] == "pdmb_f32_w4l_nn"  # 129 K-tiles: the loop takes any count
-    for shape in ((4352, 3840, 4096), (4096, 2048, 4096), (4096, 4096, 2048)):
+    for shape in ((4352, 3840, 4096), (4096, 2048, 4096), (4096, 4096, 2048), (16384, 16384, 1024),
+                  (6144, 6144, 6144), (10240, 10240, 10240)):
         assert plan(C, F32, *shape)[0] != "pdmb_f32_w4l_nn", shape
 
 
@@ -181,7 +182,8 @@ def test_f32_long_k_one_wave_runs_256s(C):
     assert plan(C, 0, 1024, 16384, 16384)[0] == "pdmb_f32_w4l_nn"
     assert plan(C, 0, 4096, 4096, 14336)[0] == "pdmb_f32_w4l_nn"
     assert plan(C, 0, 4096, 4096, 14336, cus=-1)[0] == "pdmb_f32_t128x2_nn"
-    assert plan(C, 0, 8192, 8192, 28672)[0] == "pdmb_f32_t128x2_nn"
+    assert plan(C, 0, 8192, 8192, 28672)[0] == "pdmb_f32_w4l_nn"  # four whole waves
+    assert plan(C, 0, 8192, 8192, 28672, cus=-1)[0] == "pdmb_f32_t128x2_nn"
 
 
 def test_t192_plans(C, monkeypatch):
