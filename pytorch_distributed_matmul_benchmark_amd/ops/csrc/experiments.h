@@ -28,7 +28,7 @@ static bool is_experiment(int k) {
     case kF32W4NB: case kF32W4NBP: case kF32W4NoDma: case kF32W4NoFrag: case kF32W4MfmaBar:
     case kF32W4MfmaOnly: case kF32W4Spread: case kF32W4SpreadDma: case kF32W4SpreadRd:
     case kF32W4Lean: case kF32W4Lean2: case kF32T128Lean: case kF32T128x2Lean: case kF32T64Lean:
-    case kF32T64x2Lean: case kF32W4S: case kF32W4SDbg:
+    case kF32T64x2Lean: case kF32W4S: case kF32W4SDbg: case kMfmaW4SLean:
       return true;
     default:
       return false;
@@ -82,6 +82,7 @@ static int experiment_resolve(const Problem& p, int kernel, bool fast, bool w4, 
     case kMfmaW4STall: case kMfmaW4SWide: case kMfmaW4SSnake: case kMfmaW4SMcol: case kMfmaW4SSt9:
       return (p.dtype == kBF16 && w4 && w4s_fits(p)) ? kernel : -1;
     case kMfmaW4St9: return (p.dtype == kBF16 && w4) ? kernel : -1;
+    case kMfmaW4SLean: return w4 && w4s_fits(p) && gemm_w4s_lean_fits(shape_args(p)) ? kernel : -1;
     case kMfmaW4Pers: return w4 ? kernel : -1;  // bf16 and fp16
     default: return -1;
   }
@@ -137,6 +138,7 @@ static hipError_t experiment_launch(const Problem& p, int k, const GemmArgs& a, 
     case kMfmaW4SSnake: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 19);
     case kMfmaW4SMcol: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 20);
     case kMfmaW4SSt9: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 21);
+    case kMfmaW4SLean: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 23);
     case kMfmaW4St9: {
       GemmArgs s = a;
       s.splitk = 1;
@@ -240,6 +242,7 @@ static const char* experiment_name(int kernel) {
     case kF32T64x2Lean: return "pdmb_f32_t64x2_lean";
     case kF32W4S: return "pdmb_f32_w4s";
     case kF32W4SDbg: return "pdmb_f32_w4s_dbg";
+    case kMfmaW4SLean: return "pdmb_w4s_lean";
     case kF32W4Lean: return "pdmb_f32_w4_lean";
     case kF32W4Lean2: return "pdmb_f32_w4_lean2";
     case kFp8W4Trace: return "pdmb_fp8_w4_nt_trace";

@@ -31,6 +31,7 @@ hipError_t gemm_f32_256_launch(GemmArgs a, int variant, hipStream_t stream);
 hipError_t gemm_f32_w4_launch(GemmArgs a, hipStream_t stream, int variant);
 bool gemm_f32_w4s_fits(const GemmArgs& a);  // experiments build: kF32W4S
 bool gemm_f32_w4l_fits(const GemmArgs& a);
+bool gemm_w4s_lean_fits(const GemmArgs& a);  // experiments build: kMfmaW4SLean
 bool gemm_f32_tile_supported(const GemmArgs& a, size_t align_a, size_t align_b, size_t align_c);
 bool gemm_f32_tile_ln_fits(const GemmArgs& a);
 hipError_t gemm_f32_tile_launch(GemmArgs a, hipStream_t stream, int variant);
@@ -1171,7 +1172,7 @@ static hipError_t tiled_launch(const Problem& p, int k, GemmArgs a, void* part, 
     }
   }
   a.splitk = S;
-  if ((sub >= 7 && sub <= 11) || (sub >= 13 && sub <= 21)) {  // W4S (13-16: power diag, 17-21: tile order), unsplit, one
+  if ((sub >= 7 && sub <= 11) || (sub >= 13 && sub <= 21) || sub == 23) {  // W4S (13-16: power diag, 17-21: tile order, 23: lean), unsplit, one
                                                               // workgroup per usable CU (a multiple of 8)
     if (S > 1) {
       sub = 0;

@@ -87,6 +87,30 @@ __device__ __forceinline__ void dma16_m0(u32x4 rsrc, uint32_t voff, uint32_t sof
       : "memory", "m0");
 }
 
+// LN (experiments, round 6): the MFMA of a DMA item's gap fused with the piece,
+// as gemm_f32_w4.hip's mfma_dma: M0 in one SALU from the wave's base, the MFMA
+// as the wait state M0 needs (no s_nop).
+template <int DT>
+__device__ __forceinline__ void mfma_dma_w4(f32x4& acc, const s16x8& b, const s16x8& a, u32x4 rsrc, uint32_t voff,
+                                            uint32_t soff, uint32_t lds0w, int imm) {
+  if constexpr (DT == kBF16)
+    asm volatile(
+        "s_add_u32 m0, %5, %6\n\t"
+        "v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\t"
+        "buffer_load_dwordx4 %3, %4, %7 offen lds"
+        : "+a"(acc)
+        : "v"(b), "v"(a), "v"(voff), "s"(rsrc), "s"(lds0w), "i"(imm), "s"(soff)
+        : "memory", "m0", "scc");
+  else
+    asm volatile(
+        "s_add_u32 m0, %5, %6\n\t"
+        "v_mfma_f32_16x16x32_f16 %0, %1, %2, %0\n\t"
+        "buffer_load_dwordx4 %3, %4, %7 offen lds"
+        : "+a"(acc)
+        : "v"(b), "v"(a), "v"(voff), "s"(rsrc), "s"(lds0w), "i"(imm), "s"(soff)
+        : "memory", "m0", "scc");
+}
+
 struct Frag {  // one 16-row (A) or 16-column (B) block of a K-tile: k 0..31 and 32..63
   s16x8 k[2];
 };
@@ -581,13 +605,21 @@ __device__ __forceinline__ u32x4 src_b(const Src& s, int kt, int ldb2) {
 // of VERDICT r4 #8, scripts/power_attrib.py): bit 0 drops the fragment reads
 // (the MFMAs keep re-using the registers they hold), bit 1 the LDS-DMA refills;
 // every MFMA, wait and barrier stays.
-template <int DT, int SO, int W0, int W1, bool ZERO = false, int DIAG = 0>
+// LN (experiments, round 6: kMfmaW4SLean): the descriptors are the tile's, at
+// K = 0 (rbT: B's; built once per tile), the K-tile offsets ride in the
+// voffsets (kaT for A, kbT for B: one VALU add each per K-tile instead of
+// a soffset add per A piece and a new B descriptor per K-tile), and outside
+// the first two K-tiles (W0 48, dma16_at_pad) each piece is fused with its
+// gap's MFMA (mfma_dma_w4: no s_nop).
+template <int DT, int SO, int W0, int W1, bool ZERO = false, int DIAG = 0, bool LN = false>
 __device__ __forceinline__ void ktile_s(const Ctx& c, const char* smem, u32x4 raT, uint32_t kaT,
                                         u32x4 rbT, f32x4 (&acc)[8][8], Frag (&A)[8], Frag& A7c,
-                                        Frag& A7n, Frag (&Bc)[8], Frag (&Bn)[8]) {
+                                        Frag& A7n, Frag (&Bc)[8], Frag (&Bn)[8], uint32_t kbT = 0) {
   constexpr int IL = 64;
   constexpr int SN = STAGE - SO;
   constexpr int sn = SN / STAGE;
+  const uint32_t vA = LN ? c.voffA + kaT : c.voffA, vB = LN ? c.voffB + kbT : c.voffB;
+  const uint32_t kaS = LN ? 0u : kaT;  // the A soffsets' K part
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi) {
     if (mi == 0) {
@@ -600,11 +632,27 @@ __device__ __forceinline__ void ktile_s(const Ctx& c, const char* smem, u32x4 ra
 #pragma unroll
     for (int gap = 0; gap < 16; ++gap) {
       const int ks = gap >> 3, ni = gap & 7;
+      const int it = kItems[mi][gap];
+      if constexpr (LN && W0 != 48 && !(DIAG & 2) && !ZERO) {
+        if (it == 1) {  // the gap's MFMA and DMA piece in one asm block
+          const int h = piece_of(mi, gap);
+          const s16x8& av = mi == 7 ? A7c.k[ks] : A[mi].k[ks];
+          if (h < 8) {
+            mfma_dma_w4<DT>(acc[mi][ni], Bc[ni].k[ks], av, raT, vA, (uint32_t)(h * 32 * c.lda2), c.lds0w,
+                            SO + h * 32 * 128);
+          } else {
+            const int nq = (h - 8) >> 2, kb = (h - 8) & 3;
+            mfma_dma_w4<DT>(acc[mi][ni], Bc[ni].k[ks], av, rbT, vB, (uint32_t)(kb * 16 * c.ldb2 + nq * IL * 2),
+                            c.lds0w, SN + A_BYTES + nq * BH_BYTES + kb * 16 * 256);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          continue;
+        }
+      }
       if (ZERO && ks == 0)
         mfma_zero<DT>(acc[mi][ni], Bc[ni].k[ks], mi == 7 ? A7c.k[ks] : A[mi].k[ks]);
       else
         mfma_acc<DT>(acc[mi][ni], Bc[ni].k[ks], mi == 7 ? A7c.k[ks] : A[mi].k[ks]);
-      const int it = kItems[mi][gap];
       if ((DIAG & 2) && it == 1) {
         // no refill (timing-only)
       } else if ((DIAG & 1) && it >= 100) {
@@ -615,16 +663,16 @@ __device__ __forceinline__ void ktile_s(const Ctx& c, const char* smem, u32x4 ra
           // the first two K-tiles of a tile (W0 48): soffsets hipcc may have
           // just restored with v_readlane (common.h dma16_at_pad)
           if constexpr (W0 == 48)
-            dma16_at_pad(raT, c.voffA, kaT + (uint32_t)(h * 32 * c.lda2), c.lds0w, SO + h * 32 * 128);
+            dma16_at_pad(raT, vA, kaS + (uint32_t)(h * 32 * c.lda2), c.lds0w, SO + h * 32 * 128);
           else
-            dma16_at(raT, c.voffA, kaT + (uint32_t)(h * 32 * c.lda2), c.lds0w, SO + h * 32 * 128);
+            dma16_at(raT, vA, kaS + (uint32_t)(h * 32 * c.lda2), c.lds0w, SO + h * 32 * 128);
         } else {
           const int nq = (h - 8) >> 2, kb = (h - 8) & 3;
           if constexpr (W0 == 48)
-            dma16_at_pad(rbT, c.voffB, (uint32_t)(kb * 16 * c.ldb2 + nq * IL * 2), c.lds0w,
+            dma16_at_pad(rbT, vB, (uint32_t)(kb * 16 * c.ldb2 + nq * IL * 2), c.lds0w,
                          SN + A_BYTES + nq * BH_BYTES + kb * 16 * 256);
           else
-            dma16_at(rbT, c.voffB, (uint32_t)(kb * 16 * c.ldb2 + nq * IL * 2), c.lds0w,
+            dma16_at(rbT, vB, (uint32_t)(kb * 16 * c.ldb2 + nq * IL * 2), c.lds0w,
                      SN + A_BYTES + nq * BH_BYTES + kb * 16 * 256);
         }
       } else if (it >= 100 && it < 200) {
@@ -649,7 +697,7 @@ __device__ __forceinline__ void ktile_s(const Ctx& c, const char* smem, u32x4 ra
 // wait counts the same (timing-only, WRONG results).
 // SUB: map_tile's XCD sub-block shape (0 = 4 x 8; 1 = 8 x 4 and 2 = 2 x 16 are
 // the tile-order A/Bs of kMfmaW4STall / kMfmaW4SWide).
-template <int DT, int TRACE = 0, bool NTS = true, int DIAG = 0, int SUB = 0>  // NTS: non-temporal C stores (false: A/B)
+template <int DT, int TRACE = 0, bool NTS = true, int DIAG = 0, int SUB = 0, bool LN = false>  // NTS: non-temporal C stores (false: A/B)
 __global__ void __launch_bounds__(NT, 1) gemm_w4s(GemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 4 * kEpiBuf];
   TileTrace tr;
@@ -795,32 +843,41 @@ __global__ void __launch_bounds__(NT, 1) gemm_w4s(GemmArgs a) {
                                    sel(m, (uint32_t)pc, (uint32_t)pn);
       const long long bytes = (long long)(((unsigned long long)sel(m, (uint32_t)(bc >> 32), (uint32_t)(bn >> 32)) << 32) |
                                           sel(m, (uint32_t)bc, (uint32_t)bn));
-      const long long off = (long long)k * BK * c.ldb2;
+      const long long off = LN ? 0 : (long long)k * BK * c.ldb2;  // LN: K-tile offset in the voffset
       return make_rsrc((const char*)p + off, bytes - off);
     };
+    auto tgt_kb = [&](int kt) -> uint32_t {  // LN: B's K-tile byte offset of item kt
+      const int k = kt < nk ? kt : (more ? kt - nk : nk - 1);
+      return (uint32_t)k * (uint32_t)(BK * c.ldb2);
+    };
+    const u32x4 rb0 = make_rsrc(cur.Bb, cur.b_bytes);  // LN: this tile's B from K = 0
+    auto bsrc = [&](int kt) { return LN ? rb0 : src_b(cur, kt, c.ldb2); };
+    auto bkoff = [&](int kt) { return LN ? (uint32_t)kt * (uint32_t)(BK * c.ldb2) : 0u; };
     // K-tiles 0 and 1 (32 stores or dummies per wave are younger than the
     // DMAs they wait for), then pairs whose DMA targets stay in this tile
     // (W4's instruction mix: no selects), then the last two pairs, whose
     // targets cross into the next tile (nk >= 6: host-checked).
     constexpr int KD = DIAG & 3;
-    ktile_s<DT, 0, 48, 48, true, KD>(c, smem, cur.ra, 2 * (BK * 2), src_b(cur, 3, c.ldb2), acc, A, A7a,
-                                     A7b, B0, B1);
-    ktile_s<DT, STAGE, 48, 16, false, KD>(c, smem, cur.ra, 3 * (BK * 2), src_b(cur, 4, c.ldb2), acc, A,
-                                          A7b, A7a, B1, B0);
+    ktile_s<DT, 0, 48, 48, true, KD, LN>(c, smem, cur.ra, 2 * (BK * 2), bsrc(3), acc, A, A7a, A7b, B0, B1,
+                                         bkoff(3));
+    ktile_s<DT, STAGE, 48, 16, false, KD, LN>(c, smem, cur.ra, 3 * (BK * 2), bsrc(4), acc, A, A7b, A7a, B1,
+                                              B0, bkoff(4));
     int t = 2;
     for (; t + 4 < nk; t += 2) {
-      ktile_s<DT, 0, 16, 16, false, KD>(c, smem, cur.ra, (uint32_t)(t + 2) * (BK * 2),
-                                        src_b(cur, t + 3, c.ldb2), acc, A, A7a, A7b, B0, B1);
-      ktile_s<DT, STAGE, 16, 16, false, KD>(c, smem, cur.ra, (uint32_t)(t + 3) * (BK * 2),
-                                            src_b(cur, t + 4, c.ldb2), acc, A, A7b, A7a, B1, B0);
+      ktile_s<DT, 0, 16, 16, false, KD, LN>(c, smem, cur.ra, (uint32_t)(t + 2) * (BK * 2), bsrc(t + 3), acc, A,
+                                            A7a, A7b, B0, B1, bkoff(t + 3));
+      ktile_s<DT, STAGE, 16, 16, false, KD, LN>(c, smem, cur.ra, (uint32_t)(t + 3) * (BK * 2), bsrc(t + 4), acc,
+                                                A, A7b, A7a, B1, B0, bkoff(t + 4));
     }
     for (; t < nk; t += 2) {
       u32x4 ra;
       uint32_t ka;
       tgt_a(t + 2, ra, ka);
-      ktile_s<DT, 0, 16, 16, false, KD>(c, smem, ra, ka, tgt_b(t + 3), acc, A, A7a, A7b, B0, B1);
+      ktile_s<DT, 0, 16, 16, false, KD, LN>(c, smem, ra, ka, tgt_b(t + 3), acc, A, A7a, A7b, B0, B1,
+                                            LN ? tgt_kb(t + 3) : 0u);
       tgt_a(t + 3, ra, ka);
-      ktile_s<DT, STAGE, 16, 16, false, KD>(c, smem, ra, ka, tgt_b(t + 4), acc, A, A7b, A7a, B1, B0);
+      ktile_s<DT, STAGE, 16, 16, false, KD, LN>(c, smem, ra, ka, tgt_b(t + 4), acc, A, A7b, A7a, B1, B0,
+                                                LN ? tgt_kb(t + 4) : 0u);
     }
     // The last MFMAs write their AGPRs before the epilogue reads them (asm
     // MFMAs are invisible to hipcc's hazard recognizer).
@@ -894,6 +951,13 @@ bool gemm_w4_supported(int dt, const GemmArgs& a, size_t align_a, size_t align_b
   if ((long long)256 * a.lda * 2 + (long long)a.K * 2 >= (1LL << 31)) return false;
   if ((long long)64 * a.ldb * 2 + 128 >= (1LL << 31)) return false;
   return true;
+}
+
+// kMfmaW4SLean's 32-bit voffsets carry the K-tile offset: A's 256 rows plus
+// its whole K, and B's K + 128 rows, must stay below 2^31 bytes.
+bool gemm_w4s_lean_fits(const GemmArgs& a) {
+  return (long long)256 * a.lda * 2 + (long long)a.K * 2 < (1LL << 31) &&
+         (long long)(a.K + 128) * a.ldb * 2 < (1LL << 31);
 }
 
 hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
@@ -1011,6 +1075,17 @@ hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
       if (a.supertile == 1) a.supertile = sub == 19 ? 7 : 8;
       hipLaunchKernelGGL((kw4::gemm_w4s<kBF16>), pg, block, 0, stream, a);
     }
+    return hipGetLastError();
+  }
+  if (sub == 23) {  // kMfmaW4SLean: W4S on the lean DMA issue (bf16 / fp16)
+    if (S > 1 || a.pers_grid <= 0 || a.pers_grid % 8 || (a.K / kw4::BK) % 2 || a.K / kw4::BK < 6 ||
+        !gemm_w4s_lean_fits(a))
+      return hipErrorInvalidValue;
+    const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
+    if (dt == kBF16)
+      hipLaunchKernelGGL((kw4::gemm_w4s<kBF16, 0, true, 0, 0, true>), pg, block, 0, stream, a);
+    else
+      hipLaunchKernelGGL((kw4::gemm_w4s<kF16, 0, true, 0, 0, true>), pg, block, 0, stream, a);
     return hipGetLastError();
   }
   if (sub == 8) {  // W4S with per-workgroup start / end stamps
