@@ -541,6 +541,15 @@ hipError_t gemm_f32_tile_launch(GemmArgs a, hipStream_t stream, int variant) {
     return hipGetLastError();
   }
   if (variant != 0) return hipErrorInvalidValue;
+  if (S == 1 && gemm_f32_tile_ln_fits(a)) {
+    // Unsplit kF32T128 runs the lean K-loop (round 6, bitwise equal): +0.6-0.7 %
+    // on 4096 x 1024 x 4096, 2048^3, 4096 x 2048 x 4096 (settled, two sessions,
+    // profiles/r8v_fp32_tile_lean.md). Split slices keep the plain loop (not
+    // measured lean), and so do the two-per-CU and 64-row forms (lean lost there).
+    hipLaunchKernelGGL((kf32t::gemm_f32_t128<4, true, 128, true>), dim3((unsigned)nblocks), dim3(kf32t::NT), 0,
+                       stream, a);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL((kf32t::gemm_f32_t128<4, true>), dim3((unsigned)nblocks), dim3(kf32t::NT), 0, stream, a);
   return hipGetLastError();
 }
