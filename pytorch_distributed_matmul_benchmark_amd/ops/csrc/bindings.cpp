@@ -583,6 +583,10 @@ int64_t host_stamp_alloc(int64_t bytes) {
   pdmb::set_debug_buffer(p);
   return (int64_t)(uintptr_t)p;
 }
+void host_stamp_free(int64_t ptr) {  // (clears the debug buffer it set)
+  pdmb::set_debug_buffer(nullptr);
+  if (ptr) check_hip(hipHostFree((void*)(uintptr_t)ptr), "hipHostFree");
+}
 std::vector<int64_t> host_stamp_read(int64_t ptr, int64_t n) {
   const volatile long long* q = (const volatile long long*)(uintptr_t)ptr;
   std::vector<int64_t> out((size_t)n);
@@ -649,6 +653,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("EXPERIMENTS") = pdmb::experiments_built();
   m.def("host_stamp_alloc", &host_stamp_alloc, py::arg("bytes"));
   m.def("host_stamp_read", &host_stamp_read, py::arg("ptr"), py::arg("n"));
+  m.def("host_stamp_free", &host_stamp_free, py::arg("ptr"));
   m.attr("MAX_SPLIT_TILES") = pdmb::kMaxSplitTiles;
   m.attr("ARCH") = "gfx950";
 }

@@ -7,8 +7,9 @@ GEMM has to itself), the ``gemm_tile.hip`` family (T128 / T256x128 /
 T128x2 / T192 / T192x128, split-K) for grids that under-fill the 256 CUs or
 that only 192-row tiles cut into whole waves, SCHED 3 of
 ``gemm_mfma256.hip`` for edge tiles the others do not take; exact fp32 on
-``gemm_f32_tile.hip`` (f32_t128x2 on grids of >= 2 tiles per CU, f32_t128
-split-K below that, f32_t64 = 64x128 tiles where they fill the chip unsplit, f32_t64x2 = those two per CU, split), ``gemm_f32_256.hip`` and ``gemm_f32_w4.hip`` (split-K)
+``gemm_f32_w4.hip`` (f32_w4l, the lean K-loop, on whole waves of 256x256
+tiles alone on the device), ``gemm_f32_tile.hip`` (f32_t128x2 on other grids of
+>= 2 tiles per CU, f32_t128 unsplit on the lean loop or split-K below that, f32_t64 = 64x128 tiles where they fill the chip unsplit, f32_t64x2 = those two per CU, split), ``gemm_f32_256.hip`` and ``gemm_f32_w4.hip`` (split-K)
 as the planner prices them; fp8 e4m3 on ``gemm_fp8.hip`` and
 the fp8 tile family; ``gemm_generic.hip`` for anything else. Large problems
 whose K / N / alignment miss the LDS-DMA granule are zero-padded onto the
