@@ -15,7 +15,8 @@
 # hipBLASLt, every dtype at 4k / 8k / 16k), reduce_bench (reduce_sum bandwidth), queue_probe (hardware-queue
 # false dependencies, scripts/queue_probe.py), selflaunch8 / selflaunch8_ipc / selflaunch8_chunks
 # (bench.py --gpus 8 on one GPU over gloo), mask_probe (CU-mask placement at W4S occupancy,
-# runtime/cu_mask_probe), pmc (PMC passes: scripts/gpu_pmc.sh with
+# runtime/cu_mask_probe), cli (every reference launcher at N = 1, --check), cli_dtypes
+# (run_benchmark.sh fp16 / fp32), pmc (PMC passes: scripts/gpu_pmc.sh with
 # N / KS / DT from the environment). After "--": one ad-hoc step NAME with a SECONDS limit.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -99,6 +100,8 @@ run_stage() {
          step cli_pipeline 400 backup/run_overlap_benchmark.sh 1 pipeline bfloat16 &&
          step cli_dp 400 backup/run_distributed_benchmark.sh 1 data_parallel bfloat16 --check &&
          step cli_fp8 400 ./run_benchmark.sh 1 float8_e4m3fn --check ;;
+    cli_dtypes) step cli_fp16 400 ./run_benchmark.sh 1 float16 --check &&
+                step cli_fp32 400 ./run_benchmark.sh 1 float32 --check ;;
     tests_gemm) step tests_gemm 900 $PYT tests/test_gemm_gpu.py tests/test_modes_gpu.py -m gpu ;;
     tests_overlap) step tests_overlap 900 $PYT tests/test_signal_gpu.py tests/test_overlap_gpu.py \
                      tests/test_native_bench_gpu.py tests/test_multirank_gpu.py -m gpu ;;
