@@ -403,6 +403,22 @@ inline int choose_supertile(int tiles_m, int tiles_n) {
   return 0;
 }
 
+#ifdef PDMB_EXPERIMENTS
+// Experiments (round 6): the thin round that follows the grid's aspect, in
+// place of the 16 x 16 round, for 1-4 rounds of a wide or tall grid
+// (kFp8W4SThin / kMfmaW4SThin): wide 4 x 64 then 8 x 32, tall 64 x 4 then 32 x 8.
+inline int thin_supertile(int tiles_m, int tiles_n) {
+  if (tiles_n > tiles_m) {
+    if (tiles_m % 4 == 0 && tiles_n % 64 == 0) return 4;
+    if (tiles_m % 8 == 0 && tiles_n % 32 == 0) return 2;
+  } else if (tiles_m > tiles_n) {
+    if (tiles_m % 64 == 0 && tiles_n % 4 == 0) return 5;
+    if (tiles_m % 32 == 0 && tiles_n % 8 == 0) return 3;
+  }
+  return choose_supertile(tiles_m, tiles_n);
+}
+#endif
+
 __host__ __device__ __forceinline__ void map_tile(const GemmArgs& a, int b, int& bz, int& tm, int& tn,
                                                   int sub = 0) {
   const int tpb = a.tiles_m * a.tiles_n;

@@ -82,7 +82,9 @@ enum ExperimentKernel : int {
   kF32T64Lean = 94,      //   M0 in one SALU, the DMA piece fused with its gap's MFMA; round 6)
   kF32T64x2Lean = 95,
   kF32W4SDbg = 96,       // f32_w4s stamping its progress into a host-mapped buffer (diagnostic)
-  kMfmaW4SLean = 97,     // W4S with the lean DMA issue (voffset K-offsets, tile descriptors, fused pieces)
+  kMfmaW4SLean = 97,
+  kFp8W4SThin = 98,      // fp8 W4S / W4S with the thin round that follows the grid's aspect
+  kMfmaW4SThin = 99,     //   (common.h thin_supertile) in place of the 16 x 16 round     // W4S with the lean DMA issue (voffset K-offsets, tile descriptors, fused pieces)
 };
 
 }  // namespace pdmb

@@ -28,7 +28,7 @@ static bool is_experiment(int k) {
     case kF32W4NB: case kF32W4NBP: case kF32W4NoDma: case kF32W4NoFrag: case kF32W4MfmaBar:
     case kF32W4MfmaOnly: case kF32W4Spread: case kF32W4SpreadDma: case kF32W4SpreadRd:
     case kF32W4Lean: case kF32W4Lean2: case kF32T128Lean: case kF32T128x2Lean: case kF32T64Lean:
-    case kF32T64x2Lean: case kF32W4S: case kF32W4SDbg: case kMfmaW4SLean:
+    case kF32T64x2Lean: case kF32W4S: case kF32W4SDbg: case kMfmaW4SLean: case kFp8W4SThin: case kMfmaW4SThin:
       return true;
     default:
       return false;
@@ -39,12 +39,12 @@ static bool experiment_is_fp8(int k) {
   return k == kFp8 || k == kFp8W4TS || k == kFp8W4STS || k == kFp8W4Unfused || k == kFp8T128Unfused ||
          k == kFp8W4Diag || k == kFp8W4Diag2 || k == kFp8W4Diag3 || k == kFp8W4Tall || k == kFp8W4Wide ||
          k == kFp8W4Scaled || k == kFp8W4Trace || k == kFp8W4SK4 || k == kFp8W4SK4TS || k == kFp8W4SSt9 ||
-         k == kFp8W4St9;
+         k == kFp8W4St9 || k == kFp8W4SThin;
 }
 
 static int experiment_resolve_fp8(const Problem& p, int kernel, bool s_fits) {
   if (kernel == kFp8W4STS) return s_fits ? kernel : -1;
-  if (kernel == kFp8W4SSt9) return s_fits ? kernel : -1;
+  if (kernel == kFp8W4SSt9 || kernel == kFp8W4SThin) return s_fits ? kernel : -1;
   if (kernel == kFp8W4St9) return kernel;
   if (kernel == kFp8W4SK4 || kernel == kFp8W4SK4TS)
     return gemm_fp8_w4s_k4_fits(shape_args(p)) && device_cus() % 8 == 0 ? kernel : -1;
@@ -83,6 +83,7 @@ static int experiment_resolve(const Problem& p, int kernel, bool fast, bool w4, 
       return (p.dtype == kBF16 && w4 && w4s_fits(p)) ? kernel : -1;
     case kMfmaW4St9: return (p.dtype == kBF16 && w4) ? kernel : -1;
     case kMfmaW4SLean: return w4 && w4s_fits(p) && gemm_w4s_lean_fits(shape_args(p)) ? kernel : -1;
+    case kMfmaW4SThin: return w4 && w4s_fits(p) ? kernel : -1;
     case kMfmaW4Pers: return w4 ? kernel : -1;  // bf16 and fp16
     default: return -1;
   }
@@ -139,6 +140,13 @@ static hipError_t experiment_launch(const Problem& p, int k, const GemmArgs& a, 
     case kMfmaW4SMcol: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 20);
     case kMfmaW4SSt9: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 21);
     case kMfmaW4SLean: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 23);
+    case kMfmaW4SThin: return tiled_launch(p, kMfmaW4, a, p.workspace, p.workspace_bytes, stream, 24);
+    case kFp8W4SThin: {
+      GemmArgs s = a;
+      s.splitk = 1;
+      s.pers_grid = ((p.cus > 0 ? p.cus : device_cus()) / 8) * 8;
+      return gemm_fp8_launch(s, 23, stream);
+    }
     case kMfmaW4St9: {
       GemmArgs s = a;
       s.splitk = 1;
@@ -259,6 +267,8 @@ static const char* experiment_name(int kernel) {
     case kMfmaW4SSt9: return "pdmb_w4s_st9";
     case kMfmaW4St9: return "pdmb_w4_nn_st9";
     case kFp8W4SSt9: return "pdmb_fp8_w4s_st9";
+    case kFp8W4SThin: return "pdmb_fp8_w4s_thin";
+    case kMfmaW4SThin: return "pdmb_w4s_thin";
     case kFp8W4St9: return "pdmb_fp8_w4_nt_st9";
     default: return "auto";
   }

@@ -1172,7 +1172,7 @@ static hipError_t tiled_launch(const Problem& p, int k, GemmArgs a, void* part, 
     }
   }
   a.splitk = S;
-  if ((sub >= 7 && sub <= 11) || (sub >= 13 && sub <= 21) || sub == 23) {  // W4S (13-16: power diag, 17-21: tile order, 23: lean), unsplit, one
+  if ((sub >= 7 && sub <= 11) || (sub >= 13 && sub <= 21) || sub == 23 || sub == 24) {  // W4S (13-16: power diag, 17-21, 24: tile order, 23: lean), unsplit, one
                                                               // workgroup per usable CU (a multiple of 8)
     if (S > 1) {
       sub = 0;

@@ -1161,6 +1161,15 @@ hipError_t gemm_fp8_launch(GemmArgs a, int variant, hipStream_t stream) {
         hipLaunchKernelGGL(k8::gemm_fp8_w4s<true>, pg, dim3(k8::NT4), 0, stream, a);
     }
   }
+  else if (variant == 23) {  // kFp8W4SThin: W4S with the aspect-following thin round
+    if (!gemm_fp8_w4s_fits(a) || a.pers_grid <= 0 || a.pers_grid % 8 || S > 1) return hipErrorInvalidValue;
+    a.supertile = thin_supertile(a.tiles_m, a.tiles_n);
+    const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
+    if (a.K / k8::BK < 6)
+      hipLaunchKernelGGL((k8::gemm_fp8_w4s<true, true>), pg, dim3(k8::NT4), 0, stream, a);
+    else
+      hipLaunchKernelGGL(k8::gemm_fp8_w4s<true>, pg, dim3(k8::NT4), 0, stream, a);
+  }
   else if (variant == 19 || variant == 20) {  // kFp8W4SK4 / kFp8W4SK4TS: W4S down to nk == 4
     if (!gemm_fp8_w4s_k4_fits(a) || a.pers_grid <= 0 || a.pers_grid % 8) return hipErrorInvalidValue;
     const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));

@@ -1077,6 +1077,17 @@ hipError_t gemm_w4_launch(int dt, GemmArgs a, hipStream_t stream, int sub) {
     }
     return hipGetLastError();
   }
+  if (sub == 24) {  // kMfmaW4SThin: W4S with the aspect-following thin round
+    if (S > 1 || a.pers_grid <= 0 || a.pers_grid % 8 || (a.K / kw4::BK) % 2 || a.K / kw4::BK < 6)
+      return hipErrorInvalidValue;
+    a.supertile = thin_supertile(a.tiles_m, a.tiles_n);
+    const dim3 pg((unsigned)(nblocks < a.pers_grid ? nblocks : a.pers_grid));
+    if (dt == kBF16)
+      hipLaunchKernelGGL((kw4::gemm_w4s<kBF16>), pg, block, 0, stream, a);
+    else
+      hipLaunchKernelGGL((kw4::gemm_w4s<kF16>), pg, block, 0, stream, a);
+    return hipGetLastError();
+  }
   if (sub == 23) {  // kMfmaW4SLean: W4S on the lean DMA issue (bf16 / fp16)
     if (S > 1 || a.pers_grid <= 0 || a.pers_grid % 8 || (a.K / kw4::BK) % 2 || a.K / kw4::BK < 6 ||
         !gemm_w4s_lean_fits(a))

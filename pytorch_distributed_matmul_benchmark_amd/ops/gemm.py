@@ -66,7 +66,7 @@ EXPERIMENT_KERNELS = {"mfma256": 1, "mfma256b": 3, "mfma256c": 4, "mfma256c_stam
                       "x_f32_w4_spread_rd": 88, "x_f32_w4_lean": 89, "x_f32_w4_lean2": 90, "x_f32_w4s": 91,
                       "x_f32_t128_lean": 92, "x_f32_t128x2_lean": 93, "x_f32_t64_lean": 94,
                       "x_f32_t64x2_lean": 95, "diag_f32_w4s_dbg": 96,
-                      "x_w4s_lean": 97}
+                      "x_w4s_lean": 97, "x_fp8_w4s_thin": 98, "x_w4s_thin": 99}
 KERNEL_NAMES = {0: "auto", 2: "pdmb_generic_nn", 7: "pdmb_f32_256s_nn", 9: "pdmb_mfma256d_nn",
                 16: "pdmb_fp8_w4_nt", 21: "pdmb_w4_nn", 26: "pdmb_t128_nn",
                 27: "pdmb_t128x2_nn", 28: "pdmb_t256x128_nn", 29: "pdmb_f32_w4_nn", 36: "pdmb_w4s",

@@ -423,3 +423,25 @@ def test_fp8_stream_k(shape, mode, monkeypatch):
     C2 = torch.empty_like(ref)
     assert gemm.bench_matmul(A8, B8, C2, 3, 1, graph=True) > 0
     assert torch.equal(C2, torch.matmul(Af.double(), Bf.double()).to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("kernel,base", [("x_fp8_w4s_thin", "fp8_w4s"), ("x_w4s_thin", "w4s")])
+@pytest.mark.parametrize("M,N,K", [(4096, 16384, 1024), (2048, 16384, 1024), (16384, 4096, 1024),
+                                   (16384, 2048, 1024), (8192, 8192, 1024)])
+def test_thin_round_w4s_matches_shipping_bitwise(kernel, base, M, N, K):
+    """W4S with the thin 256-tile round that follows the grid's aspect (round 6
+    experiments, common.h thin_supertile; profiles/r8zj_thin_round.md): only
+    the tile order changes, so bitwise equal to the shipping W4S, every tile
+    written (NaN-filled output), wide 4 x 64 / 8 x 32 and tall 64 x 4 / 32 x 8
+    rounds and a square grid."""
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
+    if kernel.startswith("x_fp8"):
+        A = torch.randn(M, K, device="cuda", generator=g).to(FP8)
+        B = _colmajor(torch.randn(K, N, device="cuda", generator=g).to(FP8))
+    else:
+        A = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+        B = torch.randn(K, N, device="cuda", generator=g).to(torch.bfloat16)
+    ref = gemm.matmul(A, B, kernel=base)
+    out = torch.full_like(ref, float("nan"))
+    gemm.matmul(A, B, out=out, kernel=kernel)
+    assert torch.equal(out, ref)
