@@ -35,6 +35,8 @@ def main(d, cycle=None):
         seen = set()
         rows = [r for r in csv.DictReader(open(f))
                 if "distribution" not in r["Kernel_Name"] and "fillBuffer" not in r["Kernel_Name"]]
+        if cycle:  # only the GEMMs take part in the cycle (fp8 runs also launch quantize kernels)
+            rows = [r for r in rows if "pdmb::" in r["Kernel_Name"] or "Cijk" in r["Kernel_Name"]]
         order = {did: i for i, did in enumerate(sorted({int(r["Dispatch_Id"]) for r in rows}))}
         for r in rows:
             k = r["Kernel_Name"]
