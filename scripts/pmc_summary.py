@@ -20,7 +20,7 @@ import sys
 
 
 def short(k):
-    if k.startswith("Cijk"):
+    if k.startswith(("Cijk", "Custom_Cijk")):  # hipBLASLt (tuned kernels carry a Custom_ prefix)
         return "hipBLASLt " + k.split("_MT")[1].split("_")[0] if "_MT" in k else k[:40]
     return k.replace("void ", "").split("(")[0]
 
